@@ -1,0 +1,382 @@
+// PyTorch binding of the gfx950 kernel library (csrc/kernels/*.hip).
+//
+// Every entry point validates device, dtype, contiguity and the shapes the
+// kernel's grid assumes BEFORE launching (a mis-shaped launch of a hand-written
+// kernel can fault the GPU), then launches on the caller's current HIP stream so
+// the ops are stream-ordered and capturable into HIP graphs.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+extern "C" {
+int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+            int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
+            long long workspace_elems, int accumulate, hipStream_t st);
+int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
+                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, hipStream_t st);
+int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx,
+                float* delta, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site,
+                uint32_t thr, float drop_scale, hipStream_t st);
+int fd_mask_to_bias(const void* mask, int mask_bytes, float* bias, long n, hipStream_t st);
+int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, float* mean,
+              float* rstd, int T, int D, float eps, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
+              float dscale, hipStream_t st);
+int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean,
+              const float* rstd, void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work, int T,
+              int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, int accumulate,
+              hipStream_t st);
+int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
+               const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
+               const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, hipStream_t st);
+int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sorted, const long long* perm,
+               const void* word, const void* pos, const float* gamma, const float* mean, const float* rstd,
+               float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
+               int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
+               int accumulate, hipStream_t st);
+int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, hipStream_t st);
+int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
+                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
+                float* logits, float* loss, float* dlogits, hipStream_t st);
+int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
+                uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
+                int accumulate, hipStream_t st);
+int fd_eval_metrics(const float* logits, const long long* labels, int B, double* acc, long long* counts,
+                    float* prob1, long long* preds, hipStream_t st);
+int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float lr,
+            float b1, float b2, float eps, float wd, int decoupled, hipStream_t st);
+int fd_step(int* step, uint32_t* seed, hipStream_t st);
+int fd_scale_cast(float* p, void* shadow, long long n, float scale, hipStream_t st);
+int fd_axpby(float* dst, const float* x, const float* y, float a, float b, long long n, hipStream_t st);
+}
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, what, ": kernel launcher rejected arguments (rc=", rc, ")"); }
+
+void need(const at::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void need_opt(const c10::optional<at::Tensor>& t, at::ScalarType dt, const char* name) {
+  if (t.has_value() && t->defined()) need(*t, dt, name);
+}
+template <typename T>
+T* ptr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+const uint32_t* seedp(const at::Tensor& s) {
+  TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kInt && s.numel() >= 1, "seed must be a GPU int32 tensor");
+  return reinterpret_cast<const uint32_t*>(s.data_ptr());
+}
+
+// kind 0: C[M,N] = A[M,K] B[N,K]^T ; kind 1: C[M,N] = A[M,K] B[K,N] ; kind 2: C[M,N] fp32 = A[K,M]^T B[K,N]
+void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, const at::Tensor& C,
+          const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
+          const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& workspace, bool accumulate) {
+  need(A, at::kBFloat16, "A");
+  need(B, at::kBFloat16, "B");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
+  int64_t M, N, K;
+  if (kind == 0) { M = A.size(0); K = A.size(1); N = B.size(0); TORCH_CHECK(B.size(1) == K, "NT: K mismatch"); }
+  else if (kind == 1) { M = A.size(0); K = A.size(1); N = B.size(1); TORCH_CHECK(B.size(0) == K, "NN: K mismatch"); }
+  else if (kind == 2) { K = A.size(0); M = A.size(1); N = B.size(1); TORCH_CHECK(B.size(0) == K, "TN: K mismatch"); }
+  else TORCH_CHECK(false, "bad gemm kind");
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N, "C shape mismatch: got ", C.sizes(), " want [", M, ",", N, "]");
+  TORCH_CHECK(K % 64 == 0, "gemm: K must be a multiple of 64, got ", K);
+  TORCH_CHECK(N % 64 == 0, "gemm: N must be a multiple of 64, got ", N);
+  if (kind == 2) {
+    need(C, at::kFloat, "C");
+    TORCH_CHECK(M % 128 == 0, "TN gemm: M must be a multiple of 128");
+  } else {
+    need(C, at::kBFloat16, "C");
+  }
+  need_opt(bias, at::kFloat, "bias");
+  need_opt(aux, at::kBFloat16, "aux");
+  need_opt(res, at::kBFloat16, "res");
+  need_opt(workspace, at::kFloat, "workspace");
+  if (epi == 1 || epi == 2) TORCH_CHECK(bias.has_value() && bias->numel() == N, "bias of size N required");
+  if (epi == 2 || epi == 3) TORCH_CHECK(aux.has_value() && aux->size(0) == M && aux->size(1) == N, "aux [M,N] required");
+  if (epi == 4) TORCH_CHECK(res.has_value() && res->size(0) == M && res->size(1) == N, "res [M,N] required");
+  const long long ws = (workspace.has_value() && workspace->defined()) ? workspace->numel() : 0;
+  check_rc(fd_gemm((int)kind, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
+                   (int)A.size(1), (int)B.size(1), (int)N, ptr<float>(bias), ptr<void>(aux), (int)N,
+                   ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, stream()),
+           "gemm");
+}
+
+void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
+              int64_t B, int64_t S, int64_t H, const at::Tensor& seed, int64_t site, int64_t thr, double dscale) {
+  need(qkv, at::kBFloat16, "qkv");
+  need(kbias, at::kFloat, "kbias");
+  need(ctx, at::kBFloat16, "ctx");
+  need(lse, at::kFloat, "lse");
+  TORCH_CHECK(S % 64 == 0 && S <= 512, "attention: S must be a multiple of 64 and <= 512");
+  TORCH_CHECK(qkv.numel() == B * S * 3 * H * 64 && ctx.numel() == B * S * H * 64, "attention: qkv/ctx size");
+  TORCH_CHECK(kbias.numel() == B * S && lse.numel() == B * H * S, "attention: kbias/lse size");
+  check_rc(fd_attn_fwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(), (int)B,
+                       (int)S, (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, stream()),
+           "attn_fwd");
+}
+
+void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
+              const at::Tensor& dctx, const at::Tensor& delta, const at::Tensor& dqkv, int64_t B, int64_t S, int64_t H,
+              const at::Tensor& seed, int64_t site, int64_t thr, double dscale) {
+  need(qkv, at::kBFloat16, "qkv");
+  need(kbias, at::kFloat, "kbias");
+  need(ctx, at::kBFloat16, "ctx");
+  need(lse, at::kFloat, "lse");
+  need(dctx, at::kBFloat16, "dctx");
+  need(delta, at::kFloat, "delta");
+  need(dqkv, at::kBFloat16, "dqkv");
+  TORCH_CHECK(S % 64 == 0 && S <= 512, "attention: S must be a multiple of 64 and <= 512");
+  TORCH_CHECK(qkv.numel() == B * S * 3 * H * 64 && dqkv.numel() == qkv.numel(), "attention bwd: qkv size");
+  TORCH_CHECK(ctx.numel() == B * S * H * 64 && dctx.numel() == ctx.numel(), "attention bwd: ctx size");
+  TORCH_CHECK(lse.numel() == B * H * S && delta.numel() == B * H * S && kbias.numel() == B * S, "attention bwd: stats");
+  check_rc(fd_attn_bwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(),
+                       dctx.data_ptr(), delta.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)S, (int)H,
+                       seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, stream()),
+           "attn_bwd");
+}
+
+void mask_to_bias(const at::Tensor& mask, const at::Tensor& bias) {
+  TORCH_CHECK(mask.is_cuda() && mask.is_contiguous(), "mask must be a contiguous GPU tensor");
+  need(bias, at::kFloat, "bias");
+  TORCH_CHECK(mask.numel() == bias.numel(), "mask/bias size");
+  check_rc(fd_mask_to_bias(mask.data_ptr(), (int)mask.element_size(), bias.data_ptr<float>(), (long)mask.numel(),
+                           stream()),
+           "mask_to_bias");
+}
+
+void ln_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& r, const at::Tensor& gamma, const at::Tensor& beta,
+            const at::Tensor& y, const at::Tensor& mean, const at::Tensor& rstd, double eps, const at::Tensor& seed,
+            int64_t site, int64_t thr, double dscale) {
+  need(x, at::kBFloat16, "x");
+  need_opt(r, at::kBFloat16, "r");
+  need(gamma, at::kFloat, "gamma");
+  need(beta, at::kFloat, "beta");
+  need(y, at::kBFloat16, "y");
+  need(mean, at::kFloat, "mean");
+  need(rstd, at::kFloat, "rstd");
+  const int64_t D = gamma.numel(), T = x.numel() / D;
+  TORCH_CHECK(D == 768 && x.numel() == T * D && y.numel() == x.numel() && mean.numel() == T && rstd.numel() == T,
+              "ln_fwd: shapes (D must be 768)");
+  if (r.has_value() && r->defined()) TORCH_CHECK(r->numel() == x.numel(), "ln_fwd: residual size");
+  check_rc(fd_ln_fwd(x.data_ptr(), ptr<void>(r), gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
+                     mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)T, (int)D, (float)eps, seedp(seed),
+                     (uint32_t)site, (uint32_t)thr, (float)dscale, stream()),
+           "ln_fwd");
+}
+
+void ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& r, const at::Tensor& gamma,
+            const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dz, const c10::optional<at::Tensor>& dx,
+            const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
+            const c10::optional<at::Tensor>& dbias, const at::Tensor& work, const at::Tensor& seed, int64_t site,
+            int64_t thr, double dscale, bool accumulate) {
+  need(dy, at::kBFloat16, "dy");
+  need(x, at::kBFloat16, "x");
+  need_opt(r, at::kBFloat16, "r");
+  need(gamma, at::kFloat, "gamma");
+  need(mean, at::kFloat, "mean");
+  need(rstd, at::kFloat, "rstd");
+  need(dz, at::kBFloat16, "dz");
+  need_opt(dx, at::kBFloat16, "dx");
+  need_opt(dgamma, at::kFloat, "dgamma");
+  need_opt(dbeta, at::kFloat, "dbeta");
+  need_opt(dbias, at::kFloat, "dbias");
+  need(work, at::kFloat, "work");
+  const int64_t D = gamma.numel(), T = x.numel() / D;
+  TORCH_CHECK(D == 768 && dy.numel() == T * D && dz.numel() == T * D, "ln_bwd: shapes");
+  TORCH_CHECK(work.numel() >= 256 * 3 * D, "ln_bwd: work too small");
+  if (thr != 0) TORCH_CHECK(dx.has_value() && dx->numel() == T * D, "ln_bwd: dx required with dropout");
+  check_rc(fd_ln_bwd(dy.data_ptr(), x.data_ptr(), ptr<void>(r), gamma.data_ptr<float>(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), dz.data_ptr(), ptr<void>(dx), ptr<float>(dgamma), ptr<float>(dbeta),
+                     ptr<float>(dbias), work.data_ptr<float>(), (int)T, (int)D, seedp(seed), (uint32_t)site,
+                     (uint32_t)thr, (float)dscale, accumulate ? 1 : 0, stream()),
+           "ln_bwd");
+}
+
+void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& pos, const at::Tensor& gamma,
+             const at::Tensor& beta, const at::Tensor& y, const at::Tensor& mean, const at::Tensor& rstd, int64_t S,
+             double eps, const at::Tensor& seed, int64_t site, int64_t thr, double dscale) {
+  TORCH_CHECK(ids.is_cuda() && ids.is_contiguous() && (ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt),
+              "ids must be contiguous GPU int64/int32");
+  need(word, at::kBFloat16, "word");
+  need(pos, at::kBFloat16, "pos");
+  need(gamma, at::kFloat, "gamma");
+  need(beta, at::kFloat, "beta");
+  need(y, at::kBFloat16, "y");
+  const int64_t D = gamma.numel(), T = ids.numel();
+  TORCH_CHECK(D == 768 && word.size(1) == D && pos.size(1) == D && y.numel() == T * D, "emb_fwd: shapes");
+  TORCH_CHECK(S <= pos.size(0) && T % S == 0, "emb_fwd: S exceeds position table");
+  check_rc(fd_emb_fwd(ids.data_ptr(), ids.scalar_type() == at::kLong, word.data_ptr(), pos.data_ptr(),
+                      gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(), mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), (int)T, (int)S, (int)D, (float)eps, seedp(seed), (uint32_t)site,
+                      (uint32_t)thr, (float)dscale, stream()),
+           "emb_fwd");
+}
+
+void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sorted, const at::Tensor& perm,
+             const at::Tensor& word, const at::Tensor& pos, const at::Tensor& gamma, const at::Tensor& mean,
+             const at::Tensor& rstd, const at::Tensor& dword, const at::Tensor& dpos, const at::Tensor& dgamma,
+             const at::Tensor& dbeta, const at::Tensor& dz_buf, const at::Tensor& work, int64_t S,
+             const at::Tensor& seed, int64_t site, int64_t thr, double dscale, bool accumulate) {
+  need(dy, at::kBFloat16, "dy");
+  need(sorted, at::kLong, "sorted");
+  need(perm, at::kLong, "perm");
+  need(dword, at::kFloat, "dword");
+  need(dpos, at::kFloat, "dpos");
+  need(dgamma, at::kFloat, "dgamma");
+  need(dbeta, at::kFloat, "dbeta");
+  need(dz_buf, at::kFloat, "dz_buf");
+  need(work, at::kFloat, "work");
+  const int64_t D = gamma.numel(), T = ids.numel(), V = word.size(0), P = pos.size(0);
+  TORCH_CHECK(sorted.numel() == T && perm.numel() == T && dy.numel() == T * D && dz_buf.numel() >= T * D, "emb_bwd: sizes");
+  TORCH_CHECK(dword.numel() == V * D && dpos.numel() == P * D && work.numel() >= std::max<int64_t>(T * D, 256 * 3 * D),
+              "emb_bwd: grad/work sizes");
+  check_rc(fd_emb_bwd(dy.data_ptr(), ids.data_ptr(), ids.scalar_type() == at::kLong,
+                      reinterpret_cast<const long long*>(sorted.data_ptr()),
+                      reinterpret_cast<const long long*>(perm.data_ptr()), word.data_ptr(), pos.data_ptr(),
+                      gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), dword.data_ptr<float>(),
+                      dpos.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                      dz_buf.data_ptr<float>(), work.data_ptr<float>(), (int)T, (int)S, (int)(T / S), (int)P, (int)V,
+                      (int)D, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, accumulate ? 1 : 0, stream()),
+           "emb_bwd");
+}
+
+void colsum_bf16(const at::Tensor& x, const at::Tensor& out, const at::Tensor& work, bool accumulate) {
+  need(x, at::kBFloat16, "x");
+  need(out, at::kFloat, "out");
+  need(work, at::kFloat, "work");
+  const int64_t N = out.numel(), T = x.numel() / N;
+  TORCH_CHECK(T * N == x.numel() && work.numel() >= ((T + 31) / 32) * N, "colsum: sizes");
+  check_rc(fd_colsum_bf16(x.data_ptr(), (int)T, (int)N, out.data_ptr<float>(), work.data_ptr<float>(),
+                          accumulate ? 1 : 0, stream()),
+           "colsum_bf16");
+}
+
+void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& W, const at::Tensor& bias,
+              const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& labels,
+              const at::Tensor& logits, const c10::optional<at::Tensor>& loss, const c10::optional<at::Tensor>& dlogits) {
+  need(hidden, at::kBFloat16, "hidden");
+  need(W, at::kFloat, "W");
+  need(bias, at::kFloat, "bias");
+  need(logits, at::kFloat, "logits");
+  need_opt(labels, at::kLong, "labels");
+  need_opt(loss, at::kFloat, "loss");
+  need_opt(dlogits, at::kFloat, "dlogits");
+  const int64_t D = W.size(1);
+  TORCH_CHECK(W.size(0) == 2 && hidden.numel() == B * S * D && logits.numel() == B * 2, "head_fwd: shapes");
+  if (labels.has_value() && labels->defined())
+    TORCH_CHECK(labels->numel() == B && loss.has_value() && dlogits.has_value() && dlogits->numel() == 2 * B,
+                "head_fwd: labels needs loss/dlogits");
+  check_rc(fd_head_fwd(hidden.data_ptr(), (int)B, (int)S, (int)D, W.data_ptr<float>(), bias.data_ptr<float>(),
+                       seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale,
+                       ptr<const long long>(labels), logits.data_ptr<float>(), ptr<float>(loss), ptr<float>(dlogits),
+                       stream()),
+           "head_fwd");
+}
+
+void head_bwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& W, const at::Tensor& seed, int64_t site,
+              int64_t thr, double dscale, const at::Tensor& dlogits, const at::Tensor& dW, const at::Tensor& db,
+              const at::Tensor& dhidden, bool accumulate) {
+  need(hidden, at::kBFloat16, "hidden");
+  need(W, at::kFloat, "W");
+  need(dlogits, at::kFloat, "dlogits");
+  need(dW, at::kFloat, "dW");
+  need(db, at::kFloat, "db");
+  need(dhidden, at::kBFloat16, "dhidden");
+  const int64_t D = W.size(1);
+  TORCH_CHECK(hidden.numel() == B * S * D && dhidden.numel() == hidden.numel() && dlogits.numel() == 2 * B &&
+                  dW.numel() == 2 * D && db.numel() == 2,
+              "head_bwd: shapes");
+  check_rc(fd_head_bwd(hidden.data_ptr(), (int)B, (int)S, (int)D, W.data_ptr<float>(), seedp(seed), (uint32_t)site,
+                       (uint32_t)thr, (float)dscale, dlogits.data_ptr<float>(), dW.data_ptr<float>(),
+                       db.data_ptr<float>(), dhidden.data_ptr(), accumulate ? 1 : 0, stream()),
+           "head_bwd");
+}
+
+void eval_metrics(const at::Tensor& logits, const at::Tensor& labels, const at::Tensor& acc, const at::Tensor& counts,
+                  const c10::optional<at::Tensor>& prob1, const c10::optional<at::Tensor>& preds) {
+  need(logits, at::kFloat, "logits");
+  need(labels, at::kLong, "labels");
+  need(acc, at::kDouble, "acc");
+  need(counts, at::kLong, "counts");
+  need_opt(prob1, at::kFloat, "prob1");
+  need_opt(preds, at::kLong, "preds");
+  const int64_t B = labels.numel();
+  TORCH_CHECK(logits.numel() == 2 * B && acc.numel() >= 1 && counts.numel() >= 5, "eval_metrics: shapes");
+  check_rc(fd_eval_metrics(logits.data_ptr<float>(), reinterpret_cast<const long long*>(labels.data_ptr()), (int)B,
+                           acc.data_ptr<double>(), reinterpret_cast<long long*>(counts.data_ptr()), ptr<float>(prob1),
+                           ptr<long long>(preds), stream()),
+           "eval_metrics");
+}
+
+void adam(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
+          const c10::optional<at::Tensor>& shadow, const at::Tensor& step, double lr, double b1, double b2, double eps,
+          double wd, bool decoupled) {
+  need(p, at::kFloat, "p");
+  need(g, at::kFloat, "g");
+  need(m, at::kFloat, "m");
+  need(v, at::kFloat, "v");
+  need_opt(shadow, at::kBFloat16, "shadow");
+  need(step, at::kInt, "step");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && n % 4 == 0, "adam: sizes");
+  if (shadow.has_value() && shadow->defined()) TORCH_CHECK(shadow->numel() == n, "adam: shadow size");
+  check_rc(fd_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                   ptr<void>(shadow), n, step.data_ptr<int>(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
+                   decoupled ? 1 : 0, stream()),
+           "adam");
+}
+
+void step_inc(const c10::optional<at::Tensor>& step, const c10::optional<at::Tensor>& seed) {
+  need_opt(step, at::kInt, "step");
+  need_opt(seed, at::kInt, "seed");
+  check_rc(fd_step(ptr<int>(step), ptr<uint32_t>(seed), stream()), "step");
+}
+
+void scale_cast(const at::Tensor& p, const c10::optional<at::Tensor>& shadow, double scale) {
+  need(p, at::kFloat, "p");
+  need_opt(shadow, at::kBFloat16, "shadow");
+  TORCH_CHECK(p.numel() % 4 == 0, "scale_cast: numel % 4");
+  if (shadow.has_value() && shadow->defined()) TORCH_CHECK(shadow->numel() == p.numel(), "scale_cast: shadow size");
+  check_rc(fd_scale_cast(p.data_ptr<float>(), ptr<void>(shadow), p.numel(), (float)scale, stream()), "scale_cast");
+}
+
+void axpby(const at::Tensor& dst, const at::Tensor& x, const c10::optional<at::Tensor>& y, double a, double b) {
+  need(dst, at::kFloat, "dst");
+  need(x, at::kFloat, "x");
+  need_opt(y, at::kFloat, "y");
+  TORCH_CHECK(dst.numel() == x.numel() && dst.numel() % 4 == 0, "axpby: sizes");
+  if (y.has_value() && y->defined()) TORCH_CHECK(y->numel() == x.numel(), "axpby: y size");
+  check_rc(fd_axpby(dst.data_ptr<float>(), x.data_ptr<float>(), ptr<const float>(y), (float)a, (float)b, dst.numel(),
+                    stream()),
+           "axpby");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 HIP kernels for the federated DistilBERT engine";
+  m.def("gemm", &gemm);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("mask_to_bias", &mask_to_bias);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("emb_fwd", &emb_fwd);
+  m.def("emb_bwd", &emb_bwd);
+  m.def("colsum_bf16", &colsum_bf16);
+  m.def("head_fwd", &head_fwd);
+  m.def("head_bwd", &head_bwd);
+  m.def("eval_metrics", &eval_metrics);
+  m.def("adam", &adam);
+  m.def("step_inc", &step_inc);
+  m.def("scale_cast", &scale_cast);
+  m.def("axpby", &axpby);
+}

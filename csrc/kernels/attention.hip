@@ -1,0 +1,426 @@
+// Fused multi-head self-attention forward / backward for DistilBERT (gfx950).
+//
+// Reference math: HF DistilBERT MultiHeadSelfAttention (reached from
+// client1.py:61): scores = (q / sqrt(64)) k^T, key-padding mask -> -inf,
+// softmax, dropout(p=0.1) on the probabilities, context = P v.
+//
+// Layout: qkv is the fused projection output [B*S, 3*D] (q | k | v, head h at
+// columns h*64 of each third), ctx/dctx are [B*S, D], lse is fp32 [B, H, S].
+// Head dim is fixed at 64; S must be a multiple of 64 (S <= 512 in DistilBERT).
+//
+// MI355X design:
+//  * one workgroup = 4 waves = 64 queries (fwd, dQ) or 64 keys (dK/dV) of one
+//    (batch, head); grid = (S/64, H, B) -> 768 workgroups at B32/S128.
+//  * Every product runs on v_mfma_f32_16x16x32_bf16 with the "owned" index
+//    (query for fwd/dQ, key for dK/dV) on the MFMA column = lane&15, so softmax
+//    statistics are lane-constant and each row reduction is 2 xor-shuffles
+//    (lanes l, l^16, l^32, l^48 share a row).
+//  * The score accumulator is re-used as the next MFMA's operand with a
+//    permuted k order (cdna_hip_programming.md §3 "accumulator as operand"),
+//    so P / dS never touch LDS; the matching operand is fetched with the
+//    transposing ds_read_b64_tr_b16 from the same LDS image that serves the
+//    row reads (one XOR-swizzled [64][64] image per tile, conflict-free for
+//    both read kinds).
+//  * Dropout is a stateless hash of (seed, ((b*H+h)*S+q)*S+k): regenerated in
+//    the backward, never stored.  Backward is FA2-style and atomic-free:
+//    kernel dq (query-owned) and kernel dkdv (key-owned) each recompute P.
+#include "common.h"
+
+namespace {
+
+constexpr int DH = 64;
+
+// Unified swizzle for [64 rows][64 bf16] tiles (128-byte rows, 8 chunks of 16 B):
+// ds_read_b128 row reads (16 consecutive rows, same chunk) and the tr reads
+// (8 consecutive rows, 2 adjacent chunks) are both bank-conflict free.
+DEV int sw(int r) { return (((r >> 1) & 3) << 1) | ((r >> 3) & 1); }
+DEV int tile_off(int r, int c) { return r * 128 + ((c ^ sw(r)) << 4); }
+
+// Stage a [64][64] bf16 tile (row stride ld elements) into LDS; 256 threads.
+DEV void stage_tile(char* lds, const bf16_t* src, long ld, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = i * 256 + tid;
+    const int r = id >> 3, c = id & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)r * ld + c * 8);
+    *reinterpret_cast<uint4*>(lds + tile_off(r, c)) = v;
+  }
+}
+
+// Row-read fragment: rows row0 + (lane&15), columns 32*s + 8*(lane>>4) .. +7.
+DEV bf16x8 row_frag(const char* lds, int row0, int s, int lane) {
+  const int r = row0 + (lane & 15);
+  return *reinterpret_cast<const bf16x8*>(lds + tile_off(r, s * 4 + (lane >> 4)));
+}
+
+// Transposed fragment with the permuted k order used for accumulator re-use:
+// element j of lane group g = row  32*ks + 16*(j>>2) + 4*g + (j&3), column col0 + (lane&15).
+DEV bf16x8 tr_frag(const char* lds, int col0, int ks, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  const int c = (col0 >> 3) + (p >> 1);
+  bf16x8 out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = 32 * ks + 16 * h + 4 * g + q;
+    const char* addr = lds + tile_off(r, c) + (p & 1) * 8;
+    bf16x4v v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) bf16x4v*)(addr));
+    out[4 * h + 0] = v[0];
+    out[4 * h + 1] = v[1];
+    out[4 * h + 2] = v[2];
+    out[4 * h + 3] = v[3];
+  }
+  return out;
+}
+
+// Pack accumulator tiles 2ks, 2ks+1 (4 regs each) into a bf16x8 operand in the
+// permuted k order matching tr_frag.
+DEV bf16x8 pack_acc(const f32x4& a, const f32x4& b) {
+  bf16x8 o;
+  o[0] = (short)f2bf(a[0]); o[1] = (short)f2bf(a[1]); o[2] = (short)f2bf(a[2]); o[3] = (short)f2bf(a[3]);
+  o[4] = (short)f2bf(b[0]); o[5] = (short)f2bf(b[1]); o[6] = (short)f2bf(b[2]); o[7] = (short)f2bf(b[3]);
+  return o;
+}
+
+DEV bf16x8 load_frag_global(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+struct AttnArgs {
+  const bf16_t* qkv;    // [B*S, 3D]
+  const float* kbias;   // [B, S] additive key mask (0 / -inf)
+  bf16_t* ctx;          // fwd out [B*S, D]
+  float* lse;           // [B, H, S]
+  const bf16_t* dctx;   // bwd in
+  const float* delta;   // [B, H, S]
+  bf16_t* dqkv;         // bwd out [B*S, 3D]
+  const uint32_t* seed_ptr;
+  uint32_t site;
+  uint32_t drop_threshold;
+  float drop_scale;     // 1/(1-p)
+  int B, S, H;
+  float scale;          // 1/sqrt(64)
+};
+
+DEV uint32_t site_seed(const AttnArgs& a) { return hash32(a.seed_ptr ? a.seed_ptr[0] : 0u, a.site); }
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 8192 + 256];
+  char* ks = smem;
+  char* vs = smem + 8192;
+  float* kb = reinterpret_cast<float*>(smem + 16384);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  const int q = blockIdx.x * 64 + w * 16 + (lane & 15);
+  const size_t tok0 = (size_t)b * S;
+  const uint32_t seed = site_seed(a);
+  const bool drop = a.drop_threshold != 0;
+
+  bf16x8 qf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) qf[s] = load_frag_global(a.qkv + (tok0 + q) * ld3 + h * DH + 32 * s + 8 * g);
+
+  f32x4 o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
+
+  for (int k0 = 0; k0 < S; k0 += 64) {
+    __syncthreads();
+    stage_tile(ks, a.qkv + (tok0 + k0) * ld3 + D + h * DH, ld3, tid);
+    stage_tile(vs, a.qkv + (tok0 + k0) * ld3 + 2 * D + h * DH, ld3, tid);
+    if (tid < 64) kb[tid] = a.kbias[tok0 + k0 + tid];
+    __syncthreads();
+
+    f32x4 sc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) sc[t] = mfma16(row_frag(ks, 16 * t, s, lane), qf[s], sc[t]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sc[t][r] = sc[t][r] * a.scale + kb[16 * t + 4 * g + r];
+        mx = fmaxf(mx, sc[t][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float mref = mn == -INFINITY ? 0.f : mn;
+    const float alpha = __expf(m - mref);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] *= alpha;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = __expf(sc[t][r] - mref);
+        l += pv;
+        float pd = pv;
+        if (drop) {
+          const uint32_t key = k0 + 16 * t + 4 * g + r;
+          pd = drop_keep(seed, rowidx + key, a.drop_threshold) ? pv * a.drop_scale : 0.f;
+        }
+        sc[t][r] = pd;
+      }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 pf = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(tr_frag(vs, 16 * dt, kk, lane), pf, o[dt]);
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  bf16_t* out = a.ctx + (tok0 + q) * D + h * DH;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+    *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) =
+        make_uint2(pack_bf2(o[dt][0] * inv, o[dt][1] * inv), pack_bf2(o[dt][2] * inv, o[dt][3] * inv));
+  if (g == 0) a.lse[((size_t)b * H + h) * S + q] = m + __logf(l);
+}
+
+// delta[b,h,q] = sum_d dctx * ctx  (FA2 preprocessing); one thread per (token, head).
+__global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs a) {
+  const int D = a.H * DH;
+  const long idx = blockIdx.x * 256l + threadIdx.x;
+  if (idx >= (long)a.B * a.S * a.H) return;
+  const int h = idx % a.H;
+  const long tok = idx / a.H;
+  const int b = tok / a.S, q = tok % a.S;
+  const uint4* o = reinterpret_cast<const uint4*>(a.ctx + tok * D + h * DH);
+  const uint4* d = reinterpret_cast<const uint4*>(a.dctx + tok * D + h * DH);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 x = o[i], y = d[i];
+    s += lo_bf(x.x) * lo_bf(y.x) + hi_bf(x.x) * hi_bf(y.x) + lo_bf(x.y) * lo_bf(y.y) +
+         hi_bf(x.y) * hi_bf(y.y) + lo_bf(x.z) * lo_bf(y.z) + hi_bf(x.z) * hi_bf(y.z) +
+         lo_bf(x.w) * lo_bf(y.w) + hi_bf(x.w) * hi_bf(y.w);
+  }
+  const_cast<float*>(a.delta)[((size_t)b * a.H + h) * a.S + q] = s;
+}
+
+// ------------------------------------------------------------------ backward: dQ
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 8192 + 256];
+  char* ks = smem;
+  char* vs = smem + 8192;
+  float* kb = reinterpret_cast<float*>(smem + 16384);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  const int q = blockIdx.x * 64 + w * 16 + (lane & 15);
+  const size_t tok0 = (size_t)b * S;
+  const uint32_t seed = site_seed(a);
+  const bool drop = a.drop_threshold != 0;
+
+  bf16x8 qf[2], dof[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    qf[s] = load_frag_global(a.qkv + (tok0 + q) * ld3 + h * DH + 32 * s + 8 * g);
+    dof[s] = load_frag_global(a.dctx + (tok0 + q) * D + h * DH + 32 * s + 8 * g);
+  }
+  const size_t st = ((size_t)b * H + h) * S + q;
+  const float lse = a.lse[st], dl = a.delta[st];
+  const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
+
+  f32x4 dq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < S; k0 += 64) {
+    __syncthreads();
+    stage_tile(ks, a.qkv + (tok0 + k0) * ld3 + D + h * DH, ld3, tid);
+    stage_tile(vs, a.qkv + (tok0 + k0) * ld3 + 2 * D + h * DH, ld3, tid);
+    if (tid < 64) kb[tid] = a.kbias[tok0 + k0 + tid];
+    __syncthreads();
+
+    f32x4 sc[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sc[t] = mfma16(row_frag(ks, 16 * t, s, lane), qf[s], sc[t]);
+        dp[t] = mfma16(row_frag(vs, 16 * t, s, lane), dof[s], dp[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kl = 16 * t + 4 * g + r;
+        const float pv = __expf(sc[t][r] * a.scale + kb[kl] - lse);
+        float dpv = dp[t][r];
+        if (drop)
+          dpv = drop_keep(seed, rowidx + k0 + kl, a.drop_threshold) ? dpv * a.drop_scale : 0.f;
+        sc[t][r] = pv * (dpv - dl);  // dS
+      }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 df = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(tr_frag(ks, 16 * dt, kk, lane), df, dq[dt]);
+    }
+  }
+  bf16_t* out = a.dqkv + (tok0 + q) * ld3 + h * DH;
+  const float sc = a.scale;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+    *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) =
+        make_uint2(pack_bf2(dq[dt][0] * sc, dq[dt][1] * sc), pack_bf2(dq[dt][2] * sc, dq[dt][3] * sc));
+}
+
+// ------------------------------------------------------------------ backward: dK, dV
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 8192 + 512];
+  char* qs = smem;
+  char* os = smem + 8192;  // dO tile
+  float* lse_s = reinterpret_cast<float*>(smem + 16384);
+  float* dl_s = lse_s + 64;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  const int key = blockIdx.x * 64 + w * 16 + (lane & 15);
+  const size_t tok0 = (size_t)b * S;
+  const uint32_t seed = site_seed(a);
+  const bool drop = a.drop_threshold != 0;
+
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    kf[s] = load_frag_global(a.qkv + (tok0 + key) * ld3 + D + h * DH + 32 * s + 8 * g);
+    vf[s] = load_frag_global(a.qkv + (tok0 + key) * ld3 + 2 * D + h * DH + 32 * s + 8 * g);
+  }
+  const float kbias = a.kbias[tok0 + key];
+  const size_t st0 = ((size_t)b * H + h) * S;
+  const uint32_t headidx = (uint32_t)(b * H + h) * S;
+
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dk[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  for (int q0 = 0; q0 < S; q0 += 64) {
+    __syncthreads();
+    stage_tile(qs, a.qkv + (tok0 + q0) * ld3 + h * DH, ld3, tid);
+    stage_tile(os, a.dctx + (tok0 + q0) * D + h * DH, D, tid);
+    if (tid < 64) lse_s[tid] = a.lse[st0 + q0 + tid];
+    else if (tid < 128) dl_s[tid - 64] = a.delta[st0 + q0 + tid - 64];
+    __syncthreads();
+
+    f32x4 sc[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sc[t] = mfma16(row_frag(qs, 16 * t, s, lane), kf[s], sc[t]);  // S[q][key]
+        dp[t] = mfma16(row_frag(os, 16 * t, s, lane), vf[s], dp[t]);  // dP[q][key]
+      }
+    }
+    f32x4 pd[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = 16 * t + 4 * g + r;
+        const float pv = __expf(sc[t][r] * a.scale + kbias - lse_s[ql]);
+        float dpv = dp[t][r], pdv = pv;
+        if (drop) {
+          const bool keep = drop_keep(seed, (headidx + q0 + ql) * (uint32_t)S + key, a.drop_threshold);
+          dpv = keep ? dpv * a.drop_scale : 0.f;
+          pdv = keep ? pv * a.drop_scale : 0.f;
+        }
+        pd[t][r] = pdv;
+        sc[t][r] = pv * (dpv - dl_s[ql]);  // dS
+      }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 pf = pack_acc(pd[2 * kk], pd[2 * kk + 1]);
+      const bf16x8 sf = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma16(tr_frag(os, 16 * dt, kk, lane), pf, dv[dt]);
+        dk[dt] = mfma16(tr_frag(qs, 16 * dt, kk, lane), sf, dk[dt]);
+      }
+    }
+  }
+  bf16_t* outk = a.dqkv + (tok0 + key) * ld3 + D + h * DH;
+  bf16_t* outv = a.dqkv + (tok0 + key) * ld3 + 2 * D + h * DH;
+  const float sc = a.scale;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    *reinterpret_cast<uint2*>(outk + 16 * dt + 4 * g) =
+        make_uint2(pack_bf2(dk[dt][0] * sc, dk[dt][1] * sc), pack_bf2(dk[dt][2] * sc, dk[dt][3] * sc));
+    *reinterpret_cast<uint2*>(outv + 16 * dt + 4 * g) =
+        make_uint2(pack_bf2(dv[dt][0], dv[dt][1]), pack_bf2(dv[dt][2], dv[dt][3]));
+  }
+}
+
+template <typename M>
+__global__ __launch_bounds__(256) void mask_to_bias_kernel(const M* mask, float* bias, long n) {
+  const long i = blockIdx.x * 256l + threadIdx.x;
+  if (i < n) bias[i] = mask[i] != 0 ? 0.f : -INFINITY;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
+                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale,
+                hipStream_t st) {
+  if (S % 64 != 0) return 1;
+  AttnArgs a{};
+  a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
+  a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
+  a.B = B; a.S = S; a.H = H; a.scale = 0.125f;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
+  return 0;
+}
+
+int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse,
+                const void* dctx, float* delta, void* dqkv, int B, int S, int H,
+                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale,
+                hipStream_t st) {
+  if (S % 64 != 0) return 1;
+  AttnArgs a{};
+  a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = (float*)lse;
+  a.dctx = (const bf16_t*)dctx; a.delta = delta; a.dqkv = (bf16_t*)dqkv;
+  a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
+  a.B = B; a.S = S; a.H = H; a.scale = 0.125f;
+  const long n = (long)B * S * H;
+  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
+  return 0;
+}
+
+int fd_mask_to_bias(const void* mask, int mask_bytes, float* bias, long n, hipStream_t st) {
+  const dim3 grid((n + 255) / 256);
+  if (mask_bytes == 8)
+    hipLaunchKernelGGL(mask_to_bias_kernel<long long>, grid, dim3(256), 0, st, (const long long*)mask, bias, n);
+  else if (mask_bytes == 4)
+    hipLaunchKernelGGL(mask_to_bias_kernel<int>, grid, dim3(256), 0, st, (const int*)mask, bias, n);
+  else if (mask_bytes == 1)
+    hipLaunchKernelGGL(mask_to_bias_kernel<unsigned char>, grid, dim3(256), 0, st, (const unsigned char*)mask, bias, n);
+  else
+    return 1;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+// Shared helpers for the gfx950 (CDNA4, MI355X) kernels of this framework.
+//
+// Conventions
+//  * bf16 tensors are passed as raw uint16 bits (`bf16_t`), fp32 as float.
+//  * Wave size is 64; every kernel uses 256-thread blocks (4 waves) unless noted.
+//  * MFMA: v_mfma_f32_16x16x32_bf16.  Operand lane maps (gfx950):
+//      A frag, lane l: A[row = l&15][k = 8*(l>>4) + j], j = 0..7
+//      B frag, lane l: B[k = 8*(l>>4) + j][col = l&15]
+//      C/D,   lane l: D[row = 4*(l>>4) + r][col = l&15], r = 0..3
+//  * Dropout masks come from a stateless counter hash (`drop_keep`) of
+//    (seed, element index) so the backward pass regenerates them instead of
+//    storing them; the same hash is reproduced in torch for the CPU reference.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+
+typedef uint16_t bf16_t;
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4v __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define DEV __device__ __forceinline__
+
+DEV float bf2f(uint32_t h) { return __uint_as_float(h << 16); }
+
+// Round-to-nearest-even fp32 -> bf16 (NaN kept quiet).
+DEV uint32_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+DEV uint32_t pack_bf2(float a, float b) { return f2bf(a) | (f2bf(b) << 16); }
+
+DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------- dropout hash
+// lowbias32-style finaliser over (idx * golden + seed).  Mirrored bit-exactly by
+// ops/dropout.py::keep_mask (torch int64 arithmetic) for the CPU reference.
+DEV uint32_t hash32(uint32_t seed, uint32_t idx) {
+  uint32_t x = idx * 0x9E3779B1u + seed;
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// keep iff hash >= threshold, threshold = round(p * 2^32) (0 => always keep).
+DEV bool drop_keep(uint32_t seed, uint32_t idx, uint32_t threshold) {
+  return hash32(seed, idx) >= threshold;
+}
+
+DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+DEV float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective remap of a linear workgroup id (cdna_hip_programming.md
+// T1): blocks that share an L2 (same id % 8) get a contiguous range of logical
+// tiles, so neighbouring tiles reuse operand panels from one XCD's L2.
+DEV int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}

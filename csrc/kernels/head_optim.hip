@@ -1,0 +1,278 @@
+// Classifier head + CE loss, eval metrics, Adam/AdamW and FedAvg helpers (gfx950).
+//
+// Head (client1.py:57-64, :108): pooled = hidden[:, 0, :] -> Dropout(0.3) ->
+// Linear(768, 2) -> CrossEntropy(mean).  B <= 1024 rows; one 256-thread block,
+// fixed reduction order (deterministic).  2-class CE == BCE-with-logits on z1-z0.
+//
+// Adam (client1.py:380, torch.optim.Adam defaults, bias-corrected): one launch
+// over the whole flat fp32 parameter arena (66,364,418 params) with float4
+// loads, writing the fp32 master, m, v and the bf16 compute shadow in the same
+// pass.  The step count and the dropout seed counter live on the device so the
+// whole train step can be replayed as a HIP graph.
+//
+// Eval metrics (client1.py:134-142): per-batch mean CE added to a device
+// accumulator, correct / TP / FP / FN / TN counts and P(class 1) -- replacing
+// the reference's four host syncs per eval batch.
+#include "common.h"
+
+namespace {
+
+struct HeadArgs {
+  const bf16_t* hidden;  // [B*S, D]
+  int B, S, D;
+  const float* W;        // [2, D] fp32 master
+  const float* bias;     // [2]
+  const uint32_t* seed_ptr;
+  uint32_t site, thr;
+  float dscale;
+  const long long* labels;  // nullable
+  float* logits;         // [B, 2]
+  float* loss;           // [1]
+  float* dlogits;        // [B, 2] (written when labels given)
+  // backward
+  const float* dlog_in;  // [B, 2]
+  float* dW;             // [2, D]
+  float* db;             // [2]
+  bf16_t* dhidden;       // [B*S, D]; only CLS rows written
+  int accumulate;
+};
+
+__global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
+  __shared__ float red[64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool drop = a.thr != 0;
+  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
+  float lsum = 0.f;
+  for (int b = w; b < a.B; b += 4) {
+    const bf16_t* x = a.hidden + (size_t)b * a.S * a.D;
+    float z0 = 0.f, z1 = 0.f;
+    for (int col = lane; col < a.D; col += 64) {
+      float v = bf2f(x[col]);
+      if (drop) v = drop_keep(seed, (uint32_t)(b * a.D + col), a.thr) ? v * a.dscale : 0.f;
+      z0 += v * a.W[col];
+      z1 += v * a.W[a.D + col];
+    }
+    z0 = wave_sum(z0) + a.bias[0];
+    z1 = wave_sum(z1) + a.bias[1];
+    if (lane == 0) {
+      a.logits[2 * b] = z0;
+      a.logits[2 * b + 1] = z1;
+      if (a.labels) {
+        const float mx = fmaxf(z0, z1);
+        const float lse = mx + __logf(__expf(z0 - mx) + __expf(z1 - mx));
+        const int y = (int)a.labels[b];
+        lsum += lse - (y ? z1 : z0);
+        const float p1 = __expf(z1 - lse), p0 = __expf(z0 - lse);
+        a.dlogits[2 * b] = (p0 - (y == 0)) / a.B;
+        a.dlogits[2 * b + 1] = (p1 - (y == 1)) / a.B;
+      }
+    }
+  }
+  if (a.labels) {
+    if (lane == 0) red[w] = lsum;
+    __syncthreads();
+    if (threadIdx.x == 0) a.loss[0] = (red[0] + red[1] + red[2] + red[3]) / a.B;
+  }
+}
+
+__global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
+  const bool drop = a.thr != 0;
+  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
+  for (int col = threadIdx.x; col < a.D; col += 256) {
+    float g0 = 0.f, g1 = 0.f;
+    const float w0 = a.W[col], w1 = a.W[a.D + col];
+    for (int b = 0; b < a.B; ++b) {
+      const float d0 = a.dlog_in[2 * b], d1 = a.dlog_in[2 * b + 1];
+      const bool keep = !drop || drop_keep(seed, (uint32_t)(b * a.D + col), a.thr);
+      const float sc = drop ? (keep ? a.dscale : 0.f) : 1.f;
+      const float x = bf2f(a.hidden[(size_t)b * a.S * a.D + col]) * sc;
+      g0 += d0 * x;
+      g1 += d1 * x;
+      a.dhidden[(size_t)b * a.S * a.D + col] = (bf16_t)f2bf((d0 * w0 + d1 * w1) * sc);
+    }
+    a.dW[col] = a.accumulate ? a.dW[col] + g0 : g0;
+    a.dW[a.D + col] = a.accumulate ? a.dW[a.D + col] + g1 : g1;
+  }
+  if (threadIdx.x < 2) {
+    float s = 0.f;
+    for (int b = 0; b < a.B; ++b) s += a.dlog_in[2 * b + threadIdx.x];
+    a.db[threadIdx.x] = a.accumulate ? a.db[threadIdx.x] + s : s;
+  }
+}
+
+// acc: [0] = sum of per-batch mean loss (double), counts: [0] correct [1] tp [2] fp [3] fn [4] tn
+__global__ __launch_bounds__(256) void eval_metrics_kernel(const float* logits, const long long* labels, int B,
+                                                           double* acc, long long* counts, float* prob1,
+                                                           long long* preds) {
+  __shared__ float sl[256];
+  __shared__ int sc[5][256];
+  const int t = threadIdx.x;
+  float l = 0.f;
+  int c[5] = {0, 0, 0, 0, 0};
+  for (int b = t; b < B; b += 256) {
+    const float z0 = logits[2 * b], z1 = logits[2 * b + 1];
+    const float mx = fmaxf(z0, z1);
+    const float lse = mx + logf(expf(z0 - mx) + expf(z1 - mx));
+    const int y = (int)labels[b];
+    l += lse - (y ? z1 : z0);
+    const int pred = z1 > z0 ? 1 : 0;  // torch.max picks the first index on ties
+    if (prob1) prob1[b] = expf(z1 - lse);
+    if (preds) preds[b] = pred;
+    c[0] += pred == y;
+    c[1] += pred == 1 && y == 1;
+    c[2] += pred == 1 && y == 0;
+    c[3] += pred == 0 && y == 1;
+    c[4] += pred == 0 && y == 0;
+  }
+  sl[t] = l;
+  for (int k = 0; k < 5; ++k) sc[k][t] = c[k];
+  __syncthreads();
+  if (t == 0) {
+    float s = 0.f;
+    long long cc[5] = {0, 0, 0, 0, 0};
+    for (int i = 0; i < 256; ++i) {
+      s += sl[i];
+      for (int k = 0; k < 5; ++k) cc[k] += sc[k][i];
+    }
+    acc[0] += (double)(s / B);
+    for (int k = 0; k < 5; ++k) counts[k] += cc[k];
+  }
+}
+
+struct AdamArgs {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  bf16_t* shadow;
+  long long n4;
+  const int* step;
+  float lr, b1, b2, eps, wd;
+  int decoupled;
+};
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  const int t = a.step[0];
+  const float bc1 = 1.f - powf(a.b1, (float)t);
+  const float bc2 = 1.f - powf(a.b2, (float)t);
+  const float step_size = a.lr / bc1;
+  const float inv_sqrt_bc2 = 1.f / sqrtf(bc2);
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < a.n4; i += (long long)gridDim.x * 256) {
+    float4 p = reinterpret_cast<float4*>(a.p)[i];
+    float4 g = reinterpret_cast<const float4*>(a.g)[i];
+    float4 m = reinterpret_cast<float4*>(a.m)[i];
+    float4 v = reinterpret_cast<float4*>(a.v)[i];
+    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
+    float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float gr = gg[e];
+      if (a.wd != 0.f) {
+        if (a.decoupled) pp[e] *= 1.f - a.lr * a.wd;
+        else gr += a.wd * pp[e];
+      }
+      mm[e] = a.b1 * mm[e] + (1.f - a.b1) * gr;
+      vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gr * gr;
+      const float denom = sqrtf(vv[e]) * inv_sqrt_bc2 + a.eps;
+      pp[e] -= step_size * mm[e] / denom;
+    }
+    reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    reinterpret_cast<float4*>(a.m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+    reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    if (a.shadow)
+      reinterpret_cast<uint2*>(a.shadow)[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
+  }
+}
+
+__global__ void step_kernel(int* step, uint32_t* seed) {
+  if (step) step[0] += 1;
+  if (seed) seed[0] += 1;
+}
+
+// p *= scale (optional) and shadow = bf16(p): FedAvg finalisation / shadow refresh.
+__global__ __launch_bounds__(256) void scale_cast_kernel(float* p, bf16_t* shadow, long long n4, float scale) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 v = reinterpret_cast<float4*>(p)[i];
+    if (scale != 1.f) {
+      v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+      reinterpret_cast<float4*>(p)[i] = v;
+    }
+    if (shadow) reinterpret_cast<uint2*>(shadow)[i] = make_uint2(pack_bf2(v.x, v.y), pack_bf2(v.z, v.w));
+  }
+}
+
+// dst = a * x + b * y over fp32 arenas (sample-weighted FedAvg pre-scale / blends).
+__global__ __launch_bounds__(256) void axpby_kernel(float* dst, const float* x, const float* y, float a, float b,
+                                                    long long n4) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const float4 u = reinterpret_cast<const float4*>(x)[i];
+    float4 r = make_float4(a * u.x, a * u.y, a * u.z, a * u.w);
+    if (y) {
+      const float4 w = reinterpret_cast<const float4*>(y)[i];
+      r.x += b * w.x; r.y += b * w.y; r.z += b * w.z; r.w += b * w.w;
+    }
+    reinterpret_cast<float4*>(dst)[i] = r;
+  }
+}
+
+int grid_for(long long n4) { return (int)std::min<long long>((n4 + 255) / 256, 4096); }
+
+}  // namespace
+
+extern "C" {
+
+int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
+                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
+                float* logits, float* loss, float* dlogits, hipStream_t st) {
+  if (B > 4096) return 1;
+  HeadArgs a{};
+  a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W; a.bias = bias;
+  a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.labels = labels;
+  a.logits = logits; a.loss = loss; a.dlogits = dlogits;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(1), dim3(256), 0, st, a);
+  return 0;
+}
+
+int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
+                uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
+                int accumulate, hipStream_t st) {
+  HeadArgs a{};
+  a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W;
+  a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.dlog_in = dlogits;
+  a.dW = dW; a.db = db; a.dhidden = (bf16_t*)dhidden; a.accumulate = accumulate;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(1), dim3(256), 0, st, a);
+  return 0;
+}
+
+int fd_eval_metrics(const float* logits, const long long* labels, int B, double* acc, long long* counts,
+                    float* prob1, long long* preds, hipStream_t st) {
+  hipLaunchKernelGGL(eval_metrics_kernel, dim3(1), dim3(256), 0, st, logits, labels, B, acc, counts, prob1, preds);
+  return 0;
+}
+
+int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float lr,
+            float b1, float b2, float eps, float wd, int decoupled, hipStream_t st) {
+  if (n % 4 != 0) return 1;
+  AdamArgs a{p, g, m, v, (bf16_t*)shadow, n / 4, step, lr, b1, b2, eps, wd, decoupled};
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, a);
+  return 0;
+}
+
+int fd_step(int* step, uint32_t* seed, hipStream_t st) {
+  hipLaunchKernelGGL(step_kernel, dim3(1), dim3(1), 0, st, step, seed);
+  return 0;
+}
+
+int fd_scale_cast(float* p, void* shadow, long long n, float scale, hipStream_t st) {
+  if (n % 4 != 0) return 1;
+  hipLaunchKernelGGL(scale_cast_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, p, (bf16_t*)shadow, n / 4, scale);
+  return 0;
+}
+
+int fd_axpby(float* dst, const float* x, const float* y, float a, float b, long long n, hipStream_t st) {
+  if (n % 4 != 0) return 1;
+  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, dst, x, y, a, b, n / 4);
+  return 0;
+}
+
+}  // extern "C"

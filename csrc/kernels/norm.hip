@@ -1,0 +1,450 @@
+// LayerNorm (fused residual + dropout), embedding and column-reduction kernels.
+//
+// Reference math (HF DistilBERT via client1.py:61, eps = 1e-12):
+//   embeddings : y = Dropout(LN(word[id] + pos[s]))
+//   sa block   : y = LN(attn_out + x)
+//   ffn block  : y = LN(Dropout(lin2_out) + h)
+// One wave owns one 768-wide row (12 values / lane, loaded as 8-byte bf16x4
+// chunks so a wave instruction moves 512 contiguous bytes); statistics in fp32.
+// The backward recomputes the pre-LN sum from the saved inputs and the
+// stateless dropout hash instead of storing it, writes the input gradient(s)
+// in bf16, and emits per-block partial column sums for dgamma, dbeta and the
+// producer's bias gradient, which `colsum` reduces in a fixed order
+// (deterministic, no atomics).
+#include "common.h"
+
+namespace {
+
+struct LnArgs {
+  const bf16_t* x;      // primary input (dropout applies to it)
+  const bf16_t* r;      // residual (nullable)
+  const float* gamma;
+  const float* beta;
+  bf16_t* y;
+  float* mean;
+  float* rstd;
+  int T, D;
+  float eps;
+  const uint32_t* seed_ptr;
+  uint32_t site, thr;
+  float dscale;
+  // backward
+  const bf16_t* dy;
+  bf16_t* dz;           // grad of the pre-LN sum (residual grad)
+  bf16_t* dx;           // grad of the primary input through dropout (nullable if no dropout)
+  float* part;          // [gridDim.x][3][D]: dgamma, dbeta, dbias partials
+};
+
+template <int NC>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.T) return;
+  const int D = a.D;
+  const bool drop = a.thr != 0;
+  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
+  float z[NC][4];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    const size_t off = (size_t)row * D + col;
+    const uint2 xv = *reinterpret_cast<const uint2*>(a.x + off);
+    float v[4] = {lo_bf(xv.x), hi_bf(xv.x), lo_bf(xv.y), hi_bf(xv.y)};
+    if (drop) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = drop_keep(seed, (uint32_t)(off + e), a.thr) ? v[e] * a.dscale : 0.f;
+    }
+    if (a.r) {
+      const uint2 rv = *reinterpret_cast<const uint2*>(a.r + off);
+      v[0] += lo_bf(rv.x); v[1] += hi_bf(rv.x); v[2] += lo_bf(rv.y); v[3] += hi_bf(rv.y);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { z[c][e] = v[e]; s += v[e]; }
+  }
+  const float mean = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { const float d = z[c][e] - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) / D + a.eps);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    const float4 g = *reinterpret_cast<const float4*>(a.gamma + col);
+    const float4 b = *reinterpret_cast<const float4*>(a.beta + col);
+    const float y0 = (z[c][0] - mean) * rstd * g.x + b.x, y1 = (z[c][1] - mean) * rstd * g.y + b.y;
+    const float y2 = (z[c][2] - mean) * rstd * g.z + b.z, y3 = (z[c][3] - mean) * rstd * g.w + b.w;
+    *reinterpret_cast<uint2*>(a.y + (size_t)row * D + col) = make_uint2(pack_bf2(y0, y1), pack_bf2(y2, y3));
+  }
+  if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
+}
+
+// Block-level reduction of per-lane column partials (NC*4 columns per lane,
+// 4 waves) into part[blockIdx.x][which][D].
+template <int NC>
+DEV void block_colsum(float (&acc)[NC][4], float* lds, float* out, int D) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lds[w * D + 4 * (lane + 64 * c) + e] = acc[c][e];
+  __syncthreads();
+  for (int col = threadIdx.x; col < D; col += 256)
+    out[col] = lds[col] + lds[D + col] + lds[2 * D + col] + lds[3 * D + col];
+  __syncthreads();
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][D]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int D = a.D;
+  const bool drop = a.thr != 0;
+  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
+  float dg[NC][4] = {}, db[NC][4] = {}, dbias[NC][4] = {};
+  for (int row = blockIdx.x * 4 + w; row < a.T; row += gridDim.x * 4) {
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    float xh[NC][4], gd[NC][4], dyv[NC][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = 4 * (lane + 64 * c);
+      const size_t off = (size_t)row * D + col;
+      const uint2 xv = *reinterpret_cast<const uint2*>(a.x + off);
+      float v[4] = {lo_bf(xv.x), hi_bf(xv.x), lo_bf(xv.y), hi_bf(xv.y)};
+      if (drop) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = drop_keep(seed, (uint32_t)(off + e), a.thr) ? v[e] * a.dscale : 0.f;
+      }
+      if (a.r) {
+        const uint2 rv = *reinterpret_cast<const uint2*>(a.r + off);
+        v[0] += lo_bf(rv.x); v[1] += hi_bf(rv.x); v[2] += lo_bf(rv.y); v[3] += hi_bf(rv.y);
+      }
+      const uint2 dv = *reinterpret_cast<const uint2*>(a.dy + off);
+      const float d4[4] = {lo_bf(dv.x), hi_bf(dv.x), lo_bf(dv.y), hi_bf(dv.y)};
+      const float4 g = *reinterpret_cast<const float4*>(a.gamma + col);
+      const float g4[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[c][e] = (v[e] - mean) * rstd;
+        dyv[c][e] = d4[e];
+        gd[c][e] = g4[e] * d4[e];
+        s1 += gd[c][e];
+        s2 += gd[c][e] * xh[c][e];
+      }
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = 4 * (lane + 64 * c);
+      const size_t off = (size_t)row * D + col;
+      float dz[4], dx[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dz[e] = rstd * (gd[c][e] - s1 - xh[c][e] * s2);
+        dx[e] = dz[e];
+        if (drop) dx[e] = drop_keep(seed, (uint32_t)(off + e), a.thr) ? dz[e] * a.dscale : 0.f;
+        dg[c][e] += dyv[c][e] * xh[c][e];
+        db[c][e] += dyv[c][e];
+        dbias[c][e] += dx[e];
+      }
+      *reinterpret_cast<uint2*>(a.dz + off) = make_uint2(pack_bf2(dz[0], dz[1]), pack_bf2(dz[2], dz[3]));
+      if (drop && a.dx)
+        *reinterpret_cast<uint2*>(a.dx + off) = make_uint2(pack_bf2(dx[0], dx[1]), pack_bf2(dx[2], dx[3]));
+    }
+  }
+  float* out = a.part + (size_t)blockIdx.x * 3 * D;
+  block_colsum<NC>(dg, lds, out, D);
+  block_colsum<NC>(db, lds, out + D, D);
+  block_colsum<NC>(dbias, lds, out + 2 * D, D);
+}
+
+// ------------------------------------------------------------------ embeddings
+struct EmbArgs {
+  const void* ids;   // int64 or int32 [T]
+  int ids64;
+  const bf16_t* word;
+  const bf16_t* pos;
+  const float* gamma;
+  const float* beta;
+  bf16_t* y;
+  float* mean;
+  float* rstd;
+  int T, S, D;
+  float eps;
+  const uint32_t* seed_ptr;
+  uint32_t site, thr;
+  float dscale;
+  const bf16_t* dy;
+  float* dz;       // fp32 [T][D]
+  float* part;     // [grid][2][D]
+};
+
+DEV long load_id(const EmbArgs& a, int t) {
+  return a.ids64 ? reinterpret_cast<const long long*>(a.ids)[t] : reinterpret_cast<const int*>(a.ids)[t];
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void emb_fwd_kernel(EmbArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.T) return;
+  const int D = a.D;
+  const long id = load_id(a, row);
+  const int s = row % a.S;
+  const bool drop = a.thr != 0;
+  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
+  float z[NC][4], sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    const uint2 wv = *reinterpret_cast<const uint2*>(a.word + (size_t)id * D + col);
+    const uint2 pv = *reinterpret_cast<const uint2*>(a.pos + (size_t)s * D + col);
+    z[c][0] = lo_bf(wv.x) + lo_bf(pv.x); z[c][1] = hi_bf(wv.x) + hi_bf(pv.x);
+    z[c][2] = lo_bf(wv.y) + lo_bf(pv.y); z[c][3] = hi_bf(wv.y) + hi_bf(pv.y);
+    sum += z[c][0] + z[c][1] + z[c][2] + z[c][3];
+  }
+  const float mean = wave_sum(sum) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { const float d = z[c][e] - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) / D + a.eps);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = 4 * (lane + 64 * c);
+    const size_t off = (size_t)row * D + col;
+    const float4 g = *reinterpret_cast<const float4*>(a.gamma + col);
+    const float4 b = *reinterpret_cast<const float4*>(a.beta + col);
+    float y[4] = {(z[c][0] - mean) * rstd * g.x + b.x, (z[c][1] - mean) * rstd * g.y + b.y,
+                  (z[c][2] - mean) * rstd * g.z + b.z, (z[c][3] - mean) * rstd * g.w + b.w};
+    if (drop) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = drop_keep(seed, (uint32_t)(off + e), a.thr) ? y[e] * a.dscale : 0.f;
+    }
+    *reinterpret_cast<uint2*>(a.y + off) = make_uint2(pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]));
+  }
+  if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void emb_bwd_kernel(EmbArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int D = a.D;
+  const bool drop = a.thr != 0;
+  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
+  float dg[NC][4] = {}, db[NC][4] = {};
+  for (int row = blockIdx.x * 4 + w; row < a.T; row += gridDim.x * 4) {
+    const long id = load_id(a, row);
+    const int s = row % a.S;
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    float xh[NC][4], gd[NC][4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = 4 * (lane + 64 * c);
+      const size_t off = (size_t)row * D + col;
+      const uint2 wv = *reinterpret_cast<const uint2*>(a.word + (size_t)id * D + col);
+      const uint2 pv = *reinterpret_cast<const uint2*>(a.pos + (size_t)s * D + col);
+      const float z[4] = {lo_bf(wv.x) + lo_bf(pv.x), hi_bf(wv.x) + hi_bf(pv.x), lo_bf(wv.y) + lo_bf(pv.y),
+                          hi_bf(wv.y) + hi_bf(pv.y)};
+      const uint2 dv = *reinterpret_cast<const uint2*>(a.dy + off);
+      float d4[4] = {lo_bf(dv.x), hi_bf(dv.x), lo_bf(dv.y), hi_bf(dv.y)};
+      if (drop) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d4[e] = drop_keep(seed, (uint32_t)(off + e), a.thr) ? d4[e] * a.dscale : 0.f;
+      }
+      const float4 g = *reinterpret_cast<const float4*>(a.gamma + col);
+      const float g4[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[c][e] = (z[e] - mean) * rstd;
+        gd[c][e] = g4[e] * d4[e];
+        s1 += gd[c][e];
+        s2 += gd[c][e] * xh[c][e];
+        dg[c][e] += d4[e] * xh[c][e];
+        db[c][e] += d4[e];
+      }
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = 4 * (lane + 64 * c);
+      float4 o;
+      o.x = rstd * (gd[c][0] - s1 - xh[c][0] * s2);
+      o.y = rstd * (gd[c][1] - s1 - xh[c][1] * s2);
+      o.z = rstd * (gd[c][2] - s1 - xh[c][2] * s2);
+      o.w = rstd * (gd[c][3] - s1 - xh[c][3] * s2);
+      *reinterpret_cast<float4*>(a.dz + (size_t)row * D + col) = o;
+    }
+  }
+  float* out = a.part + (size_t)blockIdx.x * 3 * D;
+  block_colsum<NC>(dg, lds, out, D);
+  block_colsum<NC>(db, lds, out + D, D);
+}
+
+// dpos[s][:] = sum_b dz[b*S + s][:], rows s >= S zeroed (first write) -- fixed order.
+__global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* dpos, int B, int S, int P,
+                                                       int D, int accumulate) {
+  const int s = blockIdx.x;
+  for (int col = threadIdx.x; col < D; col += 256) {
+    float acc = accumulate ? dpos[(size_t)s * D + col] : 0.f;
+    if (s < S)
+      for (int b = 0; b < B; ++b) acc += dz[((size_t)b * S + s) * D + col];
+    dpos[(size_t)s * D + col] = acc;
+  }
+}
+
+// Word-embedding gradient from token ids sorted on device (torch.sort):
+// pass 1 sums each run piece inside fixed 32-position chunks into piece[start];
+// pass 2 lets the run's first position add its pieces in chunk order.  Every
+// output row is written by exactly one block -> deterministic, atomic-free.
+constexpr int WCH = 32;
+__global__ __launch_bounds__(256) void word_grad_pieces_kernel(const long long* sorted, const long long* perm,
+                                                              const float* dz, float* piece, int T, int D) {
+  const int c0 = blockIdx.x * WCH, c1 = min(T, c0 + WCH);
+  for (int col = threadIdx.x; col < D; col += 256) {
+    float acc = 0.f;
+    int start = c0;
+    for (int i = c0; i < c1; ++i) {
+      acc += dz[(size_t)perm[i] * D + col];
+      if (i + 1 == c1 || sorted[i + 1] != sorted[i]) {
+        piece[(size_t)start * D + col] = acc;
+        acc = 0.f;
+        start = i + 1;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void word_grad_combine_kernel(const long long* sorted, const float* piece,
+                                                               float* dword, int T, int D, int accumulate) {
+  const int i = blockIdx.x;
+  if (i > 0 && sorted[i] == sorted[i - 1]) return;
+  const long long id = sorted[i];
+  for (int col = threadIdx.x; col < D; col += 256) {
+    float acc = piece[(size_t)i * D + col];
+    for (int j = (i / WCH + 1) * WCH; j < T && sorted[j] == id; j += WCH) acc += piece[(size_t)j * D + col];
+    float* dst = dword + (size_t)id * D + col;
+    *dst = accumulate ? *dst + acc : acc;
+  }
+}
+
+// out_k[j] = (acc ? out_k[j] : 0) + sum_blk part[blk][k][j]  for k < nout (fixed order).
+__global__ __launch_bounds__(256) void colsum_kernel(const float* part, int nblk, int stride_blk, int D,
+                                                     float* o0, float* o1, float* o2, int accumulate) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int k = blockIdx.y;
+  if (j >= D) return;
+  float* out = k == 0 ? o0 : (k == 1 ? o1 : o2);
+  if (!out) return;
+  float s = accumulate ? out[j] : 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(size_t)b * stride_blk + k * D + j];
+  out[j] = s;
+}
+
+// Column sums of a bf16 [T][N] matrix into per-block partials [grid][N] (bias grads).
+__global__ __launch_bounds__(256) void colsum_bf16_partial_kernel(const bf16_t* x, int T, int N, int rows_per_blk,
+                                                                  float* part) {
+  const int c4 = (blockIdx.y * 256 + threadIdx.x) * 4;
+  if (c4 >= N) return;
+  const int r0 = blockIdx.x * rows_per_blk, r1 = min(T, r0 + rows_per_blk);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const uint2 v = *reinterpret_cast<const uint2*>(x + (size_t)r * N + c4);
+    s0 += lo_bf(v.x); s1 += hi_bf(v.x); s2 += lo_bf(v.y); s3 += hi_bf(v.y);
+  }
+  *reinterpret_cast<float4*>(part + (size_t)blockIdx.x * N + c4) = make_float4(s0, s1, s2, s3);
+}
+
+constexpr int LN_GRID = 256;
+
+}  // namespace
+
+extern "C" {
+
+int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, float* mean,
+              float* rstd, int T, int D, float eps, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
+              float dscale, hipStream_t st) {
+  if (D != 768) return 1;
+  LnArgs a{};
+  a.x = (const bf16_t*)x; a.r = (const bf16_t*)r; a.gamma = gamma; a.beta = beta; a.y = (bf16_t*)y;
+  a.mean = mean; a.rstd = rstd; a.T = T; a.D = D; a.eps = eps;
+  a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
+  hipLaunchKernelGGL(ln_fwd_kernel<3>, dim3((T + 3) / 4), dim3(256), 0, st, a);
+  return 0;
+}
+
+// Writes dz (and dx when dropout is active); gradients of gamma/beta/producer-bias
+// go to dgamma/dbeta/dbias (nullable), first-write unless accumulate.
+int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean,
+              const float* rstd, void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work,
+              int T, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
+              int accumulate, hipStream_t st) {
+  if (D != 768) return 1;
+  LnArgs a{};
+  a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.r = (const bf16_t*)r; a.gamma = gamma;
+  a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = (bf16_t*)dz; a.dx = (bf16_t*)dx; a.part = work;
+  a.T = T; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
+  const int grid = std::min(LN_GRID, (T + 3) / 4);
+  hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(grid), dim3(256), 4 * D * sizeof(float), st, a);
+  hipLaunchKernelGGL(colsum_kernel, dim3((D + 255) / 256, 3), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
+                     dbeta, dbias, accumulate);
+  return 0;
+}
+
+int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
+               const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
+               const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, hipStream_t st) {
+  if (D != 768) return 1;
+  EmbArgs a{};
+  a.ids = ids; a.ids64 = ids64; a.word = (const bf16_t*)word; a.pos = (const bf16_t*)pos; a.gamma = gamma;
+  a.beta = beta; a.y = (bf16_t*)y; a.mean = mean; a.rstd = rstd; a.T = T; a.S = S; a.D = D; a.eps = eps;
+  a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
+  hipLaunchKernelGGL(emb_fwd_kernel<3>, dim3((T + 3) / 4), dim3(256), 0, st, a);
+  return 0;
+}
+
+// Embedding backward.  sorted/perm: torch.sort of the flattened ids (int64).
+// work must hold max(grid*3*D, T*D) floats; dz_buf T*D floats.
+int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sorted, const long long* perm,
+               const void* word, const void* pos, const float* gamma, const float* mean, const float* rstd,
+               float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
+               int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
+               int accumulate, hipStream_t st) {
+  if (D != 768) return 1;
+  EmbArgs a{};
+  a.dy = (const bf16_t*)dy; a.ids = ids; a.ids64 = ids64; a.word = (const bf16_t*)word;
+  a.pos = (const bf16_t*)pos; a.gamma = gamma; a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = dz_buf;
+  a.part = work; a.T = T; a.S = S; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
+  const int grid = std::min(LN_GRID, (T + 3) / 4);
+  hipLaunchKernelGGL(emb_bwd_kernel<3>, dim3(grid), dim3(256), 4 * D * sizeof(float), st, a);
+  hipLaunchKernelGGL(colsum_kernel, dim3((D + 255) / 256, 2), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
+                     dbeta, (float*)nullptr, accumulate);
+  hipLaunchKernelGGL(pos_grad_kernel, dim3(P), dim3(256), 0, st, dz_buf, dpos, B, S, P, D, accumulate);
+  if (!accumulate) hipMemsetAsync(dword, 0, (size_t)V * D * sizeof(float), st);
+  // piece sums reuse `work` (T*D floats)
+  hipLaunchKernelGGL(word_grad_pieces_kernel, dim3((T + WCH - 1) / WCH), dim3(256), 0, st, sorted, perm, dz_buf,
+                     work, T, D);
+  hipLaunchKernelGGL(word_grad_combine_kernel, dim3(T), dim3(256), 0, st, sorted, work, dword, T, D, 1);
+  return 0;
+}
+
+// out[N] (+)= column sums of bf16 x[T][N]; work >= ceil(T/rows)*N floats.
+int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, hipStream_t st) {
+  if (N % 4 != 0) return 1;
+  const int rows = 32;
+  const int nblk = (T + rows - 1) / rows;
+  hipLaunchKernelGGL(colsum_bf16_partial_kernel, dim3(nblk, (N / 4 + 255) / 256), dim3(256), 0, st,
+                     (const bf16_t*)x, T, N, rows, work);
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256, 1), dim3(256), 0, st, work, nblk, N, N, out,
+                     (float*)nullptr, (float*)nullptr, accumulate);
+  return 0;
+}
+
+}  // extern "C"

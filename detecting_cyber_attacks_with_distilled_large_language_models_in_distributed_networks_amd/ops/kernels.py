@@ -1,0 +1,188 @@
+"""Thin, allocation-aware Python wrappers over the gfx950 kernel extension.
+
+All functions expect GPU tensors; shapes are validated in the C++ binding
+before any launch.  Scratch buffers (split-K slabs, column-sum partials) come
+from a per-device workspace cache that only grows, so steady-state steps do no
+allocation and the whole step can be captured into a HIP graph.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from ._ext import ext
+from .dropout import threshold
+
+D_MODEL = 768
+
+_WS = {}
+
+
+def workspace(device, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
+    key = (str(device), name, dtype)
+    t = _WS.get(key)
+    if t is None or t.numel() < numel:
+        t = torch.empty(max(numel, 1), dtype=dtype, device=device)
+        _WS[key] = t
+    return t[:numel]
+
+
+def _drop(p: float):
+    thr = threshold(p)
+    return thr, (1.0 / (1.0 - p) if thr else 1.0)
+
+
+# ------------------------------------------------------------------ GEMMs
+EPI_BF16, EPI_BIAS, EPI_BIAS_GELU, EPI_GELU_BWD, EPI_ADD = 0, 1, 2, 3, 4
+
+
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu: bool = False):
+    """y = x w^T + b (bf16), optionally also returning u (pre-GELU) with y = gelu(u)."""
+    M, N = x.shape[0], w.shape[0]
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    if gelu:
+        u = torch.empty_like(y)
+        ext().gemm(0, EPI_BIAS_GELU, x, w, y, b, u, None, None, False)
+        return y, u
+    ext().gemm(0, EPI_BIAS if b is not None else EPI_BF16, x, w, y, b, None, None, None, False)
+    return y
+
+
+def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] = None,
+              res: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx = dy w  [* gelu'(u)]  [+ res]  (bf16)."""
+    M, N = dy.shape[0], w.shape[1]
+    dx = torch.empty(M, N, dtype=torch.bfloat16, device=dy.device)
+    if gelu_u is not None:
+        ext().gemm(1, EPI_GELU_BWD, dy, w, dx, None, gelu_u, None, None, False)
+    elif res is not None:
+        ext().gemm(1, EPI_ADD, dy, w, dx, None, None, res, None, False)
+    else:
+        ext().gemm(1, EPI_BF16, dy, w, dx, None, None, None, None, False)
+    return dx
+
+
+def linear_dw(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    """out[N_out, N_in] (fp32) (+)= dy^T x."""
+    M, N = dy.shape[1], x.shape[1]
+    ws = workspace(dy.device, "splitk", 8 * M * N)
+    ext().gemm(2, 5, dy, x, out, None, None, None, ws, accumulate)
+    return out
+
+
+def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    N = out.numel()
+    T = x.numel() // N
+    ws = workspace(x.device, "colsum", ((T + 31) // 32) * N)
+    ext().colsum_bf16(x, out, ws, accumulate)
+    return out
+
+
+# ------------------------------------------------------------------ attention
+def mask_bias(mask: torch.Tensor) -> torch.Tensor:
+    m = mask.contiguous()
+    if m.dtype == torch.bool:
+        m = m.to(torch.uint8)
+    bias = torch.empty(m.shape, dtype=torch.float32, device=m.device)
+    ext().mask_to_bias(m, bias)
+    return bias
+
+
+def attn_fwd(qkv, kbias, B, S, H, seed, site, p) -> Tuple[torch.Tensor, torch.Tensor]:
+    ctx = torch.empty(B * S, H * 64, dtype=torch.bfloat16, device=qkv.device)
+    lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
+    thr, sc = _drop(p)
+    ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc)
+    return ctx, lse
+
+
+def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p) -> torch.Tensor:
+    dqkv = torch.empty_like(qkv)
+    delta = workspace(qkv.device, "attn_delta", B * H * S)
+    thr, sc = _drop(p)
+    ext().attn_bwd(qkv, kbias, ctx, lse, dctx.contiguous(), delta, dqkv, B, S, H, seed, site, thr, sc)
+    return dqkv
+
+
+# ------------------------------------------------------------------ layernorm / embedding
+def ln_fwd(x, r, gamma, beta, eps, seed, site, p):
+    T = x.numel() // gamma.numel()
+    y = torch.empty_like(x)
+    mean = torch.empty(T, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(T, dtype=torch.float32, device=x.device)
+    thr, sc = _drop(p)
+    ext().ln_fwd(x, r, gamma, beta, y, mean, rstd, eps, seed, site, thr, sc)
+    return y, mean, rstd
+
+
+def ln_bwd(dy, x, r, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False):
+    D = gamma.numel()
+    dz = torch.empty_like(x)
+    thr, sc = _drop(p)
+    dx = torch.empty_like(x) if thr else None
+    ws = workspace(x.device, "ln_part", 256 * 3 * D)
+    ext().ln_bwd(dy.contiguous(), x, r, gamma, mean, rstd, dz, dx, dgamma, dbeta, dbias, ws, seed, site, thr, sc,
+                 accumulate)
+    return dz, (dx if dx is not None else dz)
+
+
+def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p):
+    T = ids.numel()
+    D = gamma.numel()
+    y = torch.empty(T, D, dtype=torch.bfloat16, device=ids.device)
+    mean = torch.empty(T, dtype=torch.float32, device=ids.device)
+    rstd = torch.empty(T, dtype=torch.float32, device=ids.device)
+    thr, sc = _drop(p)
+    ext().emb_fwd(ids.contiguous(), word, pos, gamma, beta, y, mean, rstd, S, eps, seed, site, thr, sc)
+    return y, mean, rstd
+
+
+def emb_bwd(dy, ids, sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos, dgamma, dbeta, S, seed, site, p,
+            accumulate=False):
+    T = ids.numel()
+    D = gamma.numel()
+    dz = workspace(ids.device, "emb_dz", T * D)
+    ws = workspace(ids.device, "emb_work", max(T * D, 256 * 3 * D))
+    thr, sc = _drop(p)
+    ext().emb_bwd(dy.contiguous(), ids.contiguous(), sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos,
+                  dgamma, dbeta, dz, ws, S, seed, site, thr, sc, accumulate)
+
+
+# ------------------------------------------------------------------ head / metrics / optimizer
+def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None):
+    logits = torch.empty(B, 2, dtype=torch.float32, device=hidden.device)
+    loss = dlogits = None
+    if labels is not None:
+        loss = torch.empty((), dtype=torch.float32, device=hidden.device)
+        dlogits = torch.empty(B, 2, dtype=torch.float32, device=hidden.device)
+    thr, sc = _drop(p)
+    ext().head_fwd(hidden, B, S, W, b, seed, site, thr, sc, labels, logits, loss, dlogits)
+    return logits, loss, dlogits
+
+
+def head_bwd(hidden, B, S, W, seed, site, p, dlogits, dW, db, accumulate=False):
+    dhidden = torch.zeros_like(hidden)
+    thr, sc = _drop(p)
+    ext().head_bwd(hidden, B, S, W, seed, site, thr, sc, dlogits.contiguous(), dW, db, dhidden, accumulate)
+    return dhidden
+
+
+def eval_metrics(logits, labels, acc, counts, prob1=None, preds=None):
+    ext().eval_metrics(logits, labels, acc, counts, prob1, preds)
+
+
+def adam(p, g, m, v, shadow, step, lr, b1, b2, eps, wd, decoupled):
+    ext().adam(p, g, m, v, shadow, step, lr, b1, b2, eps, wd, decoupled)
+
+
+def step_inc(step=None, seed=None):
+    ext().step_inc(step, seed)
+
+
+def scale_cast(p, shadow=None, scale=1.0):
+    ext().scale_cast(p, shadow, scale)
+
+
+def axpby(dst, x, y=None, a=1.0, b=0.0):
+    ext().axpby(dst, x, y, a, b)
