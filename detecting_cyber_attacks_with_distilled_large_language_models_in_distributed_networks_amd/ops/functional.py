@@ -1,0 +1,156 @@
+"""Fused autograd blocks of the HIP DistilBERT path.
+
+The model is three kinds of autograd nodes -- embeddings, one node per
+TransformerBlock, and the classifier head -- each with a hand-ordered backward
+that fuses across op boundaries (GELU-backward and residual-add in the dX GEMM
+epilogues, dropout + residual + LayerNorm backward in one kernel, bias grads
+out of the LN-backward column sums).  Parameter gradients are written straight
+into the fp32 gradient arena (first write after ``zero_grad``, accumulate
+otherwise), so autograd only ever carries activation gradients.
+
+Reference call stack mirrored: DistilBertModel.forward -> Embeddings ->
+6 x TransformerBlock -> [:, 0] -> Dropout(0.3) -> Linear(768, 2)
+(client1.py:60-65).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import kernels as K
+
+
+@dataclass
+class RunCtx:
+    """Per-forward shared state (one per model call)."""
+    B: int
+    S: int
+    H: int
+    kbias: torch.Tensor          # [B, S] additive key mask
+    seed: torch.Tensor           # device int32 counter
+    training: bool
+    eps: float = 1e-12
+    p_hidden: float = 0.1
+    p_attn: float = 0.1
+    p_head: float = 0.3
+
+
+class GradSink:
+    """Routes a parameter's gradient into its arena slice with first-write semantics."""
+
+    def __init__(self, arena, name: str):
+        self.arena, self.name = arena, name
+
+    @property
+    def buf(self) -> torch.Tensor:
+        return self.arena.gview(self.name)
+
+    def accumulate(self) -> bool:
+        return self.arena.mark_written(self.name)
+
+
+class EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, token, ids, word, pos, gamma, beta, sinks, rc: RunCtx):
+        p = rc.p_hidden if rc.training else 0.0
+        y, mean, rstd = K.emb_fwd(ids, word, pos, gamma, beta, rc.S, rc.eps, rc.seed, 1, p)
+        ctx.rc, ctx.sinks, ctx.p = rc, sinks, p
+        ctx.tensors = (ids, word, pos, gamma, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ids, word, pos, gamma, mean, rstd = ctx.tensors
+        s = ctx.sinks
+        srt, perm = torch.sort(ids.reshape(-1))
+        acc = s["word"].accumulate()
+        for k in ("pos", "ln_w", "ln_b"):
+            assert s[k].accumulate() == acc
+        K.emb_bwd(dy, ids, srt, perm, word, pos, gamma, mean, rstd, s["word"].buf, s["pos"].buf, s["ln_w"].buf,
+                  s["ln_b"].buf, ctx.rc.S, ctx.rc.seed, 1, ctx.p, acc)
+        return (None,) * 8
+
+
+class LayerFn(torch.autograd.Function):
+    """One post-LN TransformerBlock: 7 kernels forward, 13 backward."""
+
+    @staticmethod
+    def forward(ctx, x, L, rc: RunCtx, idx: int):
+        p_a = rc.p_attn if rc.training else 0.0
+        p_h = rc.p_hidden if rc.training else 0.0
+        attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
+        qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
+        cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a)
+        ao = K.linear_fwd(cx, L["o_w"], L["o_b"])
+        h, m1, r1 = K.ln_fwd(ao, x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0)
+        g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
+        f = K.linear_fwd(g, L["l2_w"], L["l2_b"])
+        y, m2, r2 = K.ln_fwd(f, h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed, ffn_site, p_h)
+        if torch.is_grad_enabled() or ctx.needs_input_grad[0]:
+            ctx.save_for_backward(x)
+            ctx.acts = (qkv, cx, lse, ao, h, m1, r1, u, g, f, m2, r2)
+        ctx.L, ctx.rc, ctx.sites, ctx.p = L, rc, (attn_site, ffn_site), (p_a, p_h)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        qkv, cx, lse, ao, h, m1, r1, u, g, f, m2, r2 = ctx.acts
+        L, rc = ctx.L, ctx.rc
+        G = L["sinks"]
+        attn_site, ffn_site = ctx.sites
+        p_a, p_h = ctx.p
+        acc = G["l2_w"].accumulate()
+        # output_layer_norm(dropout(lin2) + h): dz2 -> residual grad of h, df -> lin2 output grad
+        dz2, df = K.ln_bwd(dy, f, h, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, rc.seed,
+                           ffn_site, p_h, acc)
+        du = K.linear_dx(df, L["l2_w"], gelu_u=u)              # dg W2 * gelu'(u)
+        K.linear_dw(df, g, G["l2_w"].buf, acc)
+        K.colsum(du, G["l1_b"].buf, acc)
+        dh = K.linear_dx(du, L["l1_w"], res=dz2)               # du W1 + dz2
+        K.linear_dw(du, h, G["l1_w"].buf, acc)
+        # sa_layer_norm(out_lin + x)
+        dz1, _ = K.ln_bwd(dh, ao, x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf, G["o_b"].buf, rc.seed, 0,
+                          0.0, acc)
+        dcx = K.linear_dx(dz1, L["o_w"])
+        K.linear_dw(dz1, cx, G["o_w"].buf, acc)
+        dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a)
+        K.colsum(dqkv, G["qkv_b"].buf, acc)
+        dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1)
+        K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
+        for k in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_w", "ln1_b", "l1_w", "l1_b", "l2_b", "ln2_w", "ln2_b"):
+            G[k].accumulate()
+        del ctx.acts
+        return dx, None, None, None
+
+
+class HeadFn(torch.autograd.Function):
+    """CLS -> Dropout(0.3) -> Linear(768, 2); optional fused CE (mean) loss."""
+
+    @staticmethod
+    def forward(ctx, hidden, W, b, sinks, rc: RunCtx, labels: Optional[torch.Tensor]):
+        p = rc.p_head if rc.training else 0.0
+        logits, loss, dlog = K.head_fwd(hidden, rc.B, rc.S, W, b, rc.seed, 2, p, labels)
+        ctx.rc, ctx.sinks, ctx.p, ctx.W = rc, sinks, p, W
+        ctx.save_for_backward(hidden)
+        ctx.dlog = dlog
+        ctx.fused_loss = labels is not None
+        ctx.mark_non_differentiable(logits)
+        if labels is not None:
+            return loss, logits
+        return logits, logits.new_empty(0)
+
+    @staticmethod
+    def backward(ctx, g0, g1):
+        (hidden,) = ctx.saved_tensors
+        if ctx.fused_loss:
+            dlog = ctx.dlog * g0
+        else:
+            dlog = g0.float().contiguous()
+        s = ctx.sinks
+        acc = s["w"].accumulate()
+        s["b"].accumulate()
+        dh = K.head_bwd(hidden, ctx.rc.B, ctx.rc.S, ctx.W, ctx.rc.seed, 2, ctx.p, dlog, s["w"].buf, s["b"].buf, acc)
+        return dh, None, None, None, None, None

@@ -8,7 +8,7 @@ import math
 import pytest
 import torch
 
-from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as kn
 from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import reference as R
 from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops.dropout import keep_mask
 
@@ -35,7 +35,7 @@ def seed_t(v=7):
 def test_gemm_nt_bias(M, N, K):
     x, w = bf(M, K, seed=1), bf(N, K, scale=0.05, seed=2)
     b = torch.randn(N, device=DEV)
-    y = K.linear_fwd(x, w, b)
+    y = kn.linear_fwd(x, w, b)
     ref = x.float() @ w.float().t() + b
     assert rel_err(y, ref) < 1e-2
 
@@ -43,7 +43,7 @@ def test_gemm_nt_bias(M, N, K):
 def test_gemm_nt_gelu():
     x, w = bf(512, 768, seed=3), bf(3072, 768, scale=0.05, seed=4)
     b = torch.randn(3072, device=DEV) * 0.1
-    g, u = K.linear_fwd(x, w, b, gelu=True)
+    g, u = kn.linear_fwd(x, w, b, gelu=True)
     uref = x.float() @ w.float().t() + b
     assert rel_err(u, uref) < 1e-2
     assert rel_err(g, torch.nn.functional.gelu(u.float())) < 1e-2
@@ -53,14 +53,14 @@ def test_gemm_identity_asymmetric():
     # A = I with an asymmetric B catches a transposed C write (guide §3).
     x = torch.eye(128, dtype=torch.bfloat16, device=DEV)
     w = (torch.arange(128 * 128, device=DEV).view(128, 128) % 97).to(torch.bfloat16)
-    y = K.linear_fwd(x, w, None)
+    y = kn.linear_fwd(x, w, None)
     assert torch.equal(y.float(), w.float().t())
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 768, 768), (4096, 3072, 768), (320, 768, 2304)])
 def test_gemm_nn(M, N, K):
     dy, w = bf(M, K, seed=5), bf(K, N, scale=0.05, seed=6)
-    dx = K.linear_dx(dy, w)
+    dx = kn.linear_dx(dy, w)
     assert rel_err(dx, dy.float() @ w.float()) < 1e-2
 
 
@@ -68,12 +68,12 @@ def test_gemm_nn_gelu_bwd_and_add():
     dy, w = bf(256, 768, seed=7), bf(768, 3072, scale=0.05, seed=8)
     u = bf(256, 3072, seed=9)
     x = torch.nn.functional.gelu(u.float()).requires_grad_(False)
-    du = K.linear_dx(dy, w, gelu_u=u)
+    du = kn.linear_dx(dy, w, gelu_u=u)
     uu = u.float().requires_grad_(True)
     g = torch.autograd.grad(torch.nn.functional.gelu(uu), uu, dy.float() @ w.float())[0]
     assert rel_err(du, g) < 1e-2
     res = bf(256, 3072, seed=10)
-    dx = K.linear_dx(dy, w, res=res)
+    dx = kn.linear_dx(dy, w, res=res)
     assert rel_err(dx, dy.float() @ w.float() + res.float()) < 1e-2
 
 
@@ -81,17 +81,17 @@ def test_gemm_nn_gelu_bwd_and_add():
 def test_gemm_tn(M, N, T):
     dy, x = bf(T, M, seed=11), bf(T, N, seed=12)
     out = torch.empty(M, N, device=DEV)
-    K.linear_dw(dy, x, out)
+    kn.linear_dw(dy, x, out)
     ref = dy.float().t() @ x.float()
     assert rel_err(out, ref) < 2e-3
-    K.linear_dw(dy, x, out, accumulate=True)
+    kn.linear_dw(dy, x, out, accumulate=True)
     assert rel_err(out, 2 * ref) < 2e-3
 
 
 def test_colsum():
     x = bf(4096, 3072, seed=13)
     out = torch.empty(3072, device=DEV)
-    K.colsum(x, out)
+    kn.colsum(x, out)
     assert rel_err(out, x.float().sum(0)) < 1e-3
 
 
@@ -108,8 +108,8 @@ def test_attention_fwd(B, S, p):
     H = 12
     qkv = bf(B * S, 3 * H * 64, seed=14)
     mask = make_mask(B, S, 1)
-    kb = K.mask_bias(mask)
-    ctx, lse = K.attn_fwd(qkv, kb, B, S, H, seed_t(3), 16, p)
+    kb = kn.mask_bias(mask)
+    ctx, lse = kn.attn_fwd(qkv, kb, B, S, H, seed_t(3), 16, p)
     rctx, rlse = R.attention_ref(qkv.float(), mask, B, S, H, p, 3, 16)
     assert rel_err(ctx, rctx) < 2e-2
     assert (lse - rlse).abs().max().item() < 1e-3
@@ -120,10 +120,10 @@ def test_attention_bwd(B, S, p):
     H = 12
     qkv = bf(B * S, 3 * H * 64, seed=15)
     mask = make_mask(B, S, 2)
-    kb = K.mask_bias(mask)
-    ctx, lse = K.attn_fwd(qkv, kb, B, S, H, seed_t(5), 20, p)
+    kb = kn.mask_bias(mask)
+    ctx, lse = kn.attn_fwd(qkv, kb, B, S, H, seed_t(5), 20, p)
     dctx = bf(B * S, H * 64, seed=16)
-    dqkv = K.attn_bwd(qkv, kb, ctx, lse, dctx, B, S, H, seed_t(5), 20, p)
+    dqkv = kn.attn_bwd(qkv, kb, ctx, lse, dctx, B, S, H, seed_t(5), 20, p)
     q = qkv.float().requires_grad_(True)
     rctx, _ = R.attention_ref(q, mask, B, S, H, p, 5, 20)
     (g,) = torch.autograd.grad(rctx, q, dctx.float())
@@ -138,14 +138,14 @@ def test_layernorm(p, res):
     x, r = bf(T, D, seed=17), bf(T, D, seed=18)
     gamma = torch.randn(D, device=DEV) * 0.2 + 1
     beta = torch.randn(D, device=DEV) * 0.1
-    y, mean, rstd = K.ln_fwd(x, r if res else None, gamma, beta, 1e-12, seed_t(9), 33, p)
+    y, mean, rstd = kn.ln_fwd(x, r if res else None, gamma, beta, 1e-12, seed_t(9), 33, p)
     xf, rf = x.float().requires_grad_(True), r.float().requires_grad_(True)
     gf, bf_ = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
     yr = R.add_ln_ref(xf, rf if res else None, gf, bf_, 1e-12, p, 9, 33)
     assert rel_err(y, yr) < 1e-2
     dy = bf(T, D, seed=19)
     dgamma, dbeta, dbias = (torch.empty(D, device=DEV) for _ in range(3))
-    dz, dx = K.ln_bwd(dy, x, r if res else None, gamma, mean, rstd, dgamma, dbeta, dbias, seed_t(9), 33, p)
+    dz, dx = kn.ln_bwd(dy, x, r if res else None, gamma, mean, rstd, dgamma, dbeta, dbias, seed_t(9), 33, p)
     gx, gr, gg, gb = torch.autograd.grad(yr, [xf, rf, gf, bf_], dy.float())
     assert rel_err(dx, gx) < 2e-2
     assert rel_err(dz, gr) < 2e-2
@@ -163,7 +163,7 @@ def test_embedding():
     gamma = torch.randn(D, device=DEV) * 0.1 + 1
     beta = torch.randn(D, device=DEV) * 0.1
     p = 0.1
-    y, mean, rstd = K.emb_fwd(ids, word, pos, gamma, beta, S, 1e-12, seed_t(4), 1, p)
+    y, mean, rstd = kn.emb_fwd(ids, word, pos, gamma, beta, S, 1e-12, seed_t(4), 1, p)
     wf, pf = word.float().requires_grad_(True), pos.float().requires_grad_(True)
     gf, bf_ = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
     yr = R.embedding_ref(ids, wf, pf, gf, bf_, 1e-12, p, 4, 1)
@@ -173,7 +173,7 @@ def test_embedding():
     dpos = torch.full((P, D), 5.0, device=DEV)
     dgamma, dbeta = torch.empty(D, device=DEV), torch.empty(D, device=DEV)
     srt, perm = torch.sort(ids.reshape(-1))
-    K.emb_bwd(dy, ids, srt, perm, word, pos, gamma, mean, rstd, dword, dpos, dgamma, dbeta, S, seed_t(4), 1, p)
+    kn.emb_bwd(dy, ids, srt, perm, word, pos, gamma, mean, rstd, dword, dpos, dgamma, dbeta, S, seed_t(4), 1, p)
     gw, gp, gg, gb = torch.autograd.grad(yr, [wf, pf, gf, bf_], dy.float())
     assert rel_err(dword, gw) < 1e-2
     assert rel_err(dpos, gp) < 1e-2
@@ -186,7 +186,7 @@ def test_head():
     W = torch.randn(2, D, device=DEV) * 0.05
     b = torch.randn(2, device=DEV)
     labels = torch.randint(0, 2, (B,), device=DEV)
-    logits, loss, dlog = K.head_fwd(hidden, B, S, W, b, seed_t(2), 2, 0.3, labels)
+    logits, loss, dlog = kn.head_fwd(hidden, B, S, W, b, seed_t(2), 2, 0.3, labels)
     hf = hidden.float().requires_grad_(True)
     Wf, bf_ = W.clone().requires_grad_(True), b.clone().requires_grad_(True)
     lr = R.head_ref(hf, B, S, Wf, bf_, 0.3, 2, 2)
@@ -195,7 +195,7 @@ def test_head():
     assert abs(loss.item() - lref.item()) < 1e-4
     gh, gW, gb = torch.autograd.grad(lref, [hf, Wf, bf_])
     dW, db = torch.empty(2, D, device=DEV), torch.empty(2, device=DEV)
-    dh = K.head_bwd(hidden, B, S, W, seed_t(2), 2, 0.3, dlog, dW, db)
+    dh = kn.head_bwd(hidden, B, S, W, seed_t(2), 2, 0.3, dlog, dW, db)
     assert rel_err(dW, gW) < 1e-4 and rel_err(db, gb) < 1e-4
     assert rel_err(dh, gh) < 1e-2
 
@@ -212,8 +212,8 @@ def test_adam_matches_torch():
         g = torch.randn(n, device=DEV)
         ref.grad = g.clone()
         opt.step()
-        K.step_inc(step, None)
-        K.adam(p, g, m, v, shadow, step, 1e-3, 0.9, 0.999, 1e-8, 0.0, False)
+        kn.step_inc(step, None)
+        kn.adam(p, g, m, v, shadow, step, 1e-3, 0.9, 0.999, 1e-8, 0.0, False)
     assert (p - ref.detach()).abs().max().item() < 1e-6
     assert torch.equal(shadow, p.to(torch.bfloat16))
 
@@ -224,7 +224,7 @@ def test_eval_metrics():
     acc = torch.zeros(1, dtype=torch.float64, device=DEV)
     counts = torch.zeros(5, dtype=torch.int64, device=DEV)
     prob = torch.empty(37, device=DEV)
-    K.eval_metrics(logits, labels, acc, counts, prob)
+    kn.eval_metrics(logits, labels, acc, counts, prob)
     pred = logits.argmax(1)
     assert counts[0].item() == (pred == labels).sum().item()
     assert counts[1].item() == ((pred == 1) & (labels == 1)).sum().item()
@@ -238,7 +238,7 @@ def test_dropout_hash_matches_kernel():
     T, D = 8, 768
     x = torch.ones(T, D, dtype=torch.bfloat16, device=DEV)
     gamma, beta = torch.ones(D, device=DEV), torch.zeros(D, device=DEV)
-    y, _, _ = K.ln_fwd(x, None, gamma, beta, 1e-12, seed_t(11), 5, 0.5)
+    y, _, _ = kn.ln_fwd(x, None, gamma, beta, 1e-12, seed_t(11), 5, 0.5)
     keep = keep_mask(11, 5, T * D, 0.5, device=DEV).view(T, D)
     # kept elements share one value per row, dropped another
     for t in range(T):
