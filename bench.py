@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Headline benchmark: local federated-client training throughput.
+
+Metric (BASELINE.json): batches/sec/client of DistilBERT-base DDoSClassifier
+training at seq_len 128, batch 32, bf16 compute, on synthetic CICIDS2017-shaped
+flows rendered to text (random-init weights), one client per GPU.
+
+A "step" is the full reference step (client1.py:102-112): forward, CE loss,
+backward, Adam update -- here the fused HIP kernels replayed as a HIP graph.
+For N > 1 every rank is an independent federated client and the timed region
+also ends with one FedAvg round (RCCL all-reduce of the 66.4 M fp32 masters),
+i.e. communication is charged once per K steps (the reference averages once per
+3 epochs = 1,270 steps at bs32, so this over-charges it).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1 is launched by torch.distributed.run (one process per GPU, RCCL).
+Rank 0 prints ONE JSON line; value = aggregate batches/s over all clients.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+PKG = "detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd"
+BASELINE_BATCHES_PER_SEC_PER_CLIENT = 2.5  # BASELINE.md (bs16 fp32, Windows PC)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch-size", type=int, default=32)
+    ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--impl", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--layers", type=int, default=6)
+    args = ap.parse_args()
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from importlib import import_module
+    comm = import_module(f"{PKG}.parallel.comm")
+    fedavg = import_module(f"{PKG}.parallel.fedavg")
+    models = import_module(f"{PKG}.models")
+    engine = import_module(f"{PKG}.engine")
+    data = import_module(f"{PKG}.data")
+
+    di = comm.init_distributed()
+    dev = di.device
+    B, S = args.batch_size, args.seq_len
+    n_batches = args.warmup + args.steps
+    # Synthetic CICIDS2017 rows -> the reference's text template -> WordPiece ids.
+    df = data.generate_cicids2017(max(n_batches * B * 2, 4096), seed=di.rank)
+    cd = data.build_client_data(df, di.rank, data_fraction=1.0, max_len=S)
+    train = cd.train
+    loader = data.DeviceLoader(train, B, shuffle=True, device=dev, seed=di.rank, drop_last=True)
+
+    cfg = models.DistilBertConfig(n_layers=args.layers)
+    model = models.DDoSClassifier(config=cfg, device=dev, impl=args.impl, seed=0)
+    fedavg.broadcast_model(model)
+    opt = engine.ArenaAdam(model, lr=2e-5)
+    step = engine.GraphedTrainStep(engine.make_step_fn(model, opt), warmup=2,
+                                   enabled=(not args.no_graph) and args.impl == "hip" and dev.type == "cuda")
+    model.train()
+
+    def batches():
+        while True:
+            for b in loader:
+                yield b
+
+    it = batches()
+    for _ in range(args.warmup):
+        b = next(it)
+        step(b["input_ids"], b["attention_mask"], b["labels"])
+    if args.gpus > 1 or di.distributed:
+        fedavg.fedavg_(model)
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    sync()
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    loss_acc = torch.zeros((), device=dev)
+    for _ in range(args.steps):
+        b = next(it)
+        loss_acc += step(b["input_ids"], b["attention_mask"], b["labels"])
+    if di.distributed:
+        fedavg.fedavg_(model)
+    sync()
+    comm.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    dt = comm.all_reduce_max(dt)
+    loss = float(loss_acc.item()) / args.steps
+    n = di.world_size
+    per_client = args.steps / dt
+    if di.is_main:
+        out = {
+            "metric": "batches/sec/client (DistilBERT seq128 bs32) + aggregated F1 after 1 FedAvg round, 1/2/4/8 MI355X",
+            "value": round(per_client * n, 4),
+            "unit": "batches/s (sum over clients; bs32 x seq128)",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * dt / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(per_client / BASELINE_BATCHES_PER_SEC_PER_CLIENT, 3),
+            "dtype": "bf16" if args.impl == "hip" else "fp32",
+            "data": "synthetic CICIDS2017-shaped flows rendered to text, WordPiece seq128; random-init weights",
+            "config": {"model": f"DistilBERT-base ({args.layers} layers) + Linear(768,2) DDoSClassifier",
+                       "global_batch": B * n, "seq_len": S, "parallelism": f"fedavg{n} (1 client/GPU)"},
+            "per_client_batches_per_sec": round(per_client, 4),
+            "samples_per_sec_total": round(per_client * n * B, 2),
+            "tokens_per_sec_total": round(per_client * n * B * S, 1),
+            "vs_baseline_basis": "per-client batches/s / 2.5 (reference bs16 fp32 per-client rate)",
+            "impl": args.impl,
+            "hip_graph": step.graph is not None,
+            "graph_error": step.failed,
+            "mean_loss": round(loss, 5),
+        }
+        print(json.dumps(out), flush=True)
+    comm.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,77 @@
+"""Local training loop (reference ``train_model``, client1.py:96-115).
+
+Same signature and epoch log line (``Client 1 Epoch [e/E], Average Loss: x``),
+but the hot loop is device-resident: batches come from ``DeviceLoader`` (no
+H2D), the per-step loss is accumulated on the device (the reference calls
+``loss.item()`` twice per step, client1.py:111-112 -- one host sync each), the
+head + CE loss are fused (``forward_loss``), and on GPU the whole step is a
+replayed HIP graph.  One host sync per epoch.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from .graph import GraphedTrainStep
+
+
+def make_step_fn(model, optimizer, criterion=None):
+    fused = criterion is None or isinstance(criterion, torch.nn.CrossEntropyLoss)
+
+    def step(ids, mask, labels):
+        optimizer.zero_grad()
+        if fused:
+            loss, _ = model.forward_loss(ids, mask, labels)
+        else:
+            loss = criterion(model(ids, mask), labels)
+        loss.backward()
+        optimizer.step()
+        return loss.detach()
+
+    return step
+
+
+def train_model(model, train_loader, criterion=None, optimizer=None, num_epochs: int = 3, device=None,
+                log=None, use_graph: bool = True, max_steps: Optional[int] = None,
+                on_epoch: Optional[Callable] = None) -> Dict:
+    from .optim import ArenaAdam
+    optimizer = optimizer or ArenaAdam(model)
+    if log:
+        log.phase("Starting model training")
+    model.train()
+    step = GraphedTrainStep(make_step_fn(model, optimizer, criterion), enabled=use_graph and model.device.type == "cuda")
+    epoch_losses: List[float] = []
+    steps = 0
+    t0 = time.perf_counter()
+    dev = model.device
+    for epoch in range(num_epochs):
+        loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
+        nb = 0
+        te = time.perf_counter()
+        for batch in train_loader:
+            loss = step(batch["input_ids"], batch["attention_mask"], batch["labels"])
+            loss_sum += loss
+            nb += 1
+            steps += 1
+            if max_steps is not None and steps >= max_steps:
+                break
+        avg = loss_sum.item() / max(nb, 1)  # the one sync per epoch
+        dt = time.perf_counter() - te
+        epoch_losses.append(avg)
+        if log:
+            log.info(f"Epoch [{epoch + 1}/{num_epochs}], Average Loss: {avg:.4f}",
+                     batches=nb, seconds=dt, batches_per_sec=nb / dt if dt > 0 else 0.0)
+        if on_epoch:
+            on_epoch(epoch, avg)
+        if max_steps is not None and steps >= max_steps:
+            break
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    total = time.perf_counter() - t0
+    if log:
+        log.phase("Finished model training")
+    return {"epoch_losses": epoch_losses, "steps": steps, "seconds": total,
+            "batches_per_sec": steps / total if total > 0 else 0.0,
+            "graph": step.graph is not None, "graph_error": step.failed}

@@ -1,0 +1,3 @@
+"""Models: arena-backed DistilBERT ``DDoSClassifier`` (+ BERT-base teacher for distillation)."""
+from .arena import ParamArena  # noqa: F401
+from .distilbert import DDoSClassifier, DistilBertConfig, reference_state_dict_keys  # noqa: F401

@@ -1,0 +1,425 @@
+"""Arena-backed DistilBERT + ``DDoSClassifier`` (reference client1.py:53-65).
+
+Public surface kept from the reference:
+  * ``DDoSClassifier(local_model_path)`` with attributes ``.distilbert``,
+    ``.dropout`` (p=0.3) and ``.classifier`` (Linear 768->2);
+  * ``forward(input_ids, attention_mask) -> logits [B, 2]``;
+  * ``state_dict()`` with the exact 102 fp32 keys / shapes / order of the
+    reference checkpoint (``distilbert.embeddings.word_embeddings.weight`` ...
+    ``classifier.bias``), loadable by ``load_state_dict``.
+
+MI355X design: every parameter is a view into one flat fp32 arena (with a
+bf16 shadow the kernels read and a flat fp32 grad arena the backward writes),
+and ``impl="hip"`` runs the fused gfx950 kernels through three autograd node
+types (ops/functional.py).  ``impl="torch"`` is the pure-PyTorch fp32 path used
+on CPU (gloo plumbing, tests).  ``forward_loss`` fuses the head with the CE loss.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..ops import reference as R
+from .arena import ParamArena
+
+
+@dataclass
+class DistilBertConfig:
+    vocab_size: int = 30522
+    dim: int = 768
+    n_layers: int = 6
+    n_heads: int = 12
+    hidden_dim: int = 3072
+    max_position_embeddings: int = 512
+    dropout: float = 0.1
+    attention_dropout: float = 0.1
+    pad_token_id: int = 0
+    layer_norm_eps: float = 1e-12
+    initializer_range: float = 0.02
+
+
+LAYER_KEYS = [  # HF registration (= state_dict) order inside a TransformerBlock
+    ("attention.q_lin.weight", "w"), ("attention.q_lin.bias", "b"),
+    ("attention.k_lin.weight", "w"), ("attention.k_lin.bias", "b"),
+    ("attention.v_lin.weight", "w"), ("attention.v_lin.bias", "b"),
+    ("attention.out_lin.weight", "w"), ("attention.out_lin.bias", "b"),
+    ("sa_layer_norm.weight", "g"), ("sa_layer_norm.bias", "b"),
+    ("ffn.lin1.weight", "w"), ("ffn.lin1.bias", "b"),
+    ("ffn.lin2.weight", "w"), ("ffn.lin2.bias", "b"),
+    ("output_layer_norm.weight", "g"), ("output_layer_norm.bias", "b"),
+]
+
+
+def _layer_shapes(cfg: DistilBertConfig) -> Dict[str, Tuple[int, ...]]:
+    D, F = cfg.dim, cfg.hidden_dim
+    return {
+        "attention.q_lin.weight": (D, D), "attention.q_lin.bias": (D,),
+        "attention.k_lin.weight": (D, D), "attention.k_lin.bias": (D,),
+        "attention.v_lin.weight": (D, D), "attention.v_lin.bias": (D,),
+        "attention.out_lin.weight": (D, D), "attention.out_lin.bias": (D,),
+        "sa_layer_norm.weight": (D,), "sa_layer_norm.bias": (D,),
+        "ffn.lin1.weight": (F, D), "ffn.lin1.bias": (F,),
+        "ffn.lin2.weight": (D, F), "ffn.lin2.bias": (D,),
+        "output_layer_norm.weight": (D,), "output_layer_norm.bias": (D,),
+    }
+
+
+# Arena order: q/k/v weights then q/k/v biases contiguous (fused QKV views).
+_ARENA_LAYER_ORDER = [
+    "attention.q_lin.weight", "attention.k_lin.weight", "attention.v_lin.weight",
+    "attention.q_lin.bias", "attention.k_lin.bias", "attention.v_lin.bias",
+    "attention.out_lin.weight", "attention.out_lin.bias",
+    "sa_layer_norm.weight", "sa_layer_norm.bias",
+    "ffn.lin1.weight", "ffn.lin1.bias", "ffn.lin2.weight", "ffn.lin2.bias",
+    "output_layer_norm.weight", "output_layer_norm.bias",
+]
+
+
+def encoder_specs(cfg: DistilBertConfig, prefix: str) -> List[Tuple[str, Tuple[int, ...]]]:
+    D = cfg.dim
+    specs = [(f"{prefix}embeddings.word_embeddings.weight", (cfg.vocab_size, D)),
+             (f"{prefix}embeddings.position_embeddings.weight", (cfg.max_position_embeddings, D)),
+             (f"{prefix}embeddings.LayerNorm.weight", (D,)),
+             (f"{prefix}embeddings.LayerNorm.bias", (D,))]
+    shapes = _layer_shapes(cfg)
+    for i in range(cfg.n_layers):
+        for k in _ARENA_LAYER_ORDER:
+            specs.append((f"{prefix}transformer.layer.{i}.{k}", shapes[k]))
+    return specs
+
+
+class _P(nn.Module):
+    """Leaf module whose parameters are views into the arena."""
+
+    def __init__(self, arena: ParamArena, prefix: str, names=("weight", "bias")):
+        super().__init__()
+        self._arena_keys = {}
+        for n in names:
+            key = prefix + n
+            self._arena_keys[n] = key
+            self.register_parameter(n, nn.Parameter(arena.view(key)))
+
+    def rebind(self, arena: ParamArena):
+        for n, key in self._arena_keys.items():
+            p = getattr(self, n)
+            p.data = arena.view(key)
+            p.grad = arena.gview(key)
+
+
+class _Embeddings(nn.Module):
+    def __init__(self, arena, prefix, cfg):
+        super().__init__()
+        self.word_embeddings = _P(arena, prefix + "word_embeddings.", ("weight",))
+        self.position_embeddings = _P(arena, prefix + "position_embeddings.", ("weight",))
+        self.LayerNorm = _P(arena, prefix + "LayerNorm.")
+        self.dropout = nn.Dropout(cfg.dropout)
+
+
+class _Attention(nn.Module):
+    def __init__(self, arena, prefix, cfg):
+        super().__init__()
+        self.n_heads, self.dim = cfg.n_heads, cfg.dim
+        self.dropout = nn.Dropout(cfg.attention_dropout)
+        for n in ("q_lin", "k_lin", "v_lin", "out_lin"):
+            setattr(self, n, _P(arena, f"{prefix}{n}."))
+
+
+class _FFN(nn.Module):
+    def __init__(self, arena, prefix, cfg):
+        super().__init__()
+        self.dropout = nn.Dropout(cfg.dropout)
+        self.lin1 = _P(arena, prefix + "lin1.")
+        self.lin2 = _P(arena, prefix + "lin2.")
+
+
+class _Block(nn.Module):
+    def __init__(self, arena, prefix, cfg):
+        super().__init__()
+        self.attention = _Attention(arena, prefix + "attention.", cfg)
+        self.sa_layer_norm = _P(arena, prefix + "sa_layer_norm.")
+        self.ffn = _FFN(arena, prefix + "ffn.", cfg)
+        self.output_layer_norm = _P(arena, prefix + "output_layer_norm.")
+
+
+class _Transformer(nn.Module):
+    def __init__(self, arena, prefix, cfg):
+        super().__init__()
+        self.n_layers = cfg.n_layers
+        self.layer = nn.ModuleList([_Block(arena, f"{prefix}layer.{i}.", cfg) for i in range(cfg.n_layers)])
+
+
+class DistilBertEncoder(nn.Module):
+    """Module tree with HF DistilBertModel's attribute names (state_dict parity)."""
+
+    def __init__(self, arena: ParamArena, prefix: str, cfg: DistilBertConfig):
+        super().__init__()
+        self.config = cfg
+        self.prefix = prefix
+        self.embeddings = _Embeddings(arena, prefix + "embeddings.", cfg)
+        self.transformer = _Transformer(arena, prefix + "transformer.", cfg)
+
+
+# ---------------------------------------------------------------------------- init / loading
+def init_encoder_(arena: ParamArena, prefix: str, cfg: DistilBertConfig, gen: torch.Generator):
+    """HF DistilBERT _init_weights: Linear/Embedding ~ N(0, 0.02), bias 0, LN (1, 0), pad row 0."""
+    for name, shape in arena.specs:
+        if not name.startswith(prefix):
+            continue
+        v = arena.view(name)
+        if name.endswith("LayerNorm.weight") or name.endswith("layer_norm.weight"):
+            cpu = torch.ones(shape)
+        elif name.endswith(".bias"):
+            cpu = torch.zeros(shape)
+        else:
+            cpu = torch.randn(shape, generator=gen) * cfg.initializer_range
+            if name.endswith("word_embeddings.weight"):
+                cpu[cfg.pad_token_id] = 0
+        v.copy_(cpu)
+
+
+def load_hf_weights(arena: ParamArena, prefix: str, path: str) -> int:
+    """Load an HF distilbert dir (model.safetensors or pytorch_model.bin) if present."""
+    sd = None
+    st = os.path.join(path, "model.safetensors")
+    pt = os.path.join(path, "pytorch_model.bin")
+    if os.path.exists(st):
+        from safetensors.torch import load_file
+        sd = load_file(st)
+    elif os.path.exists(pt):
+        sd = torch.load(pt, map_location="cpu", weights_only=True)
+    if sd is None:
+        return 0
+    n = 0
+    for k, v in sd.items():
+        key = k if k.startswith(prefix) else prefix + k.removeprefix("distilbert.")
+        if key in arena.offsets and tuple(v.shape) == arena.offsets[key][1]:
+            arena.view(key).copy_(v.float())
+            n += 1
+    return n
+
+
+# ---------------------------------------------------------------------------- classifier
+class DDoSClassifier(nn.Module):
+    """DistilBERT + Dropout(0.3) + Linear(768, 2) (client1.py:53-65)."""
+
+    def __init__(self, local_model_path: Optional[str] = None, config: Optional[DistilBertConfig] = None,
+                 device=None, impl: str = "auto", seed: int = 0, head_dropout: float = 0.3):
+        super().__init__()
+        cfg = config or DistilBertConfig()
+        self.config = cfg
+        device = torch.device(device) if device is not None else torch.device("cpu")
+        specs = encoder_specs(cfg, "distilbert.") + [("classifier.weight", (2, cfg.dim)), ("classifier.bias", (2,))]
+        self.arena = ParamArena(specs, device="cpu", with_shadow=False)
+        gen = torch.Generator().manual_seed(seed)
+        init_encoder_(self.arena, "distilbert.", cfg, gen)
+        bound = 1.0 / math.sqrt(cfg.dim)  # nn.Linear default init
+        self.arena.view("classifier.weight").copy_(torch.rand(2, cfg.dim, generator=gen) * 2 * bound - bound)
+        self.arena.view("classifier.bias").copy_(torch.rand(2, generator=gen) * 2 * bound - bound)
+        self.loaded_pretrained = 0
+        if local_model_path is not None and os.path.isdir(local_model_path):
+            self.loaded_pretrained = load_hf_weights(self.arena, "distilbert.", local_model_path)
+        self.distilbert = DistilBertEncoder(self.arena, "distilbert.", cfg)
+        self.dropout = nn.Dropout(head_dropout)
+        self.classifier = _P(self.arena, "classifier.")
+        self.impl_request = impl
+        self.torch_counter = 0
+        self._grad_token = None
+        self._synced_version = -1
+        self._hip_cache = None
+        self.to(device)
+
+    # -------------------------------------------------------------- device management
+    def _apply(self, fn, recurse=True):
+        probe = fn(self.arena.master[:1])
+        if probe.dtype != torch.float32:
+            raise TypeError("DDoSClassifier keeps fp32 master weights; compute dtype is the bf16 shadow")
+        self.arena.to(probe.device)
+        for m in self.modules():
+            if isinstance(m, _P):
+                m.rebind(self.arena)
+        dev = probe.device
+        self.rng = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._grad_token = torch.zeros((), device=dev, requires_grad=True)
+        self._hip_cache = None
+        self._synced_version = -1
+        return self
+
+    @property
+    def device(self) -> torch.device:
+        return self.arena.device
+
+    @property
+    def impl(self) -> str:
+        if self.impl_request == "auto":
+            return "hip" if self.arena.device.type == "cuda" else "torch"
+        if self.impl_request == "hip" and self.arena.device.type != "cuda":
+            raise RuntimeError("impl='hip' needs the model on a GPU")
+        return self.impl_request
+
+    def zero_grad(self, set_to_none: bool = False):
+        # hip: first-write kernels make zeroing unnecessary; torch: autograd accumulates into the arena.
+        self.arena.zero_grad(zero_buffer=(self.impl == "torch"))
+        for m in self.modules():
+            if isinstance(m, _P):
+                for n, key in m._arena_keys.items():
+                    getattr(m, n).grad = self.arena.gview(key)
+
+    def _version(self) -> int:
+        # Parameters keep their own version counters (p.data = view), so sum them:
+        # any in-place update (load_state_dict, torch.optim, FedAvg) changes it.
+        return self.arena.master._version + sum(p._version for p in self.parameters())
+
+    def sync_shadow(self, force: bool = False):
+        """Refresh the bf16 compute shadow if the fp32 masters changed outside our Adam."""
+        v = self._version()
+        if force or v != self._synced_version:
+            self.arena.sync_shadow()
+            self._synced_version = self._version()
+
+    def mark_shadow_synced(self):
+        self._synced_version = self._version()
+
+    # -------------------------------------------------------------- HIP handles
+    def _hip_handles(self):
+        if self._hip_cache is not None:
+            return self._hip_cache
+        from ..ops.functional import GradSink
+        A = self.arena
+        pre = "distilbert."
+        emb = {
+            "word": A.sview(pre + "embeddings.word_embeddings.weight"),
+            "pos": A.sview(pre + "embeddings.position_embeddings.weight"),
+            "ln_w": A.view(pre + "embeddings.LayerNorm.weight"),
+            "ln_b": A.view(pre + "embeddings.LayerNorm.bias"),
+            "sinks": {
+                "word": GradSink(A, pre + "embeddings.word_embeddings.weight"),
+                "pos": GradSink(A, pre + "embeddings.position_embeddings.weight"),
+                "ln_w": GradSink(A, pre + "embeddings.LayerNorm.weight"),
+                "ln_b": GradSink(A, pre + "embeddings.LayerNorm.bias"),
+            },
+        }
+        layers = []
+        for i in range(self.config.n_layers):
+            lp = f"{pre}transformer.layer.{i}."
+            qkv_w = [lp + f"attention.{n}_lin.weight" for n in "qkv"]
+            qkv_b = [lp + f"attention.{n}_lin.bias" for n in "qkv"]
+            names = {
+                "o_w": lp + "attention.out_lin.weight", "o_b": lp + "attention.out_lin.bias",
+                "ln1_w": lp + "sa_layer_norm.weight", "ln1_b": lp + "sa_layer_norm.bias",
+                "l1_w": lp + "ffn.lin1.weight", "l1_b": lp + "ffn.lin1.bias",
+                "l2_w": lp + "ffn.lin2.weight", "l2_b": lp + "ffn.lin2.bias",
+                "ln2_w": lp + "output_layer_norm.weight", "ln2_b": lp + "output_layer_norm.bias",
+            }
+            L = {"qkv_w": A.span(qkv_w, "shadow"), "qkv_b": A.span(qkv_b, "master")}
+            sinks = {"qkv_w": _SpanSink(A, qkv_w), "qkv_b": _SpanSink(A, qkv_b)}
+            for k, nm in names.items():
+                L[k] = A.sview(nm) if k.endswith("_w") and not k.startswith("ln") else A.view(nm)
+                sinks[k] = GradSink(A, nm)
+            L["sinks"] = sinks
+            layers.append(L)
+        head = {"w": A.view("classifier.weight"), "b": A.view("classifier.bias"),
+                "sinks": {"w": GradSink(A, "classifier.weight"), "b": GradSink(A, "classifier.bias")}}
+        self._hip_cache = (emb, layers, head)
+        return self._hip_cache
+
+    # -------------------------------------------------------------- forward
+    def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
+        return self._run(input_ids, attention_mask, None)[1]
+
+    def forward_loss(self, input_ids, attention_mask, labels) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(mean CE loss, logits) with the head and the loss fused (one kernel)."""
+        return self._run(input_ids, attention_mask, labels)
+
+    def _run(self, input_ids, attention_mask, labels):
+        if self.impl == "hip":
+            return self._run_hip(input_ids, attention_mask, labels)
+        return self._run_torch(input_ids, attention_mask, labels)
+
+    def _run_hip(self, ids, mask, labels):
+        from ..ops import kernels as K
+        from ..ops.functional import EmbeddingFn, HeadFn, LayerFn, RunCtx
+        self.sync_shadow()
+        B, S = ids.shape
+        if S % 64:
+            pad = 64 - S % 64
+            ids = torch.nn.functional.pad(ids, (0, pad))
+            mask = torch.nn.functional.pad(mask, (0, pad))
+            S += pad
+        emb, layers, head = self._hip_handles()
+        cfg = self.config
+        rc = RunCtx(B=B, S=S, H=cfg.n_heads, kbias=K.mask_bias(mask), seed=self.rng, training=self.training,
+                    eps=cfg.layer_norm_eps, p_hidden=cfg.dropout, p_attn=cfg.attention_dropout, p_head=self.dropout.p)
+        if self.training:
+            K.step_inc(None, self.rng)
+        token = self._grad_token if torch.is_grad_enabled() else None
+        x = EmbeddingFn.apply(token, ids, emb["word"], emb["pos"], emb["ln_w"], emb["ln_b"], emb["sinks"], rc)
+        for i, L in enumerate(layers):
+            x = LayerFn.apply(x, L, rc, i)
+        if labels is not None:
+            loss, logits = HeadFn.apply(x, head["w"], head["b"], head["sinks"], rc, labels.to(torch.int64))
+            return loss, logits
+        logits, _ = HeadFn.apply(x, head["w"], head["b"], head["sinks"], rc, None)
+        return None, logits
+
+    def _run_torch(self, ids, mask, labels):
+        cfg = self.config
+        tr = self.training
+        counter = None
+        if tr:
+            self.torch_counter += 1
+            counter = self.torch_counter
+        B, S = ids.shape
+        e = self.distilbert.embeddings
+        x = R.embedding_ref(ids, e.word_embeddings.weight, e.position_embeddings.weight, e.LayerNorm.weight,
+                            e.LayerNorm.bias, cfg.layer_norm_eps, cfg.dropout if tr else 0.0, counter, 1)
+        for i, blk in enumerate(self.distilbert.transformer.layer):
+            a = blk.attention
+            P = {
+                "qkv_w": torch.cat([a.q_lin.weight, a.k_lin.weight, a.v_lin.weight]),
+                "qkv_b": torch.cat([a.q_lin.bias, a.k_lin.bias, a.v_lin.bias]),
+                "o_w": a.out_lin.weight, "o_b": a.out_lin.bias,
+                "ln1_w": blk.sa_layer_norm.weight, "ln1_b": blk.sa_layer_norm.bias,
+                "l1_w": blk.ffn.lin1.weight, "l1_b": blk.ffn.lin1.bias,
+                "l2_w": blk.ffn.lin2.weight, "l2_b": blk.ffn.lin2.bias,
+                "ln2_w": blk.output_layer_norm.weight, "ln2_b": blk.output_layer_norm.bias,
+            }
+            x = R.layer_ref(x, P, B, S, cfg.n_heads, mask, cfg.layer_norm_eps,
+                            cfg.attention_dropout if tr else 0.0, cfg.dropout if tr else 0.0, counter,
+                            16 + 4 * i, 17 + 4 * i)
+        logits = R.head_ref(x, B, S, self.classifier.weight, self.classifier.bias, self.dropout.p if tr else 0.0,
+                            counter, 2)
+        if labels is None:
+            return None, logits
+        return torch.nn.functional.cross_entropy(logits, labels), logits
+
+
+class _SpanSink:
+    """GradSink over a fused span (q/k/v) -- the three names are written together."""
+
+    def __init__(self, arena, names):
+        self.arena, self.names = arena, list(names)
+
+    @property
+    def buf(self):
+        return self.arena.span(self.names, "grad")
+
+    def accumulate(self) -> bool:
+        acc = False
+        for n in self.names:
+            acc = self.arena.mark_written(n)
+        return acc
+
+
+def reference_state_dict_keys(cfg: Optional[DistilBertConfig] = None) -> List[str]:
+    """The 102 keys of the reference checkpoint, in order."""
+    cfg = cfg or DistilBertConfig()
+    keys = ["distilbert.embeddings.word_embeddings.weight", "distilbert.embeddings.position_embeddings.weight",
+            "distilbert.embeddings.LayerNorm.weight", "distilbert.embeddings.LayerNorm.bias"]
+    for i in range(cfg.n_layers):
+        keys += [f"distilbert.transformer.layer.{i}.{k}" for k, _ in LAYER_KEYS]
+    return keys + ["classifier.weight", "classifier.bias"]

@@ -88,7 +88,7 @@ class LayerFn(torch.autograd.Function):
         g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
         f = K.linear_fwd(g, L["l2_w"], L["l2_b"])
         y, m2, r2 = K.ln_fwd(f, h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed, ffn_site, p_h)
-        if torch.is_grad_enabled() or ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0]:
             ctx.save_for_backward(x)
             ctx.acts = (qkv, cx, lse, ao, h, m1, r1, u, g, f, m2, r2)
         ctx.L, ctx.rc, ctx.sites, ctx.p = L, rc, (attn_site, ffn_site), (p_a, p_h)
