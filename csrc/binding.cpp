@@ -34,18 +34,19 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                const void* word, const void* pos, const float* gamma, const float* mean, const float* rstd,
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
-               int accumulate, hipStream_t st);
+               int accumulate, unsigned char* now, unsigned char* ever, hipStream_t st);
 int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, hipStream_t st);
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
-                float* logits, float* loss, float* dlogits, hipStream_t st);
+                float* logits, float* loss, float* dlogits, float* row_loss, hipStream_t st);
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
                 int accumulate, hipStream_t st);
 int fd_eval_metrics(const float* logits, const long long* labels, int B, double* acc, long long* counts,
                     float* prob1, long long* preds, hipStream_t st);
 int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float lr,
-            float b1, float b2, float eps, float wd, int decoupled, hipStream_t st);
+            float b1, float b2, float eps, float wd, int decoupled, const unsigned char* touched,
+            const unsigned char* now, long long skip_off, long long skip_rows, int row_len, hipStream_t st);
 int fd_step(int* step, uint32_t* seed, hipStream_t st);
 int fd_scale_cast(float* p, void* shadow, long long n, float scale, hipStream_t st);
 int fd_axpby(float* dst, const float* x, const float* y, float a, float b, long long n, hipStream_t st);
@@ -224,7 +225,13 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
              const at::Tensor& word, const at::Tensor& pos, const at::Tensor& gamma, const at::Tensor& mean,
              const at::Tensor& rstd, const at::Tensor& dword, const at::Tensor& dpos, const at::Tensor& dgamma,
              const at::Tensor& dbeta, const at::Tensor& dz_buf, const at::Tensor& work, int64_t S,
-             const at::Tensor& seed, int64_t site, int64_t thr, double dscale, bool accumulate) {
+             const at::Tensor& seed, int64_t site, int64_t thr, double dscale, bool accumulate,
+             const c10::optional<at::Tensor>& now, const c10::optional<at::Tensor>& ever) {
+  need_opt(now, at::kByte, "now");
+  need_opt(ever, at::kByte, "ever");
+  TORCH_CHECK(now.has_value() == ever.has_value(), "emb_bwd: now/ever go together");
+  if (now.has_value() && now->defined())
+    TORCH_CHECK(now->numel() == word.size(0) && ever->numel() == word.size(0), "emb_bwd: flag sizes");
   need(dy, at::kBFloat16, "dy");
   need(sorted, at::kLong, "sorted");
   need(perm, at::kLong, "perm");
@@ -244,7 +251,8 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
                       gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), dword.data_ptr<float>(),
                       dpos.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
                       dz_buf.data_ptr<float>(), work.data_ptr<float>(), (int)T, (int)S, (int)(T / S), (int)P, (int)V,
-                      (int)D, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, accumulate ? 1 : 0, stream()),
+                      (int)D, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, accumulate ? 1 : 0,
+                      ptr<unsigned char>(now), ptr<unsigned char>(ever), stream()),
            "emb_bwd");
 }
 
@@ -261,7 +269,9 @@ void colsum_bf16(const at::Tensor& x, const at::Tensor& out, const at::Tensor& w
 
 void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& W, const at::Tensor& bias,
               const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& labels,
-              const at::Tensor& logits, const c10::optional<at::Tensor>& loss, const c10::optional<at::Tensor>& dlogits) {
+              const at::Tensor& logits, const c10::optional<at::Tensor>& loss, const c10::optional<at::Tensor>& dlogits,
+              const c10::optional<at::Tensor>& row_loss) {
+  need_opt(row_loss, at::kFloat, "row_loss");
   need(hidden, at::kBFloat16, "hidden");
   need(W, at::kFloat, "W");
   need(bias, at::kFloat, "bias");
@@ -272,12 +282,13 @@ void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
   const int64_t D = W.size(1);
   TORCH_CHECK(W.size(0) == 2 && hidden.numel() == B * S * D && logits.numel() == B * 2, "head_fwd: shapes");
   if (labels.has_value() && labels->defined())
-    TORCH_CHECK(labels->numel() == B && loss.has_value() && dlogits.has_value() && dlogits->numel() == 2 * B,
-                "head_fwd: labels needs loss/dlogits");
+    TORCH_CHECK(labels->numel() == B && loss.has_value() && dlogits.has_value() && dlogits->numel() == 2 * B &&
+                    row_loss.has_value() && row_loss->numel() >= B,
+                "head_fwd: labels needs loss/dlogits/row_loss");
   check_rc(fd_head_fwd(hidden.data_ptr(), (int)B, (int)S, (int)D, W.data_ptr<float>(), bias.data_ptr<float>(),
                        seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale,
                        ptr<const long long>(labels), logits.data_ptr<float>(), ptr<float>(loss), ptr<float>(dlogits),
-                       stream()),
+                       ptr<float>(row_loss), stream()),
            "head_fwd");
 }
 
@@ -318,7 +329,15 @@ void eval_metrics(const at::Tensor& logits, const at::Tensor& labels, const at::
 
 void adam(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
           const c10::optional<at::Tensor>& shadow, const at::Tensor& step, double lr, double b1, double b2, double eps,
-          double wd, bool decoupled) {
+          double wd, bool decoupled, const c10::optional<at::Tensor>& touched, const c10::optional<at::Tensor>& now,
+          int64_t skip_off, int64_t skip_rows, int64_t row_len) {
+  need_opt(touched, at::kByte, "touched");
+  need_opt(now, at::kByte, "now");
+  if (touched.has_value() && touched->defined()) {
+    TORCH_CHECK(touched->numel() >= skip_rows && skip_off >= 0 && skip_off + skip_rows * row_len <= p.numel(),
+                "adam: skip range");
+    if (now.has_value() && now->defined()) TORCH_CHECK(now->numel() >= skip_rows, "adam: now size");
+  }
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(m, at::kFloat, "m");
@@ -330,7 +349,8 @@ void adam(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const a
   if (shadow.has_value() && shadow->defined()) TORCH_CHECK(shadow->numel() == n, "adam: shadow size");
   check_rc(fd_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                    ptr<void>(shadow), n, step.data_ptr<int>(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
-                   decoupled ? 1 : 0, stream()),
+                   decoupled ? 1 : 0, ptr<const unsigned char>(touched), ptr<const unsigned char>(now), skip_off,
+                   skip_rows, (int)row_len, stream()),
            "adam");
 }
 

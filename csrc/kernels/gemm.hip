@@ -9,23 +9,24 @@
 //   backward dx = dy W          -> A_KMAJ, !B_KMAJ  ("NN")
 //   backward dW = dy^T x        -> !A_KMAJ, !B_KMAJ ("TN", split-K fp32 slabs)
 //
-// Design (MI355X-first, see cdna_hip_programming.md §5):
+// Design (MI355X-first, cdna_hip_programming.md §5):
 //  * 256 threads = 4 waves in a 2x2 grid; each wave owns a (BM/2)x(BN/2) tile of
-//    16x16 MFMA sub-tiles; K step 64 (two 32-deep MFMA steps).
-//  * Register-staged, double-buffered LDS: the next K tile's 16-byte global loads
-//    are issued before the current tile's MFMAs and written to the other LDS
-//    buffer after them (T14) -> one barrier per K tile.
-//  * K-major operands live in LDS as [rows][64] with a 16-byte-chunk XOR swizzle
-//    (chunk ^= (row>>1)&7) so the ds_read_b128 fragment reads are conflict-free.
-//    MN-major operands live as [64 k-rows][BM] and are read with the gfx950
-//    transposing ds_read_b64_tr_b16 (T10); their chunk swizzle (fk) makes the
-//    two 16-lane groups of each half-wave hit disjoint banks.
-//  * Operands are swapped inside the MFMA (D = B^T A^T = C^T) so each lane ends
-//    up owning 4 consecutive output columns: 8-byte bf16 / 16-byte fp32 stores,
-//    and bias / residual / GELU-aux loads are vectorised the same way.
-//  * XCD-aware bijective block remap (T1) + M-major tile walk for L2 reuse.
+//    16x16 MFMA sub-tiles; K tile 64 (two 32-deep MFMA steps).
+//  * Operand tiles go HBM/L2 -> LDS with global_load_lds_dwordx4 (LDS-DMA, no
+//    VGPR round trip, no ds_write issue cost), double-buffered: tile k+1's DMA
+//    is issued before tile k's MFMAs; one vmcnt(0)+barrier per K tile.
+//  * The DMA writes LDS lane-linearly, so bank-conflict swizzles are applied on
+//    the per-lane SOURCE address and undone on the read (rule 21):
+//    K-major images [rows][64] use chunk ^= (row>>1)&7 (conflict-free
+//    ds_read_b128 fragments); MN-major images [64 k][BMN] are read with the
+//    transposing ds_read_b64_tr_b16 (T10) and use chunk ^= fk(k) so the 16-lane
+//    groups of each half-wave hit disjoint banks.
+//  * Operands are swapped inside the MFMA (D = B^T A^T = C^T) so every lane owns
+//    4 consecutive output columns: 8-byte bf16 / 16-byte fp32 stores, vectorised
+//    bias / residual / GELU-aux loads in the epilogue.
+//  * Host picks the tile (128x128 / 128x96 / 128x64) that best fills 256 CUs x
+//    2 resident blocks; XCD-aware bijective block remap (T1).
 #include "common.h"
-#include <algorithm>
 
 namespace {
 
@@ -55,6 +56,9 @@ struct GemmParams {
 
 constexpr int BKT = 64;
 
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_void;
+
 // Swizzle of 16-byte chunks for the MN-major ([k][mn]) LDS image.
 template <int BMN>
 DEV int fk(int k) {
@@ -64,45 +68,30 @@ DEV int fk(int k) {
 
 template <int ROWS, bool KMAJ>
 struct Operand {
-  // bytes of one LDS buffer
-  static constexpr int BYTES = ROWS * BKT * 2;
-  static constexpr int LOADS = ROWS * BKT / 8 / 256;  // 16-byte loads per thread
-  static constexpr int CHUNKS = KMAJ ? 8 : ROWS / 8;  // 16-byte chunks per LDS row
-  static constexpr int ROWB = KMAJ ? 128 : ROWS * 2;  // LDS row bytes
+  static constexpr int BYTES = ROWS * BKT * 2;        // one LDS buffer
+  static constexpr int PER_WAVE = BYTES / 1024 / 4;  // 1 KiB DMA pieces per wave per tile
+  static constexpr int CH = KMAJ ? 8 : ROWS / 8;      // 16-byte chunks per LDS row
+  static constexpr int ROWB = CH * 16;
+  static_assert(KMAJ || ROWS == 64 || ROWS == 128, "MN-major tiles must be 64 or 128 wide");
+  static_assert(PER_WAVE * 4 * 1024 == BYTES, "tile must split into whole 1 KiB pieces per wave");
 
-  // Global -> registers for K tile starting at k0; rows beyond `lim` read as 0
-  // (K-major only: the token dimension of activations).
-  DEV static void gload(uint4 (&r)[LOADS], const bf16_t* base, int ld, int row0, int k0, int lim,
-                        int tid) {
+  // LDS-DMA of the K tile starting at k0.  K-major rows beyond `lim` are clamped
+  // (their products land in output rows that are never stored).
+  DEV static void stage(const bf16_t* base, int ld, int row0, int k0, int lim, char* lds, int wid, int lane) {
 #pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int id = i * 256 + tid;
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int piece = wid * PER_WAVE + i;
+      const int pos = piece * 64 + lane;  // physical 16-byte chunk of the image
+      const bf16_t* src;
       if constexpr (KMAJ) {
-        const int rr = id >> 3, c = id & 7;
-        if (row0 + rr < lim)
-          r[i] = *reinterpret_cast<const uint4*>(base + (size_t)(row0 + rr) * ld + k0 + c * 8);
-        else
-          r[i] = make_uint4(0, 0, 0, 0);
+        const int r = pos >> 3, c = (pos & 7) ^ ((r >> 1) & 7);
+        const int gr = min(row0 + r, lim - 1);
+        src = base + (size_t)gr * ld + k0 + c * 8;
       } else {
-        const int kk = id / CHUNKS, c = id % CHUNKS;
-        r[i] = *reinterpret_cast<const uint4*>(base + (size_t)(k0 + kk) * ld + row0 + c * 8);
+        const int k = pos / CH, c = (pos % CH) ^ fk<ROWS>(k);
+        src = base + (size_t)(k0 + k) * ld + row0 + c * 8;
       }
-    }
-  }
-
-  DEV static void lstore(const uint4 (&r)[LOADS], char* lds, int tid) {
-#pragma unroll
-    for (int i = 0; i < LOADS; ++i) {
-      const int id = i * 256 + tid;
-      int off;
-      if constexpr (KMAJ) {
-        const int rr = id >> 3, c = id & 7;
-        off = rr * 128 + ((c ^ ((rr >> 1) & 7)) << 4);
-      } else {
-        const int kk = id / CHUNKS, c = id % CHUNKS;
-        off = kk * ROWB + ((c ^ fk<ROWS>(kk)) << 4);
-      }
-      *reinterpret_cast<uint4*>(lds + off) = r[i];
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds + piece * 1024), 16, 0, 0);
     }
   }
 
@@ -120,8 +109,7 @@ struct Operand {
       for (int h = 0; h < 2; ++h) {
         const int k = s * 32 + 8 * g + 4 * h + q;
         const char* addr = lds + k * ROWB + ((c ^ fk<ROWS>(k)) << 4) + (p & 1) * 8;
-        bf16x4v v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) bf16x4v*)(addr));
+        bf16x4v v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4v*)(addr));
         out[4 * h + 0] = v[0];
         out[4 * h + 1] = v[1];
         out[4 * h + 2] = v[2];
@@ -133,17 +121,15 @@ struct Operand {
 };
 
 template <int BM, int BN, bool AK, bool BKM, int EPI>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
   using OA = Operand<BM, AK>;
   using OB = Operand<BN, BKM>;
   constexpr int MI = BM / 32, NI = BN / 32;  // 16x16 sub-tiles per wave
-  __shared__ __attribute__((aligned(16))) char smem[2 * (OA::BYTES + OB::BYTES)];
-  char* const sa0 = smem;
-  char* const sb0 = smem + 2 * OA::BYTES;
-#define SA(b) (sa0 + (b) * OA::BYTES)
-#define SB(b) (sb0 + (b) * OB::BYTES)
+  constexpr int BUF = OA::BYTES + OB::BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 1, wc = wid & 1;
 
   // Tile walk: M-major inside each N column panel so consecutive logical tiles
@@ -162,42 +148,36 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[OA::LOADS], rb[OB::LOADS];
-  OA::gload(ra, p.A, p.lda, m0, kbeg, p.M, tid);
-  OB::gload(rb, p.B, p.ldb, n0, kbeg, p.N, tid);
-  OA::lstore(ra, SA(0), tid);
-  OB::lstore(rb, SB(0), tid);
+  OA::stage(p.A, p.lda, m0, kbeg, p.M, smem, wid, lane);
+  OB::stage(p.B, p.ldb, n0, kbeg, p.N, smem + OA::BYTES, wid, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  int buf = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {
-      OA::gload(ra, p.A, p.lda, m0, kbeg + (kt + 1) * BKT, p.M, tid);
-      OB::gload(rb, p.B, p.ldb, n0, kbeg + (kt + 1) * BKT, p.N, tid);
+    char* cur = smem + (kt & 1) * BUF;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * BUF;
+      OA::stage(p.A, p.lda, m0, kbeg + (kt + 1) * BKT, p.M, nxt, wid, lane);
+      OB::stage(p.B, p.ldb, n0, kbeg + (kt + 1) * BKT, p.N, nxt + OA::BYTES, wid, lane);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 af[MI], bfr[NI];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = OA::frag(SA(buf), wr * (BM / 2) + i * 16, s, lane);
+      for (int i = 0; i < MI; ++i) af[i] = OA::frag(cur, wr * (BM / 2) + i * 16, s, lane);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) bfr[j] = OB::frag(SB(buf), wc * (BN / 2) + j * 16, s, lane);
+      for (int j = 0; j < NI; ++j) bfr[j] = OB::frag(cur + OA::BYTES, wc * (BN / 2) + j * 16, s, lane);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
     }
-    if (more) {
-      OA::lstore(ra, SA(buf ^ 1), tid);
-      OB::lstore(rb, SB(buf ^ 1), tid);
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    buf ^= 1;
   }
 
-#undef SA
-#undef SB
   // ---------------------------------------------------------------- epilogue
   // lane owns C[m][n..n+3] of every sub-tile (operand-swapped MFMA).
 #pragma unroll
@@ -217,11 +197,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
           v0 += b.x; v1 += b.y; v2 += b.z; v3 += b.w;
         }
         if constexpr (EPI == EPI_BIAS_GELU) {
-          *reinterpret_cast<uint2*>(p.aux + (size_t)m * p.ldaux + n) =
-              make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
-          // GELU on the bf16-rounded pre-activation, exactly what the backward
-          // will see when it re-reads aux.
+          // GELU on the bf16-rounded pre-activation, exactly what the backward re-reads.
           const uint2 u = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+          *reinterpret_cast<uint2*>(p.aux + (size_t)m * p.ldaux + n) = u;
           v0 = gelu_erf(lo_bf(u.x)); v1 = gelu_erf(hi_bf(u.x));
           v2 = gelu_erf(lo_bf(u.y)); v3 = gelu_erf(hi_bf(u.y));
         }
@@ -235,17 +213,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p) {
           v0 += lo_bf(r.x); v1 += hi_bf(r.x); v2 += lo_bf(r.y); v3 += hi_bf(r.y);
         }
         bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-        *reinterpret_cast<uint2*>(C + (size_t)m * p.ldc + n) =
-            make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+        *reinterpret_cast<uint2*>(C + (size_t)m * p.ldc + n) = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
       }
     }
   }
 }
 
 // out[i] = (accumulate ? out[i] : 0) + sum_z slab[z][i]   (deterministic split-K reduce)
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slabs,
-                                                            float* __restrict__ out, long long n4,
-                                                            long long stride, int splits,
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slabs, float* __restrict__ out,
+                                                            long long n4, long long stride, int splits,
                                                             int accumulate) {
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
     float4 s = accumulate ? reinterpret_cast<float4*>(out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -260,9 +236,41 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 template <int BM, int BN, bool AK, bool BKM, int EPI>
 void launch(const GemmParams& p, int splits, hipStream_t st) {
   const int tiles = ((p.M + BM - 1) / BM) * (p.N / BN);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKM, EPI>), dim3(tiles, 1, splits), dim3(256), 0, st,
-                     p);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKM, EPI>), dim3(tiles, 1, splits), dim3(256), 0, st, p);
 }
+
+// Pick BN in {128, 96, 64} maximising (wave-quantisation efficiency x tile efficiency)
+// on 256 CUs x 2 resident blocks.
+int pick_bn(int M, int N, bool allow96) {
+  const int cand[3] = {128, 96, 64};
+  const double tile_eff[3] = {1.0, 0.93, 0.84};
+  const int slots = 512;
+  int best = 64;
+  double best_s = -1;
+  for (int c = 0; c < 3; ++c) {
+    const int bn = cand[c];
+    if (N % bn != 0 || (bn == 96 && !allow96)) continue;
+    const long tiles = (long)((M + 127) / 128) * (N / bn);
+    const long rounds = (tiles + slots - 1) / slots;
+    const double q = (double)tiles / (double)(rounds * slots);
+    const double s = q * tile_eff[c];
+    if (s > best_s) { best_s = s; best = bn; }
+  }
+  return best;
+}
+
+#define DISPATCH_BN(BN_, AK_, BK_, EPI_)                                  \
+  do {                                                                   \
+    if (BN_ == 128) launch<128, 128, AK_, BK_, EPI_>(p, 1, st);          \
+    else if (BN_ == 96) launch<128, 96, AK_, BK_, EPI_>(p, 1, st);       \
+    else launch<128, 64, AK_, BK_, EPI_>(p, 1, st);                      \
+  } while (0)
+
+#define DISPATCH_BN_NN(BN_, EPI_)                                         \
+  do {                                                                   \
+    if (BN_ == 128) launch<128, 128, true, false, EPI_>(p, 1, st);       \
+    else launch<128, 64, true, false, EPI_>(p, 1, st);                   \
+  } while (0)
 
 }  // namespace
 
@@ -271,50 +279,43 @@ extern "C" {
 
 // kind: 0 = NT (y = x W^T), 1 = NN (dx = dy W), 2 = TN (dW = dy^T x, fp32 out)
 // Returns 0 on success, nonzero on unsupported shape.
-int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda,
-            int ldb, int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres,
-            float* workspace, long long workspace_elems, int accumulate, hipStream_t st) {
-  if (K % BKT != 0 || N % 64 != 0) return 1;
+int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+            const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
+            long long workspace_elems, int accumulate, hipStream_t st) {
+  if (K % BKT != 0 || N % 64 != 0 || M <= 0) return 1;
   GemmParams p{};
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.C = C;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
   p.bias = bias; p.aux = (bf16_t*)aux; p.ldaux = ldaux; p.res = (const bf16_t*)res; p.ldres = ldres;
   p.k_split = K;
-  const bool wide = (N % 128 == 0) && ((long long)((M + 127) / 128) * (N / 128) >= 512);
   if (kind == 0) {
-    if (epi == EPI_BIAS) {
-      if (wide) launch<128, 128, true, true, EPI_BIAS>(p, 1, st);
-      else launch<128, 64, true, true, EPI_BIAS>(p, 1, st);
-    } else if (epi == EPI_BIAS_GELU) {
-      if (wide) launch<128, 128, true, true, EPI_BIAS_GELU>(p, 1, st);
-      else launch<128, 64, true, true, EPI_BIAS_GELU>(p, 1, st);
-    } else if (epi == EPI_BF16) {
-      if (wide) launch<128, 128, true, true, EPI_BF16>(p, 1, st);
-      else launch<128, 64, true, true, EPI_BF16>(p, 1, st);
-    } else return 2;
+    const int bn = pick_bn(M, N, true);
+    switch (epi) {
+      case EPI_BIAS: DISPATCH_BN(bn, true, true, EPI_BIAS); break;
+      case EPI_BIAS_GELU: DISPATCH_BN(bn, true, true, EPI_BIAS_GELU); break;
+      case EPI_BF16: DISPATCH_BN(bn, true, true, EPI_BF16); break;
+      default: return 2;
+    }
     return 0;
   }
   if (kind == 1) {
-    if (epi == EPI_BF16) {
-      if (wide) launch<128, 128, true, false, EPI_BF16>(p, 1, st);
-      else launch<128, 64, true, false, EPI_BF16>(p, 1, st);
-    } else if (epi == EPI_GELU_BWD) {
-      if (wide) launch<128, 128, true, false, EPI_GELU_BWD>(p, 1, st);
-      else launch<128, 64, true, false, EPI_GELU_BWD>(p, 1, st);
-    } else if (epi == EPI_ADD) {
-      if (wide) launch<128, 128, true, false, EPI_ADD>(p, 1, st);
-      else launch<128, 64, true, false, EPI_ADD>(p, 1, st);
-    } else return 2;
+    const int bn = pick_bn(M, N, false);
+    switch (epi) {
+      case EPI_BF16: DISPATCH_BN_NN(bn, EPI_BF16); break;
+      case EPI_GELU_BWD: DISPATCH_BN_NN(bn, EPI_GELU_BWD); break;
+      case EPI_ADD: DISPATCH_BN_NN(bn, EPI_ADD); break;
+      default: return 2;
+    }
     return 0;
   }
   if (kind == 2) {
     // dW[M=out][N=in] fp32.  Split K (the token dim) until the grid covers the
-    // chip ~2x; slabs go to `workspace` and are reduced deterministically.
+    // chip; slabs go to `workspace` and are reduced deterministically.
     if (M % 128 != 0) return 3;
-    const int tiles = (M / 128) * (N / 128 > 0 && N % 128 == 0 ? N / 128 : N / 64);
     const bool n128 = N % 128 == 0;
+    const int tiles = (M / 128) * (n128 ? N / 128 : N / 64);
     int splits = 1;
-    while (tiles * splits < 512 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 256) splits *= 2;
+    while (tiles * splits < 384 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 512) splits *= 2;
     const long long slab = (long long)M * N;
     if (splits > 1 && workspace_elems < slab * splits) splits = 1;
     p.k_split = K / splits;
@@ -325,14 +326,14 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
       else launch<128, 64, false, false, EPI_F32>(p, 1, st);
       return 0;
     }
+    if (ldc != N) return 4;
     p.C = workspace; p.ldc = N; p.slab_stride = slab;
     if (n128) launch<128, 128, false, false, EPI_F32>(p, splits, st);
     else launch<128, 64, false, false, EPI_F32>(p, splits, st);
-    if (ldc != N) return 4;
     const long long n4 = slab / 4;
     const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, workspace, out, n4, slab,
-                       splits, accumulate);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, workspace, out, n4, slab, splits,
+                       accumulate);
     return 0;
   }
   return 5;

@@ -29,6 +29,7 @@ struct HeadArgs {
   float* logits;         // [B, 2]
   float* loss;           // [1]
   float* dlogits;        // [B, 2] (written when labels given)
+  float* row_loss;       // [B] scratch
   // backward
   const float* dlog_in;  // [B, 2]
   float* dW;             // [2, D]
@@ -37,48 +38,56 @@ struct HeadArgs {
   int accumulate;
 };
 
+// One wave per batch row (grid = ceil(B/4) blocks); per-row loss to row_loss,
+// reduced in a fixed order by head_loss_mean_kernel.
 __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
-  __shared__ float red[64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= a.B) return;
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
-  float lsum = 0.f;
-  for (int b = w; b < a.B; b += 4) {
-    const bf16_t* x = a.hidden + (size_t)b * a.S * a.D;
-    float z0 = 0.f, z1 = 0.f;
-    for (int col = lane; col < a.D; col += 64) {
-      float v = bf2f(x[col]);
-      if (drop) v = drop_keep(seed, (uint32_t)(b * a.D + col), a.thr) ? v * a.dscale : 0.f;
-      z0 += v * a.W[col];
-      z1 += v * a.W[a.D + col];
+  const bf16_t* x = a.hidden + (size_t)b * a.S * a.D;
+  float z0 = 0.f, z1 = 0.f;
+  for (int col = 4 * lane; col < a.D; col += 256) {
+    const uint2 xv = *reinterpret_cast<const uint2*>(x + col);
+    float v[4] = {lo_bf(xv.x), hi_bf(xv.x), lo_bf(xv.y), hi_bf(xv.y)};
+    const float4 w0 = *reinterpret_cast<const float4*>(a.W + col);
+    const float4 w1 = *reinterpret_cast<const float4*>(a.W + a.D + col);
+    if (drop) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = drop_keep(seed, (uint32_t)(b * a.D + col + e), a.thr) ? v[e] * a.dscale : 0.f;
     }
-    z0 = wave_sum(z0) + a.bias[0];
-    z1 = wave_sum(z1) + a.bias[1];
-    if (lane == 0) {
-      a.logits[2 * b] = z0;
-      a.logits[2 * b + 1] = z1;
-      if (a.labels) {
-        const float mx = fmaxf(z0, z1);
-        const float lse = mx + __logf(__expf(z0 - mx) + __expf(z1 - mx));
-        const int y = (int)a.labels[b];
-        lsum += lse - (y ? z1 : z0);
-        const float p1 = __expf(z1 - lse), p0 = __expf(z0 - lse);
-        a.dlogits[2 * b] = (p0 - (y == 0)) / a.B;
-        a.dlogits[2 * b + 1] = (p1 - (y == 1)) / a.B;
-      }
+    z0 += v[0] * w0.x + v[1] * w0.y + v[2] * w0.z + v[3] * w0.w;
+    z1 += v[0] * w1.x + v[1] * w1.y + v[2] * w1.z + v[3] * w1.w;
+  }
+  z0 = wave_sum(z0) + a.bias[0];
+  z1 = wave_sum(z1) + a.bias[1];
+  if (lane == 0) {
+    a.logits[2 * b] = z0;
+    a.logits[2 * b + 1] = z1;
+    if (a.labels) {
+      const float mx = fmaxf(z0, z1);
+      const float lse = mx + __logf(__expf(z0 - mx) + __expf(z1 - mx));
+      const int y = (int)a.labels[b];
+      a.row_loss[b] = lse - (y ? z1 : z0);
+      const float p1 = __expf(z1 - lse), p0 = __expf(z0 - lse);
+      a.dlogits[2 * b] = (p0 - (y == 0)) / a.B;
+      a.dlogits[2 * b + 1] = (p1 - (y == 1)) / a.B;
     }
   }
-  if (a.labels) {
-    if (lane == 0) red[w] = lsum;
-    __syncthreads();
-    if (threadIdx.x == 0) a.loss[0] = (red[0] + red[1] + red[2] + red[3]) / a.B;
-  }
+}
+
+__global__ __launch_bounds__(64) void head_loss_mean_kernel(const float* row_loss, int B, float* loss) {
+  float s = 0.f;
+  for (int b = threadIdx.x; b < B; b += 64) s += row_loss[b];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) loss[0] = s / B;
 }
 
 __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
-  for (int col = threadIdx.x; col < a.D; col += 256) {
+  for (int col = blockIdx.x * 256 + threadIdx.x; col < a.D; col += gridDim.x * 256) {
     float g0 = 0.f, g1 = 0.f;
     const float w0 = a.W[col], w1 = a.W[a.D + col];
     for (int b = 0; b < a.B; ++b) {
@@ -93,7 +102,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
     a.dW[col] = a.accumulate ? a.dW[col] + g0 : g0;
     a.dW[a.D + col] = a.accumulate ? a.dW[a.D + col] + g1 : g1;
   }
-  if (threadIdx.x < 2) {
+  if (blockIdx.x == 0 && threadIdx.x < 2) {
     float s = 0.f;
     for (int b = 0; b < a.B; ++b) s += a.dlog_in[2 * b + threadIdx.x];
     a.db[threadIdx.x] = a.accumulate ? a.db[threadIdx.x] + s : s;
@@ -149,6 +158,10 @@ struct AdamArgs {
   const int* step;
   float lr, b1, b2, eps, wd;
   int decoupled;
+  long long skip_off4, skip_end4;  // float4 range whose rows may be skipped
+  int row4;                         // float4s per row in that range
+  const unsigned char* touched;     // sticky row flags: nonzero Adam state (nullable)
+  const unsigned char* now;         // rows with a valid gradient this step (nullable = all)
 };
 
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
@@ -158,8 +171,16 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const float step_size = a.lr / bc1;
   const float inv_sqrt_bc2 = 1.f / sqrtf(bc2);
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < a.n4; i += (long long)gridDim.x * 256) {
+    // Rows never touched since the moments were reset have m = v = g = 0: their
+    // Adam update is exactly zero, so skip all their traffic (wd == 0 only).
+    bool gvalid = true;
+    if (a.touched && i >= a.skip_off4 && i < a.skip_end4) {
+      const long long row = (i - a.skip_off4) / a.row4;
+      if (!a.touched[row]) continue;
+      gvalid = a.now == nullptr || a.now[row] != 0;
+    }
     float4 p = reinterpret_cast<float4*>(a.p)[i];
-    float4 g = reinterpret_cast<const float4*>(a.g)[i];
+    float4 g = gvalid ? reinterpret_cast<const float4*>(a.g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     float4 m = reinterpret_cast<float4*>(a.m)[i];
     float4 v = reinterpret_cast<float4*>(a.v)[i];
     float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
@@ -223,13 +244,15 @@ extern "C" {
 
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
-                float* logits, float* loss, float* dlogits, hipStream_t st) {
-  if (B > 4096) return 1;
+                float* logits, float* loss, float* dlogits, float* row_loss, hipStream_t st) {
+  if (B > 65536) return 1;
   HeadArgs a{};
   a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W; a.bias = bias;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.labels = labels;
-  a.logits = logits; a.loss = loss; a.dlogits = dlogits;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(1), dim3(256), 0, st, a);
+  a.logits = logits; a.loss = loss; a.dlogits = dlogits; a.row_loss = row_loss;
+  if (labels && !row_loss) return 2;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st, a);
+  if (labels) hipLaunchKernelGGL(head_loss_mean_kernel, dim3(1), dim3(64), 0, st, row_loss, B, loss);
   return 0;
 }
 
@@ -240,7 +263,7 @@ int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const u
   a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.dlog_in = dlogits;
   a.dW = dW; a.db = db; a.dhidden = (bf16_t*)dhidden; a.accumulate = accumulate;
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(1), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((D + 255) / 256), dim3(256), 0, st, a);
   return 0;
 }
 
@@ -251,9 +274,12 @@ int fd_eval_metrics(const float* logits, const long long* labels, int B, double*
 }
 
 int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float lr,
-            float b1, float b2, float eps, float wd, int decoupled, hipStream_t st) {
-  if (n % 4 != 0) return 1;
-  AdamArgs a{p, g, m, v, (bf16_t*)shadow, n / 4, step, lr, b1, b2, eps, wd, decoupled};
+            float b1, float b2, float eps, float wd, int decoupled, const unsigned char* touched,
+            const unsigned char* now, long long skip_off, long long skip_rows, int row_len, hipStream_t st) {
+  if (n % 4 != 0 || skip_off % 4 != 0 || row_len % 4 != 0) return 1;
+  if (wd != 0.f && touched) return 3;  // skipping untouched rows is exact only without weight decay
+  AdamArgs a{p, g, m, v, (bf16_t*)shadow, n / 4, step, lr, b1, b2, eps, wd, decoupled,
+             skip_off / 4, (skip_off + skip_rows * row_len) / 4, row_len / 4, touched, now};
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, a);
   return 0;
 }

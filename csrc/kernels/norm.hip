@@ -85,26 +85,30 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
 // 4 waves) into part[blockIdx.x][which][D].
 template <int NC>
 DEV void block_colsum(float (&acc)[NC][4], float* lds, float* out, int D) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int e = 0; e < 4; ++e) lds[w * D + 4 * (lane + 64 * c) + e] = acc[c][e];
   __syncthreads();
-  for (int col = threadIdx.x; col < D; col += 256)
-    out[col] = lds[col] + lds[D + col] + lds[2 * D + col] + lds[3 * D + col];
+  for (int col = threadIdx.x; col < D; col += blockDim.x) {
+    float s = 0.f;
+    for (int i = 0; i < nw; ++i) s += lds[i * D + col];
+    out[col] = s;
+  }
   __syncthreads();
 }
 
 template <int NC>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(LnArgs a) {
+__global__ __launch_bounds__(512) void ln_bwd_kernel(LnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][D]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int D = a.D;
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
   float dg[NC][4] = {}, db[NC][4] = {}, dbias[NC][4] = {};
-  for (int row = blockIdx.x * 4 + w; row < a.T; row += gridDim.x * 4) {
+  const int nw = blockDim.x >> 6;
+  for (int row = blockIdx.x * nw + w; row < a.T; row += gridDim.x * nw) {
     const float mean = a.mean[row], rstd = a.rstd[row];
     float xh[NC][4], gd[NC][4], dyv[NC][4];
     float s1 = 0.f, s2 = 0.f;
@@ -232,14 +236,15 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbArgs a) {
 }
 
 template <int NC>
-__global__ __launch_bounds__(256) void emb_bwd_kernel(EmbArgs a) {
+__global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int D = a.D;
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
   float dg[NC][4] = {}, db[NC][4] = {};
-  for (int row = blockIdx.x * 4 + w; row < a.T; row += gridDim.x * 4) {
+  const int nw = blockDim.x >> 6;
+  for (int row = blockIdx.x * nw + w; row < a.T; row += gridDim.x * nw) {
     const long id = load_id(a, row);
     const int s = row % a.S;
     const float mean = a.mean[row], rstd = a.rstd[row];
@@ -322,30 +327,56 @@ __global__ __launch_bounds__(256) void word_grad_pieces_kernel(const long long* 
   }
 }
 
+// With row flags (now/ever), only rows present in this step's batch are valid in
+// dword (now[row] = 1); the optimizer treats the rest as zero, so the 94 MB
+// table never has to be cleared.  ever[] is sticky (rows with nonzero Adam state).
 __global__ __launch_bounds__(256) void word_grad_combine_kernel(const long long* sorted, const float* piece,
-                                                               float* dword, int T, int D, int accumulate) {
+                                                               float* dword, int T, int D, int accumulate,
+                                                               unsigned char* now, unsigned char* ever) {
   const int i = blockIdx.x;
   if (i > 0 && sorted[i] == sorted[i - 1]) return;
   const long long id = sorted[i];
+  const bool add = accumulate && (now ? now[id] != 0 : true);
   for (int col = threadIdx.x; col < D; col += 256) {
     float acc = piece[(size_t)i * D + col];
     for (int j = (i / WCH + 1) * WCH; j < T && sorted[j] == id; j += WCH) acc += piece[(size_t)j * D + col];
     float* dst = dword + (size_t)id * D + col;
-    *dst = accumulate ? *dst + acc : acc;
+    *dst = add ? *dst + acc : acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && now) {
+    now[id] = 1;
+    ever[id] = 1;
   }
 }
 
 // out_k[j] = (acc ? out_k[j] : 0) + sum_blk part[blk][k][j]  for k < nout (fixed order).
+// Block = 4 partial-groups x 64 columns; each wave streams 256 contiguous bytes
+// per partial row, groups combine through LDS in a fixed order.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* part, int nblk, int stride_blk, int D,
                                                      float* o0, float* o1, float* o2, int accumulate) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
   const int k = blockIdx.y;
-  if (j >= D) return;
   float* out = k == 0 ? o0 : (k == 1 ? o1 : o2);
   if (!out) return;
-  float s = accumulate ? out[j] : 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(size_t)b * stride_blk + k * D + j];
-  out[j] = s;
+  float s0 = 0.f, s1 = 0.f;
+  if (j < D) {
+    const float* p = part + k * D + j;
+    int b = grp;
+    for (; b + 4 < nblk; b += 8) {
+      s0 += p[(size_t)b * stride_blk];
+      s1 += p[(size_t)(b + 4) * stride_blk];
+    }
+    if (b < nblk) s0 += p[(size_t)b * stride_blk];
+  }
+  red[grp][lane] = s0 + s1;
+  __syncthreads();
+  if (grp == 0 && j < D) {
+    const float s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[j] = accumulate ? out[j] + s : s;
+  }
 }
 
 // Column sums of a bf16 [T][N] matrix into per-block partials [grid][N] (bias grads).
@@ -363,6 +394,7 @@ __global__ __launch_bounds__(256) void colsum_bf16_partial_kernel(const bf16_t* 
 }
 
 constexpr int LN_GRID = 256;
+constexpr int LN_BWD_THREADS = 512;
 
 }  // namespace
 
@@ -391,9 +423,10 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
   a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.r = (const bf16_t*)r; a.gamma = gamma;
   a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = (bf16_t*)dz; a.dx = (bf16_t*)dx; a.part = work;
   a.T = T; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
-  const int grid = std::min(LN_GRID, (T + 3) / 4);
-  hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(grid), dim3(256), 4 * D * sizeof(float), st, a);
-  hipLaunchKernelGGL(colsum_kernel, dim3((D + 255) / 256, 3), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
+  const int grid = std::min(LN_GRID, (T + 7) / 8);
+  hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
+                     st, a);
+  hipLaunchKernelGGL(colsum_kernel, dim3((D + 63) / 64, 3), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, dbias, accumulate);
   return 0;
 }
@@ -416,22 +449,27 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                const void* word, const void* pos, const float* gamma, const float* mean, const float* rstd,
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
-               int accumulate, hipStream_t st) {
+               int accumulate, unsigned char* now, unsigned char* ever, hipStream_t st) {
   if (D != 768) return 1;
   EmbArgs a{};
   a.dy = (const bf16_t*)dy; a.ids = ids; a.ids64 = ids64; a.word = (const bf16_t*)word;
   a.pos = (const bf16_t*)pos; a.gamma = gamma; a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = dz_buf;
   a.part = work; a.T = T; a.S = S; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
-  const int grid = std::min(LN_GRID, (T + 3) / 4);
-  hipLaunchKernelGGL(emb_bwd_kernel<3>, dim3(grid), dim3(256), 4 * D * sizeof(float), st, a);
-  hipLaunchKernelGGL(colsum_kernel, dim3((D + 255) / 256, 2), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
+  const int grid = std::min(LN_GRID, (T + 7) / 8);
+  hipLaunchKernelGGL(emb_bwd_kernel<3>, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
+                     st, a);
+  hipLaunchKernelGGL(colsum_kernel, dim3((D + 63) / 64, 2), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, (float*)nullptr, accumulate);
   hipLaunchKernelGGL(pos_grad_kernel, dim3(P), dim3(256), 0, st, dz_buf, dpos, B, S, P, D, accumulate);
-  if (!accumulate) hipMemsetAsync(dword, 0, (size_t)V * D * sizeof(float), st);
+  if (!accumulate) {
+    if (now) hipMemsetAsync(now, 0, (size_t)V, st);
+    else hipMemsetAsync(dword, 0, (size_t)V * D * sizeof(float), st);
+  }
   // piece sums reuse `work` (T*D floats)
   hipLaunchKernelGGL(word_grad_pieces_kernel, dim3((T + WCH - 1) / WCH), dim3(256), 0, st, sorted, perm, dz_buf,
                      work, T, D);
-  hipLaunchKernelGGL(word_grad_combine_kernel, dim3(T), dim3(256), 0, st, sorted, work, dword, T, D, 1);
+  hipLaunchKernelGGL(word_grad_combine_kernel, dim3(T), dim3(256), 0, st, sorted, work, dword, T, D,
+                     now ? accumulate : 1, now, ever);
   return 0;
 }
 
@@ -442,7 +480,7 @@ int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int acc
   const int nblk = (T + rows - 1) / rows;
   hipLaunchKernelGGL(colsum_bf16_partial_kernel, dim3(nblk, (N / 4 + 255) / 256), dim3(256), 0, st,
                      (const bf16_t*)x, T, N, rows, work);
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256, 1), dim3(256), 0, st, work, nblk, N, N, out,
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, 1), dim3(256), 0, st, work, nblk, N, N, out,
                      (float*)nullptr, (float*)nullptr, accumulate);
   return 0;
 }

@@ -25,6 +25,9 @@ class ArenaAdam:
         self.arena = model.arena
         self.lr, self.betas, self.eps = lr, tuple(betas), eps
         self.weight_decay, self.decoupled = weight_decay, decoupled
+        if weight_decay != 0.0 and getattr(model, "sparse_word_grad", False):
+            model.sparse_word_grad = False  # AdamW decays every row: keep the dense word gradient
+            model._hip_cache = None
         self._alloc()
 
     def _alloc(self):
@@ -40,6 +43,8 @@ class ArenaAdam:
         self.v.zero_()
         self.step_t.zero_()
         self.host_step = 0
+        if getattr(self.model, "emb_ever", None) is not None:
+            self.model.emb_ever.zero_()
 
     def zero_grad(self, set_to_none: bool = False):
         self.model.zero_grad()
@@ -54,8 +59,18 @@ class ArenaAdam:
         if A.master.is_cuda:
             from ..ops import kernels as K
             K.step_inc(self.step_t, None)
-            K.adam(A.master, A.grad, self.m, self.v, A.shadow, self.step_t, self.lr, b1, b2, self.eps,
-                   self.weight_decay, self.decoupled)
+            sparse = (getattr(self.model, "sparse_word_grad", False) and self.weight_decay == 0.0
+                      and getattr(self.model, "emb_ever", None) is not None)
+            if sparse:
+                off, rows, rl = self.model.word_embedding_span()
+                K.adam(A.master, A.grad, self.m, self.v, A.shadow, self.step_t, self.lr, b1, b2, self.eps,
+                       self.weight_decay, self.decoupled, self.model.emb_ever, self.model.emb_now, off, rows, rl)
+            else:
+                if getattr(self.model, "emb_now", None) is not None and self.model.sparse_word_grad:
+                    raise RuntimeError("sparse word-embedding grads need weight_decay == 0 "
+                                       "(set model.sparse_word_grad = False for AdamW)")
+                K.adam(A.master, A.grad, self.m, self.v, A.shadow, self.step_t, self.lr, b1, b2, self.eps,
+                       self.weight_decay, self.decoupled)
             self.model.mark_shadow_synced()
             return
         t = self.host_step
@@ -80,6 +95,8 @@ class ArenaAdam:
                 "decoupled": self.decoupled}
 
     def load_state_dict(self, sd):
+        if getattr(self.model, "emb_ever", None) is not None:
+            self.model.emb_ever.fill_(1)  # unknown history: treat every row as having state
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
         self.step_t.fill_(int(sd["step"]))

@@ -227,6 +227,9 @@ class DDoSClassifier(nn.Module):
         self.dropout = nn.Dropout(head_dropout)
         self.classifier = _P(self.arena, "classifier.")
         self.impl_request = impl
+        # HIP path: only the word-embedding rows present in the batch carry a gradient
+        # (emb_now flags); ArenaAdam skips the rest exactly.  Set False for a dense grad.
+        self.sparse_word_grad = True
         self.torch_counter = 0
         self._grad_token = None
         self._synced_version = -1
@@ -244,6 +247,10 @@ class DDoSClassifier(nn.Module):
                 m.rebind(self.arena)
         dev = probe.device
         self.rng = torch.zeros(1, dtype=torch.int32, device=dev)
+        # Sparse word-embedding gradient (HIP path): rows valid this step / rows with Adam state.
+        V = self.config.vocab_size
+        self.emb_now = torch.zeros(V, dtype=torch.uint8, device=dev) if dev.type == "cuda" else None
+        self.emb_ever = torch.zeros(V, dtype=torch.uint8, device=dev) if dev.type == "cuda" else None
         self._grad_token = torch.zeros((), device=dev, requires_grad=True)
         self._hip_cache = None
         self._synced_version = -1
@@ -260,6 +267,19 @@ class DDoSClassifier(nn.Module):
         if self.impl_request == "hip" and self.arena.device.type != "cuda":
             raise RuntimeError("impl='hip' needs the model on a GPU")
         return self.impl_request
+
+    def word_embedding_span(self):
+        """(arena offset, rows, row_len) of the word-embedding table."""
+        off, shape = self.arena.offsets["distilbert.embeddings.word_embeddings.weight"]
+        return off, shape[0], shape[1]
+
+    def dense_grad(self, name: str) -> torch.Tensor:
+        """Gradient of ``name`` with the sparse word-embedding rows materialised (zeros elsewhere)."""
+        g = self.arena.gview(name)
+        if name.endswith("word_embeddings.weight") and self.emb_now is not None and self.sparse_word_grad \
+                and self.impl == "hip":
+            g = g * self.emb_now.to(g.dtype)[:, None]
+        return g
 
     def zero_grad(self, set_to_none: bool = False):
         # hip: first-write kernels make zeroing unnecessary; torch: autograd accumulates into the arena.
@@ -301,6 +321,7 @@ class DDoSClassifier(nn.Module):
                 "pos": GradSink(A, pre + "embeddings.position_embeddings.weight"),
                 "ln_w": GradSink(A, pre + "embeddings.LayerNorm.weight"),
                 "ln_b": GradSink(A, pre + "embeddings.LayerNorm.bias"),
+                "flags": (self.emb_now, self.emb_ever) if self.sparse_word_grad else None,
             },
         }
         layers = []

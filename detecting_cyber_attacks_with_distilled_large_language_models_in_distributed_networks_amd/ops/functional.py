@@ -68,8 +68,9 @@ class EmbeddingFn(torch.autograd.Function):
         acc = s["word"].accumulate()
         for k in ("pos", "ln_w", "ln_b"):
             assert s[k].accumulate() == acc
+        now, ever = s.get("flags") or (None, None)
         K.emb_bwd(dy, ids, srt, perm, word, pos, gamma, mean, rstd, s["word"].buf, s["pos"].buf, s["ln_w"].buf,
-                  s["ln_b"].buf, ctx.rc.S, ctx.rc.seed, 1, ctx.p, acc)
+                  s["ln_b"].buf, ctx.rc.S, ctx.rc.seed, 1, ctx.p, acc, now, ever)
         return (None,) * 8
 
 

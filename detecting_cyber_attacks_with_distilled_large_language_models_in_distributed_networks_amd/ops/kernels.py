@@ -139,25 +139,27 @@ def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p):
 
 
 def emb_bwd(dy, ids, sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos, dgamma, dbeta, S, seed, site, p,
-            accumulate=False):
+            accumulate=False, now=None, ever=None):
+    """now/ever: optional uint8 [V] row flags -> sparse word gradient (see ArenaAdam)."""
     T = ids.numel()
     D = gamma.numel()
     dz = workspace(ids.device, "emb_dz", T * D)
     ws = workspace(ids.device, "emb_work", max(T * D, 256 * 3 * D))
     thr, sc = _drop(p)
     ext().emb_bwd(dy.contiguous(), ids.contiguous(), sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos,
-                  dgamma, dbeta, dz, ws, S, seed, site, thr, sc, accumulate)
+                  dgamma, dbeta, dz, ws, S, seed, site, thr, sc, accumulate, now, ever)
 
 
 # ------------------------------------------------------------------ head / metrics / optimizer
 def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None):
     logits = torch.empty(B, 2, dtype=torch.float32, device=hidden.device)
-    loss = dlogits = None
+    loss = dlogits = row_loss = None
     if labels is not None:
         loss = torch.empty((), dtype=torch.float32, device=hidden.device)
         dlogits = torch.empty(B, 2, dtype=torch.float32, device=hidden.device)
+        row_loss = workspace(hidden.device, "head_row_loss", B)
     thr, sc = _drop(p)
-    ext().head_fwd(hidden, B, S, W, b, seed, site, thr, sc, labels, logits, loss, dlogits)
+    ext().head_fwd(hidden, B, S, W, b, seed, site, thr, sc, labels, logits, loss, dlogits, row_loss)
     return logits, loss, dlogits
 
 
@@ -172,8 +174,11 @@ def eval_metrics(logits, labels, acc, counts, prob1=None, preds=None):
     ext().eval_metrics(logits, labels, acc, counts, prob1, preds)
 
 
-def adam(p, g, m, v, shadow, step, lr, b1, b2, eps, wd, decoupled):
-    ext().adam(p, g, m, v, shadow, step, lr, b1, b2, eps, wd, decoupled)
+def adam(p, g, m, v, shadow, step, lr, b1, b2, eps, wd, decoupled, touched=None, now=None, skip_off=0, skip_rows=0,
+         row_len=4):
+    """Flat-arena Adam.  touched/now (uint8 row flags over [skip_off, skip_off+skip_rows*row_len)) let
+    the kernel skip rows with zero state and zero gradient (exact for weight_decay == 0)."""
+    ext().adam(p, g, m, v, shadow, step, lr, b1, b2, eps, wd, decoupled, touched, now, skip_off, skip_rows, row_len)
 
 
 def step_inc(step=None, seed=None):

@@ -244,3 +244,40 @@ def test_dropout_hash_matches_kernel():
     for t in range(T):
         kept = y[t][keep[t]].float()
         assert kept.numel() > 0 and (kept - kept[0]).abs().max().item() == 0
+
+
+def test_sparse_word_grad_and_adam_skip():
+    """Flagged (sparse) word-embedding grad + Adam row skipping == dense path."""
+    B, S, V, P, D = 2, 64, 30522, 512, 768
+    ids = torch.randint(5, 50, (B, S)).to(DEV)
+    word, pos = bf(V, D, scale=0.02, seed=30), bf(P, D, scale=0.02, seed=31)
+    gamma, beta = torch.ones(D, device=DEV), torch.zeros(D, device=DEV)
+    y, mean, rstd = kn.emb_fwd(ids, word, pos, gamma, beta, S, 1e-12, seed_t(1), 1, 0.1)
+    dy = bf(B * S, D, seed=32)
+    srt, perm = torch.sort(ids.reshape(-1))
+    dense = torch.full((V, D), 3.0, device=DEV)
+    sparse = torch.full((V, D), 7.0, device=DEV)  # stale garbage outside the batch rows
+    dpos, dg, db = torch.empty(P, D, device=DEV), torch.empty(D, device=DEV), torch.empty(D, device=DEV)
+    kn.emb_bwd(dy, ids, srt, perm, word, pos, gamma, mean, rstd, dense, dpos, dg, db, S, seed_t(1), 1, 0.1)
+    now = torch.zeros(V, dtype=torch.uint8, device=DEV)
+    ever = torch.zeros(V, dtype=torch.uint8, device=DEV)
+    kn.emb_bwd(dy, ids, srt, perm, word, pos, gamma, mean, rstd, sparse, dpos, dg, db, S, seed_t(1), 1, 0.1,
+               False, now, ever)
+    rows = torch.unique(ids)
+    assert now.sum().item() == rows.numel() and ever.sum().item() == rows.numel()
+    assert torch.equal(sparse[rows], dense[rows])
+    # Adam: full arena = [pad 64 | word table], skip rows by flags
+    n = 64 + V * D
+    p0 = torch.randn(n, device=DEV)
+    gd = torch.zeros(n, device=DEV)
+    gd[64:] = dense.view(-1)
+    gs = torch.zeros(n, device=DEV)
+    gs[64:] = sparse.view(-1)
+    pd_, ps_ = p0.clone(), p0.clone()
+    md, vd, ms, vs = (torch.zeros(n, device=DEV) for _ in range(4))
+    st1, st2 = torch.zeros(1, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV)
+    kn.step_inc(st1)
+    kn.step_inc(st2)
+    kn.adam(pd_, gd, md, vd, None, st1, 1e-3, 0.9, 0.999, 1e-8, 0.0, False)
+    kn.adam(ps_, gs, ms, vs, None, st2, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, ever, now, 64, V, D)
+    assert torch.equal(pd_, ps_) and torch.equal(md, ms) and torch.equal(vd, vs)
