@@ -1,0 +1,157 @@
+"""Command-line entry points (``python -m detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd <cmd>``).
+
+  client   run federated client(s): under torchrun each rank is one client on its
+           own GPU (collective FedAvg over RCCL); alone with ``--transport tcp
+           --client-index k`` it is the reference's ``python clientK.py``
+  server   the reference's ``python server.py``: TCP gather -> FedAvg -> broadcast
+  launch   spawn N local ranks (torch.distributed.run, 127.0.0.1) running ``client``
+  bench    the headline benchmark (bench.py)
+  scaling  run bench.py at several GPU counts and write the scaling curve
+  gen-data write a synthetic CICIDS2017-shaped CSV
+  tokenize print WordPiece tokens of a text
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+from .config import FedConfig
+
+PKG = __package__
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _client(argv):
+    ap = argparse.ArgumentParser(prog="client")
+    FedConfig.add_cli(ap)
+    ap.add_argument("--client-index", type=int, default=None, help="0-based client index (tcp mode)")
+    ap.add_argument("--layers", type=int, default=None, help="override DistilBERT depth (tests)")
+    ns = ap.parse_args(argv)
+    cfg = FedConfig.from_args(ns)
+    if ns.client_index is not None:
+        os.environ["RANK"] = str(ns.client_index)
+        os.environ["WORLD_SIZE"] = "1"
+        os.environ.setdefault("LOCAL_RANK", "0")
+        if cfg.num_clients is None:
+            cfg.num_clients = 2
+    from .fed.runner import FederatedClient
+    from .models import DistilBertConfig
+    mc = DistilBertConfig() if ns.layers is None else DistilBertConfig(n_layers=ns.layers)
+    client = FederatedClient(cfg, model_config=mc)
+    if ns.client_index is not None:  # tcp mode: rank 0 of a 1-process group, identity from the flag
+        client.idx, client.client_id = ns.client_index, ns.client_index + 1
+        client.log.tag, client.log.name = f"[CLIENT {client.client_id}]", f"Client {client.client_id}"
+    rep = client.run()
+    print(json.dumps(rep))
+
+
+def _server(argv):
+    ap = argparse.ArgumentParser(prog="server")
+    ap.add_argument("--num-clients", type=int, default=2)
+    ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--host", default="localhost")
+    ap.add_argument("--port-receive", type=int, default=12345)
+    ap.add_argument("--port-send", type=int, default=12346)
+    ap.add_argument("--timeout", type=float, default=300.0)
+    ap.add_argument("--out-dir", default=".")
+    ap.add_argument("--strict-compat", action="store_true")
+    ap.add_argument("--gzip-level", type=int, default=1)
+    ns = ap.parse_args(argv)
+    from .parallel.transport import FedAvgServer
+    from .utils.logging import TagLogger
+    log = TagLogger.for_server()
+    log.phase("Server starting")
+    for r in range(ns.rounds):
+        srv = FedAvgServer(ns.num_clients, ns.host, ns.port_receive, ns.port_send, ns.timeout, ns.strict_compat,
+                           save_path=os.path.join(ns.out_dir, "ddos_distilbert_model.pth"), log=log,
+                           level=ns.gzip_level)
+        log.phase(f"Round {r + 1}: waiting for {ns.num_clients} clients")
+        if srv.run_round() is None:
+            sys.exit(1)
+    log.phase("Server shutdown")
+
+
+def _launch(argv):
+    ap = argparse.ArgumentParser(prog="launch")
+    ap.add_argument("--nproc", type=int, default=1)
+    ap.add_argument("--port", type=int, default=29511)
+    ns, rest = ap.parse_known_args(argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ns.nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(ns.port), "-m", PKG, "client"] + rest
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def _bench(argv):
+    sys.exit(subprocess.call([sys.executable, os.path.join(ROOT, "bench.py")] + argv))
+
+
+def _scaling(argv):
+    ap = argparse.ArgumentParser(prog="scaling")
+    ap.add_argument("--gpus", default="1,2,4,8")
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--out", default="scaling.json")
+    ns = ap.parse_args(argv)
+    results = []
+    for i, n in enumerate(int(x) for x in ns.gpus.split(",")):
+        base = [os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", str(ns.steps), "--warmup", str(ns.warmup)]
+        if n == 1:
+            cmd = [sys.executable] + base
+        else:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                   "--master-addr", "127.0.0.1", "--master-port", str(29600 + i)] + base
+        out = subprocess.run(cmd, capture_output=True, text=True)
+        line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+        if not line:
+            print(out.stdout[-2000:], out.stderr[-2000:], file=sys.stderr)
+            continue
+        results.append(json.loads(line[-1]))
+        print(line[-1], flush=True)
+    if results:
+        base = results[0]["per_client_batches_per_sec"]
+        for r in results:
+            r["per_client_efficiency_vs_1gpu"] = round(r["per_client_batches_per_sec"] / base, 4)
+        with open(ns.out, "w") as f:
+            json.dump(results, f, indent=1)
+        from .utils.plots import plot_scaling
+        plot_scaling(results, os.path.splitext(ns.out)[0] + ".png")
+
+
+def _gen_data(argv):
+    ap = argparse.ArgumentParser(prog="gen-data")
+    ap.add_argument("--rows", type=int, default=225_745)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", default="CICIDS2017.csv")
+    ns = ap.parse_args(argv)
+    from .data.synthetic import generate_cicids2017, write_csv
+    write_csv(generate_cicids2017(ns.rows, ns.seed), ns.out)
+    print(ns.out)
+
+
+def _tokenize(argv):
+    from .data.tokenizer import WordPieceTokenizer
+    tok = WordPieceTokenizer()
+    text = " ".join(argv)
+    print(tok.tokenize(text))
+    print(tok(text, max_length=128)["input_ids"])
+
+
+COMMANDS = {"client": _client, "server": _server, "launch": _launch, "bench": _bench, "scaling": _scaling,
+            "gen-data": _gen_data, "tokenize": _tokenize}
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] not in COMMANDS:
+        print(__doc__)
+        sys.exit(0 if not argv else 2)
+    COMMANDS[argv[0]](argv[1:])
+
+
+if __name__ == "__main__":
+    main()

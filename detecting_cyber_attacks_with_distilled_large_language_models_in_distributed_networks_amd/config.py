@@ -48,6 +48,11 @@ class FedConfig:
     weighted_fedavg: bool = False           # reference is unweighted (server.py:73-76)
     participation: float = 1.0              # fraction of clients aggregated per round
     timeout_s: float = 300.0                # server.py:10 / client1.py:22
+    transport: str = "collective"           # "collective" (RCCL/gloo all-reduce) | "tcp" (reference protocol)
+    server_host: str = "localhost"          # client1.py:276,314
+    port_receive: int = 12345               # server.py:11
+    port_send: int = 12346                  # server.py:12
+    gzip_level: int = 1                     # tcp payload compression (reference: 9)
     # --- outputs ------------------------------------------------------------------------
     out_dir: str = "."
     plots: bool = True

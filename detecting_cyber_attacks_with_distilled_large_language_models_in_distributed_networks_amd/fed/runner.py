@@ -1,0 +1,208 @@
+"""Federated round orchestration: one process per GPU = one client.
+
+Reference flow per client (client1.py:353-411) + server (server.py:116-137):
+  preprocess -> split 60/20/20 -> train 3 epochs -> eval val/test -> save CSV +
+  clientN_model.pth -> upload (TCP, gzip) -> server averages -> download ->
+  eval val/test of the aggregate -> CSV + plots -> save clientN_model.pth.
+
+Here the upload/average/download triple is ``fedavg_`` (one RCCL all-reduce of
+the fp32 arena, ``parallel/fedavg.py``) and the server's duties (writing
+``ddos_distilbert_model.pth``, the cross-client report) fall to rank 0.  Extras
+over the reference: R rounds in-process, resume from the round sidecar,
+sample-weighted FedAvg, seeded partial participation, fault injection, and a
+cross-client JSON report gathered with an all-gather.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Dict, List, Optional
+
+import torch
+
+from ..config import FedConfig
+from ..data import DeviceLoader, WordPieceTokenizer, build_client_data, generate_cicids2017
+from ..engine import ArenaAdam, evaluate_model, train_model
+from ..models import DDoSClassifier, DistilBertConfig
+from ..parallel import comm
+from ..parallel.fedavg import broadcast_model, fedavg_
+from ..utils import checkpoint as ck
+from ..utils import faults
+from ..utils.logging import TagLogger
+from ..utils.metrics import save_metrics
+from ..utils.timers import PhaseTimer
+
+
+def _metrics_record(m) -> Dict:
+    return {"accuracy": float(m[0]), "loss": float(m[1]), "precision": float(m[2]), "recall": float(m[3]),
+            "f1": float(m[4]), "confusion_matrix": [[int(x) for x in row] for row in m[5]]}
+
+
+class FederatedClient:
+    def __init__(self, cfg: FedConfig, frame=None, model_config: Optional[DistilBertConfig] = None):
+        self.cfg = cfg
+        self.di = comm.init_distributed(timeout_s=cfg.timeout_s)
+        self.idx = self.di.rank                      # 0-based client index
+        self.client_id = self.idx + 1                # reference naming: Client 1, Client 2, ...
+        self.num_clients = cfg.num_clients or self.di.world_size
+        os.makedirs(cfg.out_dir, exist_ok=True)
+        self.log = TagLogger.for_client(self.client_id, enabled=cfg.verbose,
+                                        jsonl_path=os.path.join(cfg.out_dir, f"client{self.client_id}_log.jsonl"))
+        self.timer = PhaseTimer()
+        self.device = self.di.device
+        self.frame = frame
+        self.model_config = model_config or DistilBertConfig()
+
+    # ------------------------------------------------------------------ setup
+    def setup(self):
+        cfg, log = self.cfg, self.log
+        log.phase("Starting client")
+        with self.timer("preprocess"):
+            if self.frame is None:
+                if cfg.csv_path:
+                    import pandas as pd
+                    self.frame = pd.read_csv(cfg.csv_path)
+                else:
+                    # Same seeded synthetic file on every client (they sample it independently).
+                    self.frame = generate_cicids2017(cfg.synthetic_rows, seed=0)
+            self.tokenizer = WordPieceTokenizer.from_pretrained(cfg.model_path)
+            self.data = build_client_data(self.frame, self.idx, cfg.data_fraction, cfg.base_seed, cfg.max_len,
+                                          self.tokenizer, cfg.partition, self.num_clients, log=log)
+        dev = self.device
+        self.train_loader = DeviceLoader(self.data.train, cfg.batch_size, shuffle=True, device=dev,
+                                         seed=cfg.client_seed(self.idx))
+        self.val_loader = DeviceLoader(self.data.val, cfg.eval_batch_size, device=dev)
+        self.test_loader = DeviceLoader(self.data.test, cfg.eval_batch_size, device=dev)
+        mc = self.model_config
+        mc.dropout, mc.attention_dropout = cfg.hidden_dropout, cfg.attention_dropout
+        self.model = DDoSClassifier(cfg.model_path, config=mc, device=dev, impl=cfg.impl, seed=0,
+                                    head_dropout=cfg.head_dropout)
+        # Identical start for every client: rank 0's weights win.
+        broadcast_model(self.model)
+        self.start_round = 0
+        self.history: List[Dict] = []
+        if cfg.resume:
+            st = ck.load_fed_state(cfg.out_dir, self.client_id)
+            if ck.load_model(self.model, ck.client_ckpt_path(cfg.out_dir, self.client_id)):
+                log.info(f"loading pre-trained model from {ck.client_ckpt_path(cfg.out_dir, self.client_id)}")
+                if st:
+                    self.start_round = int(st.get("completed_rounds", 0))
+                    self.history = st.get("history", [])
+        log.info(f"data: {len(self.data.train)} train / {len(self.data.val)} val / {len(self.data.test)} test rows "
+                 f"(sampled {self.data.n_rows}), impl={self.model.impl}, device={dev}")
+        return self
+
+    # ------------------------------------------------------------------ one round
+    def run_round(self, r: int) -> Dict:
+        cfg, log, model = self.cfg, self.log, self.model
+        log.phase(f"Starting round {r + 1}/{cfg.rounds}")
+        opt = ArenaAdam(model, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
+                        decoupled=cfg.decoupled_weight_decay)
+        opt_path = os.path.join(cfg.out_dir, f"client{self.client_id}_optim.pth")
+        if cfg.save_optimizer and r == self.start_round:
+            ck.load_optimizer(opt, opt_path)
+        with self.timer("train"):
+            tr = train_model(model, self.train_loader, None, opt, cfg.epochs, log=log, use_graph=cfg.use_graph)
+        log.info("evaluating local model on validation set...")
+        with self.timer("eval"):
+            val_local = evaluate_model(model, self.val_loader, log=log, name="Validation")
+            log.info("evaluating local model on test set...")
+            local = evaluate_model(model, self.test_loader, log=log, name="Test")
+        sfx = "" if r == 0 else f"_round{r + 1}"
+        save_metrics(local, os.path.join(cfg.out_dir, f"client{self.client_id}_local_metrics{sfx}.csv"), log)
+        ck.save_model(model, ck.client_ckpt_path(cfg.out_dir, self.client_id))
+        if cfg.save_optimizer:
+            ck.save_optimizer(opt, opt_path)
+
+        # ---- FedAvg (replaces send_model -> server aggregate -> receive_aggregated_model)
+        part = faults.participants(r, self.num_clients, cfg.participation, cfg.base_seed)
+        contributes = self.idx in part and not faults.dropped(cfg, self.idx, r)
+        weight = float(len(self.data.train)) if cfg.weighted_fedavg else 1.0
+        faults.maybe_kill(self.idx, r)
+        with self.timer("fedavg"):
+            t0 = time.perf_counter()
+            if cfg.transport == "tcp":
+                total_w = self._tcp_exchange(contributes)
+            else:
+                total_w = fedavg_(model, weight=weight, participate=contributes)
+            if model.device.type == "cuda":
+                torch.cuda.synchronize()
+            t_fed = time.perf_counter() - t0
+        log.info(f"updated with aggregated model (participated={contributes}, total weight={total_w:g}, "
+                 f"{t_fed * 1e3:.2f} ms)")
+        if self.di.is_main:
+            ck.save_model(model, ck.global_ckpt_path(cfg.out_dir))
+        log.info("evaluating aggregated model on validation set...")
+        with self.timer("eval"):
+            val_agg = evaluate_model(model, self.val_loader, log=log, name="Validation")
+            log.info("evaluating aggregated model on test set...")
+            agg = evaluate_model(model, self.test_loader, log=log, name="Test")
+        save_metrics(agg, os.path.join(cfg.out_dir, f"client{self.client_id}_aggregated_metrics{sfx}.csv"), log)
+        if cfg.plots:
+            with self.timer("plot"):
+                from ..utils.plots import plot_evaluation
+                plot_evaluation(local, agg, os.path.join(cfg.out_dir, f"client{self.client_id}_plots"),
+                                f"Client {self.client_id}", log=log)
+        ck.save_model(model, ck.client_ckpt_path(cfg.out_dir, self.client_id))
+        rec = {"round": r + 1, "train": tr, "fedavg_ms": t_fed * 1e3, "participated": contributes,
+               "local_val": _metrics_record(val_local), "local_test": _metrics_record(local),
+               "aggregated_val": _metrics_record(val_agg), "aggregated_test": _metrics_record(agg)}
+        self.history.append(rec)
+        ck.save_fed_state(cfg.out_dir, self.client_id, {"completed_rounds": r + 1, "history": self.history})
+        return rec
+
+    def _tcp_exchange(self, contributes: bool) -> float:
+        """Reference protocol: upload to the FedAvg server, download the mean (client1.py:391-395)."""
+        from ..parallel import transport as tp
+        cfg, log = self.cfg, self.log
+        if contributes:
+            ok = tp.send_model(self.model.state_dict(), cfg.server_host, cfg.port_receive, cfg.gzip_level,
+                               cfg.timeout_s, log)
+            if not ok:
+                log.info("skipping aggregated model evaluation due to send failure")
+                return 0.0
+        agg = tp.receive_aggregated_model(cfg.server_host, cfg.port_send, timeout=cfg.timeout_s, log=log)
+        if agg is None:
+            log.info("skipping aggregated model evaluation due to connection failure")
+            return 0.0
+        self.model.load_state_dict(agg)
+        return float(self.num_clients)
+
+    # ------------------------------------------------------------------ all rounds
+    def run(self) -> Dict:
+        self.setup()
+        for r in range(self.start_round, self.cfg.rounds):
+            self.run_round(r)
+        report = self.report()
+        self.log.phase("Client shutdown")
+        return report
+
+    def report(self) -> Dict:
+        """Cross-client summary on rank 0 (gathered with an all-gather of small vectors)."""
+        last = self.history[-1] if self.history else None
+        vec = [0.0] * 8
+        if last:
+            a, l_ = last["aggregated_test"], last["local_test"]
+            vec = [a["accuracy"], a["f1"], a["precision"], a["recall"], l_["accuracy"], l_["f1"],
+                   last["train"]["batches_per_sec"], last["fedavg_ms"]]
+        allv = comm.all_gather_floats(vec)
+        rep = {"clients": [{"client": i + 1, "aggregated_test_accuracy": v[0], "aggregated_test_f1": v[1],
+                            "aggregated_test_precision": v[2], "aggregated_test_recall": v[3],
+                            "local_test_accuracy": v[4], "local_test_f1": v[5], "train_batches_per_sec": v[6],
+                            "fedavg_ms": v[7]} for i, v in enumerate(allv)],
+               "rounds": self.cfg.rounds, "world_size": self.di.world_size, "phases_s": self.timer.summary()}
+        if self.di.is_main:
+            path = os.path.join(self.cfg.out_dir, "federated_report.json")
+            with open(path, "w") as f:
+                json.dump(rep, f, indent=1)
+            self.log.info(f"federated report written to {path}")
+        return rep
+
+
+def run_federated(cfg: FedConfig, frame=None, model_config: Optional[DistilBertConfig] = None) -> Dict:
+    client = FederatedClient(cfg, frame, model_config)
+    try:
+        return client.run()
+    finally:
+        client.log.close()

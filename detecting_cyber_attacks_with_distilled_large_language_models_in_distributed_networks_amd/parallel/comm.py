@@ -55,7 +55,9 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 300.0, de
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
-        be = backend or ("nccl" if use_gpu else "gloo")
+        # RCCL needs one GPU per rank; FEDDDOS_BACKEND=gloo lets several clients share
+        # a device (functional tests on a 1-GPU box).
+        be = backend or os.environ.get("FEDDDOS_BACKEND") or ("nccl" if use_gpu else "gloo")
         kw = {}
         if be == "nccl":
             kw["device_id"] = dev
