@@ -289,20 +289,20 @@ class DDoSClassifier(nn.Module):
                 for n, key in m._arena_keys.items():
                     getattr(m, n).grad = self.arena.gview(key)
 
-    def _version(self) -> int:
+    def _param_version(self) -> int:
         # Parameters keep their own version counters (p.data = view), so sum them:
         # any in-place update (load_state_dict, torch.optim, FedAvg) changes it.
         return self.arena.master._version + sum(p._version for p in self.parameters())
 
     def sync_shadow(self, force: bool = False):
         """Refresh the bf16 compute shadow if the fp32 masters changed outside our Adam."""
-        v = self._version()
+        v = self._param_version()
         if force or v != self._synced_version:
             self.arena.sync_shadow()
-            self._synced_version = self._version()
+            self._synced_version = self._param_version()
 
     def mark_shadow_synced(self):
-        self._synced_version = self._version()
+        self._synced_version = self._param_version()
 
     # -------------------------------------------------------------- HIP handles
     def _hip_handles(self):

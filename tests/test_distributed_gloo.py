@@ -1,0 +1,122 @@
+"""Multi-process federated paths on CPU with the gloo backend (world_size 2 and 4).
+
+Mirrors BASELINE.json config 1 (2-client FedAvg plumbing, no GPU): the FedAvg
+result must equal the mean of the per-rank weights -- bit-exact for N = 2.
+"""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+PKG = "detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd"
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env(rank, world, port):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+
+
+def _fedavg_worker(rank, world, port, outdir, mode):
+    _env(rank, world, port)
+    from importlib import import_module
+    comm = import_module(f"{PKG}.parallel.comm")
+    fedavg = import_module(f"{PKG}.parallel.fedavg")
+    models = import_module(f"{PKG}.models")
+    comm.init_distributed(device="cpu")
+    m = models.DDoSClassifier(config=models.DistilBertConfig(n_layers=1), seed=100 + rank)
+    before = m.arena.master.clone()
+    torch.save(before, os.path.join(outdir, f"before{rank}.pt"))
+    if mode == "plain":
+        fedavg.fedavg_(m)
+    elif mode == "weighted":
+        fedavg.fedavg_(m, weight=float(rank + 1))
+    elif mode == "drop":
+        fedavg.fedavg_(m, participate=(rank != 1))
+    elif mode == "broadcast":
+        fedavg.broadcast_model(m)
+    torch.save(m.arena.master.clone(), os.path.join(outdir, f"after{rank}.pt"))
+    comm.shutdown()
+
+
+def _run(world, mode, tmp_path):
+    port = _free_port()
+    mp.spawn(_fedavg_worker, args=(world, port, str(tmp_path), mode), nprocs=world, join=True)
+    before = [torch.load(tmp_path / f"before{r}.pt", weights_only=True) for r in range(world)]
+    after = [torch.load(tmp_path / f"after{r}.pt", weights_only=True) for r in range(world)]
+    return before, after
+
+
+def test_fedavg_two_clients_bit_exact(tmp_path):
+    before, after = _run(2, "plain", tmp_path)
+    mean = (before[0] + before[1]) * 0.5
+    assert torch.equal(after[0], after[1])
+    assert torch.equal(after[0], mean)
+
+
+def test_fedavg_four_clients(tmp_path):
+    before, after = _run(4, "plain", tmp_path)
+    mean = torch.stack(before).mean(0)
+    for a in after:
+        assert torch.allclose(a, mean, atol=1e-7)
+
+
+def test_fedavg_weighted(tmp_path):
+    before, after = _run(2, "weighted", tmp_path)
+    ref = (before[0] * 1 + before[1] * 2) / 3
+    assert torch.allclose(after[0], ref, atol=1e-7) and torch.equal(after[0], after[1])
+
+
+def test_fedavg_dropped_client(tmp_path):
+    before, after = _run(2, "drop", tmp_path)
+    assert torch.equal(after[0], before[0]) and torch.equal(after[1], before[0])
+
+
+def test_broadcast_initial_model(tmp_path):
+    before, after = _run(2, "broadcast", tmp_path)
+    assert torch.equal(after[1], before[0])
+
+
+def _fed_worker(rank, world, port, outdir):
+    _env(rank, world, port)
+    from importlib import import_module
+    runner = import_module(f"{PKG}.fed.runner")
+    config = import_module(f"{PKG}.config")
+    models = import_module(f"{PKG}.models")
+    data = import_module(f"{PKG}.data")
+    comm = import_module(f"{PKG}.parallel.comm")
+    comm.init_distributed(device="cpu")
+    cfg = config.FedConfig(out_dir=outdir, synthetic_rows=1500, data_fraction=0.1, max_len=64, epochs=1,
+                           batch_size=8, eval_batch_size=16, plots=(rank == 0), resume=False, rounds=2,
+                           verbose=False)
+    frame = data.generate_cicids2017(cfg.synthetic_rows, seed=0)
+    runner.run_federated(cfg, frame=frame, model_config=models.DistilBertConfig(n_layers=1))
+    comm.shutdown()
+
+
+def test_two_client_federated_run(tmp_path):
+    """BASELINE.json config 1 in miniature: 2 clients x 2 rounds over gloo."""
+    port = _free_port()
+    mp.spawn(_fed_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for cid in (1, 2):
+        for name in ("local_metrics.csv", "aggregated_metrics.csv", "local_metrics_round2.csv", "model.pth"):
+            assert (tmp_path / f"client{cid}_{name}").exists(), name
+        st = json.load(open(tmp_path / f"client{cid}_fed_state.json"))
+        assert st["completed_rounds"] == 2
+    a = torch.load(tmp_path / "client1_model.pth", weights_only=True)
+    b = torch.load(tmp_path / "client2_model.pth", weights_only=True)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k   # both clients hold the aggregate
+    g = torch.load(tmp_path / "ddos_distilbert_model.pth", weights_only=True)
+    assert all(torch.equal(a[k], g[k]) for k in a)
+    rep = json.load(open(tmp_path / "federated_report.json"))
+    assert len(rep["clients"]) == 2
+    assert (tmp_path / "client1_plots" / "metrics_comparison.png").exists()

@@ -1,0 +1,97 @@
+"""TCP compatibility transport: reference framing, server gather/avg/broadcast, probe handling."""
+import socket
+import threading
+import time
+
+import pytest
+import torch
+
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.parallel import (
+    transport as tp)
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.parallel.fedavg import (
+    aggregate_state_dicts)
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.utils import faults
+
+
+def _ports(n):
+    out = []
+    for _ in range(n):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            out.append(s.getsockname()[1])
+    return out
+
+
+def test_framing_roundtrip_and_ack():
+    a, b = socket.socketpair()
+    payload = bytes(range(256)) * 20000  # 5 MB: spans several 1 MiB chunks / 4 MiB recvs
+    res = {}
+    t = threading.Thread(target=lambda: res.setdefault("data", tp.receive_chunked_data(b)))
+    t.start()
+    assert tp.send_chunked_data(a, payload)
+    t.join()
+    assert res["data"] == payload
+    a.close(); b.close()
+
+
+def test_header_wire_format():
+    a, b = socket.socketpair()
+    t = threading.Thread(target=lambda: (b.recv(64), b.sendall(tp.ACK)))
+    t.start()
+    a.sendall(b"")
+    ok = tp.send_chunked_data(a, b"xyz")
+    t.join()
+    assert ok
+    a.close(); b.close()
+
+
+def test_codec_is_weights_only_safe():
+    sd = {"w": torch.randn(3, 4), "b": torch.zeros(2)}
+    out = tp.decode_state(tp.encode_state(sd))
+    assert torch.equal(out["w"], sd["w"]) and torch.equal(out["b"], sd["b"])
+
+
+def test_aggregate_state_dicts_semantics():
+    s1 = {"a": torch.tensor([1.0, 2.0]), "pos": torch.tensor([0, 1])}
+    s2 = {"a": torch.tensor([3.0, 6.0]), "pos": torch.tensor([0, 1])}
+    out = aggregate_state_dicts([s1, s2], num_clients=2)
+    assert torch.equal(out["a"], torch.tensor([2.0, 4.0])) and torch.equal(out["pos"], s1["pos"])
+    assert aggregate_state_dicts([s1], num_clients=2) is None  # server.py:69-71 guard
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_server_round_two_clients(strict):
+    pr, ps = _ports(2)
+    srv = tp.FedAvgServer(2, "127.0.0.1", pr, ps, timeout=30, strict_compat=strict)
+    res = {}
+    th = threading.Thread(target=lambda: res.setdefault("agg", srv.run_round()))
+    th.start()
+    srv.ready.wait(10)
+    states = [{"w": torch.full((4,), float(i + 1))} for i in range(2)]
+    for s in states:
+        assert tp.send_model(s, "127.0.0.1", pr, timeout=30)
+    if not strict:
+        # a bare readiness probe must not be counted as a client (reference bug)
+        time.sleep(0.2)
+        while True:
+            try:
+                with socket.create_connection(("127.0.0.1", ps), timeout=2):
+                    break
+            except OSError:
+                time.sleep(0.1)
+    got = []
+    ths = [threading.Thread(target=lambda: got.append(
+        tp.receive_aggregated_model("127.0.0.1", ps, timeout=30, strict_compat=strict))) for _ in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    th.join(30)
+    assert len(got) == 2 and all(g is not None and torch.equal(g["w"], torch.full((4,), 1.5)) for g in got)
+    assert torch.equal(res["agg"]["w"], torch.full((4,), 1.5))
+
+
+def test_partial_participation_is_deterministic():
+    a = faults.participants(3, 8, 0.5, seed=42)
+    assert a == faults.participants(3, 8, 0.5, seed=42) and len(a) == 4
+    assert faults.participants(0, 8, 1.0) == list(range(8))
