@@ -32,7 +32,13 @@ DEV uint32_t f2bf(float f) {
   return u >> 16;
 }
 
-DEV uint32_t pack_bf2(float a, float b) { return f2bf(a) | (f2bf(b) << 16); }
+// Two fp32 -> packed bf16x2 with round-to-nearest-even; hipcc lowers the
+// __bf16 conversions to one v_cvt_pk_bf16_f32 on gfx950 (NaN stays NaN).
+DEV uint32_t pack_bf2(float a, float b) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
 
 DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
