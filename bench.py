@@ -96,6 +96,8 @@ def main():
     dt = time.perf_counter() - t0
     dt = comm.all_reduce_max(dt)
     loss = float(loss_acc.item()) / args.steps
+    if not (loss == loss and abs(loss) < 1e6):
+        raise SystemExit(f"bench: non-finite training loss {loss} -- refusing to report a throughput")
     n = di.world_size
     per_client = args.steps / dt
     if di.is_main:

@@ -36,6 +36,7 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
                int accumulate, unsigned char* now, unsigned char* ever, hipStream_t st);
 int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, hipStream_t st);
+int fd_rank_sort(const void* ids, int ids64, int T, long long* sorted, long long* perm, hipStream_t st);
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
                 float* logits, float* loss, float* dlogits, float* row_loss, hipStream_t st);
@@ -192,7 +193,7 @@ void ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::T
   need(work, at::kFloat, "work");
   const int64_t D = gamma.numel(), T = x.numel() / D;
   TORCH_CHECK(D == 768 && dy.numel() == T * D && dz.numel() == T * D, "ln_bwd: shapes");
-  TORCH_CHECK(work.numel() >= 256 * 3 * D, "ln_bwd: work too small");
+  TORCH_CHECK(work.numel() >= std::min<int64_t>(512, (T + 7) / 8) * 3 * D, "ln_bwd: work too small");
   if (thr != 0) TORCH_CHECK(dx.has_value() && dx->numel() == T * D, "ln_bwd: dx required with dropout");
   check_rc(fd_ln_bwd(dy.data_ptr(), x.data_ptr(), ptr<void>(r), gamma.data_ptr<float>(), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), dz.data_ptr(), ptr<void>(dx), ptr<float>(dgamma), ptr<float>(dbeta),
@@ -243,7 +244,7 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
   need(work, at::kFloat, "work");
   const int64_t D = gamma.numel(), T = ids.numel(), V = word.size(0), P = pos.size(0);
   TORCH_CHECK(sorted.numel() == T && perm.numel() == T && dy.numel() == T * D && dz_buf.numel() >= T * D, "emb_bwd: sizes");
-  TORCH_CHECK(dword.numel() == V * D && dpos.numel() == P * D && work.numel() >= std::max<int64_t>(T * D, 256 * 3 * D),
+  TORCH_CHECK(dword.numel() == V * D && dpos.numel() == P * D && work.numel() >= std::max<int64_t>(T * D, std::min<int64_t>(512, (T + 7) / 8) * 3 * D),
               "emb_bwd: grad/work sizes");
   check_rc(fd_emb_bwd(dy.data_ptr(), ids.data_ptr(), ids.scalar_type() == at::kLong,
                       reinterpret_cast<const long long*>(sorted.data_ptr()),
@@ -254,6 +255,19 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
                       (int)D, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, accumulate ? 1 : 0,
                       ptr<unsigned char>(now), ptr<unsigned char>(ever), stream()),
            "emb_bwd");
+}
+
+void rank_sort(const at::Tensor& ids, const at::Tensor& sorted, const at::Tensor& perm) {
+  TORCH_CHECK(ids.is_cuda() && ids.is_contiguous() && (ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt),
+              "ids must be contiguous GPU int64/int32");
+  need(sorted, at::kLong, "sorted");
+  need(perm, at::kLong, "perm");
+  TORCH_CHECK(sorted.numel() == ids.numel() && perm.numel() == ids.numel() && ids.numel() <= 16384,
+              "rank_sort: sizes (T <= 16384)");
+  check_rc(fd_rank_sort(ids.data_ptr(), ids.scalar_type() == at::kLong, (int)ids.numel(),
+                        reinterpret_cast<long long*>(sorted.data_ptr()), reinterpret_cast<long long*>(perm.data_ptr()),
+                        stream()),
+           "rank_sort");
 }
 
 void colsum_bf16(const at::Tensor& x, const at::Tensor& out, const at::Tensor& work, bool accumulate) {
@@ -392,6 +406,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("emb_fwd", &emb_fwd);
   m.def("emb_bwd", &emb_bwd);
   m.def("colsum_bf16", &colsum_bf16);
+  m.def("rank_sort", &rank_sort);
   m.def("head_fwd", &head_fwd);
   m.def("head_bwd", &head_bwd);
   m.def("eval_metrics", &eval_metrics);

@@ -230,7 +230,19 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     dof[s] = load_frag_global(a.dctx + (tok0 + q) * D + h * DH + 32 * s + 8 * g);
   }
   const size_t st = ((size_t)b * H + h) * S + q;
-  const float lse = a.lse[st], dl = a.delta[st];
+  const float lse = a.lse[st];
+  // FA2 preprocessing fused in: delta = rowsum(dO * O) for this query; the dK/dV
+  // kernel (launched after this one) reads it back.
+  float dl = 0.f;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 of = load_frag_global(a.ctx + (tok0 + q) * D + h * DH + 32 * s + 8 * g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)of[j]) * bf2f((uint16_t)dof[s][j]);
+  }
+  dl += __shfl_xor(dl, 16, 64);
+  dl += __shfl_xor(dl, 32, 64);
+  if (g == 0) const_cast<float*>(a.delta)[st] = dl;
   const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
 
   f32x4 dq[4];
@@ -403,8 +415,6 @@ int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const floa
   a.dctx = (const bf16_t*)dctx; a.delta = delta; a.dqkv = (bf16_t*)dqkv;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f;
-  const long n = (long)B * S * H;
-  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
   return 0;

@@ -293,66 +293,138 @@ __global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
   block_colsum<NC>(db, lds, out + D, D);
 }
 
-// dpos[s][:] = sum_b dz[b*S + s][:], rows s >= S zeroed (first write) -- fixed order.
-__global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* dpos, int B, int S, int P,
-                                                       int D, int accumulate) {
+// dpos[s][:] = sum_b dz[b*S + s][:] -- fixed order; all B loads of a column issued
+// back to back.  Rows s >= S are handled by a memset (first write) on the host side.
+__global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* dpos, int B, int S, int D,
+                                                       int accumulate) {
   const int s = blockIdx.x;
   for (int col = threadIdx.x; col < D; col += 256) {
     float acc = accumulate ? dpos[(size_t)s * D + col] : 0.f;
-    if (s < S)
-      for (int b = 0; b < B; ++b) acc += dz[((size_t)b * S + s) * D + col];
+    for (int b0 = 0; b0 < B; b0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = b0 + u < B ? dz[((size_t)(b0 + u) * S + s) * D + col] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u];
+    }
     dpos[(size_t)s * D + col] = acc;
   }
 }
 
-// Word-embedding gradient from token ids sorted on device (torch.sort):
-// pass 1 sums each run piece inside fixed 32-position chunks into piece[start];
-// pass 2 lets the run's first position add its pieces in chunk order.  Every
-// output row is written by exactly one block -> deterministic, atomic-free.
+// Deterministic token grouping without a library sort: the sorted position of
+// token t is the number of tokens with key (id, index) smaller than its own
+// (a rank sort; O(T^2) compares but T <= 16k and every compare is an LDS
+// broadcast).  4 threads per token each scan a quarter of the keys.
+template <typename I>
+__global__ __launch_bounds__(256) void rank_sort_kernel(const I* ids, int T, long long* sorted, long long* perm) {
+  extern __shared__ int keys[];  // T ids
+  for (int i = threadIdx.x; i < T; i += 256) keys[i] = (int)ids[i];
+  __syncthreads();
+  const int t = blockIdx.x * 64 + (threadIdx.x >> 2);
+  const int part = threadIdx.x & 3;
+  int cnt = 0;
+  int my = 0;
+  if (t < T) {
+    my = keys[t];
+    const int q = (T + 3) / 4, j0 = part * q, j1 = min(T, j0 + q);
+    for (int j = j0; j < j1; ++j) {
+      const int k = keys[j];
+      cnt += (k < my) | ((k == my) & (j < t));
+    }
+  }
+  cnt += __shfl_xor(cnt, 1, 64);
+  cnt += __shfl_xor(cnt, 2, 64);
+  if (t < T && part == 0) {
+    sorted[cnt] = my;
+    perm[cnt] = t;
+  }
+}
+
+// Word-embedding gradient over tokens grouped by id (rank sort above).  Pass 1:
+// one block per 32 sorted positions; every thread loads its 32 rows x 3 columns
+// up front, then walks the runs: a run contained in the chunk is written
+// straight to dword, a piece of a run crossing a chunk boundary goes to
+// piece[start].  Pass 2: the chunk holding a crossing run's first position adds
+// that run's pieces in chunk order.  Every output row is written by exactly one
+// block -> deterministic, atomic-free.
 constexpr int WCH = 32;
+DEV void word_row_store(float* dword, long long id, int col, float acc, bool add) {
+  float* dst = dword + (size_t)id * 768 + col;
+  *dst = add ? *dst + acc : acc;
+}
+
 __global__ __launch_bounds__(256) void word_grad_pieces_kernel(const long long* sorted, const long long* perm,
-                                                              const float* dz, float* piece, int T, int D) {
-  const int c0 = blockIdx.x * WCH, c1 = min(T, c0 + WCH);
-  for (int col = threadIdx.x; col < D; col += 256) {
-    float acc = 0.f;
-    int start = c0;
-    for (int i = c0; i < c1; ++i) {
-      acc += dz[(size_t)perm[i] * D + col];
-      if (i + 1 == c1 || sorted[i + 1] != sorted[i]) {
-        piece[(size_t)start * D + col] = acc;
-        acc = 0.f;
+                                                              const float* dz, float* piece, float* dword, int T,
+                                                              int accumulate, unsigned char* now,
+                                                              unsigned char* ever) {
+  constexpr int D = 768;
+  __shared__ long long sid[WCH + 2];
+  __shared__ long long sperm[WCH];
+  const int c0 = blockIdx.x * WCH, c1 = min(T, c0 + WCH), n = c1 - c0;
+  if (threadIdx.x < n) {
+    sid[threadIdx.x + 1] = sorted[c0 + threadIdx.x];
+    sperm[threadIdx.x] = perm[c0 + threadIdx.x];
+  }
+  if (threadIdx.x == 0) sid[0] = c0 > 0 ? sorted[c0 - 1] : -1;
+  if (threadIdx.x == 1) sid[n + 1] = c1 < T ? sorted[c1] : -1;
+  __syncthreads();
+  float v[3][WCH];
+#pragma unroll
+  for (int i = 0; i < WCH; ++i)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c][i] = i < n ? dz[(size_t)sperm[i] * D + threadIdx.x + 256 * c] : 0.f;
+  float acc[3] = {0.f, 0.f, 0.f};
+  int start = 0;
+#pragma unroll
+  for (int i = 0; i < WCH; ++i) {
+    if (i < n) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) acc[c] += v[c][i];
+      const long long id = sid[i + 1];
+      if (sid[i + 2] != id || i + 1 == n) {  // piece [start, i] ends here
+        const bool run_starts_here = sid[start] != id;        // sid[start] is the predecessor
+        const bool run_ends_here = i + 1 < n || sid[n + 1] != id;
+        if (run_starts_here && run_ends_here) {
+          const bool add = accumulate && (now ? now[id] != 0 : true);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) word_row_store(dword, id, threadIdx.x + 256 * c, acc[c], add);
+          if (threadIdx.x == 0 && now) { now[id] = 1; ever[id] = 1; }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) piece[(size_t)(c0 + start) * D + threadIdx.x + 256 * c] = acc[c];
+        }
+        acc[0] = acc[1] = acc[2] = 0.f;
         start = i + 1;
       }
     }
   }
 }
 
-// With row flags (now/ever), only rows present in this step's batch are valid in
-// dword (now[row] = 1); the optimizer treats the rest as zero, so the 94 MB
-// table never has to be cleared.  ever[] is sticky (rows with nonzero Adam state).
 __global__ __launch_bounds__(256) void word_grad_combine_kernel(const long long* sorted, const float* piece,
-                                                               float* dword, int T, int D, int accumulate,
+                                                               float* dword, int T, int accumulate,
                                                                unsigned char* now, unsigned char* ever) {
-  const int i = blockIdx.x;
-  if (i > 0 && sorted[i] == sorted[i - 1]) return;
-  const long long id = sorted[i];
+  constexpr int D = 768;
+  const int c0 = blockIdx.x * WCH, c1 = min(T, c0 + WCH);
+  if (c1 >= T || sorted[c1] != sorted[c1 - 1]) return;  // no run crosses this chunk's end
+  // first position of the crossing run (within this chunk)
+  const long long id = sorted[c1 - 1];
+  int a = c1 - 1;
+  while (a > c0 && sorted[a - 1] == id) --a;
+  if (a == c0 && c0 > 0 && sorted[c0 - 1] == id) return;  // run started in an earlier chunk
   const bool add = accumulate && (now ? now[id] != 0 : true);
   for (int col = threadIdx.x; col < D; col += 256) {
-    float acc = piece[(size_t)i * D + col];
-    for (int j = (i / WCH + 1) * WCH; j < T && sorted[j] == id; j += WCH) acc += piece[(size_t)j * D + col];
-    float* dst = dword + (size_t)id * D + col;
-    *dst = add ? *dst + acc : acc;
+    float acc = piece[(size_t)a * D + col];
+    for (int j = c1; j < T && sorted[j] == id; j += WCH) acc += piece[(size_t)j * D + col];
+    word_row_store(dword, id, col, acc, add);
   }
-  __syncthreads();
-  if (threadIdx.x == 0 && now) {
-    now[id] = 1;
-    ever[id] = 1;
-  }
+  if (threadIdx.x == 0 && now) { now[id] = 1; ever[id] = 1; }
 }
 
 // out_k[j] = (acc ? out_k[j] : 0) + sum_blk part[blk][k][j]  for k < nout (fixed order).
-// Block = 4 partial-groups x 64 columns; each wave streams 256 contiguous bytes
-// per partial row, groups combine through LDS in a fixed order.
+// Block = 4 partial-groups x 64 columns.  Every thread issues all of its partial
+// loads back to back (UNR in flight) before summing them in a fixed order, so the
+// reduction is bandwidth- not latency-bound; groups combine through LDS.
+template <int UNR>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* part, int nblk, int stride_blk, int D,
                                                      float* o0, float* o1, float* o2, int accumulate) {
   __shared__ float red[4][64];
@@ -361,21 +433,25 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* part, int nblk
   const int k = blockIdx.y;
   float* out = k == 0 ? o0 : (k == 1 ? o1 : o2);
   if (!out) return;
-  float s0 = 0.f, s1 = 0.f;
+  float s = 0.f;
   if (j < D) {
     const float* p = part + k * D + j;
-    int b = grp;
-    for (; b + 4 < nblk; b += 8) {
-      s0 += p[(size_t)b * stride_blk];
-      s1 += p[(size_t)(b + 4) * stride_blk];
+    for (int b0 = grp; b0 < nblk; b0 += 4 * UNR) {
+      float v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int b = b0 + 4 * u;
+        v[u] = b < nblk ? p[(size_t)b * stride_blk] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) s += v[u];
     }
-    if (b < nblk) s0 += p[(size_t)b * stride_blk];
   }
-  red[grp][lane] = s0 + s1;
+  red[grp][lane] = s;
   __syncthreads();
   if (grp == 0 && j < D) {
-    const float s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    out[j] = accumulate ? out[j] + s : s;
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[j] = accumulate ? out[j] + t : t;
   }
 }
 
@@ -386,14 +462,20 @@ __global__ __launch_bounds__(256) void colsum_bf16_partial_kernel(const bf16_t* 
   if (c4 >= N) return;
   const int r0 = blockIdx.x * rows_per_blk, r1 = min(T, r0 + rows_per_blk);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  for (int r = r0; r < r1; ++r) {
-    const uint2 v = *reinterpret_cast<const uint2*>(x + (size_t)r * N + c4);
-    s0 += lo_bf(v.x); s1 += hi_bf(v.x); s2 += lo_bf(v.y); s3 += hi_bf(v.y);
+  for (int rb = r0; rb < r1; rb += 16) {
+    uint2 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      v[u] = rb + u < r1 ? *reinterpret_cast<const uint2*>(x + (size_t)(rb + u) * N + c4) : make_uint2(0, 0);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      s0 += lo_bf(v[u].x); s1 += hi_bf(v[u].x); s2 += lo_bf(v[u].y); s3 += hi_bf(v[u].y);
+    }
   }
   *reinterpret_cast<float4*>(part + (size_t)blockIdx.x * N + c4) = make_float4(s0, s1, s2, s3);
 }
 
-constexpr int LN_GRID = 256;
+constexpr int LN_GRID = 512;
 constexpr int LN_BWD_THREADS = 512;
 
 }  // namespace
@@ -426,7 +508,7 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
   const int grid = std::min(LN_GRID, (T + 7) / 8);
   hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
                      st, a);
-  hipLaunchKernelGGL(colsum_kernel, dim3((D + 63) / 64, 3), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
+  hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 3), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, dbias, accumulate);
   return 0;
 }
@@ -458,29 +540,45 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
   const int grid = std::min(LN_GRID, (T + 7) / 8);
   hipLaunchKernelGGL(emb_bwd_kernel<3>, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
                      st, a);
-  hipLaunchKernelGGL(colsum_kernel, dim3((D + 63) / 64, 2), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
+  hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 2), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, (float*)nullptr, accumulate);
-  hipLaunchKernelGGL(pos_grad_kernel, dim3(P), dim3(256), 0, st, dz_buf, dpos, B, S, P, D, accumulate);
+  if (!accumulate && P > S) hipMemsetAsync(dpos + (size_t)S * D, 0, (size_t)(P - S) * D * sizeof(float), st);
+  hipLaunchKernelGGL(pos_grad_kernel, dim3(S), dim3(256), 0, st, dz_buf, dpos, B, S, D, accumulate);
   if (!accumulate) {
     if (now) hipMemsetAsync(now, 0, (size_t)V, st);
     else hipMemsetAsync(dword, 0, (size_t)V * D * sizeof(float), st);
   }
   // piece sums reuse `work` (T*D floats)
-  hipLaunchKernelGGL(word_grad_pieces_kernel, dim3((T + WCH - 1) / WCH), dim3(256), 0, st, sorted, perm, dz_buf,
-                     work, T, D);
-  hipLaunchKernelGGL(word_grad_combine_kernel, dim3(T), dim3(256), 0, st, sorted, work, dword, T, D,
-                     now ? accumulate : 1, now, ever);
+  const int chunks = (T + WCH - 1) / WCH;
+  const int acc_mode = now ? accumulate : 1;
+  hipLaunchKernelGGL(word_grad_pieces_kernel, dim3(chunks), dim3(256), 0, st, sorted, perm, dz_buf, work, dword, T,
+                     acc_mode, now, ever);
+  hipLaunchKernelGGL(word_grad_combine_kernel, dim3(chunks), dim3(256), 0, st, sorted, work, dword, T, acc_mode, now,
+                     ever);
   return 0;
 }
 
 // out[N] (+)= column sums of bf16 x[T][N]; work >= ceil(T/rows)*N floats.
+// Group token ids (int64/int32) by value: sorted ids + originating positions (int64).
+int fd_rank_sort(const void* ids, int ids64, int T, long long* sorted, long long* perm, hipStream_t st) {
+  if (T > 16384) return 1;
+  const size_t lds = (size_t)T * sizeof(int);
+  if (ids64)
+    hipLaunchKernelGGL(rank_sort_kernel<long long>, dim3((T + 63) / 64), dim3(256), lds, st, (const long long*)ids, T,
+                       sorted, perm);
+  else
+    hipLaunchKernelGGL(rank_sort_kernel<int>, dim3((T + 63) / 64), dim3(256), lds, st, (const int*)ids, T, sorted,
+                       perm);
+  return 0;
+}
+
 int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, hipStream_t st) {
   if (N % 4 != 0) return 1;
   const int rows = 32;
   const int nblk = (T + rows - 1) / rows;
   hipLaunchKernelGGL(colsum_bf16_partial_kernel, dim3(nblk, (N / 4 + 255) / 256), dim3(256), 0, st,
                      (const bf16_t*)x, T, N, rows, work);
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, 1), dim3(256), 0, st, work, nblk, N, N, out,
+  hipLaunchKernelGGL(colsum_kernel<16>, dim3((N + 63) / 64, 1), dim3(256), 0, st, work, nblk, N, N, out,
                      (float*)nullptr, (float*)nullptr, accumulate);
   return 0;
 }

@@ -64,7 +64,7 @@ class EmbeddingFn(torch.autograd.Function):
     def backward(ctx, dy):
         ids, word, pos, gamma, mean, rstd = ctx.tensors
         s = ctx.sinks
-        srt, perm = torch.sort(ids.reshape(-1))
+        srt, perm = K.group_ids(ids)
         acc = s["word"].accumulate()
         for k in ("pos", "ln_w", "ln_b"):
             assert s[k].accumulate() == acc

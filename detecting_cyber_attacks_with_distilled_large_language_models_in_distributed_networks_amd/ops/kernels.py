@@ -15,6 +15,7 @@ from ._ext import ext
 from .dropout import threshold
 
 D_MODEL = 768
+LN_GRID = 512  # must match csrc/kernels/norm.hip (partial-sum blocks of the LN backward)
 
 _WS = {}
 
@@ -121,10 +122,21 @@ def ln_bwd(dy, x, r, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, acc
     dz = torch.empty_like(x)
     thr, sc = _drop(p)
     dx = torch.empty_like(x) if thr else None
-    ws = workspace(x.device, "ln_part", 256 * 3 * D)
+    ws = workspace(x.device, "ln_part", LN_GRID * 3 * D)
     ext().ln_bwd(dy.contiguous(), x, r, gamma, mean, rstd, dz, dx, dgamma, dbeta, dbias, ws, seed, site, thr, sc,
                  accumulate)
     return dz, (dx if dx is not None else dz)
+
+
+def group_ids(ids: torch.Tensor):
+    """(sorted ids, positions) grouping equal ids -- deterministic rank sort on device."""
+    flat = ids.reshape(-1).contiguous()
+    if flat.numel() > 16384:
+        return torch.sort(flat, stable=True)
+    srt = torch.empty(flat.numel(), dtype=torch.int64, device=flat.device)
+    perm = torch.empty_like(srt)
+    ext().rank_sort(flat, srt, perm)
+    return srt, perm
 
 
 def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p):
@@ -144,7 +156,7 @@ def emb_bwd(dy, ids, sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos
     T = ids.numel()
     D = gamma.numel()
     dz = workspace(ids.device, "emb_dz", T * D)
-    ws = workspace(ids.device, "emb_work", max(T * D, 256 * 3 * D))
+    ws = workspace(ids.device, "emb_work", max(T * D, LN_GRID * 3 * D))
     thr, sc = _drop(p)
     ext().emb_bwd(dy.contiguous(), ids.contiguous(), sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos,
                   dgamma, dbeta, dz, ws, S, seed, site, thr, sc, accumulate, now, ever)

@@ -172,7 +172,9 @@ def test_embedding():
     dword = torch.full((V, D), 5.0, device=DEV)
     dpos = torch.full((P, D), 5.0, device=DEV)
     dgamma, dbeta = torch.empty(D, device=DEV), torch.empty(D, device=DEV)
-    srt, perm = torch.sort(ids.reshape(-1))
+    srt, perm = kn.group_ids(ids)
+    rs, rp = torch.sort(ids.reshape(-1), stable=True)
+    assert torch.equal(srt, rs) and torch.equal(perm, rp)
     kn.emb_bwd(dy, ids, srt, perm, word, pos, gamma, mean, rstd, dword, dpos, dgamma, dbeta, S, seed_t(4), 1, p)
     gw, gp, gg, gb = torch.autograd.grad(yr, [wf, pf, gf, bf_], dy.float())
     assert rel_err(dword, gw) < 1e-2
