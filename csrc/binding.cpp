@@ -193,7 +193,7 @@ void ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::T
   need(work, at::kFloat, "work");
   const int64_t D = gamma.numel(), T = x.numel() / D;
   TORCH_CHECK(D == 768 && dy.numel() == T * D && dz.numel() == T * D, "ln_bwd: shapes");
-  TORCH_CHECK(work.numel() >= std::min<int64_t>(512, (T + 7) / 8) * 3 * D, "ln_bwd: work too small");
+  TORCH_CHECK(work.numel() >= std::min<int64_t>(256, (T + 7) / 8) * 3 * D, "ln_bwd: work too small");
   if (thr != 0) TORCH_CHECK(dx.has_value() && dx->numel() == T * D, "ln_bwd: dx required with dropout");
   check_rc(fd_ln_bwd(dy.data_ptr(), x.data_ptr(), ptr<void>(r), gamma.data_ptr<float>(), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), dz.data_ptr(), ptr<void>(dx), ptr<float>(dgamma), ptr<float>(dbeta),
@@ -244,7 +244,7 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
   need(work, at::kFloat, "work");
   const int64_t D = gamma.numel(), T = ids.numel(), V = word.size(0), P = pos.size(0);
   TORCH_CHECK(sorted.numel() == T && perm.numel() == T && dy.numel() == T * D && dz_buf.numel() >= T * D, "emb_bwd: sizes");
-  TORCH_CHECK(dword.numel() == V * D && dpos.numel() == P * D && work.numel() >= std::max<int64_t>(T * D, std::min<int64_t>(512, (T + 7) / 8) * 3 * D),
+  TORCH_CHECK(dword.numel() == V * D && dpos.numel() == P * D && work.numel() >= std::max<int64_t>(T * D, std::min<int64_t>(256, (T + 7) / 8) * 3 * D),
               "emb_bwd: grad/work sizes");
   check_rc(fd_emb_bwd(dy.data_ptr(), ids.data_ptr(), ids.scalar_type() == at::kLong,
                       reinterpret_cast<const long long*>(sorted.data_ptr()),

@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* d
 // broadcast).  4 threads per token each scan a quarter of the keys.
 template <typename I>
 __global__ __launch_bounds__(256) void rank_sort_kernel(const I* ids, int T, long long* sorted, long long* perm) {
-  extern __shared__ int keys[];  // T ids
+  extern __shared__ __attribute__((aligned(16))) int keys[];  // T ids
   for (int i = threadIdx.x; i < T; i += 256) keys[i] = (int)ids[i];
   __syncthreads();
   const int t = blockIdx.x * 64 + (threadIdx.x >> 2);
@@ -326,8 +326,17 @@ __global__ __launch_bounds__(256) void rank_sort_kernel(const I* ids, int T, lon
   int my = 0;
   if (t < T) {
     my = keys[t];
-    const int q = (T + 3) / 4, j0 = part * q, j1 = min(T, j0 + q);
-    for (int j = j0; j < j1; ++j) {
+    // the 4 threads of a token read adjacent 16-byte groups: one ds_read_b128 each,
+    // 64 contiguous bytes per token -> no bank conflicts, 4 keys per read
+    const int T4 = T & ~15;
+    for (int j = 4 * part; j < T4; j += 16) {
+      const int4 k = *reinterpret_cast<const int4*>(keys + j);
+      cnt += (k.x < my) | ((k.x == my) & (j < t));
+      cnt += (k.y < my) | ((k.y == my) & (j + 1 < t));
+      cnt += (k.z < my) | ((k.z == my) & (j + 2 < t));
+      cnt += (k.w < my) | ((k.w == my) & (j + 3 < t));
+    }
+    for (int j = T4 + part; j < T; j += 4) {
       const int k = keys[j];
       cnt += (k < my) | ((k == my) & (j < t));
     }
@@ -412,9 +421,17 @@ __global__ __launch_bounds__(256) void word_grad_combine_kernel(const long long*
   while (a > c0 && sorted[a - 1] == id) --a;
   if (a == c0 && c0 > 0 && sorted[c0 - 1] == id) return;  // run started in an earlier chunk
   const bool add = accumulate && (now ? now[id] != 0 : true);
+  int npieces = 0;  // chunk starts c1, c1+32, ... still inside the run
+  for (int j = c1; j < T && sorted[j] == id; j += WCH) ++npieces;
   for (int col = threadIdx.x; col < D; col += 256) {
     float acc = piece[(size_t)a * D + col];
-    for (int j = c1; j < T && sorted[j] == id; j += WCH) acc += piece[(size_t)j * D + col];
+    for (int p0 = 0; p0 < npieces; p0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = p0 + u < npieces ? piece[(size_t)(c1 + (p0 + u) * WCH) * D + col] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u];
+    }
     word_row_store(dword, id, col, acc, add);
   }
   if (threadIdx.x == 0 && now) { now[id] = 1; ever[id] = 1; }
@@ -475,7 +492,7 @@ __global__ __launch_bounds__(256) void colsum_bf16_partial_kernel(const bf16_t* 
   *reinterpret_cast<float4*>(part + (size_t)blockIdx.x * N + c4) = make_float4(s0, s1, s2, s3);
 }
 
-constexpr int LN_GRID = 512;
+constexpr int LN_GRID = 256;
 constexpr int LN_BWD_THREADS = 512;
 
 }  // namespace

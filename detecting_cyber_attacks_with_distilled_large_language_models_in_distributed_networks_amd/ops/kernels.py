@@ -15,7 +15,7 @@ from ._ext import ext
 from .dropout import threshold
 
 D_MODEL = 768
-LN_GRID = 512  # must match csrc/kernels/norm.hip (partial-sum blocks of the LN backward)
+LN_GRID = 256  # must match csrc/kernels/norm.hip (partial-sum blocks of the LN backward)
 
 _WS = {}
 
