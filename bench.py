@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--impl", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--layers", type=int, default=6)
+    ap.add_argument("--teacher", action="store_true",
+                    help="distillation step (BASELINE.json config 5): BERT-base teacher fwd + DistilBERT student")
     args = ap.parse_args()
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -64,7 +66,14 @@ def main():
     model = models.DDoSClassifier(config=cfg, device=dev, impl=args.impl, seed=0)
     fedavg.broadcast_model(model)
     opt = engine.ArenaAdam(model, lr=2e-5)
-    step = engine.GraphedTrainStep(engine.make_step_fn(model, opt), warmup=2,
+    if args.teacher:
+        teacher = models.BertTeacherClassifier(config=models.bert_base_config(), device=dev, impl=args.impl)
+        fedavg.broadcast_model(teacher)
+        teacher.eval()
+        fn = engine.make_kd_step_fn(model, teacher, opt, 2.0, 0.5)
+    else:
+        fn = engine.make_step_fn(model, opt)
+    step = engine.GraphedTrainStep(fn, warmup=2,
                                    enabled=(not args.no_graph) and args.impl == "hip" and dev.type == "cuda")
     model.train()
 
@@ -114,7 +123,8 @@ def main():
             "vs_baseline": round(per_client / BASELINE_BATCHES_PER_SEC_PER_CLIENT, 3),
             "dtype": "bf16" if args.impl == "hip" else "fp32",
             "data": "synthetic CICIDS2017-shaped flows rendered to text, WordPiece seq128; random-init weights",
-            "config": {"model": f"DistilBERT-base ({args.layers} layers) + Linear(768,2) DDoSClassifier",
+            "config": {"model": f"DistilBERT-base ({args.layers} layers) + Linear(768,2) DDoSClassifier"
+                                + (" <- KD from BERT-base teacher" if args.teacher else ""),
                        "global_batch": B * n, "seq_len": S, "parallelism": f"fedavg{n} (1 client/GPU)"},
             "per_client_batches_per_sec": round(per_client, 4),
             "samples_per_sec_total": round(per_client * n * B, 2),

@@ -2,4 +2,4 @@
 from .evaluate import evaluate_model  # noqa: F401
 from .graph import GraphedTrainStep  # noqa: F401
 from .optim import ArenaAdam  # noqa: F401
-from .train import make_step_fn, train_model  # noqa: F401
+from .train import make_kd_step_fn, make_step_fn, train_model  # noqa: F401

@@ -33,15 +33,39 @@ def make_step_fn(model, optimizer, criterion=None):
     return step
 
 
+def make_kd_step_fn(student, teacher, optimizer, temperature: float = 2.0, alpha: float = 0.5):
+    """Distillation step: frozen teacher forward (no grad, eval) -> student forward ->
+    alpha * CE + (1 - alpha) * T^2 * KL(teacher || student) -> backward -> Adam."""
+    from ..models.bert import kd_loss
+
+    def step(ids, mask, labels):
+        optimizer.zero_grad()
+        with torch.no_grad():
+            t_logits = teacher(ids, mask)
+        s_logits = student(ids, mask)
+        loss = kd_loss(s_logits, t_logits, labels, temperature, alpha)
+        loss.backward()
+        optimizer.step()
+        return loss.detach()
+
+    return step
+
+
 def train_model(model, train_loader, criterion=None, optimizer=None, num_epochs: int = 3, device=None,
                 log=None, use_graph: bool = True, max_steps: Optional[int] = None,
-                on_epoch: Optional[Callable] = None) -> Dict:
+                on_epoch: Optional[Callable] = None, teacher=None, kd_temperature: float = 2.0,
+                kd_alpha: float = 0.5) -> Dict:
     from .optim import ArenaAdam
     optimizer = optimizer or ArenaAdam(model)
     if log:
-        log.phase("Starting model training")
+        log.phase("Starting model training" + (" (distillation from teacher)" if teacher is not None else ""))
     model.train()
-    step = GraphedTrainStep(make_step_fn(model, optimizer, criterion), enabled=use_graph and model.device.type == "cuda")
+    if teacher is not None:
+        teacher.eval()
+        fn = make_kd_step_fn(model, teacher, optimizer, kd_temperature, kd_alpha)
+    else:
+        fn = make_step_fn(model, optimizer, criterion)
+    step = GraphedTrainStep(fn, enabled=use_graph and model.device.type == "cuda")
     epoch_losses: List[float] = []
     steps = 0
     t0 = time.perf_counter()

@@ -80,6 +80,12 @@ class FederatedClient:
                                     head_dropout=cfg.head_dropout)
         # Identical start for every client: rank 0's weights win.
         broadcast_model(self.model)
+        self.teacher = None
+        if cfg.teacher:
+            from ..models.bert import BertTeacherClassifier, bert_base_config
+            self.teacher = BertTeacherClassifier(cfg.extra.get("teacher_path"), config=bert_base_config(),
+                                                 device=dev, impl=cfg.impl)
+            broadcast_model(self.teacher)
         self.start_round = 0
         self.history: List[Dict] = []
         if cfg.resume:
@@ -102,8 +108,16 @@ class FederatedClient:
         opt_path = os.path.join(cfg.out_dir, f"client{self.client_id}_optim.pth")
         if cfg.save_optimizer and r == self.start_round:
             ck.load_optimizer(opt, opt_path)
+        if self.teacher is not None and r == self.start_round:
+            # Local teacher fine-tune (BERT-base, same kernels), then distil into the student.
+            log.info("training BERT-base teacher")
+            t_opt = ArenaAdam(self.teacher, lr=cfg.lr)
+            with self.timer("teacher"):
+                train_model(self.teacher, self.train_loader, None, t_opt, int(cfg.extra.get("teacher_epochs", cfg.epochs)),
+                            log=log, use_graph=cfg.use_graph)
         with self.timer("train"):
-            tr = train_model(model, self.train_loader, None, opt, cfg.epochs, log=log, use_graph=cfg.use_graph)
+            tr = train_model(model, self.train_loader, None, opt, cfg.epochs, log=log, use_graph=cfg.use_graph,
+                             teacher=self.teacher, kd_temperature=cfg.kd_temperature, kd_alpha=cfg.kd_alpha)
         log.info("evaluating local model on validation set...")
         with self.timer("eval"):
             val_local = evaluate_model(model, self.val_loader, log=log, name="Validation")

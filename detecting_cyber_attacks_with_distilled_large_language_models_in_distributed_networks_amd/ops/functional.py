@@ -138,10 +138,12 @@ class HeadFn(torch.autograd.Function):
         ctx.save_for_backward(hidden)
         ctx.dlog = dlog
         ctx.fused_loss = labels is not None
-        ctx.mark_non_differentiable(logits)
         if labels is not None:
+            ctx.mark_non_differentiable(logits)  # the gradient flows through the fused loss
             return loss, logits
-        return logits, logits.new_empty(0)
+        dummy = logits.new_empty(0)
+        ctx.mark_non_differentiable(dummy)
+        return logits, dummy
 
     @staticmethod
     def backward(ctx, g0, g1):

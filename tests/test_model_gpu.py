@@ -86,3 +86,36 @@ def test_full_size_step_is_finite():
     losses = [float(step(ids, mask, labels)) for _ in range(4)]
     assert all(l == l and abs(l) < 100 for l in losses), losses
     assert torch.isfinite(m.arena.master).all()
+
+
+def test_teacher_hip_matches_torch_and_kd_graph_step():
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.models import (
+        BertTeacherClassifier, bert_base_config)
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.engine import (
+        GraphedTrainStep, make_kd_step_fn)
+    th = BertTeacherClassifier(config=bert_base_config(n_layers=2), device="cuda", impl="hip", seed=4)
+    tt = BertTeacherClassifier(config=bert_base_config(n_layers=2), device="cuda", impl="torch", seed=4)
+    ids, mask, labels = _batch(4, 128, seed=3)
+    th.eval(); tt.eval()
+    with torch.no_grad():
+        assert rel(th(ids, mask), tt(ids, mask)) < 5e-2
+    student = DDoSClassifier(config=DistilBertConfig(n_layers=2), device="cuda", impl="hip", seed=0)
+    opt = ArenaAdam(student, lr=1e-4)
+    step = GraphedTrainStep(make_kd_step_fn(student, th, opt, 2.0, 0.5), warmup=2)
+    student.train()
+    losses = [float(step(ids, mask, labels)) for _ in range(8)]
+    assert step.graph is not None, step.failed
+    assert all(l == l for l in losses) and losses[-1] < losses[0]
+
+
+def test_plain_forward_logits_are_differentiable():
+    """model(ids, mask) + an external criterion (the reference's API) backpropagates on the HIP path."""
+    m = DDoSClassifier(config=DistilBertConfig(n_layers=1), device="cuda", impl="hip", seed=0)
+    r = DDoSClassifier(config=DistilBertConfig(n_layers=1), device="cuda", impl="torch", seed=0)
+    ids, mask, labels = _batch(4, 64, seed=1)
+    m.eval(); r.eval()
+    crit = torch.nn.CrossEntropyLoss()
+    m.zero_grad(); r.zero_grad()
+    crit(m(ids, mask), labels).backward()
+    crit(r(ids, mask), labels).backward()
+    assert rel(m.dense_grad("classifier.weight"), r.arena.gview("classifier.weight")) < 5e-2
