@@ -14,6 +14,7 @@ extern "C" {
 int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
             int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
             long long workspace_elems, int accumulate, hipStream_t st);
+int fd_gemm_set_cfg(int kind, int cfg, int splits);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, hipStream_t st);
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx,
@@ -109,6 +110,11 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
                    (int)A.size(1), (int)B.size(1), (int)N, ptr<float>(bias), ptr<void>(aux), (int)N,
                    ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, stream()),
            "gemm");
+}
+
+// Tuning hook: force GEMM configuration `cfg` (-1 = measured default) for a kind.
+void gemm_set_cfg(int64_t kind, int64_t cfg, int64_t splits) {
+  check_rc(fd_gemm_set_cfg((int)kind, (int)cfg, (int)splits), "gemm_set_cfg");
 }
 
 void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
@@ -398,6 +404,7 @@ void axpby(const at::Tensor& dst, const at::Tensor& x, const c10::optional<at::T
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the federated DistilBERT engine";
   m.def("gemm", &gemm);
+  m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("mask_to_bias", &mask_to_bias);

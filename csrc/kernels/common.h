@@ -64,11 +64,29 @@ DEV bool drop_keep(uint32_t seed, uint32_t idx, uint32_t threshold) {
   return hash32(seed, idx) >= threshold;
 }
 
-DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// Exact-erf GELU (HF DistilBERT's activation) evaluated with Abramowitz-Stegun
+// 7.1.26 for erfc (|error| <= 1.5e-7, far below bf16 resolution): one v_exp and
+// one v_rcp instead of ocml erff's branchy polynomial.  The exp(-x^2/2) term is
+// shared with the derivative's pdf.
+DEV void gelu_parts(float x, float& cdf, float& pdf) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  const float e = __expf(-z * z);
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
+  const float half_erfc = 0.5f * poly * e;  // 0.5 * erfc(|x| / sqrt(2))
+  cdf = x >= 0.f ? 1.0f - half_erfc : half_erfc;
+  pdf = 0.39894228040143268f * e;
+}
+DEV float gelu_erf(float x) {
+  float c, p;
+  gelu_parts(x, c, p);
+  return x * c;
+}
 DEV float gelu_erf_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float c, p;
+  gelu_parts(x, c, p);
+  return fmaf(x, p, c);
 }
 
 DEV float wave_sum(float v) {

@@ -9,23 +9,26 @@
 //   backward dx = dy W          -> A_KMAJ, !B_KMAJ  ("NN")
 //   backward dW = dy^T x        -> !A_KMAJ, !B_KMAJ ("TN", split-K fp32 slabs)
 //
-// Design (MI355X-first, cdna_hip_programming.md §5):
-//  * 256 threads = 4 waves in a 2x2 grid; each wave owns a (BM/2)x(BN/2) tile of
-//    16x16 MFMA sub-tiles; K tile 64 (two 32-deep MFMA steps).
+// Design (MI355X-first, cdna_hip_programming.md §5, "Pipelining across barriers"):
+//  * One template over (BM, BN, waves WMxWN, LDS ring depth S); the host picks a
+//    measured configuration per shape (cfg table below) so the grid is one
+//    full round of 256 CUs wherever the shape allows.
 //  * Operand tiles go HBM/L2 -> LDS with global_load_lds_dwordx4 (LDS-DMA, no
-//    VGPR round trip, no ds_write issue cost), double-buffered: tile k+1's DMA
-//    is issued before tile k's MFMAs; one vmcnt(0)+barrier per K tile.
+//    VGPR round trip) into an S-deep ring.  Per K tile: counted vmcnt that
+//    leaves the S-2 younger tiles in flight, ONE raw s_barrier, then the DMA of
+//    tile kt+S-1 into the slot everyone just finished reading.
+//  * Both 32-deep fragment sets of a K tile are read up front, so the second
+//    set's ds_reads overlap the first set's MFMAs.
 //  * The DMA writes LDS lane-linearly, so bank-conflict swizzles are applied on
 //    the per-lane SOURCE address and undone on the read (rule 21):
 //    K-major images [rows][64] use chunk ^= (row>>1)&7 (conflict-free
-//    ds_read_b128 fragments); MN-major images [64 k][BMN] are read with the
-//    transposing ds_read_b64_tr_b16 (T10) and use chunk ^= fk(k) so the 16-lane
-//    groups of each half-wave hit disjoint banks.
+//    ds_read_b128 fragments); MN-major images are [64 k][64|128 mn] sub-images
+//    read with the transposing ds_read_b64_tr_b16 (T10), chunk ^= fk(k).
 //  * Operands are swapped inside the MFMA (D = B^T A^T = C^T) so every lane owns
-//    4 consecutive output columns: 8-byte bf16 / 16-byte fp32 stores, vectorised
-//    bias / residual / GELU-aux loads in the epilogue.
-//  * Host picks the tile (128x128 / 128x96 / 128x64) that best fills 256 CUs x
-//    2 resident blocks; XCD-aware bijective block remap (T1).
+//    4 consecutive output columns.  The epilogue parks the tile in LDS and the
+//    whole block writes contiguous 16-byte row chunks (the per-lane 16-row x
+//    32-byte store pattern is store-issue bound).
+//  * XCD-aware bijective block remap (T1) + group-M tile walk sized to the L2.
 #include "common.h"
 
 #include <cstdlib>
@@ -55,14 +58,15 @@ struct GemmParams {
   int k_split;           // K elements per split (multiple of 64)
   long long slab_stride; // elements between fp32 slabs
   int group_m;           // tile-walk group height (L2 working-set control)
-  int diag;              // FD_GEMM_DIAG bits (profiling only): 1 no in-loop DMA, 2 no MFMA, 4 no stores
+  int diag;              // FD_GEMM_DIAG bits (profiling only): 1 no in-loop DMA, 4 no stores
 };
+
+constexpr int BKT = 64;
+constexpr int LDS_MAX = 163840;
 
 // Logical tile id -> (tm, tn).  After the XCD remap each XCD owns a contiguous
 // range of logical ids; walking them in groups of `gm` M-tiles x all N-tiles
-// means the blocks resident on one XCD share gm A-panels and a few B-panels,
-// a working set sized by the host to fit the XCD's 4 MiB L2 (instead of every
-// XCD streaming all of A from the Infinity Cache).
+// means the blocks resident on one XCD share gm A-panels and a few B-panels.
 DEV void tile_coords(int lid, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
   const int per_group = gm * tiles_n;
   const int group = lid / per_group;
@@ -73,53 +77,49 @@ DEV void tile_coords(int lid, int tiles_m, int tiles_n, int gm, int& tm, int& tn
   tn = in_group / rows;
 }
 
-constexpr int BKT = 64;
-
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void gbl_void;
 
-// Swizzle of 16-byte chunks for the MN-major ([k][mn]) LDS image.
-template <int BMN>
+// Swizzle of 16-byte chunks for an MN-major ([k][mn]) sub-image of width W.
+template <int W>
 DEV int fk(int k) {
-  if constexpr (BMN == 128) return ((k & 3) | ((k >> 1) & 4)) << 1;
+  if constexpr (W == 128) return ((k & 3) | ((k >> 1) & 4)) << 1;
   else return (((k >> 1) & 1) | ((k >> 2) & 2)) << 1;
 }
 
-// K-major chunk swizzle: 128-byte rows (BK=64) -> chunk ^ ((r>>1)&7);
-// 64-byte rows (BK=32) -> chunk ^ ((r>>2)&3).  Either way 16 consecutive rows
-// reading the same logical chunk land on 16 distinct 16-byte bank slots.
-template <int BK>
-DEV int ksw(int r) {
-  if constexpr (BK == 64) return (r >> 1) & 7;
-  else return (r >> 2) & 3;
-}
+// K-major chunk swizzle for 128-byte rows: 16 consecutive rows reading the same
+// logical chunk land on 16 distinct 16-byte bank slots.
+DEV int ksw(int r) { return (r >> 1) & 7; }
 
-template <int ROWS, bool KMAJ, int BK = BKT, int NWAVES = 4>
+template <int ROWS, bool KMAJ, int NWAVES>
 struct Operand {
-  static constexpr int BYTES = ROWS * BK * 2;              // one LDS buffer
-  static constexpr int PER_WAVE = BYTES / 1024 / NWAVES;  // 1 KiB DMA pieces per wave per tile
-  static constexpr int CH = KMAJ ? BK / 8 : ROWS / 8; // 16-byte chunks per LDS row
-  static constexpr int ROWB = CH * 16;
-  static_assert(KMAJ || ROWS == 64 || ROWS == 128, "MN-major tiles must be 64 or 128 wide");
-  static_assert(PER_WAVE * NWAVES * 1024 == BYTES, "tile must split into whole 1 KiB pieces per wave");
+  static constexpr int BYTES = ROWS * BKT * 2;              // one LDS slot
+  static constexpr int PER_WAVE = BYTES / 1024 / NWAVES;   // 1 KiB DMA pieces per wave per tile
+  // MN-major: [BKT][SUB] sub-images stacked along mn
+  static constexpr int SUB = (ROWS % 128 == 0) ? 128 : 64;
+  static constexpr int SUB_BYTES = BKT * SUB * 2;
+  static constexpr int SUB_CH = SUB / 8;
 
   // LDS-DMA of the K tile starting at k0.  K-major rows beyond `lim` are clamped
-  // (their products land in output rows that are never stored).
+  // (their products land in output rows that are never stored).  Scalar tile
+  // base + 32-bit per-lane byte offset (loop-invariant, one VGPR per piece).
   DEV static void stage(const bf16_t* base, int ld, int row0, int k0, int lim, char* lds, int wid, int lane) {
+    const char* sbase = reinterpret_cast<const char*>(KMAJ ? base + k0 : base + (size_t)k0 * ld + row0);
 #pragma unroll
     for (int i = 0; i < PER_WAVE; ++i) {
       const int piece = wid * PER_WAVE + i;
-      const int pos = piece * 64 + lane;  // physical 16-byte chunk of the image
-      const bf16_t* src;
+      const int pos = piece * 64 + lane;  // physical 16-byte chunk of the slot
+      uint32_t off;
       if constexpr (KMAJ) {
-        const int r = pos / CH, c = (pos % CH) ^ ksw<BK>(r);
+        const int r = pos >> 3, c = (pos & 7) ^ ksw(r);
         const int gr = min(row0 + r, lim - 1);
-        src = base + (size_t)gr * ld + k0 + c * 8;
+        off = (uint32_t)(gr * ld + c * 8) * 2u;
       } else {
-        const int k = pos / CH, c = (pos % CH) ^ fk<ROWS>(k);
-        src = base + (size_t)(k0 + k) * ld + row0 + c * 8;
+        const int sub = pos / (SUB_BYTES / 16), lp = pos % (SUB_BYTES / 16);
+        const int k = lp / SUB_CH, c = (lp % SUB_CH) ^ fk<SUB>(k);
+        off = (uint32_t)(k * ld + sub * SUB + c * 8) * 2u;
       }
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds + piece * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(sbase + off), (lds_void*)(lds + piece * 1024), 16, 0, 0);
     }
   }
 
@@ -128,15 +128,17 @@ struct Operand {
     if constexpr (KMAJ) {
       const int row = row0 + (lane & 15);
       const int c = s * 4 + (lane >> 4);
-      return *reinterpret_cast<const bf16x8*>(lds + row * ROWB + ((c ^ ksw<BK>(row)) << 4));
+      return *reinterpret_cast<const bf16x8*>(lds + row * 128 + ((c ^ ksw(row)) << 4));
     } else {
+      const char* img = lds + (row0 / SUB) * SUB_BYTES;
+      const int r0 = row0 % SUB;
       const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
-      const int c = (row0 >> 3) + (p >> 1);
+      const int c = (r0 >> 3) + (p >> 1);
       bf16x8 out;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int k = s * 32 + 8 * g + 4 * h + q;
-        const char* addr = lds + k * ROWB + ((c ^ fk<ROWS>(k)) << 4) + (p & 1) * 8;
+        const char* addr = img + k * (SUB * 2) + ((c ^ fk<SUB>(k)) << 4) + (p & 1) * 8;
         bf16x4v v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4v*)(addr));
         out[4 * h + 0] = v[0];
         out[4 * h + 1] = v[1];
@@ -148,56 +150,154 @@ struct Operand {
   }
 };
 
-template <int EPI>
-DEV void epilogue(const GemmParams& p, int m, int n, float v0, float v1, float v2, float v3) {
-  if constexpr (EPI == EPI_F32) {
-    float* C = reinterpret_cast<float*>(p.C) + (size_t)blockIdx.z * p.slab_stride;
-    *reinterpret_cast<float4*>(C + (size_t)m * p.ldc + n) = make_float4(v0, v1, v2, v3);
-  } else {
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
-      const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
-      v0 += b.x; v1 += b.y; v2 += b.z; v3 += b.w;
+// ---------------------------------------------------------------- epilogue
+// Each wave parks its accumulators in LDS (bias applied; bf16, or fp32 when the
+// finishing math needs per-element operands and the fp32 tile fits), then the
+// block writes full contiguous rows with 16-byte stores.  Row pitch = payload
+// + 16 B: the 16-row ds_write groups land on distinct banks for BN in
+// {64, 96, 128, 192, 256}.
+template <int EPI, int BM, int BN>
+struct EpiTraits {
+  static constexpr bool ELEM = (EPI == EPI_ADD || EPI == EPI_GELU_BWD);
+  static constexpr bool F32S = EPI == EPI_F32 || (ELEM && BM * (BN * 4 + 16) <= LDS_MAX);
+  static constexpr int ES = F32S ? 4 : 2;
+  static constexpr int BYTES = BM * (BN * ES + 16);
+};
+
+template <int BM, int BN, int TM, int TN, int EPI, int NT>
+DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int m0, int n0,
+                         int wr, int wc, int lane, int tid) {
+  using TR = EpiTraits<EPI, BM, BN>;
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int LDC = BN * TR::ES + 16;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int r = wr * TM + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int c = wc * TN + j * 16 + 4 * (lane >> 4);
+      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+        const float4 b = *reinterpret_cast<const float4*>(p.bias + n0 + c);
+        v0 += b.x; v1 += b.y; v2 += b.z; v3 += b.w;
+      }
+      if constexpr (TR::ELEM && !TR::F32S) {  // big tile: finish in registers (scattered 8-byte loads)
+        const int m = min(m0 + r, p.M - 1), n = n0 + c;
+        if constexpr (EPI == EPI_GELU_BWD) {
+          const uint2 u = *reinterpret_cast<const uint2*>(p.aux + (size_t)m * p.ldaux + n);
+          v0 *= gelu_erf_grad(lo_bf(u.x)); v1 *= gelu_erf_grad(hi_bf(u.x));
+          v2 *= gelu_erf_grad(lo_bf(u.y)); v3 *= gelu_erf_grad(hi_bf(u.y));
+        } else {
+          const uint2 r2 = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldres + n);
+          v0 += lo_bf(r2.x); v1 += hi_bf(r2.x); v2 += lo_bf(r2.y); v3 += hi_bf(r2.y);
+        }
+      }
+      if constexpr (TR::F32S) {
+        *reinterpret_cast<float4*>(smem + r * LDC + c * 4) = make_float4(v0, v1, v2, v3);
+      } else {
+        *reinterpret_cast<uint2*>(smem + r * LDC + c * 2) = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+      }
     }
-    if constexpr (EPI == EPI_BIAS_GELU) {
-      // GELU on the bf16-rounded pre-activation, exactly what the backward re-reads.
-      const uint2 u = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
-      *reinterpret_cast<uint2*>(p.aux + (size_t)m * p.ldaux + n) = u;
-      v0 = gelu_erf(lo_bf(u.x)); v1 = gelu_erf(hi_bf(u.x));
-      v2 = gelu_erf(lo_bf(u.y)); v3 = gelu_erf(hi_bf(u.y));
-    }
-    if constexpr (EPI == EPI_GELU_BWD) {
-      const uint2 u = *reinterpret_cast<const uint2*>(p.aux + (size_t)m * p.ldaux + n);
-      v0 *= gelu_erf_grad(lo_bf(u.x)); v1 *= gelu_erf_grad(hi_bf(u.x));
-      v2 *= gelu_erf_grad(lo_bf(u.y)); v3 *= gelu_erf_grad(hi_bf(u.y));
-    }
-    if constexpr (EPI == EPI_ADD) {
-      const uint2 r = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldres + n);
-      v0 += lo_bf(r.x); v1 += hi_bf(r.x); v2 += lo_bf(r.y); v3 += hi_bf(r.y);
-    }
+  }
+  __syncthreads();
+  if (p.diag & 4) return;
+  if constexpr (!TR::F32S) {
+    constexpr int CPR = BN / 8;  // 16-byte chunks (8 bf16) per row
     bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-    *reinterpret_cast<uint2*>(C + (size_t)m * p.ldc + n) = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+#pragma unroll 4
+    for (int id = tid; id < BM * CPR; id += NT) {
+      const int r = id / CPR, cc = id - r * CPR;
+      const int m = m0 + r;
+      if (m >= p.M) break;  // rows ascend with id
+      const uint4 u = *reinterpret_cast<const uint4*>(smem + r * LDC + cc * 16);
+      const int n = n0 + cc * 8;
+      if constexpr (EPI == EPI_BIAS_GELU) {
+        // GELU on the bf16-rounded pre-activation, exactly what the backward re-reads.
+        *reinterpret_cast<uint4*>(p.aux + (size_t)m * p.ldaux + n) = u;
+        uint4 y;
+        y.x = pack_bf2(gelu_erf(lo_bf(u.x)), gelu_erf(hi_bf(u.x)));
+        y.y = pack_bf2(gelu_erf(lo_bf(u.y)), gelu_erf(hi_bf(u.y)));
+        y.z = pack_bf2(gelu_erf(lo_bf(u.z)), gelu_erf(hi_bf(u.z)));
+        y.w = pack_bf2(gelu_erf(lo_bf(u.w)), gelu_erf(hi_bf(u.w)));
+        *reinterpret_cast<uint4*>(C + (size_t)m * p.ldc + n) = y;
+      } else {
+        *reinterpret_cast<uint4*>(C + (size_t)m * p.ldc + n) = u;
+      }
+    }
+  } else {
+    constexpr int CPR = BN / 4;  // 4 fp32 per chunk
+#pragma unroll 4
+    for (int id = tid; id < BM * CPR; id += NT) {
+      const int r = id / CPR, cc = id - r * CPR;
+      const int m = m0 + r;
+      if (m >= p.M) break;
+      const float4 v = *reinterpret_cast<const float4*>(smem + r * LDC + cc * 16);
+      const int n = n0 + cc * 4;
+      if constexpr (EPI == EPI_F32) {
+        float* C = reinterpret_cast<float*>(p.C) + (size_t)blockIdx.z * p.slab_stride;
+        *reinterpret_cast<float4*>(C + (size_t)m * p.ldc + n) = v;
+      } else {
+        float v0 = v.x, v1 = v.y, v2 = v.z, v3 = v.w;
+        if constexpr (EPI == EPI_GELU_BWD) {
+          const uint2 u = *reinterpret_cast<const uint2*>(p.aux + (size_t)m * p.ldaux + n);
+          v0 *= gelu_erf_grad(lo_bf(u.x)); v1 *= gelu_erf_grad(hi_bf(u.x));
+          v2 *= gelu_erf_grad(lo_bf(u.y)); v3 *= gelu_erf_grad(hi_bf(u.y));
+        } else {  // EPI_ADD
+          const uint2 r2 = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldres + n);
+          v0 += lo_bf(r2.x); v1 += hi_bf(r2.x); v2 += lo_bf(r2.y); v3 += hi_bf(r2.y);
+        }
+        bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+        *reinterpret_cast<uint2*>(C + (size_t)m * p.ldc + n) = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+      }
+    }
   }
 }
 
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM = 2, int WN = 2>
-__global__ __launch_bounds__(64 * WM * WN, 8 / (WM * WN) > 0 ? 8 / (WM * WN) : 1) void gemm_kernel(GemmParams p) {
-  constexpr int NW = WM * WN;
-  using OA = Operand<BM, AK, BKT, NW>;
-  using OB = Operand<BN, BKM, BKT, NW>;
+template <int N>
+DEV void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Counted wait for "all but the youngest n*L LDS-DMA ops" (n = tiles still allowed in flight).
+template <int L, int MAXN>
+DEV void wait_tiles(int n) {
+  if constexpr (MAXN >= 2) { if (n >= 2) { wait_vm<2 * L>(); return; } }
+  if constexpr (MAXN >= 1) { if (n >= 1) { wait_vm<L>(); return; } }
+  wait_vm<0>();
+}
+
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+struct GemmCfg {
+  static constexpr int NW = WM * WN;
+  using OA = Operand<BM, AK, NW>;
+  using OB = Operand<BN, BKM, NW>;
+  static constexpr int BUF = OA::BYTES + OB::BYTES;
+  static constexpr int EPI_BYTES = EpiTraits<EPI, BM, BN>::BYTES;
+  static constexpr int SMEM = S * BUF > EPI_BYTES ? S * BUF : EPI_BYTES;
+  static constexpr bool VALID = SMEM <= LDS_MAX && (BKM || BN % 64 == 0) && (AK || BM % 64 == 0) &&
+                                (BM / WM) % 16 == 0 && (BN / WN) % 16 == 0 &&
+                                OA::PER_WAVE * NW * 1024 == OA::BYTES && OB::PER_WAVE * NW * 1024 == OB::BYTES;
+};
+
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p) {
+  using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
+  using OA = typename G::OA;
+  using OB = typename G::OB;
+  constexpr int NW = G::NW;
   constexpr int TM = BM / WM, TN = BN / WN;  // per-wave tile
   constexpr int MI = TM / 16, NI = TN / 16;  // 16x16 sub-tiles per wave
-  constexpr int BUF = OA::BYTES + OB::BYTES;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+  constexpr int BUF = G::BUF;
+  constexpr int L = OA::PER_WAVE + OB::PER_WAVE;  // DMA ops per wave per K tile
+  static_assert(S >= 2 && S <= 4, "ring depth");
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / WN, wc = wid % WN;
 
-  // Tile walk: M-major inside each N column panel so consecutive logical tiles
-  // share the B (weight) panel; XCD remap keeps those on one L2.
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = p.N / BN;
-  const int nwg = tiles_m * tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   int tm, tn;
   tile_coords(bid, tiles_m, tiles_n, p.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
@@ -210,153 +310,55 @@ __global__ __launch_bounds__(64 * WM * WN, 8 / (WM * WN) > 0 ? 8 / (WM * WN) : 1
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  OA::stage(p.A, p.lda, m0, kbeg, p.M, smem, wid, lane);
-  OB::stage(p.B, p.ldb, n0, kbeg, p.N, smem + OA::BYTES, wid, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * BUF;
-    if (kt + 1 < nk && !(p.diag & 1)) {
-      char* nxt = smem + ((kt + 1) & 1) * BUF;
-      OA::stage(p.A, p.lda, m0, kbeg + (kt + 1) * BKT, p.M, nxt, wid, lane);
-      OB::stage(p.B, p.ldb, n0, kbeg + (kt + 1) * BKT, p.N, nxt + OA::BYTES, wid, lane);
-    }
+  auto issue = [&](int t) {
+    char* b = smem + (t % S) * BUF;
+    OA::stage(p.A, p.lda, m0, kbeg + t * BKT, p.M, b, wid, lane);
+    OB::stage(p.B, p.ldb, n0, kbeg + t * BKT, p.N, b + OA::BYTES, wid, lane);
+  };
+  bf16x8 a0[MI], b0[NI], a1[MI], b1[NI];
+  auto read_frags = [&](const char* cur) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[MI], bfr[NI];
+    for (int i = 0; i < MI; ++i) a0[i] = OA::frag(cur, wr * TM + i * 16, 0, lane);
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = OA::frag(cur, wr * TM + i * 16, s, lane);
+    for (int j = 0; j < NI; ++j) b0[j] = OB::frag(cur + OA::BYTES, wc * TN + j * 16, 0, lane);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) bfr[j] = OB::frag(cur + OA::BYTES, wc * TN + j * 16, s, lane);
-      if (p.diag & 2) {
+    for (int i = 0; i < MI; ++i) a1[i] = OA::frag(cur, wr * TM + i * 16, 1, lane);
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NI; ++j) acc[i][j][0] += (float)(af[i][0] ^ bfr[j][1]);
-        continue;
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  if (p.diag & 4) {
-    float t = 0.f;
+    for (int j = 0; j < NI; ++j) b1[j] = OB::frag(cur + OA::BYTES, wc * TN + j * 16, 1, lane);
+  };
+  auto mfmas = [&]() {
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NI; ++j) t += acc[i][j][0] + acc[i][j][3];
-    if (t != 1234.5f) return;
-  }
-
-  // ---------------------------------------------------------------- epilogue
-  // lane owns C[m][n..n+3] of every sub-tile (operand-swapped MFMA).
+      for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b0[j], a0[i], acc[i][j]);
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int m = m0 + wr * TM + i * 16 + (lane & 15);
-    if (m >= p.M) continue;
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int n = n0 + wc * TN + j * 16 + 4 * (lane >> 4);
-      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-      epilogue<EPI>(p, m, n, v0, v1, v2, v3);
-    }
-  }
-}
-
-template <int N>
-DEV void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// Counted wait for "all but the youngest n*L LDS-DMA ops" (n = stages still allowed in flight).
-template <int L, int MAXN>
-DEV void wait_stages(int n) {
-  if constexpr (MAXN >= 3) { if (n >= 3) { wait_vm<3 * L>(); return; } }
-  if constexpr (MAXN >= 2) { if (n >= 2) { wait_vm<2 * L>(); return; } }
-  if constexpr (MAXN >= 1) { if (n >= 1) { wait_vm<L>(); return; } }
-  wait_vm<0>();
-}
-
-// Multi-stage ring variant: STAGES LDS buffers, tile t+STAGES-1's DMA issued while
-// tile t is consumed; a counted vmcnt (never 0 in steady state) + ONE raw s_barrier
-// per K tile keeps STAGES-2 tiles in flight across the barrier
-// (cdna_hip_programming.md "Pipelining across barriers").
-template <int BM, int BN, int BK, int STAGES, bool AK, bool BKM, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_pipe_kernel(GemmParams p) {
-  using OA = Operand<BM, AK, BK>;
-  using OB = Operand<BN, BKM, BK>;
-  constexpr int MI = BM / 32, NI = BN / 32;
-  constexpr int BUF = OA::BYTES + OB::BYTES;
-  constexpr int L = OA::PER_WAVE + OB::PER_WAVE;  // DMA ops per wave per stage
-  constexpr int SUB = BK / 32;                     // 32-deep MFMA steps per tile
-  __shared__ __attribute__((aligned(1024))) char smem[STAGES * BUF];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = p.N / BN;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  int tm, tn;
-  tile_coords(bid, tiles_m, tiles_n, p.group_m, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.z * p.k_split;
-  const int nk = p.k_split / BK;
-
-  f32x4 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto issue = [&](int t) {
-    char* b = smem + (t % STAGES) * BUF;
-    OA::stage(p.A, p.lda, m0, kbeg + t * BK, p.M, b, wid, lane);
-    OB::stage(p.B, p.ldb, n0, kbeg + t * BK, p.N, b + OA::BYTES, wid, lane);
+      for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b1[j], a1[i], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
   };
-#pragma unroll
-  for (int t = 0; t < STAGES - 1; ++t)
-    if (t < nk) issue(t);
 
-  for (int t = 0; t < nk; ++t) {
-    const int ahead = min(STAGES - 2, nk - 1 - t);  // younger stages allowed in flight
-    wait_stages<L, STAGES - 2>(ahead);
-    __builtin_amdgcn_s_barrier();
-    if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
-    const char* cur = smem + (t % STAGES) * BUF;
+  {
 #pragma unroll
-    for (int s = 0; s < SUB; ++s) {
-      bf16x8 af[MI], bfr[NI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = OA::frag(cur, wr * (BM / 2) + i * 16, s, lane);
-#pragma unroll
-      for (int j = 0; j < NI; ++j) bfr[j] = OB::frag(cur + OA::BYTES, wc * (BN / 2) + j * 16, s, lane);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
+    for (int t = 0; t < S - 1; ++t)
+      if (t < nk) issue(t);
+
+    for (int kt = 0; kt < nk; ++kt) {
+      // this wave's DMA for tile kt has landed (younger tiles stay in flight) ...
+      wait_tiles<L, S - 2>(min(S - 2, nk - 1 - kt));
+      // ... and everyone's has; everyone is also done reading tile kt-1's slot.
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + S - 1 < nk && !(p.diag & 1)) issue(kt + S - 1);
+      read_frags(smem + (kt % S) * BUF);
+      mfmas();
     }
   }
-
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int m = m0 + wr * (BM / 2) + i * 16 + (lane & 15);
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int n = n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4);
-      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-      epilogue<EPI>(p, m, n, v0, v1, v2, v3);
-    }
-  }
+  // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
+  // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
+  __syncthreads();
+  staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid);
 }
 
 // out[i] = (accumulate ? out[i] : 0) + sum_z slab[z][i]   (deterministic split-K reduce)
@@ -373,98 +375,112 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-// Kernel variants (FD_GEMM_VARIANT env for A/B benchmarking; default picks per kind):
-//   0: 2-stage ring, BK=64        1: 4-stage ring, BK=32
-//   2: 3-stage ring, BK=64        3: 3-stage ring, BK=32
-int variant_override() {
-  static int v = [] {
-    const char* e = getenv("FD_GEMM_VARIANT");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
-}
+// ---------------------------------------------------------------- configurations
+// id: BM x BN, waves WM x WN, ring depth S   (LDS = max(S*(BM+BN)*128 B, epilogue))
+//  0: 128 x  64, 2x2, S3      1: 128 x 128, 2x2, S2      2: 128 x  96, 2x2, S2 (K-major B)
+//  3: 256 x 192, 4x2, S2      4: 256 x 128, 4x2, S3      5:  64 x 192, 1x4, S3
+//  6: 128 x 192, 2x4, S2      7: 256 x  96, 4x1, S3 (K-major B)
+//  8: 128 x  64, 2x2, S2      9: 128 x  96, 2x2, S3 (K-major B)
+// 10: 128 x 128, 2x2, S3     11: 256 x 256, 2x4, S2     12: 256 x 128, 4x2, S2
+// (A ping-pong variant -- the two 4-wave halves of an 8-wave block staggered by
+// one barrier phase so one half's LDS reads overlap the other's MFMAs -- was
+// correct but measured 1.5-3x slower on these shapes; not kept.)
+constexpr int NCFG = 13;
+struct CfgDesc { int bm, bn, wm, wn, s; };
+constexpr CfgDesc CFGS[NCFG] = {{128, 64, 2, 2, 3}, {128, 128, 2, 2, 2}, {128, 96, 2, 2, 2}, {256, 192, 4, 2, 2},
+                                {256, 128, 4, 2, 3}, {64, 192, 1, 4, 3}, {128, 192, 2, 4, 2}, {256, 96, 4, 1, 3},
+                                {128, 64, 2, 2, 2},  {128, 96, 2, 2, 3}, {128, 128, 2, 2, 3}, {256, 256, 2, 4, 2},
+                                {256, 128, 4, 2, 2}};
 
-template <int BM, int BN, bool AK, bool BKM, int EPI>
-void launch(const GemmParams& p, int splits, hipStream_t st, int variant) {
-  const dim3 grid(((p.M + BM - 1) / BM) * (p.N / BN), 1, splits);
-  switch (variant) {
-    case 1: hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, 32, 4, AK, BKM, EPI>), grid, dim3(256), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, 64, 3, AK, BKM, EPI>), grid, dim3(256), 0, st, p); break;
-    case 3: hipLaunchKernelGGL((gemm_pipe_kernel<BM, BN, 32, 3, AK, BKM, EPI>), grid, dim3(256), 0, st, p); break;
-    default: hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKM, EPI>), grid, dim3(256), 0, st, p); break;
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+bool launch_cfg(const GemmParams& p, int splits, hipStream_t st) {
+  using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
+  if constexpr (!G::VALID) {
+    return false;
+  } else {
+    if (p.N % BN != 0) return false;
+    const dim3 grid(((p.M + BM - 1) / BM) * (p.N / BN), 1, splits);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKM, EPI, WM, WN, S>), grid, dim3(64 * WM * WN), 0, st, p);
+    return true;
   }
-}
-
-// Pick BN in {128, 96, 64} maximising (wave-quantisation efficiency x tile efficiency)
-// on 256 CUs x 2 resident blocks.
-int pick_bn(int M, int N, bool allow96) {
-  const int cand[3] = {128, 96, 64};
-  const double tile_eff[3] = {1.0, 0.93, 0.84};
-  const int slots = 512;
-  int best = 64;
-  double best_s = -1;
-  for (int c = 0; c < 3; ++c) {
-    const int bn = cand[c];
-    if (N % bn != 0 || (bn == 96 && !allow96)) continue;
-    const long tiles = (long)((M + 127) / 128) * (N / bn);
-    const long rounds = (tiles + slots - 1) / slots;
-    const double q = (double)tiles / (double)(rounds * slots);
-    const double s = q * tile_eff[c];
-    if (s > best_s) { best_s = s; best = bn; }
-  }
-  return best;
-}
-
-// Tile configurations of the 2-stage kernel (FD_GEMM_TILE=<id> forces one):
-//   0: 128x128 (2x2 waves)  1: 128x96 (2x2, K-major B only)  2: 128x64 (2x2)
-//   3: 256x128 (4x2)        4: 256x192 (4x2, K-major B only) 5: 256x64 (4x2)
-int tile_override() {
-  static int v = [] {
-    const char* e = getenv("FD_GEMM_TILE");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
 }
 
 template <bool AK, bool BKM, int EPI>
-bool launch_tile(const GemmParams& p, int tile, int splits, hipStream_t st) {
-  auto grid = [&](int bm, int bn) { return dim3(((p.M + bm - 1) / bm) * (p.N / bn), 1, splits); };
-  switch (tile) {
-    case 0: if (p.N % 128) return false;
-      hipLaunchKernelGGL((gemm_kernel<128, 128, AK, BKM, EPI>), grid(128, 128), dim3(256), 0, st, p); return true;
-    case 1: if constexpr (BKM) { if (p.N % 96) return false;
-      hipLaunchKernelGGL((gemm_kernel<128, 96, AK, BKM, EPI>), grid(128, 96), dim3(256), 0, st, p); return true; }
-      return false;
-    case 2: if (p.N % 64) return false;
-      hipLaunchKernelGGL((gemm_kernel<128, 64, AK, BKM, EPI>), grid(128, 64), dim3(256), 0, st, p); return true;
-    case 3: if constexpr (AK) { if (p.N % 128) return false;
-      hipLaunchKernelGGL((gemm_kernel<256, 128, AK, BKM, EPI, 4, 2>), grid(256, 128), dim3(512), 0, st, p); return true; }
-      return false;
-    case 4: if constexpr (BKM && AK) { if (p.N % 192) return false;
-      hipLaunchKernelGGL((gemm_kernel<256, 192, AK, BKM, EPI, 4, 2>), grid(256, 192), dim3(512), 0, st, p); return true; }
-      return false;
-    case 5: if constexpr (AK) { if (p.N % 64) return false;
-      hipLaunchKernelGGL((gemm_kernel<256, 64, AK, BKM, EPI, 4, 2>), grid(256, 64), dim3(512), 0, st, p); return true; }
-      return false;
+bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st) {
+  switch (id) {
+    case 0: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 3>(p, splits, st);
+    case 1: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 2>(p, splits, st);
+    case 2: return launch_cfg<128, 96, AK, BKM, EPI, 2, 2, 2>(p, splits, st);
+    case 3: return launch_cfg<256, 192, AK, BKM, EPI, 4, 2, 2>(p, splits, st);
+    case 4: return launch_cfg<256, 128, AK, BKM, EPI, 4, 2, 3>(p, splits, st);
+    case 5: return launch_cfg<64, 192, AK, BKM, EPI, 1, 4, 3>(p, splits, st);
+    case 6: return launch_cfg<128, 192, AK, BKM, EPI, 2, 4, 2>(p, splits, st);
+    case 7: return launch_cfg<256, 96, AK, BKM, EPI, 4, 1, 3>(p, splits, st);
+    case 8: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 2>(p, splits, st);
+    case 9: return launch_cfg<128, 96, AK, BKM, EPI, 2, 2, 3>(p, splits, st);
+    case 10: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 3>(p, splits, st);
+    case 11: return launch_cfg<256, 256, AK, BKM, EPI, 2, 4, 2>(p, splits, st);
+    case 12: return launch_cfg<256, 128, AK, BKM, EPI, 4, 2, 2>(p, splits, st);
   }
   return false;
 }
 
-// BN = 96 only exists for the 2-stage BK=64 kernel (96-row tiles do not split into
-// whole 1 KiB DMA pieces per wave at BK=32).
-template <bool AK, bool BKM, int EPI>
-void dispatch(const GemmParams& p, int bn, int splits, hipStream_t st, int variant) {
-  const int to = tile_override();
-  if (to >= 0 && variant == 0 && launch_tile<AK, BKM, EPI>(p, to, splits, st)) return;
-  if constexpr (BKM) {
-    if (bn == 96 && variant == 0) {
-      const dim3 grid(((p.M + 127) / 128) * (p.N / 96), 1, splits);
-      hipLaunchKernelGGL((gemm_kernel<128, 96, AK, BKM, EPI>), grid, dim3(256), 0, st, p);
-      return;
-    }
+// Tuning overrides: per GEMM kind a forced config id / split count (-1 = auto),
+// set from FD_GEMM_CFG_{NT,NN,TN} / FD_GEMM_SPLITS or at run time (fd_gemm_set_cfg).
+int g_cfg_override[3] = {-2, -2, -2};
+int g_splits_override = -2;
+
+int cfg_override(int kind) {
+  if (g_cfg_override[kind] == -2) {
+    const char* names[3] = {"FD_GEMM_CFG_NT", "FD_GEMM_CFG_NN", "FD_GEMM_CFG_TN"};
+    const char* e = getenv(names[kind]);
+    g_cfg_override[kind] = e ? atoi(e) : -1;
   }
-  if (bn == 128) launch<128, 128, AK, BKM, EPI>(p, splits, st, variant);
-  else launch<128, 64, AK, BKM, EPI>(p, splits, st, variant);
+  return g_cfg_override[kind];
+}
+int splits_override() {
+  if (g_splits_override == -2) {
+    const char* e = getenv("FD_GEMM_SPLITS");
+    g_splits_override = e ? atoi(e) : -1;
+  }
+  return g_splits_override;
+}
+
+long long tiles_of(int id, int M, int N) {
+  const CfgDesc& c = CFGS[id];
+  if (N % c.bn) return 0;
+  return (long long)((M + c.bm - 1) / c.bm) * (N / c.bn);
+}
+
+// Default configuration per kind/shape, measured on MI355X at the DistilBERT
+// shapes (M = 4096 tokens; scripts/gemm_sweep.py -> profiles/r1_gemm_cfg_sweep.txt).
+// Occupancy wins over ring depth: the 2-3 blocks/CU configs (S2) beat the
+// 1 block/CU S3 rings at every shape; 8-wave 256x192 / 128x192 only where they
+// make one full round of tiles.
+int pick_cfg(int kind, int M, int N, int K) {
+  if (kind == 0) {  // NT forward
+    if (N % 192 == 0 && N >= 3072 && M >= 2048) return 3;
+    if (N % 192 == 0 && N >= 1536 && M >= 2048) return 6;
+    return K >= 2048 ? 0 : 8;
+  }
+  if (kind == 1) {  // NN dX
+    if (N % 192 == 0 && N >= 3072 && M >= 2048) return 3;
+    return 8;
+  }
+  return (N % 128 == 0 && M > 1024 && M < 3072 && N < 3072) ? 1 : 8;  // TN dW
+}
+
+template <bool AK, bool BKM>
+bool launch_epi(int epi, const GemmParams& p, int id, int splits, hipStream_t st) {
+  switch (epi) {
+    case EPI_BF16: return launch_id<AK, BKM, EPI_BF16>(p, id, splits, st);
+    case EPI_BIAS: if constexpr (AK && BKM) return launch_id<AK, BKM, EPI_BIAS>(p, id, splits, st); break;
+    case EPI_BIAS_GELU: if constexpr (AK && BKM) return launch_id<AK, BKM, EPI_BIAS_GELU>(p, id, splits, st); break;
+    case EPI_GELU_BWD: if constexpr (AK && !BKM) return launch_id<AK, BKM, EPI_GELU_BWD>(p, id, splits, st); break;
+    case EPI_ADD: if constexpr (AK && !BKM) return launch_id<AK, BKM, EPI_ADD>(p, id, splits, st); break;
+    case EPI_F32: if constexpr (!AK && !BKM) return launch_id<AK, BKM, EPI_F32>(p, id, splits, st); break;
+  }
+  return false;
 }
 
 }  // namespace
@@ -472,12 +488,20 @@ void dispatch(const GemmParams& p, int bn, int splits, hipStream_t st, int varia
 // ---------------------------------------------------------------- C ABI
 extern "C" {
 
+// Force a configuration id / split count for a GEMM kind (tuning; -1 = auto).
+int fd_gemm_set_cfg(int kind, int cfg, int splits) {
+  if (kind < 0 || kind > 2 || cfg < -1 || cfg >= NCFG) return 1;
+  g_cfg_override[kind] = cfg;
+  if (kind == 2) g_splits_override = splits;
+  return 0;
+}
+
 // kind: 0 = NT (y = x W^T), 1 = NN (dx = dy W), 2 = TN (dW = dy^T x, fp32 out)
 // Returns 0 on success, nonzero on unsupported shape.
 int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
             const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
             long long workspace_elems, int accumulate, hipStream_t st) {
-  if (K % BKT != 0 || N % 64 != 0 || M <= 0) return 1;
+  if (K % BKT != 0 || N % 64 != 0 || M <= 0 || kind < 0 || kind > 2) return 1;
   GemmParams p{};
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.C = C;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
@@ -487,80 +511,55 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
     static const int diag = [] { const char* e = getenv("FD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
     p.diag = diag;
   }
-  // Group height: A-panels of gm x 128 rows x K (bf16) should take ~half of a 4 MiB L2.
+  int id = cfg_override(kind);
+  if (id < 0) id = pick_cfg(kind, M, N, K);
+  // Group height: A-panels of gm x BM rows x K (bf16) should take ~half of a 4 MiB L2.
   {
-    const long long panel = 128ll * K * 2;
+    const long long panel = (long long)CFGS[id].bm * K * 2;
     int gm = (int)std::max(1ll, std::min(16ll, (2ll << 20) / panel));
     const char* e = getenv("FD_GEMM_GROUP_M");
     if (e) gm = atoi(e);
-    p.group_m = gm;
+    p.group_m = std::max(1, gm);
   }
-  const int ov = variant_override();
   if (kind == 0) {
-    const int var = ov >= 0 ? ov : 0;
-    // Measured on MI355X (scripts/gemm_bench.py, FD_GEMM_TILE sweep): 128x64 tiles win
-    // for the DistilBERT forward shapes except the wide FFN1 (N = 3072), where the
-    // 8-wave 256x192 tile does (one round of 256 tiles at M = 4096).
-    if (var == 0 && tile_override() < 0) {
-      const int tile = (N % 192 == 0 && N >= 3072 && M >= 2048) ? 4 : 2;
-      bool ok = false;
-      switch (epi) {
-        case EPI_BIAS: ok = launch_tile<true, true, EPI_BIAS>(p, tile, 1, st); break;
-        case EPI_BIAS_GELU: ok = launch_tile<true, true, EPI_BIAS_GELU>(p, tile, 1, st); break;
-        case EPI_BF16: ok = launch_tile<true, true, EPI_BF16>(p, tile, 1, st); break;
-        default: return 2;
-      }
-      if (ok) return 0;
-    }
-    const int bn = pick_bn(M, N, var == 0);
-    switch (epi) {
-      case EPI_BIAS: dispatch<true, true, EPI_BIAS>(p, bn, 1, st, var); break;
-      case EPI_BIAS_GELU: dispatch<true, true, EPI_BIAS_GELU>(p, bn, 1, st, var); break;
-      case EPI_BF16: dispatch<true, true, EPI_BF16>(p, bn, 1, st, var); break;
-      default: return 2;
-    }
-    return 0;
+    if (epi != EPI_BF16 && epi != EPI_BIAS && epi != EPI_BIAS_GELU) return 2;
+    if (launch_epi<true, true>(epi, p, id, 1, st)) return 0;
+    return launch_epi<true, true>(epi, p, 0, 1, st) ? 0 : 2;  // 128x64 fits any N % 64 == 0
   }
   if (kind == 1) {
-    const int var = ov >= 0 ? ov : 0;
-    const int bn = pick_bn(M, N, false);
-    switch (epi) {
-      case EPI_BF16: dispatch<true, false, EPI_BF16>(p, bn, 1, st, var); break;
-      case EPI_GELU_BWD: dispatch<true, false, EPI_GELU_BWD>(p, bn, 1, st, var); break;
-      case EPI_ADD: dispatch<true, false, EPI_ADD>(p, bn, 1, st, var); break;
-      default: return 2;
-    }
-    return 0;
+    if (epi != EPI_BF16 && epi != EPI_GELU_BWD && epi != EPI_ADD) return 2;
+    if (launch_epi<true, false>(epi, p, id, 1, st)) return 0;
+    return launch_epi<true, false>(epi, p, 0, 1, st) ? 0 : 2;
   }
-  if (kind == 2) {
-    // dW[M=out][N=in] fp32.  Split K (the token dim) until the grid covers the
-    // chip; slabs go to `workspace` and are reduced deterministically.
-    if (M % 128 != 0) return 3;
-    const int var = ov >= 0 ? ov : 0;
-    // Measured: 128x64 for dW of out_lin / lin1 / lin2, 128x128 for the fused QKV dW.
-    const int bn = (N % 128 == 0 && M > 1024 && M < 3072 && N < 3072) ? 128 : 64;
-    const int tiles = (M / 128) * (N / bn);
-    int splits = 1;
-    while (tiles * splits < 384 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 512) splits *= 2;
-    const long long slab = (long long)M * N;
-    if (splits > 1 && workspace_elems < slab * splits) splits = 1;
-    p.k_split = K / splits;
-    float* out = (float*)C;
-    if (splits == 1 && !accumulate) {
-      p.slab_stride = 0;
-      dispatch<false, false, EPI_F32>(p, bn, 1, st, var);
-      return 0;
-    }
-    if (ldc != N) return 4;
-    p.C = workspace; p.ldc = N; p.slab_stride = slab;
-    dispatch<false, false, EPI_F32>(p, bn, splits, st, var);
-    const long long n4 = slab / 4;
-    const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, workspace, out, n4, slab, splits,
-                       accumulate);
-    return 0;
+  // kind 2: dW[M=out][N=in] fp32.  Split K (the token dim) until the grid covers
+  // the chip; slabs go to `workspace` and are reduced deterministically.
+  if (M % 128 != 0) return 3;
+  if (N % CFGS[id].bn != 0 || M % CFGS[id].bm != 0) id = 8;
+  const long long tiles = tiles_of(id, M, N);
+  int splits = 1;
+  const int so = splits_override();
+  if (so > 0) {
+    splits = so;
+    if (K % (splits * BKT) != 0) return 6;
+  } else {
+    while (tiles * splits < 400 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 512) splits *= 2;
   }
-  return 5;
+  const long long slab = (long long)M * N;
+  if (splits > 1 && workspace_elems < slab * splits) splits = 1;
+  p.k_split = K / splits;
+  float* out = (float*)C;
+  if (splits == 1 && !accumulate) {
+    p.slab_stride = 0;
+    return launch_epi<false, false>(EPI_F32, p, id, 1, st) ? 0 : 7;
+  }
+  if (ldc != N) return 4;
+  p.C = workspace; p.ldc = N; p.slab_stride = slab;
+  if (!launch_epi<false, false>(EPI_F32, p, id, splits, st)) return 7;
+  const long long n4 = slab / 4;
+  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, workspace, out, n4, slab, splits,
+                     accumulate);
+  return 0;
 }
 
 }  // extern "C"

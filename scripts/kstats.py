@@ -1,8 +1,12 @@
 """Summarise a rocprofv3 kernel_stats.csv: top kernels, per-step ms."""
 import csv, sys
 path = sys.argv[1]
-steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
 rows = list(csv.DictReader(open(path)))
+arg = sys.argv[2] if len(sys.argv) > 2 else "1"
+if arg == "auto":  # one Adam launch per training step
+    steps = float(next(r['Calls'] for r in rows if 'adam_kernel' in r['Name']))
+else:
+    steps = float(arg)
 tot = sum(float(r['TotalDurationNs']) for r in rows)
 print(f"{'ms/step':>8} {'%':>6} {'calls':>6} {'avg_us':>8}  kernel")
 for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:int(sys.argv[3]) if len(sys.argv) > 3 else 30]:

@@ -49,6 +49,17 @@ def test_gemm_nt_gelu():
     assert rel_err(g, torch.nn.functional.gelu(u.float())) < 1e-2
 
 
+@pytest.mark.parametrize("M", [4096, 4000])
+def test_gemm_nt_gelu_wide_tile(M):
+    # N = 3072 at M >= 2048 takes the 8-wave 256x192 tile; M = 4000 leaves a partial row tile.
+    x, w = bf(M, 768, seed=21), bf(3072, 768, scale=0.05, seed=22)
+    b = torch.randn(3072, device=DEV) * 0.1
+    g, u = kn.linear_fwd(x, w, b, gelu=True)
+    uref = x.float() @ w.float().t() + b
+    assert rel_err(u, uref) < 1e-2
+    assert rel_err(g, torch.nn.functional.gelu(u.float())) < 1e-2
+
+
 def test_gemm_identity_asymmetric():
     # A = I with an asymmetric B catches a transposed C write (guide §3).
     x = torch.eye(128, dtype=torch.bfloat16, device=DEV)
@@ -64,15 +75,16 @@ def test_gemm_nn(M, N, K):
     assert rel_err(dx, dy.float() @ w.float()) < 1e-2
 
 
-def test_gemm_nn_gelu_bwd_and_add():
-    dy, w = bf(256, 768, seed=7), bf(768, 3072, scale=0.05, seed=8)
-    u = bf(256, 3072, seed=9)
+@pytest.mark.parametrize("M", [256, 4000])
+def test_gemm_nn_gelu_bwd_and_add(M):
+    dy, w = bf(M, 768, seed=7), bf(768, 3072, scale=0.05, seed=8)
+    u = bf(M, 3072, seed=9)
     x = torch.nn.functional.gelu(u.float()).requires_grad_(False)
     du = kn.linear_dx(dy, w, gelu_u=u)
     uu = u.float().requires_grad_(True)
     g = torch.autograd.grad(torch.nn.functional.gelu(uu), uu, dy.float() @ w.float())[0]
     assert rel_err(du, g) < 1e-2
-    res = bf(256, 3072, seed=10)
+    res = bf(M, 3072, seed=10)
     dx = kn.linear_dx(dy, w, res=res)
     assert rel_err(dx, dy.float() @ w.float() + res.float()) < 1e-2
 
