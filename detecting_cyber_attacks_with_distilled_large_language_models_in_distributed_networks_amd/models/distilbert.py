@@ -230,6 +230,8 @@ class DDoSClassifier(nn.Module):
         # HIP path: only the word-embedding rows present in the batch carry a gradient
         # (emb_now flags); ArenaAdam skips the rest exactly.  Set False for a dense grad.
         self.sparse_word_grad = True
+        # set by an overlapping optimizer (engine/optim.py): called per block during backward
+        self.layer_grads_hook = None
         self.torch_counter = 0
         self._grad_token = None
         self._synced_version = -1
@@ -267,6 +269,14 @@ class DDoSClassifier(nn.Module):
         if self.impl_request == "hip" and self.arena.device.type != "cuda":
             raise RuntimeError("impl='hip' needs the model on a GPU")
         return self.impl_request
+
+    def layer_span(self, i: int) -> Tuple[int, int]:
+        """(arena offset, length) of transformer block i's parameters (contiguous, 64-aligned)."""
+        pre = f"distilbert.transformer.layer.{i}."
+        offs = [(o, math.prod(sh)) for nm, (o, sh) in self.arena.offsets.items() if nm.startswith(pre)]
+        lo = min(o for o, _ in offs)
+        hi = max(o + n for o, n in offs)
+        return lo, (hi - lo + 63) // 64 * 64
 
     def word_embedding_span(self):
         """(arena offset, rows, row_len) of the word-embedding table."""
@@ -374,7 +384,8 @@ class DDoSClassifier(nn.Module):
         emb, layers, head = self._hip_handles()
         cfg = self.config
         rc = RunCtx(B=B, S=S, H=cfg.n_heads, kbias=K.mask_bias(mask), seed=self.rng, training=self.training,
-                    eps=cfg.layer_norm_eps, p_hidden=cfg.dropout, p_attn=cfg.attention_dropout, p_head=self.dropout.p)
+                    eps=cfg.layer_norm_eps, p_hidden=cfg.dropout, p_attn=cfg.attention_dropout, p_head=self.dropout.p,
+                    on_layer_grads=self.layer_grads_hook if torch.is_grad_enabled() else None)
         if self.training:
             K.step_inc(None, self.rng)
         token = self._grad_token if torch.is_grad_enabled() else None

@@ -15,7 +15,7 @@ Reference call stack mirrored: DistilBertModel.forward -> Embeddings ->
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Optional
+from typing import Callable, Optional
 
 import torch
 
@@ -35,6 +35,9 @@ class RunCtx:
     p_hidden: float = 0.1
     p_attn: float = 0.1
     p_head: float = 0.3
+    # called with the layer index once a block's parameter gradients are final
+    # (lets the optimizer update that block on a side stream during the rest of backward)
+    on_layer_grads: Optional[Callable[[int], None]] = None
 
 
 class GradSink:
@@ -79,6 +82,7 @@ class LayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, L, rc: RunCtx, idx: int):
+        ctx.idx = idx
         p_a = rc.p_attn if rc.training else 0.0
         p_h = rc.p_hidden if rc.training else 0.0
         attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
@@ -124,6 +128,8 @@ class LayerFn(torch.autograd.Function):
         for k in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_w", "ln1_b", "l1_w", "l1_b", "l2_b", "ln2_w", "ln2_b"):
             G[k].accumulate()
         del ctx.acts
+        if rc.on_layer_grads is not None:
+            rc.on_layer_grads(ctx.idx)
         return dx, None, None, None
 
 

@@ -3,8 +3,9 @@ import csv, sys
 path = sys.argv[1]
 rows = list(csv.DictReader(open(path)))
 arg = sys.argv[2] if len(sys.argv) > 2 else "1"
-if arg == "auto":  # one Adam launch per training step
-    steps = float(next(r['Calls'] for r in rows if 'adam_kernel' in r['Name']))
+if arg == "auto":
+    # step_kernel runs twice per training step (dropout seed + Adam step counter)
+    steps = float(next(r['Calls'] for r in rows if 'step_kernel' in r['Name'])) / 2
 else:
     steps = float(arg)
 tot = sum(float(r['TotalDurationNs']) for r in rows)

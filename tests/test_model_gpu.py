@@ -119,3 +119,28 @@ def test_plain_forward_logits_are_differentiable():
     crit(m(ids, mask), labels).backward()
     crit(r(ids, mask), labels).backward()
     assert rel(m.dense_grad("classifier.weight"), r.arena.gview("classifier.weight")) < 5e-2
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_overlapped_adam_matches_single_pass(graph):
+    """Per-block Adam on a side stream during backward == one Adam pass after backward (bitwise)."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.engine import (
+        GraphedTrainStep, make_step_fn)
+    cfg = DistilBertConfig(n_layers=3)
+    models, steps = [], []
+    for overlap in (True, False):
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=5)
+        m.train()
+        opt = ArenaAdam(m, lr=1e-3, overlap=overlap)
+        assert (m.layer_grads_hook is not None) == overlap
+        models.append(m)
+        steps.append(GraphedTrainStep(make_step_fn(m, opt), warmup=1, enabled=graph))
+    for it in range(4):
+        ids, mask, labels = _batch(8, 128, seed=it)
+        for st in steps:
+            st(ids, mask, labels)
+    torch.cuda.synchronize()
+    assert torch.equal(models[0].arena.master, models[1].arena.master)
+    assert torch.equal(models[0].arena.shadow, models[1].arena.shadow)
+    if graph:
+        assert all(st.graph is not None for st in steps)
