@@ -253,6 +253,24 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
   }
 }
 
+// Scheduling hints for one K tile: the first 32-deep fragment set's ds_reads,
+// then each of its MFMAs followed by RPM of the second set's ds_reads (their
+// latency hides under the MFMA pipe), then the second set's MFMAs.
+template <int N, int RPM>
+DEV void sched_interleave() {
+  if constexpr (N > 0) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, RPM, 0);  // DS read
+    sched_interleave<N - 1, RPM>();
+  }
+}
+template <int R, int M>
+DEV void sched_ktile() {
+  __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+  sched_interleave<M, (R + M - 1) / M>();
+  __builtin_amdgcn_sched_group_barrier(0x008, M, 0);
+}
+
 template <int N>
 DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -290,6 +308,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p) {
   constexpr int BUF = G::BUF;
   constexpr int L = OA::PER_WAVE + OB::PER_WAVE;  // DMA ops per wave per K tile
   static_assert(S >= 2 && S <= 4, "ring depth");
+#ifndef FD_GEMM_SCHED
+#define FD_GEMM_SCHED 1
+#endif
+  constexpr bool SCHED = FD_GEMM_SCHED;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -327,7 +349,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p) {
     for (int j = 0; j < NI; ++j) b1[j] = OB::frag(cur + OA::BYTES, wc * TN + j * 16, 1, lane);
   };
   auto mfmas = [&]() {
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!SCHED) __builtin_amdgcn_s_setprio(1);  // (s_setprio would split the scheduling region)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -336,7 +358,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p) {
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b1[j], a1[i], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!SCHED) __builtin_amdgcn_s_setprio(0);
   };
 
   {
@@ -353,6 +375,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p) {
       if (kt + S - 1 < nk && !(p.diag & 1)) issue(kt + S - 1);
       read_frags(smem + (kt % S) * BUF);
       mfmas();
+      if constexpr (SCHED) sched_ktile<MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2), MI * NI>();
     }
   }
   // every DMA has been waited for (the last iteration waits vmcnt(0)); after this

@@ -35,50 +35,92 @@ struct LnArgs {
   float* part;          // [gridDim.x][3][D]: dgamma, dbeta, dbias partials
 };
 
-template <int NC>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= a.T) return;
-  const int D = a.D;
-  const bool drop = a.thr != 0;
-  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
-  float z[NC][4];
-  float s = 0.f;
+// Half-wave row layout for D = 768: 32 lanes own a row, lane hl holds columns
+// 8*(hl + 32c) .. +7 for c = 0..2 (three 16-byte bf16x8 loads), so one wave
+// moves two rows per instruction and row statistics reduce in 5 xor-shuffles.
+constexpr int HL = 32, CH = 3;  // lanes per row, 8-wide chunks per lane (D = HL * CH * 8)
+
+DEV float half_sum(float v) {
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int col = 4 * (lane + 64 * c);
-    const size_t off = (size_t)row * D + col;
-    const uint2 xv = *reinterpret_cast<const uint2*>(a.x + off);
-    float v[4] = {lo_bf(xv.x), hi_bf(xv.x), lo_bf(xv.y), hi_bf(xv.y)};
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DEV void unpack8(const uint4& u, float (&f)[8]) {
+  f[0] = lo_bf(u.x); f[1] = hi_bf(u.x); f[2] = lo_bf(u.y); f[3] = hi_bf(u.y);
+  f[4] = lo_bf(u.z); f[5] = hi_bf(u.z); f[6] = lo_bf(u.w); f[7] = hi_bf(u.w);
+}
+DEV uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
+}
+
+// z = dropout(x) + r for one lane's 24 elements of `row`; keep bits recorded (bit 8c+e).
+DEV void ln_load_sum(const LnArgs& a, int row, int hl, bool drop, uint32_t seed, float (&z)[CH][8],
+                     uint32_t& keep) {
+  uint4 xv[CH], rv[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const size_t off = (size_t)row * a.D + 8 * (hl + HL * c);
+    xv[c] = *reinterpret_cast<const uint4*>(a.x + off);
+    if (a.r) rv[c] = *reinterpret_cast<const uint4*>(a.r + off);
+  }
+  keep = 0xffffffu;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const size_t off = (size_t)row * a.D + 8 * (hl + HL * c);
+    unpack8(xv[c], z[c]);
     if (drop) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = drop_keep(seed, (uint32_t)(off + e), a.thr) ? v[e] * a.dscale : 0.f;
+      for (int e = 0; e < 8; ++e) {
+        const bool k = drop_keep(seed, (uint32_t)(off + e), a.thr);
+        z[c][e] = k ? z[c][e] * a.dscale : 0.f;
+        if (!k) keep &= ~(1u << (8 * c + e));
+      }
     }
     if (a.r) {
-      const uint2 rv = *reinterpret_cast<const uint2*>(a.r + off);
-      v[0] += lo_bf(rv.x); v[1] += hi_bf(rv.x); v[2] += lo_bf(rv.y); v[3] += hi_bf(rv.y);
-    }
+      float rr[8];
+      unpack8(rv[c], rr);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { z[c][e] = v[e]; s += v[e]; }
+      for (int e = 0; e < 8; ++e) z[c][e] += rr[e];
+    }
   }
-  const float mean = wave_sum(s) / D;
+}
+
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
+  const int lane = threadIdx.x & 63, hl = lane & (HL - 1);
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (row >= a.T) return;  // whole half-waves exit together (T rows, 2 per wave)
+  const bool drop = a.thr != 0;
+  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
+  float z[CH][8];
+  uint32_t keep;
+  ln_load_sum(a, row, hl, drop, seed, z, keep);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += z[c][e];
+  const float mean = half_sum(s) / a.D;
   float q = 0.f;
 #pragma unroll
-  for (int c = 0; c < NC; ++c)
+  for (int c = 0; c < CH; ++c)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { const float d = z[c][e] - mean; q += d * d; }
-  const float rstd = rsqrtf(wave_sum(q) / D + a.eps);
+    for (int e = 0; e < 8; ++e) { const float d = z[c][e] - mean; q += d * d; }
+  const float rstd = rsqrtf(half_sum(q) / a.D + a.eps);
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int col = 4 * (lane + 64 * c);
-    const float4 g = *reinterpret_cast<const float4*>(a.gamma + col);
-    const float4 b = *reinterpret_cast<const float4*>(a.beta + col);
-    const float y0 = (z[c][0] - mean) * rstd * g.x + b.x, y1 = (z[c][1] - mean) * rstd * g.y + b.y;
-    const float y2 = (z[c][2] - mean) * rstd * g.z + b.z, y3 = (z[c][3] - mean) * rstd * g.w + b.w;
-    *reinterpret_cast<uint2*>(a.y + (size_t)row * D + col) = make_uint2(pack_bf2(y0, y1), pack_bf2(y2, y3));
+  for (int c = 0; c < CH; ++c) {
+    const int col = 8 * (hl + HL * c);
+    const float4 g0 = *reinterpret_cast<const float4*>(a.gamma + col);
+    const float4 g1 = *reinterpret_cast<const float4*>(a.gamma + col + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(a.beta + col);
+    const float4 b1 = *reinterpret_cast<const float4*>(a.beta + col + 4);
+    const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    float y[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[e] = (z[c][e] - mean) * rstd * g[e] + b[e];
+    *reinterpret_cast<uint4*>(a.y + (size_t)row * a.D + col) = pack8(y);
   }
-  if (lane == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
+  if (hl == 0) { a.mean[row] = mean; a.rstd[row] = rstd; }
 }
 
 // Block-level reduction of per-lane column partials (NC*4 columns per lane,
@@ -99,71 +141,89 @@ DEV void block_colsum(float (&acc)[NC][4], float* lds, float* out, int D) {
   __syncthreads();
 }
 
-template <int NC>
+// 16 rows per 512-thread block per iteration (two per wave); per-lane column
+// partials for dgamma / dbeta / producer-bias, folded across the two half-waves
+// and the 8 waves into part[blockIdx.x][3][D] (fixed order: deterministic).
 __global__ __launch_bounds__(512) void ln_bwd_kernel(LnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][D]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [8 waves][D]
+  const int lane = threadIdx.x & 63, hl = lane & (HL - 1), w = threadIdx.x >> 6;
   const int D = a.D;
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
-  float dg[NC][4] = {}, db[NC][4] = {}, dbias[NC][4] = {};
-  const int nw = blockDim.x >> 6;
-  for (int row = blockIdx.x * nw + w; row < a.T; row += gridDim.x * nw) {
+  float dg[CH][8] = {}, db[CH][8] = {}, dbias[CH][8] = {};
+  const int rows_per_iter = (blockDim.x >> 5);
+  for (int row = blockIdx.x * rows_per_iter + (threadIdx.x >> 5); row < a.T; row += gridDim.x * rows_per_iter) {
+    uint4 dv[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      dv[c] = *reinterpret_cast<const uint4*>(a.dy + (size_t)row * D + 8 * (hl + HL * c));
+    float xh[CH][8];
+    uint32_t keep;
+    ln_load_sum(a, row, hl, drop, seed, xh, keep);
     const float mean = a.mean[row], rstd = a.rstd[row];
-    float xh[NC][4], gd[NC][4], dyv[NC][4];
+    float dyv[CH][8], gd[CH][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int col = 4 * (lane + 64 * c);
-      const size_t off = (size_t)row * D + col;
-      const uint2 xv = *reinterpret_cast<const uint2*>(a.x + off);
-      float v[4] = {lo_bf(xv.x), hi_bf(xv.x), lo_bf(xv.y), hi_bf(xv.y)};
-      if (drop) {
+    for (int c = 0; c < CH; ++c) {
+      const int col = 8 * (hl + HL * c);
+      const float4 g0 = *reinterpret_cast<const float4*>(a.gamma + col);
+      const float4 g1 = *reinterpret_cast<const float4*>(a.gamma + col + 4);
+      const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      unpack8(dv[c], dyv[c]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = drop_keep(seed, (uint32_t)(off + e), a.thr) ? v[e] * a.dscale : 0.f;
-      }
-      if (a.r) {
-        const uint2 rv = *reinterpret_cast<const uint2*>(a.r + off);
-        v[0] += lo_bf(rv.x); v[1] += hi_bf(rv.x); v[2] += lo_bf(rv.y); v[3] += hi_bf(rv.y);
-      }
-      const uint2 dv = *reinterpret_cast<const uint2*>(a.dy + off);
-      const float d4[4] = {lo_bf(dv.x), hi_bf(dv.x), lo_bf(dv.y), hi_bf(dv.y)};
-      const float4 g = *reinterpret_cast<const float4*>(a.gamma + col);
-      const float g4[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        xh[c][e] = (v[e] - mean) * rstd;
-        dyv[c][e] = d4[e];
-        gd[c][e] = g4[e] * d4[e];
+      for (int e = 0; e < 8; ++e) {
+        xh[c][e] = (xh[c][e] - mean) * rstd;
+        gd[c][e] = g[e] * dyv[c][e];
         s1 += gd[c][e];
         s2 += gd[c][e] * xh[c][e];
       }
     }
-    s1 = wave_sum(s1) / D;
-    s2 = wave_sum(s2) / D;
+    s1 = half_sum(s1) / D;
+    s2 = half_sum(s2) / D;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int col = 4 * (lane + 64 * c);
-      const size_t off = (size_t)row * D + col;
-      float dz[4], dx[4];
+    for (int c = 0; c < CH; ++c) {
+      const size_t off = (size_t)row * D + 8 * (hl + HL * c);
+      float dz[8], dx[8];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < 8; ++e) {
         dz[e] = rstd * (gd[c][e] - s1 - xh[c][e] * s2);
-        dx[e] = dz[e];
-        if (drop) dx[e] = drop_keep(seed, (uint32_t)(off + e), a.thr) ? dz[e] * a.dscale : 0.f;
+        dx[e] = ((keep >> (8 * c + e)) & 1u) ? dz[e] * (drop ? a.dscale : 1.f) : 0.f;
         dg[c][e] += dyv[c][e] * xh[c][e];
         db[c][e] += dyv[c][e];
         dbias[c][e] += dx[e];
       }
-      *reinterpret_cast<uint2*>(a.dz + off) = make_uint2(pack_bf2(dz[0], dz[1]), pack_bf2(dz[2], dz[3]));
-      if (drop && a.dx)
-        *reinterpret_cast<uint2*>(a.dx + off) = make_uint2(pack_bf2(dx[0], dx[1]), pack_bf2(dx[2], dx[3]));
+      *reinterpret_cast<uint4*>(a.dz + off) = pack8(dz);
+      if (drop && a.dx) *reinterpret_cast<uint4*>(a.dx + off) = pack8(dx);
     }
   }
+  // fold the two half-waves (same columns, different rows), then the 8 waves
   float* out = a.part + (size_t)blockIdx.x * 3 * D;
-  block_colsum<NC>(dg, lds, out, D);
-  block_colsum<NC>(db, lds, out + D, D);
-  block_colsum<NC>(dbias, lds, out + 2 * D, D);
+  float (*accs[3])[8] = {dg, db, dbias};
+#pragma unroll
+  for (int which = 0; which < 3; ++which) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) accs[which][c][e] += __shfl_xor(accs[which][c][e], 32, 64);
+    if (lane < HL) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        float* dst = lds + w * D + 8 * (hl + HL * c);
+        *reinterpret_cast<float4*>(dst) =
+            make_float4(accs[which][c][0], accs[which][c][1], accs[which][c][2], accs[which][c][3]);
+        *reinterpret_cast<float4*>(dst + 4) =
+            make_float4(accs[which][c][4], accs[which][c][5], accs[which][c][6], accs[which][c][7]);
+      }
+    }
+    __syncthreads();
+    const int nw = blockDim.x >> 6;
+    for (int col = threadIdx.x; col < D; col += blockDim.x) {
+      float sum = 0.f;
+      for (int i = 0; i < nw; ++i) sum += lds[i * D + col];
+      out[which * D + col] = sum;
+    }
+    __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------------ embeddings
@@ -507,7 +567,7 @@ int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* bet
   a.x = (const bf16_t*)x; a.r = (const bf16_t*)r; a.gamma = gamma; a.beta = beta; a.y = (bf16_t*)y;
   a.mean = mean; a.rstd = rstd; a.T = T; a.D = D; a.eps = eps;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
-  hipLaunchKernelGGL(ln_fwd_kernel<3>, dim3((T + 3) / 4), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3((T + 7) / 8), dim3(256), 0, st, a);
   return 0;
 }
 
@@ -522,8 +582,8 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
   a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.r = (const bf16_t*)r; a.gamma = gamma;
   a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = (bf16_t*)dz; a.dx = (bf16_t*)dx; a.part = work;
   a.T = T; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
-  const int grid = std::min(LN_GRID, (T + 7) / 8);
-  hipLaunchKernelGGL(ln_bwd_kernel<3>, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
+  const int grid = std::min(LN_GRID, (T + 15) / 16);
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
                      st, a);
   hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 3), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, dbias, accumulate);
