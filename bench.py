@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--impl", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--layers", type=int, default=6)
+    ap.add_argument("--comm", default="torch", choices=["torch", "rccl"],
+                    help="FedAvg collective: torch.distributed (RCCL) or the framework's NativeComm (RCCL)")
     ap.add_argument("--teacher", action="store_true",
                     help="distillation step (BASELINE.json config 5): BERT-base teacher fwd + DistilBERT student")
     args = ap.parse_args()
@@ -64,11 +66,14 @@ def main():
 
     cfg = models.DistilBertConfig(n_layers=args.layers)
     model = models.DDoSClassifier(config=cfg, device=dev, impl=args.impl, seed=0)
-    fedavg.broadcast_model(model)
+    ncomm = None
+    if args.comm == "rccl" and dev.type == "cuda":
+        ncomm = import_module(f"{PKG}.parallel.rccl").NativeComm()
+    fedavg.broadcast_model(model, comm=ncomm)
     opt = engine.ArenaAdam(model, lr=2e-5)
     if args.teacher:
         teacher = models.BertTeacherClassifier(config=models.bert_base_config(), device=dev, impl=args.impl)
-        fedavg.broadcast_model(teacher)
+        fedavg.broadcast_model(teacher, comm=ncomm)
         teacher.eval()
         fn = engine.make_kd_step_fn(model, teacher, opt, 2.0, 0.5)
     else:
@@ -87,7 +92,7 @@ def main():
         b = next(it)
         step(b["input_ids"], b["attention_mask"], b["labels"])
     if args.gpus > 1 or di.distributed:
-        fedavg.fedavg_(model)
+        fedavg.fedavg_(model, comm=ncomm)
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     sync()
     comm.barrier()
@@ -98,7 +103,7 @@ def main():
         b = next(it)
         loss_acc += step(b["input_ids"], b["attention_mask"], b["labels"])
     if di.distributed:
-        fedavg.fedavg_(model)
+        fedavg.fedavg_(model, comm=ncomm)
     sync()
     comm.barrier()
     sync()
@@ -131,6 +136,7 @@ def main():
             "tokens_per_sec_total": round(per_client * n * B * S, 1),
             "vs_baseline_basis": "per-client batches/s / 2.5 (reference bs16 fp32 per-client rate)",
             "impl": args.impl,
+            "comm": args.comm,
             "hip_graph": step.graph is not None,
             "graph_error": step.failed,
             "mean_loss": round(loss, 5),

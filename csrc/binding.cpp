@@ -15,6 +15,15 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
             int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
             long long workspace_elems, int accumulate, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
+const char* fd_comm_last_error();
+int fd_comm_load(const char* path);
+int fd_comm_unique_id_bytes();
+int fd_comm_get_unique_id(void* out);
+int fd_comm_init(void** comm, int nranks, int rank, const void* id_bytes);
+int fd_comm_destroy(void* comm);
+int fd_comm_allreduce(void* comm, const void* send, void* recv, long long count, int dtype, int op, hipStream_t st);
+int fd_comm_broadcast(void* comm, void* buf, long long count, int dtype, int root, hipStream_t st);
+int fd_comm_allgather(void* comm, const void* send, void* recv, long long count, int dtype, hipStream_t st);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, hipStream_t st);
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx,
@@ -110,6 +119,61 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
                    (int)A.size(1), (int)B.size(1), (int)N, ptr<float>(bias), ptr<void>(aux), (int)N,
                    ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, stream()),
            "gemm");
+}
+
+// ---------------------------------------------------------------- native RCCL communicator
+int comm_dtype(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kDouble: return 2;
+    case at::kLong: return 3;
+    default: TORCH_CHECK(false, "comm: unsupported dtype ", t.scalar_type());
+  }
+  return 0;
+}
+void comm_check(int rc, const char* what) { TORCH_CHECK(rc == 0, what, " failed: ", fd_comm_last_error()); }
+
+void comm_load(const std::string& path) { comm_check(fd_comm_load(path.c_str()), "comm_load"); }
+
+at::Tensor comm_unique_id() {
+  at::Tensor id = at::empty({fd_comm_unique_id_bytes()}, at::TensorOptions().dtype(at::kByte));
+  comm_check(fd_comm_get_unique_id(id.data_ptr()), "ncclGetUniqueId");
+  return id;
+}
+int64_t comm_init(int64_t nranks, int64_t rank, const at::Tensor& id) {
+  TORCH_CHECK(!id.is_cuda() && id.scalar_type() == at::kByte && id.numel() == fd_comm_unique_id_bytes(),
+              "comm_init: id must be the CPU uint8 tensor from comm_unique_id()");
+  TORCH_CHECK(rank >= 0 && rank < nranks, "comm_init: bad rank");
+  void* c = nullptr;
+  comm_check(fd_comm_init(&c, (int)nranks, (int)rank, id.contiguous().data_ptr()), "ncclCommInitRank");
+  return reinterpret_cast<int64_t>(c);
+}
+void comm_destroy(int64_t h) { comm_check(fd_comm_destroy(reinterpret_cast<void*>(h)), "ncclCommDestroy"); }
+void comm_allreduce(int64_t h, const at::Tensor& t, int64_t op) {
+  TORCH_CHECK(h != 0, "comm_allreduce: communicator not initialised");
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "comm_allreduce: contiguous GPU tensor required");
+  TORCH_CHECK(op >= 0 && op <= 2, "comm_allreduce: op must be 0 (sum), 1 (avg) or 2 (max)");
+  comm_check(fd_comm_allreduce(reinterpret_cast<void*>(h), t.data_ptr(), t.data_ptr(), t.numel(), comm_dtype(t),
+                               (int)op, stream()),
+             "ncclAllReduce");
+}
+void comm_broadcast(int64_t h, const at::Tensor& t, int64_t root) {
+  TORCH_CHECK(h != 0, "comm_broadcast: communicator not initialised");
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "comm_broadcast: contiguous GPU tensor required");
+  comm_check(fd_comm_broadcast(reinterpret_cast<void*>(h), t.data_ptr(), t.numel(), comm_dtype(t), (int)root,
+                               stream()),
+             "ncclBroadcast");
+}
+void comm_allgather(int64_t h, const at::Tensor& send, const at::Tensor& recv) {
+  TORCH_CHECK(h != 0, "comm_allgather: communicator not initialised");
+  TORCH_CHECK(send.is_cuda() && recv.is_cuda() && send.is_contiguous() && recv.is_contiguous(),
+              "comm_allgather: contiguous GPU tensors required");
+  TORCH_CHECK(send.scalar_type() == recv.scalar_type() && recv.numel() % send.numel() == 0,
+              "comm_allgather: recv must hold nranks x send");
+  comm_check(fd_comm_allgather(reinterpret_cast<void*>(h), send.data_ptr(), recv.data_ptr(), send.numel(),
+                               comm_dtype(send), stream()),
+             "ncclAllGather");
 }
 
 // Tuning hook: force GEMM configuration `cfg` (-1 = measured default) for a kind.
@@ -405,6 +469,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the federated DistilBERT engine";
   m.def("gemm", &gemm);
   m.def("gemm_set_cfg", &gemm_set_cfg);
+  m.def("comm_load", &comm_load);
+  m.def("comm_unique_id", &comm_unique_id);
+  m.def("comm_init", &comm_init);
+  m.def("comm_destroy", &comm_destroy);
+  m.def("comm_allreduce", &comm_allreduce);
+  m.def("comm_broadcast", &comm_broadcast);
+  m.def("comm_allgather", &comm_allgather);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("mask_to_bias", &mask_to_bias);

@@ -1,7 +1,8 @@
 """In-tree native build: gfx950 HIP kernel library + torch binding, and the C++ text front-end.
 
 Outputs (git-ignored, but shipped to the GPU box with the repo snapshot):
-  ops/_hip_kernels<EXT_SUFFIX>      csrc/kernels/*.hip (hipcc --offload-arch=gfx950) + csrc/binding.cpp
+  ops/_hip_kernels<EXT_SUFFIX>      csrc/kernels/*.hip (hipcc --offload-arch=gfx950) + csrc/comm/*.cpp
+                                    (native RCCL communicator) + csrc/binding.cpp
   data/_text_native_impl<EXT_SUFFIX> csrc/text/text_native.cpp (g++, pybind11)
 
 Kernel objects compile in parallel and are rebuilt only when a source (or the
@@ -46,7 +47,7 @@ def _run(cmd, verbose=False):
 
 def build_text(verbose=False, force=False) -> str:
     src = os.path.join(CSRC, "text", "text_native.cpp")
-    if not force and not _newer(TEXT_OUT, [src]):
+    if not force and not _newer(TEXT_OUT, [src, os.path.join(CSRC, "text", "text_core.h")]):
         return TEXT_OUT
     import pybind11
     cmd = ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread",
@@ -83,6 +84,11 @@ def build_hip(verbose=False, force=False, jobs=None) -> str:
         if force or _newer(o, [s] + headers):
             jobs_list.append(([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                                "-munsafe-fp-atomics", "-I" + kdir, "-c", s, "-o", o], o))
+    for s in sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp"))):
+        o = os.path.join(BUILD, "comm_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(o, [s]):
+            jobs_list.append(([HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-c", s, "-o", o], o))
     inc, defs, libdir = _torch_flags()
     bo = os.path.join(BUILD, "binding.o")
     objs.append(bo)
@@ -96,6 +102,7 @@ def build_hip(verbose=False, force=False, jobs=None) -> str:
     if force or jobs_list or _newer(HIP_OUT, objs):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + [
             "-L" + libdir, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+            "-ldl",  # RCCL is bound at run time from torch's copy (csrc/comm/rccl_comm.cpp)
             "-Wl,-rpath," + libdir, "-o", HIP_OUT + ".tmp"]
         _run(cmd, verbose)
         os.replace(HIP_OUT + ".tmp", HIP_OUT)

@@ -49,6 +49,7 @@ class FedConfig:
     participation: float = 1.0              # fraction of clients aggregated per round
     timeout_s: float = 300.0                # server.py:10 / client1.py:22
     transport: str = "collective"           # "collective" (RCCL/gloo all-reduce) | "tcp" (reference protocol)
+    comm: str = "torch"                     # collective backend: "torch" (torch.distributed) | "rccl" (NativeComm)
     server_host: str = "localhost"          # client1.py:276,314
     port_receive: int = 12345               # server.py:11
     port_send: int = 12346                  # server.py:12

@@ -78,14 +78,19 @@ class FederatedClient:
         mc.dropout, mc.attention_dropout = cfg.hidden_dropout, cfg.attention_dropout
         self.model = DDoSClassifier(cfg.model_path, config=mc, device=dev, impl=cfg.impl, seed=0,
                                     head_dropout=cfg.head_dropout)
+        self.comm = None
+        if cfg.comm == "rccl" and dev.type == "cuda":
+            from ..parallel.rccl import NativeComm
+            self.comm = NativeComm()
+            log.info(f"native RCCL communicator: {self.comm.world_size} ranks")
         # Identical start for every client: rank 0's weights win.
-        broadcast_model(self.model)
+        broadcast_model(self.model, comm=self.comm)
         self.teacher = None
         if cfg.teacher:
             from ..models.bert import BertTeacherClassifier, bert_base_config
             self.teacher = BertTeacherClassifier(cfg.extra.get("teacher_path"), config=bert_base_config(),
                                                  device=dev, impl=cfg.impl)
-            broadcast_model(self.teacher)
+            broadcast_model(self.teacher, comm=self.comm)
         self.start_round = 0
         self.history: List[Dict] = []
         if cfg.resume:
@@ -139,7 +144,7 @@ class FederatedClient:
             if cfg.transport == "tcp":
                 total_w = self._tcp_exchange(contributes)
             else:
-                total_w = fedavg_(model, weight=weight, participate=contributes)
+                total_w = fedavg_(model, weight=weight, participate=contributes, comm=self.comm)
             if model.device.type == "cuda":
                 torch.cuda.synchronize()
             t_fed = time.perf_counter() - t0

@@ -33,20 +33,26 @@ def _dist_on() -> bool:
 
 
 @torch.no_grad()
-def broadcast_model(model, src: int = 0):
-    """Make every client start from rank ``src``'s weights (identical init)."""
+def broadcast_model(model, src: int = 0, comm=None):
+    """Make every client start from rank ``src``'s weights (identical init).
+
+    comm: optional ``parallel.rccl.NativeComm`` (framework-owned RCCL communicator)."""
     if _dist_on():
-        dist.broadcast(model.arena.master, src=src)
+        if comm is not None:
+            comm.broadcast_(model.arena.master, root=src)
+        else:
+            dist.broadcast(model.arena.master, src=src)
     model.sync_shadow(force=True)
 
 
 @torch.no_grad()
-def fedavg_(model, weight: float = 1.0, participate: bool = True) -> float:
+def fedavg_(model, weight: float = 1.0, participate: bool = True, comm=None) -> float:
     """In-place FedAvg of ``model`` across all ranks; returns the total weight.
 
     weight:      this client's aggregation weight (1 = unweighted, n_k = sample-weighted)
     participate: False -> this client's update is dropped this round (fault injection /
                  partial participation); it still receives the aggregate.
+    comm:        optional ``parallel.rccl.NativeComm``; default is the torch.distributed group.
     """
     A = model.arena
     w = float(weight) if participate else 0.0
@@ -57,7 +63,15 @@ def fedavg_(model, weight: float = 1.0, participate: bool = True) -> float:
         return w
     dev = A.master.device
     wt = torch.tensor([w], dtype=torch.float64, device=dev)
-    dist.all_reduce(wt, op=dist.ReduceOp.SUM)
+    use_native = comm is not None and A.master.is_cuda
+
+    def allreduce(t):
+        if use_native:
+            comm.all_reduce_(t, "sum")
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+
+    allreduce(wt)
     total = float(wt.item())
     if total <= 0:
         raise RuntimeError("FedAvg round with no participating clients")
@@ -65,7 +79,7 @@ def fedavg_(model, weight: float = 1.0, participate: bool = True) -> float:
         from ..ops import kernels as K
         if w != 1.0:
             K.scale_cast(A.master, None, w)          # pre-scale (0 drops the update)
-        dist.all_reduce(A.master, op=dist.ReduceOp.SUM)
+        allreduce(A.master)
         K.scale_cast(A.master, A.shadow, 1.0 / total)  # fused 1/W scale + bf16 shadow refresh
         model.mark_shadow_synced()
     else:

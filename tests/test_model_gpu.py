@@ -144,3 +144,25 @@ def test_overlapped_adam_matches_single_pass(graph):
     assert torch.equal(models[0].arena.shadow, models[1].arena.shadow)
     if graph:
         assert all(st.graph is not None for st in steps)
+
+
+def test_training_is_bitwise_deterministic():
+    """identical seeds + batches -> bitwise-identical weights and losses
+    (no float atomics on any reduction path: split-K slabs, column partials and the
+    embedding-gradient rank sort all reduce in a fixed order)."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.engine import (
+        GraphedTrainStep, make_step_fn)
+    runs = []
+    for _ in range(2):
+        m = DDoSClassifier(config=DistilBertConfig(n_layers=2), device="cuda", impl="hip", seed=9)
+        m.train()
+        st = GraphedTrainStep(make_step_fn(m, ArenaAdam(m, lr=1e-3)), warmup=1)
+        losses = []
+        for it in range(4):
+            ids, mask, labels = _batch(16, 128, seed=100 + it)
+            losses.append(st(ids, mask, labels).clone())
+        torch.cuda.synchronize()
+        runs.append((torch.stack(losses), m.arena.master.clone(), m.arena.grad.clone()))
+    assert torch.equal(runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert torch.equal(runs[0][2], runs[1][2])
