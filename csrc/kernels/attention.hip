@@ -22,7 +22,10 @@
 //    row reads (one XOR-swizzled [64][64] image per tile, conflict-free for
 //    both read kinds).
 //  * Dropout is a stateless hash of (seed, ((b*H+h)*S+q)*S+k): regenerated in
-//    the backward, never stored.  Backward is FA2-style and atomic-free:
+//    the backward, never stored.
+//  * Padding-aware: key tiles whose 64 keys are all masked are
+//    skipped in all three kernels (their probabilities are exactly 0), so a
+//    batch padded to S = 256 with ~100 real tokens does half the work.  Backward is FA2-style and atomic-free:
 //    kernel dq (query-owned) and kernel dkdv (key-owned) each recompute P.
 #include "common.h"
 
@@ -127,10 +130,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
 
   for (int k0 = 0; k0 < S; k0 += 64) {
-    __syncthreads();
+    // Padding-aware: a key tile whose 64 keys are all masked contributes exp(-inf) = 0
+    // to every row -- skip it (exact).  The barrier also retires the previous tile's reads.
+    const float kbv = a.kbias[tok0 + k0 + (tid & 63)];
+    if (!__syncthreads_or(kbv != -INFINITY)) continue;
     stage_tile(ks, a.qkv + (tok0 + k0) * ld3 + D + h * DH, ld3, tid);
     stage_tile(vs, a.qkv + (tok0 + k0) * ld3 + 2 * D + h * DH, ld3, tid);
-    if (tid < 64) kb[tid] = a.kbias[tok0 + k0 + tid];
+    if (tid < 64) kb[tid] = kbv;
     __syncthreads();
 
     f32x4 sc[4];
@@ -250,10 +256,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int k0 = 0; k0 < S; k0 += 64) {
-    __syncthreads();
+    const float kbv = a.kbias[tok0 + k0 + (tid & 63)];
+    if (!__syncthreads_or(kbv != -INFINITY)) continue;  // fully masked key tile: dS = 0 (exact skip)
     stage_tile(ks, a.qkv + (tok0 + k0) * ld3 + D + h * DH, ld3, tid);
     stage_tile(vs, a.qkv + (tok0 + k0) * ld3 + 2 * D + h * DH, ld3, tid);
-    if (tid < 64) kb[tid] = a.kbias[tok0 + k0 + tid];
+    if (tid < 64) kb[tid] = kbv;
     __syncthreads();
 
     f32x4 sc[4], dp[4];
@@ -315,6 +322,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
     vf[s] = load_frag_global(a.qkv + (tok0 + key) * ld3 + 2 * D + h * DH + 32 * s + 8 * g);
   }
   const float kbias = a.kbias[tok0 + key];
+  bf16_t* outk = a.dqkv + (tok0 + key) * ld3 + D + h * DH;
+  bf16_t* outv = a.dqkv + (tok0 + key) * ld3 + 2 * D + h * DH;
+  if (!__syncthreads_or(kbias != -INFINITY)) {
+    // every key of this tile is masked: P[:, key] = 0 -> dK = dV = 0 (exact skip)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      *reinterpret_cast<uint2*>(outk + 16 * dt + 4 * g) = make_uint2(0u, 0u);
+      *reinterpret_cast<uint2*>(outv + 16 * dt + 4 * g) = make_uint2(0u, 0u);
+    }
+    return;
+  }
   const size_t st0 = ((size_t)b * H + h) * S;
   const uint32_t headidx = (uint32_t)(b * H + h) * S;
 
@@ -371,8 +389,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
       }
     }
   }
-  bf16_t* outk = a.dqkv + (tok0 + key) * ld3 + D + h * DH;
-  bf16_t* outv = a.dqkv + (tok0 + key) * ld3 + 2 * D + h * DH;
   const float sc = a.scale;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {

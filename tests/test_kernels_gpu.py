@@ -115,6 +115,29 @@ def make_mask(B, S, seed=0):
     return m.to(DEV)
 
 
+def test_attention_skips_padded_key_tiles():
+    # rows 1 and 2 leave whole 64-key tiles fully masked (skipped by all three kernels)
+    B, S, H, p = 3, 256, 12, 0.1
+    lens = torch.tensor([256, 70, 130])
+    mask = (torch.arange(S)[None, :] < lens[:, None]).long().to(DEV)
+    qkv = bf(B * S, 3 * H * 64, seed=31)
+    kb = kn.mask_bias(mask)
+    ctx, lse = kn.attn_fwd(qkv, kb, B, S, H, seed_t(7), 24, p)
+    q = qkv.float().requires_grad_(True)
+    rctx, rlse = R.attention_ref(q, mask, B, S, H, p, 7, 24)
+    assert rel_err(ctx, rctx) < 2e-2
+    assert (lse - rlse).abs().max().item() < 1e-3
+    dctx = bf(B * S, H * 64, seed=32)
+    dqkv = kn.attn_bwd(qkv, kb, ctx, lse, dctx, B, S, H, seed_t(7), 24, p)
+    (g,) = torch.autograd.grad(rctx, q, dctx.float())
+    for part in range(3):
+        sl = slice(part * H * 64, (part + 1) * H * 64)
+        assert rel_err(dqkv[:, sl], g[:, sl]) < 3e-2, part
+    # masked keys get exactly zero dK / dV
+    dk = dqkv.view(B, S, 3, H * 64)[1, 128:, 1:]
+    assert torch.count_nonzero(dk) == 0
+
+
 @pytest.mark.parametrize("B,S,p", [(2, 128, 0.0), (3, 128, 0.1), (2, 256, 0.1), (1, 64, 0.0)])
 def test_attention_fwd(B, S, p):
     H = 12
