@@ -15,6 +15,8 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
             int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
             long long workspace_elems, int accumulate, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
+int fd_transpose_batched(const void* const* srcs, void* const* dsts, const int* rows, const int* cols, int n,
+                         hipStream_t st);
 const char* fd_comm_last_error();
 int fd_comm_load(const char* path);
 int fd_comm_unique_id_bytes();
@@ -174,6 +176,28 @@ void comm_allgather(int64_t h, const at::Tensor& send, const at::Tensor& recv) {
   comm_check(fd_comm_allgather(reinterpret_cast<void*>(h), send.data_ptr(), recv.data_ptr(), send.numel(),
                                comm_dtype(send), stream()),
              "ncclAllGather");
+}
+
+// dsts[i] = srcs[i]^T for a batch of bf16 matrices (one launch).
+void transpose_batched(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
+  TORCH_CHECK(srcs.size() == dsts.size() && srcs.size() <= 32, "transpose_batched: 1..32 matching matrices");
+  std::vector<const void*> sp;
+  std::vector<void*> dp;
+  std::vector<int> rows, cols;
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    need(srcs[i], at::kBFloat16, "transpose src");
+    need(dsts[i], at::kBFloat16, "transpose dst");
+    TORCH_CHECK(srcs[i].dim() == 2 && dsts[i].dim() == 2 && dsts[i].size(0) == srcs[i].size(1) &&
+                    dsts[i].size(1) == srcs[i].size(0),
+                "transpose_batched: dst must be src^T shaped");
+    TORCH_CHECK(srcs[i].size(0) % 64 == 0 && srcs[i].size(1) % 64 == 0, "transpose_batched: dims % 64");
+    sp.push_back(srcs[i].data_ptr());
+    dp.push_back(dsts[i].data_ptr());
+    rows.push_back((int)srcs[i].size(0));
+    cols.push_back((int)srcs[i].size(1));
+  }
+  check_rc(fd_transpose_batched(sp.data(), dp.data(), rows.data(), cols.data(), (int)sp.size(), stream()),
+           "transpose_batched");
 }
 
 // Tuning hook: force GEMM configuration `cfg` (-1 = measured default) for a kind.
@@ -469,6 +493,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the federated DistilBERT engine";
   m.def("gemm", &gemm);
   m.def("gemm_set_cfg", &gemm_set_cfg);
+  m.def("transpose_batched", &transpose_batched);
   m.def("comm_load", &comm_load);
   m.def("comm_unique_id", &comm_unique_id);
   m.def("comm_init", &comm_init);

@@ -499,8 +499,8 @@ bool launch_epi(int epi, const GemmParams& p, int id, int splits, hipStream_t st
     case EPI_BF16: return launch_id<AK, BKM, EPI_BF16>(p, id, splits, st);
     case EPI_BIAS: if constexpr (AK && BKM) return launch_id<AK, BKM, EPI_BIAS>(p, id, splits, st); break;
     case EPI_BIAS_GELU: if constexpr (AK && BKM) return launch_id<AK, BKM, EPI_BIAS_GELU>(p, id, splits, st); break;
-    case EPI_GELU_BWD: if constexpr (AK && !BKM) return launch_id<AK, BKM, EPI_GELU_BWD>(p, id, splits, st); break;
-    case EPI_ADD: if constexpr (AK && !BKM) return launch_id<AK, BKM, EPI_ADD>(p, id, splits, st); break;
+    case EPI_GELU_BWD: if constexpr (AK) return launch_id<AK, BKM, EPI_GELU_BWD>(p, id, splits, st); break;
+    case EPI_ADD: if constexpr (AK) return launch_id<AK, BKM, EPI_ADD>(p, id, splits, st); break;
     case EPI_F32: if constexpr (!AK && !BKM) return launch_id<AK, BKM, EPI_F32>(p, id, splits, st); break;
   }
   return false;
@@ -544,8 +544,8 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
     if (e) gm = atoi(e);
     p.group_m = std::max(1, gm);
   }
-  if (kind == 0) {
-    if (epi != EPI_BF16 && epi != EPI_BIAS && epi != EPI_BIAS_GELU) return 2;
+  if (kind == 0) {  // also dX = dy (W^T)^T with a transposed weight copy: GELU' / residual epilogues
+    if (epi == EPI_F32) return 2;
     if (launch_epi<true, true>(epi, p, id, 1, st)) return 0;
     return launch_epi<true, true>(epi, p, 0, 1, st) ? 0 : 2;  // 128x64 fits any N % 64 == 0
   }

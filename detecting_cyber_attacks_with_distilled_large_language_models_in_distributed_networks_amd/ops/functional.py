@@ -111,19 +111,20 @@ class LayerFn(torch.autograd.Function):
         # output_layer_norm(dropout(lin2) + h): dz2 -> residual grad of h, df -> lin2 output grad
         dz2, df = K.ln_bwd(dy, f, h, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, rc.seed,
                            ffn_site, p_h, acc)
-        du = K.linear_dx(df, L["l2_w"], gelu_u=u)              # dg W2 * gelu'(u)
+        wt = L.get("wT") or {}
+        du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"))  # dg W2 * gelu'(u)
         K.linear_dw(df, g, G["l2_w"].buf, acc)
         K.colsum(du, G["l1_b"].buf, acc)
-        dh = K.linear_dx(du, L["l1_w"], res=dz2)               # du W1 + dz2
+        dh = K.linear_dx(du, L["l1_w"], res=dz2, wt=wt.get("l1_w"))    # du W1 + dz2
         K.linear_dw(du, h, G["l1_w"].buf, acc)
         # sa_layer_norm(out_lin + x)
         dz1, _ = K.ln_bwd(dh, ao, x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf, G["o_b"].buf, rc.seed, 0,
                           0.0, acc)
-        dcx = K.linear_dx(dz1, L["o_w"])
+        dcx = K.linear_dx(dz1, L["o_w"], wt=wt.get("o_w"))
         K.linear_dw(dz1, cx, G["o_w"].buf, acc)
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a)
         K.colsum(dqkv, G["qkv_b"].buf, acc)
-        dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1)
+        dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt.get("qkv_w"))
         K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
         for k in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_w", "ln1_b", "l1_w", "l1_b", "l2_b", "ln2_w", "ln2_b"):
             G[k].accumulate()

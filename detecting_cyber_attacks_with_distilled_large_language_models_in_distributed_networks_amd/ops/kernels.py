@@ -51,10 +51,17 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu
 
 
 def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] = None,
-              res: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dx = dy w  [* gelu'(u)]  [+ res]  (bf16)."""
+              res: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx = dy w  [* gelu'(u)]  [+ res]  (bf16).
+
+    With ``wt`` (= w^T, contiguous) the product runs as the K-major "NT" kernel
+    dx = dy (w^T)^T, whose operand staging is faster than the MN-major read of w."""
     M, N = dy.shape[0], w.shape[1]
     dx = torch.empty(M, N, dtype=torch.bfloat16, device=dy.device)
+    if wt is not None:
+        epi = EPI_GELU_BWD if gelu_u is not None else (EPI_ADD if res is not None else EPI_BF16)
+        ext().gemm(0, epi, dy, wt, dx, None, gelu_u, res, None, False)
+        return dx
     if gelu_u is not None:
         ext().gemm(1, EPI_GELU_BWD, dy, w, dx, None, gelu_u, None, None, False)
     elif res is not None:
@@ -70,6 +77,12 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: 
     ws = workspace(dy.device, "splitk", 8 * M * N)
     ext().gemm(2, 5, dy, x, out, None, None, None, ws, accumulate)
     return out
+
+
+def transpose_many(srcs, dsts):
+    """dsts[i] = srcs[i]^T (bf16, one launch for up to 32 matrices)."""
+    for i in range(0, len(srcs), 32):
+        ext().transpose_batched(list(srcs[i:i + 32]), list(dsts[i:i + 32]))
 
 
 def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:

@@ -318,3 +318,27 @@ def test_sparse_word_grad_and_adam_skip():
     kn.adam(pd_, gd, md, vd, None, st1, 1e-3, 0.9, 0.999, 1e-8, 0.0, False)
     kn.adam(ps_, gs, ms, vs, None, st2, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, ever, now, 64, V, D)
     assert torch.equal(pd_, ps_) and torch.equal(md, ms) and torch.equal(vd, vs)
+
+
+def test_transpose_batched():
+    srcs = [bf(2304, 768, seed=40), bf(768, 768, seed=41), bf(3072, 768, seed=42), bf(768, 3072, seed=43),
+            bf(64, 128, seed=44)]
+    dsts = [torch.empty(s.shape[1], s.shape[0], dtype=torch.bfloat16, device=DEV) for s in srcs]
+    kn.transpose_many(srcs, dsts)
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(d, s.t())
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 768, 3072), (4000, 3072, 768), (512, 768, 2304)])
+def test_linear_dx_transposed_weight(M, N, K):
+    # dx = dy W through the NT kernel on W^T, with every dX epilogue, == the NN kernel
+    dy, w = bf(M, K, seed=45), bf(K, N, scale=0.05, seed=46)
+    wt = w.t().contiguous()
+    u, res = bf(M, N, seed=47), bf(M, N, seed=48)
+    ref = dy.float() @ w.float()
+    assert rel_err(kn.linear_dx(dy, w, wt=wt), ref) < 1e-2
+    assert rel_err(kn.linear_dx(dy, w, res=res, wt=wt), ref + res.float()) < 1e-2
+    uu = u.float().requires_grad_(True)
+    g = torch.autograd.grad(torch.nn.functional.gelu(uu), uu, ref)[0]
+    assert rel_err(kn.linear_dx(dy, w, gelu_u=u, wt=wt), g) < 1e-2
+    assert torch.equal(kn.linear_dx(dy, w, res=res, wt=wt), kn.linear_dx(dy, w, res=res, wt=wt))
