@@ -44,7 +44,9 @@ class FedConfig:
     use_graph: bool = True                  # capture the train step in a HIP graph
     # --- federation (server.py:10-13) -------------------------------------------------
     rounds: int = 1
-    num_clients: Optional[int] = None       # None -> world size
+    num_clients: Optional[int] = None       # None -> world size / gpus_per_client
+    gpus_per_client: int = 1                # >1: each client is k data-parallel GPUs (parallel/dp.py)
+    dp_graph: bool = False                  # capture data-parallel steps (collectives) in the HIP graph
     weighted_fedavg: bool = False           # reference is unweighted (server.py:73-76)
     participation: float = 1.0              # fraction of clients aggregated per round
     timeout_s: float = 300.0                # server.py:10 / client1.py:22

@@ -52,7 +52,11 @@ class ArenaAdam:
         use = (self.overlap and dev.type == "cuda" and hasattr(self.model, "layer_span")
                and getattr(self.model, "impl", "hip") == "hip")
         self._side = torch.cuda.Stream(device=dev) if use else None
-        self.model.layer_grads_hook = self._on_layer_grads if use else None
+        if use:
+            prev = self.model.layer_grads_hook
+            if prev is not None and not isinstance(getattr(prev, "__self__", None), ArenaAdam):
+                raise RuntimeError("ArenaAdam(overlap=True) cannot share the backward hook (data-parallel GradSync?)")
+            self.model.layer_grads_hook = self._on_layer_grads
 
     def _begin(self):
         """Advance the device step counter once per step, before the first update launch."""

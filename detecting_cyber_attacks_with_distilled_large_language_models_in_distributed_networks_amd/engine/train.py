@@ -54,15 +54,23 @@ def make_kd_step_fn(student, teacher, optimizer, temperature: float = 2.0, alpha
 def train_model(model, train_loader, criterion=None, optimizer=None, num_epochs: int = 3, device=None,
                 log=None, use_graph: bool = True, max_steps: Optional[int] = None,
                 on_epoch: Optional[Callable] = None, teacher=None, kd_temperature: float = 2.0,
-                kd_alpha: float = 0.5) -> Dict:
+                kd_alpha: float = 0.5, grad_sync=None) -> Dict:
+    """grad_sync: a ``parallel.dp.GradSync`` when this client spans k GPUs (the loader
+    must then be the replica's ``DPShardLoader``); the step sums the replicas' gradients
+    before Adam and the epoch loss is the client-batch mean over all replicas."""
     from .optim import ArenaAdam
     optimizer = optimizer or ArenaAdam(model)
     if log:
         log.phase("Starting model training" + (" (distillation from teacher)" if teacher is not None else ""))
     model.train()
     if teacher is not None:
+        if grad_sync is not None:
+            raise NotImplementedError("distillation with data-parallel clients")
         teacher.eval()
         fn = make_kd_step_fn(model, teacher, optimizer, kd_temperature, kd_alpha)
+    elif grad_sync is not None:
+        from ..parallel.dp import make_dp_step_fn
+        fn = make_dp_step_fn(model, optimizer, grad_sync)
     else:
         fn = make_step_fn(model, optimizer, criterion)
     step = GraphedTrainStep(fn, enabled=use_graph and model.device.type == "cuda")
@@ -75,12 +83,17 @@ def train_model(model, train_loader, criterion=None, optimizer=None, num_epochs:
         nb = 0
         te = time.perf_counter()
         for batch in train_loader:
+            if grad_sync is not None:
+                grad_sync.set_loss_scale(batch.get("loss_scale", 1.0))
             loss = step(batch["input_ids"], batch["attention_mask"], batch["labels"])
             loss_sum += loss
             nb += 1
             steps += 1
             if max_steps is not None and steps >= max_steps:
                 break
+        if grad_sync is not None:  # replica shares of each client-batch mean -> the mean
+            import torch.distributed as dist
+            dist.all_reduce(loss_sum, group=grad_sync.group)
         avg = loss_sum.item() / max(nb, 1)  # the one sync per epoch
         dt = time.perf_counter() - te
         epoch_losses.append(avg)

@@ -9,8 +9,10 @@ Here the upload/average/download triple is ``fedavg_`` (one RCCL all-reduce of
 the fp32 arena, ``parallel/fedavg.py``) and the server's duties (writing
 ``ddos_distilbert_model.pth``, the cross-client report) fall to rank 0.  Extras
 over the reference: R rounds in-process, resume from the round sidecar,
-sample-weighted FedAvg, seeded partial participation, fault injection, and a
-cross-client JSON report gathered with an all-gather.
+sample-weighted FedAvg, seeded partial participation, fault injection, a
+cross-client JSON report gathered with an all-gather, and clients that span
+``gpus_per_client`` data-parallel GPUs (parallel/dp.py; replica 0 of each
+client does the client's file output).
 """
 from __future__ import annotations
 
@@ -26,6 +28,7 @@ from ..data import DeviceLoader, WordPieceTokenizer, build_client_data, generate
 from ..engine import ArenaAdam, evaluate_model, train_model
 from ..models import DDoSClassifier, DistilBertConfig
 from ..parallel import comm
+from ..parallel.dp import DPShardLoader, GradSync, dp_seed_offset, make_topology
 from ..parallel.fedavg import broadcast_model, fedavg_
 from ..utils import checkpoint as ck
 from ..utils import faults
@@ -43,12 +46,15 @@ class FederatedClient:
     def __init__(self, cfg: FedConfig, frame=None, model_config: Optional[DistilBertConfig] = None):
         self.cfg = cfg
         self.di = comm.init_distributed(timeout_s=cfg.timeout_s)
-        self.idx = self.di.rank                      # 0-based client index
+        self.topo = make_topology(cfg.gpus_per_client)
+        self.idx = self.topo.client_idx              # 0-based client index
         self.client_id = self.idx + 1                # reference naming: Client 1, Client 2, ...
-        self.num_clients = cfg.num_clients or self.di.world_size
+        self.num_clients = cfg.num_clients or self.topo.num_clients
+        self.writer = self.topo.dp_rank == 0         # replica 0 writes the client's files
         os.makedirs(cfg.out_dir, exist_ok=True)
-        self.log = TagLogger.for_client(self.client_id, enabled=cfg.verbose,
-                                        jsonl_path=os.path.join(cfg.out_dir, f"client{self.client_id}_log.jsonl"))
+        sfx = "" if self.writer else f"_replica{self.topo.dp_rank}"
+        self.log = TagLogger.for_client(self.client_id, enabled=cfg.verbose and self.writer,
+                                        jsonl_path=os.path.join(cfg.out_dir, f"client{self.client_id}{sfx}_log.jsonl"))
         self.timer = PhaseTimer()
         self.device = self.di.device
         self.frame = frame
@@ -72,6 +78,8 @@ class FederatedClient:
         dev = self.device
         self.train_loader = DeviceLoader(self.data.train, cfg.batch_size, shuffle=True, device=dev,
                                          seed=cfg.client_seed(self.idx))
+        if self.topo.dp:
+            self.train_loader = DPShardLoader(self.train_loader, self.topo.dp_rank, self.topo.gpus_per_client)
         self.val_loader = DeviceLoader(self.data.val, cfg.eval_batch_size, device=dev)
         self.test_loader = DeviceLoader(self.data.test, cfg.eval_batch_size, device=dev)
         mc = self.model_config
@@ -85,6 +93,12 @@ class FederatedClient:
             log.info(f"native RCCL communicator: {self.comm.world_size} ranks")
         # Identical start for every client: rank 0's weights win.
         broadcast_model(self.model, comm=self.comm)
+        self.grad_sync = None
+        if self.topo.dp:
+            dp_seed_offset(self.model, self.topo.dp_rank)
+            self.grad_sync = GradSync(self.model, self.topo.dp_group, self.topo.gpus_per_client,
+                                      max_rows=cfg.batch_size * cfg.max_len)
+            log.info(f"data-parallel client: replica {self.topo.dp_rank + 1}/{self.topo.gpus_per_client}")
         self.teacher = None
         if cfg.teacher:
             from ..models.bert import BertTeacherClassifier, bert_base_config
@@ -121,27 +135,33 @@ class FederatedClient:
                 train_model(self.teacher, self.train_loader, None, t_opt, int(cfg.extra.get("teacher_epochs", cfg.epochs)),
                             log=log, use_graph=cfg.use_graph)
         with self.timer("train"):
-            tr = train_model(model, self.train_loader, None, opt, cfg.epochs, log=log, use_graph=cfg.use_graph,
-                             teacher=self.teacher, kd_temperature=cfg.kd_temperature, kd_alpha=cfg.kd_alpha)
+            use_graph = cfg.use_graph and (self.grad_sync is None or cfg.dp_graph)
+            tr = train_model(model, self.train_loader, None, opt, cfg.epochs, log=log, use_graph=use_graph,
+                             teacher=self.teacher, kd_temperature=cfg.kd_temperature, kd_alpha=cfg.kd_alpha,
+                             grad_sync=self.grad_sync)
         log.info("evaluating local model on validation set...")
         with self.timer("eval"):
             val_local = evaluate_model(model, self.val_loader, log=log, name="Validation")
             log.info("evaluating local model on test set...")
             local = evaluate_model(model, self.test_loader, log=log, name="Test")
         sfx = "" if r == 0 else f"_round{r + 1}"
-        save_metrics(local, os.path.join(cfg.out_dir, f"client{self.client_id}_local_metrics{sfx}.csv"), log)
-        ck.save_model(model, ck.client_ckpt_path(cfg.out_dir, self.client_id))
-        if cfg.save_optimizer:
-            ck.save_optimizer(opt, opt_path)
+        if self.writer:
+            save_metrics(local, os.path.join(cfg.out_dir, f"client{self.client_id}_local_metrics{sfx}.csv"), log)
+            ck.save_model(model, ck.client_ckpt_path(cfg.out_dir, self.client_id))
+            if cfg.save_optimizer:
+                ck.save_optimizer(opt, opt_path)
 
         # ---- FedAvg (replaces send_model -> server aggregate -> receive_aggregated_model)
         part = faults.participants(r, self.num_clients, cfg.participation, cfg.base_seed)
         contributes = self.idx in part and not faults.dropped(cfg, self.idx, r)
         weight = float(len(self.data.train)) if cfg.weighted_fedavg else 1.0
+        weight /= self.topo.gpus_per_client  # k identical replicas per client share its weight
         faults.maybe_kill(self.idx, r)
         with self.timer("fedavg"):
             t0 = time.perf_counter()
             if cfg.transport == "tcp":
+                if self.topo.dp:
+                    raise NotImplementedError("tcp transport with data-parallel clients")
                 total_w = self._tcp_exchange(contributes)
             else:
                 total_w = fedavg_(model, weight=weight, participate=contributes, comm=self.comm)
@@ -157,18 +177,21 @@ class FederatedClient:
             val_agg = evaluate_model(model, self.val_loader, log=log, name="Validation")
             log.info("evaluating aggregated model on test set...")
             agg = evaluate_model(model, self.test_loader, log=log, name="Test")
-        save_metrics(agg, os.path.join(cfg.out_dir, f"client{self.client_id}_aggregated_metrics{sfx}.csv"), log)
-        if cfg.plots:
+        if self.writer:
+            save_metrics(agg, os.path.join(cfg.out_dir, f"client{self.client_id}_aggregated_metrics{sfx}.csv"), log)
+        if cfg.plots and self.writer:
             with self.timer("plot"):
                 from ..utils.plots import plot_evaluation
                 plot_evaluation(local, agg, os.path.join(cfg.out_dir, f"client{self.client_id}_plots"),
                                 f"Client {self.client_id}", log=log)
-        ck.save_model(model, ck.client_ckpt_path(cfg.out_dir, self.client_id))
+        if self.writer:
+            ck.save_model(model, ck.client_ckpt_path(cfg.out_dir, self.client_id))
         rec = {"round": r + 1, "train": tr, "fedavg_ms": t_fed * 1e3, "participated": contributes,
                "local_val": _metrics_record(val_local), "local_test": _metrics_record(local),
                "aggregated_val": _metrics_record(val_agg), "aggregated_test": _metrics_record(agg)}
         self.history.append(rec)
-        ck.save_fed_state(cfg.out_dir, self.client_id, {"completed_rounds": r + 1, "history": self.history})
+        if self.writer:
+            ck.save_fed_state(cfg.out_dir, self.client_id, {"completed_rounds": r + 1, "history": self.history})
         return rec
 
     def _tcp_exchange(self, contributes: bool) -> float:
@@ -205,12 +228,13 @@ class FederatedClient:
             a, l_ = last["aggregated_test"], last["local_test"]
             vec = [a["accuracy"], a["f1"], a["precision"], a["recall"], l_["accuracy"], l_["f1"],
                    last["train"]["batches_per_sec"], last["fedavg_ms"]]
-        allv = comm.all_gather_floats(vec)
+        allv = comm.all_gather_floats(vec)[::self.topo.gpus_per_client]  # replica 0 of each client
         rep = {"clients": [{"client": i + 1, "aggregated_test_accuracy": v[0], "aggregated_test_f1": v[1],
                             "aggregated_test_precision": v[2], "aggregated_test_recall": v[3],
                             "local_test_accuracy": v[4], "local_test_f1": v[5], "train_batches_per_sec": v[6],
                             "fedavg_ms": v[7]} for i, v in enumerate(allv)],
-               "rounds": self.cfg.rounds, "world_size": self.di.world_size, "phases_s": self.timer.summary()}
+               "rounds": self.cfg.rounds, "world_size": self.di.world_size,
+               "gpus_per_client": self.topo.gpus_per_client, "phases_s": self.timer.summary()}
         if self.di.is_main:
             path = os.path.join(self.cfg.out_dir, "federated_report.json")
             with open(path, "w") as f:

@@ -1,0 +1,144 @@
+"""Intra-client data parallelism (parallel/dp.py) on CPU with gloo.
+
+* 1 client x 2 replicas: after the gradient exchange each replica holds exactly the
+  gradient of the client-batch mean loss (= single-process full-batch gradient).
+* 2 clients x 2 replicas (world 4): the federated runner end to end -- replicas stay
+  identical, FedAvg averages the two clients, only replica 0 writes client files.
+"""
+import json
+import os
+import socket
+
+import torch
+import torch.multiprocessing as mp
+
+PKG = "detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd"
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env(rank, world, port):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+
+
+def _batch(n=7, S=32, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(1000, 2000, (n, S), generator=g)
+    ids[:, 0] = 101
+    mask = torch.ones(n, S, dtype=torch.int64)
+    mask[1::2, 20:] = 0
+    labels = torch.randint(0, 2, (n,), generator=g)
+    return ids, mask, labels
+
+
+def _model():
+    from importlib import import_module
+    models = import_module(f"{PKG}.models")
+    cfg = models.DistilBertConfig(n_layers=1, dropout=0.0, attention_dropout=0.0)
+    m = models.DDoSClassifier(config=cfg, seed=5, head_dropout=0.0, impl="torch")
+    m.train()
+    return m
+
+
+def _grad_worker(rank, world, port, outdir):
+    _env(rank, world, port)
+    from importlib import import_module
+    comm = import_module(f"{PKG}.parallel.comm")
+    dp = import_module(f"{PKG}.parallel.dp")
+    comm.init_distributed(device="cpu")
+    topo = dp.make_topology(2)
+    assert topo.num_clients == 1 and topo.dp_rank == rank
+    m = _model()
+    ids, mask, labels = _batch()
+    b = {"input_ids": ids, "attention_mask": mask, "labels": labels}
+
+    class _L:  # minimal loader: one client batch of 7 rows (unequal 4 / 3 shares)
+        n, batch_size, drop_last = 7, 7, False
+
+        def __iter__(self):
+            yield b
+
+    shard = next(iter(dp.DPShardLoader(_L(), topo.dp_rank, 2)))
+    sync = dp.GradSync(m, topo.dp_group, 2)
+    sync.set_loss_scale(shard["loss_scale"])
+    m.zero_grad()
+    loss, _ = m.forward_loss(shard["input_ids"], shard["attention_mask"], shard["labels"])
+    (loss * sync.loss_scale).backward()
+    sync.finish()
+    torch.save(m.arena.grad.clone(), os.path.join(outdir, f"grad{rank}.pt"))
+    comm.shutdown()
+
+
+def test_dp_gradient_equals_full_batch(tmp_path):
+    port = _free_port()
+    mp.spawn(_grad_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    g0 = torch.load(tmp_path / "grad0.pt", weights_only=True)
+    g1 = torch.load(tmp_path / "grad1.pt", weights_only=True)
+    assert torch.equal(g0, g1)  # both replicas hold the same summed gradient
+    m = _model()
+    ids, mask, labels = _batch()
+    m.zero_grad()
+    loss, _ = m.forward_loss(ids, mask, labels)
+    loss.backward()
+    ref = m.arena.grad
+    assert torch.allclose(g0, ref, rtol=1e-4, atol=1e-7), (g0 - ref).abs().max()
+
+
+def test_shard_loader_splits_and_skips():
+    from importlib import import_module
+    dp = import_module(f"{PKG}.parallel.dp")
+    data = import_module(f"{PKG}.data")
+
+    class _DS:
+        def __init__(self, n):
+            self.input_ids = torch.arange(n * 4).view(n, 4)
+            self.attention_mask = torch.ones(n, 4, dtype=torch.int64)
+            self.labels = torch.arange(n)
+
+        def __len__(self):
+            return len(self.labels)
+
+    loader = data.DeviceLoader(_DS(17), 8)  # batches of 8, 8, 1
+    shards = [list(dp.DPShardLoader(loader, r, 2)) for r in range(2)]
+    assert len(dp.DPShardLoader(loader, 0, 2)) == 2 == len(shards[0])  # the 1-row tail is skipped
+    for b0, b1 in zip(*shards):
+        assert b0["loss_scale"] + b1["loss_scale"] == 1.0
+        assert set(b0["labels"].tolist()).isdisjoint(b1["labels"].tolist())
+
+
+def _fed_worker(rank, world, port, outdir):
+    _env(rank, world, port)
+    from importlib import import_module
+    runner = import_module(f"{PKG}.fed.runner")
+    config = import_module(f"{PKG}.config")
+    models = import_module(f"{PKG}.models")
+    data = import_module(f"{PKG}.data")
+    comm = import_module(f"{PKG}.parallel.comm")
+    comm.init_distributed(device="cpu")
+    cfg = config.FedConfig(out_dir=outdir, synthetic_rows=800, data_fraction=0.1, max_len=64, epochs=1,
+                           batch_size=8, eval_batch_size=16, plots=False, resume=False, rounds=1,
+                           verbose=False, gpus_per_client=2)
+    frame = data.generate_cicids2017(cfg.synthetic_rows, seed=0)
+    client = runner.FederatedClient(cfg, frame=frame, model_config=models.DistilBertConfig(n_layers=1))
+    client.run()
+    torch.save(client.model.arena.master.clone(), os.path.join(outdir, f"master{rank}.pt"))
+    comm.shutdown()
+
+
+def test_two_dp_clients_federated_run(tmp_path):
+    port = _free_port()
+    mp.spawn(_fed_worker, args=(4, port, str(tmp_path)), nprocs=4, join=True)
+    ms = [torch.load(tmp_path / f"master{r}.pt", weights_only=True) for r in range(4)]
+    for m in ms[1:]:
+        assert torch.equal(ms[0], m)  # replicas identical, and FedAvg made the clients identical
+    rep = json.load(open(tmp_path / "federated_report.json"))
+    assert len(rep["clients"]) == 2 and rep["gpus_per_client"] == 2
+    for cid in (1, 2):
+        assert (tmp_path / f"client{cid}_local_metrics.csv").exists()
+        assert (tmp_path / f"client{cid}_model.pth").exists()
+    assert not (tmp_path / "client3_model.pth").exists()
