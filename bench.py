@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--layers", type=int, default=6)
     ap.add_argument("--comm", default="torch", choices=["torch", "rccl"],
                     help="FedAvg collective: torch.distributed (RCCL) or the framework's NativeComm (RCCL)")
+    ap.add_argument("--gpus-per-client", type=int, default=1,
+                    help="k > 1: each federated client is k data-parallel GPUs (per-step gradient all-reduce); "
+                         "--batch-size stays the per-client batch")
     ap.add_argument("--teacher", action="store_true",
                     help="distillation step (BASELINE.json config 5): BERT-base teacher fwd + DistilBERT student")
     args = ap.parse_args()
@@ -56,13 +59,18 @@ def main():
 
     di = comm.init_distributed()
     dev = di.device
+    dp = import_module(f"{PKG}.parallel.dp")
+    topo = dp.make_topology(args.gpus_per_client)
+    client = topo.client_idx
     B, S = args.batch_size, args.seq_len
     n_batches = args.warmup + args.steps
     # Synthetic CICIDS2017 rows -> the reference's text template -> WordPiece ids.
-    df = data.generate_cicids2017(max(n_batches * B * 2, 4096), seed=di.rank)
-    cd = data.build_client_data(df, di.rank, data_fraction=1.0, max_len=S)
+    df = data.generate_cicids2017(max(n_batches * B * 2, 4096), seed=client)
+    cd = data.build_client_data(df, client, data_fraction=1.0, max_len=S)
     train = cd.train
-    loader = data.DeviceLoader(train, B, shuffle=True, device=dev, seed=di.rank, drop_last=True)
+    loader = data.DeviceLoader(train, B, shuffle=True, device=dev, seed=client, drop_last=True)
+    if topo.dp:
+        loader = dp.DPShardLoader(loader, topo.dp_rank, topo.gpus_per_client)
 
     cfg = models.DistilBertConfig(n_layers=args.layers)
     model = models.DDoSClassifier(config=cfg, device=dev, impl=args.impl, seed=0)
@@ -71,15 +79,23 @@ def main():
         ncomm = import_module(f"{PKG}.parallel.rccl").NativeComm()
     fedavg.broadcast_model(model, comm=ncomm)
     opt = engine.ArenaAdam(model, lr=2e-5)
-    if args.teacher:
+    gsync = None
+    if topo.dp:
+        if args.teacher:
+            raise SystemExit("--teacher with --gpus-per-client > 1 is not supported")
+        dp.dp_seed_offset(model, topo.dp_rank)
+        gsync = dp.GradSync(model, topo.dp_group, topo.gpus_per_client, max_rows=B * S)
+        gsync.set_loss_scale(1.0 / topo.gpus_per_client)
+        fn = dp.make_dp_step_fn(model, opt, gsync)
+    elif args.teacher:
         teacher = models.BertTeacherClassifier(config=models.bert_base_config(), device=dev, impl=args.impl)
         fedavg.broadcast_model(teacher, comm=ncomm)
         teacher.eval()
         fn = engine.make_kd_step_fn(model, teacher, opt, 2.0, 0.5)
     else:
         fn = engine.make_step_fn(model, opt)
-    step = engine.GraphedTrainStep(fn, warmup=2,
-                                   enabled=(not args.no_graph) and args.impl == "hip" and dev.type == "cuda")
+    step = engine.GraphedTrainStep(fn, warmup=2, enabled=(not args.no_graph) and args.impl == "hip"
+                                   and dev.type == "cuda" and gsync is None)
     model.train()
 
     def batches():
@@ -91,8 +107,9 @@ def main():
     for _ in range(args.warmup):
         b = next(it)
         step(b["input_ids"], b["attention_mask"], b["labels"])
+    k = topo.gpus_per_client
     if args.gpus > 1 or di.distributed:
-        fedavg.fedavg_(model, comm=ncomm)
+        fedavg.fedavg_(model, weight=1.0 / k, comm=ncomm)
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     sync()
     comm.barrier()
@@ -103,7 +120,7 @@ def main():
         b = next(it)
         loss_acc += step(b["input_ids"], b["attention_mask"], b["labels"])
     if di.distributed:
-        fedavg.fedavg_(model, comm=ncomm)
+        fedavg.fedavg_(model, weight=1.0 / k, comm=ncomm)
     sync()
     comm.barrier()
     sync()
@@ -113,11 +130,12 @@ def main():
     if not (loss == loss and abs(loss) < 1e6):
         raise SystemExit(f"bench: non-finite training loss {loss} -- refusing to report a throughput")
     n = di.world_size
+    clients = topo.num_clients
     per_client = args.steps / dt
     if di.is_main:
         out = {
             "metric": "batches/sec/client (DistilBERT seq128 bs32) + aggregated F1 after 1 FedAvg round, 1/2/4/8 MI355X",
-            "value": round(per_client * n, 4),
+            "value": round(per_client * clients, 4),
             "unit": "batches/s (sum over clients; bs32 x seq128)",
             "n_gpus": n,
             "steps": args.steps,
@@ -130,10 +148,11 @@ def main():
             "data": "synthetic CICIDS2017-shaped flows rendered to text, WordPiece seq128; random-init weights",
             "config": {"model": f"DistilBERT-base ({args.layers} layers) + Linear(768,2) DDoSClassifier"
                                 + (" <- KD from BERT-base teacher" if args.teacher else ""),
-                       "global_batch": B * n, "seq_len": S, "parallelism": f"fedavg{n} (1 client/GPU)"},
+                       "global_batch": B * clients, "seq_len": S,
+                       "parallelism": f"fedavg{n} (1 client/GPU)" if k == 1 else f"fedavg{clients} x dp{k}"},
             "per_client_batches_per_sec": round(per_client, 4),
-            "samples_per_sec_total": round(per_client * n * B, 2),
-            "tokens_per_sec_total": round(per_client * n * B * S, 1),
+            "samples_per_sec_total": round(per_client * clients * B, 2),
+            "tokens_per_sec_total": round(per_client * clients * B * S, 1),
             "vs_baseline_basis": "per-client batches/s / 2.5 (reference bs16 fp32 per-client rate)",
             "impl": args.impl,
             "comm": args.comm,
