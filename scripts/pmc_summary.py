@@ -5,7 +5,9 @@ pass directories and prints, per kernel family: calls per step, mean time, MFMA
 busy share, LDS bank-conflict rate, L2 hit rate and HBM read/write bandwidth.
 
 Conventions (MI355X_MICROARCH.md "rocprofv3 PMC slots"):
-  MFMA busy  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * 256 CUs * 4 SIMDs)   (gfx94x formula)
+  MFMA busy  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs)  (rocprofv3's MfmaUtil;
+               the per-dispatch CSV value of GRBM_GUI_ACTIVE is summed over the 8 XCDs, the derived
+               metric takes the max -- calibrated: FFN1 fwd at 594 TFLOP/s = 24 % of 2.5 PF reads 22.6 %)
   LDS conf   = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   L2 hit     = TCC_HIT / (TCC_HIT + TCC_MISS)
   HBM rd/wr  = FETCH_SIZE / WRITE_SIZE (KiB) / kernel time; on gfx950 FETCH_SIZE reads
@@ -38,7 +40,7 @@ for f in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), rec
     seen = set()
     for r in csv.DictReader(open(f)):
         k = family(r["Kernel_Name"])
-        counters[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        counters[k][(pas, r["Counter_Name"])] += float(r["Counter_Value"])
         key = (pas, r.get("Dispatch_Id") or r.get("Correlation_Id"))
         if key not in seen:
             seen.add(key)
@@ -59,12 +61,13 @@ for k in sorted(dur, key=lambda k: -dur[k]):
     n = ncalls[k]
     t = dur[k] / max(n, 1)
     tot += dur[k]
-    per = lambda name, pas: c[name] / max(calls[k][pas], 1)  # noqa: E731  per-dispatch mean
-    gui = per("GRBM_GUI_ACTIVE", "sq")
+    per = lambda name, pas: c[(pas, name)] / max(calls[k][pas], 1)  # noqa: E731  per-dispatch mean
+    gui = per("GRBM_GUI_ACTIVE", "sq") / 8
     mf = per("SQ_VALU_MFMA_BUSY_CYCLES", "sq") / (gui * CUS * 4) if gui else 0.0
-    lds = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"] if c["SQ_LDS_IDX_ACTIVE"] else 0.0
-    hm = c["TCC_HIT_sum"] + c["TCC_MISS_sum"]
-    hit = c["TCC_HIT_sum"] / hm if hm else 0.0
+    la = c[("sq", "SQ_LDS_IDX_ACTIVE")]
+    lds = c[("sq", "SQ_LDS_BANK_CONFLICT")] / la if la else 0.0
+    hm = c[("l2", "TCC_HIT_sum")] + c[("l2", "TCC_MISS_sum")]
+    hit = c[("l2", "TCC_HIT_sum")] / hm if hm else 0.0
     rd = per("FETCH_SIZE", "rd") * 1024 / t / 1e9 if t else 0.0
     wr = per("WRITE_SIZE", "wr") * 1024 / t / 1e9 if t else 0.0
     print(f"{k:72s} {n / steps:8.1f} {t * 1e6:7.1f} {100 * mf:6.1f} {100 * lds:6.1f}% {100 * hit:5.1f}% "
