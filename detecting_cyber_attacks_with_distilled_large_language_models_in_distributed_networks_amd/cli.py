@@ -78,9 +78,13 @@ def _launch(argv):
     ap = argparse.ArgumentParser(prog="launch")
     ap.add_argument("--nproc", type=int, default=1)
     ap.add_argument("--port", type=int, default=29511)
+    ap.add_argument("--max-restarts", type=int, default=0,
+                    help="elastic recovery: restart the group this many times; clients resume at the "
+                         "first unfinished round")
     ns, rest = ap.parse_known_args(argv)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ns.nproc}",
-           "--master-addr", "127.0.0.1", "--master-port", str(ns.port), "-m", PKG, "client"] + rest
+           f"--max-restarts={ns.max_restarts}", "--master-addr", "127.0.0.1", "--master-port", str(ns.port),
+           "-m", PKG, "client"] + rest
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     sys.exit(subprocess.call(cmd, env=env))

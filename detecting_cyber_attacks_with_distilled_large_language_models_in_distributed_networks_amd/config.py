@@ -50,6 +50,8 @@ class FedConfig:
     weighted_fedavg: bool = False           # reference is unweighted (server.py:73-76)
     participation: float = 1.0              # fraction of clients aggregated per round
     timeout_s: float = 300.0                # server.py:10 / client1.py:22
+    heartbeat_s: float = 1.0                # failure detection (parallel/health.py); 0 disables
+    heartbeat_stale_s: float = 10.0         # a peer silent this long is declared dead
     transport: str = "collective"           # "collective" (RCCL/gloo all-reduce) | "tcp" (reference protocol)
     comm: str = "torch"                     # collective backend: "torch" (torch.distributed) | "rccl" (NativeComm)
     server_host: str = "localhost"          # client1.py:276,314

@@ -27,7 +27,7 @@ from ..config import FedConfig
 from ..data import DeviceLoader, WordPieceTokenizer, build_client_data, generate_cicids2017
 from ..engine import ArenaAdam, evaluate_model, train_model
 from ..models import DDoSClassifier, DistilBertConfig
-from ..parallel import comm
+from ..parallel import comm, health
 from ..parallel.dp import DPShardLoader, GradSync, dp_seed_offset, make_topology
 from ..parallel.fedavg import broadcast_model, fedavg_
 from ..utils import checkpoint as ck
@@ -109,11 +109,22 @@ class FederatedClient:
         self.history: List[Dict] = []
         if cfg.resume:
             st = ck.load_fed_state(cfg.out_dir, self.client_id)
-            if ck.load_model(self.model, ck.client_ckpt_path(cfg.out_dir, self.client_id)):
-                log.info(f"loading pre-trained model from {ck.client_ckpt_path(cfg.out_dir, self.client_id)}")
+            path = ck.client_ckpt_path(cfg.out_dir, self.client_id)
+            if st and int(st.get("completed_rounds", 0)) > 0 and os.path.exists(ck.global_ckpt_path(cfg.out_dir)):
+                # a crash inside round r leaves clientN_model.pth = the round-r LOCAL model; the
+                # round's true starting point is the last aggregate (identical on every client)
+                path = ck.global_ckpt_path(cfg.out_dir)
+            if ck.load_model(self.model, path):
+                log.info(f"loading pre-trained model from {path}")
                 if st:
                     self.start_round = int(st.get("completed_rounds", 0))
                     self.history = st.get("history", [])
+        self.health = None
+        if self.di.distributed and cfg.heartbeat_s > 0 and cfg.transport != "tcp":
+            self.health = health.start(cfg.heartbeat_s, cfg.heartbeat_stale_s, cfg.timeout_s)
+        restarts = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+        if restarts:
+            log.info(f"elastic restart #{restarts}: resuming at round {self.start_round + 1}")
         log.info(f"data: {len(self.data.train)} train / {len(self.data.val)} val / {len(self.data.test)} test rows "
                  f"(sampled {self.data.n_rows}), impl={self.model.impl}, device={dev}")
         return self
@@ -156,7 +167,13 @@ class FederatedClient:
         contributes = self.idx in part and not faults.dropped(cfg, self.idx, r)
         weight = float(len(self.data.train)) if cfg.weighted_fedavg else 1.0
         weight /= self.topo.gpus_per_client  # k identical replicas per client share its weight
-        faults.maybe_kill(self.idx, r)
+        faults.maybe_kill(self.idx, r, cfg.out_dir, self.topo.dp_rank)
+        if self.health is not None:
+            try:  # every client alive and here, or fail fast naming the dead rank
+                self.health.barrier(f"fedavg/{r}")
+            except health.PeerFailure as e:
+                log.info(f"[ERROR] {e}; aborting round {r + 1} (restart resumes from the last completed round)")
+                raise
         with self.timer("fedavg"):
             t0 = time.perf_counter()
             if cfg.transport == "tcp":
@@ -214,9 +231,12 @@ class FederatedClient:
     # ------------------------------------------------------------------ all rounds
     def run(self) -> Dict:
         self.setup()
-        for r in range(self.start_round, self.cfg.rounds):
-            self.run_round(r)
-        report = self.report()
+        try:
+            for r in range(self.start_round, self.cfg.rounds):
+                self.run_round(r)
+            report = self.report()
+        finally:
+            health.stop()
         self.log.phase("Client shutdown")
         return report
 

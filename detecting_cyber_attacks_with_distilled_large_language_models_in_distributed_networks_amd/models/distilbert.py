@@ -235,6 +235,12 @@ class DDoSClassifier(nn.Module):
         # HIP path: backward dX GEMMs read W^T copies (K-major staging is ~30% faster than
         # reading W MN-major; the per-step transpose of the encoder weights is ~85 MB r+w)
         self.transposed_dx = True
+        # HIP path: weight-gradient work of the backward on a side stream (ops/functional.py).
+        # Bitwise identical either way; measured on MI355X at bs32 x seq128 (scripts/gpu_ab.sh,
+        # 3 A/B pairs): 3.24 ms/step with vs 3.20 without -- the concurrent dW and dX grids slow
+        # each other ~30 % (LDS-bound co-residency), so the gain is eaten.  Off by default.
+        self.wgrad_stream = False
+        self._wgrad = None
         self.torch_counter = 0
         self._grad_token = None
         self._synced_version = -1
@@ -258,6 +264,7 @@ class DDoSClassifier(nn.Module):
         self.emb_ever = torch.zeros(V, dtype=torch.uint8, device=dev) if dev.type == "cuda" else None
         self._grad_token = torch.zeros((), device=dev, requires_grad=True)
         self._hip_cache = None
+        self._wgrad = None
         self._synced_version = -1
         return self
 
@@ -390,9 +397,13 @@ class DDoSClassifier(nn.Module):
             S += pad
         emb, layers, head = self._hip_handles()
         cfg = self.config
+        grad = torch.is_grad_enabled()
+        if grad and self.wgrad_stream and self._wgrad is None:
+            self._wgrad = torch.cuda.Stream(device=self.arena.device)
         rc = RunCtx(B=B, S=S, H=cfg.n_heads, kbias=K.mask_bias(mask), seed=self.rng, training=self.training,
                     eps=cfg.layer_norm_eps, p_hidden=cfg.dropout, p_attn=cfg.attention_dropout, p_head=self.dropout.p,
-                    on_layer_grads=self.layer_grads_hook if torch.is_grad_enabled() else None)
+                    on_layer_grads=self.layer_grads_hook if grad else None,
+                    wgrad=self._wgrad if grad and self.wgrad_stream else None)
         if self.training:
             K.step_inc(None, self.rng)
         token = self._grad_token if torch.is_grad_enabled() else None

@@ -38,6 +38,32 @@ class RunCtx:
     # called with the layer index once a block's parameter gradients are final
     # (lets the optimizer update that block on a side stream during the rest of backward)
     on_layer_grads: Optional[Callable[[int], None]] = None
+    # side stream for the weight-gradient work (dW GEMMs, split-K reduces, bias column
+    # sums): it is off the backward's critical path (dX -> LN bwd -> attention bwd ->
+    # dX ...), so it runs concurrently with it and fills the CUs the one-round dX grids
+    # leave idle.  Joined at the end of the embedding backward (the last node).
+    wgrad: Optional["torch.cuda.Stream"] = None
+
+
+class _WGrad:
+    """Fork weight-gradient work onto ``rc.wgrad`` (no-op without a side stream)."""
+
+    def __init__(self, rc: RunCtx):
+        self.side = rc.wgrad
+        self.cur = torch.cuda.current_stream() if self.side is not None else None
+
+    def fork(self, *tensors):
+        """Side stream waits for everything issued so far; ``tensors`` may be freed by
+        the main stream while the side stream still reads them -> record the use."""
+        if self.side is None:
+            return
+        self.side.wait_stream(self.cur)
+        for t in tensors:
+            t.record_stream(self.side)
+
+    def ctx(self):
+        import contextlib
+        return torch.cuda.stream(self.side) if self.side is not None else contextlib.nullcontext()
 
 
 class GradSink:
@@ -74,6 +100,8 @@ class EmbeddingFn(torch.autograd.Function):
         now, ever = s.get("flags") or (None, None)
         K.emb_bwd(dy, ids, srt, perm, word, pos, gamma, mean, rstd, s["word"].buf, s["pos"].buf, s["ln_w"].buf,
                   s["ln_b"].buf, ctx.rc.S, ctx.rc.seed, 1, ctx.p, acc, now, ever)
+        if ctx.rc.wgrad is not None:  # join the weight-gradient stream: every grad is final after this node
+            torch.cuda.current_stream().wait_stream(ctx.rc.wgrad)
         return (None,) * 8
 
 
@@ -108,29 +136,37 @@ class LayerFn(torch.autograd.Function):
         attn_site, ffn_site = ctx.sites
         p_a, p_h = ctx.p
         acc = G["l2_w"].accumulate()
+        wg = _WGrad(rc)  # dW / bias-sum work -> side stream, dX chain stays on the main stream
         # output_layer_norm(dropout(lin2) + h): dz2 -> residual grad of h, df -> lin2 output grad
         dz2, df = K.ln_bwd(dy, f, h, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, rc.seed,
                            ffn_site, p_h, acc)
         wt = L.get("wT") or {}
         du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"))  # dg W2 * gelu'(u)
-        K.linear_dw(df, g, G["l2_w"].buf, acc)
-        K.colsum(du, G["l1_b"].buf, acc)
+        wg.fork(df, g, du, h)
+        with wg.ctx():
+            K.linear_dw(df, g, G["l2_w"].buf, acc)
+            K.colsum(du, G["l1_b"].buf, acc)
+            K.linear_dw(du, h, G["l1_w"].buf, acc)
         dh = K.linear_dx(du, L["l1_w"], res=dz2, wt=wt.get("l1_w"))    # du W1 + dz2
-        K.linear_dw(du, h, G["l1_w"].buf, acc)
         # sa_layer_norm(out_lin + x)
         dz1, _ = K.ln_bwd(dh, ao, x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf, G["o_b"].buf, rc.seed, 0,
                           0.0, acc)
         dcx = K.linear_dx(dz1, L["o_w"], wt=wt.get("o_w"))
-        K.linear_dw(dz1, cx, G["o_w"].buf, acc)
+        wg.fork(dz1, cx)
+        with wg.ctx():
+            K.linear_dw(dz1, cx, G["o_w"].buf, acc)
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a)
-        K.colsum(dqkv, G["qkv_b"].buf, acc)
+        wg.fork(dqkv, x)
+        with wg.ctx():
+            K.colsum(dqkv, G["qkv_b"].buf, acc)
+            K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
         dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt.get("qkv_w"))
-        K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
         for k in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_w", "ln1_b", "l1_w", "l1_b", "l2_b", "ln2_w", "ln2_b"):
             G[k].accumulate()
         del ctx.acts
         if rc.on_layer_grads is not None:
-            rc.on_layer_grads(ctx.idx)
+            with wg.ctx():  # ordered after this block's dW work (and, via the forks, its LN grads)
+                rc.on_layer_grads(ctx.idx)
         return dx, None, None, None
 
 

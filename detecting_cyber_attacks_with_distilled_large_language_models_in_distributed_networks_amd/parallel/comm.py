@@ -61,6 +61,14 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 300.0, de
         kw = {}
         if be == "nccl":
             kw["device_id"] = dev
+        restart = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+        if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True" and restart != "0":
+            # Elastic restart: the torchrun agent's store outlives the failed attempt, and
+            # its rendezvous keys (peer addresses of the dead processes) would be reused.
+            # Rendezvous the new group under a prefix of its own.
+            store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), is_master=False,
+                                  timeout=datetime.timedelta(seconds=timeout_s))
+            kw["store"] = dist.PrefixStore(f"fedddos_pg/{restart}", store)
         dist.init_process_group(be, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     _INFO = DistInfo(rank, world, local, be, dev)
