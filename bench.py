@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--seq-len", type=int, default=128)
     ap.add_argument("--impl", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-group-dw", action="store_true", help="one launch per weight gradient (A/B)")
     ap.add_argument("--wgrad-stream", action="store_true",
                     help="run the backward's weight-gradient work on a side stream (A/B; measured slower)")
     ap.add_argument("--layers", type=int, default=6)
@@ -77,6 +78,7 @@ def main():
     cfg = models.DistilBertConfig(n_layers=args.layers)
     model = models.DDoSClassifier(config=cfg, device=dev, impl=args.impl, seed=0)
     model.wgrad_stream = args.wgrad_stream
+    model.group_dw = not args.no_group_dw
     ncomm = None
     if args.comm == "rccl" and dev.type == "cuda":
         ncomm = import_module(f"{PKG}.parallel.rccl").NativeComm()

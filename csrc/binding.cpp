@@ -15,6 +15,8 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
             int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
             long long workspace_elems, int accumulate, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
+int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
+                int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, hipStream_t st);
 int fd_transpose_batched(const void* const* srcs, void* const* dsts, const int* rows, const int* cols, int n,
                          hipStream_t st);
 const char* fd_comm_last_error();
@@ -121,6 +123,30 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
                    (int)A.size(1), (int)B.size(1), (int)N, ptr<float>(bias), ptr<void>(aux), (int)N,
                    ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, stream()),
            "gemm");
+}
+
+// Grouped weight gradients: C0 (+)= A0^T B0 and C1 (+)= A1^T B1 in one launch (shared K = tokens).
+void gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C0, const at::Tensor& A1,
+              const at::Tensor& B1, const at::Tensor& C1, const at::Tensor& workspace, bool accumulate) {
+  const at::Tensor* As[2] = {&A0, &A1};
+  const at::Tensor* Bs[2] = {&B0, &B1};
+  const at::Tensor* Cs[2] = {&C0, &C1};
+  const int64_t K = A0.size(0);
+  for (int i = 0; i < 2; ++i) {
+    need(*As[i], at::kBFloat16, "A");
+    need(*Bs[i], at::kBFloat16, "B");
+    need(*Cs[i], at::kFloat, "C");
+    TORCH_CHECK(As[i]->dim() == 2 && Bs[i]->dim() == 2 && Cs[i]->dim() == 2, "gemm_dw2 operands must be 2-D");
+    TORCH_CHECK(As[i]->size(0) == K && Bs[i]->size(0) == K, "gemm_dw2: all operands need K = ", K, " rows");
+    TORCH_CHECK(Cs[i]->size(0) == As[i]->size(1) && Cs[i]->size(1) == Bs[i]->size(1), "gemm_dw2: C shape mismatch");
+    TORCH_CHECK(As[i]->size(1) % 128 == 0 && Bs[i]->size(1) % 64 == 0, "gemm_dw2: M % 128 and N % 64 required");
+  }
+  TORCH_CHECK(K % 64 == 0, "gemm_dw2: K must be a multiple of 64");
+  need(workspace, at::kFloat, "workspace");
+  check_rc(fd_gemm_dw2(A0.data_ptr(), B0.data_ptr(), C0.data_ptr<float>(), (int)A0.size(1), (int)B0.size(1),
+                       A1.data_ptr(), B1.data_ptr(), C1.data_ptr<float>(), (int)A1.size(1), (int)B1.size(1), (int)K,
+                       workspace.data_ptr<float>(), workspace.numel(), accumulate ? 1 : 0, stream()),
+           "gemm_dw2");
 }
 
 // ---------------------------------------------------------------- native RCCL communicator
@@ -493,6 +519,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the federated DistilBERT engine";
   m.def("gemm", &gemm);
   m.def("gemm_set_cfg", &gemm_set_cfg);
+  m.def("gemm_dw2", &gemm_dw2);
   m.def("transpose_batched", &transpose_batched);
   m.def("comm_load", &comm_load);
   m.def("comm_unique_id", &comm_unique_id);

@@ -297,8 +297,18 @@ struct GemmCfg {
                                 OA::PER_WAVE * NW * 1024 == OA::BYTES && OB::PER_WAVE * NW * 1024 == OB::BYTES;
 };
 
+// Grouped launch (weight gradients): a second problem with the same K and kinds whose
+// tiles follow the first's in the logical tile order, so two dW GEMMs that become ready
+// together (lin1 + lin2, out_lin + qkv) fill the chip as one grid instead of two
+// split-K launches each with its own slab round trip.
+struct GemmGroup {
+  GemmParams q;   // second problem (used when ntiles0 < total tiles)
+  int ntiles0;    // tiles of the first problem
+  int ntiles;     // tiles of both
+};
+
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
-__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p) {
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, GemmGroup grp) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   using OA = typename G::OA;
   using OB = typename G::OB;
@@ -318,8 +328,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / WN, wc = wid % WN;
 
+  int bid = xcd_remap(blockIdx.x, grp.ntiles);
+  const bool second = bid >= grp.ntiles0;  // block-uniform
+  const GemmParams& p = second ? grp.q : p0;
+  if (second) bid -= grp.ntiles0;
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = p.N / BN;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   int tm, tn;
   tile_coords(bid, tiles_m, tiles_n, p.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
@@ -416,34 +429,42 @@ constexpr CfgDesc CFGS[NCFG] = {{128, 64, 2, 2, 3}, {128, 128, 2, 2, 2}, {128, 9
                                 {256, 128, 4, 2, 2}};
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
-bool launch_cfg(const GemmParams& p, int splits, hipStream_t st) {
+bool launch_cfg(const GemmParams& p, int splits, hipStream_t st, const GemmParams* q) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   if constexpr (!G::VALID) {
     return false;
   } else {
     if (p.N % BN != 0) return false;
-    const dim3 grid(((p.M + BM - 1) / BM) * (p.N / BN), 1, splits);
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKM, EPI, WM, WN, S>), grid, dim3(64 * WM * WN), 0, st, p);
+    GemmGroup grp{};
+    grp.ntiles0 = ((p.M + BM - 1) / BM) * (p.N / BN);
+    grp.ntiles = grp.ntiles0;
+    if (q) {
+      if (q->N % BN != 0 || q->M % BM != 0) return false;
+      grp.q = *q;
+      grp.ntiles += (q->M / BM) * (q->N / BN);
+    }
+    const dim3 grid(grp.ntiles, 1, splits);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKM, EPI, WM, WN, S>), grid, dim3(64 * WM * WN), 0, st, p, grp);
     return true;
   }
 }
 
 template <bool AK, bool BKM, int EPI>
-bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st) {
+bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st, const GemmParams* q = nullptr) {
   switch (id) {
-    case 0: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 3>(p, splits, st);
-    case 1: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 2>(p, splits, st);
-    case 2: return launch_cfg<128, 96, AK, BKM, EPI, 2, 2, 2>(p, splits, st);
-    case 3: return launch_cfg<256, 192, AK, BKM, EPI, 4, 2, 2>(p, splits, st);
-    case 4: return launch_cfg<256, 128, AK, BKM, EPI, 4, 2, 3>(p, splits, st);
-    case 5: return launch_cfg<64, 192, AK, BKM, EPI, 1, 4, 3>(p, splits, st);
-    case 6: return launch_cfg<128, 192, AK, BKM, EPI, 2, 4, 2>(p, splits, st);
-    case 7: return launch_cfg<256, 96, AK, BKM, EPI, 4, 1, 3>(p, splits, st);
-    case 8: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 2>(p, splits, st);
-    case 9: return launch_cfg<128, 96, AK, BKM, EPI, 2, 2, 3>(p, splits, st);
-    case 10: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 3>(p, splits, st);
-    case 11: return launch_cfg<256, 256, AK, BKM, EPI, 2, 4, 2>(p, splits, st);
-    case 12: return launch_cfg<256, 128, AK, BKM, EPI, 4, 2, 2>(p, splits, st);
+    case 0: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
+    case 1: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 2>(p, splits, st, q);
+    case 2: return launch_cfg<128, 96, AK, BKM, EPI, 2, 2, 2>(p, splits, st, q);
+    case 3: return launch_cfg<256, 192, AK, BKM, EPI, 4, 2, 2>(p, splits, st, q);
+    case 4: return launch_cfg<256, 128, AK, BKM, EPI, 4, 2, 3>(p, splits, st, q);
+    case 5: return launch_cfg<64, 192, AK, BKM, EPI, 1, 4, 3>(p, splits, st, q);
+    case 6: return launch_cfg<128, 192, AK, BKM, EPI, 2, 4, 2>(p, splits, st, q);
+    case 7: return launch_cfg<256, 96, AK, BKM, EPI, 4, 1, 3>(p, splits, st, q);
+    case 8: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 2>(p, splits, st, q);
+    case 9: return launch_cfg<128, 96, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
+    case 10: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
+    case 11: return launch_cfg<256, 256, AK, BKM, EPI, 2, 4, 2>(p, splits, st, q);
+    case 12: return launch_cfg<256, 128, AK, BKM, EPI, 4, 2, 2>(p, splits, st, q);
   }
   return false;
 }
@@ -582,6 +603,55 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
   const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, workspace, out, n4, slab, splits,
                      accumulate);
+  return 0;
+}
+
+// Two weight-gradient GEMMs over the same token dimension in ONE launch:
+//   C0[M0][N0] (+)= A0^T B0,  C1[M1][N1] (+)= A1^T B1   (A_i [K][M_i], B_i [K][N_i] bf16; C_i fp32)
+// Split K only while the combined grid is under one round; slabs of problem 0 then 1.
+int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
+                int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, hipStream_t st) {
+  if (K % BKT != 0 || M0 % 128 || M1 % 128 || N0 % 64 || N1 % 64 || M0 <= 0 || M1 <= 0) return 1;
+  int id = cfg_override(2);
+  if (id < 0) id = 8;
+  if (M0 % CFGS[id].bm || M1 % CFGS[id].bm || N0 % CFGS[id].bn || N1 % CFGS[id].bn) id = 8;
+  static const int diag = [] { const char* e = getenv("FD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
+  GemmParams p[2]{};
+  const void* As[2] = {A0, A1};
+  const void* Bs[2] = {B0, B1};
+  float* Cs[2] = {C0, C1};
+  const int Ms[2] = {M0, M1}, Ns[2] = {N0, N1};
+  const long long panel = (long long)CFGS[id].bm * K * 2;
+  const int gm = (int)std::max(1ll, std::min(16ll, (2ll << 20) / panel));
+  for (int i = 0; i < 2; ++i) {
+    p[i].A = (const bf16_t*)As[i]; p[i].B = (const bf16_t*)Bs[i]; p[i].C = Cs[i];
+    p[i].M = Ms[i]; p[i].N = Ns[i]; p[i].K = K; p[i].lda = Ms[i]; p[i].ldb = Ns[i]; p[i].ldc = Ns[i];
+    p[i].group_m = gm; p[i].diag = diag;
+  }
+  const long long tiles = tiles_of(id, M0, N0) + tiles_of(id, M1, N1);
+  int splits = 1;
+  const int so = splits_override();
+  if (so > 0) {
+    splits = so;
+    if (K % (splits * BKT) != 0) return 6;
+  } else {
+    while (tiles * splits < 400 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 512) splits *= 2;
+  }
+  const long long slab0 = (long long)M0 * N0, slab1 = (long long)M1 * N1;
+  if (splits > 1 && workspace_elems < (slab0 + slab1) * splits) splits = 1;
+  for (int i = 0; i < 2; ++i) p[i].k_split = K / splits;
+  if (splits == 1 && !accumulate) {
+    return launch_id<false, false, EPI_F32>(p[0], id, 1, st, &p[1]) ? 0 : 7;
+  }
+  p[0].C = workspace; p[0].slab_stride = slab0;
+  p[1].C = workspace + slab0 * splits; p[1].slab_stride = slab1;
+  if (!launch_id<false, false, EPI_F32>(p[0], id, splits, st, &p[1])) return 7;
+  for (int i = 0; i < 2; ++i) {
+    const long long n4 = (i ? slab1 : slab0) / 4;
+    const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)p[i].C, Cs[i], n4,
+                       i ? slab1 : slab0, splits, accumulate);
+  }
   return 0;
 }
 

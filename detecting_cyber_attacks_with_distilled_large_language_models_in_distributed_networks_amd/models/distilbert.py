@@ -241,6 +241,8 @@ class DDoSClassifier(nn.Module):
         # each other ~30 % (LDS-bound co-residency), so the gain is eaten.  Off by default.
         self.wgrad_stream = False
         self._wgrad = None
+        # HIP path: grouped weight-gradient GEMMs (RunCtx.group_dw)
+        self.group_dw = True
         self.torch_counter = 0
         self._grad_token = None
         self._synced_version = -1
@@ -403,7 +405,7 @@ class DDoSClassifier(nn.Module):
         rc = RunCtx(B=B, S=S, H=cfg.n_heads, kbias=K.mask_bias(mask), seed=self.rng, training=self.training,
                     eps=cfg.layer_norm_eps, p_hidden=cfg.dropout, p_attn=cfg.attention_dropout, p_head=self.dropout.p,
                     on_layer_grads=self.layer_grads_hook if grad else None,
-                    wgrad=self._wgrad if grad and self.wgrad_stream else None)
+                    wgrad=self._wgrad if grad and self.wgrad_stream else None, group_dw=self.group_dw)
         if self.training:
             K.step_inc(None, self.rng)
         token = self._grad_token if torch.is_grad_enabled() else None

@@ -43,6 +43,9 @@ class RunCtx:
     # dX ...), so it runs concurrently with it and fills the CUs the one-round dX grids
     # leave idle.  Joined at the end of the embedding backward (the last node).
     wgrad: Optional["torch.cuda.Stream"] = None
+    # launch the weight gradients that become ready together (lin2 + lin1, out_lin + qkv)
+    # as one grouped GEMM grid (fewer split-K slab round trips; csrc/kernels/gemm.hip)
+    group_dw: bool = True
 
 
 class _WGrad:
@@ -144,22 +147,29 @@ class LayerFn(torch.autograd.Function):
         du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"))  # dg W2 * gelu'(u)
         wg.fork(df, g, du, h)
         with wg.ctx():
-            K.linear_dw(df, g, G["l2_w"].buf, acc)
+            if rc.group_dw:
+                K.linear_dw2(df, g, G["l2_w"].buf, du, h, G["l1_w"].buf, acc)
+            else:
+                K.linear_dw(df, g, G["l2_w"].buf, acc)
+                K.linear_dw(du, h, G["l1_w"].buf, acc)
             K.colsum(du, G["l1_b"].buf, acc)
-            K.linear_dw(du, h, G["l1_w"].buf, acc)
         dh = K.linear_dx(du, L["l1_w"], res=dz2, wt=wt.get("l1_w"))    # du W1 + dz2
         # sa_layer_norm(out_lin + x)
         dz1, _ = K.ln_bwd(dh, ao, x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf, G["o_b"].buf, rc.seed, 0,
                           0.0, acc)
         dcx = K.linear_dx(dz1, L["o_w"], wt=wt.get("o_w"))
-        wg.fork(dz1, cx)
-        with wg.ctx():
-            K.linear_dw(dz1, cx, G["o_w"].buf, acc)
+        if not rc.group_dw:
+            wg.fork(dz1, cx)
+            with wg.ctx():
+                K.linear_dw(dz1, cx, G["o_w"].buf, acc)
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a)
-        wg.fork(dqkv, x)
+        wg.fork(dqkv, x, dz1, cx)
         with wg.ctx():
+            if rc.group_dw:
+                K.linear_dw2(dz1, cx, G["o_w"].buf, dqkv, x, G["qkv_w"].buf, acc)
+            else:
+                K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
             K.colsum(dqkv, G["qkv_b"].buf, acc)
-            K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
         dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt.get("qkv_w"))
         for k in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_w", "ln1_b", "l1_w", "l1_b", "l2_b", "ln2_w", "ln2_b"):
             G[k].accumulate()

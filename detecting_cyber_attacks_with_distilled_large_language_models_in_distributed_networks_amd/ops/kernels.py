@@ -79,6 +79,14 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: 
     return out
 
 
+def linear_dw2(dy0: torch.Tensor, x0: torch.Tensor, out0: torch.Tensor, dy1: torch.Tensor, x1: torch.Tensor,
+               out1: torch.Tensor, accumulate: bool = False):
+    """Two weight gradients that become ready together, one launch: out_i (+)= dy_i^T x_i."""
+    n = out0.numel() + out1.numel()
+    ws = workspace(dy0.device, "splitk", 8 * n)
+    ext().gemm_dw2(dy0, x0, out0, dy1, x1, out1, ws, accumulate)
+
+
 def transpose_many(srcs, dsts):
     """dsts[i] = srcs[i]^T (bf16, one launch for up to 32 matrices)."""
     for i in range(0, len(srcs), 32):

@@ -100,6 +100,24 @@ def test_gemm_tn(M, N, T):
     assert rel_err(out, 2 * ref) < 2e-3
 
 
+@pytest.mark.parametrize("shapes,T", [(((768, 3072), (3072, 768)), 4096),   # lin2 + lin1 (no split)
+                                      (((768, 768), (2304, 768)), 4096),    # out_lin + qkv (split-K)
+                                      (((768, 768), (2304, 768)), 512)])
+def test_gemm_tn_grouped(shapes, T):
+    """Two dW GEMMs in one grouped launch == two separate torch fp32 products (plain and accumulate)."""
+    (M0, N0), (M1, N1) = shapes
+    dy0, x0, dy1, x1 = bf(T, M0, seed=21), bf(T, N0, seed=22), bf(T, M1, seed=23), bf(T, N1, seed=24)
+    o0, o1 = torch.empty(M0, N0, device=DEV), torch.empty(M1, N1, device=DEV)
+    kn.linear_dw2(dy0, x0, o0, dy1, x1, o1)
+    r0, r1 = dy0.float().t() @ x0.float(), dy1.float().t() @ x1.float()
+    assert rel_err(o0, r0) < 2e-3 and rel_err(o1, r1) < 2e-3
+    kn.linear_dw2(dy0, x0, o0, dy1, x1, o1, accumulate=True)
+    assert rel_err(o0, 2 * r0) < 2e-3 and rel_err(o1, 2 * r1) < 2e-3
+    single = torch.empty(M1, N1, device=DEV)
+    kn.linear_dw(dy1, x1, single)
+    assert rel_err(o1, 2 * single) < 1e-5  # same tile math as the single launch
+
+
 def test_colsum():
     x = bf(4096, 3072, seed=13)
     out = torch.empty(3072, device=DEV)
