@@ -29,18 +29,19 @@ int fd_comm_allreduce(void* comm, const void* send, void* recv, long long count,
 int fd_comm_broadcast(void* comm, void* buf, long long count, int dtype, int root, hipStream_t st);
 int fd_comm_allgather(void* comm, const void* send, void* recv, long long count, int dtype, hipStream_t st);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
-                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, hipStream_t st);
+                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
+                hipStream_t st);
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx,
                 float* delta, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site,
-                uint32_t thr, float drop_scale, hipStream_t st);
+                uint32_t thr, float drop_scale, const int* cu, hipStream_t st);
 int fd_mask_to_bias(const void* mask, int mask_bytes, float* bias, long n, hipStream_t st);
 int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, float* mean,
               float* rstd, int T, int D, float eps, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
-              float dscale, hipStream_t st);
+              float dscale, const int* row_map, hipStream_t st);
 int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean,
               const float* rstd, void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work, int T,
               int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, int accumulate,
-              hipStream_t st);
+              const int* row_map, hipStream_t st);
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, hipStream_t st);
@@ -231,23 +232,47 @@ void gemm_set_cfg(int64_t kind, int64_t cfg, int64_t splits) {
   check_rc(fd_gemm_set_cfg((int)kind, (int)cfg, (int)splits), "gemm_set_cfg");
 }
 
+// Varlen (packed) mode: `cu` = int32 [B+1] sequence starts in the packed rows of qkv/ctx
+// (sequence b = rows cu[b] .. cu[b+1]-1, at most S long); the kernels clamp every row
+// read to its sequence and never write outside it.  The caller guarantees cu[B] <= rows
+// (the device values cannot be read here without a sync).
+void check_cu(const c10::optional<at::Tensor>& cu, int64_t B, int64_t rows_qkv, int64_t rows_ctx) {
+  if (!(cu.has_value() && cu->defined())) return;
+  need(*cu, at::kInt, "cu");
+  TORCH_CHECK(cu->numel() == B + 1, "attention: cu must have B+1 entries");
+  TORCH_CHECK(rows_qkv >= 1 && rows_qkv == rows_ctx, "attention: packed qkv/ctx row counts differ");
+}
+
+// Optional int32 [T] packed-row -> padded-row map (dropout-hash indexing only).
+const int* map_ptr(const c10::optional<at::Tensor>& m, int64_t T) {
+  if (!(m.has_value() && m->defined())) return nullptr;
+  need(*m, at::kInt, "row_map");
+  TORCH_CHECK(m->numel() == T, "row_map must have one entry per row");
+  return m->data_ptr<int>();
+}
+
 void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
-              int64_t B, int64_t S, int64_t H, const at::Tensor& seed, int64_t site, int64_t thr, double dscale) {
+              int64_t B, int64_t S, int64_t H, const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
+              const c10::optional<at::Tensor>& cu) {
   need(qkv, at::kBFloat16, "qkv");
   need(kbias, at::kFloat, "kbias");
   need(ctx, at::kBFloat16, "ctx");
   need(lse, at::kFloat, "lse");
   TORCH_CHECK(S % 64 == 0 && S <= 512, "attention: S must be a multiple of 64 and <= 512");
-  TORCH_CHECK(qkv.numel() == B * S * 3 * H * 64 && ctx.numel() == B * S * H * 64, "attention: qkv/ctx size");
-  TORCH_CHECK(kbias.numel() == B * S && lse.numel() == B * H * S, "attention: kbias/lse size");
+  const bool varlen = cu.has_value() && cu->defined();
+  const int64_t rows = varlen ? qkv.numel() / (3 * H * 64) : B * S;
+  TORCH_CHECK(qkv.numel() == rows * 3 * H * 64 && ctx.numel() == rows * H * 64, "attention: qkv/ctx size");
+  TORCH_CHECK((varlen || kbias.numel() == B * S) && lse.numel() == B * H * S, "attention: kbias/lse size");
+  check_cu(cu, B, rows, ctx.numel() / (H * 64));
   check_rc(fd_attn_fwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(), (int)B,
-                       (int)S, (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, stream()),
+                       (int)S, (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu),
+                       stream()),
            "attn_fwd");
 }
 
 void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
               const at::Tensor& dctx, const at::Tensor& delta, const at::Tensor& dqkv, int64_t B, int64_t S, int64_t H,
-              const at::Tensor& seed, int64_t site, int64_t thr, double dscale) {
+              const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& cu) {
   need(qkv, at::kBFloat16, "qkv");
   need(kbias, at::kFloat, "kbias");
   need(ctx, at::kBFloat16, "ctx");
@@ -256,12 +281,16 @@ void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
   need(delta, at::kFloat, "delta");
   need(dqkv, at::kBFloat16, "dqkv");
   TORCH_CHECK(S % 64 == 0 && S <= 512, "attention: S must be a multiple of 64 and <= 512");
-  TORCH_CHECK(qkv.numel() == B * S * 3 * H * 64 && dqkv.numel() == qkv.numel(), "attention bwd: qkv size");
-  TORCH_CHECK(ctx.numel() == B * S * H * 64 && dctx.numel() == ctx.numel(), "attention bwd: ctx size");
-  TORCH_CHECK(lse.numel() == B * H * S && delta.numel() == B * H * S && kbias.numel() == B * S, "attention bwd: stats");
+  const bool varlen = cu.has_value() && cu->defined();
+  const int64_t rows = varlen ? qkv.numel() / (3 * H * 64) : B * S;
+  TORCH_CHECK(qkv.numel() == rows * 3 * H * 64 && dqkv.numel() == qkv.numel(), "attention bwd: qkv size");
+  TORCH_CHECK(ctx.numel() == rows * H * 64 && dctx.numel() == ctx.numel(), "attention bwd: ctx size");
+  TORCH_CHECK(lse.numel() == B * H * S && delta.numel() == B * H * S && (varlen || kbias.numel() == B * S),
+              "attention bwd: stats");
+  check_cu(cu, B, rows, ctx.numel() / (H * 64));
   check_rc(fd_attn_bwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(),
                        dctx.data_ptr(), delta.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)S, (int)H,
-                       seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, stream()),
+                       seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), stream()),
            "attn_bwd");
 }
 
@@ -276,7 +305,7 @@ void mask_to_bias(const at::Tensor& mask, const at::Tensor& bias) {
 
 void ln_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& r, const at::Tensor& gamma, const at::Tensor& beta,
             const at::Tensor& y, const at::Tensor& mean, const at::Tensor& rstd, double eps, const at::Tensor& seed,
-            int64_t site, int64_t thr, double dscale) {
+            int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& row_map) {
   need(x, at::kBFloat16, "x");
   need_opt(r, at::kBFloat16, "r");
   need(gamma, at::kFloat, "gamma");
@@ -290,7 +319,7 @@ void ln_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& r, const at::T
   if (r.has_value() && r->defined()) TORCH_CHECK(r->numel() == x.numel(), "ln_fwd: residual size");
   check_rc(fd_ln_fwd(x.data_ptr(), ptr<void>(r), gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
                      mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)T, (int)D, (float)eps, seedp(seed),
-                     (uint32_t)site, (uint32_t)thr, (float)dscale, stream()),
+                     (uint32_t)site, (uint32_t)thr, (float)dscale, map_ptr(row_map, T), stream()),
            "ln_fwd");
 }
 
@@ -298,7 +327,7 @@ void ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::T
             const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dz, const c10::optional<at::Tensor>& dx,
             const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
             const c10::optional<at::Tensor>& dbias, const at::Tensor& work, const at::Tensor& seed, int64_t site,
-            int64_t thr, double dscale, bool accumulate) {
+            int64_t thr, double dscale, bool accumulate, const c10::optional<at::Tensor>& row_map) {
   need(dy, at::kBFloat16, "dy");
   need(x, at::kBFloat16, "x");
   need_opt(r, at::kBFloat16, "r");
@@ -318,7 +347,7 @@ void ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::T
   check_rc(fd_ln_bwd(dy.data_ptr(), x.data_ptr(), ptr<void>(r), gamma.data_ptr<float>(), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), dz.data_ptr(), ptr<void>(dx), ptr<float>(dgamma), ptr<float>(dbeta),
                      ptr<float>(dbias), work.data_ptr<float>(), (int)T, (int)D, seedp(seed), (uint32_t)site,
-                     (uint32_t)thr, (float)dscale, accumulate ? 1 : 0, stream()),
+                     (uint32_t)thr, (float)dscale, accumulate ? 1 : 0, map_ptr(row_map, T), stream()),
            "ln_bwd");
 }
 

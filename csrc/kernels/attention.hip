@@ -39,13 +39,15 @@ constexpr int DH = 64;
 DEV int sw(int r) { return (((r >> 1) & 3) << 1) | ((r >> 3) & 1); }
 DEV int tile_off(int r, int c) { return r * 128 + ((c ^ sw(r)) << 4); }
 
-// Stage a [64][64] bf16 tile (row stride ld elements) into LDS; 256 threads.
-DEV void stage_tile(char* lds, const bf16_t* src, long ld, int tid) {
+// Stage a [64][64] bf16 tile (row stride ld elements) into LDS; 256 threads.  Rows at or
+// beyond `nrows` re-read row nrows-1 (varlen: never read past the sequence / buffer end;
+// those rows are masked out of every product).
+DEV void stage_tile(char* lds, const bf16_t* src, long ld, int tid, int nrows = 64) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int id = i * 256 + tid;
     const int r = id >> 3, c = id & 7;
-    const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)r * ld + c * 8);
+    const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)min(r, nrows - 1) * ld + c * 8);
     *reinterpret_cast<uint4*>(lds + tile_off(r, c)) = v;
   }
 }
@@ -101,7 +103,24 @@ struct AttnArgs {
   float drop_scale;     // 1/(1-p)
   int B, S, H;
   float scale;          // 1/sqrt(64)
+  const int* cu;        // varlen: int32 [B+1] packed sequence starts (nullable = padded [B*S] layout)
 };
+
+// Sequence b's first packed row and length.  Padded layout: b*S and S (keys masked by kbias).
+DEV void seq_span(const AttnArgs& a, int b, int& tok0, int& len) {
+  if (a.cu) {
+    tok0 = a.cu[b];
+    len = a.cu[b + 1] - tok0;
+  } else {
+    tok0 = b * a.S;
+    len = a.S;
+  }
+}
+// Additive key mask: kbias (padded layout) or k < len (varlen).
+DEV float key_bias(const AttnArgs& a, int tok0, int len, int k) {
+  if (a.cu) return k < len ? 0.f : -INFINITY;
+  return a.kbias[tok0 + k];
+}
 
 DEV uint32_t site_seed(const AttnArgs& a) { return hash32(a.seed_ptr ? a.seed_ptr[0] : 0u, a.site); }
 
@@ -114,14 +133,18 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  int tok0i, len;
+  seq_span(a, b, tok0i, len);
+  if (blockIdx.x * 64 >= len) return;  // varlen: query tile past the sequence (whole block)
   const int q = blockIdx.x * 64 + w * 16 + (lane & 15);
-  const size_t tok0 = (size_t)b * S;
+  const int qr = min(q, len - 1);       // row actually read
+  const size_t tok0 = (size_t)tok0i;
   const uint32_t seed = site_seed(a);
   const bool drop = a.drop_threshold != 0;
 
   bf16x8 qf[2];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) qf[s] = load_frag_global(a.qkv + (tok0 + q) * ld3 + h * DH + 32 * s + 8 * g);
+  for (int s = 0; s < 2; ++s) qf[s] = load_frag_global(a.qkv + (tok0 + qr) * ld3 + h * DH + 32 * s + 8 * g);
 
   f32x4 o[4];
 #pragma unroll
@@ -129,13 +152,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   float m = -INFINITY, l = 0.f;
   const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
 
-  for (int k0 = 0; k0 < S; k0 += 64) {
+  for (int k0 = 0; k0 < len; k0 += 64) {
     // Padding-aware: a key tile whose 64 keys are all masked contributes exp(-inf) = 0
     // to every row -- skip it (exact).  The barrier also retires the previous tile's reads.
-    const float kbv = a.kbias[tok0 + k0 + (tid & 63)];
+    const float kbv = key_bias(a, tok0i, len, k0 + (tid & 63));
     if (!__syncthreads_or(kbv != -INFINITY)) continue;
-    stage_tile(ks, a.qkv + (tok0 + k0) * ld3 + D + h * DH, ld3, tid);
-    stage_tile(vs, a.qkv + (tok0 + k0) * ld3 + 2 * D + h * DH, ld3, tid);
+    stage_tile(ks, a.qkv + (tok0 + k0) * ld3 + D + h * DH, ld3, tid, len - k0);
+    stage_tile(vs, a.qkv + (tok0 + k0) * ld3 + 2 * D + h * DH, ld3, tid, len - k0);
     if (tid < 64) kb[tid] = kbv;
     __syncthreads();
 
@@ -186,6 +209,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   const float inv = 1.f / l;
+  if (q >= len) return;  // varlen tail rows of the last query tile belong to the next sequence
   bf16_t* out = a.ctx + (tok0 + q) * D + h * DH;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
@@ -224,42 +248,46 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  int tok0i, len;
+  seq_span(a, b, tok0i, len);
+  if (blockIdx.x * 64 >= len) return;
   const int q = blockIdx.x * 64 + w * 16 + (lane & 15);
-  const size_t tok0 = (size_t)b * S;
+  const int qr = min(q, len - 1);
+  const size_t tok0 = (size_t)tok0i;
   const uint32_t seed = site_seed(a);
   const bool drop = a.drop_threshold != 0;
 
   bf16x8 qf[2], dof[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    qf[s] = load_frag_global(a.qkv + (tok0 + q) * ld3 + h * DH + 32 * s + 8 * g);
-    dof[s] = load_frag_global(a.dctx + (tok0 + q) * D + h * DH + 32 * s + 8 * g);
+    qf[s] = load_frag_global(a.qkv + (tok0 + qr) * ld3 + h * DH + 32 * s + 8 * g);
+    dof[s] = load_frag_global(a.dctx + (tok0 + qr) * D + h * DH + 32 * s + 8 * g);
   }
   const size_t st = ((size_t)b * H + h) * S + q;
-  const float lse = a.lse[st];
+  const float lse = a.lse[((size_t)b * H + h) * S + qr];
   // FA2 preprocessing fused in: delta = rowsum(dO * O) for this query; the dK/dV
   // kernel (launched after this one) reads it back.
   float dl = 0.f;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const bf16x8 of = load_frag_global(a.ctx + (tok0 + q) * D + h * DH + 32 * s + 8 * g);
+    const bf16x8 of = load_frag_global(a.ctx + (tok0 + qr) * D + h * DH + 32 * s + 8 * g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)of[j]) * bf2f((uint16_t)dof[s][j]);
   }
   dl += __shfl_xor(dl, 16, 64);
   dl += __shfl_xor(dl, 32, 64);
-  if (g == 0) const_cast<float*>(a.delta)[st] = dl;
+  if (g == 0 && q < len) const_cast<float*>(a.delta)[st] = dl;
   const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
 
   f32x4 dq[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = 0; k0 < S; k0 += 64) {
-    const float kbv = a.kbias[tok0 + k0 + (tid & 63)];
+  for (int k0 = 0; k0 < len; k0 += 64) {
+    const float kbv = key_bias(a, tok0i, len, k0 + (tid & 63));
     if (!__syncthreads_or(kbv != -INFINITY)) continue;  // fully masked key tile: dS = 0 (exact skip)
-    stage_tile(ks, a.qkv + (tok0 + k0) * ld3 + D + h * DH, ld3, tid);
-    stage_tile(vs, a.qkv + (tok0 + k0) * ld3 + 2 * D + h * DH, ld3, tid);
+    stage_tile(ks, a.qkv + (tok0 + k0) * ld3 + D + h * DH, ld3, tid, len - k0);
+    stage_tile(vs, a.qkv + (tok0 + k0) * ld3 + 2 * D + h * DH, ld3, tid, len - k0);
     if (tid < 64) kb[tid] = kbv;
     __syncthreads();
 
@@ -292,6 +320,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
       for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(tr_frag(ks, 16 * dt, kk, lane), df, dq[dt]);
     }
   }
+  if (q >= len) return;
   bf16_t* out = a.dqkv + (tok0 + q) * ld3 + h * DH;
   const float sc = a.scale;
 #pragma unroll
@@ -310,18 +339,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  int tok0i, len;
+  seq_span(a, b, tok0i, len);
+  if (blockIdx.x * 64 >= len) return;  // varlen: key tile past the sequence (writes nothing)
   const int key = blockIdx.x * 64 + w * 16 + (lane & 15);
-  const size_t tok0 = (size_t)b * S;
+  const int kr = min(key, len - 1);
+  const size_t tok0 = (size_t)tok0i;
   const uint32_t seed = site_seed(a);
   const bool drop = a.drop_threshold != 0;
 
   bf16x8 kf[2], vf[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    kf[s] = load_frag_global(a.qkv + (tok0 + key) * ld3 + D + h * DH + 32 * s + 8 * g);
-    vf[s] = load_frag_global(a.qkv + (tok0 + key) * ld3 + 2 * D + h * DH + 32 * s + 8 * g);
+    kf[s] = load_frag_global(a.qkv + (tok0 + kr) * ld3 + D + h * DH + 32 * s + 8 * g);
+    vf[s] = load_frag_global(a.qkv + (tok0 + kr) * ld3 + 2 * D + h * DH + 32 * s + 8 * g);
   }
-  const float kbias = a.kbias[tok0 + key];
+  const float kbias = key_bias(a, tok0i, len, key);
   bf16_t* outk = a.dqkv + (tok0 + key) * ld3 + D + h * DH;
   bf16_t* outv = a.dqkv + (tok0 + key) * ld3 + 2 * D + h * DH;
   if (!__syncthreads_or(kbias != -INFINITY)) {
@@ -343,12 +376,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
     dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  for (int q0 = 0; q0 < S; q0 += 64) {
+  for (int q0 = 0; q0 < len; q0 += 64) {
     __syncthreads();
-    stage_tile(qs, a.qkv + (tok0 + q0) * ld3 + h * DH, ld3, tid);
-    stage_tile(os, a.dctx + (tok0 + q0) * D + h * DH, D, tid);
-    if (tid < 64) lse_s[tid] = a.lse[st0 + q0 + tid];
-    else if (tid < 128) dl_s[tid - 64] = a.delta[st0 + q0 + tid - 64];
+    stage_tile(qs, a.qkv + (tok0 + q0) * ld3 + h * DH, ld3, tid, len - q0);
+    stage_tile(os, a.dctx + (tok0 + q0) * D + h * DH, D, tid, len - q0);
+    // query rows past the sequence: lse = +inf makes their P (and dS) exactly 0
+    if (tid < 64) lse_s[tid] = q0 + tid < len ? a.lse[st0 + q0 + tid] : INFINITY;
+    else if (tid < 128) dl_s[tid - 64] = q0 + tid - 64 < len ? a.delta[st0 + q0 + tid - 64] : 0.f;
     __syncthreads();
 
     f32x4 sc[4], dp[4];
@@ -390,6 +424,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
     }
   }
   const float sc = a.scale;
+  if (key >= len) return;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
     *reinterpret_cast<uint2*>(outk + 16 * dt + 4 * g) =
@@ -410,10 +445,11 @@ __global__ __launch_bounds__(256) void mask_to_bias_kernel(const M* mask, float*
 extern "C" {
 
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
-                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale,
+                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
                 hipStream_t st) {
   if (S % 64 != 0) return 1;
   AttnArgs a{};
+  a.cu = cu;
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f;
@@ -423,10 +459,11 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
 
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse,
                 const void* dctx, float* delta, void* dqkv, int B, int S, int H,
-                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale,
+                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
                 hipStream_t st) {
   if (S % 64 != 0) return 1;
   AttnArgs a{};
+  a.cu = cu;
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = (float*)lse;
   a.dctx = (const bf16_t*)dctx; a.delta = delta; a.dqkv = (bf16_t*)dqkv;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;

@@ -15,6 +15,8 @@
 // the reference's four host syncs per eval batch.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 struct HeadArgs {
@@ -164,6 +166,18 @@ struct AdamArgs {
   const unsigned char* now;         // rows with a valid gradient this step (nullable = all)
 };
 
+// NT: the moments (and the gradient) are touched once per step -> stream them with
+// nontemporal loads/stores so they do not evict the weights / bf16 shadow the next
+// forward re-reads from L2 / MALL.
+DEV float4 ld_nt(const float4* p) {
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+DEV void st_nt(float4* p, float4 v) {
+  __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
+}
+
+template <bool NT>
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const int t = a.step[0];
   const float bc1 = 1.f - powf(a.b1, (float)t);
@@ -180,9 +194,16 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
       gvalid = a.now == nullptr || a.now[row] != 0;
     }
     float4 p = reinterpret_cast<float4*>(a.p)[i];
-    float4 g = gvalid ? reinterpret_cast<const float4*>(a.g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 m = reinterpret_cast<float4*>(a.m)[i];
-    float4 v = reinterpret_cast<float4*>(a.v)[i];
+    float4 g, m, v;
+    if constexpr (NT) {
+      g = gvalid ? ld_nt(reinterpret_cast<const float4*>(a.g) + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      m = ld_nt(reinterpret_cast<const float4*>(a.m) + i);
+      v = ld_nt(reinterpret_cast<const float4*>(a.v) + i);
+    } else {
+      g = gvalid ? reinterpret_cast<const float4*>(a.g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      m = reinterpret_cast<float4*>(a.m)[i];
+      v = reinterpret_cast<float4*>(a.v)[i];
+    }
     float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
     float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -198,8 +219,13 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
       pp[e] -= step_size * mm[e] / denom;
     }
     reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-    reinterpret_cast<float4*>(a.m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
-    reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    if constexpr (NT) {
+      st_nt(reinterpret_cast<float4*>(a.m) + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
+      st_nt(reinterpret_cast<float4*>(a.v) + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
+    } else {
+      reinterpret_cast<float4*>(a.m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+      reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    }
     if (a.shadow)
       reinterpret_cast<uint2*>(a.shadow)[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
   }
@@ -280,7 +306,11 @@ int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long lon
   if (wd != 0.f && touched) return 3;  // skipping untouched rows is exact only without weight decay
   AdamArgs a{p, g, m, v, (bf16_t*)shadow, n / 4, step, lr, b1, b2, eps, wd, decoupled,
              skip_off / 4, (skip_off + skip_rows * row_len) / 4, row_len / 4, touched, now};
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, a);
+  static const bool nt = [] { const char* e = getenv("FD_ADAM_NT"); return e ? atoi(e) != 0 : true; }();
+  if (nt)
+    hipLaunchKernelGGL(adam_kernel<true>, dim3(grid_for(n / 4)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(adam_kernel<false>, dim3(grid_for(n / 4)), dim3(256), 0, st, a);
   return 0;
 }
 

@@ -33,6 +33,9 @@ struct LnArgs {
   bf16_t* dz;           // grad of the pre-LN sum (residual grad)
   bf16_t* dx;           // grad of the primary input through dropout (nullable if no dropout)
   float* part;          // [gridDim.x][3][D]: dgamma, dbeta, dbias partials
+  // packed (unpadded) rows: row -> row of the padded [B*S] layout, used only to index the
+  // dropout hash so a packed batch draws exactly the padded batch's masks (nullable)
+  const int* row_map;
 };
 
 // Half-wave row layout for D = 768: 32 lanes own a row, lane hl holds columns
@@ -64,9 +67,10 @@ DEV void ln_load_sum(const LnArgs& a, int row, int hl, bool drop, uint32_t seed,
     if (a.r) rv[c] = *reinterpret_cast<const uint4*>(a.r + off);
   }
   keep = 0xffffffu;
+  const size_t hrow = a.row_map ? (size_t)(unsigned)a.row_map[row] : (size_t)row;  // dropout-hash row
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
-    const size_t off = (size_t)row * a.D + 8 * (hl + HL * c);
+    const size_t off = hrow * a.D + 8 * (hl + HL * c);
     unpack8(xv[c], z[c]);
     if (drop) {
 #pragma unroll
@@ -561,12 +565,12 @@ extern "C" {
 
 int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, float* mean,
               float* rstd, int T, int D, float eps, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
-              float dscale, hipStream_t st) {
+              float dscale, const int* row_map, hipStream_t st) {
   if (D != 768) return 1;
   LnArgs a{};
   a.x = (const bf16_t*)x; a.r = (const bf16_t*)r; a.gamma = gamma; a.beta = beta; a.y = (bf16_t*)y;
   a.mean = mean; a.rstd = rstd; a.T = T; a.D = D; a.eps = eps;
-  a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
+  a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.row_map = row_map;
   hipLaunchKernelGGL(ln_fwd_kernel, dim3((T + 7) / 8), dim3(256), 0, st, a);
   return 0;
 }
@@ -576,12 +580,12 @@ int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* bet
 int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean,
               const float* rstd, void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work,
               int T, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
-              int accumulate, hipStream_t st) {
+              int accumulate, const int* row_map, hipStream_t st) {
   if (D != 768) return 1;
   LnArgs a{};
   a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.r = (const bf16_t*)r; a.gamma = gamma;
   a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = (bf16_t*)dz; a.dx = (bf16_t*)dx; a.part = work;
-  a.T = T; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
+  a.T = T; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.row_map = row_map;
   const int grid = std::min(LN_GRID, (T + 15) / 16);
   hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
                      st, a);

@@ -52,6 +52,9 @@ class DeviceLoader:
         self.mask = dataset.attention_mask.to(self.device)
         self.labels = dataset.labels.to(self.device)
         self.n = len(dataset)
+        # host copy of the per-row real-token counts: every batch carries ``n_tokens`` (a
+        # Python int, no device sync) for the model's unpadded path
+        self.lengths = dataset.attention_mask.detach().to("cpu").sum(1).to(torch.int64)
         self.batch_size, self.shuffle, self.drop_last = batch_size, shuffle, drop_last
         self.gen = torch.Generator(device="cpu").manual_seed(seed)
         self.epoch = 0
@@ -63,18 +66,21 @@ class DeviceLoader:
 
     def __iter__(self):
         if self.shuffle:
-            perm = torch.randperm(self.n, generator=self.gen).to(self.device)
+            perm_cpu = torch.randperm(self.n, generator=self.gen)
+            perm = perm_cpu.to(self.device)
         else:
             perm = None
         self.epoch += 1
         for i in range(len(self)):
             lo, hi = i * self.batch_size, min(self.n, (i + 1) * self.batch_size)
             if perm is None:
-                yield {"input_ids": self.ids[lo:hi], "attention_mask": self.mask[lo:hi], "labels": self.labels[lo:hi]}
+                yield {"input_ids": self.ids[lo:hi], "attention_mask": self.mask[lo:hi], "labels": self.labels[lo:hi],
+                       "n_tokens": int(self.lengths[lo:hi].sum())}
             else:
                 idx = perm[lo:hi]
                 yield {"input_ids": self.ids.index_select(0, idx), "attention_mask": self.mask.index_select(0, idx),
-                       "labels": self.labels.index_select(0, idx)}
+                       "labels": self.labels.index_select(0, idx),
+                       "n_tokens": int(self.lengths[perm_cpu[lo:hi]].sum())}
 
 
 @dataclass

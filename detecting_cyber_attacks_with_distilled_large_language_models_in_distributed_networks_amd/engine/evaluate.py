@@ -35,8 +35,12 @@ def evaluate_model(model, loader, criterion=None, device=None, log=None, name: s
         from ..ops import kernels as K
         acc = torch.zeros(1, dtype=torch.float64, device=dev)
         counts = torch.zeros(5, dtype=torch.int64, device=dev)
+        packed = getattr(model, "impl", None) == "hip"
         for batch in loader:
-            logits = model(batch["input_ids"], batch["attention_mask"])
+            if packed and batch.get("n_tokens") is not None:  # unpadded blocks (no host sync)
+                logits = model(batch["input_ids"], batch["attention_mask"], tokens=batch["n_tokens"])
+            else:
+                logits = model(batch["input_ids"], batch["attention_mask"])
             b = logits.shape[0]
             lab = batch["labels"]
             K.eval_metrics(logits, lab, acc, counts, probs[off:off + b], preds[off:off + b])

@@ -11,6 +11,13 @@ on the real batches, and they populate allocator pools / workspaces); the next
 call captures, then replays the capture for its own batch.  Batches whose shape
 differs from the captured one (the last partial batch, drop_last=False) run
 eagerly.
+
+Unpadded model path: a batch also carries its real-token count; ``bucket(tokens,
+B, S)`` (the model's ``packed_rows``) maps it to the packed row count the step
+is shaped by, and one graph is captured per (batch shape, bucket) -- a handful
+for CICIDS2017 text (76-86 real tokens of 128).  Inside a graph everything that
+depends on the actual batch (row maps, sequence starts) is computed on device
+from the mask, so any batch of the same bucket replays it.
 """
 from __future__ import annotations
 
@@ -20,49 +27,61 @@ import torch
 
 
 class GraphedTrainStep:
-    def __init__(self, step_fn: Callable[[torch.Tensor, torch.Tensor, torch.Tensor], torch.Tensor],
-                 warmup: int = 2, enabled: bool = True):
+    def __init__(self, step_fn: Callable[..., torch.Tensor], warmup: int = 2, enabled: bool = True,
+                 bucket: Optional[Callable[[int, int, int], int]] = None, max_graphs: int = 8):
         self.step_fn = step_fn
         self.warmup = warmup
         self.enabled = enabled and torch.cuda.is_available()
+        self.bucket = bucket
+        self.max_graphs = max_graphs
         self.calls = 0
-        self.graph: Optional[torch.cuda.CUDAGraph] = None
-        self.shape = None
-        self.static: Dict[str, torch.Tensor] = {}
-        self.static_loss: Optional[torch.Tensor] = None
+        self.graphs: Dict[tuple, tuple] = {}  # key -> (graph, static inputs, static loss)
         self.failed: Optional[str] = None
 
-    def __call__(self, ids: torch.Tensor, mask: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    @property
+    def graph(self) -> Optional[torch.cuda.CUDAGraph]:
+        """The first captured graph (None until a capture succeeded)."""
+        return next(iter(self.graphs.values()))[0] if self.graphs else None
+
+    def _key(self, ids, tokens):
+        if tokens is None or self.bucket is None:
+            return tuple(ids.shape), None
+        B, S = ids.shape[0], ids.shape[1]
+        return tuple(ids.shape), int(self.bucket(tokens, B, S))
+
+    def __call__(self, ids: torch.Tensor, mask: torch.Tensor, labels: torch.Tensor,
+                 tokens: Optional[int] = None) -> torch.Tensor:
         self.calls += 1
         if not self.enabled or self.failed:
-            return self.step_fn(ids, mask, labels)
-        if self.graph is not None:
-            if ids.shape != self.shape:
-                return self.step_fn(ids, mask, labels)
-            self.static["ids"].copy_(ids)
-            self.static["mask"].copy_(mask)
-            self.static["labels"].copy_(labels)
-            self.graph.replay()
-            return self.static_loss
-        if self.calls <= self.warmup:
+            return self.step_fn(ids, mask, labels, tokens)
+        key = self._key(ids, tokens)
+        hit = self.graphs.get(key)
+        if hit is not None:
+            g, static, loss = hit
+            static["ids"].copy_(ids)
+            static["mask"].copy_(mask)
+            static["labels"].copy_(labels)
+            g.replay()
+            return loss
+        if self.calls <= self.warmup or len(self.graphs) >= self.max_graphs:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                loss = self.step_fn(ids, mask, labels)
+                loss = self.step_fn(ids, mask, labels, tokens)
             torch.cuda.current_stream().wait_stream(s)
             return loss
-        # capture
-        self.shape = ids.shape
-        self.static = {"ids": ids.clone(), "mask": mask.clone(), "labels": labels.clone()}
+        # capture (the bucket's own row count stands in for the batch's token count:
+        # every device-side quantity is recomputed from the mask on each replay)
+        static = {"ids": ids.clone(), "mask": mask.clone(), "labels": labels.clone()}
         g = torch.cuda.CUDAGraph()
         try:
             torch.cuda.synchronize()
             with torch.cuda.graph(g):
-                self.static_loss = self.step_fn(self.static["ids"], self.static["mask"], self.static["labels"])
+                loss = self.step_fn(static["ids"], static["mask"], static["labels"], key[1])
         except Exception as e:  # pragma: no cover - capture support varies by op
             self.failed = f"{type(e).__name__}: {e}"
             torch.cuda.synchronize()
-            return self.step_fn(ids, mask, labels)
-        self.graph = g
+            return self.step_fn(ids, mask, labels, tokens)
+        self.graphs[key] = (g, static, loss)
         g.replay()
-        return self.static_loss
+        return loss

@@ -20,12 +20,12 @@ from .graph import GraphedTrainStep
 def make_step_fn(model, optimizer, criterion=None):
     fused = criterion is None or isinstance(criterion, torch.nn.CrossEntropyLoss)
 
-    def step(ids, mask, labels):
+    def step(ids, mask, labels, tokens=None):
         optimizer.zero_grad()
         if fused:
-            loss, _ = model.forward_loss(ids, mask, labels)
+            loss, _ = model.forward_loss(ids, mask, labels, tokens=tokens)
         else:
-            loss = criterion(model(ids, mask), labels)
+            loss = criterion(model(ids, mask, tokens=tokens), labels)
         loss.backward()
         optimizer.step()
         return loss.detach()
@@ -38,11 +38,11 @@ def make_kd_step_fn(student, teacher, optimizer, temperature: float = 2.0, alpha
     alpha * CE + (1 - alpha) * T^2 * KL(teacher || student) -> backward -> Adam."""
     from ..models.bert import kd_loss
 
-    def step(ids, mask, labels):
+    def step(ids, mask, labels, tokens=None):
         optimizer.zero_grad()
         with torch.no_grad():
-            t_logits = teacher(ids, mask)
-        s_logits = student(ids, mask)
+            t_logits = teacher(ids, mask, tokens=tokens)
+        s_logits = student(ids, mask, tokens=tokens)
         loss = kd_loss(s_logits, t_logits, labels, temperature, alpha)
         loss.backward()
         optimizer.step()
@@ -73,7 +73,8 @@ def train_model(model, train_loader, criterion=None, optimizer=None, num_epochs:
         fn = make_dp_step_fn(model, optimizer, grad_sync)
     else:
         fn = make_step_fn(model, optimizer, criterion)
-    step = GraphedTrainStep(fn, enabled=use_graph and model.device.type == "cuda")
+    step = GraphedTrainStep(fn, enabled=use_graph and model.device.type == "cuda",
+                            bucket=getattr(model, "packed_rows", None))
     epoch_losses: List[float] = []
     steps = 0
     t0 = time.perf_counter()
@@ -85,7 +86,7 @@ def train_model(model, train_loader, criterion=None, optimizer=None, num_epochs:
         for batch in train_loader:
             if grad_sync is not None:
                 grad_sync.set_loss_scale(batch.get("loss_scale", 1.0))
-            loss = step(batch["input_ids"], batch["attention_mask"], batch["labels"])
+            loss = step(batch["input_ids"], batch["attention_mask"], batch["labels"], batch.get("n_tokens"))
             loss_sum += loss
             nb += 1
             steps += 1

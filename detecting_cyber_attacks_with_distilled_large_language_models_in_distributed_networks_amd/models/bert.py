@@ -80,9 +80,9 @@ class BertTeacherClassifier(DDoSClassifier):
         emb["pos"] = (pos32 + self.token_type_embeddings[0].detach()).to(torch.bfloat16).contiguous()
         return emb, layers, head
 
-    def _run_hip(self, ids, mask, labels):
+    def _run_hip(self, ids, mask, labels, tokens=None):
         self._hip_cache = None  # the folded table follows the (possibly updated) weights
-        return super()._run_hip(ids, mask, labels)
+        return super()._run_hip(ids, mask, labels, tokens)
 
     def _run_torch(self, ids, mask, labels):
         with torch.no_grad():

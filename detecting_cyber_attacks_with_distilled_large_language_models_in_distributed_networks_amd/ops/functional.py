@@ -46,6 +46,11 @@ class RunCtx:
     # launch the weight gradients that become ready together (lin2 + lin1, out_lin + qkv)
     # as one grouped GEMM grid (fewer split-K slab round trips; csrc/kernels/gemm.hip)
     group_dw: bool = True
+    # unpadded (packed) token layout: the transformer blocks run on the batch's real
+    # tokens only.  cu = int32 [B+1] sequence starts (varlen attention), row_map = int32
+    # [rows] packed -> padded row (-1 for the bucket's filler rows; dropout-hash index).
+    cu: Optional[torch.Tensor] = None
+    row_map: Optional[torch.Tensor] = None
 
 
 class _WGrad:
@@ -118,12 +123,12 @@ class LayerFn(torch.autograd.Function):
         p_h = rc.p_hidden if rc.training else 0.0
         attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
         qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
-        cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a)
+        cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu)
         ao = K.linear_fwd(cx, L["o_w"], L["o_b"])
         h, m1, r1 = K.ln_fwd(ao, x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0)
         g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
         f = K.linear_fwd(g, L["l2_w"], L["l2_b"])
-        y, m2, r2 = K.ln_fwd(f, h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed, ffn_site, p_h)
+        y, m2, r2 = K.ln_fwd(f, h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed, ffn_site, p_h, rc.row_map)
         if ctx.needs_input_grad[0]:
             ctx.save_for_backward(x)
             ctx.acts = (qkv, cx, lse, ao, h, m1, r1, u, g, f, m2, r2)
@@ -142,7 +147,7 @@ class LayerFn(torch.autograd.Function):
         wg = _WGrad(rc)  # dW / bias-sum work -> side stream, dX chain stays on the main stream
         # output_layer_norm(dropout(lin2) + h): dz2 -> residual grad of h, df -> lin2 output grad
         dz2, df = K.ln_bwd(dy, f, h, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, rc.seed,
-                           ffn_site, p_h, acc)
+                           ffn_site, p_h, acc, rc.row_map)
         wt = L.get("wT") or {}
         du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"))  # dg W2 * gelu'(u)
         wg.fork(df, g, du, h)
@@ -162,7 +167,7 @@ class LayerFn(torch.autograd.Function):
             wg.fork(dz1, cx)
             with wg.ctx():
                 K.linear_dw(dz1, cx, G["o_w"].buf, acc)
-        dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a)
+        dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu)
         wg.fork(dqkv, x, dz1, cx)
         with wg.ctx():
             if rc.group_dw:

@@ -111,41 +111,46 @@ def mask_bias(mask: torch.Tensor) -> torch.Tensor:
     return bias
 
 
-def attn_fwd(qkv, kbias, B, S, H, seed, site, p) -> Tuple[torch.Tensor, torch.Tensor]:
-    ctx = torch.empty(B * S, H * 64, dtype=torch.bfloat16, device=qkv.device)
+def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """cu (int32 [B+1]): varlen mode -- qkv/ctx hold packed sequences (rows cu[b]..cu[b+1]-1);
+    rows past cu[B] are zero in ctx (the kernels never write them)."""
+    rows = qkv.shape[0] if cu is not None else B * S
+    alloc = torch.zeros if cu is not None else torch.empty
+    ctx = alloc(rows, H * 64, dtype=torch.bfloat16, device=qkv.device)
     lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
     thr, sc = _drop(p)
-    ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc)
+    ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu)
     return ctx, lse
 
 
-def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p) -> torch.Tensor:
-    dqkv = torch.empty_like(qkv)
+def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None) -> torch.Tensor:
+    dqkv = torch.zeros_like(qkv) if cu is not None else torch.empty_like(qkv)
     delta = workspace(qkv.device, "attn_delta", B * H * S)
     thr, sc = _drop(p)
-    ext().attn_bwd(qkv, kbias, ctx, lse, dctx.contiguous(), delta, dqkv, B, S, H, seed, site, thr, sc)
+    ext().attn_bwd(qkv, kbias, ctx, lse, dctx.contiguous(), delta, dqkv, B, S, H, seed, site, thr, sc, cu)
     return dqkv
 
 
 # ------------------------------------------------------------------ layernorm / embedding
-def ln_fwd(x, r, gamma, beta, eps, seed, site, p):
+def ln_fwd(x, r, gamma, beta, eps, seed, site, p, row_map=None):
+    """row_map (int32 [T]): packed row -> padded row, for the dropout hash only."""
     T = x.numel() // gamma.numel()
     y = torch.empty_like(x)
     mean = torch.empty(T, dtype=torch.float32, device=x.device)
     rstd = torch.empty(T, dtype=torch.float32, device=x.device)
     thr, sc = _drop(p)
-    ext().ln_fwd(x, r, gamma, beta, y, mean, rstd, eps, seed, site, thr, sc)
+    ext().ln_fwd(x, r, gamma, beta, y, mean, rstd, eps, seed, site, thr, sc, row_map if thr else None)
     return y, mean, rstd
 
 
-def ln_bwd(dy, x, r, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False):
+def ln_bwd(dy, x, r, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False, row_map=None):
     D = gamma.numel()
     dz = torch.empty_like(x)
     thr, sc = _drop(p)
     dx = torch.empty_like(x) if thr else None
     ws = workspace(x.device, "ln_part", LN_GRID * 3 * D)
     ext().ln_bwd(dy.contiguous(), x, r, gamma, mean, rstd, dz, dx, dgamma, dbeta, dbias, ws, seed, site, thr, sc,
-                 accumulate)
+                 accumulate, row_map if thr else None)
     return dz, (dx if dx is not None else dz)
 
 

@@ -106,7 +106,7 @@ class DPShardLoader:
             n = b["labels"].shape[0]
             if n < self.k:
                 continue
-            parts = {key: torch.tensor_split(v, self.k)[self.dp_rank] for key, v in b.items()}
+            parts = {key: torch.tensor_split(v, self.k)[self.dp_rank] for key, v in b.items() if torch.is_tensor(v)}
             parts["loss_scale"] = parts["labels"].shape[0] / n
             yield parts
 
@@ -203,7 +203,7 @@ def make_dp_step_fn(model, optimizer, sync: GradSync):
     if getattr(optimizer, "overlap", False):
         raise ValueError("data-parallel clients need ArenaAdam(overlap=False)")
 
-    def step(ids, mask, labels):
+    def step(ids, mask, labels, tokens=None):  # shards run the padded path (no per-shard token count)
         optimizer.zero_grad()
         loss, _ = model.forward_loss(ids, mask, labels)
         scaled = loss * sync.loss_scale

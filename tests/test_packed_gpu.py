@@ -1,0 +1,106 @@
+"""Unpadded (packed-token) HIP path == padded path.
+
+Padding positions never reach a real token (keys are masked) or the loss (the
+head reads [CLS]), so running the transformer blocks on the real tokens only is
+the same math.  The packed path also hashes dropout by the padded row, so even
+with dropout on the two paths draw identical masks.
+"""
+import pytest
+import torch
+
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.engine import (
+    ArenaAdam, GraphedTrainStep, make_step_fn)
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.models import (
+    DDoSClassifier, DistilBertConfig)
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(B, S, lo, hi, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(1000, 2000, (B, S), generator=g)
+    lens = torch.randint(lo, hi + 1, (B,), generator=g)
+    mask = (torch.arange(S)[None] < lens[:, None]).long()
+    ids = ids * mask
+    ids[:, 0] = 101
+    labels = torch.randint(0, 2, (B,), generator=g)
+    return ids.cuda(), mask.cuda(), labels.cuda(), int(lens.sum())
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-8)).item()
+
+
+def test_varlen_attention_matches_padded():
+    B, S, H = 6, 128, 12
+    g = torch.Generator(device="cuda").manual_seed(1)
+    lens = torch.tensor([128, 77, 64, 1, 100, 65])
+    qkv_pad = (torch.randn(B * S, 3 * H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    mask = (torch.arange(S)[None] < lens[:, None]).cuda()
+    kb = K.mask_bias(mask.to(torch.int64))
+    seed = torch.tensor([7], dtype=torch.int32, device="cuda")
+    idx = torch.nonzero(mask.reshape(-1)).squeeze(1)
+    cu = torch.zeros(B + 1, dtype=torch.int32, device="cuda")
+    cu[1:] = torch.cumsum(lens, 0).to(torch.int32).cuda()
+    qkv = torch.cat([qkv_pad.index_select(0, idx), torch.zeros(64, 3 * H * 64, dtype=torch.bfloat16,
+                                                                 device="cuda")])  # + filler rows
+    for p in (0.0, 0.1):
+        ctx_p, lse_p = K.attn_fwd(qkv_pad, kb, B, S, H, seed, 40, p)
+        ctx_v, lse_v = K.attn_fwd(qkv, kb, B, S, H, seed, 40, p, cu=cu)
+        n = int(cu[-1])
+        assert torch.equal(ctx_v[:n], ctx_p.index_select(0, idx))
+        assert not ctx_v[n:].any()  # filler rows untouched (zero)
+        dctx_pad = (torch.randn(B * S, H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+        dctx_pad = dctx_pad * mask.reshape(-1, 1)  # padding rows carry no gradient
+        dctx = torch.cat([dctx_pad.index_select(0, idx), torch.zeros(64, H * 64, dtype=torch.bfloat16, device="cuda")])
+        d_p = K.attn_bwd(qkv_pad, kb, ctx_p, lse_p, dctx_pad, B, S, H, seed, 40, p)
+        d_v = K.attn_bwd(qkv, kb, ctx_v, lse_v, dctx, B, S, H, seed, 40, p, cu=cu)
+        assert rel(d_v[:n], d_p.index_select(0, idx)) < 1e-6
+        assert not d_v[n:].any()
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_packed_model_matches_padded(train):
+    cfg = DistilBertConfig(n_layers=2)
+    m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=4)
+    m.train(train)
+    ids, mask, labels, tokens = _batch(16, 128, 70, 90)
+    assert m.packed_rows(tokens, 16, 128) < 16 * 128
+    outs = []
+    for tok in (None, tokens):
+        m.rng.zero_()
+        m.zero_grad()
+        loss, logits = m.forward_loss(ids, mask, labels, tokens=tok)
+        loss.backward()
+        torch.cuda.synchronize()
+        outs.append((loss.detach().clone(), logits.clone(), m.arena.grad.clone(), m.emb_now.clone()))
+    (l0, z0, g0, e0), (l1, z1, g1, e1) = outs
+    assert rel(z1, z0) < 1e-3 and abs(float(l1 - l0)) < 1e-3
+    assert torch.equal(e0, e1)
+    dense = torch.ones_like(g0, dtype=torch.bool)
+    woff, V, D = m.word_embedding_span()
+    dense[woff:woff + V * D] = False
+    assert rel(g1[dense], g0[dense]) < 2e-2
+    rows = e0.bool()
+    assert rel(g1[woff:woff + V * D].view(V, D)[rows], g0[woff:woff + V * D].view(V, D)[rows]) < 2e-2
+
+
+def test_packed_graph_buckets_match_eager():
+    """Graph replays across batches of different real-token counts (one graph per bucket)
+    track the eager packed path step for step."""
+    cfg = DistilBertConfig(n_layers=2)
+    models = [DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=6) for _ in range(2)]
+    steps = []
+    for m, graph in zip(models, (True, False)):
+        m.train()
+        steps.append(GraphedTrainStep(make_step_fn(m, ArenaAdam(m, lr=1e-3)), warmup=1, enabled=graph,
+                                      bucket=m.packed_rows))
+    for it in range(6):
+        lo, hi = ((40, 60), (70, 90), (40, 60))[it % 3]
+        ids, mask, labels, tokens = _batch(16, 128, lo, hi, seed=50 + it)
+        losses = [st(ids, mask, labels, tokens) for st in steps]
+        torch.cuda.synchronize()
+        assert abs(float(losses[0] - losses[1])) < 1e-5, it
+    assert len(steps[0].graphs) >= 2 and steps[0].failed is None
+    assert torch.equal(models[0].arena.master, models[1].arena.master)
