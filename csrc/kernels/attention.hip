@@ -104,7 +104,24 @@ struct AttnArgs {
   int B, S, H;
   float scale;          // 1/sqrt(64)
   const int* cu;        // varlen: int32 [B+1] packed sequence starts (nullable = padded [B*S] layout)
+  int rows;             // varlen: packed rows of qkv/ctx (rows cu[B] .. rows-1 are bucket filler)
 };
+
+// Varlen: the extra grid slice z == B zeroes head h's columns of the filler rows
+// (cu[B] .. rows-1) of `out` (`nsec` 64-wide sections, row stride ld): they are read by
+// the next GEMMs and must be finite, and no sequence block ever writes them.
+DEV void zero_filler(const AttnArgs& a, bf16_t* out, long ld, int nsec, int h) {
+  const int first = a.cu[a.B];
+  const int tid = threadIdx.x;
+  for (int r0 = first + blockIdx.x * 64; r0 < a.rows; r0 += gridDim.x * 64) {
+    for (int id = tid; id < 64 * nsec * 8; id += 256) {
+      const int r = r0 + id / (nsec * 8), c = id % (nsec * 8);
+      if (r < a.rows)
+        *reinterpret_cast<uint4*>(out + (size_t)r * ld + (size_t)(c >> 3) * (a.H * DH) + h * DH + (c & 7) * 8) =
+            make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+}
 
 // Sequence b's first packed row and length.  Padded layout: b*S and S (keys masked by kbias).
 DEV void seq_span(const AttnArgs& a, int b, int& tok0, int& len) {
@@ -133,6 +150,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  if (b == a.B) {  // varlen filler slice
+    zero_filler(a, a.ctx, D, 1, h);
+    return;
+  }
   int tok0i, len;
   seq_span(a, b, tok0i, len);
   if (blockIdx.x * 64 >= len) return;  // varlen: query tile past the sequence (whole block)
@@ -248,6 +269,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  if (b == a.B) {  // varlen filler slice: dq | dk | dv columns of head h
+    zero_filler(a, a.dqkv, ld3, 3, h);
+    return;
+  }
   int tok0i, len;
   seq_span(a, b, tok0i, len);
   if (blockIdx.x * 64 >= len) return;
@@ -446,29 +471,29 @@ extern "C" {
 
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                hipStream_t st) {
+                int rows, hipStream_t st) {
   if (S % 64 != 0) return 1;
   AttnArgs a{};
   a.cu = cu;
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
-  a.B = B; a.S = S; a.H = H; a.scale = 0.125f;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
+  a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
   return 0;
 }
 
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse,
                 const void* dctx, float* delta, void* dqkv, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                hipStream_t st) {
+                int rows, hipStream_t st) {
   if (S % 64 != 0) return 1;
   AttnArgs a{};
   a.cu = cu;
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = (float*)lse;
   a.dctx = (const bf16_t*)dctx; a.delta = delta; a.dqkv = (bf16_t*)dqkv;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
-  a.B = B; a.S = S; a.H = H; a.scale = 0.125f;
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
+  a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
   return 0;
 }

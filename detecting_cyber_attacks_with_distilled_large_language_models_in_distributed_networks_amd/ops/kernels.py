@@ -113,10 +113,9 @@ def mask_bias(mask: torch.Tensor) -> torch.Tensor:
 
 def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """cu (int32 [B+1]): varlen mode -- qkv/ctx hold packed sequences (rows cu[b]..cu[b+1]-1);
-    rows past cu[B] are zero in ctx (the kernels never write them)."""
+    the kernel zeroes ctx's filler rows past cu[B] itself."""
     rows = qkv.shape[0] if cu is not None else B * S
-    alloc = torch.zeros if cu is not None else torch.empty
-    ctx = alloc(rows, H * 64, dtype=torch.bfloat16, device=qkv.device)
+    ctx = torch.empty(rows, H * 64, dtype=torch.bfloat16, device=qkv.device)
     lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
     thr, sc = _drop(p)
     ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu)
@@ -124,7 +123,7 @@ def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None) -> Tuple[torch.Tensor,
 
 
 def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None) -> torch.Tensor:
-    dqkv = torch.zeros_like(qkv) if cu is not None else torch.empty_like(qkv)
+    dqkv = torch.empty_like(qkv)  # varlen: filler rows zeroed by the dQ kernel
     delta = workspace(qkv.device, "attn_delta", B * H * S)
     thr, sc = _drop(p)
     ext().attn_bwd(qkv, kbias, ctx, lse, dctx.contiguous(), delta, dqkv, B, S, H, seed, site, thr, sc, cu)
