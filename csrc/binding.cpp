@@ -41,7 +41,7 @@ int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* bet
 int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean,
               const float* rstd, void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work, int T,
               int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, int accumulate,
-              const int* row_map, hipStream_t st);
+              const int* row_map, int defer, hipStream_t st);
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, hipStream_t st);
@@ -50,7 +50,10 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
                int accumulate, unsigned char* now, unsigned char* ever, hipStream_t st);
-int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, hipStream_t st);
+int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, int defer, int* nblk_out,
+                   hipStream_t st);
+int fd_colsum_batched(int n, const float* const* parts, float* const* outs, const int* nblk, const int* stride,
+                      const int* D, const int* nout, const int* accumulate, hipStream_t st);
 int fd_rank_sort(const void* ids, int ids64, int T, long long* sorted, long long* perm, hipStream_t st);
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
@@ -327,7 +330,7 @@ void ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::T
             const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dz, const c10::optional<at::Tensor>& dx,
             const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
             const c10::optional<at::Tensor>& dbias, const at::Tensor& work, const at::Tensor& seed, int64_t site,
-            int64_t thr, double dscale, bool accumulate, const c10::optional<at::Tensor>& row_map) {
+            int64_t thr, double dscale, bool accumulate, const c10::optional<at::Tensor>& row_map, bool defer) {
   need(dy, at::kBFloat16, "dy");
   need(x, at::kBFloat16, "x");
   need_opt(r, at::kBFloat16, "r");
@@ -347,7 +350,7 @@ void ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::T
   check_rc(fd_ln_bwd(dy.data_ptr(), x.data_ptr(), ptr<void>(r), gamma.data_ptr<float>(), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), dz.data_ptr(), ptr<void>(dx), ptr<float>(dgamma), ptr<float>(dbeta),
                      ptr<float>(dbias), work.data_ptr<float>(), (int)T, (int)D, seedp(seed), (uint32_t)site,
-                     (uint32_t)thr, (float)dscale, accumulate ? 1 : 0, map_ptr(row_map, T), stream()),
+                     (uint32_t)thr, (float)dscale, accumulate ? 1 : 0, map_ptr(row_map, T), defer ? 1 : 0, stream()),
            "ln_bwd");
 }
 
@@ -419,15 +422,51 @@ void rank_sort(const at::Tensor& ids, const at::Tensor& sorted, const at::Tensor
            "rank_sort");
 }
 
-void colsum_bf16(const at::Tensor& x, const at::Tensor& out, const at::Tensor& work, bool accumulate) {
+// Returns the number of partial rows left in `work` (what a deferred job must reduce).
+int64_t colsum_bf16(const at::Tensor& x, const at::Tensor& out, const at::Tensor& work, bool accumulate, bool defer) {
   need(x, at::kBFloat16, "x");
   need(out, at::kFloat, "out");
   need(work, at::kFloat, "work");
   const int64_t N = out.numel(), T = x.numel() / N;
   TORCH_CHECK(T * N == x.numel() && work.numel() >= ((T + 31) / 32) * N, "colsum: sizes");
+  int nblk = 0;
   check_rc(fd_colsum_bf16(x.data_ptr(), (int)T, (int)N, out.data_ptr<float>(), work.data_ptr<float>(),
-                          accumulate ? 1 : 0, stream()),
+                          accumulate ? 1 : 0, defer ? 1 : 0, &nblk, stream()),
            "colsum_bf16");
+  return nblk;
+}
+
+// One launch finalising many deferred column sums: job i reduces parts[i] ([nblk][stride] fp32)
+// into outs[i][k] (k < 3, fp32 [D] or None) = sum over blocks of columns k*D .. k*D+D-1.
+void colsum_batched(const std::vector<at::Tensor>& parts, const std::vector<std::vector<c10::optional<at::Tensor>>>& outs,
+                    const std::vector<int64_t>& nblk, const std::vector<int64_t>& stride, const std::vector<int64_t>& D,
+                    const std::vector<int64_t>& accumulate) {
+  const size_t n = parts.size();
+  TORCH_CHECK(outs.size() == n && nblk.size() == n && stride.size() == n && D.size() == n && accumulate.size() == n,
+              "colsum_batched: ragged job lists");
+  std::vector<const float*> pp(n);
+  std::vector<float*> op(3 * n, nullptr);
+  std::vector<int> nb(n), sd(n), dd(n), no(n), ac(n);
+  for (size_t i = 0; i < n; ++i) {
+    need(parts[i], at::kFloat, "colsum part");
+    TORCH_CHECK(outs[i].size() >= 1 && outs[i].size() <= 3, "colsum_batched: 1..3 outputs per job");
+    TORCH_CHECK(stride[i] >= (int64_t)outs[i].size() * D[i] && parts[i].numel() >= nblk[i] * stride[i],
+                "colsum_batched: partial buffer too small");
+    for (size_t k = 0; k < outs[i].size(); ++k) {
+      if (outs[i][k].has_value() && outs[i][k]->defined()) {
+        need(*outs[i][k], at::kFloat, "colsum out");
+        TORCH_CHECK(outs[i][k]->numel() == D[i], "colsum_batched: output size");
+        op[3 * i + k] = outs[i][k]->data_ptr<float>();
+      }
+    }
+    pp[i] = parts[i].data_ptr<float>();
+    nb[i] = (int)nblk[i]; sd[i] = (int)stride[i]; dd[i] = (int)D[i];
+    no[i] = (int)outs[i].size(); ac[i] = accumulate[i] ? 1 : 0;
+  }
+  if (n == 0) return;
+  check_rc(fd_colsum_batched((int)n, pp.data(), op.data(), nb.data(), sd.data(), dd.data(), no.data(), ac.data(),
+                             stream()),
+           "colsum_batched");
 }
 
 void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& W, const at::Tensor& bias,
@@ -565,6 +604,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("emb_fwd", &emb_fwd);
   m.def("emb_bwd", &emb_bwd);
   m.def("colsum_bf16", &colsum_bf16);
+  m.def("colsum_batched", &colsum_batched);
   m.def("rank_sort", &rank_sort);
   m.def("head_fwd", &head_fwd);
   m.def("head_bwd", &head_bwd);

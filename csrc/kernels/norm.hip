@@ -556,6 +556,56 @@ __global__ __launch_bounds__(256) void colsum_bf16_partial_kernel(const bf16_t* 
   *reinterpret_cast<float4*>(part + (size_t)blockIdx.x * N + c4) = make_float4(s0, s1, s2, s3);
 }
 
+// Deferred column-sum finalisation: every bias / LayerNorm-affine gradient of the
+// backward leaves its per-block partials in a slot of its own, and ONE launch at the
+// end of the backward reduces all of them (instead of one small launch per producer).
+// Same per-column fixed-order sum as colsum_kernel: bitwise identical results.
+constexpr int COLSUM_MAXJ = 32;
+struct ColsumJob {
+  const float* part;
+  float* out[3];
+  int nblk, stride_blk, D, nout, accumulate;
+};
+struct ColsumBatch {
+  ColsumJob j[COLSUM_MAXJ];
+  int start[COLSUM_MAXJ + 1];  // first block of job i (blocks = ceil(D/64) * nout)
+  int n;
+};
+
+template <int UNR>
+__global__ __launch_bounds__(256) void colsum_batched_kernel(ColsumBatch cb) {
+  __shared__ float red[4][64];
+  int ji = 0;
+  while (ji + 1 < cb.n && (int)blockIdx.x >= cb.start[ji + 1]) ++ji;
+  const ColsumJob& jb = cb.j[ji];
+  const int local = blockIdx.x - cb.start[ji];
+  const int cblk = (jb.D + 63) / 64;
+  const int k = local / cblk;
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int j = (local - k * cblk) * 64 + lane;
+  float* out = jb.out[k];
+  float s = 0.f;
+  if (j < jb.D) {
+    const float* p = jb.part + k * jb.D + j;
+    for (int b0 = grp; b0 < jb.nblk; b0 += 4 * UNR) {
+      float v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int b = b0 + 4 * u;
+        v[u] = b < jb.nblk ? p[(size_t)b * jb.stride_blk] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) s += v[u];
+    }
+  }
+  red[grp][lane] = s;
+  __syncthreads();
+  if (grp == 0 && j < jb.D && out) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[j] = jb.accumulate ? out[j] + t : t;
+  }
+}
+
 constexpr int LN_GRID = 256;
 constexpr int LN_BWD_THREADS = 512;
 
@@ -580,7 +630,7 @@ int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* bet
 int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean,
               const float* rstd, void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work,
               int T, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
-              int accumulate, const int* row_map, hipStream_t st) {
+              int accumulate, const int* row_map, int defer, hipStream_t st) {
   if (D != 768) return 1;
   LnArgs a{};
   a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.r = (const bf16_t*)r; a.gamma = gamma;
@@ -589,7 +639,7 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
   const int grid = std::min(LN_GRID, (T + 15) / 16);
   hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
                      st, a);
-  hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 3), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
+  if (!defer) hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 3), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, dbias, accumulate);
   return 0;
 }
@@ -653,14 +703,39 @@ int fd_rank_sort(const void* ids, int ids64, int T, long long* sorted, long long
   return 0;
 }
 
-int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, hipStream_t st) {
+// defer: leave the [nblk][N] partials in `work` (finalised later by fd_colsum_batched); returns nblk.
+int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, int defer, int* nblk_out,
+                   hipStream_t st) {
   if (N % 4 != 0) return 1;
   const int rows = 32;
   const int nblk = (T + rows - 1) / rows;
+  if (nblk_out) *nblk_out = nblk;
   hipLaunchKernelGGL(colsum_bf16_partial_kernel, dim3(nblk, (N / 4 + 255) / 256), dim3(256), 0, st,
                      (const bf16_t*)x, T, N, rows, work);
-  hipLaunchKernelGGL(colsum_kernel<16>, dim3((N + 63) / 64, 1), dim3(256), 0, st, work, nblk, N, N, out,
-                     (float*)nullptr, (float*)nullptr, accumulate);
+  if (!defer)
+    hipLaunchKernelGGL(colsum_kernel<16>, dim3((N + 63) / 64, 1), dim3(256), 0, st, work, nblk, N, N, out,
+                       (float*)nullptr, (float*)nullptr, accumulate);
+  return 0;
+}
+
+// parts[i]: [nblk[i]][stride[i]] partials, output k of job i = columns k*D .. k*D+D-1.
+int fd_colsum_batched(int n, const float* const* parts, float* const* outs /* n x 3 */, const int* nblk,
+                      const int* stride, const int* D, const int* nout, const int* accumulate, hipStream_t st) {
+  for (int base = 0; base < n; base += COLSUM_MAXJ) {
+    ColsumBatch cb{};
+    cb.n = std::min(COLSUM_MAXJ, n - base);
+    int blocks = 0;
+    for (int i = 0; i < cb.n; ++i) {
+      const int g = base + i;
+      if (nout[g] < 1 || nout[g] > 3 || D[g] <= 0) return 1;
+      cb.j[i] = ColsumJob{parts[g], {outs[3 * g], outs[3 * g + 1], outs[3 * g + 2]}, nblk[g], stride[g], D[g],
+                          nout[g], accumulate[g]};
+      cb.start[i] = blocks;
+      blocks += ((D[g] + 63) / 64) * nout[g];
+    }
+    cb.start[cb.n] = blocks;
+    hipLaunchKernelGGL(colsum_batched_kernel<16>, dim3(blocks), dim3(256), 0, st, cb);
+  }
   return 0;
 }
 

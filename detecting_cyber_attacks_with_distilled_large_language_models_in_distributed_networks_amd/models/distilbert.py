@@ -249,6 +249,8 @@ class DDoSClassifier(nn.Module):
         # to `pack_quantum` so a handful of shapes (HIP graphs) cover every batch.
         self.unpad = True
         self.pack_quantum = 128
+        # HIP path: finalise all bias / LN-affine column sums of a backward in one launch
+        self.defer_colsum = True
         self.torch_counter = 0
         self._grad_token = None
         self._synced_version = -1
@@ -423,6 +425,8 @@ class DDoSClassifier(nn.Module):
                     eps=cfg.layer_norm_eps, p_hidden=cfg.dropout, p_attn=cfg.attention_dropout, p_head=self.dropout.p,
                     on_layer_grads=self.layer_grads_hook if grad else None,
                     wgrad=self._wgrad if grad and self.wgrad_stream else None, group_dw=self.group_dw)
+        if grad and self.defer_colsum and self.layer_grads_hook is None:
+            rc.colsum_jobs = []  # (a per-block hook needs each block's grads final at once)
         if self.training:
             K.step_inc(None, self.rng)
         token = self._grad_token if torch.is_grad_enabled() else None

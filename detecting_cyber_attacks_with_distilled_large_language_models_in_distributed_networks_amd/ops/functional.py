@@ -51,6 +51,9 @@ class RunCtx:
     # [rows] packed -> padded row (-1 for the bucket's filler rows; dropout-hash index).
     cu: Optional[torch.Tensor] = None
     row_map: Optional[torch.Tensor] = None
+    # deferred column sums (bias / LN-affine grads): producers leave partials, the end of
+    # the backward finalises all of them in one launch (None = finalise immediately)
+    colsum_jobs: Optional[list] = None
 
 
 class _WGrad:
@@ -110,6 +113,8 @@ class EmbeddingFn(torch.autograd.Function):
                   s["ln_b"].buf, ctx.rc.S, ctx.rc.seed, 1, ctx.p, acc, now, ever)
         if ctx.rc.wgrad is not None:  # join the weight-gradient stream: every grad is final after this node
             torch.cuda.current_stream().wait_stream(ctx.rc.wgrad)
+        if ctx.rc.colsum_jobs:
+            K.colsum_flush(ctx.rc.colsum_jobs)
         return (None,) * 8
 
 
@@ -146,8 +151,9 @@ class LayerFn(torch.autograd.Function):
         acc = G["l2_w"].accumulate()
         wg = _WGrad(rc)  # dW / bias-sum work -> side stream, dX chain stays on the main stream
         # output_layer_norm(dropout(lin2) + h): dz2 -> residual grad of h, df -> lin2 output grad
+        jobs = rc.colsum_jobs
         dz2, df = K.ln_bwd(dy, f, h, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, rc.seed,
-                           ffn_site, p_h, acc, rc.row_map)
+                           ffn_site, p_h, acc, rc.row_map, jobs)
         wt = L.get("wT") or {}
         du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"))  # dg W2 * gelu'(u)
         wg.fork(df, g, du, h)
@@ -157,11 +163,11 @@ class LayerFn(torch.autograd.Function):
             else:
                 K.linear_dw(df, g, G["l2_w"].buf, acc)
                 K.linear_dw(du, h, G["l1_w"].buf, acc)
-            K.colsum(du, G["l1_b"].buf, acc)
+            K.colsum(du, G["l1_b"].buf, acc, jobs)
         dh = K.linear_dx(du, L["l1_w"], res=dz2, wt=wt.get("l1_w"))    # du W1 + dz2
         # sa_layer_norm(out_lin + x)
         dz1, _ = K.ln_bwd(dh, ao, x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf, G["o_b"].buf, rc.seed, 0,
-                          0.0, acc)
+                          0.0, acc, None, jobs)
         dcx = K.linear_dx(dz1, L["o_w"], wt=wt.get("o_w"))
         if not rc.group_dw:
             wg.fork(dz1, cx)
@@ -174,7 +180,7 @@ class LayerFn(torch.autograd.Function):
                 K.linear_dw2(dz1, cx, G["o_w"].buf, dqkv, x, G["qkv_w"].buf, acc)
             else:
                 K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
-            K.colsum(dqkv, G["qkv_b"].buf, acc)
+            K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
         dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt.get("qkv_w"))
         for k in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_w", "ln1_b", "l1_w", "l1_b", "l2_b", "ln2_w", "ln2_b"):
             G[k].accumulate()

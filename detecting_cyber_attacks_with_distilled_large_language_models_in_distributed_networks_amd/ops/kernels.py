@@ -93,12 +93,27 @@ def transpose_many(srcs, dsts):
         ext().transpose_batched(list(srcs[i:i + 32]), list(dsts[i:i + 32]))
 
 
-def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = False, jobs: Optional[list] = None) -> torch.Tensor:
+    """out (+)= column sums of x.  With ``jobs`` (a deferred-colsum list) only the per-block
+    partials are computed now, into a slot of their own; ``colsum_flush`` finalises them."""
     N = out.numel()
     T = x.numel() // N
-    ws = workspace(x.device, "colsum", ((T + 31) // 32) * N)
-    ext().colsum_bf16(x, out, ws, accumulate)
+    if jobs is None:
+        ws = workspace(x.device, "colsum", ((T + 31) // 32) * N)
+        ext().colsum_bf16(x, out, ws, accumulate, False)
+        return out
+    ws = workspace(x.device, f"colsum_job{len(jobs)}", ((T + 31) // 32) * N)
+    nblk = ext().colsum_bf16(x, out, ws, accumulate, True)
+    jobs.append((ws, [out], nblk, N, N, accumulate))
     return out
+
+
+def colsum_flush(jobs: list):
+    """Finalise every deferred column sum in one launch (bitwise = the immediate path)."""
+    if jobs:
+        ext().colsum_batched([j[0] for j in jobs], [j[1] for j in jobs], [j[2] for j in jobs],
+                             [j[3] for j in jobs], [j[4] for j in jobs], [int(j[5]) for j in jobs])
+        jobs.clear()
 
 
 # ------------------------------------------------------------------ attention
@@ -142,14 +157,20 @@ def ln_fwd(x, r, gamma, beta, eps, seed, site, p, row_map=None):
     return y, mean, rstd
 
 
-def ln_bwd(dy, x, r, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False, row_map=None):
+def ln_bwd(dy, x, r, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False, row_map=None,
+           jobs: Optional[list] = None):
+    """jobs: deferred-colsum list -> the dgamma/dbeta/dbias partials wait for ``colsum_flush``."""
     D = gamma.numel()
+    T = x.numel() // D
     dz = torch.empty_like(x)
     thr, sc = _drop(p)
     dx = torch.empty_like(x) if thr else None
-    ws = workspace(x.device, "ln_part", LN_GRID * 3 * D)
+    key = "ln_part" if jobs is None else f"ln_part_job{len(jobs)}"
+    ws = workspace(x.device, key, LN_GRID * 3 * D)
     ext().ln_bwd(dy.contiguous(), x, r, gamma, mean, rstd, dz, dx, dgamma, dbeta, dbias, ws, seed, site, thr, sc,
-                 accumulate, row_map if thr else None)
+                 accumulate, row_map if thr else None, jobs is not None)
+    if jobs is not None:
+        jobs.append((ws, [dgamma, dbeta, dbias], min(LN_GRID, (T + 15) // 16), 3 * D, D, accumulate))
     return dz, (dx if dx is not None else dz)
 
 

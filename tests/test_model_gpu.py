@@ -192,3 +192,23 @@ def test_wgrad_side_stream_matches_serial(graph):
     assert torch.equal(models[0].arena.master, models[1].arena.master)
     if graph:
         assert all(st.graph is not None for st in steps)
+
+
+def test_deferred_colsum_matches_immediate():
+    """All bias / LN-affine column sums finalised in one batched launch at the end of the
+    backward == each finalised right after its producer (bitwise; same fixed-order sum)."""
+    cfg = DistilBertConfig(n_layers=2)
+    grads = []
+    for defer in (True, False):
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=12)
+        m.defer_colsum = defer
+        m.train()
+        ids, mask, labels = _batch(16, 128, seed=300)
+        for acc_step in range(2):  # second backward accumulates (deferred jobs carry the flag)
+            if acc_step == 0:
+                m.zero_grad()
+            loss, _ = m.forward_loss(ids, mask, labels)
+            loss.backward()
+        torch.cuda.synchronize()
+        grads.append(m.arena.grad.clone())
+    assert torch.equal(grads[0], grads[1])
