@@ -29,6 +29,8 @@
 //    kernel dq (query-owned) and kernel dkdv (key-owned) each recompute P.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int DH = 64;
@@ -465,6 +467,311 @@ __global__ __launch_bounds__(256) void mask_to_bias_kernel(const M* mask, float*
   if (i < n) bias[i] = mask[i] != 0 ? 0.f : -INFINITY;
 }
 
+
+// ------------------------------------------------------------------ S <= 128: one block per (b, h)
+// Short sequences (DistilBERT at seq128; CICIDS2017 sentences are ~80 tokens) make the
+// 64-row kernels above latency-bound: every block pays a dependent global-load round
+// trip per 64-key tile, the second query tile of an 80-token sequence is 3/4 idle, and
+// the backward stages K/V and Q/dO twice (dQ and dK/dV kernels).  Here one 8-wave
+// block owns a whole (sequence, head): all tiles are staged in ONE round trip (every
+// load in flight together), and the backward is fused -- phase 1 (waves own 16 query
+// rows) computes delta = rowsum(dO*O) and dQ, phase 2 (waves own 16 keys) computes dK
+// and dV from the same LDS images, delta never leaving LDS.  Same fragment layouts,
+// same per-element arithmetic order and dropout indices as the 64-row kernels.
+
+// Stage rows [0, 64*nt) of a [rows][64]-per-head operand into nt swizzled [64][64]
+// images (8 KiB apart); rows >= len re-read row len-1.  512 threads.
+DEV void stage_rows(char* lds, const bf16_t* src, long ld, int tid, int nt, int len) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = i * 512 + tid;
+    const int r = id >> 3, c = id & 7;
+    if (r < 64 * nt) {
+      const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)min(r, len - 1) * ld + c * 8);
+      *reinterpret_cast<uint4*>(lds + (r >> 6) * 8192 + tile_off(r & 63, c)) = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 512];
+  char* ks = smem;
+  char* vs = smem + 2 * 8192;
+  float* kb = reinterpret_cast<float*>(smem + 4 * 8192);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  if (b == a.B) {
+    zero_filler(a, a.ctx, D, 1, h);
+    return;
+  }
+  int tok0i, len;
+  seq_span(a, b, tok0i, len);
+  const int nt = (len + 63) >> 6;
+  const size_t tok0 = (size_t)tok0i;
+  stage_rows(ks, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
+  stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
+  if (tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) : -INFINITY;
+  __syncthreads();
+  const int q0 = w * 16;
+  if (q0 >= len) return;  // no barrier follows
+  const uint32_t seed = site_seed(a);
+  const bool drop = a.drop_threshold != 0;
+  const int q = q0 + (lane & 15);
+  const int qr = min(q, len - 1);
+  bf16x8 qf[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) qf[s2] = load_frag_global(a.qkv + (tok0 + qr) * ld3 + h * DH + 32 * s2 + 8 * g);
+  f32x4 o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
+  for (int kt = 0; kt < nt; ++kt) {
+    if (!__any(kb[kt * 64 + lane] != -INFINITY)) continue;  // fully masked key tile (exact skip)
+    const char* kst = ks + kt * 8192;
+    const char* vst = vs + kt * 8192;
+    const int k0 = kt * 64;
+    f32x4 sc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) sc[t] = mfma16(row_frag(kst, 16 * t, s2, lane), qf[s2], sc[t]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sc[t][r] = sc[t][r] * a.scale + kb[k0 + 16 * t + 4 * g + r];
+        mx = fmaxf(mx, sc[t][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float mref = mn == -INFINITY ? 0.f : mn;
+    const float alpha = __expf(m - mref);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] *= alpha;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = __expf(sc[t][r] - mref);
+        l += pv;
+        float pd = pv;
+        if (drop) {
+          const uint32_t key = k0 + 16 * t + 4 * g + r;
+          pd = drop_keep(seed, rowidx + key, a.drop_threshold) ? pv * a.drop_scale : 0.f;
+        }
+        sc[t][r] = pd;
+      }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 pf = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(tr_frag(vst, 16 * dt, kk, lane), pf, o[dt]);
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (q >= len) return;
+  const float inv = 1.f / l;
+  bf16_t* out = a.ctx + (tok0 + q) * D + h * DH;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+    *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) =
+        make_uint2(pack_bf2(o[dt][0] * inv, o[dt][1] * inv), pack_bf2(o[dt][2] * inv, o[dt][3] * inv));
+  if (g == 0) a.lse[((size_t)b * H + h) * S + q] = m + __logf(l);
+}
+
+__global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * 8192 + 3 * 512];
+  char* qs = smem;
+  char* ks = smem + 2 * 8192;
+  char* vs = smem + 4 * 8192;
+  char* os = smem + 6 * 8192;  // dO
+  float* kb = reinterpret_cast<float*>(smem + 8 * 8192);
+  float* lse_s = kb + 128;
+  float* dl_s = lse_s + 128;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  if (b == a.B) {
+    zero_filler(a, a.dqkv, ld3, 3, h);
+    return;
+  }
+  int tok0i, len;
+  seq_span(a, b, tok0i, len);
+  const int nt = (len + 63) >> 6;
+  const size_t tok0 = (size_t)tok0i;
+  const size_t st0 = ((size_t)b * H + h) * S;
+  stage_rows(qs, a.qkv + tok0 * ld3 + h * DH, ld3, tid, nt, len);
+  stage_rows(ks, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
+  stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
+  stage_rows(os, a.dctx + tok0 * D + h * DH, D, tid, nt, len);
+  if (tid < 128) {
+    kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) : -INFINITY;
+    // query rows past the sequence: lse = +inf makes their P (and dS) exactly 0
+    lse_s[tid] = tid < len ? a.lse[st0 + tid] : INFINITY;
+    dl_s[tid] = 0.f;
+  }
+  __syncthreads();
+  const uint32_t seed = site_seed(a);
+  const bool drop = a.drop_threshold != 0;
+  const float sc_out = a.scale;
+
+  // ---- phase 1: dQ and delta; wave w owns queries 16w .. 16w+15
+  const int q0 = w * 16;
+  if (q0 < len) {
+    const int q = q0 + (lane & 15);
+    const int qr = min(q, len - 1);
+    const char* qst = qs + (q0 >> 6) * 8192;
+    const char* ost = os + (q0 >> 6) * 8192;
+    bf16x8 qf[2], dof[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      qf[s2] = row_frag(qst, q0 & 63, s2, lane);
+      dof[s2] = row_frag(ost, q0 & 63, s2, lane);
+    }
+    const float lse = lse_s[qr];
+    float dl = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 of = load_frag_global(a.ctx + (tok0 + qr) * D + h * DH + 32 * s2 + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)of[j]) * bf2f((uint16_t)dof[s2][j]);
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    if (g == 0 && q < len) dl_s[q] = dl;
+    const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
+    f32x4 dq[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nt; ++kt) {
+      if (!__any(kb[kt * 64 + lane] != -INFINITY)) continue;  // fully masked key tile: dS = 0
+      const char* kst = ks + kt * 8192;
+      const char* vst = vs + kt * 8192;
+      f32x4 sc[4], dp[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          sc[t] = mfma16(row_frag(kst, 16 * t, s2, lane), qf[s2], sc[t]);
+          dp[t] = mfma16(row_frag(vst, 16 * t, s2, lane), dof[s2], dp[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kl = 16 * t + 4 * g + r;
+          const float pv = __expf(sc[t][r] * a.scale + kb[kt * 64 + kl] - lse);
+          float dpv = dp[t][r];
+          if (drop) dpv = drop_keep(seed, rowidx + kt * 64 + kl, a.drop_threshold) ? dpv * a.drop_scale : 0.f;
+          sc[t][r] = pv * (dpv - dl);  // dS
+        }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 df = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(tr_frag(kst, 16 * dt, kk, lane), df, dq[dt]);
+      }
+    }
+    if (q < len) {
+      bf16_t* out = a.dqkv + (tok0 + q) * ld3 + h * DH;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) = make_uint2(
+            pack_bf2(dq[dt][0] * sc_out, dq[dt][1] * sc_out), pack_bf2(dq[dt][2] * sc_out, dq[dt][3] * sc_out));
+    }
+  }
+  __syncthreads();  // delta of every query row is in LDS
+
+  // ---- phase 2: dK and dV; wave w owns keys 16w .. 16w+15
+  const int key0 = w * 16;
+  if (key0 >= len) return;
+  const int key = key0 + (lane & 15);
+  const char* kst = ks + (key0 >> 6) * 8192;
+  const char* vst = vs + (key0 >> 6) * 8192;
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    kf[s2] = row_frag(kst, key0 & 63, s2, lane);
+    vf[s2] = row_frag(vst, key0 & 63, s2, lane);
+  }
+  const float kbias = kb[key];
+  const uint32_t headidx = (uint32_t)(b * H + h) * S;
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dk[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int qt = 0; qt < nt; ++qt) {
+    const char* qst = qs + qt * 8192;
+    const char* ost = os + qt * 8192;
+    f32x4 sc[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        sc[t] = mfma16(row_frag(qst, 16 * t, s2, lane), kf[s2], sc[t]);  // S[q][key]
+        dp[t] = mfma16(row_frag(ost, 16 * t, s2, lane), vf[s2], dp[t]);  // dP[q][key]
+      }
+    }
+    f32x4 pd[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = qt * 64 + 16 * t + 4 * g + r;
+        const float pv = __expf(sc[t][r] * a.scale + kbias - lse_s[ql]);
+        float dpv = dp[t][r], pdv = pv;
+        if (drop) {
+          const bool keep = drop_keep(seed, (headidx + ql) * (uint32_t)S + key, a.drop_threshold);
+          dpv = keep ? dpv * a.drop_scale : 0.f;
+          pdv = keep ? pv * a.drop_scale : 0.f;
+        }
+        pd[t][r] = pdv;
+        sc[t][r] = pv * (dpv - dl_s[ql]);  // dS
+      }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 pf = pack_acc(pd[2 * kk], pd[2 * kk + 1]);
+      const bf16x8 sf = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma16(tr_frag(ost, 16 * dt, kk, lane), pf, dv[dt]);
+        dk[dt] = mfma16(tr_frag(qst, 16 * dt, kk, lane), sf, dk[dt]);
+      }
+    }
+  }
+  if (key >= len) return;
+  bf16_t* outk = a.dqkv + (tok0 + key) * ld3 + D + h * DH;
+  bf16_t* outv = a.dqkv + (tok0 + key) * ld3 + 2 * D + h * DH;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    *reinterpret_cast<uint2*>(outk + 16 * dt + 4 * g) = make_uint2(
+        pack_bf2(dk[dt][0] * sc_out, dk[dt][1] * sc_out), pack_bf2(dk[dt][2] * sc_out, dk[dt][3] * sc_out));
+    *reinterpret_cast<uint2*>(outv + 16 * dt + 4 * g) =
+        make_uint2(pack_bf2(dv[dt][0], dv[dt][1]), pack_bf2(dv[dt][2], dv[dt][3]));
+  }
+}
+
+bool use_s128(int S) {
+  static const int on = [] { const char* e = getenv("FD_ATTN_S128"); return e ? atoi(e) : 1; }();
+  return on && S <= 128;
+}
+
 }  // namespace
 
 extern "C" {
@@ -478,7 +785,10 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
+  if (use_s128(S))
+    hipLaunchKernelGGL(attn_fwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
   return 0;
 }
 
@@ -493,6 +803,10 @@ int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const floa
   a.dctx = (const bf16_t*)dctx; a.delta = delta; a.dqkv = (bf16_t*)dqkv;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
+  if (use_s128(S)) {
+    hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
+    return 0;
+  }
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
   return 0;

@@ -384,29 +384,33 @@ __global__ __launch_bounds__(256) void rank_sort_kernel(const I* ids, int T, lon
   extern __shared__ __attribute__((aligned(16))) int keys[];  // T ids
   for (int i = threadIdx.x; i < T; i += 256) keys[i] = (int)ids[i];
   __syncthreads();
-  const int t = blockIdx.x * 64 + (threadIdx.x >> 2);
-  const int part = threadIdx.x & 3;
+  // 16 tokens per block, 16 threads per token (grid = T/16 blocks: ~256 for a bs32 batch,
+  // one per CU, instead of T/64 blocks that left 3/4 of the chip idle)
+  const int t = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int part = threadIdx.x & 15;
   int cnt = 0;
   int my = 0;
   if (t < T) {
     my = keys[t];
-    // the 4 threads of a token read adjacent 16-byte groups: one ds_read_b128 each,
-    // 64 contiguous bytes per token -> no bank conflicts, 4 keys per read
-    const int T4 = T & ~15;
-    for (int j = 4 * part; j < T4; j += 16) {
+    // the 16 threads of a token read adjacent 16-byte groups: one ds_read_b128 each,
+    // 256 contiguous bytes per token (the wave's 4 tokens read the same bytes: broadcast)
+    const int T4 = T & ~63;
+    for (int j = 4 * part; j < T4; j += 64) {
       const int4 k = *reinterpret_cast<const int4*>(keys + j);
       cnt += (k.x < my) | ((k.x == my) & (j < t));
       cnt += (k.y < my) | ((k.y == my) & (j + 1 < t));
       cnt += (k.z < my) | ((k.z == my) & (j + 2 < t));
       cnt += (k.w < my) | ((k.w == my) & (j + 3 < t));
     }
-    for (int j = T4 + part; j < T; j += 4) {
+    for (int j = T4 + part; j < T; j += 16) {
       const int k = keys[j];
       cnt += (k < my) | ((k == my) & (j < t));
     }
   }
   cnt += __shfl_xor(cnt, 1, 64);
   cnt += __shfl_xor(cnt, 2, 64);
+  cnt += __shfl_xor(cnt, 4, 64);
+  cnt += __shfl_xor(cnt, 8, 64);
   if (t < T && part == 0) {
     sorted[cnt] = my;
     perm[cnt] = t;
@@ -695,10 +699,10 @@ int fd_rank_sort(const void* ids, int ids64, int T, long long* sorted, long long
   if (T > 16384) return 1;
   const size_t lds = (size_t)T * sizeof(int);
   if (ids64)
-    hipLaunchKernelGGL(rank_sort_kernel<long long>, dim3((T + 63) / 64), dim3(256), lds, st, (const long long*)ids, T,
+    hipLaunchKernelGGL(rank_sort_kernel<long long>, dim3((T + 15) / 16), dim3(256), lds, st, (const long long*)ids, T,
                        sorted, perm);
   else
-    hipLaunchKernelGGL(rank_sort_kernel<int>, dim3((T + 63) / 64), dim3(256), lds, st, (const int*)ids, T, sorted,
+    hipLaunchKernelGGL(rank_sort_kernel<int>, dim3((T + 15) / 16), dim3(256), lds, st, (const int*)ids, T, sorted,
                        perm);
   return 0;
 }

@@ -360,3 +360,13 @@ def test_linear_dx_transposed_weight(M, N, K):
     g = torch.autograd.grad(torch.nn.functional.gelu(uu), uu, ref)[0]
     assert rel_err(kn.linear_dx(dy, w, gelu_u=u, wt=wt), g) < 1e-2
     assert torch.equal(kn.linear_dx(dy, w, res=res, wt=wt), kn.linear_dx(dy, w, res=res, wt=wt))
+
+
+@pytest.mark.parametrize("T", [4096, 1000, 37])
+def test_rank_sort_matches_stable_sort(T):
+    g = torch.Generator().manual_seed(T)
+    ids = torch.randint(0, 300, (T,), generator=g).to(DEV)
+    ids[: T // 4] = 0  # a long run (padding id)
+    srt, perm = kn.group_ids(ids)
+    ref_s, ref_p = torch.sort(ids, stable=True)
+    assert torch.equal(srt, ref_s) and torch.equal(perm, ref_p)

@@ -32,10 +32,11 @@ def rel(a, b):
     return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-8)).item()
 
 
-def test_varlen_attention_matches_padded():
-    B, S, H = 6, 128, 12
+@pytest.mark.parametrize("S", [128, 256])  # one-block-per-(b,h) kernels (S <= 128) and the 64-row tiles
+def test_varlen_attention_matches_padded(S):
+    B, H = 6, 12
     g = torch.Generator(device="cuda").manual_seed(1)
-    lens = torch.tensor([128, 77, 64, 1, 100, 65])
+    lens = torch.tensor([S, 77, 64, 1, 100, 65]) if S == 128 else torch.tensor([256, 77, 129, 1, 200, 65])
     qkv_pad = (torch.randn(B * S, 3 * H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
     mask = (torch.arange(S)[None] < lens[:, None]).cuda()
     kb = K.mask_bias(mask.to(torch.int64))
