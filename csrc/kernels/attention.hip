@@ -728,25 +728,29 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
         dp[t] = mfma16(row_frag(ost, 16 * t, s2, lane), vf[s2], dp[t]);  // dP[q][key]
       }
     }
-    f32x4 pd[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = qt * 64 + 16 * t + 4 * g + r;
-        const float pv = __expf(sc[t][r] * a.scale + kbias - lse_s[ql]);
-        float dpv = dp[t][r], pdv = pv;
-        if (drop) {
-          const bool keep = drop_keep(seed, (headidx + ql) * (uint32_t)S + key, a.drop_threshold);
-          dpv = keep ? dpv * a.drop_scale : 0.f;
-          pdv = keep ? pv * a.drop_scale : 0.f;
-        }
-        pd[t][r] = pdv;
-        sc[t][r] = pv * (dpv - dl_s[ql]);  // dS
-      }
+    // one 32-query half at a time: P / dS of tiles 2kk, 2kk+1 are packed to bf16 right away
+    // (keeps the live set under 128 VGPRs -> two blocks per CU)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 pf = pack_acc(pd[2 * kk], pd[2 * kk + 1]);
+      f32x4 pd[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = 2 * kk + u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = qt * 64 + 16 * t + 4 * g + r;
+          const float pv = __expf(sc[t][r] * a.scale + kbias - lse_s[ql]);
+          float dpv = dp[t][r], pdv = pv;
+          if (drop) {
+            const bool keep = drop_keep(seed, (headidx + ql) * (uint32_t)S + key, a.drop_threshold);
+            dpv = keep ? dpv * a.drop_scale : 0.f;
+            pdv = keep ? pv * a.drop_scale : 0.f;
+          }
+          pd[u][r] = pdv;
+          sc[t][r] = pv * (dpv - dl_s[ql]);  // dS
+        }
+      }
+      const bf16x8 pf = pack_acc(pd[0], pd[1]);
       const bf16x8 sf = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {

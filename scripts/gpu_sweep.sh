@@ -5,4 +5,4 @@ timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -x -q -k "gemm or l
 rc=$?; tail -3 $O/tests.log
 # only numerical failures (rc 1) may continue; a crash / fault / timeout ends the call
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests rc=$rc: stopping"; exit $rc; fi
-timeout -k 10 900 python scripts/gemm_sweep.py > $O/sweep.txt 2>&1; rc=$?; tail -22 $O/sweep.txt; exit $rc
+timeout -k 10 900 python scripts/gemm_sweep.py ${2:-2688} > $O/sweep.txt 2>&1; rc=$?; tail -22 $O/sweep.txt; exit $rc
