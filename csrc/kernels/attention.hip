@@ -509,19 +509,19 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   seq_span(a, b, tok0i, len);
   const int nt = (len + 63) >> 6;
   const size_t tok0 = (size_t)tok0i;
+  const int q0 = w * 16;
+  const int q = q0 + (lane & 15);
+  const int qr = min(q, len - 1);
+  bf16x8 qf[2];  // this wave's Q rows, fetched together with the K/V staging loads
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) qf[s2] = load_frag_global(a.qkv + (tok0 + qr) * ld3 + h * DH + 32 * s2 + 8 * g);
   stage_rows(ks, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
   stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
   if (tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) : -INFINITY;
   __syncthreads();
-  const int q0 = w * 16;
   if (q0 >= len) return;  // no barrier follows
   const uint32_t seed = site_seed(a);
   const bool drop = a.drop_threshold != 0;
-  const int q = q0 + (lane & 15);
-  const int qr = min(q, len - 1);
-  bf16x8 qf[2];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) qf[s2] = load_frag_global(a.qkv + (tok0 + qr) * ld3 + h * DH + 32 * s2 + 8 * g);
   f32x4 o[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -609,6 +609,15 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   const int nt = (len + 63) >> 6;
   const size_t tok0 = (size_t)tok0i;
   const size_t st0 = ((size_t)b * H + h) * S;
+  // phase 1's O rows (for delta) are fetched together with the staging loads: no second
+  // dependent global round trip after the barrier
+  const int q0 = w * 16;
+  bf16x8 of[2];
+  {
+    const int qr = min(q0 + (lane & 15), len - 1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) of[s2] = load_frag_global(a.ctx + (tok0 + qr) * D + h * DH + 32 * s2 + 8 * g);
+  }
   stage_rows(qs, a.qkv + tok0 * ld3 + h * DH, ld3, tid, nt, len);
   stage_rows(ks, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
   stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
@@ -625,7 +634,6 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   const float sc_out = a.scale;
 
   // ---- phase 1: dQ and delta; wave w owns queries 16w .. 16w+15
-  const int q0 = w * 16;
   if (q0 < len) {
     const int q = q0 + (lane & 15);
     const int qr = min(q, len - 1);
@@ -640,11 +648,9 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
     const float lse = lse_s[qr];
     float dl = 0.f;
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 of = load_frag_global(a.ctx + (tok0 + qr) * D + h * DH + 32 * s2 + 8 * g);
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)of[j]) * bf2f((uint16_t)dof[s2][j]);
-    }
+      for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)of[s2][j]) * bf2f((uint16_t)dof[s2][j]);
     dl += __shfl_xor(dl, 16, 64);
     dl += __shfl_xor(dl, 32, 64);
     if (g == 0 && q < len) dl_s[q] = dl;
