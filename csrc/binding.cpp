@@ -41,7 +41,7 @@ int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* bet
 int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean,
               const float* rstd, void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work, int T,
               int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, int accumulate,
-              const int* row_map, int defer, hipStream_t st);
+              const int* row_map, int defer, int* nblk_out, hipStream_t st);
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, hipStream_t st);
@@ -326,11 +326,12 @@ void ln_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& r, const at::T
            "ln_fwd");
 }
 
-void ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& r, const at::Tensor& gamma,
+int64_t ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& r, const at::Tensor& gamma,
             const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dz, const c10::optional<at::Tensor>& dx,
             const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
             const c10::optional<at::Tensor>& dbias, const at::Tensor& work, const at::Tensor& seed, int64_t site,
             int64_t thr, double dscale, bool accumulate, const c10::optional<at::Tensor>& row_map, bool defer) {
+  // returns the number of [3][D] partial rows written to `work` (a deferred colsum job reduces them)
   need(dy, at::kBFloat16, "dy");
   need(x, at::kBFloat16, "x");
   need_opt(r, at::kBFloat16, "r");
@@ -345,13 +346,16 @@ void ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::T
   need(work, at::kFloat, "work");
   const int64_t D = gamma.numel(), T = x.numel() / D;
   TORCH_CHECK(D == 768 && dy.numel() == T * D && dz.numel() == T * D, "ln_bwd: shapes");
-  TORCH_CHECK(work.numel() >= std::min<int64_t>(256, (T + 7) / 8) * 3 * D, "ln_bwd: work too small");
+  TORCH_CHECK(work.numel() >= std::min<int64_t>(512, (T + 7) / 8) * 3 * D, "ln_bwd: work too small");
   if (thr != 0) TORCH_CHECK(dx.has_value() && dx->numel() == T * D, "ln_bwd: dx required with dropout");
+  int nblk = 0;
   check_rc(fd_ln_bwd(dy.data_ptr(), x.data_ptr(), ptr<void>(r), gamma.data_ptr<float>(), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), dz.data_ptr(), ptr<void>(dx), ptr<float>(dgamma), ptr<float>(dbeta),
                      ptr<float>(dbias), work.data_ptr<float>(), (int)T, (int)D, seedp(seed), (uint32_t)site,
-                     (uint32_t)thr, (float)dscale, accumulate ? 1 : 0, map_ptr(row_map, T), defer ? 1 : 0, stream()),
+                     (uint32_t)thr, (float)dscale, accumulate ? 1 : 0, map_ptr(row_map, T), defer ? 1 : 0, &nblk,
+                     stream()),
            "ln_bwd");
+  return nblk;
 }
 
 void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& pos, const at::Tensor& gamma,

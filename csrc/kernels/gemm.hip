@@ -502,8 +502,11 @@ long long tiles_of(int id, int M, int N) {
 // 1 block/CU S3 rings at every shape; 8-wave 256x192 / 128x192 only where they
 // make one full round of tiles.
 int pick_cfg(int kind, int M, int N, int K) {
-  if (kind == 0) {  // NT forward
-    if (N % 192 == 0 && N >= 3072 && M >= 2048) return 3;
+  if (kind == 0) {  // NT forward (and dX on transposed weights)
+    // FFN1 forward / FFN2 dX (N = 3072): 256x192 fills the chip at M = 4096 (padded bs32),
+    // 128x128 wins at the packed M ~ 2.7 k (21.5 vs 25.7 us; profiles/r1_gemm_cfg_sweep_T2688_packed.txt)
+    if (N % 192 == 0 && N >= 3072 && M >= 3584) return 3;
+    if (N % 128 == 0 && N >= 3072 && M >= 2048) return 1;
     if (N % 192 == 0 && N >= 1536 && M >= 2048) return 6;
     return K >= 2048 ? 0 : 8;
   }

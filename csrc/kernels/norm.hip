@@ -13,6 +13,8 @@
 // (deterministic, no atomics).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 struct LnArgs {
@@ -612,6 +614,14 @@ __global__ __launch_bounds__(256) void colsum_batched_kernel(ColsumBatch cb) {
 
 constexpr int LN_GRID = 256;
 constexpr int LN_BWD_THREADS = 512;
+// LayerNorm backward: 256-thread blocks (8 rows per pass) on up to 512 blocks, so a packed
+// ~2.7 k-row batch spreads over every CU (512-thread blocks gave 168 blocks); FD_LN_BWD_WIDE=0
+// restores 512 threads x 256 blocks.  The partial rows are finalised by the batched colsum.
+constexpr int LN_BWD_GRID_MAX = 512;
+int ln_bwd_threads() {
+  static const int t = [] { const char* e = getenv("FD_LN_BWD_WIDE"); return (e && atoi(e) == 0) ? 512 : 256; }();
+  return t;
+}
 
 }  // namespace
 
@@ -634,14 +644,16 @@ int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* bet
 int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean,
               const float* rstd, void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work,
               int T, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
-              int accumulate, const int* row_map, int defer, hipStream_t st) {
+              int accumulate, const int* row_map, int defer, int* nblk_out, hipStream_t st) {
   if (D != 768) return 1;
   LnArgs a{};
   a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.r = (const bf16_t*)r; a.gamma = gamma;
   a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = (bf16_t*)dz; a.dx = (bf16_t*)dx; a.part = work;
   a.T = T; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.row_map = row_map;
-  const int grid = std::min(LN_GRID, (T + 15) / 16);
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
+  const int thr_n = ln_bwd_threads(), rows = thr_n / 32;
+  const int grid = std::min(thr_n == 256 ? LN_BWD_GRID_MAX : LN_GRID, (T + rows - 1) / rows);
+  if (nblk_out) *nblk_out = grid;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(thr_n), (thr_n / 64) * D * sizeof(float),
                      st, a);
   if (!defer) hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 3), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, dbias, accumulate);

@@ -15,7 +15,8 @@ from ._ext import ext
 from .dropout import threshold
 
 D_MODEL = 768
-LN_GRID = 256  # must match csrc/kernels/norm.hip (partial-sum blocks of the LN backward)
+LN_GRID = 256  # must match csrc/kernels/norm.hip (partial-sum blocks of the embedding backward)
+LN_BWD_PARTS = 512  # upper bound on the LN backward's partial-sum blocks (csrc/kernels/norm.hip)
 
 _WS = {}
 
@@ -166,11 +167,11 @@ def ln_bwd(dy, x, r, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, acc
     thr, sc = _drop(p)
     dx = torch.empty_like(x) if thr else None
     key = "ln_part" if jobs is None else f"ln_part_job{len(jobs)}"
-    ws = workspace(x.device, key, LN_GRID * 3 * D)
-    ext().ln_bwd(dy.contiguous(), x, r, gamma, mean, rstd, dz, dx, dgamma, dbeta, dbias, ws, seed, site, thr, sc,
-                 accumulate, row_map if thr else None, jobs is not None)
+    ws = workspace(x.device, key, LN_BWD_PARTS * 3 * D)
+    nblk = ext().ln_bwd(dy.contiguous(), x, r, gamma, mean, rstd, dz, dx, dgamma, dbeta, dbias, ws, seed, site, thr,
+                        sc, accumulate, row_map if thr else None, jobs is not None)
     if jobs is not None:
-        jobs.append((ws, [dgamma, dbeta, dbias], min(LN_GRID, (T + 15) // 16), 3 * D, D, accumulate))
+        jobs.append((ws, [dgamma, dbeta, dbias], nblk, 3 * D, D, accumulate))
     return dz, (dx if dx is not None else dz)
 
 
