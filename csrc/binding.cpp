@@ -44,12 +44,12 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
               const int* row_map, int defer, int* nblk_out, hipStream_t st);
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
-               const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, hipStream_t st);
+               const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const int* row_map, hipStream_t st);
 int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sorted, const long long* perm,
                const void* word, const void* pos, const float* gamma, const float* mean, const float* rstd,
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
-               int accumulate, unsigned char* now, unsigned char* ever, hipStream_t st);
+               int accumulate, unsigned char* now, unsigned char* ever, const int* row_map, const int* cu, hipStream_t st);
 int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, int defer, int* nblk_out,
                    hipStream_t st);
 int fd_colsum_batched(int n, const float* const* parts, float* const* outs, const int* nblk, const int* stride,
@@ -360,7 +360,8 @@ int64_t ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at
 
 void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& pos, const at::Tensor& gamma,
              const at::Tensor& beta, const at::Tensor& y, const at::Tensor& mean, const at::Tensor& rstd, int64_t S,
-             double eps, const at::Tensor& seed, int64_t site, int64_t thr, double dscale) {
+             double eps, const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
+             const c10::optional<at::Tensor>& row_map) {
   TORCH_CHECK(ids.is_cuda() && ids.is_contiguous() && (ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt),
               "ids must be contiguous GPU int64/int32");
   need(word, at::kBFloat16, "word");
@@ -370,11 +371,12 @@ void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& po
   need(y, at::kBFloat16, "y");
   const int64_t D = gamma.numel(), T = ids.numel();
   TORCH_CHECK(D == 768 && word.size(1) == D && pos.size(1) == D && y.numel() == T * D, "emb_fwd: shapes");
-  TORCH_CHECK(S <= pos.size(0) && T % S == 0, "emb_fwd: S exceeds position table");
+  const bool packed = row_map.has_value() && row_map->defined();
+  TORCH_CHECK(S <= pos.size(0) && (packed || T % S == 0), "emb_fwd: S exceeds position table");
   check_rc(fd_emb_fwd(ids.data_ptr(), ids.scalar_type() == at::kLong, word.data_ptr(), pos.data_ptr(),
                       gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(), mean.data_ptr<float>(),
                       rstd.data_ptr<float>(), (int)T, (int)S, (int)D, (float)eps, seedp(seed), (uint32_t)site,
-                      (uint32_t)thr, (float)dscale, stream()),
+                      (uint32_t)thr, (float)dscale, map_ptr(row_map, T), stream()),
            "emb_fwd");
 }
 
@@ -383,7 +385,8 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
              const at::Tensor& rstd, const at::Tensor& dword, const at::Tensor& dpos, const at::Tensor& dgamma,
              const at::Tensor& dbeta, const at::Tensor& dz_buf, const at::Tensor& work, int64_t S,
              const at::Tensor& seed, int64_t site, int64_t thr, double dscale, bool accumulate,
-             const c10::optional<at::Tensor>& now, const c10::optional<at::Tensor>& ever) {
+             const c10::optional<at::Tensor>& now, const c10::optional<at::Tensor>& ever,
+             const c10::optional<at::Tensor>& row_map, const c10::optional<at::Tensor>& cu) {
   need_opt(now, at::kByte, "now");
   need_opt(ever, at::kByte, "ever");
   TORCH_CHECK(now.has_value() == ever.has_value(), "emb_bwd: now/ever go together");
@@ -400,6 +403,11 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
   need(work, at::kFloat, "work");
   const int64_t D = gamma.numel(), T = ids.numel(), V = word.size(0), P = pos.size(0);
   TORCH_CHECK(sorted.numel() == T && perm.numel() == T && dy.numel() == T * D && dz_buf.numel() >= T * D, "emb_bwd: sizes");
+  const bool packed = cu.has_value() && cu->defined();
+  TORCH_CHECK(packed == (row_map.has_value() && row_map->defined()), "emb_bwd: row_map and cu go together");
+  if (packed) need(*cu, at::kInt, "cu");
+  TORCH_CHECK(S <= P && (packed || T % S == 0), "emb_bwd: S / layout");
+  const int64_t nseq = packed ? cu->numel() - 1 : T / S;
   TORCH_CHECK(dword.numel() == V * D && dpos.numel() == P * D && work.numel() >= std::max<int64_t>(T * D, std::min<int64_t>(256, (T + 7) / 8) * 3 * D),
               "emb_bwd: grad/work sizes");
   check_rc(fd_emb_bwd(dy.data_ptr(), ids.data_ptr(), ids.scalar_type() == at::kLong,
@@ -407,9 +415,9 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
                       reinterpret_cast<const long long*>(perm.data_ptr()), word.data_ptr(), pos.data_ptr(),
                       gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), dword.data_ptr<float>(),
                       dpos.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-                      dz_buf.data_ptr<float>(), work.data_ptr<float>(), (int)T, (int)S, (int)(T / S), (int)P, (int)V,
+                      dz_buf.data_ptr<float>(), work.data_ptr<float>(), (int)T, (int)S, (int)nseq, (int)P, (int)V,
                       (int)D, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, accumulate ? 1 : 0,
-                      ptr<unsigned char>(now), ptr<unsigned char>(ever), stream()),
+                      ptr<unsigned char>(now), ptr<unsigned char>(ever), map_ptr(row_map, T), ptr<int>(cu), stream()),
            "emb_bwd");
 }
 

@@ -251,7 +251,12 @@ struct EmbArgs {
   const bf16_t* dy;
   float* dz;       // fp32 [T][D]
   float* part;     // [grid][2][D]
+  // packed rows (unpadded step): row -> padded row (position = padded row % S, dropout
+  // hashed by the padded row; -1 = bucket filler, treated as padded row 0)
+  const int* row_map;
 };
+
+DEV int padded_row(const EmbArgs& a, int row) { return a.row_map ? max(a.row_map[row], 0) : row; }
 
 DEV long load_id(const EmbArgs& a, int t) {
   return a.ids64 ? reinterpret_cast<const long long*>(a.ids)[t] : reinterpret_cast<const int*>(a.ids)[t];
@@ -264,7 +269,8 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbArgs a) {
   if (row >= a.T) return;
   const int D = a.D;
   const long id = load_id(a, row);
-  const int s = row % a.S;
+  const int prow = padded_row(a, row);
+  const int s = prow % a.S;
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
   float z[NC][4], sum = 0.f;
@@ -293,8 +299,9 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbArgs a) {
     float y[4] = {(z[c][0] - mean) * rstd * g.x + b.x, (z[c][1] - mean) * rstd * g.y + b.y,
                   (z[c][2] - mean) * rstd * g.z + b.z, (z[c][3] - mean) * rstd * g.w + b.w};
     if (drop) {
+      const size_t hoff = (size_t)prow * D + col;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = drop_keep(seed, (uint32_t)(off + e), a.thr) ? y[e] * a.dscale : 0.f;
+      for (int e = 0; e < 4; ++e) y[e] = drop_keep(seed, (uint32_t)(hoff + e), a.thr) ? y[e] * a.dscale : 0.f;
     }
     *reinterpret_cast<uint2*>(a.y + off) = make_uint2(pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]));
   }
@@ -312,7 +319,8 @@ __global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
   const int nw = blockDim.x >> 6;
   for (int row = blockIdx.x * nw + w; row < a.T; row += gridDim.x * nw) {
     const long id = load_id(a, row);
-    const int s = row % a.S;
+    const int prow = padded_row(a, row);
+    const int s = prow % a.S;
     const float mean = a.mean[row], rstd = a.rstd[row];
     float xh[NC][4], gd[NC][4], s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -326,8 +334,9 @@ __global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
       const uint2 dv = *reinterpret_cast<const uint2*>(a.dy + off);
       float d4[4] = {lo_bf(dv.x), hi_bf(dv.x), lo_bf(dv.y), hi_bf(dv.y)};
       if (drop) {
+        const size_t hoff = (size_t)prow * D + col;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) d4[e] = drop_keep(seed, (uint32_t)(off + e), a.thr) ? d4[e] * a.dscale : 0.f;
+        for (int e = 0; e < 4; ++e) d4[e] = drop_keep(seed, (uint32_t)(hoff + e), a.thr) ? d4[e] * a.dscale : 0.f;
       }
       const float4 g = *reinterpret_cast<const float4*>(a.gamma + col);
       const float g4[4] = {g.x, g.y, g.z, g.w};
@@ -361,15 +370,23 @@ __global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
 
 // dpos[s][:] = sum_b dz[b*S + s][:] -- fixed order; all B loads of a column issued
 // back to back.  Rows s >= S are handled by a memset (first write) on the host side.
+// cu (packed rows): sequence b's position s is row cu[b] + s when s < its length; the
+// padded layout's extra terms are exact zeros, so both layouts give the same sums.
 __global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* dpos, int B, int S, int D,
-                                                       int accumulate) {
+                                                       int accumulate, const int* cu) {
   const int s = blockIdx.x;
   for (int col = threadIdx.x; col < D; col += 256) {
     float acc = accumulate ? dpos[(size_t)s * D + col] : 0.f;
     for (int b0 = 0; b0 < B; b0 += 16) {
       float v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = b0 + u < B ? dz[((size_t)(b0 + u) * S + s) * D + col] : 0.f;
+      for (int u = 0; u < 16; ++u) {
+        const int b = b0 + u;
+        if (cu)
+          v[u] = b < B && s < cu[b + 1] - cu[b] ? dz[((size_t)cu[b] + s) * D + col] : 0.f;
+        else
+          v[u] = b < B ? dz[((size_t)b * S + s) * D + col] : 0.f;
+      }
 #pragma unroll
       for (int u = 0; u < 16; ++u) acc += v[u];
     }
@@ -614,12 +631,12 @@ __global__ __launch_bounds__(256) void colsum_batched_kernel(ColsumBatch cb) {
 
 constexpr int LN_GRID = 256;
 constexpr int LN_BWD_THREADS = 512;
-// LayerNorm backward: 256-thread blocks (8 rows per pass) on up to 512 blocks, so a packed
-// ~2.7 k-row batch spreads over every CU (512-thread blocks gave 168 blocks); FD_LN_BWD_WIDE=0
-// restores 512 threads x 256 blocks.  The partial rows are finalised by the batched colsum.
+// LayerNorm backward: 512-thread blocks (16 rows per pass) on up to 256 blocks.  FD_LN_BWD_WIDE=1
+// selects 256-thread blocks on up to 512 (spreads a packed ~2.7 k-row batch over every CU) --
+// measured SLOWER, 2.476 vs 2.448 ms/step (more partial rows for the batched colsum).
 constexpr int LN_BWD_GRID_MAX = 512;
 int ln_bwd_threads() {
-  static const int t = [] { const char* e = getenv("FD_LN_BWD_WIDE"); return (e && atoi(e) == 0) ? 512 : 256; }();
+  static const int t = [] { const char* e = getenv("FD_LN_BWD_WIDE"); return (e && atoi(e) == 1) ? 256 : 512; }();
   return t;
 }
 
@@ -662,12 +679,13 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
 
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
-               const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, hipStream_t st) {
+               const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const int* row_map,
+               hipStream_t st) {
   if (D != 768) return 1;
   EmbArgs a{};
   a.ids = ids; a.ids64 = ids64; a.word = (const bf16_t*)word; a.pos = (const bf16_t*)pos; a.gamma = gamma;
   a.beta = beta; a.y = (bf16_t*)y; a.mean = mean; a.rstd = rstd; a.T = T; a.S = S; a.D = D; a.eps = eps;
-  a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
+  a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.row_map = row_map;
   hipLaunchKernelGGL(emb_fwd_kernel<3>, dim3((T + 3) / 4), dim3(256), 0, st, a);
   return 0;
 }
@@ -678,19 +696,21 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                const void* word, const void* pos, const float* gamma, const float* mean, const float* rstd,
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
-               int accumulate, unsigned char* now, unsigned char* ever, hipStream_t st) {
+               int accumulate, unsigned char* now, unsigned char* ever, const int* row_map, const int* cu,
+               hipStream_t st) {
   if (D != 768) return 1;
   EmbArgs a{};
   a.dy = (const bf16_t*)dy; a.ids = ids; a.ids64 = ids64; a.word = (const bf16_t*)word;
   a.pos = (const bf16_t*)pos; a.gamma = gamma; a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = dz_buf;
   a.part = work; a.T = T; a.S = S; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
+  a.row_map = row_map;
   const int grid = std::min(LN_GRID, (T + 7) / 8);
   hipLaunchKernelGGL(emb_bwd_kernel<3>, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
                      st, a);
   hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 2), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, (float*)nullptr, accumulate);
   if (!accumulate && P > S) hipMemsetAsync(dpos + (size_t)S * D, 0, (size_t)(P - S) * D * sizeof(float), st);
-  hipLaunchKernelGGL(pos_grad_kernel, dim3(S), dim3(256), 0, st, dz_buf, dpos, B, S, D, accumulate);
+  hipLaunchKernelGGL(pos_grad_kernel, dim3(S), dim3(256), 0, st, dz_buf, dpos, B, S, D, accumulate, cu);
   if (!accumulate) {
     if (now) hipMemsetAsync(now, 0, (size_t)V, st);
     else hipMemsetAsync(dword, 0, (size_t)V * D * sizeof(float), st);

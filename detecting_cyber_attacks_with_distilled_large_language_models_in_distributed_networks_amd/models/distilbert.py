@@ -432,23 +432,24 @@ class DDoSClassifier(nn.Module):
         token = self._grad_token if torch.is_grad_enabled() else None
         if token is not None and self.transposed_dx:
             K.transpose_many([L[k] for L in layers for k in L["wT"]], [L["wT"][k] for L in layers for k in L["wT"]])
-        x = EmbeddingFn.apply(token, ids, emb["word"], emb["pos"], emb["ln_w"], emb["ln_b"], emb["sinks"], rc)
         hrc = rc
         if tokens is not None and self.unpad and self.packed_rows(tokens, B, S) < B * S:
-            # Unpadded blocks: gather the real tokens (sequence-contiguous, filler rows at the
-            # end), varlen attention over cu, dropout hashed by the padded row (same masks as
-            # the padded path).  Filler rows repeat padded row 0: finite, and their gradient
-            # is exactly 0 (they reach neither a real token nor the loss).
+            # Unpadded step: only the real tokens (sequence-contiguous, filler rows at the end)
+            # are embedded and run through the blocks; varlen attention over cu; positions and
+            # dropout follow the padded row (same masks as the padded path).  Filler rows act
+            # as padded row 0: finite, and their gradient is exactly 0 (they reach neither a
+            # real token nor the loss).
             rows = self.packed_rows(tokens, B, S)
             m = mask.reshape(-1)
             row_map = torch.nonzero_static(m, size=rows, fill_value=-1).squeeze(1).to(torch.int32)
             cu = torch.zeros(B + 1, dtype=torch.int32, device=ids.device)
             cu[1:] = torch.cumsum(mask.sum(1, dtype=torch.int32), 0, dtype=torch.int32)
-            x = x.index_select(0, row_map.clamp(min=0))
+            ids = ids.reshape(-1).index_select(0, row_map.clamp(min=0))
             rc.cu, rc.row_map = cu, row_map
             # the head reads one [CLS] row per sequence: present it as a [B, 1] layout
             hrc = RunCtx(B=B, S=1, H=rc.H, kbias=rc.kbias, seed=rc.seed, training=rc.training, eps=rc.eps,
                          p_hidden=rc.p_hidden, p_attn=rc.p_attn, p_head=rc.p_head)
+        x = EmbeddingFn.apply(token, ids, emb["word"], emb["pos"], emb["ln_w"], emb["ln_b"], emb["sinks"], rc)
         for i, L in enumerate(layers):
             x = LayerFn.apply(x, L, rc, i)
         if rc.cu is not None:

@@ -95,7 +95,7 @@ class EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, token, ids, word, pos, gamma, beta, sinks, rc: RunCtx):
         p = rc.p_hidden if rc.training else 0.0
-        y, mean, rstd = K.emb_fwd(ids, word, pos, gamma, beta, rc.S, rc.eps, rc.seed, 1, p)
+        y, mean, rstd = K.emb_fwd(ids, word, pos, gamma, beta, rc.S, rc.eps, rc.seed, 1, p, rc.row_map)
         ctx.rc, ctx.sinks, ctx.p = rc, sinks, p
         ctx.tensors = (ids, word, pos, gamma, mean, rstd)
         return y
@@ -110,7 +110,7 @@ class EmbeddingFn(torch.autograd.Function):
             assert s[k].accumulate() == acc
         now, ever = s.get("flags") or (None, None)
         K.emb_bwd(dy, ids, srt, perm, word, pos, gamma, mean, rstd, s["word"].buf, s["pos"].buf, s["ln_w"].buf,
-                  s["ln_b"].buf, ctx.rc.S, ctx.rc.seed, 1, ctx.p, acc, now, ever)
+                  s["ln_b"].buf, ctx.rc.S, ctx.rc.seed, 1, ctx.p, acc, now, ever, ctx.rc.row_map, ctx.rc.cu)
         if ctx.rc.wgrad is not None:  # join the weight-gradient stream: every grad is final after this node
             torch.cuda.current_stream().wait_stream(ctx.rc.wgrad)
         if ctx.rc.colsum_jobs:

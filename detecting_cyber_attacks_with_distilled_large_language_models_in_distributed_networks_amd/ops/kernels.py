@@ -186,27 +186,29 @@ def group_ids(ids: torch.Tensor):
     return srt, perm
 
 
-def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p):
+def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p, row_map=None):
+    """row_map (int32 [T]): ``ids`` are packed real tokens; positions and dropout follow the padded row."""
     T = ids.numel()
     D = gamma.numel()
     y = torch.empty(T, D, dtype=torch.bfloat16, device=ids.device)
     mean = torch.empty(T, dtype=torch.float32, device=ids.device)
     rstd = torch.empty(T, dtype=torch.float32, device=ids.device)
     thr, sc = _drop(p)
-    ext().emb_fwd(ids.contiguous(), word, pos, gamma, beta, y, mean, rstd, S, eps, seed, site, thr, sc)
+    ext().emb_fwd(ids.contiguous(), word, pos, gamma, beta, y, mean, rstd, S, eps, seed, site, thr, sc, row_map)
     return y, mean, rstd
 
 
 def emb_bwd(dy, ids, sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos, dgamma, dbeta, S, seed, site, p,
-            accumulate=False, now=None, ever=None):
-    """now/ever: optional uint8 [V] row flags -> sparse word gradient (see ArenaAdam)."""
+            accumulate=False, now=None, ever=None, row_map=None, cu=None):
+    """now/ever: optional uint8 [V] row flags -> sparse word gradient (see ArenaAdam).
+    row_map / cu: packed rows (position gradient summed per sequence over cu)."""
     T = ids.numel()
     D = gamma.numel()
     dz = workspace(ids.device, "emb_dz", T * D)
     ws = workspace(ids.device, "emb_work", max(T * D, LN_GRID * 3 * D))
     thr, sc = _drop(p)
     ext().emb_bwd(dy.contiguous(), ids.contiguous(), sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos,
-                  dgamma, dbeta, dz, ws, S, seed, site, thr, sc, accumulate, now, ever)
+                  dgamma, dbeta, dz, ws, S, seed, site, thr, sc, accumulate, now, ever, row_map, cu)
 
 
 # ------------------------------------------------------------------ head / metrics / optimizer

@@ -97,3 +97,34 @@ def test_split_sizes_match_reference():
     n = 22574
     (a, _), (b, _), (c, _) = split_60_20_20(list(range(n)), [0] * n, 42)
     assert (len(a), len(b), len(c)) == (13544, 4515, 4515)
+
+
+REF_CSV = "/root/reference/CICIDS2017.csv"
+
+
+@pytest.mark.skipif(not __import__("os").path.exists(REF_CSV), reason="reference CSV not mounted")
+@pytest.mark.parametrize("seed", [42, 43])
+def test_preprocess_reference_csv_parity(seed):
+    """The reference's own committed sample (2,885 rows, 3 with Infinity) through our
+    preprocess_data == the reference pipeline written out in plain pandas (client1.py:68-93):
+    inf -> NaN -> column mean, 10 % sample with the client seed, the 10-sentence template."""
+    texts, labels = preprocess_data(REF_CSV, data_fraction=0.1, seed=seed)
+    df = pd.read_csv(REF_CSV)
+    df = df.replace([np.inf, -np.inf], np.nan)
+    df = df.fillna(df.mean(numeric_only=True))
+    df = df.sample(frac=0.1, random_state=seed)
+
+    def row_text(r):
+        return (f"Destination port is {r['Destination Port']}. Flow duration is {r['Flow Duration']} microseconds. "
+                f"Total forward packets are {r['Total Fwd Packets']}. "
+                f"Total backward packets are {r['Total Backward Packets']}. "
+                f"Total length of forward packets is {r['Total Length of Fwd Packets']} bytes. "
+                f"Total length of backward packets is {r['Total Length of Bwd Packets']} bytes. "
+                f"Maximum forward packet length is {r['Fwd Packet Length Max']}. "
+                f"Minimum forward packet length is {r['Fwd Packet Length Min']}. "
+                f"Flow bytes per second is {r['Flow Bytes/s']}. Flow packets per second is {r['Flow Packets/s']}.")
+    ref_texts = df.apply(row_text, axis=1).tolist()
+    ref_labels = df["Label"].apply(lambda x: 1 if x == "DDoS" else 0).tolist()
+    assert len(texts) == len(ref_texts) == round(0.1 * len(pd.read_csv(REF_CSV)))
+    assert texts == ref_texts
+    assert labels == ref_labels and set(labels) == {0}  # the committed sample is all BENIGN

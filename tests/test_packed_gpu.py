@@ -78,12 +78,14 @@ def test_packed_model_matches_padded(train):
         outs.append((loss.detach().clone(), logits.clone(), m.arena.grad.clone(), m.emb_now.clone()))
     (l0, z0, g0, e0), (l1, z1, g1, e1) = outs
     assert rel(z1, z0) < 1e-3 and abs(float(l1 - l0)) < 1e-3
-    assert torch.equal(e0, e1)
+    # padded path also flags [PAD] (id 0, whose gradient is exactly 0); packed never sees it
+    assert torch.equal(e0[1:], e1[1:]) and int(e1[0]) == 0
     dense = torch.ones_like(g0, dtype=torch.bool)
     woff, V, D = m.word_embedding_span()
     dense[woff:woff + V * D] = False
     assert rel(g1[dense], g0[dense]) < 2e-2
-    rows = e0.bool()
+    assert not g0[woff:woff + D].any()  # the [PAD] row's padded-path gradient is exactly 0
+    rows = e1.bool()
     assert rel(g1[woff:woff + V * D].view(V, D)[rows], g0[woff:woff + V * D].view(V, D)[rows]) < 2e-2
 
 
