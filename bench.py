@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--gpus-per-client", type=int, default=1,
                     help="k > 1: each federated client is k data-parallel GPUs (per-step gradient all-reduce); "
                          "--batch-size stays the per-client batch")
+    ap.add_argument("--mode", default="train", choices=["train", "infer"],
+                    help="infer: serving throughput of the HIP-graph forward (reference evaluate_model rate)")
     ap.add_argument("--teacher", action="store_true",
                     help="distillation step (BASELINE.json config 5): BERT-base teacher fwd + DistilBERT student")
     args = ap.parse_args()
@@ -113,6 +115,8 @@ def main():
                 yield b
 
     it = batches()
+    if args.mode == "infer":
+        return _bench_infer(args, model, it, di, comm, B, S)
     for _ in range(args.warmup):
         b = next(it)
         step(b["input_ids"], b["attention_mask"], b["labels"], b.get("n_tokens"))
@@ -182,6 +186,47 @@ def main():
             "mean_loss": round(loss, 5),
         }
         print(json.dumps(out), flush=True)
+    comm.shutdown()
+
+
+def _bench_infer(args, model, it, di, comm, B, S):
+    """Inference batches/s (no grad, HIP-graph forward, probabilities + labels on device).
+    Reference: evaluate_model at 8.87-14.0 batches/s of 16 rows (client1_terminal_output.txt:16,21)."""
+    from importlib import import_module
+    engine = import_module(f"{PKG}.engine")
+    fwd = engine.GraphedForward(model, enabled=not args.no_graph)
+    model.eval()
+    dev = model.device
+    batches = [next(it) for _ in range(args.warmup + args.steps)]
+    for b in batches:  # warm every (shape, bucket) graph before timing
+        fwd(b["input_ids"], b["attention_mask"], b.get("n_tokens"))
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    probs = torch.empty(args.steps, B, device=dev)
+    sync()
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i, b in enumerate(batches[args.warmup:]):
+        logits = fwd(b["input_ids"], b["attention_mask"], b.get("n_tokens"))
+        probs[i] = torch.softmax(logits.float(), dim=1)[:, 1]
+    sync()
+    comm.barrier()
+    sync()
+    dt = comm.all_reduce_max(time.perf_counter() - t0)
+    n = di.world_size
+    per = args.steps / dt
+    if di.is_main:
+        print(json.dumps({
+            "metric": f"inference batches/sec/GPU (DistilBERT DDoSClassifier seq{S} bs{B})", "value": round(per * n, 3),
+            "unit": f"batches/s (sum over GPUs; bs{B} x seq{S})", "n_gpus": n, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": round(per * B / (14.0 * 16), 3),
+            "vs_baseline_basis": "rows/s / 224 (reference evaluate_model best: 14.0 batches/s x 16 rows)",
+            "dtype": "bf16" if args.impl == "hip" else "fp32", "data": "synthetic CICIDS2017-shaped flows; random-init",
+            "config": {"model": "DistilBERT-base + Linear(768,2)", "global_batch": B * n, "seq_len": S,
+                       "parallelism": f"replicated x{n}"},
+            "rows_per_sec_total": round(per * n * B, 1), "hip_graphs": len(fwd.graphs), "graph_error": fwd.failed}),
+            flush=True)
     comm.shutdown()
 
 

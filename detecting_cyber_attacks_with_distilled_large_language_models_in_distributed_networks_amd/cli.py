@@ -5,6 +5,8 @@
            --client-index k`` it is the reference's ``python clientK.py``
   server   the reference's ``python server.py``: TCP gather -> FedAvg -> broadcast
   launch   spawn N local ranks (torch.distributed.run, 127.0.0.1) running ``client``
+  predict  classify every row of a CICIDS2017-format CSV with a trained checkpoint (serving path:
+           unpadded HIP forward replayed from HIP graphs); writes probabilities + labels
   bench    the headline benchmark (bench.py)
   scaling  run bench.py at several GPU counts and write the scaling curve
   gen-data write a synthetic CICIDS2017-shaped CSV
@@ -90,6 +92,48 @@ def _launch(argv):
     sys.exit(subprocess.call(cmd, env=env))
 
 
+def _predict(argv):
+    ap = argparse.ArgumentParser(prog="predict")
+    ap.add_argument("--checkpoint", required=True, help="clientN_model.pth / ddos_distilbert_model.pth")
+    ap.add_argument("--csv", default=None, help="CICIDS2017-format CSV (default: synthetic rows)")
+    ap.add_argument("--rows", type=int, default=20000, help="synthetic rows when --csv is not given")
+    ap.add_argument("--batch-size", type=int, default=64)
+    ap.add_argument("--max-len", type=int, default=128)
+    ap.add_argument("--out", default="predictions.csv")
+    ap.add_argument("--no-graph", action="store_true")
+    ns = ap.parse_args(argv)
+    import numpy as np
+    import pandas as pd
+    import torch
+    from .data import CICIDS2017Dataset, DeviceLoader, WordPieceTokenizer, generate_cicids2017
+    from .data.featurize import clean_frame, render_texts
+    from .engine import predict
+    from .models import DDoSClassifier
+    from .utils.checkpoint import load_model
+    from .utils.metrics import binary_prf
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    frame = pd.read_csv(ns.csv) if ns.csv else generate_cicids2017(ns.rows, seed=7)
+    frame = clean_frame(frame)
+    texts = render_texts(frame)
+    has_label = "Label" in frame.columns
+    labels = (frame["Label"].to_numpy() == "DDoS").astype(np.int64) if has_label else np.zeros(len(frame), np.int64)
+    ds = CICIDS2017Dataset(texts, labels.tolist(), WordPieceTokenizer(), ns.max_len)
+    model = DDoSClassifier(device=dev)
+    if not load_model(model, ns.checkpoint):
+        raise SystemExit(f"cannot load {ns.checkpoint}")
+    probs, preds, timing = predict(model, DeviceLoader(ds, ns.batch_size, device=dev), graphed=not ns.no_graph)
+    out = pd.DataFrame({"row": np.arange(len(preds)), "prob_ddos": probs, "pred": preds})
+    if has_label:
+        out["label"] = labels
+        tp = int(((preds == 1) & (labels == 1)).sum())
+        fp = int(((preds == 1) & (labels == 0)).sum())
+        fn = int(((preds == 0) & (labels == 1)).sum())
+        p_, r_, f1 = binary_prf(tp, fp, fn)
+        timing.update(accuracy=float(100.0 * (preds == labels).mean()), precision=p_, recall=r_, f1=f1)
+    out.to_csv(ns.out, index=False)
+    print(json.dumps({"out": ns.out, **timing}))
+
+
 def _bench(argv):
     sys.exit(subprocess.call([sys.executable, os.path.join(ROOT, "bench.py")] + argv))
 
@@ -145,7 +189,8 @@ def _tokenize(argv):
     print(tok(text, max_length=128)["input_ids"])
 
 
-COMMANDS = {"client": _client, "server": _server, "launch": _launch, "bench": _bench, "scaling": _scaling,
+COMMANDS = {"client": _client, "server": _server, "launch": _launch, "predict": _predict, "bench": _bench,
+            "scaling": _scaling,
             "gen-data": _gen_data, "tokenize": _tokenize}
 
 

@@ -36,9 +36,16 @@ def evaluate_model(model, loader, criterion=None, device=None, log=None, name: s
         acc = torch.zeros(1, dtype=torch.float64, device=dev)
         counts = torch.zeros(5, dtype=torch.int64, device=dev)
         packed = getattr(model, "impl", None) == "hip"
+        fwd = None
+        if packed:  # unpadded HIP forward replayed from graphs (cached on the model across evals)
+            from .infer import GraphedForward
+            fwd = getattr(model, "_graphed_eval", None)
+            if fwd is None or fwd.model is not model:
+                fwd = GraphedForward(model)
+                model._graphed_eval = fwd
         for batch in loader:
-            if packed and batch.get("n_tokens") is not None:  # unpadded blocks (no host sync)
-                logits = model(batch["input_ids"], batch["attention_mask"], tokens=batch["n_tokens"])
+            if fwd is not None and batch.get("n_tokens") is not None:
+                logits = fwd(batch["input_ids"], batch["attention_mask"], batch["n_tokens"])
             else:
                 logits = model(batch["input_ids"], batch["attention_mask"])
             b = logits.shape[0]
