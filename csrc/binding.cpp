@@ -50,6 +50,8 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
                int accumulate, unsigned char* now, unsigned char* ever, const int* row_map, const int* cu, hipStream_t st);
+int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
+            int* cu, long long* ids_packed, hipStream_t st);
 int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, int defer, int* nblk_out,
                    hipStream_t st);
 int fd_colsum_batched(int n, const float* const* parts, float* const* outs, const int* nblk, const int* stride,
@@ -57,10 +59,10 @@ int fd_colsum_batched(int n, const float* const* parts, float* const* outs, cons
 int fd_rank_sort(const void* ids, int ids64, int T, long long* sorted, long long* perm, hipStream_t st);
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
-                float* logits, float* loss, float* dlogits, float* row_loss, hipStream_t st);
+                float* logits, float* loss, float* dlogits, float* row_loss, const int* cls, int T, hipStream_t st);
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
-                int accumulate, hipStream_t st);
+                int accumulate, const int* cls, int T, hipStream_t st);
 int fd_eval_metrics(const float* logits, const long long* labels, int B, double* acc, long long* counts,
                     float* prob1, long long* preds, hipStream_t st);
 int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float lr,
@@ -151,6 +153,22 @@ void gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C0, 
                        A1.data_ptr(), B1.data_ptr(), C1.data_ptr<float>(), (int)A1.size(1), (int)B1.size(1), (int)K,
                        workspace.data_ptr<float>(), workspace.numel(), accumulate ? 1 : 0, stream()),
            "gemm_dw2");
+}
+
+// Unpadded-step layout in one launch: row_map [rows] int32, cu [B+1] int32, ids_packed [rows] int64.
+void pack(const at::Tensor& mask, const at::Tensor& ids, const at::Tensor& row_map, const at::Tensor& cu,
+          const at::Tensor& ids_packed) {
+  TORCH_CHECK(mask.is_cuda() && mask.is_contiguous() && ids.is_cuda() && ids.is_contiguous(), "pack: GPU inputs");
+  TORCH_CHECK(mask.dim() == 2 && ids.sizes() == mask.sizes(), "pack: mask and ids must both be [B, S]");
+  need(row_map, at::kInt, "row_map");
+  need(cu, at::kInt, "cu");
+  need(ids_packed, at::kLong, "ids_packed");
+  const int64_t B = mask.size(0), S = mask.size(1);
+  TORCH_CHECK(cu.numel() == B + 1 && ids_packed.numel() == row_map.numel() && row_map.numel() >= 1, "pack: sizes");
+  check_rc(fd_pack(mask.data_ptr(), (int)mask.element_size(), ids.data_ptr(), (int)ids.element_size(), (int)B, (int)S,
+                   (int)row_map.numel(), row_map.data_ptr<int>(), cu.data_ptr<int>(),
+                   reinterpret_cast<long long*>(ids_packed.data_ptr()), stream()),
+           "pack");
 }
 
 // ---------------------------------------------------------------- native RCCL communicator
@@ -484,8 +502,9 @@ void colsum_batched(const std::vector<at::Tensor>& parts, const std::vector<std:
 void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& W, const at::Tensor& bias,
               const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& labels,
               const at::Tensor& logits, const c10::optional<at::Tensor>& loss, const c10::optional<at::Tensor>& dlogits,
-              const c10::optional<at::Tensor>& row_loss) {
+              const c10::optional<at::Tensor>& row_loss, const c10::optional<at::Tensor>& cls) {
   need_opt(row_loss, at::kFloat, "row_loss");
+  need_opt(cls, at::kInt, "cls");
   need(hidden, at::kBFloat16, "hidden");
   need(W, at::kFloat, "W");
   need(bias, at::kFloat, "bias");
@@ -494,7 +513,10 @@ void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
   need_opt(loss, at::kFloat, "loss");
   need_opt(dlogits, at::kFloat, "dlogits");
   const int64_t D = W.size(1);
-  TORCH_CHECK(W.size(0) == 2 && hidden.numel() == B * S * D && logits.numel() == B * 2, "head_fwd: shapes");
+  const bool packed = cls.has_value() && cls->defined();
+  TORCH_CHECK(W.size(0) == 2 && hidden.numel() % D == 0 && (packed || hidden.numel() == B * S * D) &&
+                  logits.numel() == B * 2 && (!packed || cls->numel() == B),
+              "head_fwd: shapes");
   if (labels.has_value() && labels->defined())
     TORCH_CHECK(labels->numel() == B && loss.has_value() && dlogits.has_value() && dlogits->numel() == 2 * B &&
                     row_loss.has_value() && row_loss->numel() >= B,
@@ -502,13 +524,14 @@ void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
   check_rc(fd_head_fwd(hidden.data_ptr(), (int)B, (int)S, (int)D, W.data_ptr<float>(), bias.data_ptr<float>(),
                        seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale,
                        ptr<const long long>(labels), logits.data_ptr<float>(), ptr<float>(loss), ptr<float>(dlogits),
-                       ptr<float>(row_loss), stream()),
+                       ptr<float>(row_loss), ptr<int>(cls), (int)(hidden.numel() / D), stream()),
            "head_fwd");
 }
 
 void head_bwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& W, const at::Tensor& seed, int64_t site,
               int64_t thr, double dscale, const at::Tensor& dlogits, const at::Tensor& dW, const at::Tensor& db,
-              const at::Tensor& dhidden, bool accumulate) {
+              const at::Tensor& dhidden, bool accumulate, const c10::optional<at::Tensor>& cls) {
+  need_opt(cls, at::kInt, "cls");
   need(hidden, at::kBFloat16, "hidden");
   need(W, at::kFloat, "W");
   need(dlogits, at::kFloat, "dlogits");
@@ -516,12 +539,15 @@ void head_bwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
   need(db, at::kFloat, "db");
   need(dhidden, at::kBFloat16, "dhidden");
   const int64_t D = W.size(1);
-  TORCH_CHECK(hidden.numel() == B * S * D && dhidden.numel() == hidden.numel() && dlogits.numel() == 2 * B &&
-                  dW.numel() == 2 * D && db.numel() == 2,
+  const bool packed = cls.has_value() && cls->defined();
+  TORCH_CHECK(hidden.numel() % D == 0 && (packed || hidden.numel() == B * S * D) && (!packed || cls->numel() == B) &&
+                  dhidden.numel() == hidden.numel() && dlogits.numel() == 2 * B && dW.numel() == 2 * D &&
+                  db.numel() == 2,
               "head_bwd: shapes");
   check_rc(fd_head_bwd(hidden.data_ptr(), (int)B, (int)S, (int)D, W.data_ptr<float>(), seedp(seed), (uint32_t)site,
                        (uint32_t)thr, (float)dscale, dlogits.data_ptr<float>(), dW.data_ptr<float>(),
-                       db.data_ptr<float>(), dhidden.data_ptr(), accumulate ? 1 : 0, stream()),
+                       db.data_ptr<float>(), dhidden.data_ptr(), accumulate ? 1 : 0, ptr<int>(cls),
+                       (int)(hidden.numel() / D), stream()),
            "head_bwd");
 }
 
@@ -600,6 +626,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm);
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_dw2", &gemm_dw2);
+  m.def("pack", &pack);
   m.def("transpose_batched", &transpose_batched);
   m.def("comm_load", &comm_load);
   m.def("comm_unique_id", &comm_unique_id);

@@ -38,7 +38,15 @@ struct HeadArgs {
   float* db;             // [2]
   bf16_t* dhidden;       // [B*S, D]; only CLS rows written
   int accumulate;
+  // packed (unpadded) rows: sequence b's [CLS] is row cls[b] of a [T, D] hidden (nullable:
+  // padded layout, row b*S); rows are clamped to T-1
+  const int* cls;
+  int T;
 };
+
+DEV size_t cls_row(const HeadArgs& a, int b) {
+  return a.cls ? (size_t)min(max(a.cls[b], 0), a.T - 1) : (size_t)b * a.S;
+}
 
 // One wave per batch row (grid = ceil(B/4) blocks); per-row loss to row_loss,
 // reduced in a fixed order by head_loss_mean_kernel.
@@ -48,7 +56,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
   if (b >= a.B) return;
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
-  const bf16_t* x = a.hidden + (size_t)b * a.S * a.D;
+  const bf16_t* x = a.hidden + cls_row(a, b) * a.D;
   float z0 = 0.f, z1 = 0.f;
   for (int col = 4 * lane; col < a.D; col += 256) {
     const uint2 xv = *reinterpret_cast<const uint2*>(x + col);
@@ -96,10 +104,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
       const float d0 = a.dlog_in[2 * b], d1 = a.dlog_in[2 * b + 1];
       const bool keep = !drop || drop_keep(seed, (uint32_t)(b * a.D + col), a.thr);
       const float sc = drop ? (keep ? a.dscale : 0.f) : 1.f;
-      const float x = bf2f(a.hidden[(size_t)b * a.S * a.D + col]) * sc;
+      const float x = bf2f(a.hidden[cls_row(a, b) * a.D + col]) * sc;
       g0 += d0 * x;
       g1 += d1 * x;
-      a.dhidden[(size_t)b * a.S * a.D + col] = (bf16_t)f2bf((d0 * w0 + d1 * w1) * sc);
+      a.dhidden[cls_row(a, b) * a.D + col] = (bf16_t)f2bf((d0 * w0 + d1 * w1) * sc);
     }
     a.dW[col] = a.accumulate ? a.dW[col] + g0 : g0;
     a.dW[a.D + col] = a.accumulate ? a.dW[a.D + col] + g1 : g1;
@@ -270,9 +278,10 @@ extern "C" {
 
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
-                float* logits, float* loss, float* dlogits, float* row_loss, hipStream_t st) {
+                float* logits, float* loss, float* dlogits, float* row_loss, const int* cls, int T, hipStream_t st) {
   if (B > 65536) return 1;
   HeadArgs a{};
+  a.cls = cls; a.T = T;
   a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W; a.bias = bias;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.labels = labels;
   a.logits = logits; a.loss = loss; a.dlogits = dlogits; a.row_loss = row_loss;
@@ -284,8 +293,9 @@ int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const f
 
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
-                int accumulate, hipStream_t st) {
+                int accumulate, const int* cls, int T, hipStream_t st) {
   HeadArgs a{};
+  a.cls = cls; a.T = T;
   a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.dlog_in = dlogits;
   a.dW = dW; a.db = db; a.dhidden = (bf16_t*)dhidden; a.accumulate = accumulate;

@@ -1,0 +1,93 @@
+// Unpadded-step bookkeeping in one launch (gfx950).
+//
+// From the padded batch (mask, ids: [B, S]) build the packed layout the model runs on:
+//   row_map[r]    padded position of packed row r (-1 for the bucket's filler rows)
+//   cu[b]         first packed row of sequence b (cu[B] = real tokens)
+//   ids_packed[r] token id of packed row r (filler rows repeat position 0's id)
+// i.e. a stream compaction of the mask.  One 1024-thread workgroup scans the B*S flags in
+// 4096-position chunks (wave prefix sums through DPP shuffles, wave totals through LDS),
+// replacing the ~10 small library launches (nonzero_static = flag + block sums + scan +
+// scatter, mask sum, cumsum, clamp, gather) it took in torch.  Reference: the padding
+// the reference computes on (client1.py:38-45, padding='max_length').
+#include "common.h"
+
+namespace {
+
+template <typename M, typename I>
+__global__ __launch_bounds__(1024) void pack_kernel(const M* mask, const I* ids, int n, int S, int B, int rows,
+                                                    int* row_map, int* cu, long long* ids_packed) {
+  __shared__ int wsum[16];
+  __shared__ int carry_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) carry_s = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 4096) {
+    int f[4], local = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = base + 4 * tid + j;
+      f[j] = (p < n && mask[p] != 0) ? 1 : 0;
+      local += f[j];
+    }
+    // inclusive wave scan
+    int incl = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int before = 0;
+    for (int i = 0; i < w; ++i) before += wsum[i];
+    const int carry = carry_s;
+    int off = carry + before + incl - local;  // exclusive prefix of this thread's first position
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = base + 4 * tid + j;
+      if (p < n && p % S == 0) cu[p / S] = off;  // tokens before sequence p / S
+      if (f[j]) {
+        if (off < rows) {
+          row_map[off] = p;
+          ids_packed[off] = (long long)ids[p];
+        }
+        ++off;
+      }
+    }
+    __syncthreads();  // every wave has read carry_s and wsum
+    if (tid == 1023) carry_s = off;  // the last thread's running offset = new carry
+    __syncthreads();
+  }
+  const int total = carry_s;
+  if (tid == 0) cu[B] = total;
+  const long long id0 = (long long)ids[0];
+  for (int r = total + tid; r < rows; r += 1024) {
+    row_map[r] = -1;
+    ids_packed[r] = id0;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// mask_bytes / ids_bytes: 8 (int64) or 4 (int32) / 1 (uint8 mask).  n = B * S <= 1 << 20.
+int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
+            int* cu, long long* ids_packed, hipStream_t st) {
+  const int n = B * S;
+  if (B <= 0 || S <= 0 || rows <= 0 || n > (1 << 20)) return 1;
+#define FD_PACK(MT, IT)                                                                                        \
+  hipLaunchKernelGGL((pack_kernel<MT, IT>), dim3(1), dim3(1024), 0, st, (const MT*)mask, (const IT*)ids, n, S, B, \
+                     rows, row_map, cu, ids_packed)
+  if (mask_bytes == 8 && ids_bytes == 8) FD_PACK(long long, long long);
+  else if (mask_bytes == 8 && ids_bytes == 4) FD_PACK(long long, int);
+  else if (mask_bytes == 4 && ids_bytes == 8) FD_PACK(int, long long);
+  else if (mask_bytes == 4 && ids_bytes == 4) FD_PACK(int, int);
+  else if (mask_bytes == 1 && ids_bytes == 8) FD_PACK(unsigned char, long long);
+  else if (mask_bytes == 1 && ids_bytes == 4) FD_PACK(unsigned char, int);
+  else return 2;
+#undef FD_PACK
+  return 0;
+}
+
+}  // extern "C"

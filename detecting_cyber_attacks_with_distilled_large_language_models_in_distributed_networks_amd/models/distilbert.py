@@ -251,6 +251,9 @@ class DDoSClassifier(nn.Module):
         self.pack_quantum = 128
         # HIP path: finalise all bias / LN-affine column sums of a backward in one launch
         self.defer_colsum = True
+        # HIP path: the per-step W^T copies are built on a side stream concurrently with the forward
+        self.overlap_transpose = True
+        self._tstream = None
         self.torch_counter = 0
         self._grad_token = None
         self._synced_version = -1
@@ -275,6 +278,7 @@ class DDoSClassifier(nn.Module):
         self._grad_token = torch.zeros((), device=dev, requires_grad=True)
         self._hip_cache = None
         self._wgrad = None
+        self._tstream = None
         self._synced_version = -1
         return self
 
@@ -421,7 +425,10 @@ class DDoSClassifier(nn.Module):
         grad = torch.is_grad_enabled()
         if grad and self.wgrad_stream and self._wgrad is None:
             self._wgrad = torch.cuda.Stream(device=self.arena.device)
-        rc = RunCtx(B=B, S=S, H=cfg.n_heads, kbias=K.mask_bias(mask), seed=self.rng, training=self.training,
+        packed = tokens is not None and self.unpad and self.packed_rows(tokens, B, S) < B * S
+        # varlen attention masks keys by sequence length; the padded path needs the additive bias
+        kbias = self._no_bias() if packed else K.mask_bias(mask)
+        rc = RunCtx(B=B, S=S, H=cfg.n_heads, kbias=kbias, seed=self.rng, training=self.training,
                     eps=cfg.layer_norm_eps, p_hidden=cfg.dropout, p_attn=cfg.attention_dropout, p_head=self.dropout.p,
                     on_layer_grads=self.layer_grads_hook if grad else None,
                     wgrad=self._wgrad if grad and self.wgrad_stream else None, group_dw=self.group_dw)
@@ -431,34 +438,43 @@ class DDoSClassifier(nn.Module):
             K.step_inc(None, self.rng)
         token = self._grad_token if torch.is_grad_enabled() else None
         if token is not None and self.transposed_dx:
-            K.transpose_many([L[k] for L in layers for k in L["wT"]], [L["wT"][k] for L in layers for k in L["wT"]])
-        hrc = rc
-        if tokens is not None and self.unpad and self.packed_rows(tokens, B, S) < B * S:
+            srcs = [L[k] for L in layers for k in L["wT"]]
+            dsts = [L["wT"][k] for L in layers for k in L["wT"]]
+            if self.overlap_transpose:
+                # the W^T copies are first read by the backward: build them on a side stream
+                # while the forward runs (joined at the head's backward, the first backward node)
+                if self._tstream is None:
+                    self._tstream = torch.cuda.Stream(device=self.arena.device)
+                self._tstream.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self._tstream):
+                    K.transpose_many(srcs, dsts)
+                rc.join_stream = self._tstream
+            else:
+                K.transpose_many(srcs, dsts)
+        if packed:
             # Unpadded step: only the real tokens (sequence-contiguous, filler rows at the end)
             # are embedded and run through the blocks; varlen attention over cu; positions and
-            # dropout follow the padded row (same masks as the padded path).  Filler rows act
-            # as padded row 0: finite, and their gradient is exactly 0 (they reach neither a
-            # real token nor the loss).
-            rows = self.packed_rows(tokens, B, S)
-            m = mask.reshape(-1)
-            row_map = torch.nonzero_static(m, size=rows, fill_value=-1).squeeze(1).to(torch.int32)
-            cu = torch.zeros(B + 1, dtype=torch.int32, device=ids.device)
-            cu[1:] = torch.cumsum(mask.sum(1, dtype=torch.int32), 0, dtype=torch.int32)
-            ids = ids.reshape(-1).index_select(0, row_map.clamp(min=0))
-            rc.cu, rc.row_map = cu, row_map
-            # the head reads one [CLS] row per sequence: present it as a [B, 1] layout
-            hrc = RunCtx(B=B, S=1, H=rc.H, kbias=rc.kbias, seed=rc.seed, training=rc.training, eps=rc.eps,
-                         p_hidden=rc.p_hidden, p_attn=rc.p_attn, p_head=rc.p_head)
+            # dropout follow the padded row (same masks as the padded path); the head reads
+            # row cu[b] for sequence b's [CLS].  Filler rows act as padded row 0: finite, and
+            # their gradient is exactly 0 (they reach neither a real token nor the loss).
+            # The layout (row map, sequence starts, packed ids) is one kernel (ops/packing).
+            rc.row_map, rc.cu, ids = K.pack(mask, ids, self.packed_rows(tokens, B, S))
         x = EmbeddingFn.apply(token, ids, emb["word"], emb["pos"], emb["ln_w"], emb["ln_b"], emb["sinks"], rc)
         for i, L in enumerate(layers):
             x = LayerFn.apply(x, L, rc, i)
-        if rc.cu is not None:
-            x = x.index_select(0, rc.cu[:-1])
         if labels is not None:
-            loss, logits = HeadFn.apply(x, head["w"], head["b"], head["sinks"], hrc, labels.to(torch.int64))
+            loss, logits = HeadFn.apply(x, head["w"], head["b"], head["sinks"], rc, labels.to(torch.int64))
             return loss, logits
-        logits, _ = HeadFn.apply(x, head["w"], head["b"], head["sinks"], hrc, None)
+        logits, _ = HeadFn.apply(x, head["w"], head["b"], head["sinks"], rc, None)
         return None, logits
+
+    def _no_bias(self) -> torch.Tensor:
+        """Placeholder key-bias tensor for the varlen path (the kernels do not read it)."""
+        t = getattr(self, "_nobias", None)
+        if t is None or t.device != self.arena.device:
+            t = torch.zeros(1, dtype=torch.float32, device=self.arena.device)
+            self._nobias = t
+        return t
 
     def _run_torch(self, ids, mask, labels):
         cfg = self.config

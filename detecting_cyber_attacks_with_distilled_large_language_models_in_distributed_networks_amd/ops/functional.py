@@ -54,6 +54,9 @@ class RunCtx:
     # deferred column sums (bias / LN-affine grads): producers leave partials, the end of
     # the backward finalises all of them in one launch (None = finalise immediately)
     colsum_jobs: Optional[list] = None
+    # side stream that produced data the backward reads (the W^T copies): joined at the
+    # first backward node (the head)
+    join_stream: Optional["torch.cuda.Stream"] = None
 
 
 class _WGrad:
@@ -197,7 +200,8 @@ class HeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, hidden, W, b, sinks, rc: RunCtx, labels: Optional[torch.Tensor]):
         p = rc.p_head if rc.training else 0.0
-        logits, loss, dlog = K.head_fwd(hidden, rc.B, rc.S, W, b, rc.seed, 2, p, labels)
+        cls = rc.cu[:-1] if rc.cu is not None else None  # packed: [CLS] = first row of each sequence
+        logits, loss, dlog = K.head_fwd(hidden, rc.B, rc.S, W, b, rc.seed, 2, p, labels, cls)
         ctx.rc, ctx.sinks, ctx.p, ctx.W = rc, sinks, p, W
         ctx.save_for_backward(hidden)
         ctx.dlog = dlog
@@ -211,6 +215,8 @@ class HeadFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g0, g1):
+        if ctx.rc.join_stream is not None:
+            torch.cuda.current_stream().wait_stream(ctx.rc.join_stream)
         (hidden,) = ctx.saved_tensors
         if ctx.fused_loss:
             dlog = ctx.dlog * g0
@@ -219,5 +225,7 @@ class HeadFn(torch.autograd.Function):
         s = ctx.sinks
         acc = s["w"].accumulate()
         s["b"].accumulate()
-        dh = K.head_bwd(hidden, ctx.rc.B, ctx.rc.S, ctx.W, ctx.rc.seed, 2, ctx.p, dlog, s["w"].buf, s["b"].buf, acc)
+        cls = ctx.rc.cu[:-1] if ctx.rc.cu is not None else None
+        dh = K.head_bwd(hidden, ctx.rc.B, ctx.rc.S, ctx.W, ctx.rc.seed, 2, ctx.p, dlog, s["w"].buf, s["b"].buf, acc,
+                        cls)
         return dh, None, None, None, None, None

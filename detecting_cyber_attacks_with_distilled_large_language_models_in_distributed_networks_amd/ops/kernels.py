@@ -117,6 +117,19 @@ def colsum_flush(jobs: list):
         jobs.clear()
 
 
+# ------------------------------------------------------------------ unpadded layout
+def pack(mask: torch.Tensor, ids: torch.Tensor, rows: int):
+    """(row_map int32 [rows], cu int32 [B+1], ids_packed int64 [rows]) of a [B, S] batch: the
+    real tokens in order (filler rows: row_map -1, id of position 0) -- one launch."""
+    B = mask.shape[0]
+    row_map = torch.empty(rows, dtype=torch.int32, device=mask.device)
+    cu = torch.empty(B + 1, dtype=torch.int32, device=mask.device)
+    ids_packed = torch.empty(rows, dtype=torch.int64, device=mask.device)
+    m = mask if mask.dtype != torch.bool else mask.to(torch.uint8)
+    ext().pack(m.contiguous(), ids.contiguous(), row_map, cu, ids_packed)
+    return row_map, cu, ids_packed
+
+
 # ------------------------------------------------------------------ attention
 def mask_bias(mask: torch.Tensor) -> torch.Tensor:
     m = mask.contiguous()
@@ -212,7 +225,8 @@ def emb_bwd(dy, ids, sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos
 
 
 # ------------------------------------------------------------------ head / metrics / optimizer
-def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None):
+def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None, cls=None):
+    """cls (int32 [B]): packed layout -- sequence b's [CLS] is row cls[b] of hidden."""
     logits = torch.empty(B, 2, dtype=torch.float32, device=hidden.device)
     loss = dlogits = row_loss = None
     if labels is not None:
@@ -220,14 +234,14 @@ def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None):
         dlogits = torch.empty(B, 2, dtype=torch.float32, device=hidden.device)
         row_loss = workspace(hidden.device, "head_row_loss", B)
     thr, sc = _drop(p)
-    ext().head_fwd(hidden, B, S, W, b, seed, site, thr, sc, labels, logits, loss, dlogits, row_loss)
+    ext().head_fwd(hidden, B, S, W, b, seed, site, thr, sc, labels, logits, loss, dlogits, row_loss, cls)
     return logits, loss, dlogits
 
 
-def head_bwd(hidden, B, S, W, seed, site, p, dlogits, dW, db, accumulate=False):
+def head_bwd(hidden, B, S, W, seed, site, p, dlogits, dW, db, accumulate=False, cls=None):
     dhidden = torch.zeros_like(hidden)
     thr, sc = _drop(p)
-    ext().head_bwd(hidden, B, S, W, seed, site, thr, sc, dlogits.contiguous(), dW, db, dhidden, accumulate)
+    ext().head_bwd(hidden, B, S, W, seed, site, thr, sc, dlogits.contiguous(), dW, db, dhidden, accumulate, cls)
     return dhidden
 
 

@@ -107,3 +107,28 @@ def test_packed_graph_buckets_match_eager():
         assert abs(float(losses[0] - losses[1])) < 1e-5, it
     assert len(steps[0].graphs) >= 2 and steps[0].failed is None
     assert torch.equal(models[0].arena.master, models[1].arena.master)
+
+
+@pytest.mark.parametrize("B,S", [(32, 128), (64, 256), (3, 64)])
+def test_pack_kernel_matches_torch(B, S):
+    """One-launch packing == nonzero / cumsum / gather in torch (prefix and holey masks)."""
+    g = torch.Generator().manual_seed(B * S)
+    lens = torch.randint(1, S + 1, (B,), generator=g)
+    mask = (torch.arange(S)[None] < lens[:, None]).long()
+    mask[1, 0] = 0 if B > 2 else mask[1, 0]  # a hole: the general (non-prefix) case still compacts
+    ids = torch.randint(0, 30000, (B, S), generator=g)
+    mask, ids = mask.cuda(), ids.cuda()
+    total = int(mask.sum())
+    rows = (total + 127) // 128 * 128
+    row_map, cu, idp = K.pack(mask, ids, rows)
+    ref_map = torch.nonzero(mask.reshape(-1)).squeeze(1)
+    assert torch.equal(row_map[:total].long(), ref_map)
+    assert (row_map[total:] == -1).all()
+    ref_cu = torch.zeros(B + 1, dtype=torch.long)
+    ref_cu[1:] = torch.cumsum(mask.sum(1).cpu(), 0)
+    assert torch.equal(cu.cpu().long(), ref_cu)
+    assert torch.equal(idp[:total], ids.reshape(-1)[ref_map])
+    assert (idp[total:] == ids.reshape(-1)[0]).all()
+    # a row budget smaller than the real tokens never writes past it
+    small_map, _, _ = K.pack(mask, ids, 64)
+    assert torch.equal(small_map.long(), ref_map[:64])
