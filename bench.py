@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--impl", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-group-dw", action="store_true", help="one launch per weight gradient (A/B)")
-    ap.add_argument("--no-overlap-transpose", action="store_true", help="W^T copies on the main stream (A/B)")
+    ap.add_argument("--overlap-transpose", action="store_true", help="W^T copies on a side stream (A/B; slower)")
     ap.add_argument("--padded", action="store_true",
                     help="run the blocks on all B*S positions instead of the packed real tokens (A/B)")
     ap.add_argument("--wgrad-stream", action="store_true",
@@ -105,7 +105,7 @@ def main():
     else:
         fn = engine.make_step_fn(model, opt)
     model.unpad = not args.padded
-    model.overlap_transpose = not args.no_overlap_transpose
+    model.overlap_transpose = args.overlap_transpose
     step = engine.GraphedTrainStep(fn, warmup=2, enabled=(not args.no_graph) and args.impl == "hip"
                                    and dev.type == "cuda" and gsync is None,
                                    bucket=getattr(model, "packed_rows", None))

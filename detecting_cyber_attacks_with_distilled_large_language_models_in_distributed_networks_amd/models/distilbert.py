@@ -251,8 +251,10 @@ class DDoSClassifier(nn.Module):
         self.pack_quantum = 128
         # HIP path: finalise all bias / LN-affine column sums of a backward in one launch
         self.defer_colsum = True
-        # HIP path: the per-step W^T copies are built on a side stream concurrently with the forward
-        self.overlap_transpose = True
+        # HIP path: build the per-step W^T copies on a side stream concurrently with the forward.
+        # Measured SLOWER on MI355X (2.48 vs 2.36 ms/step, profiles/r1_ab_transpose_overlap_slower.txt):
+        # the memory-bound transposes stretch the concurrent forward GEMMs.  Off by default.
+        self.overlap_transpose = False
         self._tstream = None
         self.torch_counter = 0
         self._grad_token = None
