@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-group-dw", action="store_true", help="one launch per weight gradient (A/B)")
     ap.add_argument("--overlap-transpose", action="store_true", help="W^T copies on a side stream (A/B; slower)")
+    ap.add_argument("--spinup-seconds", type=float, default=1.0,
+                    help="busy the GPU with a plain matmul loop before the warmup steps (a GPU that was idle "
+                         "runs the first ~100 ms of work measurably slower); no model state is touched")
     ap.add_argument("--padded", action="store_true",
                     help="run the blocks on all B*S positions instead of the packed real tokens (A/B)")
     ap.add_argument("--wgrad-stream", action="store_true",
@@ -117,6 +120,14 @@ def main():
                 yield b
 
     it = batches()
+    if dev.type == "cuda" and args.spinup_seconds > 0:
+        a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+        t_end = time.perf_counter() + args.spinup_seconds
+        while time.perf_counter() < t_end:
+            for _ in range(20):
+                a = (a @ a).clamp_(-1.0, 1.0)
+            torch.cuda.synchronize()
+        del a
     if args.mode == "infer":
         return _bench_infer(args, model, it, di, comm, B, S)
     for _ in range(args.warmup):
@@ -181,6 +192,7 @@ def main():
             "vs_baseline_basis": "per-client batches/s / 2.5 (reference bs16 fp32 per-client rate)",
             "impl": args.impl,
             "comm": args.comm,
+            "spinup_s": args.spinup_seconds,
             "hip_graph": step.graph is not None,
             "hip_graphs": len(getattr(step, "graphs", {})),
             "unpadded": bool(getattr(model, "unpad", False)) and args.impl == "hip",

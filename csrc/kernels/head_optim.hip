@@ -185,7 +185,7 @@ DEV void st_nt(float4* p, float4 v) {
   __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
 }
 
-template <bool NT>
+template <bool NT, bool NTP = false>
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const int t = a.step[0];
   const float bc1 = 1.f - powf(a.b1, (float)t);
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
       if (!a.touched[row]) continue;
       gvalid = a.now == nullptr || a.now[row] != 0;
     }
-    float4 p = reinterpret_cast<float4*>(a.p)[i];
+    float4 p = NTP ? ld_nt(reinterpret_cast<const float4*>(a.p) + i) : reinterpret_cast<float4*>(a.p)[i];
     float4 g, m, v;
     if constexpr (NT) {
       g = gvalid ? ld_nt(reinterpret_cast<const float4*>(a.g) + i) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -226,7 +226,10 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
       const float denom = sqrtf(vv[e]) * inv_sqrt_bc2 + a.eps;
       pp[e] -= step_size * mm[e] / denom;
     }
-    reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    if constexpr (NTP)
+      st_nt(reinterpret_cast<float4*>(a.p) + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
+    else
+      reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
     if constexpr (NT) {
       st_nt(reinterpret_cast<float4*>(a.m) + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
       st_nt(reinterpret_cast<float4*>(a.v) + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
@@ -316,11 +319,15 @@ int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long lon
   if (wd != 0.f && touched) return 3;  // skipping untouched rows is exact only without weight decay
   AdamArgs a{p, g, m, v, (bf16_t*)shadow, n / 4, step, lr, b1, b2, eps, wd, decoupled,
              skip_off / 4, (skip_off + skip_rows * row_len) / 4, row_len / 4, touched, now};
-  static const bool nt = [] { const char* e = getenv("FD_ADAM_NT"); return e ? atoi(e) != 0 : true; }();
-  if (nt)
-    hipLaunchKernelGGL(adam_kernel<true>, dim3(grid_for(n / 4)), dim3(256), 0, st, a);
+  // FD_ADAM_NT: 0 = default cache policy, 1 = nontemporal g/m/v, 2 = also the fp32 master (default:
+  // 2.336 vs 2.366-2.387 ms/step, profiles/r1_ab_adam_nt_master.txt -- only the bf16 shadow is re-read soon)
+  static const int nt = [] { const char* e = getenv("FD_ADAM_NT"); return e ? atoi(e) : 2; }();
+  if (nt == 2)
+    hipLaunchKernelGGL((adam_kernel<true, true>), dim3(grid_for(n / 4)), dim3(256), 0, st, a);
+  else if (nt)
+    hipLaunchKernelGGL((adam_kernel<true, false>), dim3(grid_for(n / 4)), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(adam_kernel<false>, dim3(grid_for(n / 4)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((adam_kernel<false, false>), dim3(grid_for(n / 4)), dim3(256), 0, st, a);
   return 0;
 }
 

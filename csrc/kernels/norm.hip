@@ -372,10 +372,11 @@ __global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
 // back to back.  Rows s >= S are handled by a memset (first write) on the host side.
 // cu (packed rows): sequence b's position s is row cu[b] + s when s < its length; the
 // padded layout's extra terms are exact zeros, so both layouts give the same sums.
+// grid (S, ceil(D/256)): one thread per (position, column), 16 sequences' loads in flight.
 __global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* dpos, int B, int S, int D,
                                                        int accumulate, const int* cu) {
   const int s = blockIdx.x;
-  for (int col = threadIdx.x; col < D; col += 256) {
+  for (int col = blockIdx.y * 256 + threadIdx.x; col < D; col += gridDim.y * 256) {
     float acc = accumulate ? dpos[(size_t)s * D + col] : 0.f;
     for (int b0 = 0; b0 < B; b0 += 16) {
       float v[16];
@@ -710,7 +711,8 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
   hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 2), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, (float*)nullptr, accumulate);
   if (!accumulate && P > S) hipMemsetAsync(dpos + (size_t)S * D, 0, (size_t)(P - S) * D * sizeof(float), st);
-  hipLaunchKernelGGL(pos_grad_kernel, dim3(S), dim3(256), 0, st, dz_buf, dpos, B, S, D, accumulate, cu);
+  hipLaunchKernelGGL(pos_grad_kernel, dim3(S, (D + 255) / 256), dim3(256), 0, st, dz_buf, dpos, B, S, D, accumulate,
+                     cu);
   if (!accumulate) {
     if (now) hipMemsetAsync(now, 0, (size_t)V, st);
     else hipMemsetAsync(dword, 0, (size_t)V * D * sizeof(float), st);
