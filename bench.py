@@ -24,6 +24,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 PKG = "detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd"
@@ -44,6 +45,8 @@ def main():
     ap.add_argument("--spinup-seconds", type=float, default=1.0,
                     help="busy the GPU with a plain matmul loop before the warmup steps (a GPU that was idle "
                          "runs the first ~100 ms of work measurably slower); no model state is touched")
+    ap.add_argument("--no-quality", action="store_true",
+                    help="skip the post-timing aggregated-F1 evaluation (kernel profiles of the step alone)")
     ap.add_argument("--padded", action="store_true",
                     help="run the blocks on all B*S positions instead of the packed real tokens (A/B)")
     ap.add_argument("--wgrad-stream", action="store_true",
@@ -163,6 +166,11 @@ def main():
     dt = time.perf_counter() - t0
     dt = comm.all_reduce_max(dt)
     loss = float(loss_acc.item()) / args.steps
+    # Second half of the metric: the FedAvg-aggregated model (the all-reduce that closes the
+    # timed region) scored on every client's held-out test split -- counts summed over
+    # clients, one F1 (untimed; the reference's evaluate_model after aggregation,
+    # client1.py:118-150 / 330-340).
+    quality = {} if args.no_quality else _aggregated_quality(model, cd.test, dev, topo, engine, data, di)
     if not (loss == loss and abs(loss) < 1e6):
         raise SystemExit(f"bench: non-finite training loss {loss} -- refusing to report a throughput")
     n = di.world_size
@@ -198,9 +206,31 @@ def main():
             "unpadded": bool(getattr(model, "unpad", False)) and args.impl == "hip",
             "graph_error": step.failed,
             "mean_loss": round(loss, 5),
+            **quality,
         }
         print(json.dumps(out), flush=True)
     comm.shutdown()
+
+
+def _aggregated_quality(model, test, dev, topo, engine, data, di):
+    """Accuracy / F1 of the aggregated model over all clients' test rows (one replica per client)."""
+    loader = data.DeviceLoader(test, 256, shuffle=False, device=dev, drop_last=False)
+    res = engine.evaluate_model(model, loader)
+    lab = np.asarray(res[6], dtype=np.int64)
+    pred = (np.asarray(res[7]) > 0.5).astype(np.int64)
+    c = torch.tensor([int(((pred == 1) & (lab == 1)).sum()), int(((pred == 1) & (lab == 0)).sum()),
+                      int(((pred == 0) & (lab == 1)).sum()), int(((pred == 0) & (lab == 0)).sum())],
+                     dtype=torch.float64, device=dev)
+    if topo.dp_rank != 0:
+        c.zero_()  # data-parallel replicas hold the same client's split
+    if di.distributed:
+        torch.distributed.all_reduce(c)
+    tp, fp, fn, tn = c.tolist()
+    prec = tp / (tp + fp) if tp + fp else 0.0
+    rec = tp / (tp + fn) if tp + fn else 0.0
+    f1 = 2 * prec * rec / (prec + rec) if prec + rec else 0.0
+    return {"aggregated_f1": round(f1, 5), "aggregated_accuracy_pct": round(100.0 * (tp + tn) / max(tp + fp + fn + tn, 1), 3),
+            "eval_rows": int(tp + fp + fn + tn), "fedavg_rounds": 1 if di.distributed else 0}
 
 
 def _bench_infer(args, model, it, di, comm, B, S):

@@ -4,7 +4,7 @@
 # 4 TCC with FETCH_SIZE = 3 / WRITE_SIZE = 2, 2 GRBM), then a per-kernel summary.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-pmc}; mkdir -p $O
-ARGS="bench.py --no-graph --steps ${2:-4} --warmup 2"
+ARGS="bench.py --no-graph --steps ${2:-4} --warmup 2 --spinup-seconds 0 --no-quality"
 run() {  # name, counters...
   local n=$1; shift
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $O/$n -- python3 $ARGS > $O/$n.log 2>&1 ||
