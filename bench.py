@@ -47,6 +47,8 @@ def main():
                          "runs the first ~100 ms of work measurably slower); no model state is touched")
     ap.add_argument("--no-quality", action="store_true",
                     help="skip the post-timing aggregated-F1 evaluation (kernel profiles of the step alone)")
+    ap.add_argument("--fused-adam", action="store_true",
+                    help="apply Adam inside the weight-gradient GEMM epilogues (A/B; measured no faster)")
     ap.add_argument("--padded", action="store_true",
                     help="run the blocks on all B*S positions instead of the packed real tokens (A/B)")
     ap.add_argument("--wgrad-stream", action="store_true",
@@ -94,7 +96,7 @@ def main():
     if args.comm == "rccl" and dev.type == "cuda":
         ncomm = import_module(f"{PKG}.parallel.rccl").NativeComm()
     fedavg.broadcast_model(model, comm=ncomm)
-    opt = engine.ArenaAdam(model, lr=2e-5)
+    opt = engine.ArenaAdam(model, lr=2e-5, fuse_dw=args.fused_adam)
     gsync = None
     if topo.dp:
         if args.teacher:
@@ -204,6 +206,7 @@ def main():
             "hip_graph": step.graph is not None,
             "hip_graphs": len(getattr(step, "graphs", {})),
             "unpadded": bool(getattr(model, "unpad", False)) and args.impl == "hip",
+            "fused_adam": bool(opt.can_fuse()) and gsync is None,
             "graph_error": step.failed,
             "mean_loss": round(loss, 5),
             **quality,

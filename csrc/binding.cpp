@@ -9,14 +9,20 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
+
+#include "kernels/adam_epi.h"
 
 extern "C" {
 int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
             int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
-            long long workspace_elems, int accumulate, hipStream_t st);
+            long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+            hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
+int fd_gemm_set_fixup(int on);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
-                int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, hipStream_t st);
+                int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, int* tile_cnt,
+                long long ncnt, const FdAdamEpi* adams, hipStream_t st);
 int fd_transpose_batched(const void* const* srcs, void* const* dsts, const int* rows, const int* cols, int n,
                          hipStream_t st);
 const char* fd_comm_last_error();
@@ -67,7 +73,8 @@ int fd_eval_metrics(const float* logits, const long long* labels, int B, double*
                     float* prob1, long long* preds, hipStream_t st);
 int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float lr,
             float b1, float b2, float eps, float wd, int decoupled, const unsigned char* touched,
-            const unsigned char* now, long long skip_off, long long skip_rows, int row_len, hipStream_t st);
+            const unsigned char* now, long long skip_off, long long skip_rows, int row_len, const long long* runs,
+            int nruns, long long run_total4, hipStream_t st);
 int fd_step(int* step, uint32_t* seed, hipStream_t st);
 int fd_scale_cast(float* p, void* shadow, long long n, float scale, hipStream_t st);
 int fd_axpby(float* dst, const float* x, const float* y, float a, float b, long long n, hipStream_t st);
@@ -127,13 +134,79 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
   const long long ws = (workspace.has_value() && workspace->defined()) ? workspace->numel() : 0;
   check_rc(fd_gemm((int)kind, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
                    (int)A.size(1), (int)B.size(1), (int)N, ptr<float>(bias), ptr<void>(aux), (int)N,
-                   ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, stream()),
+                   ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, nullptr, 0, nullptr,
+                   stream()),
            "gemm");
+}
+
+// Adam descriptors for fused weight-gradient epilogues.  st = [p, m, v, shadow] per problem
+// + the device step counter last; hp = [lr, b1, b2, eps, wd, decoupled].  Each state tensor
+// must be laid out exactly like the gradient it replaces (same numel, contiguous).
+void adam_descs(const std::vector<at::Tensor>& st, const std::vector<double>& hp, const at::Tensor* const* grads,
+                int nprob, FdAdamEpi* out) {
+  TORCH_CHECK((int)st.size() == 4 * nprob + 1, "fused adam: expected ", 4 * nprob + 1, " state tensors");
+  TORCH_CHECK(hp.size() == 6, "fused adam: hyper-parameters [lr, b1, b2, eps, wd, decoupled]");
+  const at::Tensor& step = st.back();
+  need(step, at::kInt, "adam step");
+  for (int i = 0; i < nprob; ++i) {
+    const int64_t n = grads[i]->numel();
+    for (int k = 0; k < 3; ++k) {
+      need(st[4 * i + k], at::kFloat, "adam state");
+      TORCH_CHECK(st[4 * i + k].numel() == n, "fused adam: state size mismatch");
+    }
+    const at::Tensor& sh = st[4 * i + 3];
+    if (sh.defined() && sh.numel() > 0) {
+      need(sh, at::kBFloat16, "adam shadow");
+      TORCH_CHECK(sh.numel() == n, "fused adam: shadow size mismatch");
+    }
+    FdAdamEpi& a = out[i];
+    a.p = st[4 * i].data_ptr<float>();
+    a.m = st[4 * i + 1].data_ptr<float>();
+    a.v = st[4 * i + 2].data_ptr<float>();
+    a.sh = (sh.defined() && sh.numel() > 0) ? reinterpret_cast<uint16_t*>(sh.data_ptr()) : nullptr;
+    a.step = step.data_ptr<int>();
+    a.lr = (float)hp[0]; a.b1 = (float)hp[1]; a.b2 = (float)hp[2]; a.eps = (float)hp[3]; a.wd = (float)hp[4];
+    a.decoupled = hp[5] != 0.0 ? 1 : 0;
+  }
+}
+
+int* counters_ptr(const c10::optional<at::Tensor>& c, long long* n) {
+  *n = 0;
+  if (!c.has_value() || !c->defined()) return nullptr;
+  need(*c, at::kInt, "tile counters");
+  *n = c->numel();
+  return c->data_ptr<int>();
+}
+
+// Weight gradient C[M][N] (+)= A^T B (fp32), split-K reduced in-kernel through `counters`
+// (int32, zero-initialised, self-resetting), optionally with Adam fused into the epilogue.
+void gemm_dw(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, const at::Tensor& workspace,
+             bool accumulate, const c10::optional<at::Tensor>& counters, const std::vector<at::Tensor>& adam,
+             const std::vector<double>& hp) {
+  need(A, at::kBFloat16, "A");
+  need(B, at::kBFloat16, "B");
+  need(C, at::kFloat, "C");
+  need(workspace, at::kFloat, "workspace");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm_dw operands must be 2-D");
+  const int64_t K = A.size(0), M = A.size(1), N = B.size(1);
+  TORCH_CHECK(B.size(0) == K && C.size(0) == M && C.size(1) == N, "gemm_dw: shape mismatch");
+  TORCH_CHECK(K % 64 == 0 && M % 128 == 0 && N % 64 == 0, "gemm_dw: K % 64, M % 128, N % 64 required");
+  FdAdamEpi ad{};
+  const at::Tensor* gs[1] = {&C};
+  if (!adam.empty()) adam_descs(adam, hp, gs, 1, &ad);
+  long long ncnt;
+  int* cnt = counters_ptr(counters, &ncnt);
+  check_rc(fd_gemm(2, 5, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K, (int)M, (int)N, (int)N,
+                   nullptr, nullptr, 0, nullptr, 0, workspace.data_ptr<float>(), workspace.numel(),
+                   accumulate ? 1 : 0, cnt, ncnt, adam.empty() ? nullptr : &ad, stream()),
+           "gemm_dw");
 }
 
 // Grouped weight gradients: C0 (+)= A0^T B0 and C1 (+)= A1^T B1 in one launch (shared K = tokens).
 void gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C0, const at::Tensor& A1,
-              const at::Tensor& B1, const at::Tensor& C1, const at::Tensor& workspace, bool accumulate) {
+              const at::Tensor& B1, const at::Tensor& C1, const at::Tensor& workspace, bool accumulate,
+              const c10::optional<at::Tensor>& counters, const std::vector<at::Tensor>& adam,
+              const std::vector<double>& hp) {
   const at::Tensor* As[2] = {&A0, &A1};
   const at::Tensor* Bs[2] = {&B0, &B1};
   const at::Tensor* Cs[2] = {&C0, &C1};
@@ -149,9 +222,14 @@ void gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C0, 
   }
   TORCH_CHECK(K % 64 == 0, "gemm_dw2: K must be a multiple of 64");
   need(workspace, at::kFloat, "workspace");
+  FdAdamEpi ad[2]{};
+  if (!adam.empty()) adam_descs(adam, hp, Cs, 2, ad);
+  long long ncnt;
+  int* cnt = counters_ptr(counters, &ncnt);
   check_rc(fd_gemm_dw2(A0.data_ptr(), B0.data_ptr(), C0.data_ptr<float>(), (int)A0.size(1), (int)B0.size(1),
                        A1.data_ptr(), B1.data_ptr(), C1.data_ptr<float>(), (int)A1.size(1), (int)B1.size(1), (int)K,
-                       workspace.data_ptr<float>(), workspace.numel(), accumulate ? 1 : 0, stream()),
+                       workspace.data_ptr<float>(), workspace.numel(), accumulate ? 1 : 0, cnt, ncnt,
+                       adam.empty() ? nullptr : ad, stream()),
            "gemm_dw2");
 }
 
@@ -570,7 +648,8 @@ void eval_metrics(const at::Tensor& logits, const at::Tensor& labels, const at::
 void adam(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
           const c10::optional<at::Tensor>& shadow, const at::Tensor& step, double lr, double b1, double b2, double eps,
           double wd, bool decoupled, const c10::optional<at::Tensor>& touched, const c10::optional<at::Tensor>& now,
-          int64_t skip_off, int64_t skip_rows, int64_t row_len) {
+          int64_t skip_off, int64_t skip_rows, int64_t row_len, const c10::optional<at::Tensor>& runs,
+          int64_t run_total4, int64_t run_end4) {
   need_opt(touched, at::kByte, "touched");
   need_opt(now, at::kByte, "now");
   if (touched.has_value() && touched->defined()) {
@@ -587,10 +666,24 @@ void adam(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const a
   const int64_t n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && n % 4 == 0, "adam: sizes");
   if (shadow.has_value() && shadow->defined()) TORCH_CHECK(shadow->numel() == n, "adam: shadow size");
+  // run table [start4, count4, prefix4] x nruns (int64, on the device).  The caller built it on
+  // the host (engine/optim.py) and passes its total and its largest end, checked here against
+  // the arena so the kernel's indexing stays in bounds.
+  const long long* rp = nullptr;
+  int nruns = 0;
+  long long total4 = 0;
+  if (runs.has_value() && runs->defined()) {
+    need(*runs, at::kLong, "adam runs");
+    TORCH_CHECK(runs->dim() == 2 && runs->size(1) == 3 && runs->size(0) > 0, "adam runs: [nruns, 3]");
+    TORCH_CHECK(run_total4 > 0 && run_end4 <= n / 4, "adam runs: total / end outside the arena");
+    nruns = (int)runs->size(0);
+    rp = reinterpret_cast<const long long*>(runs->data_ptr<int64_t>());
+    total4 = run_total4;
+  }
   check_rc(fd_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                    ptr<void>(shadow), n, step.data_ptr<int>(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
                    decoupled ? 1 : 0, ptr<const unsigned char>(touched), ptr<const unsigned char>(now), skip_off,
-                   skip_rows, (int)row_len, stream()),
+                   skip_rows, (int)row_len, rp, nruns, total4, stream()),
            "adam");
 }
 
@@ -626,6 +719,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm);
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_dw2", &gemm_dw2);
+  m.def("gemm_dw", &gemm_dw);
+  m.def("gemm_set_fixup", [](bool on) { fd_gemm_set_fixup(on ? 1 : 0); });
   m.def("pack", &pack);
   m.def("transpose_batched", &transpose_batched);
   m.def("comm_load", &comm_load);

@@ -30,6 +30,7 @@
 //    32-byte store pattern is store-issue bound).
 //  * XCD-aware bijective block remap (T1) + group-M tile walk sized to the L2.
 #include "common.h"
+#include "adam_epi.h"
 
 #include <cstdlib>
 
@@ -59,6 +60,16 @@ struct GemmParams {
   long long slab_stride; // elements between fp32 slabs
   int group_m;           // tile-walk group height (L2 working-set control)
   int diag;              // FD_GEMM_DIAG bits (profiling only): 1 no in-loop DMA, 4 no stores
+  // EPI_F32 destinations (weight gradients).  out == nullptr: legacy slab mode (slab z of C,
+  // reduced by splitk_reduce_kernel).  Otherwise the final [M][N] fp32 gradient:
+  //   tile_cnt == nullptr -> one K split, the tile goes straight to out (+= out if accumulate);
+  //   tile_cnt != nullptr -> split-K fixup: every split stores its slab into C, the last split
+  //   of a tile to arrive sums the slabs in z order (bitwise what splitk_reduce computes) and
+  //   finishes the tile; the per-tile arrival counters reset themselves for the next launch.
+  float* out;
+  int* tile_cnt;
+  int accumulate;
+  FdAdamEpi adam;        // adam.p != nullptr: apply Adam to the finished tile instead of storing it
 };
 
 constexpr int BKT = 64;
@@ -164,9 +175,115 @@ struct EpiTraits {
   static constexpr int BYTES = BM * (BN * ES + 16);
 };
 
+DEV float4 ld_nt4(const float* p) {
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+DEV void st_nt4(float* p, float4 v) {
+  __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
+}
+
+// Adam on 4 consecutive elements of a finished gradient tile: the same arithmetic, in the
+// same order, as adam_kernel (head_optim.hip), so a fused step matches the unfused one.
+DEV void adam_epi4(const FdAdamEpi& a, size_t i, float4 g4, float step_size, float inv_sqrt_bc2) {
+  const float4 p4 = ld_nt4(a.p + i), m4 = ld_nt4(a.m + i), v4 = ld_nt4(a.v + i);
+  float pp[4] = {p4.x, p4.y, p4.z, p4.w}, gg[4] = {g4.x, g4.y, g4.z, g4.w};
+  float mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float gr = gg[e];
+    if (a.wd != 0.f) {
+      if (a.decoupled) pp[e] *= 1.f - a.lr * a.wd;
+      else gr += a.wd * pp[e];
+    }
+    mm[e] = a.b1 * mm[e] + (1.f - a.b1) * gr;
+    vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gr * gr;
+    const float denom = sqrtf(vv[e]) * inv_sqrt_bc2 + a.eps;
+    pp[e] -= step_size * mm[e] / denom;
+  }
+  st_nt4(a.p + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
+  st_nt4(a.m + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
+  st_nt4(a.v + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
+  if (a.sh) *reinterpret_cast<uint2*>(a.sh + i) = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
+}
+
+// Weight-gradient (fp32) epilogue; see GemmParams::out for the three modes.
+template <int BM, int BN, int NT>
+DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0, int n0, int tid, int slot) {
+  constexpr int CPR = BN / 4;  // 4 fp32 per chunk
+  if (p.out == nullptr) {      // legacy: slab z, reduced by a separate launch
+    float* C = reinterpret_cast<float*>(p.C) + (size_t)blockIdx.z * p.slab_stride;
+#pragma unroll 4
+    for (int id = tid; id < BM * CPR; id += NT) {
+      const int r = id / CPR, cc = id - r * CPR;
+      const int m = m0 + r;
+      if (m >= p.M) break;
+      *reinterpret_cast<float4*>(C + (size_t)m * p.ldc + n0 + cc * 4) =
+          *reinterpret_cast<const float4*>(smem + r * ldc_lds + cc * 16);
+    }
+    return;
+  }
+  const bool fix = p.tile_cnt != nullptr;
+  if (fix) {
+    float* C = reinterpret_cast<float*>(p.C) + (size_t)blockIdx.z * p.slab_stride;
+#pragma unroll 4
+    for (int id = tid; id < BM * CPR; id += NT) {
+      const int r = id / CPR, cc = id - r * CPR;
+      const int m = m0 + r;
+      if (m >= p.M) break;
+      *reinterpret_cast<float4*>(C + (size_t)m * p.ldc + n0 + cc * 4) =
+          *reinterpret_cast<const float4*>(smem + r * ldc_lds + cc * 16);
+    }
+    // release this split's slab at device scope (other XCDs' L2s), then count the arrival
+    __shared__ int s_last;
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(p.tile_cnt + slot, 1) == (int)gridDim.z - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // acquire: the other splits' slabs are visible
+  }
+  const bool adam = p.adam.p != nullptr;
+  float step_size = 0.f, inv_sqrt_bc2 = 0.f;
+  if (adam) {
+    const int t = p.adam.step[0];
+    const float bc1 = 1.f - powf(p.adam.b1, (float)t);
+    const float bc2 = 1.f - powf(p.adam.b2, (float)t);
+    step_size = p.adam.lr / bc1;
+    inv_sqrt_bc2 = 1.f / sqrtf(bc2);
+  }
+  const float* slabs = reinterpret_cast<const float*>(p.C);
+#pragma unroll 2
+  for (int id = tid; id < BM * CPR; id += NT) {
+    const int r = id / CPR, cc = id - r * CPR;
+    const int m = m0 + r;
+    if (m >= p.M) break;
+    const size_t i = (size_t)m * p.ldc + n0 + cc * 4;
+    float4 g;
+    if (fix) {
+      g = p.accumulate ? *reinterpret_cast<const float4*>(p.out + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int z = 0; z < (int)gridDim.z; ++z) {
+        const float4 s = ld_nt4(slabs + z * p.slab_stride + i);
+        g.x += s.x; g.y += s.y; g.z += s.z; g.w += s.w;
+      }
+    } else {
+      const float4 t = *reinterpret_cast<const float4*>(smem + r * ldc_lds + cc * 16);
+      if (p.accumulate) {
+        g = *reinterpret_cast<const float4*>(p.out + i);
+        g.x += t.x; g.y += t.y; g.z += t.z; g.w += t.w;
+      } else {
+        g = t;
+      }
+    }
+    if (adam) adam_epi4(p.adam, i, g, step_size, inv_sqrt_bc2);
+    else *reinterpret_cast<float4*>(p.out + i) = g;
+  }
+  if (fix && tid == 0) p.tile_cnt[slot] = 0;  // ready for the next launch / graph replay
+}
+
 template <int BM, int BN, int TM, int TN, int EPI, int NT>
 DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int m0, int n0,
-                         int wr, int wc, int lane, int tid) {
+                         int wr, int wc, int lane, int tid, int slot) {
   using TR = EpiTraits<EPI, BM, BN>;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int LDC = BN * TR::ES + 16;
@@ -224,6 +341,8 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
         *reinterpret_cast<uint4*>(C + (size_t)m * p.ldc + n) = u;
       }
     }
+  } else if constexpr (EPI == EPI_F32) {
+    f32_epilogue<BM, BN, NT>(p, smem, LDC, m0, n0, tid, slot);
   } else {
     constexpr int CPR = BN / 4;  // 4 fp32 per chunk
 #pragma unroll 4
@@ -233,10 +352,7 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
       if (m >= p.M) break;
       const float4 v = *reinterpret_cast<const float4*>(smem + r * LDC + cc * 16);
       const int n = n0 + cc * 4;
-      if constexpr (EPI == EPI_F32) {
-        float* C = reinterpret_cast<float*>(p.C) + (size_t)blockIdx.z * p.slab_stride;
-        *reinterpret_cast<float4*>(C + (size_t)m * p.ldc + n) = v;
-      } else {
+      {
         float v0 = v.x, v1 = v.y, v2 = v.z, v3 = v.w;
         if constexpr (EPI == EPI_GELU_BWD) {
           const uint2 u = *reinterpret_cast<const uint2*>(p.aux + (size_t)m * p.ldaux + n);
@@ -329,6 +445,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
   const int wr = wid / WN, wc = wid % WN;
 
   int bid = xcd_remap(blockIdx.x, grp.ntiles);
+  const int slot = bid;  // unique per tile of the (grouped) grid: split-K arrival counter
   const bool second = bid >= grp.ntiles0;  // block-uniform
   const GemmParams& p = second ? grp.q : p0;
   if (second) bid -= grp.ntiles0;
@@ -394,7 +511,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
   // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
   // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
   __syncthreads();
-  staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid);
+  staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid, slot);
 }
 
 // out[i] = (accumulate ? out[i] : 0) + sum_z slab[z][i]   (deterministic split-K reduce)
@@ -418,15 +535,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 //  6: 128 x 192, 2x4, S2      7: 256 x  96, 4x1, S3 (K-major B)
 //  8: 128 x  64, 2x2, S2      9: 128 x  96, 2x2, S3 (K-major B)
 // 10: 128 x 128, 2x2, S3     11: 256 x 256, 2x4, S2     12: 256 x 128, 4x2, S2
+// 13:  64 x  64, 2x2, S3     14:  64 x 128, 2x2, S3  (small tiles: 2-4 blocks/CU at N = 768)
 // (A ping-pong variant -- the two 4-wave halves of an 8-wave block staggered by
 // one barrier phase so one half's LDS reads overlap the other's MFMAs -- was
 // correct but measured 1.5-3x slower on these shapes; not kept.)
-constexpr int NCFG = 13;
+constexpr int NCFG = 15;
 struct CfgDesc { int bm, bn, wm, wn, s; };
 constexpr CfgDesc CFGS[NCFG] = {{128, 64, 2, 2, 3}, {128, 128, 2, 2, 2}, {128, 96, 2, 2, 2}, {256, 192, 4, 2, 2},
                                 {256, 128, 4, 2, 3}, {64, 192, 1, 4, 3}, {128, 192, 2, 4, 2}, {256, 96, 4, 1, 3},
                                 {128, 64, 2, 2, 2},  {128, 96, 2, 2, 3}, {128, 128, 2, 2, 3}, {256, 256, 2, 4, 2},
-                                {256, 128, 4, 2, 2}};
+                                {256, 128, 4, 2, 2}, {64, 64, 2, 2, 3},    {64, 128, 2, 2, 3}};
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
 bool launch_cfg(const GemmParams& p, int splits, hipStream_t st, const GemmParams* q) {
@@ -465,6 +583,8 @@ bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st, const Ge
     case 10: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
     case 11: return launch_cfg<256, 256, AK, BKM, EPI, 2, 4, 2>(p, splits, st, q);
     case 12: return launch_cfg<256, 128, AK, BKM, EPI, 4, 2, 2>(p, splits, st, q);
+    case 13: return launch_cfg<64, 64, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
+    case 14: return launch_cfg<64, 128, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
   }
   return false;
 }
@@ -508,6 +628,13 @@ int pick_cfg(int kind, int M, int N, int K) {
     if (N % 192 == 0 && N >= 3072 && M >= 3584) return 3;
     if (N % 128 == 0 && N >= 3072 && M >= 2048) return 1;
     if (N % 192 == 0 && N >= 1536 && M >= 2048) return 6;
+    // N = 768 (out_lin fwd, FFN2 fwd, every dX back to the hidden size): 64x64 tiles give
+    // 2x the blocks of 128x64, so each CU runs 2-3 of them.  Faster in isolation (7.6 vs
+    // 7.8-8.1 us at K = 768, 17.9 vs 19.5 us at K = 2304; profiles/r1_gemm_cfg_sweep_T2688_
+    // small_tiles.txt) but not in the step (2.370 vs 2.367 ms, 3 A/B pairs,
+    // profiles/r1_ab_small_tiles.txt): opt-in with FD_GEMM_SMALL_TILES=1.
+    static const bool small = [] { const char* e = getenv("FD_GEMM_SMALL_TILES"); return e && atoi(e) != 0; }();
+    if (small && N < 1536 && M >= 1024) return 13;
     return K >= 2048 ? 0 : 8;
   }
   if (kind == 1) {  // NN dX
@@ -530,10 +657,73 @@ bool launch_epi(int epi, const GemmParams& p, int id, int splits, hipStream_t st
   return false;
 }
 
+// Split-K weight gradients: 0 = slabs + a separate reduce launch (default), 1 = in-kernel
+// fixup by the last-arriving split (FD_GEMM_FIXUP=1 / fd_gemm_set_fixup).  The fixup needs a
+// device-scope release/acquire pair per block (L2 writeback + invalidate across the 8 XCDs'
+// L2s); measured on MI355X at bs32 x seq128 that costs ~40 us per launch, far more than the
+// 5 us reduce launch it saves (2.89 vs 2.38 ms/step, profiles/r1_ab_fused_adam_fixup.txt).
+int g_fixup = -1;
+bool fixup_enabled() {
+  if (g_fixup < 0) {
+    const char* e = getenv("FD_GEMM_FIXUP");
+    g_fixup = (e && atoi(e) != 0) ? 1 : 0;
+  }
+  return g_fixup == 1;
+}
+
+// Launch the weight-gradient GEMM(s) ps[0..nprob) (ps[i].C = final fp32 gradient, k_split
+// unset) with `splits` K splits: direct (one split), in-kernel split-K fixup (arrival
+// counters), or legacy slabs + reduce.  adams[i].p != nullptr fuses Adam into the epilogue
+// (direct / fixup only: the legacy path falls back to one split).
+int dw_launch(GemmParams* ps, int nprob, int id, int splits, int K, float* workspace, long long workspace_elems,
+              int accumulate, int* cnt, long long ncnt, const FdAdamEpi* adams, hipStream_t st) {
+  long long tiles = 0, slab_total = 0;
+  bool fused = false;
+  for (int i = 0; i < nprob; ++i) {
+    tiles += tiles_of(id, ps[i].M, ps[i].N);
+    slab_total += (long long)ps[i].M * ps[i].N;
+    if (adams && adams[i].p) fused = true;
+  }
+  if (splits > 1 && workspace_elems < slab_total * splits) splits = 1;
+  const bool fix = splits > 1 && cnt != nullptr && ncnt >= tiles && fixup_enabled();
+  if (splits > 1 && !fix && fused) splits = 1;
+  float* finals[2] = {(float*)ps[0].C, nprob > 1 ? (float*)ps[1].C : nullptr};
+  long long off = 0;
+  for (int i = 0; i < nprob; ++i) {
+    GemmParams& p = ps[i];
+    p.k_split = K / splits;
+    p.accumulate = accumulate;
+    if (adams) p.adam = adams[i];
+    if (splits == 1) {
+      p.out = finals[i]; p.tile_cnt = nullptr; p.slab_stride = 0;
+    } else {
+      p.C = workspace + off; p.slab_stride = (long long)p.M * p.N; p.ldc = p.N;
+      off += p.slab_stride * splits;
+      p.out = fix ? finals[i] : nullptr;
+      p.tile_cnt = fix ? cnt : nullptr;
+    }
+  }
+  if (!launch_id<false, false, EPI_F32>(ps[0], id, splits, st, nprob > 1 ? &ps[1] : nullptr)) return 7;
+  if (splits > 1 && !fix) {
+    for (int i = 0; i < nprob; ++i) {
+      const long long n4 = ps[i].slab_stride / 4;
+      const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ps[i].C, finals[i], n4,
+                         ps[i].slab_stride, splits, accumulate);
+    }
+  }
+  return 0;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- C ABI
 extern "C" {
+
+int fd_gemm_set_fixup(int on) {
+  g_fixup = on ? 1 : 0;
+  return 0;
+}
 
 // Force a configuration id / split count for a GEMM kind (tuning; -1 = auto).
 int fd_gemm_set_cfg(int kind, int cfg, int splits) {
@@ -547,7 +737,8 @@ int fd_gemm_set_cfg(int kind, int cfg, int splits) {
 // Returns 0 on success, nonzero on unsupported shape.
 int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
             const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
-            long long workspace_elems, int accumulate, hipStream_t st) {
+            long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+            hipStream_t st) {
   if (K % BKT != 0 || N % 64 != 0 || M <= 0 || kind < 0 || kind > 2) return 1;
   GemmParams p{};
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.C = C;
@@ -591,29 +782,16 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
   } else {
     while (tiles * splits < 400 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 512) splits *= 2;
   }
-  const long long slab = (long long)M * N;
-  if (splits > 1 && workspace_elems < slab * splits) splits = 1;
-  p.k_split = K / splits;
-  float* out = (float*)C;
-  if (splits == 1 && !accumulate) {
-    p.slab_stride = 0;
-    return launch_epi<false, false>(EPI_F32, p, id, 1, st) ? 0 : 7;
-  }
   if (ldc != N) return 4;
-  p.C = workspace; p.ldc = N; p.slab_stride = slab;
-  if (!launch_epi<false, false>(EPI_F32, p, id, splits, st)) return 7;
-  const long long n4 = slab / 4;
-  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, workspace, out, n4, slab, splits,
-                     accumulate);
-  return 0;
+  return dw_launch(&p, 1, id, splits, K, workspace, workspace_elems, accumulate, tile_cnt, ncnt, adam, st);
 }
 
 // Two weight-gradient GEMMs over the same token dimension in ONE launch:
 //   C0[M0][N0] (+)= A0^T B0,  C1[M1][N1] (+)= A1^T B1   (A_i [K][M_i], B_i [K][N_i] bf16; C_i fp32)
 // Split K only while the combined grid is under one round; slabs of problem 0 then 1.
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
-                int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, hipStream_t st) {
+                int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, int* tile_cnt,
+                long long ncnt, const FdAdamEpi* adams, hipStream_t st) {
   if (K % BKT != 0 || M0 % 128 || M1 % 128 || N0 % 64 || N1 % 64 || M0 <= 0 || M1 <= 0) return 1;
   int id = cfg_override(2);
   if (id < 0) id = 8;
@@ -640,22 +818,7 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
   } else {
     while (tiles * splits < 400 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 512) splits *= 2;
   }
-  const long long slab0 = (long long)M0 * N0, slab1 = (long long)M1 * N1;
-  if (splits > 1 && workspace_elems < (slab0 + slab1) * splits) splits = 1;
-  for (int i = 0; i < 2; ++i) p[i].k_split = K / splits;
-  if (splits == 1 && !accumulate) {
-    return launch_id<false, false, EPI_F32>(p[0], id, 1, st, &p[1]) ? 0 : 7;
-  }
-  p[0].C = workspace; p[0].slab_stride = slab0;
-  p[1].C = workspace + slab0 * splits; p[1].slab_stride = slab1;
-  if (!launch_id<false, false, EPI_F32>(p[0], id, splits, st, &p[1])) return 7;
-  for (int i = 0; i < 2; ++i) {
-    const long long n4 = (i ? slab1 : slab0) / 4;
-    const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)p[i].C, Cs[i], n4,
-                       i ? slab1 : slab0, splits, accumulate);
-  }
-  return 0;
+  return dw_launch(p, 2, id, splits, K, workspace, workspace_elems, accumulate, tile_cnt, ncnt, adams, st);
 }
 
 }  // extern "C"

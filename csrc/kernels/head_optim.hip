@@ -172,7 +172,23 @@ struct AdamArgs {
   int row4;                         // float4s per row in that range
   const unsigned char* touched;     // sticky row flags: nonzero Adam state (nullable)
   const unsigned char* now;         // rows with a valid gradient this step (nullable = all)
+  // Disjoint float4 runs of the arena to update ([start4, count4, first virtual index] each,
+  // ascending), nullable = all of [0, n4).  Used when the weight-gradient GEMMs already
+  // applied Adam to the encoder matrices in their epilogues: one launch covers the rest.
+  const long long* runs;
+  int nruns;
 };
+
+// virtual index -> arena float4 index through the run table (binary search on the prefix)
+DEV long long run_index(const long long* runs, int nruns, long long i) {
+  int lo = 0, hi = nruns - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (runs[3 * mid + 2] <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  return runs[3 * lo] + (i - runs[3 * lo + 2]);
+}
 
 // NT: the moments (and the gradient) are touched once per step -> stream them with
 // nontemporal loads/stores so they do not evict the weights / bf16 shadow the next
@@ -192,7 +208,8 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const float bc2 = 1.f - powf(a.b2, (float)t);
   const float step_size = a.lr / bc1;
   const float inv_sqrt_bc2 = 1.f / sqrtf(bc2);
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < a.n4; i += (long long)gridDim.x * 256) {
+  for (long long vi = blockIdx.x * 256ll + threadIdx.x; vi < a.n4; vi += (long long)gridDim.x * 256) {
+    const long long i = a.runs ? run_index(a.runs, a.nruns, vi) : vi;
     // Rows never touched since the moments were reset have m = v = g = 0: their
     // Adam update is exactly zero, so skip all their traffic (wd == 0 only).
     bool gvalid = true;
@@ -314,11 +331,13 @@ int fd_eval_metrics(const float* logits, const long long* labels, int B, double*
 
 int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float lr,
             float b1, float b2, float eps, float wd, int decoupled, const unsigned char* touched,
-            const unsigned char* now, long long skip_off, long long skip_rows, int row_len, hipStream_t st) {
+            const unsigned char* now, long long skip_off, long long skip_rows, int row_len, const long long* runs,
+            int nruns, long long run_total4, hipStream_t st) {
   if (n % 4 != 0 || skip_off % 4 != 0 || row_len % 4 != 0) return 1;
   if (wd != 0.f && touched) return 3;  // skipping untouched rows is exact only without weight decay
-  AdamArgs a{p, g, m, v, (bf16_t*)shadow, n / 4, step, lr, b1, b2, eps, wd, decoupled,
-             skip_off / 4, (skip_off + skip_rows * row_len) / 4, row_len / 4, touched, now};
+  if (runs && (nruns <= 0 || run_total4 <= 0)) return 4;
+  AdamArgs a{p, g, m, v, (bf16_t*)shadow, runs ? run_total4 : n / 4, step, lr, b1, b2, eps, wd, decoupled,
+             skip_off / 4, (skip_off + skip_rows * row_len) / 4, row_len / 4, touched, now, runs, nruns};
   // FD_ADAM_NT: 0 = default cache policy, 1 = nontemporal g/m/v, 2 = also the fp32 master (default:
   // 2.336 vs 2.366-2.387 ms/step, profiles/r1_ab_adam_nt_master.txt -- only the bf16 shadow is re-read soon)
   static const int nt = [] { const char* e = getenv("FD_ADAM_NT"); return e ? atoi(e) : 2; }();

@@ -19,6 +19,23 @@ as flat torch ops.
 Measured on MI355X (bs32 x seq128): overlap makes the step SLOWER (3.86 vs
 3.51 ms) -- the concurrent Adam blocks take CU slots from the one-round GEMM
 grids and HBM bandwidth from LayerNorm/colsum -- so it is off by default.
+
+Fused mode (``fuse_dw=True``; active inside a training step's
+``fused_adam_scope``): the encoder's 24 weight matrices (89 % of the dense
+parameters) are updated by the weight-gradient GEMMs themselves -- the epilogue
+applies Adam to the finished fp32 gradient tile (csrc/kernels/gemm.hip
+``adam_epi4``, same arithmetic as the Adam kernel) instead of storing it, so the
+gradient never round-trips through HBM and the p/m/v/shadow traffic streams
+while other tiles of the grid are still on the MFMAs.  ``step()`` then updates
+the rest (embeddings, biases, LayerNorms, head) in one launch over a run table.
+The W^T copies the backward's dX GEMMs read are taken before the step, so a
+block's later dX GEMMs still see the pre-update weights.  Bitwise identical to
+the unfused step (tests/test_fused_adam_gpu.py), but measured on MI355X at bs32 x
+seq128 it does not pay: the dW grids run as one round, so every tile reaches its
+Adam epilogue at the same time and the ~1.1 GB of optimizer traffic no longer
+overlaps anything (dW GEMMs +260 us vs Adam -180 us and the split-K reduces
+-64 us; 2.39-2.42 vs 2.37-2.38 ms/step, profiles/r1_ab_fused_adam_fixup.txt).
+Off by default.
 """
 from __future__ import annotations
 
@@ -30,9 +47,12 @@ import torch
 
 class ArenaAdam:
     def __init__(self, model, lr: float = 2e-5, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, decoupled: bool = False, overlap: bool = False):
+                 weight_decay: float = 0.0, decoupled: bool = False, overlap: bool = False,
+                 fuse_dw: bool = False):
         self.model = model
         self.overlap = overlap
+        self.fuse_dw = fuse_dw
+        self._run_tables = {}
         self.arena = model.arena
         self.lr, self.betas, self.eps = lr, tuple(betas), eps
         self.weight_decay, self.decoupled = weight_decay, decoupled
@@ -95,6 +115,46 @@ class ArenaAdam:
             self._update(off, n, False)
         self._done.append((off, n))
 
+    def can_fuse(self) -> bool:
+        """Whether the model's weight-gradient GEMMs may apply this optimizer's step."""
+        m = self.model
+        return (self.fuse_dw and not self.overlap and self.arena.device.type == "cuda"
+                and getattr(m, "impl", "") == "hip" and getattr(m, "transposed_dx", False)
+                and getattr(m, "group_dw", False) and getattr(m, "layer_grads_hook", None) is None
+                and self.arena.shadow is not None)
+
+    def fused_args(self, grads):
+        """(state tensors, hyper-parameters) for a weight-gradient GEMM that applies Adam to
+        ``grads`` (arena grad views) in its epilogue; those spans are skipped by ``step()``."""
+        from ..ops import kernels as K  # noqa: F401  (extension must be present)
+        self._begin()
+        A = self.arena
+        base = A.grad.data_ptr()
+        st = []
+        for g in grads:
+            off = (g.data_ptr() - base) // A.grad.element_size()
+            n = g.numel()
+            if not (0 <= off and off + n <= A.numel) or not g.is_contiguous():
+                raise ValueError("fused Adam: gradient is not a contiguous arena view")
+            st += [A.master[off:off + n], self.m[off:off + n], self.v[off:off + n], A.shadow[off:off + n]]
+            self._done.append((off, n))
+        st.append(self.step_t)
+        b1, b2 = self.betas
+        return st, [self.lr, b1, b2, self.eps, self.weight_decay, 1.0 if self.decoupled else 0.0]
+
+    def _runs_table(self, runs):
+        """Cached device run table for ``runs`` (built during the eager warm-up steps, so a
+        graph capture never needs a host->device copy)."""
+        key = tuple(runs)
+        t = self._run_tables.get(key)
+        if t is None:
+            if torch.cuda.is_current_stream_capturing():
+                return None
+            from ..ops import kernels as K
+            t = K.adam_runs(runs, self.arena.device)
+            self._run_tables[key] = t
+        return t
+
     def reset_state(self):
         """FedAvg rounds restart the moments (the reference re-creates Adam each run)."""
         self.m.zero_()
@@ -131,8 +191,21 @@ class ArenaAdam:
             if pos < A.numel:
                 runs.append((pos, A.numel - pos))
             woff = self.model.word_embedding_span()[0] if sparse else -1
-            for off, n in runs:
-                self._update(off, n, sparse and off <= woff < off + n)
+            table = self._runs_table(runs) if len(runs) > 1 else None
+            if table is not None:  # everything left (fused-GEMM spans excluded) in one launch
+                from ..ops import kernels as K
+                b1, b2 = self.betas
+                if sparse:
+                    _, rows, rl = self.model.word_embedding_span()
+                    K.adam(A.master, A.grad, self.m, self.v, A.shadow, self.step_t, self.lr, b1, b2, self.eps,
+                           self.weight_decay, self.decoupled, self.model.emb_ever, self.model.emb_now, woff, rows,
+                           rl, runs=table)
+                else:
+                    K.adam(A.master, A.grad, self.m, self.v, A.shadow, self.step_t, self.lr, b1, b2, self.eps,
+                           self.weight_decay, self.decoupled, runs=table)
+            else:
+                for off, n in runs:
+                    self._update(off, n, sparse and off <= woff < off + n)
             if self._side is not None:
                 torch.cuda.current_stream(A.device).wait_stream(self._side)
             self._done = []

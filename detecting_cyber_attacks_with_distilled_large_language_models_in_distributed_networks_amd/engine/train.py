@@ -17,16 +17,39 @@ import torch
 from .graph import GraphedTrainStep
 
 
+class fused_adam_scope:
+    """Within a training step (forward + backward, then ``optimizer.step()``), let the
+    model's weight-gradient GEMMs apply the optimizer's Adam step in their epilogues
+    (engine/optim.py, fused mode).  Outside the scope -- gradient accumulation, a bare
+    ``backward()``, data-parallel steps whose gradients must be all-reduced first --
+    gradients are materialised as usual."""
+
+    def __init__(self, model, optimizer):
+        self.model = model
+        self.opt = optimizer if getattr(optimizer, "can_fuse", lambda: False)() else None
+
+    def __enter__(self):
+        if self.opt is not None:
+            self.model.fused_opt = self.opt
+        return self
+
+    def __exit__(self, *exc):
+        if self.opt is not None:
+            self.model.fused_opt = None
+        return False
+
+
 def make_step_fn(model, optimizer, criterion=None):
     fused = criterion is None or isinstance(criterion, torch.nn.CrossEntropyLoss)
 
     def step(ids, mask, labels, tokens=None):
         optimizer.zero_grad()
-        if fused:
-            loss, _ = model.forward_loss(ids, mask, labels, tokens=tokens)
-        else:
-            loss = criterion(model(ids, mask, tokens=tokens), labels)
-        loss.backward()
+        with fused_adam_scope(model, optimizer):
+            if fused:
+                loss, _ = model.forward_loss(ids, mask, labels, tokens=tokens)
+            else:
+                loss = criterion(model(ids, mask, tokens=tokens), labels)
+            loss.backward()
         optimizer.step()
         return loss.detach()
 
@@ -42,9 +65,10 @@ def make_kd_step_fn(student, teacher, optimizer, temperature: float = 2.0, alpha
         optimizer.zero_grad()
         with torch.no_grad():
             t_logits = teacher(ids, mask, tokens=tokens)
-        s_logits = student(ids, mask, tokens=tokens)
-        loss = kd_loss(s_logits, t_logits, labels, temperature, alpha)
-        loss.backward()
+        with fused_adam_scope(student, optimizer):
+            s_logits = student(ids, mask, tokens=tokens)
+            loss = kd_loss(s_logits, t_logits, labels, temperature, alpha)
+            loss.backward()
         optimizer.step()
         return loss.detach()
 

@@ -256,6 +256,9 @@ class DDoSClassifier(nn.Module):
         # the memory-bound transposes stretch the concurrent forward GEMMs.  Off by default.
         self.overlap_transpose = False
         self._tstream = None
+        # optimizer that applies Adam inside the weight-gradient GEMM epilogues; set only for
+        # the duration of a training step (engine/train.py fused_adam_scope)
+        self.fused_opt = None
         self.torch_counter = 0
         self._grad_token = None
         self._synced_version = -1
@@ -436,6 +439,9 @@ class DDoSClassifier(nn.Module):
                     wgrad=self._wgrad if grad and self.wgrad_stream else None, group_dw=self.group_dw)
         if grad and self.defer_colsum and self.layer_grads_hook is None:
             rc.colsum_jobs = []  # (a per-block hook needs each block's grads final at once)
+        if (grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None
+                and not self.wgrad_stream and self.transposed_dx):
+            rc.fused_adam = self.fused_opt
         if self.training:
             K.step_inc(None, self.rng)
         token = self._grad_token if torch.is_grad_enabled() else None

@@ -57,6 +57,9 @@ class RunCtx:
     # side stream that produced data the backward reads (the W^T copies): joined at the
     # first backward node (the head)
     join_stream: Optional["torch.cuda.Stream"] = None
+    # optimizer whose Adam step the weight-gradient GEMMs apply in their epilogues
+    # (engine/optim.py ArenaAdam.fused_args; set only inside a training step's scope)
+    fused_adam: Optional[object] = None
 
 
 class _WGrad:
@@ -158,11 +161,18 @@ class LayerFn(torch.autograd.Function):
         dz2, df = K.ln_bwd(dy, f, h, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, rc.seed,
                            ffn_site, p_h, acc, rc.row_map, jobs)
         wt = L.get("wT") or {}
+        # Adam fused into the grouped dW epilogues: the weights are updated in the middle of
+        # this backward, so every later reader must use the W^T copies taken before the step
+        fa = rc.fused_adam
+        if fa is not None and (acc or not rc.group_dw or rc.wgrad is not None or wt.get("l1_w") is None
+                               or wt.get("qkv_w") is None):
+            fa = None
         du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"))  # dg W2 * gelu'(u)
         wg.fork(df, g, du, h)
         with wg.ctx():
             if rc.group_dw:
-                K.linear_dw2(df, g, G["l2_w"].buf, du, h, G["l1_w"].buf, acc)
+                K.linear_dw2(df, g, G["l2_w"].buf, du, h, G["l1_w"].buf, acc,
+                             adam=fa.fused_args([G["l2_w"].buf, G["l1_w"].buf]) if fa else None)
             else:
                 K.linear_dw(df, g, G["l2_w"].buf, acc)
                 K.linear_dw(du, h, G["l1_w"].buf, acc)
@@ -180,7 +190,8 @@ class LayerFn(torch.autograd.Function):
         wg.fork(dqkv, x, dz1, cx)
         with wg.ctx():
             if rc.group_dw:
-                K.linear_dw2(dz1, cx, G["o_w"].buf, dqkv, x, G["qkv_w"].buf, acc)
+                K.linear_dw2(dz1, cx, G["o_w"].buf, dqkv, x, G["qkv_w"].buf, acc,
+                             adam=fa.fused_args([G["o_w"].buf, G["qkv_w"].buf]) if fa else None)
             else:
                 K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
             K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)

@@ -72,20 +72,46 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] 
     return dx
 
 
-def linear_dw(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
-    """out[N_out, N_in] (fp32) (+)= dy^T x."""
+TILE_COUNTERS = 8192
+
+
+def tile_counters(device) -> torch.Tensor:
+    """Split-K arrival counters of the weight-gradient GEMMs (zeroed once; every launch
+    leaves them at zero again).  Fixed size, never reallocated: graphs keep the pointer."""
+    key = (str(device), "tile_cnt", torch.int32)
+    t = _WS.get(key)
+    if t is None:
+        t = torch.zeros(TILE_COUNTERS, dtype=torch.int32, device=device)
+        _WS[key] = t
+    return t
+
+
+def set_splitk_fixup(on: bool):
+    """Split-K weight gradients reduced inside the GEMM by the last-arriving split (True) or by a
+    separate reduce launch (False, the measured-faster default; csrc/kernels/gemm.hip)."""
+    ext().gemm_set_fixup(bool(on))
+
+
+def linear_dw(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
+              adam=None) -> torch.Tensor:
+    """out[N_out, N_in] (fp32) (+)= dy^T x; split-K partials are reduced inside the GEMM.
+    adam = (state, hyper) from ``ArenaAdam.fused_args``: apply Adam to the finished gradient
+    instead of storing it."""
     M, N = dy.shape[1], x.shape[1]
     ws = workspace(dy.device, "splitk", 8 * M * N)
-    ext().gemm(2, 5, dy, x, out, None, None, None, ws, accumulate)
+    st, hp = adam if adam is not None else ([], [])
+    ext().gemm_dw(dy, x, out, ws, accumulate, tile_counters(dy.device), st, hp)
     return out
 
 
 def linear_dw2(dy0: torch.Tensor, x0: torch.Tensor, out0: torch.Tensor, dy1: torch.Tensor, x1: torch.Tensor,
-               out1: torch.Tensor, accumulate: bool = False):
-    """Two weight gradients that become ready together, one launch: out_i (+)= dy_i^T x_i."""
+               out1: torch.Tensor, accumulate: bool = False, adam=None):
+    """Two weight gradients that become ready together, one launch: out_i (+)= dy_i^T x_i
+    (adam: fused optimizer step for both, see ``linear_dw``)."""
     n = out0.numel() + out1.numel()
     ws = workspace(dy0.device, "splitk", 8 * n)
-    ext().gemm_dw2(dy0, x0, out0, dy1, x1, out1, ws, accumulate)
+    st, hp = adam if adam is not None else ([], [])
+    ext().gemm_dw2(dy0, x0, out0, dy1, x1, out1, ws, accumulate, tile_counters(dy0.device), st, hp)
 
 
 def transpose_many(srcs, dsts):
@@ -250,10 +276,27 @@ def eval_metrics(logits, labels, acc, counts, prob1=None, preds=None):
 
 
 def adam(p, g, m, v, shadow, step, lr, b1, b2, eps, wd, decoupled, touched=None, now=None, skip_off=0, skip_rows=0,
-         row_len=4):
+         row_len=4, runs=None):
     """Flat-arena Adam.  touched/now (uint8 row flags over [skip_off, skip_off+skip_rows*row_len)) let
-    the kernel skip rows with zero state and zero gradient (exact for weight_decay == 0)."""
-    ext().adam(p, g, m, v, shadow, step, lr, b1, b2, eps, wd, decoupled, touched, now, skip_off, skip_rows, row_len)
+    the kernel skip rows with zero state and zero gradient (exact for weight_decay == 0).
+    runs = (device int64 [n, 3] table, total float4s, largest end float4) from ``adam_runs``:
+    update only those element runs, in one launch."""
+    table, total4, end4 = runs if runs is not None else (None, 0, 0)
+    ext().adam(p, g, m, v, shadow, step, lr, b1, b2, eps, wd, decoupled, touched, now, skip_off, skip_rows, row_len,
+               table, total4, end4)
+
+
+def adam_runs(spans, device):
+    """[(offset, numel)] element runs (multiples of 4, ascending, disjoint) -> the kernel's
+    run table [start4, count4, prefix4] on ``device`` + its total and largest end (float4s)."""
+    rows, pre, end = [], 0, 0
+    for off, n in spans:
+        if off % 4 or n % 4 or off < end:
+            raise ValueError(f"adam run ({off}, {n}) not float4-aligned / ascending")
+        rows.append((off // 4, n // 4, pre))
+        pre += n // 4
+        end = off + n
+    return torch.tensor(rows, dtype=torch.int64, device=device), pre, end // 4
 
 
 def step_inc(step=None, seed=None):

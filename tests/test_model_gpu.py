@@ -131,7 +131,7 @@ def test_overlapped_adam_matches_single_pass(graph):
     for overlap in (True, False):
         m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=5)
         m.train()
-        opt = ArenaAdam(m, lr=1e-3, overlap=overlap)
+        opt = ArenaAdam(m, lr=1e-3, overlap=overlap, fuse_dw=False)
         assert (m.layer_grads_hook is not None) == overlap
         models.append(m)
         steps.append(GraphedTrainStep(make_step_fn(m, opt), warmup=1, enabled=graph))
@@ -181,7 +181,8 @@ def test_wgrad_side_stream_matches_serial(graph):
         m.wgrad_stream = side
         m.train()
         models.append(m)
-        steps.append(GraphedTrainStep(make_step_fn(m, ArenaAdam(m, lr=1e-3)), warmup=1, enabled=graph))
+        steps.append(GraphedTrainStep(make_step_fn(m, ArenaAdam(m, lr=1e-3, fuse_dw=False)), warmup=1,
+                                      enabled=graph))
     for it in range(4):
         ids, mask, labels = _batch(16, 128, seed=200 + it)
         for st in steps:
