@@ -99,12 +99,15 @@ def main():
     opt = engine.ArenaAdam(model, lr=2e-5, fuse_dw=args.fused_adam)
     gsync = None
     if topo.dp:
+        teacher = None
         if args.teacher:
-            raise SystemExit("--teacher with --gpus-per-client > 1 is not supported")
+            teacher = models.BertTeacherClassifier(config=models.bert_base_config(), device=dev, impl=args.impl)
+            fedavg.broadcast_model(teacher, comm=ncomm)
+            teacher.eval()
         dp.dp_seed_offset(model, topo.dp_rank)
         gsync = dp.GradSync(model, topo.dp_group, topo.gpus_per_client, max_rows=B * S)
         gsync.set_loss_scale(1.0 / topo.gpus_per_client)
-        fn = dp.make_dp_step_fn(model, opt, gsync)
+        fn = dp.make_dp_step_fn(model, opt, gsync, teacher, 2.0, 0.5)
     elif args.teacher:
         teacher = models.BertTeacherClassifier(config=models.bert_base_config(), device=dev, impl=args.impl)
         fedavg.broadcast_model(teacher, comm=ncomm)

@@ -88,10 +88,12 @@ def train_model(model, train_loader, criterion=None, optimizer=None, num_epochs:
         log.phase("Starting model training" + (" (distillation from teacher)" if teacher is not None else ""))
     model.train()
     if teacher is not None:
-        if grad_sync is not None:
-            raise NotImplementedError("distillation with data-parallel clients")
         teacher.eval()
-        fn = make_kd_step_fn(model, teacher, optimizer, kd_temperature, kd_alpha)
+        if grad_sync is not None:
+            from ..parallel.dp import make_dp_step_fn
+            fn = make_dp_step_fn(model, optimizer, grad_sync, teacher, kd_temperature, kd_alpha)
+        else:
+            fn = make_kd_step_fn(model, teacher, optimizer, kd_temperature, kd_alpha)
     elif grad_sync is not None:
         from ..parallel.dp import make_dp_step_fn
         fn = make_dp_step_fn(model, optimizer, grad_sync)

@@ -105,6 +105,12 @@ class FederatedClient:
             self.teacher = BertTeacherClassifier(cfg.extra.get("teacher_path"), config=bert_base_config(),
                                                  device=dev, impl=cfg.impl)
             broadcast_model(self.teacher, comm=self.comm)
+        self.teacher_sync = None
+        if self.teacher is not None and self.topo.dp:
+            # the teacher fine-tune is data-parallel too, so every replica distils from the same teacher
+            dp_seed_offset(self.teacher, self.topo.dp_rank)
+            self.teacher_sync = GradSync(self.teacher, self.topo.dp_group, self.topo.gpus_per_client,
+                                         max_rows=cfg.batch_size * cfg.max_len)
         self.start_round = 0
         self.history: List[Dict] = []
         if cfg.resume:
@@ -144,7 +150,8 @@ class FederatedClient:
             t_opt = ArenaAdam(self.teacher, lr=cfg.lr)
             with self.timer("teacher"):
                 train_model(self.teacher, self.train_loader, None, t_opt, int(cfg.extra.get("teacher_epochs", cfg.epochs)),
-                            log=log, use_graph=cfg.use_graph)
+                            log=log, use_graph=cfg.use_graph and (self.teacher_sync is None or cfg.dp_graph),
+                            grad_sync=self.teacher_sync)
         with self.timer("train"):
             use_graph = cfg.use_graph and (self.grad_sync is None or cfg.dp_graph)
             tr = train_model(model, self.train_loader, None, opt, cfg.epochs, log=log, use_graph=use_graph,
@@ -177,9 +184,11 @@ class FederatedClient:
         with self.timer("fedavg"):
             t0 = time.perf_counter()
             if cfg.transport == "tcp":
+                # one upload per client (its replica 0, as the reference's one process per
+                # client); the other replicas take the aggregate from it
+                total_w = self._tcp_exchange(contributes) if self.topo.dp_rank == 0 else 0.0
                 if self.topo.dp:
-                    raise NotImplementedError("tcp transport with data-parallel clients")
-                total_w = self._tcp_exchange(contributes)
+                    total_w = self._dp_share_model(total_w)
             else:
                 total_w = fedavg_(model, weight=weight, participate=contributes, comm=self.comm)
             if model.device.type == "cuda":
@@ -227,6 +236,18 @@ class FederatedClient:
             return 0.0
         self.model.load_state_dict(agg)
         return float(self.num_clients)
+
+    def _dp_share_model(self, total_w: float) -> float:
+        """Replica 0 of this client -> the client's other replicas: weights + FedAvg weight."""
+        import torch.distributed as dist
+        A = self.model.arena
+        src = self.topo.client_ranks(self.topo.client_idx)[0]
+        dist.broadcast(A.master, src=src, group=self.topo.dp_group)
+        t = torch.tensor([total_w], dtype=torch.float64, device=A.device)
+        dist.broadcast(t, src=src, group=self.topo.dp_group)
+        if hasattr(self.model, "sync_shadow"):
+            self.model.sync_shadow(force=True)
+        return float(t.item())
 
     # ------------------------------------------------------------------ all rounds
     def run(self) -> Dict:

@@ -196,16 +196,28 @@ class GradSync:
             self.model.layer_grads_hook = self._prev_hook
 
 
-def make_dp_step_fn(model, optimizer, sync: GradSync):
+def make_dp_step_fn(model, optimizer, sync: GradSync, teacher=None, temperature: float = 2.0,
+                    alpha: float = 0.5):
     """Data-parallel train step: scaled local loss -> backward (overlapped block
     all-reduces) -> finish the exchange -> Adam.  Returns this replica's share of
-    the client-batch mean loss (sum over replicas = the client-batch mean)."""
+    the client-batch mean loss (sum over replicas = the client-batch mean).
+
+    teacher: distillation (engine/train.py make_kd_step_fn) on the replica's shard -- the
+    frozen teacher is identical on every replica, so the shard-mean KD losses, scaled by
+    the shard shares, sum to the client-batch KD loss exactly as the CE loss does."""
     if getattr(optimizer, "overlap", False):
         raise ValueError("data-parallel clients need ArenaAdam(overlap=False)")
+    if teacher is not None:
+        from ..models.bert import kd_loss
 
     def step(ids, mask, labels, tokens=None):  # shards run the padded path (no per-shard token count)
         optimizer.zero_grad()
-        loss, _ = model.forward_loss(ids, mask, labels)
+        if teacher is None:
+            loss, _ = model.forward_loss(ids, mask, labels)
+        else:
+            with torch.no_grad():
+                t_logits = teacher(ids, mask)
+            loss = kd_loss(model(ids, mask), t_logits, labels, temperature, alpha)
         scaled = loss * sync.loss_scale
         scaled.backward()
         sync.finish()

@@ -142,3 +142,108 @@ def test_two_dp_clients_federated_run(tmp_path):
         assert (tmp_path / f"client{cid}_local_metrics.csv").exists()
         assert (tmp_path / f"client{cid}_model.pth").exists()
     assert not (tmp_path / "client3_model.pth").exists()
+
+
+def _kd_grad_worker(rank, world, port, outdir):
+    _env(rank, world, port)
+    from importlib import import_module
+    comm = import_module(f"{PKG}.parallel.comm")
+    dp = import_module(f"{PKG}.parallel.dp")
+    comm.init_distributed(device="cpu")
+    topo = dp.make_topology(2)
+    m, t = _model(), _teacher()
+    ids, mask, labels = _batch()
+    b = {"input_ids": ids, "attention_mask": mask, "labels": labels}
+
+    class _L:
+        n, batch_size, drop_last = 7, 7, False
+
+        def __iter__(self):
+            yield b
+
+    class _NoStep:  # keep the exchanged gradient for inspection
+        overlap = False
+
+        def zero_grad(self):
+            m.zero_grad()
+
+        def step(self):
+            pass
+
+    shard = next(iter(dp.DPShardLoader(_L(), topo.dp_rank, 2)))
+    sync = dp.GradSync(m, topo.dp_group, 2)
+    sync.set_loss_scale(shard["loss_scale"])
+    step = dp.make_dp_step_fn(m, _NoStep(), sync, teacher=t, temperature=2.0, alpha=0.5)
+    step(shard["input_ids"], shard["attention_mask"], shard["labels"])
+    torch.save(m.arena.grad.clone(), os.path.join(outdir, f"kdgrad{rank}.pt"))
+    comm.shutdown()
+
+
+def _teacher():
+    from importlib import import_module
+    models = import_module(f"{PKG}.models")
+    cfg = models.DistilBertConfig(n_layers=2, dropout=0.0, attention_dropout=0.0)
+    t = models.BertTeacherClassifier(config=cfg, seed=11, head_dropout=0.0, impl="torch")
+    t.eval()
+    return t
+
+
+def test_dp_distillation_gradient_equals_full_batch(tmp_path):
+    """KD on a data-parallel client: the replicas' shard-weighted KD gradients sum to the
+    full-batch KD gradient (same frozen teacher on every replica)."""
+    from importlib import import_module
+    kd_loss = import_module(f"{PKG}.models.bert").kd_loss
+    port = _free_port()
+    mp.spawn(_kd_grad_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    g0 = torch.load(tmp_path / "kdgrad0.pt", weights_only=True)
+    g1 = torch.load(tmp_path / "kdgrad1.pt", weights_only=True)
+    assert torch.equal(g0, g1)
+    m, t = _model(), _teacher()
+    ids, mask, labels = _batch()
+    m.zero_grad()
+    with torch.no_grad():
+        tl = t(ids, mask)
+    kd_loss(m(ids, mask), tl, labels, 2.0, 0.5).backward()
+    ref = m.arena.grad
+    assert torch.allclose(g0, ref, rtol=1e-4, atol=1e-7), (g0 - ref).abs().max()
+
+
+def _tcp_fed_worker(rank, world, port, outdir, pr, ps):
+    _env(rank, world, port)
+    from importlib import import_module
+    runner = import_module(f"{PKG}.fed.runner")
+    config = import_module(f"{PKG}.config")
+    models = import_module(f"{PKG}.models")
+    data = import_module(f"{PKG}.data")
+    comm = import_module(f"{PKG}.parallel.comm")
+    comm.init_distributed(device="cpu")
+    cfg = config.FedConfig(out_dir=outdir, synthetic_rows=800, data_fraction=0.1, max_len=64, epochs=1,
+                           batch_size=8, eval_batch_size=16, plots=False, resume=False, rounds=1,
+                           verbose=False, gpus_per_client=2, transport="tcp", server_host="127.0.0.1",
+                           port_receive=pr, port_send=ps, timeout_s=60.0)
+    frame = data.generate_cicids2017(cfg.synthetic_rows, seed=0)
+    client = runner.FederatedClient(cfg, frame=frame, model_config=models.DistilBertConfig(n_layers=1))
+    client.run()
+    torch.save(client.model.arena.master.clone(), os.path.join(outdir, f"tcpmaster{rank}.pt"))
+    comm.shutdown()
+
+
+def test_two_dp_clients_over_the_reference_tcp_protocol(tmp_path):
+    """2 clients x 2 replicas with the reference's star TCP exchange: one upload per client
+    (replica 0), the server's mean reaches every replica of both clients."""
+    import threading
+    from importlib import import_module
+    tp = import_module(f"{PKG}.parallel.transport")
+    pr, ps = _free_port(), _free_port()
+    srv = tp.FedAvgServer(2, "127.0.0.1", pr, ps, timeout=60)
+    res = {}
+    th = threading.Thread(target=lambda: res.setdefault("agg", srv.run_round()), daemon=True)
+    th.start()
+    srv.ready.wait(10)
+    port = _free_port()
+    mp.spawn(_tcp_fed_worker, args=(4, port, str(tmp_path), pr, ps), nprocs=4, join=True)
+    th.join(60)
+    ms = [torch.load(tmp_path / f"tcpmaster{r}.pt", weights_only=True) for r in range(4)]
+    for m in ms[1:]:
+        assert torch.equal(ms[0], m)  # every replica of both clients holds the server's mean
+    assert res.get("agg") is not None and len(srv.received) == 2
