@@ -47,6 +47,8 @@ def main():
                          "runs the first ~100 ms of work measurably slower); no model state is touched")
     ap.add_argument("--no-quality", action="store_true",
                     help="skip the post-timing aggregated-F1 evaluation (kernel profiles of the step alone)")
+    ap.add_argument("--no-defer-dw", action="store_true",
+                    help="reduce each split-K weight gradient right after its GEMM instead of once per step (A/B)")
     ap.add_argument("--fused-adam", action="store_true",
                     help="apply Adam inside the weight-gradient GEMM epilogues (A/B; measured no faster)")
     ap.add_argument("--padded", action="store_true",
@@ -92,6 +94,7 @@ def main():
     model = models.DDoSClassifier(config=cfg, device=dev, impl=args.impl, seed=0)
     model.wgrad_stream = args.wgrad_stream
     model.group_dw = not args.no_group_dw
+    model.defer_dw_reduce = not args.no_defer_dw
     ncomm = None
     if args.comm == "rccl" and dev.type == "cuda":
         ncomm = import_module(f"{PKG}.parallel.rccl").NativeComm()

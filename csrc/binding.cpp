@@ -22,7 +22,10 @@ int fd_gemm_set_cfg(int kind, int cfg, int splits);
 int fd_gemm_set_fixup(int on);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
                 int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, int* tile_cnt,
-                long long ncnt, const FdAdamEpi* adams, hipStream_t st);
+                long long ncnt, const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st);
+int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K);
+int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
+                             const int* splits, const int* accumulate, hipStream_t st);
 int fd_transpose_batched(const void* const* srcs, void* const* dsts, const int* rows, const int* cols, int n,
                          hipStream_t st);
 const char* fd_comm_last_error();
@@ -203,10 +206,10 @@ void gemm_dw(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, cons
 }
 
 // Grouped weight gradients: C0 (+)= A0^T B0 and C1 (+)= A1^T B1 in one launch (shared K = tokens).
-void gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C0, const at::Tensor& A1,
-              const at::Tensor& B1, const at::Tensor& C1, const at::Tensor& workspace, bool accumulate,
-              const c10::optional<at::Tensor>& counters, const std::vector<at::Tensor>& adam,
-              const std::vector<double>& hp) {
+int64_t gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C0, const at::Tensor& A1,
+                 const at::Tensor& B1, const at::Tensor& C1, const at::Tensor& workspace, bool accumulate,
+                 const c10::optional<at::Tensor>& counters, const std::vector<at::Tensor>& adam,
+                 const std::vector<double>& hp, bool defer) {
   const at::Tensor* As[2] = {&A0, &A1};
   const at::Tensor* Bs[2] = {&B0, &B1};
   const at::Tensor* Cs[2] = {&C0, &C1};
@@ -226,11 +229,37 @@ void gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C0, 
   if (!adam.empty()) adam_descs(adam, hp, Cs, 2, ad);
   long long ncnt;
   int* cnt = counters_ptr(counters, &ncnt);
+  int splits = 0;
   check_rc(fd_gemm_dw2(A0.data_ptr(), B0.data_ptr(), C0.data_ptr<float>(), (int)A0.size(1), (int)B0.size(1),
                        A1.data_ptr(), B1.data_ptr(), C1.data_ptr<float>(), (int)A1.size(1), (int)B1.size(1), (int)K,
                        workspace.data_ptr<float>(), workspace.numel(), accumulate ? 1 : 0, cnt, ncnt,
-                       adam.empty() ? nullptr : ad, stream()),
+                       adam.empty() ? nullptr : ad, defer ? 1 : 0, &splits, stream()),
            "gemm_dw2");
+  return splits;  // > 0: slabs left in `workspace` (problem 0 then 1) for splitk_reduce_batched
+}
+
+// Finish deferred split-K weight gradients: out_i (+)= sum_z slabs_i[z] (z order), one launch.
+void splitk_reduce_batched(const std::vector<at::Tensor>& slabs, const std::vector<at::Tensor>& outs,
+                           const std::vector<int64_t>& splits, const std::vector<int64_t>& accumulate) {
+  const size_t n = slabs.size();
+  TORCH_CHECK(outs.size() == n && splits.size() == n && accumulate.size() == n, "splitk_reduce_batched: ragged");
+  std::vector<const float*> sp(n);
+  std::vector<float*> op(n);
+  std::vector<long long> ne(n);
+  std::vector<int> sl(n), ac(n);
+  for (size_t i = 0; i < n; ++i) {
+    need(slabs[i], at::kFloat, "slabs");
+    need(outs[i], at::kFloat, "out");
+    TORCH_CHECK(splits[i] >= 1 && outs[i].numel() % 4 == 0 && slabs[i].numel() >= splits[i] * outs[i].numel(),
+                "splitk_reduce_batched: slab buffer smaller than splits x out");
+    sp[i] = slabs[i].data_ptr<float>();
+    op[i] = outs[i].data_ptr<float>();
+    ne[i] = outs[i].numel();
+    sl[i] = (int)splits[i];
+    ac[i] = accumulate[i] ? 1 : 0;
+  }
+  if (n) check_rc(fd_splitk_reduce_batched((int)n, sp.data(), op.data(), ne.data(), sl.data(), ac.data(), stream()),
+                  "splitk_reduce_batched");
 }
 
 // Unpadded-step layout in one launch: row_map [rows] int32, cu [B+1] int32, ids_packed [rows] int64.
@@ -720,6 +749,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_dw2", &gemm_dw2);
   m.def("gemm_dw", &gemm_dw);
+  m.def("splitk_reduce_batched", &splitk_reduce_batched);
+  m.def("gemm_dw2_splits", [](int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K) {
+    return (int64_t)fd_gemm_dw2_splits((int)M0, (int)N0, (int)M1, (int)N1, (int)K);
+  });
   m.def("gemm_set_fixup", [](bool on) { fd_gemm_set_fixup(on ? 1 : 0); });
   m.def("pack", &pack);
   m.def("transpose_batched", &transpose_batched);

@@ -528,6 +528,36 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// Deferred split-K reduces of a whole backward in one launch: job i owns blocks
+// [start[i], start[i+1]) and reduces exactly like splitk_reduce_kernel (same z order).
+constexpr int RED_MAXJ = 16;
+struct ReduceJob {
+  const float* slabs;
+  float* out;
+  long long n4, stride;
+  int splits, accumulate;
+};
+struct ReduceBatch {
+  ReduceJob j[RED_MAXJ];
+  int start[RED_MAXJ + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void splitk_reduce_batched_kernel(ReduceBatch rb) {
+  int ji = 0;
+  while (ji + 1 < rb.n && (int)blockIdx.x >= rb.start[ji + 1]) ++ji;
+  const ReduceJob& jb = rb.j[ji];
+  const int b0 = rb.start[ji], nb = rb.start[ji + 1] - b0;
+  for (long long i = (blockIdx.x - b0) * 256ll + threadIdx.x; i < jb.n4; i += (long long)nb * 256) {
+    float4 s = jb.accumulate ? reinterpret_cast<float4*>(jb.out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int z = 0; z < jb.splits; ++z) {
+      const float4 v = reinterpret_cast<const float4*>(jb.slabs + z * jb.stride)[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    reinterpret_cast<float4*>(jb.out)[i] = s;
+  }
+}
+
 // ---------------------------------------------------------------- configurations
 // id: BM x BN, waves WM x WN, ring depth S   (LDS = max(S*(BM+BN)*128 B, epilogue))
 //  0: 128 x  64, 2x2, S3      1: 128 x 128, 2x2, S2      2: 128 x  96, 2x2, S2 (K-major B)
@@ -676,7 +706,9 @@ bool fixup_enabled() {
 // counters), or legacy slabs + reduce.  adams[i].p != nullptr fuses Adam into the epilogue
 // (direct / fixup only: the legacy path falls back to one split).
 int dw_launch(GemmParams* ps, int nprob, int id, int splits, int K, float* workspace, long long workspace_elems,
-              int accumulate, int* cnt, long long ncnt, const FdAdamEpi* adams, hipStream_t st) {
+              int accumulate, int* cnt, long long ncnt, const FdAdamEpi* adams, int defer, int* splits_out,
+              hipStream_t st) {
+  if (splits_out) *splits_out = 0;
   long long tiles = 0, slab_total = 0;
   bool fused = false;
   for (int i = 0; i < nprob; ++i) {
@@ -704,6 +736,10 @@ int dw_launch(GemmParams* ps, int nprob, int id, int splits, int K, float* works
     }
   }
   if (!launch_id<false, false, EPI_F32>(ps[0], id, splits, st, nprob > 1 ? &ps[1] : nullptr)) return 7;
+  if (splits > 1 && !fix && defer) {  // the caller reduces the slabs later (fd_splitk_reduce_batched)
+    if (splits_out) *splits_out = splits;
+    return 0;
+  }
   if (splits > 1 && !fix) {
     for (int i = 0; i < nprob; ++i) {
       const long long n4 = ps[i].slab_stride / 4;
@@ -783,15 +819,34 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
     while (tiles * splits < 400 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 512) splits *= 2;
   }
   if (ldc != N) return 4;
-  return dw_launch(&p, 1, id, splits, K, workspace, workspace_elems, accumulate, tile_cnt, ncnt, adam, st);
+  return dw_launch(&p, 1, id, splits, K, workspace, workspace_elems, accumulate, tile_cnt, ncnt, adam, 0, nullptr,
+                   st);
 }
 
 // Two weight-gradient GEMMs over the same token dimension in ONE launch:
 //   C0[M0][N0] (+)= A0^T B0,  C1[M1][N1] (+)= A1^T B1   (A_i [K][M_i], B_i [K][N_i] bf16; C_i fp32)
 // Split K only while the combined grid is under one round; slabs of problem 0 then 1.
+// K splits fd_gemm_dw2 plans for these shapes (<= 0: unsupported) -- lets the caller size a
+// slab buffer of its own for a deferred reduce.
+int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K) {
+  int id = cfg_override(2);
+  if (id < 0) id = 8;
+  if (M0 % CFGS[id].bm || M1 % CFGS[id].bm || N0 % CFGS[id].bn || N1 % CFGS[id].bn) id = 8;
+  const long long tiles = tiles_of(id, M0, N0) + tiles_of(id, M1, N1);
+  int splits = 1;
+  const int so = splits_override();
+  if (so > 0) {
+    splits = so;
+    if (K % (splits * BKT) != 0) return 0;
+  } else {
+    while (tiles * splits < 400 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 512) splits *= 2;
+  }
+  return splits;
+}
+
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
                 int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, int* tile_cnt,
-                long long ncnt, const FdAdamEpi* adams, hipStream_t st) {
+                long long ncnt, const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st) {
   if (K % BKT != 0 || M0 % 128 || M1 % 128 || N0 % 64 || N1 % 64 || M0 <= 0 || M1 <= 0) return 1;
   int id = cfg_override(2);
   if (id < 0) id = 8;
@@ -809,16 +864,30 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
     p[i].M = Ms[i]; p[i].N = Ns[i]; p[i].K = K; p[i].lda = Ms[i]; p[i].ldb = Ns[i]; p[i].ldc = Ns[i];
     p[i].group_m = gm; p[i].diag = diag;
   }
-  const long long tiles = tiles_of(id, M0, N0) + tiles_of(id, M1, N1);
-  int splits = 1;
-  const int so = splits_override();
-  if (so > 0) {
-    splits = so;
-    if (K % (splits * BKT) != 0) return 6;
-  } else {
-    while (tiles * splits < 400 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 512) splits *= 2;
+  const int splits = fd_gemm_dw2_splits(M0, N0, M1, N1, K);
+  if (splits <= 0) return 6;
+  return dw_launch(p, 2, id, splits, K, workspace, workspace_elems, accumulate, tile_cnt, ncnt, adams, defer,
+                   splits_out, st);
+}
+
+// Reduce n deferred split-K weight gradients (slab layout of fd_gemm_dw2) in one launch.
+int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
+                             const int* splits, const int* accumulate, hipStream_t st) {
+  for (int base = 0; base < n; base += RED_MAXJ) {
+    ReduceBatch rb{};
+    rb.n = std::min(RED_MAXJ, n - base);
+    int blocks = 0;
+    for (int i = 0; i < rb.n; ++i) {
+      const int k = base + i;
+      if (numel[k] % 4 || splits[k] < 1) return 1;
+      rb.j[i] = ReduceJob{slabs[k], outs[k], numel[k] / 4, numel[k], splits[k], accumulate[k]};
+      rb.start[i] = blocks;
+      blocks += (int)std::min<long long>((numel[k] / 4 + 1023) / 1024, 1024);  // ~4 float4 per thread
+    }
+    rb.start[rb.n] = blocks;
+    hipLaunchKernelGGL(splitk_reduce_batched_kernel, dim3(blocks), dim3(256), 0, st, rb);
   }
-  return dw_launch(p, 2, id, splits, K, workspace, workspace_elems, accumulate, tile_cnt, ncnt, adams, st);
+  return 0;
 }
 
 }  // extern "C"

@@ -251,6 +251,8 @@ class DDoSClassifier(nn.Module):
         self.pack_quantum = 128
         # HIP path: finalise all bias / LN-affine column sums of a backward in one launch
         self.defer_colsum = True
+        # HIP path: reduce all split-K weight-gradient slabs of a backward in one launch
+        self.defer_dw_reduce = True
         # HIP path: build the per-step W^T copies on a side stream concurrently with the forward.
         # Measured SLOWER on MI355X (2.48 vs 2.36 ms/step, profiles/r1_ab_transpose_overlap_slower.txt):
         # the memory-bound transposes stretch the concurrent forward GEMMs.  Off by default.
@@ -439,6 +441,8 @@ class DDoSClassifier(nn.Module):
                     wgrad=self._wgrad if grad and self.wgrad_stream else None, group_dw=self.group_dw)
         if grad and self.defer_colsum and self.layer_grads_hook is None:
             rc.colsum_jobs = []  # (a per-block hook needs each block's grads final at once)
+        if grad and self.defer_dw_reduce and self.layer_grads_hook is None:
+            rc.dw_jobs = []
         if (grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None
                 and not self.wgrad_stream and self.transposed_dx):
             rc.fused_adam = self.fused_opt

@@ -54,6 +54,8 @@ class RunCtx:
     # deferred column sums (bias / LN-affine grads): producers leave partials, the end of
     # the backward finalises all of them in one launch (None = finalise immediately)
     colsum_jobs: Optional[list] = None
+    # deferred split-K weight-gradient reduces (ops/kernels.py dw_flush), same life cycle
+    dw_jobs: Optional[list] = None
     # side stream that produced data the backward reads (the W^T copies): joined at the
     # first backward node (the head)
     join_stream: Optional["torch.cuda.Stream"] = None
@@ -121,6 +123,8 @@ class EmbeddingFn(torch.autograd.Function):
             torch.cuda.current_stream().wait_stream(ctx.rc.wgrad)
         if ctx.rc.colsum_jobs:
             K.colsum_flush(ctx.rc.colsum_jobs)
+        if ctx.rc.dw_jobs:
+            K.dw_flush(ctx.rc.dw_jobs)
         return (None,) * 8
 
 
@@ -172,7 +176,7 @@ class LayerFn(torch.autograd.Function):
         with wg.ctx():
             if rc.group_dw:
                 K.linear_dw2(df, g, G["l2_w"].buf, du, h, G["l1_w"].buf, acc,
-                             adam=fa.fused_args([G["l2_w"].buf, G["l1_w"].buf]) if fa else None)
+                             adam=fa.fused_args([G["l2_w"].buf, G["l1_w"].buf]) if fa else None, jobs=rc.dw_jobs)
             else:
                 K.linear_dw(df, g, G["l2_w"].buf, acc)
                 K.linear_dw(du, h, G["l1_w"].buf, acc)
@@ -191,7 +195,7 @@ class LayerFn(torch.autograd.Function):
         with wg.ctx():
             if rc.group_dw:
                 K.linear_dw2(dz1, cx, G["o_w"].buf, dqkv, x, G["qkv_w"].buf, acc,
-                             adam=fa.fused_args([G["o_w"].buf, G["qkv_w"].buf]) if fa else None)
+                             adam=fa.fused_args([G["o_w"].buf, G["qkv_w"].buf]) if fa else None, jobs=rc.dw_jobs)
             else:
                 K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
             K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)

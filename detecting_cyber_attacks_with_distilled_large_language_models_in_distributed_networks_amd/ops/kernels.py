@@ -105,13 +105,33 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: 
 
 
 def linear_dw2(dy0: torch.Tensor, x0: torch.Tensor, out0: torch.Tensor, dy1: torch.Tensor, x1: torch.Tensor,
-               out1: torch.Tensor, accumulate: bool = False, adam=None):
+               out1: torch.Tensor, accumulate: bool = False, adam=None, jobs: Optional[list] = None):
     """Two weight gradients that become ready together, one launch: out_i (+)= dy_i^T x_i
-    (adam: fused optimizer step for both, see ``linear_dw``)."""
+    (adam: fused optimizer step for both, see ``linear_dw``).  jobs: a deferred-reduce list --
+    a split-K launch leaves its fp32 slabs in a buffer of its own and ``dw_flush`` reduces
+    every deferred gradient of the backward in one launch (same z order: bitwise equal)."""
     n = out0.numel() + out1.numel()
-    ws = workspace(dy0.device, "splitk", 8 * n)
+    defer = False
+    if jobs is not None and adam is None:
+        planned = ext().gemm_dw2_splits(dy0.shape[1], x0.shape[1], dy1.shape[1], x1.shape[1], dy0.shape[0])
+        defer = planned > 1
+    # a deferred launch keeps its slabs until the flush: a buffer of its own, sized to the plan
+    ws = workspace(dy0.device, f"splitk_def{len(jobs)}", planned * n) if defer else \
+        workspace(dy0.device, "splitk", 8 * n)
     st, hp = adam if adam is not None else ([], [])
-    ext().gemm_dw2(dy0, x0, out0, dy1, x1, out1, ws, accumulate, tile_counters(dy0.device), st, hp)
+    splits = ext().gemm_dw2(dy0, x0, out0, dy1, x1, out1, ws, accumulate, tile_counters(dy0.device), st, hp, defer)
+    if splits:
+        s0 = splits * out0.numel()
+        jobs.append((ws[:s0], out0, splits, accumulate))
+        jobs.append((ws[s0:s0 + splits * out1.numel()], out1, splits, accumulate))
+
+
+def dw_flush(jobs: list):
+    """Reduce every deferred split-K weight gradient in one launch."""
+    if jobs:
+        ext().splitk_reduce_batched([j[0] for j in jobs], [j[1] for j in jobs], [j[2] for j in jobs],
+                                    [int(j[3]) for j in jobs])
+        jobs.clear()
 
 
 def transpose_many(srcs, dsts):

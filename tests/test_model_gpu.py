@@ -213,3 +213,30 @@ def test_deferred_colsum_matches_immediate():
         torch.cuda.synchronize()
         grads.append(m.arena.grad.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("tokens", [False, True])
+def test_deferred_dw_reduce_matches_immediate(tokens):
+    """Split-K weight-gradient slabs of the whole backward reduced in one batched launch at
+    the end == each reduced right after its GEMM (bitwise; same z order), including an
+    accumulating second backward and the packed-token path (K = packed rows)."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import (
+        kernels as K)
+    cfg = DistilBertConfig(n_layers=2)
+    grads = []
+    for defer in (True, False):
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=12)
+        m.defer_dw_reduce = defer
+        m.train()
+        ids, mask, labels = _batch(16, 128, seed=301)
+        tok = int(mask.sum()) if tokens else None
+        for acc_step in range(2):
+            if acc_step == 0:
+                m.zero_grad()
+            loss, _ = m.forward_loss(ids, mask, labels, tokens=tok)
+            loss.backward()
+        torch.cuda.synchronize()
+        grads.append(m.arena.grad.clone())
+    # the out_lin + qkv pair does split at these shapes, so the deferred path was exercised
+    assert K.ext().gemm_dw2_splits(768, 768, 2304, 768, 16 * 128) > 1
+    assert torch.equal(grads[0], grads[1])
