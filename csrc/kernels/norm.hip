@@ -373,9 +373,21 @@ __global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
 // cu (packed rows): sequence b's position s is row cu[b] + s when s < its length; the
 // padded layout's extra terms are exact zeros, so both layouts give the same sums.
 // grid (S, ceil(D/256)): one thread per (position, column), 16 sequences' loads in flight.
+// Rows s < S: position gradient (sum over sequences).  Rows S <= s < gridDim.x (first write
+// only): zero -- those positions never occur.  Also clears the `now` row flags (V bytes) the
+// word-gradient kernels set next, so neither needs a memset launch of its own.
 __global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* dpos, int B, int S, int D,
-                                                       int accumulate, const int* cu) {
+                                                       int accumulate, const int* cu, unsigned char* now, int V) {
   const int s = blockIdx.x;
+  if (now) {
+    const long long nthr = (long long)gridDim.x * gridDim.y * 256;
+    for (long long i = ((long long)blockIdx.x * gridDim.y + blockIdx.y) * 256 + threadIdx.x; i < V; i += nthr)
+      now[i] = 0;
+  }
+  if (s >= S) {
+    for (int col = blockIdx.y * 256 + threadIdx.x; col < D; col += gridDim.y * 256) dpos[(size_t)s * D + col] = 0.f;
+    return;
+  }
   for (int col = blockIdx.y * 256 + threadIdx.x; col < D; col += gridDim.y * 256) {
     float acc = accumulate ? dpos[(size_t)s * D + col] : 0.f;
     for (int b0 = 0; b0 < B; b0 += 16) {
@@ -710,13 +722,9 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                      st, a);
   hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 2), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, (float*)nullptr, accumulate);
-  if (!accumulate && P > S) hipMemsetAsync(dpos + (size_t)S * D, 0, (size_t)(P - S) * D * sizeof(float), st);
-  hipLaunchKernelGGL(pos_grad_kernel, dim3(S, (D + 255) / 256), dim3(256), 0, st, dz_buf, dpos, B, S, D, accumulate,
-                     cu);
-  if (!accumulate) {
-    if (now) hipMemsetAsync(now, 0, (size_t)V, st);
-    else hipMemsetAsync(dword, 0, (size_t)V * D * sizeof(float), st);
-  }
+  hipLaunchKernelGGL(pos_grad_kernel, dim3(!accumulate && P > S ? P : S, (D + 255) / 256), dim3(256), 0, st, dz_buf,
+                     dpos, B, S, D, accumulate, cu, !accumulate ? now : nullptr, V);
+  if (!accumulate && !now) hipMemsetAsync(dword, 0, (size_t)V * D * sizeof(float), st);
   // piece sums reuse `work` (T*D floats)
   const int chunks = (T + WCH - 1) / WCH;
   const int acc_mode = now ? accumulate : 1;

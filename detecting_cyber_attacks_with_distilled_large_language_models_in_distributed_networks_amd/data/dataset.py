@@ -64,14 +64,40 @@ class DeviceLoader:
             return self.n // self.batch_size
         return (self.n + self.batch_size - 1) // self.batch_size
 
+    def _epoch_blocks(self, perm: Optional[torch.Tensor], nfull: int) -> Optional[torch.Tensor]:
+        """The epoch's full batches gathered once into one buffer, batch i = row i laid out as
+        ids | mask | labels back to back: a step reads three contiguous views of one block
+        (one gather per epoch instead of three per step, and a graph replay refreshes its
+        inputs with one copy).  None when the dtypes differ."""
+        if nfull == 0 or not (self.ids.dtype == self.mask.dtype == self.labels.dtype):
+            return None
+        B, S = self.batch_size, self.ids.shape[1]
+        rows = nfull * B
+        sel = (lambda t: t.index_select(0, perm[:rows])) if perm is not None else (lambda t: t[:rows])
+        blk = torch.empty(nfull, B * (2 * S + 1), dtype=self.ids.dtype, device=self.device)
+        blk[:, :B * S].copy_(sel(self.ids).reshape(nfull, B * S))
+        blk[:, B * S:2 * B * S].copy_(sel(self.mask).reshape(nfull, B * S))
+        blk[:, 2 * B * S:].copy_(sel(self.labels).reshape(nfull, B))
+        return blk
+
     def __iter__(self):
         if self.shuffle:
             perm_cpu = torch.randperm(self.n, generator=self.gen)
             perm = perm_cpu.to(self.device)
         else:
-            perm = None
+            perm_cpu = perm = None
         self.epoch += 1
+        B, S = self.batch_size, self.ids.shape[1]
+        nfull = self.n // B
+        blocks = self._epoch_blocks(perm, nfull) if self.ids.dim() == 2 else None
         for i in range(len(self)):
+            if blocks is not None and i < nfull:
+                row = blocks[i]
+                lo, hi = i * B, (i + 1) * B
+                lens = self.lengths[perm_cpu[lo:hi]] if perm_cpu is not None else self.lengths[lo:hi]
+                yield {"input_ids": row[:B * S].view(B, S), "attention_mask": row[B * S:2 * B * S].view(B, S),
+                       "labels": row[2 * B * S:], "n_tokens": int(lens.sum())}
+                continue
             lo, hi = i * self.batch_size, min(self.n, (i + 1) * self.batch_size)
             if perm is None:
                 yield {"input_ids": self.ids[lo:hi], "attention_mask": self.mask[lo:hi], "labels": self.labels[lo:hi],

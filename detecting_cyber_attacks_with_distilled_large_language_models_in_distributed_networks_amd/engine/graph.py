@@ -26,6 +26,38 @@ from typing import Callable, Dict, Optional
 import torch
 
 
+def contiguous_block(*ts: torch.Tensor) -> Optional[torch.Tensor]:
+    """A flat view over ``ts`` if they lie back to back in one storage with one dtype
+    (DeviceLoader's batch layout: ids | mask | labels), else None -- lets a graph replay
+    refresh its static inputs with ONE copy instead of one per tensor."""
+    t0 = ts[0]
+    es = t0.element_size()
+    ptr = t0.data_ptr()
+    for t in ts:
+        if not t.is_contiguous() or t.dtype != t0.dtype or t.device != t0.device or t.data_ptr() != ptr:
+            return None
+        if t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr():
+            return None
+        ptr += t.numel() * es
+    n = sum(t.numel() for t in ts)
+    return torch.as_strided(t0, (n,), (1,))
+
+
+def static_block(*ts: torch.Tensor):
+    """Clones of ``ts`` laid out back to back in one buffer (+ that buffer), or plain clones
+    (+ None) when the dtypes differ."""
+    if any(t.dtype != ts[0].dtype for t in ts):
+        return [t.clone() for t in ts], None
+    flat = torch.empty(sum(t.numel() for t in ts), dtype=ts[0].dtype, device=ts[0].device)
+    out, off = [], 0
+    for t in ts:
+        v = flat[off:off + t.numel()].view(t.shape)
+        v.copy_(t)
+        out.append(v)
+        off += t.numel()
+    return out, flat
+
+
 class GraphedTrainStep:
     def __init__(self, step_fn: Callable[..., torch.Tensor], warmup: int = 2, enabled: bool = True,
                  bucket: Optional[Callable[[int, int, int], int]] = None, max_graphs: int = 8):
@@ -58,9 +90,13 @@ class GraphedTrainStep:
         hit = self.graphs.get(key)
         if hit is not None:
             g, static, loss = hit
-            static["ids"].copy_(ids)
-            static["mask"].copy_(mask)
-            static["labels"].copy_(labels)
+            blk = contiguous_block(ids, mask, labels) if static["flat"] is not None else None
+            if blk is not None:
+                static["flat"].copy_(blk)
+            else:
+                static["ids"].copy_(ids)
+                static["mask"].copy_(mask)
+                static["labels"].copy_(labels)
             g.replay()
             return loss
         if self.calls <= self.warmup or len(self.graphs) >= self.max_graphs:
@@ -72,7 +108,8 @@ class GraphedTrainStep:
             return loss
         # capture (the bucket's own row count stands in for the batch's token count:
         # every device-side quantity is recomputed from the mask on each replay)
-        static = {"ids": ids.clone(), "mask": mask.clone(), "labels": labels.clone()}
+        (s_ids, s_mask, s_lab), flat = static_block(ids, mask, labels)
+        static = {"ids": s_ids, "mask": s_mask, "labels": s_lab, "flat": flat}
         g = torch.cuda.CUDAGraph()
         try:
             torch.cuda.synchronize()

@@ -15,6 +15,8 @@ from typing import Dict, Optional, Tuple
 import numpy as np
 import torch
 
+from .graph import contiguous_block, static_block
+
 
 class GraphedForward:
     """No-grad logits of ``model`` replayed from HIP graphs (eager on CPU / torch impl)."""
@@ -46,13 +48,18 @@ class GraphedForward:
             if hasattr(m, "sync_shadow"):
                 m.sync_shadow()
             g, static, out = hit
-            static["ids"].copy_(ids)
-            static["mask"].copy_(mask)
+            blk = contiguous_block(ids, mask) if static["flat"] is not None else None
+            if blk is not None:
+                static["flat"].copy_(blk)
+            else:
+                static["ids"].copy_(ids)
+                static["mask"].copy_(mask)
             g.replay()
             return out
         if len(self.graphs) >= self.max_graphs:
             return m(ids, mask, tokens=tokens)
-        static = {"ids": ids.clone(), "mask": mask.clone()}
+        (s_ids, s_mask), flat = static_block(ids, mask)
+        static = {"ids": s_ids, "mask": s_mask, "flat": flat}
         # one eager pass on a side stream warms the allocator / workspaces before capture
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())

@@ -128,3 +128,31 @@ def test_preprocess_reference_csv_parity(seed):
     assert len(texts) == len(ref_texts) == round(0.1 * len(pd.read_csv(REF_CSV)))
     assert texts == ref_texts
     assert labels == ref_labels and set(labels) == {0}  # the committed sample is all BENIGN
+
+
+def test_device_loader_blocked_batches_keep_order_and_layout():
+    """Full batches come from one per-epoch buffer (ids | mask | labels back to back) with the
+    same rows, order and token counts as a per-batch gather; the short tail batch does not."""
+    import torch
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd import data
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.engine.graph import (
+        contiguous_block, static_block)
+    df = data.generate_cicids2017(600, seed=1)
+    ds = data.build_client_data(df, 0, data_fraction=1.0, max_len=64).train
+    for shuffle in (False, True):
+        L = data.DeviceLoader(ds, 32, shuffle=shuffle, seed=3)
+        perm = torch.randperm(L.n, generator=torch.Generator().manual_seed(3)) if shuffle else torch.arange(L.n)
+        for i, b in enumerate(L):
+            idx = perm[i * 32:(i + 1) * 32]
+            assert torch.equal(b["input_ids"], ds.input_ids[idx])
+            assert torch.equal(b["attention_mask"], ds.attention_mask[idx])
+            assert torch.equal(b["labels"], ds.labels[idx])
+            assert b["n_tokens"] == int(ds.attention_mask[idx].sum())
+            blk = contiguous_block(b["input_ids"], b["attention_mask"], b["labels"])
+            assert (blk is not None) == (len(idx) == 32)
+            if blk is not None:
+                (si, sm, sl), flat = static_block(b["input_ids"], b["attention_mask"], b["labels"])
+                flat.zero_()
+                flat.copy_(blk)  # one copy refreshes all three static inputs
+                assert torch.equal(si, b["input_ids"]) and torch.equal(sm, b["attention_mask"])
+                assert torch.equal(sl, b["labels"])
