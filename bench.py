@@ -49,6 +49,8 @@ def main():
                     help="skip the post-timing aggregated-F1 evaluation (kernel profiles of the step alone)")
     ap.add_argument("--no-defer-dw", action="store_true",
                     help="reduce each split-K weight gradient right after its GEMM instead of once per step (A/B)")
+    ap.add_argument("--no-fuse-colsum", action="store_true",
+                    help="separate column-sum pass for FFN lin1's bias gradient (A/B)")
     ap.add_argument("--fused-adam", action="store_true",
                     help="apply Adam inside the weight-gradient GEMM epilogues (A/B; measured no faster)")
     ap.add_argument("--padded", action="store_true",
@@ -95,6 +97,7 @@ def main():
     model.wgrad_stream = args.wgrad_stream
     model.group_dw = not args.no_group_dw
     model.defer_dw_reduce = not args.no_defer_dw
+    model.fuse_colsum = not args.no_fuse_colsum
     ncomm = None
     if args.comm == "rccl" and dev.type == "cuda":
         ncomm = import_module(f"{PKG}.parallel.rccl").NativeComm()

@@ -17,7 +17,7 @@ extern "C" {
 int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
             int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
             long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
-            hipStream_t st);
+            float* colsum, int* colsum_blocks, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
 int fd_gemm_set_fixup(int on);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
@@ -138,8 +138,36 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
   check_rc(fd_gemm((int)kind, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
                    (int)A.size(1), (int)B.size(1), (int)N, ptr<float>(bias), ptr<void>(aux), (int)N,
                    ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, nullptr, 0, nullptr,
-                   stream()),
+                   nullptr, nullptr, stream()),
            "gemm");
+}
+
+// NT dX GEMM (GELU' or residual epilogue) that also leaves per-M-tile column sums of its bf16
+// output in `colsum` ([ceil(M / 128)][N] fp32; returns the tile count) for a deferred
+// producer-bias gradient.
+int64_t gemm_colsum(int64_t epi, const at::Tensor& A, const at::Tensor& B, const at::Tensor& C,
+                    const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& res,
+                    const at::Tensor& colsum) {
+  need(A, at::kBFloat16, "A");
+  need(B, at::kBFloat16, "B");
+  need(C, at::kBFloat16, "C");
+  need(colsum, at::kFloat, "colsum");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm_colsum operands must be 2-D");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_colsum: shape mismatch");
+  TORCH_CHECK(K % 64 == 0 && N % 64 == 0, "gemm_colsum: K % 64 and N % 64 required");
+  TORCH_CHECK(epi == 3 || epi == 4, "gemm_colsum: GELU' (3) or residual (4) epilogue");
+  need_opt(aux, at::kBFloat16, "aux");
+  need_opt(res, at::kBFloat16, "res");
+  if (epi == 3) TORCH_CHECK(aux.has_value() && aux->size(0) == M && aux->size(1) == N, "aux [M,N] required");
+  if (epi == 4) TORCH_CHECK(res.has_value() && res->size(0) == M && res->size(1) == N, "res [M,N] required");
+  TORCH_CHECK(colsum.numel() >= ((M + 127) / 128) * N, "gemm_colsum: colsum needs ceil(M/128) x N floats");
+  int blocks = 0;
+  check_rc(fd_gemm(0, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K, (int)K, (int)K,
+                   (int)N, nullptr, ptr<void>(aux), (int)N, ptr<void>(res), (int)N, nullptr, 0, 0, nullptr, 0,
+                   nullptr, colsum.data_ptr<float>(), &blocks, stream()),
+           "gemm_colsum");
+  return blocks;
 }
 
 // Adam descriptors for fused weight-gradient epilogues.  st = [p, m, v, shadow] per problem
@@ -201,7 +229,7 @@ void gemm_dw(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, cons
   int* cnt = counters_ptr(counters, &ncnt);
   check_rc(fd_gemm(2, 5, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K, (int)M, (int)N, (int)N,
                    nullptr, nullptr, 0, nullptr, 0, workspace.data_ptr<float>(), workspace.numel(),
-                   accumulate ? 1 : 0, cnt, ncnt, adam.empty() ? nullptr : &ad, stream()),
+                   accumulate ? 1 : 0, cnt, ncnt, adam.empty() ? nullptr : &ad, nullptr, nullptr, stream()),
            "gemm_dw");
 }
 
@@ -749,6 +777,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_dw2", &gemm_dw2);
   m.def("gemm_dw", &gemm_dw);
+  m.def("gemm_colsum", &gemm_colsum);
   m.def("splitk_reduce_batched", &splitk_reduce_batched);
   m.def("gemm_dw2_splits", [](int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K) {
     return (int64_t)fd_gemm_dw2_splits((int)M0, (int)N0, (int)M1, (int)N1, (int)K);

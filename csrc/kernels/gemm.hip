@@ -70,6 +70,9 @@ struct GemmParams {
   int* tile_cnt;
   int accumulate;
   FdAdamEpi adam;        // adam.p != nullptr: apply Adam to the finished tile instead of storing it
+  // EPI_GELU_BWD / EPI_ADD with a staged fp32 tile: column sums of the stored output per M
+  // tile, [ceil(M / BM)][N] fp32 (the producer-bias gradient, e.g. FFN lin1's bias)
+  float* colsum;
 };
 
 constexpr int BKT = 64;
@@ -345,6 +348,8 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
     f32_epilogue<BM, BN, NT>(p, smem, LDC, m0, n0, tid, slot);
   } else {
     constexpr int CPR = BN / 4;  // 4 fp32 per chunk
+    constexpr bool CS_OK = NT % CPR == 0;  // a thread keeps one column chunk for the whole tile
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};  // column sums of this thread's rows (p.colsum)
 #pragma unroll 4
     for (int id = tid; id < BM * CPR; id += NT) {
       const int r = id / CPR, cc = id - r * CPR;
@@ -363,7 +368,27 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
           v0 += lo_bf(r2.x); v1 += hi_bf(r2.x); v2 += lo_bf(r2.y); v3 += hi_bf(r2.y);
         }
         bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-        *reinterpret_cast<uint2*>(C + (size_t)m * p.ldc + n) = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+        const uint2 o = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+        *reinterpret_cast<uint2*>(C + (size_t)m * p.ldc + n) = o;
+        // the sums are of the stored (bf16) values: what a separate column sum would read
+        if constexpr (CS_OK) { cs[0] += lo_bf(o.x); cs[1] += hi_bf(o.x); cs[2] += lo_bf(o.y); cs[3] += hi_bf(o.y); }
+      }
+    }
+    if (CS_OK && p.colsum) {
+      // per-tile column partials [tiles_m][N] (fixed order: deterministic), finalised by the
+      // batched column-sum launch at the end of the backward (norm.hip fd_colsum_batched)
+      constexpr int G = CS_OK ? NT / CPR : 1;  // threads sharing a column chunk
+      float* red = reinterpret_cast<float*>(smem);
+      __syncthreads();  // every thread is done reading the staged tile
+      const int cc = tid % CPR, g = tid / CPR;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[g * BN + cc * 4 + e] = cs[e];
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < G; ++i) s += red[i * BN + c];
+        p.colsum[(size_t)(m0 / BM) * p.N + n0 + c] = s;
       }
     }
   }
@@ -774,7 +799,7 @@ int fd_gemm_set_cfg(int kind, int cfg, int splits) {
 int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
             const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
             long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
-            hipStream_t st) {
+            float* colsum, int* colsum_blocks, hipStream_t st) {
   if (K % BKT != 0 || N % 64 != 0 || M <= 0 || kind < 0 || kind > 2) return 1;
   GemmParams p{};
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.C = C;
@@ -794,6 +819,13 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
     const char* e = getenv("FD_GEMM_GROUP_M");
     if (e) gm = atoi(e);
     p.group_m = std::max(1, gm);
+  }
+  if (colsum) {
+    // only the staged-fp32 epilogues sum columns: 128 x {128, 64} tiles (never 256-row ones)
+    if (kind != 0 || (epi != EPI_GELU_BWD && epi != EPI_ADD)) return 2;
+    if (CFGS[id].bm != 128 || (CFGS[id].bn != 128 && CFGS[id].bn != 64) || N % CFGS[id].bn) id = 0;
+    p.colsum = colsum;
+    if (colsum_blocks) *colsum_blocks = (M + CFGS[id].bm - 1) / CFGS[id].bm;
   }
   if (kind == 0) {  // also dX = dy (W^T)^T with a transposed weight copy: GELU' / residual epilogues
     if (epi == EPI_F32) return 2;

@@ -56,6 +56,8 @@ class RunCtx:
     colsum_jobs: Optional[list] = None
     # deferred split-K weight-gradient reduces (ops/kernels.py dw_flush), same life cycle
     dw_jobs: Optional[list] = None
+    # lin1's bias gradient from the GELU' dX GEMM's epilogue (needs colsum_jobs)
+    fuse_colsum: bool = True
     # side stream that produced data the backward reads (the W^T copies): joined at the
     # first backward node (the head)
     join_stream: Optional["torch.cuda.Stream"] = None
@@ -171,7 +173,11 @@ class LayerFn(torch.autograd.Function):
         if fa is not None and (acc or not rc.group_dw or rc.wgrad is not None or wt.get("l1_w") is None
                                or wt.get("qkv_w") is None):
             fa = None
-        du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"))  # dg W2 * gelu'(u)
+        # dg W2 * gelu'(u); with deferred column sums and no weight-gradient side stream the
+        # epilogue also leaves lin1's bias-gradient partials (no separate pass over du)
+        fuse_cs = jobs is not None and rc.wgrad is None and rc.fuse_colsum and wt.get("l2_w") is not None
+        du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"),
+                         colsum=(jobs, G["l1_b"].buf, acc) if fuse_cs else None)
         wg.fork(df, g, du, h)
         with wg.ctx():
             if rc.group_dw:
@@ -180,7 +186,8 @@ class LayerFn(torch.autograd.Function):
             else:
                 K.linear_dw(df, g, G["l2_w"].buf, acc)
                 K.linear_dw(du, h, G["l1_w"].buf, acc)
-            K.colsum(du, G["l1_b"].buf, acc, jobs)
+            if not fuse_cs:
+                K.colsum(du, G["l1_b"].buf, acc, jobs)
         dh = K.linear_dx(du, L["l1_w"], res=dz2, wt=wt.get("l1_w"))    # du W1 + dz2
         # sa_layer_norm(out_lin + x)
         dz1, _ = K.ln_bwd(dh, ao, x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf, G["o_b"].buf, rc.seed, 0,

@@ -19,13 +19,22 @@ LN_GRID = 256  # must match csrc/kernels/norm.hip (partial-sum blocks of the emb
 LN_BWD_PARTS = 512  # upper bound on the LN backward's partial-sum blocks (csrc/kernels/norm.hip)
 
 _WS = {}
+# Outgrown workspaces are kept alive, never freed: a HIP graph captured earlier (another
+# packed-row bucket, another batch shape) still holds their addresses, and returning them to
+# the caching allocator would let a later allocation alias memory that graph writes on replay.
+_WS_RETIRED = []
 
 
 def workspace(device, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
     key = (str(device), name, dtype)
     t = _WS.get(key)
     if t is None or t.numel() < numel:
-        t = torch.empty(max(numel, 1), dtype=dtype, device=device)
+        if t is not None:
+            _WS_RETIRED.append(t)
+            numel_alloc = max(numel, t.numel() + t.numel() // 2)  # grow geometrically: few retirements
+        else:
+            numel_alloc = numel
+        t = torch.empty(max(numel_alloc, 1), dtype=dtype, device=device)
         _WS[key] = t
     return t[:numel]
 
@@ -52,13 +61,26 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu
 
 
 def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] = None,
-              res: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
+              res: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None,
+              colsum: Optional[tuple] = None) -> torch.Tensor:
     """dx = dy w  [* gelu'(u)]  [+ res]  (bf16).
 
     With ``wt`` (= w^T, contiguous) the product runs as the K-major "NT" kernel
-    dx = dy (w^T)^T, whose operand staging is faster than the MN-major read of w."""
+    dx = dy (w^T)^T, whose operand staging is faster than the MN-major read of w.
+    colsum = (deferred colsum jobs, out, accumulate): the GEMM epilogue also leaves the
+    column sums of dx per M tile (the producer-bias gradient) as a deferred job, instead
+    of a separate column-sum pass over dx.  Returns dx."""
     M, N = dy.shape[0], w.shape[1]
     dx = torch.empty(M, N, dtype=torch.bfloat16, device=dy.device)
+    if colsum is not None and wt is not None and (gelu_u is not None or res is not None):
+        jobs, out, acc = colsum
+        ws = workspace(dy.device, f"colsum_job{len(jobs)}", ((M + 127) // 128) * N)
+        epi = EPI_GELU_BWD if gelu_u is not None else EPI_ADD
+        nblk = ext().gemm_colsum(epi, dy, wt, dx, gelu_u, res, ws)
+        jobs.append((ws, [out], nblk, N, N, acc))
+        return dx
+    if colsum is not None:
+        raise ValueError("fused column sums need the transposed weight and a GELU' / residual epilogue")
     if wt is not None:
         epi = EPI_GELU_BWD if gelu_u is not None else (EPI_ADD if res is not None else EPI_BF16)
         ext().gemm(0, epi, dy, wt, dx, None, gelu_u, res, None, False)

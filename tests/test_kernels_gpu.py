@@ -370,3 +370,22 @@ def test_rank_sort_matches_stable_sort(T):
     srt, perm = kn.group_ids(ids)
     ref_s, ref_p = torch.sort(ids, stable=True)
     assert torch.equal(srt, ref_s) and torch.equal(perm, ref_p)
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(2688, 3072, 768, 3), (2700, 768, 3072, 4), (300, 3072, 768, 3)])
+def test_gemm_epilogue_column_sums(M, N, K, epi):
+    """NT dX GEMM with GELU' / residual epilogue + per-tile column sums of its bf16 output."""
+    dy, wt = bf(M, K, seed=31), bf(N, K, seed=32)
+    aux = bf(M, N, seed=33)
+    ref_dx = kn.linear_dx(dy, wt.t().contiguous(), gelu_u=aux if epi == 3 else None,
+                          res=aux if epi == 4 else None, wt=wt)
+    dx = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    tiles = (M + 127) // 128
+    part = torch.full((tiles * N,), float("nan"), device=DEV)
+    nblk = kn.ext().gemm_colsum(epi, dy, wt, dx, aux if epi == 3 else None, aux if epi == 4 else None, part)
+    torch.cuda.synchronize()
+    assert nblk == tiles
+    assert torch.equal(dx, ref_dx)
+    col = part.view(tiles, N).sum(0)
+    ref = dx.float().sum(0)
+    assert rel_err(col, ref) < 1e-5

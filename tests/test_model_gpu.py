@@ -130,6 +130,7 @@ def test_overlapped_adam_matches_single_pass(graph):
     models, steps = [], []
     for overlap in (True, False):
         m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=5)
+        m.fuse_colsum = False  # (a per-block hook disables the deferred sums it needs)
         m.train()
         opt = ArenaAdam(m, lr=1e-3, overlap=overlap, fuse_dw=False)
         assert (m.layer_grads_hook is not None) == overlap
@@ -179,6 +180,7 @@ def test_wgrad_side_stream_matches_serial(graph):
     for side in (True, False):
         m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=11)
         m.wgrad_stream = side
+        m.fuse_colsum = False  # (not combined with the side stream)
         m.train()
         models.append(m)
         steps.append(GraphedTrainStep(make_step_fn(m, ArenaAdam(m, lr=1e-3, fuse_dw=False)), warmup=1,
@@ -203,6 +205,7 @@ def test_deferred_colsum_matches_immediate():
     for defer in (True, False):
         m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=12)
         m.defer_colsum = defer
+        m.fuse_colsum = False  # (the fused lin1-bias sum has its own order: test below)
         m.train()
         ids, mask, labels = _batch(16, 128, seed=300)
         for acc_step in range(2):  # second backward accumulates (deferred jobs carry the flag)
@@ -240,3 +243,27 @@ def test_deferred_dw_reduce_matches_immediate(tokens):
     # the out_lin + qkv pair does split at these shapes, so the deferred path was exercised
     assert K.ext().gemm_dw2_splits(768, 768, 2304, 768, 16 * 128) > 1
     assert torch.equal(grads[0], grads[1])
+
+
+def test_fused_lin1_bias_colsum_matches_separate_pass():
+    """lin1's bias gradient summed in the GELU' dX GEMM epilogue == the separate column-sum
+    pass (same bf16 values, different fp32 summation order); every other gradient bitwise."""
+    cfg = DistilBertConfig(n_layers=2)
+    grads = []
+    for fuse in (True, False):
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=14)
+        m.fuse_colsum = fuse
+        m.train()
+        ids, mask, labels = _batch(16, 128, seed=302)
+        m.zero_grad()
+        loss, _ = m.forward_loss(ids, mask, labels, tokens=int(mask.sum()))
+        loss.backward()
+        torch.cuda.synchronize()
+        grads.append(m.arena.grad.clone())
+    sel = torch.zeros_like(grads[0], dtype=torch.bool)
+    for i in range(cfg.n_layers):
+        off, shape = m.arena.offsets[f"distilbert.transformer.layer.{i}.ffn.lin1.bias"]
+        sel[off:off + shape[0]] = True
+        a, b = grads[0][off:off + shape[0]], grads[1][off:off + shape[0]]
+        assert rel(a, b) < 1e-5, rel(a, b)
+    assert torch.equal(grads[0][~sel], grads[1][~sel])
