@@ -823,7 +823,12 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
   if (colsum) {
     // only the staged-fp32 epilogues sum columns: 128 x {128, 64} tiles (never 256-row ones)
     if (kind != 0 || (epi != EPI_GELU_BWD && epi != EPI_ADD)) return 2;
-    if (CFGS[id].bm != 128 || (CFGS[id].bn != 128 && CFGS[id].bn != 64) || N % CFGS[id].bn) id = 0;
+    if (CFGS[id].bm != 128 || (CFGS[id].bn != 128 && CFGS[id].bn != 64) || N % CFGS[id].bn) {
+      // the shape's tile has no staged-fp32 epilogue (e.g. 256 x 192 at M >= 3.5 k): launch
+      // nothing, report 0 blocks -- the caller runs the plain GEMM + a column-sum pass
+      if (colsum_blocks) *colsum_blocks = 0;
+      return 0;
+    }
     p.colsum = colsum;
     if (colsum_blocks) *colsum_blocks = (M + CFGS[id].bm - 1) / CFGS[id].bm;
   }

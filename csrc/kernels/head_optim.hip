@@ -94,20 +94,60 @@ __global__ __launch_bounds__(64) void head_loss_mean_kernel(const float* row_los
   if (threadIdx.x == 0) loss[0] = s / B;
 }
 
+// Is `row` some sequence's [CLS] row (the rows the compute blocks write)?
+DEV bool is_cls_row(const HeadArgs& a, int row) {
+  if (!a.cls) return row % a.S == 0 && row / a.S < a.B;
+  int lo = 0, hi = a.B - 1;  // cls = sequence starts: ascending
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int)cls_row(a, mid) < row) lo = mid + 1;
+    else hi = mid;
+  }
+  return (int)cls_row(a, lo) == row;
+}
+
+// Blocks [0, ceil(D/256)): dW / db and the [CLS] rows of dhidden.  Blocks beyond: zero every
+// other row of dhidden (so the caller needs no separate fill launch).
 __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
+  const int nc = (a.D + 255) / 256;
+  if ((int)blockIdx.x >= nc) {
+    const int per_row = a.D / 8;  // uint4 chunks
+    const long long total = (long long)a.T * per_row;
+    for (long long i = (long long)(blockIdx.x - nc) * 256 + threadIdx.x; i < total;
+         i += (long long)(gridDim.x - nc) * 256) {
+      const int row = (int)(i / per_row);
+      if (!is_cls_row(a, row)) reinterpret_cast<uint4*>(a.dhidden)[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    return;
+  }
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
-  for (int col = blockIdx.x * 256 + threadIdx.x; col < a.D; col += gridDim.x * 256) {
+  for (int col = blockIdx.x * 256 + threadIdx.x; col < a.D; col += nc * 256) {
     float g0 = 0.f, g1 = 0.f;
     const float w0 = a.W[col], w1 = a.W[a.D + col];
-    for (int b = 0; b < a.B; ++b) {
-      const float d0 = a.dlog_in[2 * b], d1 = a.dlog_in[2 * b + 1];
-      const bool keep = !drop || drop_keep(seed, (uint32_t)(b * a.D + col), a.thr);
-      const float sc = drop ? (keep ? a.dscale : 0.f) : 1.f;
-      const float x = bf2f(a.hidden[cls_row(a, b) * a.D + col]) * sc;
-      g0 += d0 * x;
-      g1 += d1 * x;
-      a.dhidden[cls_row(a, b) * a.D + col] = (bf16_t)f2bf((d0 * w0 + d1 * w1) * sc);
+    for (int b0 = 0; b0 < a.B; b0 += 8) {
+      // 8 rows' loads in flight before any store (dhidden may alias nothing here, but the
+      // compiler cannot know: hoisting by hand)
+      float x[8];
+      size_t row[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = min(b0 + u, a.B - 1);
+        row[u] = cls_row(a, b);
+        x[u] = bf2f(a.hidden[row[u] * a.D + col]);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + u;
+        if (b >= a.B) break;
+        const float d0 = a.dlog_in[2 * b], d1 = a.dlog_in[2 * b + 1];
+        const bool keep = !drop || drop_keep(seed, (uint32_t)(b * a.D + col), a.thr);
+        const float sc = drop ? (keep ? a.dscale : 0.f) : 1.f;
+        const float xv = x[u] * sc;
+        g0 += d0 * xv;
+        g1 += d1 * xv;
+        a.dhidden[row[u] * a.D + col] = (bf16_t)f2bf((d0 * w0 + d1 * w1) * sc);
+      }
     }
     a.dW[col] = a.accumulate ? a.dW[col] + g0 : g0;
     a.dW[a.D + col] = a.accumulate ? a.dW[a.D + col] + g1 : g1;
@@ -319,7 +359,11 @@ int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const u
   a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.dlog_in = dlogits;
   a.dW = dW; a.db = db; a.dhidden = (bf16_t*)dhidden; a.accumulate = accumulate;
-  hipLaunchKernelGGL(head_bwd_kernel, dim3((D + 255) / 256), dim3(256), 0, st, a);
+  if (D % 8) return 1;
+  // compute blocks + zeroing blocks (~4 uint4 stores per thread over the non-[CLS] rows)
+  const long long chunks = (long long)T * (D / 8);
+  const int zb = (int)std::min<long long>((chunks + 1023) / 1024, 1024);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((D + 255) / 256 + zb), dim3(256), 0, st, a);
   return 0;
 }
 

@@ -78,13 +78,17 @@ class ArenaAdam:
                 raise RuntimeError("ArenaAdam(overlap=True) cannot share the backward hook (data-parallel GradSync?)")
             self.model.layer_grads_hook = self._on_layer_grads
 
-    def _begin(self):
-        """Advance the device step counter once per step, before the first update launch."""
+    def _begin(self, seed: Optional[torch.Tensor] = None):
+        """Advance the device step counter once per step, before the first update launch.
+        ``seed``: the model's dropout counter, advanced by the same launch (the model's training
+        forward calls this inside a step scope: one tiny kernel instead of two)."""
+        from ..ops import kernels as K
         if not self._begun:
-            from ..ops import kernels as K
-            K.step_inc(self.step_t, None)
+            K.step_inc(self.step_t, seed)
             self.host_step += 1
             self._begun = True
+        elif seed is not None:
+            K.step_inc(None, seed)
 
     def _update(self, off: int, n: int, sparse: bool):
         from ..ops import kernels as K

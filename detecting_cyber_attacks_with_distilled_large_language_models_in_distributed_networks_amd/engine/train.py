@@ -27,15 +27,24 @@ class fused_adam_scope:
     def __init__(self, model, optimizer):
         self.model = model
         self.opt = optimizer if getattr(optimizer, "can_fuse", lambda: False)() else None
+        # the optimizer whose device step counter the model's training forward may advance
+        # together with its dropout seed (ArenaAdam._begin(seed)); GPU arenas only
+        self.step_opt = optimizer if (hasattr(optimizer, "_begin") and hasattr(model, "step_opt")
+                                      and getattr(getattr(optimizer, "arena", None), "device",
+                                                  torch.device("cpu")).type == "cuda") else None
 
     def __enter__(self):
         if self.opt is not None:
             self.model.fused_opt = self.opt
+        if self.step_opt is not None:
+            self.model.step_opt = self.step_opt
         return self
 
     def __exit__(self, *exc):
         if self.opt is not None:
             self.model.fused_opt = None
+        if self.step_opt is not None:
+            self.model.step_opt = None
         return False
 
 

@@ -263,6 +263,9 @@ class DDoSClassifier(nn.Module):
         # optimizer that applies Adam inside the weight-gradient GEMM epilogues; set only for
         # the duration of a training step (engine/train.py fused_adam_scope)
         self.fused_opt = None
+        # optimizer of the running training step (same scope): its step counter is advanced
+        # by the forward's dropout-seed launch
+        self.step_opt = None
         self.torch_counter = 0
         self._grad_token = None
         self._synced_version = -1
@@ -450,7 +453,10 @@ class DDoSClassifier(nn.Module):
                 and not self.wgrad_stream and self.transposed_dx):
             rc.fused_adam = self.fused_opt
         if self.training:
-            K.step_inc(None, self.rng)
+            if grad and self.step_opt is not None:
+                self.step_opt._begin(seed=self.rng)  # Adam step + dropout seed: one launch
+            else:
+                K.step_inc(None, self.rng)
         token = self._grad_token if torch.is_grad_enabled() else None
         if token is not None and self.transposed_dx:
             srcs = [L[k] for L in layers for k in L["wT"]]

@@ -77,7 +77,12 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] 
         ws = workspace(dy.device, f"colsum_job{len(jobs)}", ((M + 127) // 128) * N)
         epi = EPI_GELU_BWD if gelu_u is not None else EPI_ADD
         nblk = ext().gemm_colsum(epi, dy, wt, dx, gelu_u, res, ws)
-        jobs.append((ws, [out], nblk, N, N, acc))
+        if nblk:
+            jobs.append((ws, [out], nblk, N, N, acc))
+            return dx
+        # this shape's tile has no fused column sums: plain GEMM, then the separate pass
+        ext().gemm(0, epi, dy, wt, dx, None, gelu_u, res, None, False)
+        _colsum_pass(dx, out, acc, jobs)
         return dx
     if colsum is not None:
         raise ValueError("fused column sums need the transposed weight and a GELU' / residual epilogue")
@@ -160,6 +165,10 @@ def transpose_many(srcs, dsts):
     """dsts[i] = srcs[i]^T (bf16, one launch for up to 32 matrices)."""
     for i in range(0, len(srcs), 32):
         ext().transpose_batched(list(srcs[i:i + 32]), list(dsts[i:i + 32]))
+
+
+def _colsum_pass(x, out, accumulate, jobs):  # (linear_dx's `colsum` argument shadows colsum())
+    return colsum(x, out, accumulate, jobs)
 
 
 def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = False, jobs: Optional[list] = None) -> torch.Tensor:
@@ -307,7 +316,7 @@ def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None, cls=None):
 
 
 def head_bwd(hidden, B, S, W, seed, site, p, dlogits, dW, db, accumulate=False, cls=None):
-    dhidden = torch.zeros_like(hidden)
+    dhidden = torch.empty_like(hidden)  # the kernel writes every row ([CLS] rows: gradient, others: 0)
     thr, sc = _drop(p)
     ext().head_bwd(hidden, B, S, W, seed, site, thr, sc, dlogits.contiguous(), dW, db, dhidden, accumulate, cls)
     return dhidden

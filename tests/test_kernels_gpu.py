@@ -389,3 +389,34 @@ def test_gemm_epilogue_column_sums(M, N, K, epi):
     col = part.view(tiles, N).sum(0)
     ref = dx.float().sum(0)
     assert rel_err(col, ref) < 1e-5
+
+
+def test_head_bwd_packed_rows_and_zeroing():
+    """Packed layout ([CLS] = first row of each sequence, one empty sequence): the [CLS] rows
+    carry the gradient, every other row of dhidden is exactly 0 (written by the kernel)."""
+    lens = torch.tensor([5, 0, 7, 1, 3] + [4] * 27)
+    B, D = len(lens), 768
+    cu = torch.zeros(B + 1, dtype=torch.int32)
+    cu[1:] = torch.cumsum(lens, 0)
+    T = int(cu[-1]) + 11  # + filler rows
+    hidden = bf(T, D, seed=24)
+    W = torch.randn(2, D, device=DEV) * 0.05
+    b = torch.randn(2, device=DEV)
+    labels = torch.randint(0, 2, (B,), device=DEV)
+    cls = cu[:-1].to(DEV)
+    logits, loss, dlog = kn.head_fwd(hidden, B, 1, W, b, seed_t(2), 2, 0.0, labels, cls)
+    junk = torch.full((T, D), float("nan"), dtype=torch.bfloat16, device=DEV)
+    del junk  # the caching allocator hands this block to dhidden: stale NaNs unless zeroed
+    dW, db = torch.empty(2, D, device=DEV), torch.empty(2, device=DEV)
+    dh = kn.head_bwd(hidden, B, 1, W, seed_t(2), 2, 0.0, dlog, dW, db, cls=cls)
+    torch.cuda.synchronize()
+    rows = torch.clamp(cls.long(), max=T - 1)
+    want = torch.zeros(T, D, device=DEV)
+    for i in range(B):  # a repeated row (empty sequence) takes the later sequence's value
+        want[rows[i]] = dlog[i, 0] * W[0] + dlog[i, 1] * W[1]
+    assert rel_err(dh, want) < 1e-2
+    other = torch.ones(T, dtype=torch.bool, device=DEV)
+    other[rows] = False
+    assert (dh[other] == 0).all()
+    x = hidden.float()[rows]
+    assert rel_err(dW, dlog.t() @ x) < 1e-4
