@@ -71,7 +71,7 @@ int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const f
                 float* logits, float* loss, float* dlogits, float* row_loss, const int* cls, int T, hipStream_t st);
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
-                int accumulate, const int* cls, int T, hipStream_t st);
+                int accumulate, const int* cls, int T, const float* gscale, hipStream_t st);
 int fd_eval_metrics(const float* logits, const long long* labels, int B, double* acc, long long* counts,
                     float* prob1, long long* preds, hipStream_t st);
 int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float lr,
@@ -665,8 +665,11 @@ void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
 
 void head_bwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& W, const at::Tensor& seed, int64_t site,
               int64_t thr, double dscale, const at::Tensor& dlogits, const at::Tensor& dW, const at::Tensor& db,
-              const at::Tensor& dhidden, bool accumulate, const c10::optional<at::Tensor>& cls) {
+              const at::Tensor& dhidden, bool accumulate, const c10::optional<at::Tensor>& cls,
+              const c10::optional<at::Tensor>& gscale) {
   need_opt(cls, at::kInt, "cls");
+  need_opt(gscale, at::kFloat, "gscale");
+  if (gscale.has_value() && gscale->defined()) TORCH_CHECK(gscale->numel() == 1, "head_bwd: gscale is a scalar");
   need(hidden, at::kBFloat16, "hidden");
   need(W, at::kFloat, "W");
   need(dlogits, at::kFloat, "dlogits");
@@ -682,7 +685,7 @@ void head_bwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
   check_rc(fd_head_bwd(hidden.data_ptr(), (int)B, (int)S, (int)D, W.data_ptr<float>(), seedp(seed), (uint32_t)site,
                        (uint32_t)thr, (float)dscale, dlogits.data_ptr<float>(), dW.data_ptr<float>(),
                        db.data_ptr<float>(), dhidden.data_ptr(), accumulate ? 1 : 0, ptr<int>(cls),
-                       (int)(hidden.numel() / D), stream()),
+                       (int)(hidden.numel() / D), ptr<float>(gscale), stream()),
            "head_bwd");
 }
 

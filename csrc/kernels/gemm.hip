@@ -420,6 +420,8 @@ DEV void wait_vm() {
 // Counted wait for "all but the youngest n*L LDS-DMA ops" (n = tiles still allowed in flight).
 template <int L, int MAXN>
 DEV void wait_tiles(int n) {
+  if constexpr (MAXN >= 4) { if (n >= 4) { wait_vm<4 * L>(); return; } }
+  if constexpr (MAXN >= 3) { if (n >= 3) { wait_vm<3 * L>(); return; } }
   if constexpr (MAXN >= 2) { if (n >= 2) { wait_vm<2 * L>(); return; } }
   if constexpr (MAXN >= 1) { if (n >= 1) { wait_vm<L>(); return; } }
   wait_vm<0>();
@@ -458,7 +460,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
   constexpr int MI = TM / 16, NI = TN / 16;  // 16x16 sub-tiles per wave
   constexpr int BUF = G::BUF;
   constexpr int L = OA::PER_WAVE + OB::PER_WAVE;  // DMA ops per wave per K tile
-  static_assert(S >= 2 && S <= 4, "ring depth");
+  static_assert(S >= 2 && S <= 6, "ring depth");
+  static_assert((S - 2) * L <= 63, "vmcnt is 6 bits");
 #ifndef FD_GEMM_SCHED
 #define FD_GEMM_SCHED 1
 #endif
@@ -591,15 +594,18 @@ __global__ __launch_bounds__(256) void splitk_reduce_batched_kernel(ReduceBatch 
 //  8: 128 x  64, 2x2, S2      9: 128 x  96, 2x2, S3 (K-major B)
 // 10: 128 x 128, 2x2, S3     11: 256 x 256, 2x4, S2     12: 256 x 128, 4x2, S2
 // 13:  64 x  64, 2x2, S3     14:  64 x 128, 2x2, S3  (small tiles: 2-4 blocks/CU at N = 768)
+// 15: 128 x  64, 2x2, S4     16: 128 x  64, 2x2, S5     17: 128 x 128, 2x2, S4  (deep rings:
+//     more LDS-DMA bytes in flight per CU where the grid is one block per CU)
 // (A ping-pong variant -- the two 4-wave halves of an 8-wave block staggered by
 // one barrier phase so one half's LDS reads overlap the other's MFMAs -- was
 // correct but measured 1.5-3x slower on these shapes; not kept.)
-constexpr int NCFG = 15;
+constexpr int NCFG = 18;
 struct CfgDesc { int bm, bn, wm, wn, s; };
 constexpr CfgDesc CFGS[NCFG] = {{128, 64, 2, 2, 3}, {128, 128, 2, 2, 2}, {128, 96, 2, 2, 2}, {256, 192, 4, 2, 2},
                                 {256, 128, 4, 2, 3}, {64, 192, 1, 4, 3}, {128, 192, 2, 4, 2}, {256, 96, 4, 1, 3},
                                 {128, 64, 2, 2, 2},  {128, 96, 2, 2, 3}, {128, 128, 2, 2, 3}, {256, 256, 2, 4, 2},
-                                {256, 128, 4, 2, 2}, {64, 64, 2, 2, 3},    {64, 128, 2, 2, 3}};
+                                {256, 128, 4, 2, 2}, {64, 64, 2, 2, 3},    {64, 128, 2, 2, 3},  {128, 64, 2, 2, 4},
+                                {128, 64, 2, 2, 5},  {128, 128, 2, 2, 4}};
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
 bool launch_cfg(const GemmParams& p, int splits, hipStream_t st, const GemmParams* q) {
@@ -640,6 +646,9 @@ bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st, const Ge
     case 12: return launch_cfg<256, 128, AK, BKM, EPI, 4, 2, 2>(p, splits, st, q);
     case 13: return launch_cfg<64, 64, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
     case 14: return launch_cfg<64, 128, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
+    case 15: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 4>(p, splits, st, q);
+    case 16: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 5>(p, splits, st, q);
+    case 17: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 4>(p, splits, st, q);
   }
   return false;
 }

@@ -34,6 +34,7 @@ struct HeadArgs {
   float* row_loss;       // [B] scratch
   // backward
   const float* dlog_in;  // [B, 2]
+  const float* gscale;   // nullable: dlog_in is scaled by gscale[0] (upstream grad of a fused loss)
   float* dW;             // [2, D]
   float* db;             // [2]
   bf16_t* dhidden;       // [B*S, D]; only CLS rows written
@@ -140,7 +141,9 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
       for (int u = 0; u < 8; ++u) {
         const int b = b0 + u;
         if (b >= a.B) break;
-        const float d0 = a.dlog_in[2 * b], d1 = a.dlog_in[2 * b + 1];
+        const float gs = a.gscale ? a.gscale[0] : 1.f;
+        const float d0 = a.gscale ? a.dlog_in[2 * b] * gs : a.dlog_in[2 * b];
+        const float d1 = a.gscale ? a.dlog_in[2 * b + 1] * gs : a.dlog_in[2 * b + 1];
         const bool keep = !drop || drop_keep(seed, (uint32_t)(b * a.D + col), a.thr);
         const float sc = drop ? (keep ? a.dscale : 0.f) : 1.f;
         const float xv = x[u] * sc;
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
   }
   if (blockIdx.x == 0 && threadIdx.x < 2) {
     float s = 0.f;
-    for (int b = 0; b < a.B; ++b) s += a.dlog_in[2 * b + threadIdx.x];
+    for (int b = 0; b < a.B; ++b) s += a.gscale ? a.dlog_in[2 * b + threadIdx.x] * a.gscale[0] : a.dlog_in[2 * b + threadIdx.x];
     a.db[threadIdx.x] = a.accumulate ? a.db[threadIdx.x] + s : s;
   }
 }
@@ -353,8 +356,9 @@ int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const f
 
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
-                int accumulate, const int* cls, int T, hipStream_t st) {
+                int accumulate, const int* cls, int T, const float* gscale, hipStream_t st) {
   HeadArgs a{};
+  a.gscale = gscale;
   a.cls = cls; a.T = T;
   a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.dlog_in = dlogits;

@@ -48,6 +48,18 @@ class fused_adam_scope:
         return False
 
 
+_ONES = {}
+
+
+def _one(device) -> torch.Tensor:
+    """Persistent scalar 1.0 seeding ``backward`` (autograd would launch a fill per step)."""
+    t = _ONES.get(str(device))
+    if t is None:
+        t = torch.ones((), dtype=torch.float32, device=device)
+        _ONES[str(device)] = t
+    return t
+
+
 def make_step_fn(model, optimizer, criterion=None):
     fused = criterion is None or isinstance(criterion, torch.nn.CrossEntropyLoss)
 
@@ -58,7 +70,7 @@ def make_step_fn(model, optimizer, criterion=None):
                 loss, _ = model.forward_loss(ids, mask, labels, tokens=tokens)
             else:
                 loss = criterion(model(ids, mask, tokens=tokens), labels)
-            loss.backward()
+            loss.backward(_one(loss.device) if loss.dtype == torch.float32 and loss.dim() == 0 else None)
         optimizer.step()
         return loss.detach()
 

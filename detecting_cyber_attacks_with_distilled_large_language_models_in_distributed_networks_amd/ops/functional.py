@@ -228,6 +228,7 @@ class HeadFn(torch.autograd.Function):
         ctx.save_for_backward(hidden)
         ctx.dlog = dlog
         ctx.fused_loss = labels is not None
+        ctx.set_materialize_grads(False)  # the unused output's grad stays None (no fill launch)
         if labels is not None:
             ctx.mark_non_differentiable(logits)  # the gradient flows through the fused loss
             return loss, logits
@@ -240,14 +241,20 @@ class HeadFn(torch.autograd.Function):
         if ctx.rc.join_stream is not None:
             torch.cuda.current_stream().wait_stream(ctx.rc.join_stream)
         (hidden,) = ctx.saved_tensors
+        gscale = None
         if ctx.fused_loss:
-            dlog = ctx.dlog * g0
+            if g0 is None:
+                return (None,) * 6
+            dlog = ctx.dlog
+            gscale = g0.float().reshape(1)  # scaled inside the kernel (no elementwise launch)
         else:
+            if g0 is None:
+                return (None,) * 6
             dlog = g0.float().contiguous()
         s = ctx.sinks
         acc = s["w"].accumulate()
         s["b"].accumulate()
         cls = ctx.rc.cu[:-1] if ctx.rc.cu is not None else None
         dh = K.head_bwd(hidden, ctx.rc.B, ctx.rc.S, ctx.W, ctx.rc.seed, 2, ctx.p, dlog, s["w"].buf, s["b"].buf, acc,
-                        cls)
+                        cls, gscale)
         return dh, None, None, None, None, None

@@ -315,10 +315,12 @@ def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None, cls=None):
     return logits, loss, dlogits
 
 
-def head_bwd(hidden, B, S, W, seed, site, p, dlogits, dW, db, accumulate=False, cls=None):
+def head_bwd(hidden, B, S, W, seed, site, p, dlogits, dW, db, accumulate=False, cls=None, gscale=None):
+    """gscale: optional fp32 scalar tensor multiplying dlogits (a fused loss's upstream grad)."""
     dhidden = torch.empty_like(hidden)  # the kernel writes every row ([CLS] rows: gradient, others: 0)
     thr, sc = _drop(p)
-    ext().head_bwd(hidden, B, S, W, seed, site, thr, sc, dlogits.contiguous(), dW, db, dhidden, accumulate, cls)
+    ext().head_bwd(hidden, B, S, W, seed, site, thr, sc, dlogits.contiguous(), dW, db, dhidden, accumulate, cls,
+                   gscale)
     return dhidden
 
 
