@@ -596,16 +596,19 @@ __global__ __launch_bounds__(256) void splitk_reduce_batched_kernel(ReduceBatch 
 // 13:  64 x  64, 2x2, S3     14:  64 x 128, 2x2, S3  (small tiles: 2-4 blocks/CU at N = 768)
 // 15: 128 x  64, 2x2, S4     16: 128 x  64, 2x2, S5     17: 128 x 128, 2x2, S4  (deep rings:
 //     more LDS-DMA bytes in flight per CU where the grid is one block per CU)
+// 18: 128 x  64, 4x2, S3     19: 128 x  64, 4x2, S2     20: 128 x  64, 2x4, S3
+// 21: 128 x 128, 4x2, S3  (8-wave blocks: two waves per SIMD where the grid is one block per CU)
 // (A ping-pong variant -- the two 4-wave halves of an 8-wave block staggered by
 // one barrier phase so one half's LDS reads overlap the other's MFMAs -- was
 // correct but measured 1.5-3x slower on these shapes; not kept.)
-constexpr int NCFG = 18;
+constexpr int NCFG = 22;
 struct CfgDesc { int bm, bn, wm, wn, s; };
 constexpr CfgDesc CFGS[NCFG] = {{128, 64, 2, 2, 3}, {128, 128, 2, 2, 2}, {128, 96, 2, 2, 2}, {256, 192, 4, 2, 2},
                                 {256, 128, 4, 2, 3}, {64, 192, 1, 4, 3}, {128, 192, 2, 4, 2}, {256, 96, 4, 1, 3},
                                 {128, 64, 2, 2, 2},  {128, 96, 2, 2, 3}, {128, 128, 2, 2, 3}, {256, 256, 2, 4, 2},
                                 {256, 128, 4, 2, 2}, {64, 64, 2, 2, 3},    {64, 128, 2, 2, 3},  {128, 64, 2, 2, 4},
-                                {128, 64, 2, 2, 5},  {128, 128, 2, 2, 4}};
+                                {128, 64, 2, 2, 5},  {128, 128, 2, 2, 4}, {128, 64, 4, 2, 3},  {128, 64, 4, 2, 2},
+                                {128, 64, 2, 4, 3},  {128, 128, 4, 2, 3}};
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
 bool launch_cfg(const GemmParams& p, int splits, hipStream_t st, const GemmParams* q) {
@@ -649,6 +652,10 @@ bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st, const Ge
     case 15: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 4>(p, splits, st, q);
     case 16: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 5>(p, splits, st, q);
     case 17: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 4>(p, splits, st, q);
+    case 18: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 3>(p, splits, st, q);
+    case 19: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 2>(p, splits, st, q);
+    case 20: return launch_cfg<128, 64, AK, BKM, EPI, 2, 4, 3>(p, splits, st, q);
+    case 21: return launch_cfg<128, 128, AK, BKM, EPI, 4, 2, 3>(p, splits, st, q);
   }
   return false;
 }
@@ -716,7 +723,7 @@ bool launch_epi(int epi, const GemmParams& p, int id, int splits, hipStream_t st
     case EPI_BIAS_GELU: if constexpr (AK && BKM) return launch_id<AK, BKM, EPI_BIAS_GELU>(p, id, splits, st); break;
     case EPI_GELU_BWD: if constexpr (AK) return launch_id<AK, BKM, EPI_GELU_BWD>(p, id, splits, st); break;
     case EPI_ADD: if constexpr (AK) return launch_id<AK, BKM, EPI_ADD>(p, id, splits, st); break;
-    case EPI_F32: if constexpr (!AK && !BKM) return launch_id<AK, BKM, EPI_F32>(p, id, splits, st); break;
+    case EPI_F32: if constexpr (BKM == AK) return launch_id<AK, BKM, EPI_F32>(p, id, splits, st); break;
   }
   return false;
 }
@@ -840,6 +847,16 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
     }
     p.colsum = colsum;
     if (colsum_blocks) *colsum_blocks = (M + CFGS[id].bm - 1) / CFGS[id].bm;
+  }
+  if (kind == 0 && epi == EPI_F32) {
+    // fp32 split-K partials of an NT product into workspace slabs [splits][M][N] (no reduce:
+    // the caller reduces and applies the epilogue); splits from FD_GEMM_SPLITS (default 2)
+    const int so = splits_override();
+    const int splits = so > 0 ? so : 2;
+    if (K % (splits * BKT) != 0 || workspace_elems < (long long)splits * M * N) return 6;
+    p.k_split = K / splits;
+    p.C = workspace; p.ldc = N; p.slab_stride = (long long)M * N;
+    return launch_epi<true, true>(EPI_F32, p, id, splits, st) ? 0 : 2;
   }
   if (kind == 0) {  // also dX = dy (W^T)^T with a transposed weight copy: GELU' / residual epilogues
     if (epi == EPI_F32) return 2;
