@@ -519,7 +519,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
     if constexpr (!SCHED) __builtin_amdgcn_s_setprio(0);
   };
 
-  {
+  if constexpr (S < 6) {
 #pragma unroll
     for (int t = 0; t < S - 1; ++t)
       if (t < nk) issue(t);
@@ -534,6 +534,33 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
       read_frags(smem + (kt % S) * BUF);
       mfmas();
       if constexpr (SCHED) sched_ktile<MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2), MI * NI>();
+    }
+  } else {
+    // Two K tiles per barrier (S >= 6): the slots of the pair read in the previous step are
+    // refilled after ONE barrier, S - 4 tiles stay in flight across it -- half the barriers
+    // and waits of the loop above for the same bytes in flight.
+#pragma unroll
+    for (int t = 0; t < S - 2; ++t)
+      if (t < nk) issue(t);
+
+    for (int kt = 0; kt < nk; kt += 2) {
+      const int issued = min(nk, S - 2 + kt);
+      const int need = min(kt + 2, nk);
+      wait_tiles<L, S - 4>(min(S - 4, max(0, issued - need)));
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (!(p.diag & 1)) {
+        if (kt + S - 2 < nk) issue(kt + S - 2);  // slot of tile kt-2
+        if (kt + S - 1 < nk) issue(kt + S - 1);  // slot of tile kt-1
+      }
+      read_frags(smem + (kt % S) * BUF);
+      mfmas();
+      if constexpr (SCHED) sched_ktile<MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2), MI * NI>();
+      if (kt + 1 < nk) {
+        read_frags(smem + ((kt + 1) % S) * BUF);
+        mfmas();
+        if constexpr (SCHED) sched_ktile<MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2), MI * NI>();
+      }
     }
   }
   // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
@@ -598,17 +625,19 @@ __global__ __launch_bounds__(256) void splitk_reduce_batched_kernel(ReduceBatch 
 //     more LDS-DMA bytes in flight per CU where the grid is one block per CU)
 // 18: 128 x  64, 4x2, S3     19: 128 x  64, 4x2, S2     20: 128 x  64, 2x4, S3
 // 21: 128 x 128, 4x2, S3  (8-wave blocks: two waves per SIMD where the grid is one block per CU)
+// 22: 128 x  64, 2x2, S6     23:  64 x  64, 2x2, S6     24: 128 x  64, 4x2, S6  (two K tiles per barrier)
 // (A ping-pong variant -- the two 4-wave halves of an 8-wave block staggered by
 // one barrier phase so one half's LDS reads overlap the other's MFMAs -- was
 // correct but measured 1.5-3x slower on these shapes; not kept.)
-constexpr int NCFG = 22;
+constexpr int NCFG = 25;
 struct CfgDesc { int bm, bn, wm, wn, s; };
 constexpr CfgDesc CFGS[NCFG] = {{128, 64, 2, 2, 3}, {128, 128, 2, 2, 2}, {128, 96, 2, 2, 2}, {256, 192, 4, 2, 2},
                                 {256, 128, 4, 2, 3}, {64, 192, 1, 4, 3}, {128, 192, 2, 4, 2}, {256, 96, 4, 1, 3},
                                 {128, 64, 2, 2, 2},  {128, 96, 2, 2, 3}, {128, 128, 2, 2, 3}, {256, 256, 2, 4, 2},
                                 {256, 128, 4, 2, 2}, {64, 64, 2, 2, 3},    {64, 128, 2, 2, 3},  {128, 64, 2, 2, 4},
                                 {128, 64, 2, 2, 5},  {128, 128, 2, 2, 4}, {128, 64, 4, 2, 3},  {128, 64, 4, 2, 2},
-                                {128, 64, 2, 4, 3},  {128, 128, 4, 2, 3}};
+                                {128, 64, 2, 4, 3},  {128, 128, 4, 2, 3}, {128, 64, 2, 2, 6},  {64, 64, 2, 2, 6},
+                                {128, 64, 4, 2, 6}};
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
 bool launch_cfg(const GemmParams& p, int splits, hipStream_t st, const GemmParams* q) {
@@ -656,6 +685,9 @@ bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st, const Ge
     case 19: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 2>(p, splits, st, q);
     case 20: return launch_cfg<128, 64, AK, BKM, EPI, 2, 4, 3>(p, splits, st, q);
     case 21: return launch_cfg<128, 128, AK, BKM, EPI, 4, 2, 3>(p, splits, st, q);
+    case 22: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 6>(p, splits, st, q);
+    case 23: return launch_cfg<64, 64, AK, BKM, EPI, 2, 2, 6>(p, splits, st, q);
+    case 24: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 6>(p, splits, st, q);
   }
   return false;
 }
@@ -706,6 +738,12 @@ int pick_cfg(int kind, int M, int N, int K) {
     // profiles/r1_ab_small_tiles.txt): opt-in with FD_GEMM_SMALL_TILES=1.
     static const bool small = [] { const char* e = getenv("FD_GEMM_SMALL_TILES"); return e && atoi(e) != 0; }();
     if (small && N < 1536 && M >= 1024) return 13;
+    // N = 768 at M <= 4 k (the packed / padded bs32 step): 8-wave 128 x 64 tiles with two K
+    // tiles per barrier (cfg 24) -- one block per CU still gets two waves per SIMD, and the
+    // loop pays half the barriers.  2.21-2.25 vs 2.28 ms/step in the model (3 A/B pairs,
+    // profiles/r1_ab_narrow_cfg24.txt).  FD_GEMM_NARROW_CFG=<id> overrides (-1: the rule below).
+    static const int narrow = [] { const char* e = getenv("FD_GEMM_NARROW_CFG"); return e ? atoi(e) : 24; }();
+    if (narrow >= 0 && narrow < NCFG && N < 1536 && M >= 1024 && M <= 4096) return narrow;
     return K >= 2048 ? 0 : 8;
   }
   if (kind == 1) {  // NN dX

@@ -18,7 +18,7 @@ from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed
 from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops._ext import ext
 
 T = int(sys.argv[1]) if len(sys.argv) > 1 else 2688
-NCFG = 22
+NCFG = 25
 g = torch.Generator(device="cuda").manual_seed(0)
 
 
