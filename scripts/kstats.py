@@ -4,8 +4,8 @@ path = sys.argv[1]
 rows = list(csv.DictReader(open(path)))
 arg = sys.argv[2] if len(sys.argv) > 2 else "1"
 if arg == "auto":
-    # step_kernel runs twice per training step (dropout seed + Adam step counter)
-    steps = float(next(r['Calls'] for r in rows if 'step_kernel' in r['Name'])) / 2
+    # the single-launch Adam kernel runs once per training step
+    steps = float(next(r['Calls'] for r in rows if 'adam_kernel' in r['Name']))
 else:
     steps = float(arg)
 tot = sum(float(r['TotalDurationNs']) for r in rows)
