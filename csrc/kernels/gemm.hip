@@ -929,10 +929,25 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
 // Split K only while the combined grid is under one round; slabs of problem 0 then 1.
 // K splits fd_gemm_dw2 plans for these shapes (<= 0: unsupported) -- lets the caller size a
 // slab buffer of its own for a deferred reduce.
-int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K) {
+// Tile configuration of a grouped dW pair.  Default 128 x 64 (cfg 8); pairs too small to give
+// 400 such tiles (o + qkv: 288) use FD_GEMM_DW_SMALL_CFG, the others FD_GEMM_DW_BIG_CFG
+// (-1 = cfg 8).  A 64 x 64 small-pair grid has 576 tiles, so it runs unsplit: no fp32 slabs,
+// no reduce (scripts/dw_split_probe.py).
+int dw2_cfg(int M0, int N0, int M1, int N1) {
   int id = cfg_override(2);
-  if (id < 0) id = 8;
+  if (id < 0) {
+    static const int small_cfg = [] { const char* e = getenv("FD_GEMM_DW_SMALL_CFG"); return e ? atoi(e) : -1; }();
+    static const int big_cfg = [] { const char* e = getenv("FD_GEMM_DW_BIG_CFG"); return e ? atoi(e) : -1; }();
+    const bool small = tiles_of(8, M0, N0) + tiles_of(8, M1, N1) < 400;
+    id = small ? small_cfg : big_cfg;
+    if (id < 0 || id >= NCFG) id = 8;
+  }
   if (M0 % CFGS[id].bm || M1 % CFGS[id].bm || N0 % CFGS[id].bn || N1 % CFGS[id].bn) id = 8;
+  return id;
+}
+
+int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K) {
+  const int id = dw2_cfg(M0, N0, M1, N1);
   const long long tiles = tiles_of(id, M0, N0) + tiles_of(id, M1, N1);
   int splits = 1;
   const int so = splits_override();
@@ -949,9 +964,7 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
                 int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, int* tile_cnt,
                 long long ncnt, const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st) {
   if (K % BKT != 0 || M0 % 128 || M1 % 128 || N0 % 64 || N1 % 64 || M0 <= 0 || M1 <= 0) return 1;
-  int id = cfg_override(2);
-  if (id < 0) id = 8;
-  if (M0 % CFGS[id].bm || M1 % CFGS[id].bm || N0 % CFGS[id].bn || N1 % CFGS[id].bn) id = 8;
+  const int id = dw2_cfg(M0, N0, M1, N1);
   static const int diag = [] { const char* e = getenv("FD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
   GemmParams p[2]{};
   const void* As[2] = {A0, A1};
