@@ -97,6 +97,17 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
   if (row >= a.T) return;  // whole half-waves exit together (T rows, 2 per wave)
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
+  // gamma / beta are fetched before the row data so their round trip overlaps it (issued
+  // after the mean reduction they added two dependent memory round trips to the kernel).
+  float4 gb[CH][4];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = 8 * (hl + HL * c);
+    gb[c][0] = *reinterpret_cast<const float4*>(a.gamma + col);
+    gb[c][1] = *reinterpret_cast<const float4*>(a.gamma + col + 4);
+    gb[c][2] = *reinterpret_cast<const float4*>(a.beta + col);
+    gb[c][3] = *reinterpret_cast<const float4*>(a.beta + col + 4);
+  }
   float z[CH][8];
   uint32_t keep;
   ln_load_sum(a, row, hl, drop, seed, z, keep);
@@ -115,10 +126,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     const int col = 8 * (hl + HL * c);
-    const float4 g0 = *reinterpret_cast<const float4*>(a.gamma + col);
-    const float4 g1 = *reinterpret_cast<const float4*>(a.gamma + col + 4);
-    const float4 b0 = *reinterpret_cast<const float4*>(a.beta + col);
-    const float4 b1 = *reinterpret_cast<const float4*>(a.beta + col + 4);
+    const float4 g0 = gb[c][0], g1 = gb[c][1], b0 = gb[c][2], b1 = gb[c][3];
     const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
     const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
     float y[8];
@@ -157,8 +165,18 @@ __global__ __launch_bounds__(512) void ln_bwd_kernel(LnArgs a) {
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
   float dg[CH][8] = {}, db[CH][8] = {}, dbias[CH][8] = {};
+  // gamma and the row statistics are fetched ahead of the row data (after the data wait
+  // they cost a second dependent round trip per row)
+  float4 gm[CH][2];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = 8 * (hl + HL * c);
+    gm[c][0] = *reinterpret_cast<const float4*>(a.gamma + col);
+    gm[c][1] = *reinterpret_cast<const float4*>(a.gamma + col + 4);
+  }
   const int rows_per_iter = (blockDim.x >> 5);
   for (int row = blockIdx.x * rows_per_iter + (threadIdx.x >> 5); row < a.T; row += gridDim.x * rows_per_iter) {
+    const float mean = a.mean[row], rstd = a.rstd[row];
     uint4 dv[CH];
 #pragma unroll
     for (int c = 0; c < CH; ++c)
@@ -166,14 +184,11 @@ __global__ __launch_bounds__(512) void ln_bwd_kernel(LnArgs a) {
     float xh[CH][8];
     uint32_t keep;
     ln_load_sum(a, row, hl, drop, seed, xh, keep);
-    const float mean = a.mean[row], rstd = a.rstd[row];
     float dyv[CH][8], gd[CH][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      const int col = 8 * (hl + HL * c);
-      const float4 g0 = *reinterpret_cast<const float4*>(a.gamma + col);
-      const float4 g1 = *reinterpret_cast<const float4*>(a.gamma + col + 4);
+      const float4 g0 = gm[c][0], g1 = gm[c][1];
       const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
       unpack8(dv[c], dyv[c]);
 #pragma unroll
