@@ -18,6 +18,10 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
             int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
             long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
             float* colsum, int* colsum_blocks, hipStream_t st);
+int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+               int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
+               long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+               float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
 int fd_gemm_set_fixup(int on);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
@@ -109,7 +113,8 @@ const uint32_t* seedp(const at::Tensor& s) {
 // kind 0: C[M,N] = A[M,K] B[N,K]^T ; kind 1: C[M,N] = A[M,K] B[K,N] ; kind 2: C[M,N] fp32 = A[K,M]^T B[K,N]
 void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, const at::Tensor& C,
           const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
-          const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& workspace, bool accumulate) {
+          const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& workspace, bool accumulate,
+          const c10::optional<at::Tensor>& aux_out) {
   need(A, at::kBFloat16, "A");
   need(B, at::kBFloat16, "B");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
@@ -134,11 +139,15 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
   if (epi == 1 || epi == 2) TORCH_CHECK(bias.has_value() && bias->numel() == N, "bias of size N required");
   if (epi == 2 || epi == 3) TORCH_CHECK(aux.has_value() && aux->size(0) == M && aux->size(1) == N, "aux [M,N] required");
   if (epi == 4) TORCH_CHECK(res.has_value() && res->size(0) == M && res->size(1) == N, "res [M,N] required");
+  need_opt(aux_out, at::kBFloat16, "aux_out");
+  if (aux_out.has_value() && aux_out->defined())
+    TORCH_CHECK(epi == 3 && kind != 2 && aux_out->size(0) == M && aux_out->size(1) == N,
+                "aux_out [M,N] only with the GELU' epilogue");
   const long long ws = (workspace.has_value() && workspace->defined()) ? workspace->numel() : 0;
-  check_rc(fd_gemm((int)kind, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
-                   (int)A.size(1), (int)B.size(1), (int)N, ptr<float>(bias), ptr<void>(aux), (int)N,
-                   ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, nullptr, 0, nullptr,
-                   nullptr, nullptr, stream()),
+  check_rc(fd_gemm_ex((int)kind, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
+                      (int)A.size(1), (int)B.size(1), (int)N, ptr<float>(bias), ptr<void>(aux), (int)N,
+                      ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, nullptr, 0, nullptr,
+                      nullptr, nullptr, ptr<void>(aux_out), stream()),
            "gemm");
 }
 
@@ -147,7 +156,7 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
 // producer-bias gradient.
 int64_t gemm_colsum(int64_t epi, const at::Tensor& A, const at::Tensor& B, const at::Tensor& C,
                     const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& res,
-                    const at::Tensor& colsum) {
+                    const at::Tensor& colsum, const c10::optional<at::Tensor>& aux_out) {
   need(A, at::kBFloat16, "A");
   need(B, at::kBFloat16, "B");
   need(C, at::kBFloat16, "C");
@@ -162,10 +171,13 @@ int64_t gemm_colsum(int64_t epi, const at::Tensor& A, const at::Tensor& B, const
   if (epi == 3) TORCH_CHECK(aux.has_value() && aux->size(0) == M && aux->size(1) == N, "aux [M,N] required");
   if (epi == 4) TORCH_CHECK(res.has_value() && res->size(0) == M && res->size(1) == N, "res [M,N] required");
   TORCH_CHECK(colsum.numel() >= ((M + 127) / 128) * N, "gemm_colsum: colsum needs ceil(M/128) x N floats");
+  need_opt(aux_out, at::kBFloat16, "aux_out");
+  if (aux_out.has_value() && aux_out->defined())
+    TORCH_CHECK(epi == 3 && aux_out->size(0) == M && aux_out->size(1) == N, "aux_out [M,N] only with GELU'");
   int blocks = 0;
-  check_rc(fd_gemm(0, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K, (int)K, (int)K,
-                   (int)N, nullptr, ptr<void>(aux), (int)N, ptr<void>(res), (int)N, nullptr, 0, 0, nullptr, 0,
-                   nullptr, colsum.data_ptr<float>(), &blocks, stream()),
+  check_rc(fd_gemm_ex(0, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K, (int)K,
+                      (int)K, (int)N, nullptr, ptr<void>(aux), (int)N, ptr<void>(res), (int)N, nullptr, 0, 0,
+                      nullptr, 0, nullptr, colsum.data_ptr<float>(), &blocks, ptr<void>(aux_out), stream()),
            "gemm_colsum");
   return blocks;
 }
@@ -776,11 +788,13 @@ void axpby(const at::Tensor& dst, const at::Tensor& x, const c10::optional<at::T
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the federated DistilBERT engine";
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("kind"), py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"),
+        py::arg("aux"), py::arg("res"), py::arg("workspace"), py::arg("accumulate"), py::arg("aux_out") = py::none());
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_dw2", &gemm_dw2);
   m.def("gemm_dw", &gemm_dw);
-  m.def("gemm_colsum", &gemm_colsum);
+  m.def("gemm_colsum", &gemm_colsum, py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("aux"),
+        py::arg("res"), py::arg("colsum"), py::arg("aux_out") = py::none());
   m.def("splitk_reduce_batched", &splitk_reduce_batched);
   m.def("gemm_dw2_splits", [](int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K) {
     return (int64_t)fd_gemm_dw2_splits((int)M0, (int)N0, (int)M1, (int)N1, (int)K);

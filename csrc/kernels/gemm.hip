@@ -73,6 +73,10 @@ struct GemmParams {
   // EPI_GELU_BWD / EPI_ADD with a staged fp32 tile: column sums of the stored output per M
   // tile, [ceil(M / BM)][N] fp32 (the producer-bias gradient, e.g. FFN lin1's bias)
   float* colsum;
+  // EPI_GELU_BWD: also write gelu(aux) here (ld = ldaux; nullable).  The backward re-creates
+  // the FFN activation g = gelu(u) next to its consumer (lin2's weight gradient) instead of
+  // the forward keeping it: bitwise the forward's values (same bf16 u, same gelu_erf).
+  bf16_t* aux_out;
 };
 
 constexpr int BKT = 64;
@@ -284,6 +288,13 @@ DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0
   if (fix && tid == 0) p.tile_cnt[slot] = 0;  // ready for the next launch / graph replay
 }
 
+// aux_out[m][n..n+3] = gelu(aux[m][n..n+3]) from the 4 bf16 pre-activations already loaded
+DEV void gelu_remat(const GemmParams& p, int m, int n, const uint2& u) {
+  *reinterpret_cast<uint2*>(p.aux_out + (size_t)m * p.ldaux + n) =
+      make_uint2(pack_bf2(gelu_erf(lo_bf(u.x)), gelu_erf(hi_bf(u.x))),
+                 pack_bf2(gelu_erf(lo_bf(u.y)), gelu_erf(hi_bf(u.y))));
+}
+
 template <int BM, int BN, int TM, int TN, int EPI, int NT>
 DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int m0, int n0,
                          int wr, int wc, int lane, int tid, int slot) {
@@ -307,6 +318,7 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
           const uint2 u = *reinterpret_cast<const uint2*>(p.aux + (size_t)m * p.ldaux + n);
           v0 *= gelu_erf_grad(lo_bf(u.x)); v1 *= gelu_erf_grad(hi_bf(u.x));
           v2 *= gelu_erf_grad(lo_bf(u.y)); v3 *= gelu_erf_grad(hi_bf(u.y));
+          if (p.aux_out && m0 + r < p.M) gelu_remat(p, m, n, u);
         } else {
           const uint2 r2 = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldres + n);
           v0 += lo_bf(r2.x); v1 += hi_bf(r2.x); v2 += lo_bf(r2.y); v3 += hi_bf(r2.y);
@@ -363,6 +375,7 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
           const uint2 u = *reinterpret_cast<const uint2*>(p.aux + (size_t)m * p.ldaux + n);
           v0 *= gelu_erf_grad(lo_bf(u.x)); v1 *= gelu_erf_grad(hi_bf(u.x));
           v2 *= gelu_erf_grad(lo_bf(u.y)); v3 *= gelu_erf_grad(hi_bf(u.y));
+          if (p.aux_out) gelu_remat(p, m, n, u);
         } else {  // EPI_ADD
           const uint2 r2 = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldres + n);
           v0 += lo_bf(r2.x); v1 += hi_bf(r2.x); v2 += lo_bf(r2.y); v3 += hi_bf(r2.y);
@@ -850,12 +863,28 @@ int fd_gemm_set_cfg(int kind, int cfg, int splits) {
 
 // kind: 0 = NT (y = x W^T), 1 = NN (dx = dy W), 2 = TN (dW = dy^T x, fp32 out)
 // Returns 0 on success, nonzero on unsupported shape.
+int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+               int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
+               long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+               float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st);
+
 int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
             const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
             long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
             float* colsum, int* colsum_blocks, hipStream_t st) {
+  return fd_gemm_ex(kind, epi, A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, res, ldres, workspace,
+                    workspace_elems, accumulate, tile_cnt, ncnt, adam, colsum, colsum_blocks, nullptr, st);
+}
+
+// fd_gemm + aux_out: the GELU' epilogue also re-creates gelu(aux) (nullable; EPI_GELU_BWD only).
+int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+               int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
+               long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+               float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st) {
   if (K % BKT != 0 || N % 64 != 0 || M <= 0 || kind < 0 || kind > 2) return 1;
+  if (aux_out && (epi != EPI_GELU_BWD || kind == 2)) return 7;
   GemmParams p{};
+  p.aux_out = (bf16_t*)aux_out;
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.C = C;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
   p.bias = bias; p.aux = (bf16_t*)aux; p.ldaux = ldaux; p.res = (const bf16_t*)res; p.ldres = ldres;

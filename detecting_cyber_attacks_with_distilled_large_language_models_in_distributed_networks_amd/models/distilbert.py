@@ -255,6 +255,9 @@ class DDoSClassifier(nn.Module):
         self.defer_dw_reduce = True
         # HIP path: FFN lin1's bias gradient summed in the GELU' dX GEMM epilogue
         self.fuse_colsum = True
+        # HIP path: the backward re-creates the FFN activation gelu(u) in the GELU' dX epilogue
+        # instead of the forward keeping it (FD_REMAT_GELU=0: keep it)
+        self.remat_gelu = os.environ.get("FD_REMAT_GELU", "1") != "0"
         # HIP path: build the per-step W^T copies on a side stream concurrently with the forward.
         # Measured SLOWER on MI355X (2.48 vs 2.36 ms/step, profiles/r1_ab_transpose_overlap_slower.txt):
         # the memory-bound transposes stretch the concurrent forward GEMMs.  Off by default.
@@ -449,6 +452,7 @@ class DDoSClassifier(nn.Module):
         if grad and self.defer_dw_reduce and self.layer_grads_hook is None:
             rc.dw_jobs = []
         rc.fuse_colsum = self.fuse_colsum
+        rc.remat_gelu = self.remat_gelu
         if (grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None
                 and not self.wgrad_stream and self.transposed_dx):
             rc.fused_adam = self.fused_opt

@@ -58,6 +58,9 @@ class RunCtx:
     dw_jobs: Optional[list] = None
     # lin1's bias gradient from the GELU' dX GEMM's epilogue (needs colsum_jobs)
     fuse_colsum: bool = True
+    # FFN activation g = gelu(u) not kept by the forward: the backward's GELU' dX GEMM re-creates
+    # it next to its consumer (lin2's dW), so ~16.5 MB/layer less stays live across the step
+    remat_gelu: bool = True
     # side stream that produced data the backward reads (the W^T copies): joined at the
     # first backward node (the head)
     join_stream: Optional["torch.cuda.Stream"] = None
@@ -148,7 +151,7 @@ class LayerFn(torch.autograd.Function):
         y, m2, r2 = K.ln_fwd(f, h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed, ffn_site, p_h, rc.row_map)
         if ctx.needs_input_grad[0]:
             ctx.save_for_backward(x)
-            ctx.acts = (qkv, cx, lse, ao, h, m1, r1, u, g, f, m2, r2)
+            ctx.acts = (qkv, cx, lse, ao, h, m1, r1, u, None if rc.remat_gelu else g, f, m2, r2)
         ctx.L, ctx.rc, ctx.sites, ctx.p = L, rc, (attn_site, ffn_site), (p_a, p_h)
         return y
 
@@ -176,8 +179,11 @@ class LayerFn(torch.autograd.Function):
         # dg W2 * gelu'(u); with deferred column sums and no weight-gradient side stream the
         # epilogue also leaves lin1's bias-gradient partials (no separate pass over du)
         fuse_cs = jobs is not None and rc.wgrad is None and rc.fuse_colsum and wt.get("l2_w") is not None
+        g_out = torch.empty_like(u) if g is None else None  # re-created gelu(u) (RunCtx.remat_gelu)
         du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"),
-                         colsum=(jobs, G["l1_b"].buf, acc) if fuse_cs else None)
+                         colsum=(jobs, G["l1_b"].buf, acc) if fuse_cs else None, aux_out=g_out)
+        if g is None:
+            g = g_out
         wg.fork(df, g, du, h)
         with wg.ctx():
             if rc.group_dw:

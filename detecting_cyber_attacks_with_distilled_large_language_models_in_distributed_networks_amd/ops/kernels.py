@@ -62,36 +62,37 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu
 
 def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] = None,
               res: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None,
-              colsum: Optional[tuple] = None) -> torch.Tensor:
+              colsum: Optional[tuple] = None, aux_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx = dy w  [* gelu'(u)]  [+ res]  (bf16).
 
     With ``wt`` (= w^T, contiguous) the product runs as the K-major "NT" kernel
     dx = dy (w^T)^T, whose operand staging is faster than the MN-major read of w.
     colsum = (deferred colsum jobs, out, accumulate): the GEMM epilogue also leaves the
     column sums of dx per M tile (the producer-bias gradient) as a deferred job, instead
-    of a separate column-sum pass over dx.  Returns dx."""
+    of a separate column-sum pass over dx.  aux_out (with gelu_u): the epilogue also writes
+    gelu(gelu_u) there -- the forward's activation, bitwise.  Returns dx."""
     M, N = dy.shape[0], w.shape[1]
     dx = torch.empty(M, N, dtype=torch.bfloat16, device=dy.device)
     if colsum is not None and wt is not None and (gelu_u is not None or res is not None):
         jobs, out, acc = colsum
         ws = workspace(dy.device, f"colsum_job{len(jobs)}", ((M + 127) // 128) * N)
         epi = EPI_GELU_BWD if gelu_u is not None else EPI_ADD
-        nblk = ext().gemm_colsum(epi, dy, wt, dx, gelu_u, res, ws)
+        nblk = ext().gemm_colsum(epi, dy, wt, dx, gelu_u, res, ws, aux_out)
         if nblk:
             jobs.append((ws, [out], nblk, N, N, acc))
             return dx
         # this shape's tile has no fused column sums: plain GEMM, then the separate pass
-        ext().gemm(0, epi, dy, wt, dx, None, gelu_u, res, None, False)
+        ext().gemm(0, epi, dy, wt, dx, None, gelu_u, res, None, False, aux_out)
         _colsum_pass(dx, out, acc, jobs)
         return dx
     if colsum is not None:
         raise ValueError("fused column sums need the transposed weight and a GELU' / residual epilogue")
     if wt is not None:
         epi = EPI_GELU_BWD if gelu_u is not None else (EPI_ADD if res is not None else EPI_BF16)
-        ext().gemm(0, epi, dy, wt, dx, None, gelu_u, res, None, False)
+        ext().gemm(0, epi, dy, wt, dx, None, gelu_u, res, None, False, aux_out if gelu_u is not None else None)
         return dx
     if gelu_u is not None:
-        ext().gemm(1, EPI_GELU_BWD, dy, w, dx, None, gelu_u, None, None, False)
+        ext().gemm(1, EPI_GELU_BWD, dy, w, dx, None, gelu_u, None, None, False, aux_out)
     elif res is not None:
         ext().gemm(1, EPI_ADD, dy, w, dx, None, None, res, None, False)
     else:

@@ -420,3 +420,25 @@ def test_head_bwd_packed_rows_and_zeroing():
     assert (dh[other] == 0).all()
     x = hidden.float()[rows]
     assert rel_err(dW, dlog.t() @ x) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(2688, 3072, 768), (4000, 3072, 768), (256, 3072, 768)])
+def test_gelu_bwd_rematerialises_activation(M, N, K):
+    # The GELU' dX epilogue's aux_out re-creates the forward activation gelu(u) bitwise
+    # (forward: EPI_BIAS_GELU on x W1^T + b), on every dX path: NT, NT + fused column sums, NN.
+    x, w1, b1 = bf(M, K, seed=60), bf(N, K, scale=0.05, seed=61), bf(N, seed=62).float()
+    g, u = kn.linear_fwd(x, w1, b1, gelu=True)
+    dy, w2 = bf(M, 768, seed=63), bf(768, N, scale=0.05, seed=64)
+    wt = w2.t().contiguous()
+    base = kn.linear_dx(dy, w2, gelu_u=u, wt=wt)
+    for kw in ({"wt": wt}, {}):
+        out = torch.full_like(u, float("nan"))
+        du = kn.linear_dx(dy, w2, gelu_u=u, aux_out=out, **kw)
+        assert torch.equal(out, g)
+        if kw:
+            assert torch.equal(du, base)
+    jobs = []
+    bgrad = torch.zeros(N, device=DEV)
+    out = torch.full_like(u, float("nan"))
+    du = kn.linear_dx(dy, w2, gelu_u=u, wt=wt, colsum=(jobs, bgrad, False), aux_out=out)
+    assert torch.equal(out, g) and torch.equal(du, base)
