@@ -19,6 +19,7 @@ Rank 0 prints ONE JSON line; value = aggregate batches/s over all clients.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -45,6 +46,8 @@ def main():
     ap.add_argument("--spinup-seconds", type=float, default=1.0,
                     help="busy the GPU with a plain matmul loop before the warmup steps (a GPU that was idle "
                          "runs the first ~100 ms of work measurably slower); no model state is touched")
+    ap.add_argument("--step-events", action="store_true",
+                    help="diagnostic: per-step GPU times from events recorded between the timed steps")
     ap.add_argument("--no-quality", action="store_true",
                     help="skip the post-timing aggregated-F1 evaluation (kernel profiles of the step alone)")
     ap.add_argument("--no-defer-dw", action="store_true",
@@ -163,19 +166,33 @@ def main():
             if key not in step.graphs and key not in primed and not step.failed:
                 primed.add(key)
                 step(b["input_ids"], b["attention_mask"], b["labels"], b.get("n_tokens"))
+    # the warmup steps accumulate their loss exactly like the timed loop, so the first timed
+    # step does not pay the one-time load of torch's add kernel (~13 ms on a fresh process)
+    warm_acc = torch.zeros((), device=dev)
     for b in warm[n_early:]:
-        step(b["input_ids"], b["attention_mask"], b["labels"], b.get("n_tokens"))
+        warm_acc += step(b["input_ids"], b["attention_mask"], b["labels"], b.get("n_tokens"))
     k = topo.gpus_per_client
     if args.gpus > 1 or di.distributed:
         fedavg.fedavg_(model, weight=1.0 / k, comm=ncomm)
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    # Python's cyclic GC is collected here and paused over the timed loop (host-side
+    # housekeeping kept out of the timed region; the host submits 50 steps in ~3 ms).
+    gc.collect()
+    gc.disable()
+    loss_acc = torch.zeros((), device=dev)
     sync()
     comm.barrier()
     sync()
     t0 = time.perf_counter()
-    loss_acc = torch.zeros((), device=dev)
-    for b in timed:
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(timed) + 1)] if args.step_events else None
+    if evs:
+        evs[0].record()
+    for i, b in enumerate(timed):
         loss_acc += step(b["input_ids"], b["attention_mask"], b["labels"], b.get("n_tokens"))
+        if evs:
+            evs[i + 1].record()
+    host_s = time.perf_counter() - t0  # host-side submission of the K steps (diagnostic)
+    gc.enable()
     if di.distributed:
         fedavg.fedavg_(model, weight=1.0 / k, comm=ncomm)
     sync()
@@ -224,6 +241,8 @@ def main():
             "unpadded": bool(getattr(model, "unpad", False)) and args.impl == "hip",
             "fused_adam": bool(opt.can_fuse()) and gsync is None,
             "graph_error": step.failed,
+            "host_submit_ms": round(1000.0 * host_s, 2),
+            **({"step_ms": [round(evs[i].elapsed_time(evs[i + 1]), 3) for i in range(len(timed))]} if evs else {}),
             "mean_loss": round(loss, 5),
             **quality,
         }
