@@ -1,20 +1,37 @@
 #!/usr/bin/env python3
-"""Headline benchmark: local federated-client training throughput.
+"""Headline benchmark: local federated-client training throughput + aggregated F1.
 
 Metric (BASELINE.json): batches/sec/client of DistilBERT-base DDoSClassifier
 training at seq_len 128, batch 32, bf16 compute, on synthetic CICIDS2017-shaped
-flows rendered to text (random-init weights), one client per GPU.
+flows rendered to text (random-init weights), one client per GPU -- plus the
+aggregated test F1 after 3 local epochs + 1 FedAvg round.
 
-A "step" is the full reference step (client1.py:102-112): forward, CE loss,
-backward, Adam update -- here the fused HIP kernels replayed as a HIP graph.
-For N > 1 every rank is an independent federated client and the timed region
-also ends with one FedAvg round (RCCL all-reduce of the 66.4 M fp32 masters),
-i.e. communication is charged once per K steps (the reference averages once per
-3 epochs = 1,270 steps at bs32, so this over-charges it).
+Two phases, one process per GPU:
+
+1. Throughput (timed).  A "step" is the full reference step (client1.py:102-112):
+   forward, CE loss, backward, Adam update -- here the fused HIP kernels replayed
+   as a HIP graph.  W untimed warmup steps, then EXACTLY K timed steps between a
+   barrier + device sync on both sides; the time is the MAX over ranks.  For N > 1
+   every rank is an independent federated client and the timed region also ends
+   with one FedAvg round (RCCL all-reduce of the 66.4 M fp32 masters), i.e. the
+   communication is charged once per K steps (the reference averages once per 3
+   epochs = 1,270 steps at bs32, so this over-charges it).  The batches are the
+   client's real training split (below).
+2. Quality (untimed, after the timed window).  The real BASELINE.json config-2/3
+   protocol through the framework's own federated client (fed/runner.py):
+   a 225,745-row synthetic CICIDS2017 file, a 10 % sample per client (seed
+   42 + client), 60/20/20 split (13,544 / 4,515 / 4,515 rows), 3 local epochs of
+   Adam lr 2e-5 at bs32 from the same random init on every client, ONE FedAvg
+   round over all ranks, then ``evaluate_model`` of the aggregate on each
+   client's 4,515 test rows (client1.py:379-401; reference numbers
+   client1_aggregated_metrics.csv:2 / client2_aggregated_metrics.csv:2).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-N > 1 is launched by torch.distributed.run (one process per GPU, RCCL).
-Rank 0 prints ONE JSON line; value = aggregate batches/s over all clients.
+With --gpus N > 1 and no torch.distributed environment, bench.py starts
+``python -m torch.distributed.run --nproc-per-node N`` as a CHILD process
+(before any GPU call; the parent never touches the GPU) and exits with its
+status; every rank checks WORLD_SIZE == N.  Rank 0 prints ONE JSON line;
+value = aggregate batches/s over all clients.
 """
 from __future__ import annotations
 
@@ -22,6 +39,8 @@ import argparse
 import gc
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,9 +49,10 @@ import torch
 
 PKG = "detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd"
 BASELINE_BATCHES_PER_SEC_PER_CLIENT = 2.5  # BASELINE.md (bs16 fp32, Windows PC)
+HEADLINE_METRIC = "batches/sec/client (DistilBERT seq128 bs32) + aggregated F1 after 1 FedAvg round, 1/2/4/8 MI355X"
 
 
-def main():
+def _args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -49,7 +69,11 @@ def main():
     ap.add_argument("--step-events", action="store_true",
                     help="diagnostic: per-step GPU times from events recorded between the timed steps")
     ap.add_argument("--no-quality", action="store_true",
-                    help="skip the post-timing aggregated-F1 evaluation (kernel profiles of the step alone)")
+                    help="skip the post-timing 3-epoch + FedAvg quality protocol (kernel profiles of the step alone)")
+    ap.add_argument("--quality-rows", type=int, default=None,
+                    help="rows of the synthetic file the quality protocol samples 10 %% of "
+                         "(default 225,745 on GPU = the Friday-DDoS file; 2,000 on CPU)")
+    ap.add_argument("--quality-epochs", type=int, default=None, help="local epochs (default 3 on GPU, 1 on CPU)")
     ap.add_argument("--no-defer-dw", action="store_true",
                     help="reduce each split-K weight gradient right after its GEMM instead of once per step (A/B)")
     ap.add_argument("--no-fuse-colsum", action="store_true",
@@ -70,7 +94,39 @@ def main():
                     help="infer: serving throughput of the HIP-graph forward (reference evaluate_model rate)")
     ap.add_argument("--teacher", action="store_true",
                     help="distillation step (BASELINE.json config 5): BERT-base teacher fwd + DistilBERT student")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(args) -> int:
+    """--gpus N > 1 without a torch.distributed environment: run N ranks as a child
+    ``torch.distributed.run`` (one process per GPU, rendezvous on 127.0.0.1) and return its
+    exit status.  Nothing here initialises the GPU (device_count() does not, on this image)."""
+    ngpu = torch.cuda.device_count()
+    shared = os.environ.get("FEDDDOS_BACKEND") == "gloo"  # functional runs: ranks may share a device
+    if ngpu and ngpu < args.gpus and not shared:
+        print(f"bench: --gpus {args.gpus} needs {args.gpus} GPUs (one rank per GPU over RCCL), "
+              f"but this machine has {ngpu}; refusing to report a smaller run", file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    args = _args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn(args))
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from importlib import import_module
@@ -79,55 +135,67 @@ def main():
     models = import_module(f"{PKG}.models")
     engine = import_module(f"{PKG}.engine")
     data = import_module(f"{PKG}.data")
+    runner = import_module(f"{PKG}.fed.runner")
+    config = import_module(f"{PKG}.config")
 
     di = comm.init_distributed()
+    if di.world_size != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the process group has {di.world_size} rank(s)")
     dev = di.device
-    dp = import_module(f"{PKG}.parallel.dp")
-    topo = dp.make_topology(args.gpus_per_client)
-    client = topo.client_idx
+    if di.distributed and dev.type == "cuda" and di.backend != "nccl" and "FEDDDOS_BACKEND" not in os.environ:
+        raise SystemExit(f"bench: GPU ranks must use RCCL (backend 'nccl'), got {di.backend!r}")
     B, S = args.batch_size, args.seq_len
-    n_batches = args.warmup + args.steps
-    # Synthetic CICIDS2017 rows -> the reference's text template -> WordPiece ids.
-    df = data.generate_cicids2017(max(n_batches * B * 2, 4096), seed=client)
-    cd = data.build_client_data(df, client, data_fraction=1.0, max_len=S)
-    train = cd.train
-    loader = data.DeviceLoader(train, B, shuffle=True, device=dev, seed=client, drop_last=True)
-    if topo.dp:
-        loader = dp.DPShardLoader(loader, topo.dp_rank, topo.gpus_per_client)
+    on_gpu = dev.type == "cuda"
 
+    # ---- the client: its data split (also the throughput batches) and, later, the protocol
+    q_rows = args.quality_rows or (225_745 if on_gpu else 2_000)
+    q_epochs = args.quality_epochs or (3 if on_gpu else 1)
+    fc = config.FedConfig(synthetic_rows=q_rows, batch_size=B, eval_batch_size=16, epochs=q_epochs, rounds=1,
+                          max_len=S, impl=args.impl, gpus_per_client=args.gpus_per_client, comm=args.comm,
+                          out_dir=os.path.join(os.environ.get("TMPDIR", "/tmp"), f"fedddos_bench_{os.getpid()}"),
+                          plots=False, resume=False, save_checkpoints=False, heartbeat_s=0.0, verbose=False,
+                          teacher="bert-base" if args.teacher else None)
+    client = runner.FederatedClient(fc, model_config=models.DistilBertConfig(n_layers=args.layers))
+    topo = client.topo
+    k = topo.gpus_per_client
+    t_setup = time.perf_counter()
+    client.setup()
+    t_setup = time.perf_counter() - t_setup
+    train = client.data.train
+    loader = data.DeviceLoader(train, B, shuffle=True, device=dev, seed=topo.client_idx, drop_last=True)
+    if topo.dp:
+        loader = import_module(f"{PKG}.parallel.dp").DPShardLoader(loader, topo.dp_rank, k)
+
+    # ---- the throughput model (same architecture and init; discarded after the timed window)
     cfg = models.DistilBertConfig(n_layers=args.layers)
     model = models.DDoSClassifier(config=cfg, device=dev, impl=args.impl, seed=0)
     model.wgrad_stream = args.wgrad_stream
     model.group_dw = not args.no_group_dw
     model.defer_dw_reduce = not args.no_defer_dw
     model.fuse_colsum = not args.no_fuse_colsum
-    ncomm = None
-    if args.comm == "rccl" and dev.type == "cuda":
-        ncomm = import_module(f"{PKG}.parallel.rccl").NativeComm()
+    ncomm = client.comm
     fedavg.broadcast_model(model, comm=ncomm)
     opt = engine.ArenaAdam(model, lr=2e-5, fuse_dw=args.fused_adam)
     gsync = None
-    if topo.dp:
-        teacher = None
-        if args.teacher:
-            teacher = models.BertTeacherClassifier(config=models.bert_base_config(), device=dev, impl=args.impl)
-            fedavg.broadcast_model(teacher, comm=ncomm)
-            teacher.eval()
-        dp.dp_seed_offset(model, topo.dp_rank)
-        gsync = dp.GradSync(model, topo.dp_group, topo.gpus_per_client, max_rows=B * S)
-        gsync.set_loss_scale(1.0 / topo.gpus_per_client)
-        fn = dp.make_dp_step_fn(model, opt, gsync, teacher, 2.0, 0.5)
-    elif args.teacher:
+    teacher = None
+    if args.teacher:
         teacher = models.BertTeacherClassifier(config=models.bert_base_config(), device=dev, impl=args.impl)
         fedavg.broadcast_model(teacher, comm=ncomm)
         teacher.eval()
+    if topo.dp:
+        dp = import_module(f"{PKG}.parallel.dp")
+        dp.dp_seed_offset(model, topo.dp_rank)
+        gsync = dp.GradSync(model, topo.dp_group, k, max_rows=B * S)
+        gsync.set_loss_scale(1.0 / k)
+        fn = dp.make_dp_step_fn(model, opt, gsync, teacher, 2.0, 0.5)
+    elif args.teacher:
         fn = engine.make_kd_step_fn(model, teacher, opt, 2.0, 0.5)
     else:
         fn = engine.make_step_fn(model, opt)
     model.unpad = not args.padded
     model.overlap_transpose = args.overlap_transpose
     step = engine.GraphedTrainStep(fn, warmup=2, enabled=(not args.no_graph) and args.impl == "hip"
-                                   and dev.type == "cuda" and gsync is None,
+                                   and on_gpu and gsync is None,
                                    bucket=getattr(model, "packed_rows", None))
     model.train()
 
@@ -137,7 +205,7 @@ def main():
                 yield b
 
     it = batches()
-    if dev.type == "cuda" and args.spinup_seconds > 0:
+    if on_gpu and args.spinup_seconds > 0:
         a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
         t_end = time.perf_counter() + args.spinup_seconds
         while time.perf_counter() < t_end:
@@ -150,10 +218,7 @@ def main():
     # The timed batches are drawn up front; any packed-row bucket among them without a
     # captured graph yet gets one extra (untimed) training step on that batch, so no HIP
     # graph capture happens inside the timed region.  The W warmup steps run after that
-    # host-side work, right before the timed region, so the GPU enters it at full clock
-    # (drawing the batches first left it idle for a few ms: ~9 ms more per timed run).
-    # (The first warmup steps run before the draw: the graph wrapper's eager calls, so the
-    # priming below captures.)
+    # host-side work, right before the timed region, so the GPU enters it at full clock.
     warm = [next(it) for _ in range(args.warmup)]
     n_early = min(len(warm), max(0, step.warmup) if step.enabled else 0)
     for b in warm[:n_early]:
@@ -167,16 +232,15 @@ def main():
                 primed.add(key)
                 step(b["input_ids"], b["attention_mask"], b["labels"], b.get("n_tokens"))
     # the warmup steps accumulate their loss exactly like the timed loop, so the first timed
-    # step does not pay the one-time load of torch's add kernel (~13 ms on a fresh process)
+    # step does not pay the one-time load of torch's add kernel
     warm_acc = torch.zeros((), device=dev)
     for b in warm[n_early:]:
         warm_acc += step(b["input_ids"], b["attention_mask"], b["labels"], b.get("n_tokens"))
-    k = topo.gpus_per_client
-    if args.gpus > 1 or di.distributed:
+    if di.distributed:
         fedavg.fedavg_(model, weight=1.0 / k, comm=ncomm)
-    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
     # Python's cyclic GC is collected here and paused over the timed loop (host-side
-    # housekeeping kept out of the timed region; the host submits 50 steps in ~3 ms).
+    # housekeeping kept out of the timed region).
     gc.collect()
     gc.disable()
     loss_acc = torch.zeros((), device=dev)
@@ -198,24 +262,40 @@ def main():
     sync()
     comm.barrier()
     sync()
-    dt = time.perf_counter() - t0
-    dt = comm.all_reduce_max(dt)
+    dt_rank = time.perf_counter() - t0
+    per_rank_ms = [round(1000.0 * v[0] / args.steps, 4) for v in comm.all_gather_floats([dt_rank])]
+    dt = comm.all_reduce_max(dt_rank)
     loss = float(loss_acc.item()) / args.steps
-    # Second half of the metric: the FedAvg-aggregated model (the all-reduce that closes the
-    # timed region) scored on every client's held-out test split -- counts summed over
-    # clients, one F1 (untimed; the reference's evaluate_model after aggregation,
-    # client1.py:118-150 / 330-340).
-    quality = {} if args.no_quality else _aggregated_quality(model, cd.test, dev, topo, engine, data, di)
     if not (loss == loss and abs(loss) < 1e6):
         raise SystemExit(f"bench: non-finite training loss {loss} -- refusing to report a throughput")
+    tok = [int(b["n_tokens"]) for b in timed if b.get("n_tokens") is not None]
+    real_frac = (sum(tok) / (len(tok) * B * S)) if tok else 1.0
+    rows_frac = (sum(model.packed_rows(t, B, S) for t in tok) / (len(tok) * B * S)) \
+        if tok and model.unpad and args.impl == "hip" else 1.0
+    comm_stats = _fedavg_timing(model, di, fedavg, comm, ncomm, k, sync)
+    graphs = len(getattr(step, "graphs", {}))
+    graph_ok = step.graph is not None
+    graph_err = step.failed
+    fused = bool(opt.can_fuse()) and gsync is None
+    del step, fn, opt, model, warm, timed, it, loader, gsync, teacher
+    gc.collect()
+    if on_gpu:
+        torch.cuda.empty_cache()
+
+    # ---- quality: 3 local epochs + 1 FedAvg round through the federated client (untimed)
+    quality = {} if args.no_quality else _quality(client, di, comm, q_rows, q_epochs, on_gpu)
     n = di.world_size
     clients = topo.num_clients
     per_client = args.steps / dt
     if di.is_main:
+        default_cfg = (S == 128 and B == 32 and args.layers == 6 and not args.teacher)
+        metric = HEADLINE_METRIC if default_cfg else (
+            f"batches/sec/client (DistilBERT{'' if args.layers == 6 else f' {args.layers}-layer'} seq{S} bs{B}"
+            + (" KD from BERT-base teacher" if args.teacher else "") + ") + aggregated F1 after 1 FedAvg round")
         out = {
-            "metric": "batches/sec/client (DistilBERT seq128 bs32) + aggregated F1 after 1 FedAvg round, 1/2/4/8 MI355X",
+            "metric": metric,
             "value": round(per_client * clients, 4),
-            "unit": "batches/s (sum over clients; bs32 x seq128)",
+            "unit": f"batches/s (sum over clients; bs{B} x seq{S})",
             "n_gpus": n,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -224,7 +304,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(per_client / BASELINE_BATCHES_PER_SEC_PER_CLIENT, 3),
             "dtype": "bf16" if args.impl == "hip" else "fp32",
-            "data": "synthetic CICIDS2017-shaped flows rendered to text, WordPiece seq128; random-init weights",
+            "data": "synthetic CICIDS2017-shaped flows rendered to text (the client's 10 % sample of a "
+                    f"{q_rows:,}-row synthetic file), WordPiece seq{S}; random-init weights",
             "config": {"model": f"DistilBERT-base ({args.layers} layers) + Linear(768,2) DDoSClassifier"
                                 + (" <- KD from BERT-base teacher" if args.teacher else ""),
                        "global_batch": B * clients, "seq_len": S,
@@ -233,42 +314,98 @@ def main():
             "samples_per_sec_total": round(per_client * clients * B, 2),
             "tokens_per_sec_total": round(per_client * clients * B * S, 1),
             "vs_baseline_basis": "per-client batches/s / 2.5 (reference bs16 fp32 per-client rate)",
+            "per_rank_ms_per_step": per_rank_ms,
+            "backend": di.backend,
+            "real_token_fraction": round(real_frac, 4),
+            "packed_row_fraction": round(rows_frac, 4),
             "impl": args.impl,
             "comm": args.comm,
             "spinup_s": args.spinup_seconds,
-            "hip_graph": step.graph is not None,
-            "hip_graphs": len(getattr(step, "graphs", {})),
-            "unpadded": bool(getattr(model, "unpad", False)) and args.impl == "hip",
-            "fused_adam": bool(opt.can_fuse()) and gsync is None,
-            "graph_error": step.failed,
+            "setup_s": round(t_setup, 2),
+            "hip_graph": graph_ok,
+            "hip_graphs": graphs,
+            "unpadded": bool(rows_frac < 1.0),
+            "fused_adam": fused,
+            "graph_error": graph_err,
             "host_submit_ms": round(1000.0 * host_s, 2),
-            **({"step_ms": [round(evs[i].elapsed_time(evs[i + 1]), 3) for i in range(len(timed))]} if evs else {}),
+            **({"step_ms": [round(evs[i].elapsed_time(evs[i + 1]), 3) for i in range(len(evs) - 1)]} if evs else {}),
             "mean_loss": round(loss, 5),
+            **comm_stats,
             **quality,
         }
         print(json.dumps(out), flush=True)
     comm.shutdown()
 
 
-def _aggregated_quality(model, test, dev, topo, engine, data, di):
-    """Accuracy / F1 of the aggregated model over all clients' test rows (one replica per client)."""
-    loader = data.DeviceLoader(test, 256, shuffle=False, device=dev, drop_last=False)
-    res = engine.evaluate_model(model, loader)
-    lab = np.asarray(res[6], dtype=np.int64)
-    pred = (np.asarray(res[7]) > 0.5).astype(np.int64)
-    c = torch.tensor([int(((pred == 1) & (lab == 1)).sum()), int(((pred == 1) & (lab == 0)).sum()),
-                      int(((pred == 0) & (lab == 1)).sum()), int(((pred == 0) & (lab == 0)).sum())],
-                     dtype=torch.float64, device=dev)
-    if topo.dp_rank != 0:
-        c.zero_()  # data-parallel replicas hold the same client's split
-    if di.distributed:
-        torch.distributed.all_reduce(c)
-    tp, fp, fn, tn = c.tolist()
+def _fedavg_timing(model, di, fedavg, comm, ncomm, k, sync):
+    """FedAvg round time (all-reduce of the 265 MB fp32 arena + fused scale/cast) and the raw
+    all-reduce's bus bandwidth, 2(N-1)/N x bytes / t (untimed diagnostics, max over ranks)."""
+    if not di.distributed:
+        return {"fedavg_ms": None, "allreduce_ms": None, "allreduce_busbw_GBps": None}
+    A = model.arena.master
+    nbytes = A.numel() * A.element_size()
+    n = di.world_size
+    fed, raw = [], []
+    scratch = torch.empty_like(A)
+    for _ in range(3):
+        sync()
+        comm.barrier()
+        t = time.perf_counter()
+        fedavg.fedavg_(model, weight=1.0 / k, comm=ncomm)
+        sync()
+        fed.append(time.perf_counter() - t)
+    import torch.distributed as dist
+    for _ in range(3):
+        scratch.copy_(A)
+        sync()
+        comm.barrier()
+        t = time.perf_counter()
+        if ncomm is not None and scratch.is_cuda:
+            ncomm.all_reduce_(scratch, "sum")
+        else:
+            dist.all_reduce(scratch)
+        sync()
+        raw.append(time.perf_counter() - t)
+    del scratch
+    f = comm.all_reduce_max(min(fed))
+    r = comm.all_reduce_max(min(raw))
+    return {"fedavg_ms": round(1e3 * f, 3), "allreduce_ms": round(1e3 * r, 3),
+            "allreduce_bytes": nbytes,
+            "allreduce_busbw_GBps": round(2.0 * (n - 1) / n * nbytes / r / 1e9, 2)}
+
+
+def _quality(client, di, comm, rows, epochs, on_gpu):
+    """Run round 1 of the federated client (fed/runner.py run_round: local train -> local eval
+    -> FedAvg -> aggregated eval) and pool the aggregated test confusion matrices of all clients."""
+    t0 = time.perf_counter()
+    rec = client.run_round(0)
+    if on_gpu:
+        torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    agg, loc = rec["aggregated_test"], rec["local_test"]
+    (tn, fp), (fn, tp) = agg["confusion_matrix"] if len(agg["confusion_matrix"]) == 2 else ((0, 0), (0, 0))
+    writer = 1.0 if client.topo.dp_rank == 0 else 0.0  # data-parallel replicas share one client's split
+    vec = [writer * v for v in (tp, fp, fn, tn, agg["accuracy"], agg["f1"], loc["accuracy"], loc["f1"])]
+    allv = [v for v in comm.all_gather_floats(vec + [writer]) if v[-1] > 0]
+    tp, fp, fn, tn = (sum(v[i] for v in allv) for i in range(4))
     prec = tp / (tp + fp) if tp + fp else 0.0
-    rec = tp / (tp + fn) if tp + fn else 0.0
-    f1 = 2 * prec * rec / (prec + rec) if prec + rec else 0.0
-    return {"aggregated_f1": round(f1, 5), "aggregated_accuracy_pct": round(100.0 * (tp + tn) / max(tp + fp + fn + tn, 1), 3),
-            "eval_rows": int(tp + fp + fn + tn), "fedavg_rounds": 1 if di.distributed else 0}
+    rec_ = tp / (tp + fn) if tp + fn else 0.0
+    f1 = 2 * prec * rec_ / (prec + rec_) if prec + rec_ else 0.0
+    total = tp + fp + fn + tn
+    tr = rec["train"]
+    return {"aggregated_f1": round(f1, 5),
+            "aggregated_accuracy_pct": round(100.0 * (tp + tn) / max(total, 1), 3),
+            "aggregated_confusion": [[int(tn), int(fp)], [int(fn), int(tp)]],
+            "min_client_aggregated_accuracy_pct": round(min(v[4] for v in allv), 3),
+            "min_client_aggregated_f1": round(min(v[5] for v in allv), 5),
+            "mean_client_local_accuracy_pct": round(float(np.mean([v[6] for v in allv])), 3),
+            "mean_client_local_f1": round(float(np.mean([v[7] for v in allv])), 5),
+            "eval_rows": int(total), "eval_rows_per_client": int(total) // max(len(allv), 1),
+            "train_rows_per_client": len(client.data.train), "quality_clients": len(allv),
+            "fedavg_rounds": 1, "local_epochs": epochs, "quality_file_rows": rows,
+            "quality_epoch_losses": [round(x, 5) for x in tr["epoch_losses"]],
+            "quality_train_steps": tr["steps"], "quality_train_batches_per_sec": round(tr["batches_per_sec"], 2),
+            "quality_fedavg_ms": round(rec["fedavg_ms"], 3), "quality_wall_s": round(wall, 2)}
 
 
 def _bench_infer(args, model, it, di, comm, B, S):

@@ -63,6 +63,7 @@ class FedConfig:
     plots: bool = True
     resume: bool = True                     # client1.py:375-377 loads clientN_model.pth
     save_optimizer: bool = False
+    save_checkpoints: bool = True           # clientN_model.pth / ddos_distilbert_model.pth (bench: off)
     # --- fault injection -------------------------------------------------
     drop_client: Optional[int] = None       # client whose update is dropped ...
     drop_round: Optional[int] = None        # ... at this round

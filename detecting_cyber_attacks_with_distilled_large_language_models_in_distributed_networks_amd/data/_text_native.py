@@ -1,4 +1,4 @@
-"""Loader for the C++ text extension (data/_text_native_impl*.so); builds it on demand."""
+"""Loader for the C++ text extension (<repo>/_so/_text_native_impl.so, _build.py); builds it on demand."""
 from __future__ import annotations
 
 import os
@@ -13,15 +13,15 @@ def load():
     if _MOD is not None or _TRIED:
         return _MOD
     _TRIED = True
+    from .. import _build
     try:
-        from . import _text_native_impl as m
+        m = _build.load_text()
     except ImportError:
         if os.environ.get("FEDDDOS_AUTOBUILD", "1") != "1":
             return None
         try:
-            from .. import _build
             _build.build_text()
-            from . import _text_native_impl as m  # noqa: F811
+            m = _build.load_text()
         except Exception:
             return None
     _MOD = m

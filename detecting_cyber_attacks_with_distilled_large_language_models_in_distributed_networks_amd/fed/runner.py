@@ -114,17 +114,7 @@ class FederatedClient:
         self.start_round = 0
         self.history: List[Dict] = []
         if cfg.resume:
-            st = ck.load_fed_state(cfg.out_dir, self.client_id)
-            path = ck.client_ckpt_path(cfg.out_dir, self.client_id)
-            if st and int(st.get("completed_rounds", 0)) > 0 and os.path.exists(ck.global_ckpt_path(cfg.out_dir)):
-                # a crash inside round r leaves clientN_model.pth = the round-r LOCAL model; the
-                # round's true starting point is the last aggregate (identical on every client)
-                path = ck.global_ckpt_path(cfg.out_dir)
-            if ck.load_model(self.model, path):
-                log.info(f"loading pre-trained model from {path}")
-                if st:
-                    self.start_round = int(st.get("completed_rounds", 0))
-                    self.history = st.get("history", [])
+            self._resume()
         self.health = None
         if self.di.distributed and cfg.heartbeat_s > 0 and cfg.transport != "tcp":
             self.health = health.start(cfg.heartbeat_s, cfg.heartbeat_stale_s, cfg.timeout_s)
@@ -134,6 +124,40 @@ class FederatedClient:
         log.info(f"data: {len(self.data.train)} train / {len(self.data.val)} val / {len(self.data.test)} test rows "
                  f"(sampled {self.data.n_rows}), impl={self.model.impl}, device={dev}")
         return self
+
+    def _resume(self):
+        """Pick ONE resume round for the whole world and start every client from that round's
+        aggregate.
+
+        The source of truth is the round tag of ``ddos_distilbert_model.pth``, which rank 0
+        writes right after FedAvg and before any client records the round in its fed_state.
+        Rank 0 can tag round r+1 only after every client has finished round r, so after a crash
+        the tag is the last round whose aggregate exists, whatever each client's own sidecar
+        says.  The tag is MIN-reduced over the world so every rank agrees even if one cannot
+        see the file; rank 0 loads the aggregate and broadcasts it.  A client's own
+        ``clientN_model.pth`` is never the resume point of a collective run: after a crash
+        inside a round it holds that round's LOCAL model (fed/runner.py run_round saves it
+        before FedAvg).  Single-process runs with no sidecar keep the reference behaviour of
+        loading it (client1.py:375-377: re-running the script is the next round)."""
+        cfg, log = self.cfg, self.log
+        st = ck.load_fed_state(cfg.out_dir, self.client_id)
+        tagged = ck.load_global_round(cfg.out_dir)
+        start = int(comm.all_reduce_min(float(tagged))) if self.di.distributed else tagged
+        if start > 0:
+            path = ck.global_ckpt_path(cfg.out_dir)
+            if self.di.is_main or not self.di.distributed:
+                ck.load_model(self.model, path)
+            broadcast_model(self.model, comm=self.comm)
+            self.start_round = start
+            self.history = [h for h in (st or {}).get("history", []) if int(h.get("round", 0)) <= start]
+            done = int((st or {}).get("completed_rounds", 0))
+            if done != start:
+                log.info(f"client sidecar says {done} completed round(s); the aggregate says {start}")
+            log.info(f"loading pre-trained model from {path} (aggregate of round {start})")
+        elif st is None and not self.di.distributed:
+            path = ck.client_ckpt_path(cfg.out_dir, self.client_id)
+            if ck.load_model(self.model, path):
+                log.info(f"loading pre-trained model from {path}")
 
     # ------------------------------------------------------------------ one round
     def run_round(self, r: int) -> Dict:
@@ -165,7 +189,8 @@ class FederatedClient:
         sfx = "" if r == 0 else f"_round{r + 1}"
         if self.writer:
             save_metrics(local, os.path.join(cfg.out_dir, f"client{self.client_id}_local_metrics{sfx}.csv"), log)
-            ck.save_model(model, ck.client_ckpt_path(cfg.out_dir, self.client_id))
+            if cfg.save_checkpoints:
+                ck.save_model(model, ck.client_ckpt_path(cfg.out_dir, self.client_id))
             if cfg.save_optimizer:
                 ck.save_optimizer(opt, opt_path)
 
@@ -174,7 +199,7 @@ class FederatedClient:
         contributes = self.idx in part and not faults.dropped(cfg, self.idx, r)
         weight = float(len(self.data.train)) if cfg.weighted_fedavg else 1.0
         weight /= self.topo.gpus_per_client  # k identical replicas per client share its weight
-        faults.maybe_kill(self.idx, r, cfg.out_dir, self.topo.dp_rank)
+        faults.maybe_kill(self.idx, r, cfg.out_dir, self.topo.dp_rank, phase="fedavg")
         if self.health is not None:
             try:  # every client alive and here, or fail fast naming the dead rank
                 self.health.barrier(f"fedavg/{r}")
@@ -196,8 +221,9 @@ class FederatedClient:
             t_fed = time.perf_counter() - t0
         log.info(f"updated with aggregated model (participated={contributes}, total weight={total_w:g}, "
                  f"{t_fed * 1e3:.2f} ms)")
-        if self.di.is_main:
-            ck.save_model(model, ck.global_ckpt_path(cfg.out_dir))
+        if self.di.is_main and cfg.save_checkpoints:
+            ck.save_global(model, cfg.out_dir, r + 1)  # weights, then the round tag (_resume)
+        faults.maybe_kill(self.idx, r, cfg.out_dir, self.topo.dp_rank, phase="post_fedavg")
         log.info("evaluating aggregated model on validation set...")
         with self.timer("eval"):
             val_agg = evaluate_model(model, self.val_loader, log=log, name="Validation")
@@ -210,7 +236,7 @@ class FederatedClient:
                 from ..utils.plots import plot_evaluation
                 plot_evaluation(local, agg, os.path.join(cfg.out_dir, f"client{self.client_id}_plots"),
                                 f"Client {self.client_id}", log=log)
-        if self.writer:
+        if self.writer and cfg.save_checkpoints:
             ck.save_model(model, ck.client_ckpt_path(cfg.out_dir, self.client_id))
         rec = {"round": r + 1, "train": tr, "fedavg_ms": t_fed * 1e3, "participated": contributes,
                "local_val": _metrics_record(val_local), "local_test": _metrics_record(local),

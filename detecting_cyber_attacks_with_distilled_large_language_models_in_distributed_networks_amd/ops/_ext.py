@@ -1,4 +1,4 @@
-"""Loader for the in-tree gfx950 kernel extension (ops/_hip_kernels*.so).
+"""Loader for the in-tree gfx950 kernel extension (<repo>/_so/_hip_kernels.so, _build.py).
 
 GPU tensors always go through the HIP kernels: if the extension is missing on a
 machine with a GPU, ``ext()`` raises instead of silently falling back to
@@ -16,14 +16,14 @@ def ext():
     global _EXT, _ERR
     if _EXT is not None:
         return _EXT
+    from .. import _build
     try:
-        from . import _hip_kernels as m  # noqa: F401
+        m = _build.load_hip()
     except ImportError as e:  # pragma: no cover - depends on build state
         _ERR = e
         if os.environ.get("FEDDDOS_AUTOBUILD", "1") == "1":
-            from .. import _build
             _build.build_hip()
-            from . import _hip_kernels as m  # noqa: F811
+            m = _build.load_hip()
         else:
             raise RuntimeError(
                 "gfx950 kernel extension is not built; run "

@@ -102,6 +102,14 @@ def all_reduce_max(x: float) -> float:
     return float(t.item())
 
 
+def all_reduce_min(x: float) -> float:
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=info().device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
 def all_gather_floats(vals: List[float]) -> List[List[float]]:
     """Gather a small per-rank float vector (metrics) to every rank."""
     if not (dist.is_available() and dist.is_initialized()):

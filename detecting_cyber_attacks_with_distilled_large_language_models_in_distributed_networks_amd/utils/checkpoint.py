@@ -55,6 +55,33 @@ def load_model(model, path: str, strict: bool = True) -> bool:
     return True
 
 
+def global_tag_path(out_dir: str) -> str:
+    return os.path.join(out_dir, "ddos_distilbert_model.json")
+
+
+def save_global(model, out_dir: str, round_done: int) -> str:
+    """Rank 0: the round-``round_done`` aggregate, then its round tag (written after the
+    weights, so a tag never names a checkpoint that is not on disk yet)."""
+    path = save_model(model, global_ckpt_path(out_dir))
+    tag = global_tag_path(out_dir)
+    with open(tag + ".tmp", "w") as f:
+        json.dump({"round": int(round_done)}, f)
+    os.replace(tag + ".tmp", tag)
+    return path
+
+
+def load_global_round(out_dir: str) -> int:
+    """Round whose aggregate ``ddos_distilbert_model.pth`` holds (0: none / untagged)."""
+    tag = global_tag_path(out_dir)
+    if not (os.path.exists(tag) and os.path.exists(global_ckpt_path(out_dir))):
+        return 0
+    try:
+        with open(tag) as f:
+            return int(json.load(f).get("round", 0))
+    except (OSError, ValueError):
+        return 0
+
+
 def save_optimizer(opt, path: str):
     _atomic_save(opt.state_dict(), path)
 

@@ -2,8 +2,10 @@
 
 Knobs (config fields or env):
   drop_client / drop_round   drop client k's update at round r (it still receives the aggregate)
-  FEDDDOS_KILL_CLIENT=k, FEDDDOS_KILL_ROUND=r
-                              hard-exit client k at the start of round r's FedAvg; the
+  FEDDDOS_KILL_CLIENT=k, FEDDDOS_KILL_ROUND=r, FEDDDOS_KILL_AT=fedavg|post_fedavg
+                              hard-exit client k at the start of round r's FedAvg (default),
+                              or after it (aggregate written by rank 0, before the client
+                              records the round in its fed_state sidecar); the
                               survivors' health-checked barrier (parallel/health.py) names
                               the dead rank within seconds.  One-shot per (k, r) when a
                               marker directory is given, so an elastic restart
@@ -32,9 +34,12 @@ def dropped(cfg, client_idx: int, round_idx: int) -> bool:
         (cfg.drop_round is None or cfg.drop_round == round_idx)
 
 
-def maybe_kill(client_idx: int, round_idx: int, marker_dir: Optional[str] = None, replica: int = 0):
+def maybe_kill(client_idx: int, round_idx: int, marker_dir: Optional[str] = None, replica: int = 0,
+               phase: str = "fedavg"):
     k = os.environ.get("FEDDDOS_KILL_CLIENT")
     r = os.environ.get("FEDDDOS_KILL_ROUND")
+    if os.environ.get("FEDDDOS_KILL_AT", "fedavg") != phase:
+        return
     if k is not None and int(k) == client_idx and (r is None or int(r) == round_idx):
         if marker_dir is not None:
             marker = os.path.join(marker_dir, f".killed_client{client_idx}_round{round_idx}_r{replica}")
