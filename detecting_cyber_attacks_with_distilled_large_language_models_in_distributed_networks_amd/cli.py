@@ -59,7 +59,9 @@ def _server(argv):
     ap.add_argument("--port-send", type=int, default=12346)
     ap.add_argument("--timeout", type=float, default=300.0)
     ap.add_argument("--out-dir", default=".")
-    ap.add_argument("--strict-compat", action="store_true")
+    ap.add_argument("--strict-compat", action="store_true",
+                    help="drop the GET handshake on downloads (the reference's framing); the payload codec "
+                         "stays gzip(torch.save) + weights-only load, so reference pickle clients cannot connect")
     ap.add_argument("--gzip-level", type=int, default=1)
     ns = ap.parse_args(argv)
     from .parallel.transport import FedAvgServer

@@ -52,7 +52,7 @@ class FedConfig:
     timeout_s: float = 300.0                # server.py:10 / client1.py:22
     heartbeat_s: float = 1.0                # failure detection (parallel/health.py); 0 disables
     heartbeat_stale_s: float = 10.0         # a peer silent this long is declared dead
-    transport: str = "collective"           # "collective" (RCCL/gloo all-reduce) | "tcp" (reference protocol)
+    transport: str = "collective"           # "collective" (RCCL/gloo all-reduce) | "tcp" (reference framing; weights-only payload)
     comm: str = "torch"                     # collective backend: "torch" (torch.distributed) | "rccl" (NativeComm)
     server_host: str = "localhost"          # client1.py:276,314
     port_receive: int = 12345               # server.py:11

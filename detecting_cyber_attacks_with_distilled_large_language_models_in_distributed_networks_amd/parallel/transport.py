@@ -13,11 +13,18 @@ Ports: uploads to 12345, downloads from 12346 (server.py:11-12).
 Deliberate differences:
   * payload codec: gzip(torch.save(state_dict)) decoded with
     ``torch.load(weights_only=True)`` -- never unpickle bytes from a socket
-    (the reference uses pickle.loads); gzip level defaults to 1, not 9 (the
-    level-9 compress is 11 s of the reference's ~20 s round, SURVEY 6);
+    (the reference sends gzip(pickle.dumps(state_dict)) and decodes it with
+    pickle.loads, client1.py:228-243).  ONLY THE FRAMING is compatible: this
+    server cannot decode a reference client's payload and a reference server
+    cannot decode ours.  gzip level defaults to 1, not 9 (the level-9 compress is
+    11 s of the reference's ~20 s round, SURVEY 6);
   * download requests start with b"GET\\n" so a readiness probe (the reference's
     wait_for_server) is never mistaken for a client (the WinError 10053 bug,
-    SURVEY 5.3); ``strict_compat=True`` restores the reference behaviour;
+    SURVEY 5.3); ``strict_compat=True`` only drops that handshake (the
+    reference's download framing), it does not change the payload codec;
+  * a failed or timed-out accept counts against the server's error budget and
+    the round carries on with the clients that did connect (the reference's
+    upload accept raises uncaught after 300 s, server.py:119,126);
   * server-side client ids follow the order uploads complete, and are logged.
 """
 from __future__ import annotations
@@ -172,7 +179,11 @@ class FedAvgServer:
         finally:
             conn.close()
 
-    def gather(self):
+    def gather(self, max_errors: int = 5):
+        """Accept up to N uploads; an accept that times out or fails counts against
+        ``max_errors`` (the reference's retry budget, server.py:92-112) instead of aborting the
+        round, so the clients that did connect are still aggregated / answered."""
+        errors = 0
         with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as srv:
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             srv.bind((self.host, self.port_receive))
@@ -180,13 +191,21 @@ class FedAvgServer:
             srv.settimeout(self.timeout)
             self.ready.set()
             threads = []
-            while len(threads) < self.n:
-                conn, addr = srv.accept()
+            while len(threads) < self.n and errors < max_errors:
+                try:
+                    conn, addr = srv.accept()
+                except OSError as e:  # socket.timeout is an OSError
+                    errors += 1
+                    if self.log:
+                        self.log.phase(f"[ERROR] accept failed ({errors}/{max_errors}): {e}")
+                    continue
                 t = threading.Thread(target=self._handle, args=(conn, addr, len(threads)))
                 t.start()
                 threads.append(t)
             for t in threads:
                 t.join()
+        if self.log and len(threads) < self.n:
+            self.log.phase(f"[ERROR] gave up after {errors} accept errors: {len(threads)}/{self.n} clients connected")
         return self.received
 
     def broadcast(self, state: Dict[str, torch.Tensor], max_errors: int = 5) -> int:
@@ -198,7 +217,13 @@ class FedAvgServer:
             srv.listen(self.n)
             srv.settimeout(self.timeout)
             while served < self.n and errors < max_errors:
-                conn, addr = srv.accept()
+                try:
+                    conn, addr = srv.accept()
+                except OSError as e:
+                    errors += 1
+                    if self.log:
+                        self.log.phase(f"[ERROR] accept failed ({errors}/{max_errors}): {e}")
+                    continue
                 try:
                     conn.settimeout(self.timeout)
                     if not self.strict:
@@ -218,6 +243,8 @@ class FedAvgServer:
                         self.log.phase(f"[ERROR] send to {addr}: {e}")
                 finally:
                     conn.close()
+        if self.log and served < self.n:
+            self.log.phase(f"[ERROR] served {served}/{self.n} clients before giving up ({errors} errors)")
         return served
 
     def run_round(self):

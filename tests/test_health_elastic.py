@@ -80,3 +80,32 @@ def test_elastic_restart_resumes_round(tmp_path):
         st = json.load(open(tmp_path / f"client{cid}_fed_state.json"))
         assert st["completed_rounds"] == 2
         assert [h["round"] for h in st["history"]] == [1, 2]
+
+
+def test_elastic_restart_after_fedavg_first_round(tmp_path):
+    """Client 2 dies in round 1 AFTER the FedAvg all-reduce, before it records the round
+    (ranks could then resume at different rounds, or from a client's LOCAL model).
+    The restarted group must agree on one resume round -- the round tag of the aggregate -- and
+    finish with every client holding the same final aggregate."""
+    import torch
+    env = dict(os.environ, FEDDDOS_KILL_CLIENT="1", FEDDDOS_KILL_ROUND="0", FEDDDOS_KILL_AT="post_fedavg",
+               PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", PKG, "launch", "--nproc", "2", "--port", str(_free_port()), "--max-restarts", "1",
+           "--out-dir", str(tmp_path), "--synthetic-rows", "600", "--max-len", "64", "--epochs", "1",
+           "--batch-size", "8", "--eval-batch-size", "32", "--rounds", "2", "--plots", "false", "--layers", "1",
+           "--heartbeat-s", "0.2", "--heartbeat-stale-s", "3"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=540)
+    log = out.stdout + out.stderr
+    assert out.returncode == 0, log[-3000:]
+    assert (tmp_path / ".killed_client1_round0_r0").exists()
+    assert "elastic restart #1" in log
+    assert json.load(open(tmp_path / "ddos_distilbert_model.json"))["round"] == 2
+    for cid in (1, 2):
+        st = json.load(open(tmp_path / f"client{cid}_fed_state.json"))
+        assert st["completed_rounds"] == 2
+        rounds = [h["round"] for h in st["history"]]
+        assert rounds[-1] == 2 and rounds == sorted(set(rounds))
+    g = torch.load(tmp_path / "ddos_distilbert_model.pth", weights_only=True)
+    for cid in (1, 2):
+        c = torch.load(tmp_path / f"client{cid}_model.pth", weights_only=True)
+        assert all(torch.equal(g[k], c[k]) for k in g)

@@ -95,3 +95,20 @@ def test_partial_participation_is_deterministic():
     a = faults.participants(3, 8, 0.5, seed=42)
     assert a == faults.participants(3, 8, 0.5, seed=42) and len(a) == 4
     assert faults.participants(0, 8, 1.0) == list(range(8))
+
+
+def test_server_gather_survives_missing_client():
+    """One of two clients never connects: accept timeouts count against the error budget and the
+    server returns the one upload it got (then aggregate() refuses the round, server.py:69-71),
+    instead of raising out of run_round."""
+    pr, ps = _ports(2)
+    srv = tp.FedAvgServer(2, "127.0.0.1", pr, ps, timeout=0.5)
+    res = {}
+    t = threading.Thread(target=lambda: res.setdefault("got", srv.gather(max_errors=2)))
+    t.start()
+    srv.ready.wait(5)
+    assert tp.send_model({"w": torch.ones(3)}, "127.0.0.1", pr, timeout=5)
+    t.join(20)
+    assert not t.is_alive()
+    assert len(res["got"]) == 1
+    assert srv.aggregate(res["got"]) is None
