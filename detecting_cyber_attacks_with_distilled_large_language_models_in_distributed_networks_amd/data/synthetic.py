@@ -66,14 +66,28 @@ DDOS_FRACTION = 0.57     # 2,586 / 4,515 test positives
 INF_FRACTION = 0.001     # 3 of 2,885 committed rows carry 'Infinity'
 
 
+HARD_OVERLAP = 0.04      # "hard" profile: irreducible label noise (~1.7 % of rows)
+HARD_LOOKALIKE = 0.30    # "hard" profile: BENIGN HTTP flows shaped like the flood
+
+
 def generate_cicids2017(n_rows: int = 225_745, seed: int = 0,
                         ddos_fraction: float = DDOS_FRACTION,
-                        overlap: float = 0.0004) -> pd.DataFrame:
+                        overlap: float = 0.0004, hard: bool = False) -> pd.DataFrame:
     """Return a DataFrame with CICIDS2017 columns (pandas-deduplicated names).
 
     ``overlap`` is the fraction of BENIGN rows drawn from the DDoS feature
     distribution (irreducible error; ~0.04 % -> accuracy ceiling ~99.98 %).
+
+    ``hard=True`` is a profile for numerics tests whose accuracy must land well
+    below 100 % so a loss curve carries information: overlap rises to
+    ``HARD_OVERLAP`` and ``HARD_LOOKALIKE`` of the remaining BENIGN rows become
+    port-80 flows with the flood's packet counts and small forward packets, told
+    apart only by a backward payload that is drawn from a wider range (and from
+    the flood's own payload values a third of the time).  The default profile's
+    rows are unchanged (the look-alikes are drawn from a separate RNG stream).
     """
+    if hard and overlap == 0.0004:
+        overlap = HARD_OVERLAP
     rng = np.random.default_rng(seed)
     n = int(n_rows)
     is_ddos = rng.random(n) < ddos_fraction
@@ -127,6 +141,10 @@ def generate_cicids2017(n_rows: int = 225_745, seed: int = 0,
     fwd_len[b], bwd_len[b] = flen, blen
     dur[b] = np.where(kind == 0, rng.integers(20, 200_000, nb),
                       np.exp(rng.uniform(np.log(3), np.log(1.2e8), nb)).astype(np.int64))
+
+    if hard:
+        _lookalikes(np.random.default_rng(seed + 1_000_003), b, port, dur, nfwd, nbwd, fwd_max, fwd_min,
+                    fwd_len, bwd_len, bwd_max, bwd_min)
 
     # Zero-duration flows -> Infinity rates (client1.py:87 handles them).
     zero = rng.random(n) < INF_FRACTION
@@ -206,6 +224,24 @@ def generate_cicids2017(n_rows: int = 225_745, seed: int = 0,
     names = dedup_columns(CICIDS2017_COLUMNS)
     assert set(names) == set(cols), set(names) ^ set(cols)
     return pd.DataFrame({k: cols[k] for k in names})
+
+
+def _lookalikes(rng, b, port, dur, nfwd, nbwd, fwd_max, fwd_min, fwd_len, bwd_len, bwd_max, bwd_min):
+    """Turn ``HARD_LOOKALIKE`` of the BENIGN rows ``b`` into flood-shaped HTTP flows (in place)."""
+    sel = b[rng.random(b.size) < HARD_LOOKALIKE]
+    m = sel.size
+    port[sel] = 80
+    dur[sel] = np.exp(rng.uniform(np.log(5e2), np.log(1.2e8), m)).astype(np.int64)
+    nfwd[sel] = rng.integers(1, 11, m)
+    nbwd[sel] = np.where(rng.random(m) < 0.2, 0, rng.integers(2, 9, m))
+    fwd_max[sel] = rng.choice(np.array([0, 6, 20, 31, 46]), m)
+    fwd_min[sel] = 0
+    fwd_len[sel] = np.minimum(fwd_max[sel] * rng.integers(1, 3, m), fwd_max[sel] * nfwd[sel])
+    pay = np.where(rng.random(m) < 1.0 / 3.0, rng.choice(np.array([11595, 11601, 11607, 5840, 7300]), m),
+                   rng.integers(2000, 14000, m))
+    bwd_len[sel] = np.where(nbwd[sel] > 0, pay, 0)
+    bwd_max[sel] = np.where(nbwd[sel] > 0, np.minimum(bwd_len[sel], 5840 + rng.integers(0, 2, m) * 1460), 0)
+    bwd_min[sel] = 0
 
 
 def write_csv(df: pd.DataFrame, path: str) -> None:
