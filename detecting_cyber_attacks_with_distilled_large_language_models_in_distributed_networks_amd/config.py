@@ -61,6 +61,7 @@ class FedConfig:
     # --- outputs ------------------------------------------------------------------------
     out_dir: str = "."
     plots: bool = True
+    plot_dpi: int = 0                       # 0: reference per-client DPI (client 1 default, client 2: 300)
     resume: bool = True                     # client1.py:375-377 loads clientN_model.pth
     save_optimizer: bool = False
     save_checkpoints: bool = True           # clientN_model.pth / ddos_distilbert_model.pth (bench: off)

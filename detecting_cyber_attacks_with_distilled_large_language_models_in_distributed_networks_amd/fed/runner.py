@@ -233,9 +233,10 @@ class FederatedClient:
             save_metrics(agg, os.path.join(cfg.out_dir, f"client{self.client_id}_aggregated_metrics{sfx}.csv"), log)
         if cfg.plots and self.writer:
             with self.timer("plot"):
-                from ..utils.plots import plot_evaluation
+                from ..utils.plots import plot_evaluation, reference_dpi
+                dpi = cfg.plot_dpi if cfg.plot_dpi > 0 else reference_dpi(self.client_id)
                 plot_evaluation(local, agg, os.path.join(cfg.out_dir, f"client{self.client_id}_plots"),
-                                f"Client {self.client_id}", log=log)
+                                f"Client {self.client_id}", dpi=dpi, log=log)
         if self.writer and cfg.save_checkpoints:
             ck.save_model(model, ck.client_ckpt_path(cfg.out_dir, self.client_id))
         rec = {"round": r + 1, "train": tr, "fedavg_ms": t_fed * 1e3, "participated": contributes,

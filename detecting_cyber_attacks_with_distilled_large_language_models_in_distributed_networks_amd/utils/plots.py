@@ -7,6 +7,14 @@ Accuracy/Precision/Recall/F1).  seaborn is not installed here, so the heatmap is
 an annotated ``imshow``.  The reference defines ROC / precision-recall plots but
 never calls them (client1.py:167-193); they are available via ``curves=True``.
 Titles follow the code (the committed PNGs have local/aggregated swapped).
+
+Artefact parity, stated plainly: the figure sizes, colours (``darkorange``/``navy``/
+``purple``; ``#1f77b4``/``#ff7f0e``), labels and axis limits below deliberately follow
+client1.py:157-218 call for call, because the three PNGs are part of the reference's
+observable output.  These are leaf matplotlib calls with no design freedom worth taking;
+everything upstream of them (metrics on device, one sync) is this framework's own.
+DPI: client 1 uses matplotlib's default, client 2 saves at ``dpi=300``
+(client2.py:155,171,183,207) -- ``reference_dpi(client_id)``.
 """
 from __future__ import annotations
 
@@ -97,6 +105,11 @@ def plot_metrics_comparison(local_metrics, aggregated_metrics, path: str, client
     fig.savefig(path, dpi=dpi)
     plt.close(fig)
     return path
+
+
+def reference_dpi(client_id: int) -> Optional[int]:
+    """The reference's per-client DPI: client1.py saves at the default, client2.py at 300."""
+    return None if int(client_id) == 1 else 300
 
 
 def plot_evaluation(local_metrics, aggregated_metrics=None, output_dir: str = "client1_plots",
