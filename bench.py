@@ -78,8 +78,9 @@ def _args(argv=None):
                     help="reduce each split-K weight gradient right after its GEMM instead of once per step (A/B)")
     ap.add_argument("--no-fuse-colsum", action="store_true",
                     help="separate column-sum pass for FFN lin1's bias gradient (A/B)")
-    ap.add_argument("--fused-adam", action="store_true",
-                    help="apply Adam inside the weight-gradient GEMM epilogues (A/B; measured no faster)")
+    ap.add_argument("--no-fused-adam", action="store_true",
+                    help="store the weight gradients and run Adam separately instead of applying it in the "
+                         "all-layer weight-gradient GEMM's epilogue (A/B)")
     ap.add_argument("--padded", action="store_true",
                     help="run the blocks on all B*S positions instead of the packed real tokens (A/B)")
     ap.add_argument("--wgrad-stream", action="store_true",
@@ -175,7 +176,7 @@ def main():
     model.fuse_colsum = not args.no_fuse_colsum
     ncomm = client.comm
     fedavg.broadcast_model(model, comm=ncomm)
-    opt = engine.ArenaAdam(model, lr=2e-5, fuse_dw=args.fused_adam)
+    opt = engine.ArenaAdam(model, lr=2e-5, fuse_dw=not args.no_fused_adam)
     gsync = None
     teacher = None
     if args.teacher:

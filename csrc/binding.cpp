@@ -28,6 +28,8 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
                 int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, int* tile_cnt,
                 long long ncnt, const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st);
 int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K);
+int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg,
+                     hipStream_t st);
 int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
                              const int* splits, const int* accumulate, hipStream_t st);
 int fd_transpose_batched(const void* const* srcs, void* const* dsts, const int* rows, const int* cols, int n,
@@ -276,6 +278,55 @@ int64_t gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C
                        adam.empty() ? nullptr : ad, defer ? 1 : 0, &splits, stream()),
            "gemm_dw2");
   return splits;  // > 0: slabs left in `workspace` (problem 0 then 1) for splitk_reduce_batched
+}
+
+// Every weight gradient of a backward in one launch (gemm.hip gemm_dw_batch_kernel):
+// Cs[i] (+)= As[i]^T Bs[i] (fp32), As[i] [K][M_i], Bs[i] [K][N_i] bf16 (one K for all).
+// adam: empty, or [p, m, v, shadow] per problem + the device step counter last (fused
+// optimizer step instead of storing the gradients; hp = [lr, b1, b2, eps, wd, decoupled]).
+void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tensor>& Bs,
+                   const std::vector<at::Tensor>& Cs, const std::vector<int64_t>& accumulate,
+                   const std::vector<at::Tensor>& adam, const std::vector<double>& hp, int64_t cfg) {
+  const size_t n = As.size();
+  TORCH_CHECK(n > 0 && n <= 32, "gemm_dw_batch: 1..32 problems, got ", n);
+  TORCH_CHECK(Bs.size() == n && Cs.size() == n && accumulate.size() == n, "gemm_dw_batch: ragged problem lists");
+  const int64_t K = As[0].size(0);
+  TORCH_CHECK(K > 0 && K % 64 == 0, "gemm_dw_batch: K (tokens) must be a positive multiple of 64, got ", K);
+  std::vector<const at::Tensor*> cs(n);
+  std::vector<FdDwProb> pr(n);
+  for (size_t i = 0; i < n; ++i) {
+    need(As[i], at::kBFloat16, "A");
+    need(Bs[i], at::kBFloat16, "B");
+    need(Cs[i], at::kFloat, "C");
+    TORCH_CHECK(As[i].dim() == 2 && Bs[i].dim() == 2 && Cs[i].dim() == 2, "gemm_dw_batch operands must be 2-D");
+    TORCH_CHECK(As[i].size(0) == K && Bs[i].size(0) == K, "gemm_dw_batch: every operand needs K = ", K, " rows");
+    TORCH_CHECK(Cs[i].size(0) == As[i].size(1) && Cs[i].size(1) == Bs[i].size(1), "gemm_dw_batch: C shape mismatch");
+    TORCH_CHECK(As[i].size(1) % 128 == 0 && Bs[i].size(1) % 64 == 0, "gemm_dw_batch: M % 128 and N % 64 required");
+    cs[i] = &Cs[i];
+    FdDwProb& q = pr[i];
+    q = FdDwProb{};
+    q.A = reinterpret_cast<const uint16_t*>(As[i].data_ptr());
+    q.B = reinterpret_cast<const uint16_t*>(Bs[i].data_ptr());
+    q.C = Cs[i].data_ptr<float>();
+    q.M = (int)As[i].size(1);
+    q.N = (int)Bs[i].size(1);
+    q.accumulate = accumulate[i] ? 1 : 0;
+  }
+  std::vector<FdAdamEpi> ad(n);
+  const int* step = nullptr;
+  float hyper[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (!adam.empty()) {
+    adam_descs(adam, hp, cs.data(), (int)n, ad.data());
+    for (size_t i = 0; i < n; ++i) {
+      TORCH_CHECK(!accumulate[i], "gemm_dw_batch: a fused Adam step cannot accumulate into a gradient");
+      pr[i].p = ad[i].p; pr[i].m = ad[i].m; pr[i].v = ad[i].v; pr[i].sh = ad[i].sh;
+    }
+    step = ad[0].step;
+    hyper[0] = ad[0].lr; hyper[1] = ad[0].b1; hyper[2] = ad[0].b2; hyper[3] = ad[0].eps; hyper[4] = ad[0].wd;
+    hyper[5] = (float)ad[0].decoupled;
+  }
+  check_rc(fd_gemm_dw_batch((int)n, pr.data(), (int)K, step, adam.empty() ? nullptr : hyper, (int)cfg, stream()),
+           "gemm_dw_batch");
 }
 
 // Finish deferred split-K weight gradients: out_i (+)= sum_z slabs_i[z] (z order), one launch.
@@ -793,6 +844,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_dw2", &gemm_dw2);
   m.def("gemm_dw", &gemm_dw);
+  m.def("gemm_dw_batch", &gemm_dw_batch, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("accumulate"),
+        py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1);
   m.def("gemm_colsum", &gemm_colsum, py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("aux"),
         py::arg("res"), py::arg("colsum"), py::arg("aux_out") = py::none());
   m.def("splitk_reduce_batched", &splitk_reduce_batched);

@@ -16,3 +16,19 @@ struct FdAdamEpi {
   float lr, b1, b2, eps, wd;
   int decoupled;      // AdamW-style decay
 };
+
+// One weight-gradient problem of the all-layer launch (gemm.hip gemm_dw_batch_kernel):
+// C[M][N] (+)= A^T B with A [K][M], B [K][N] bf16 (same K for every problem).  p != nullptr:
+// apply Adam to the finished gradient tile (state laid out like C) instead of storing it.
+struct FdDwProb {
+  const uint16_t* A;
+  const uint16_t* B;
+  float* C;
+  float* p;
+  float* m;
+  float* v;
+  uint16_t* sh;       // bf16 shadow (nullable)
+  int M, N;
+  int tile0;          // filled by the launcher
+  int accumulate;
+};

@@ -463,8 +463,14 @@ struct GemmGroup {
   int ntiles;     // tiles of both
 };
 
+#ifndef FD_GEMM_SCHED
+#define FD_GEMM_SCHED 1
+#endif
+
+// One output tile of problem p: the K loop over the LDS-DMA ring, then the epilogue.
+// bid = the tile's index within p (walked in group-M order), slot = split-K arrival slot.
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
-__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, GemmGroup grp) {
+DEV void gemm_tile(const GemmParams& p, int bid, int slot, char* smem) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   using OA = typename G::OA;
   using OB = typename G::OB;
@@ -475,21 +481,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
   constexpr int L = OA::PER_WAVE + OB::PER_WAVE;  // DMA ops per wave per K tile
   static_assert(S >= 2 && S <= 6, "ring depth");
   static_assert((S - 2) * L <= 63, "vmcnt is 6 bits");
-#ifndef FD_GEMM_SCHED
-#define FD_GEMM_SCHED 1
-#endif
   constexpr bool SCHED = FD_GEMM_SCHED;
-  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / WN, wc = wid % WN;
-
-  int bid = xcd_remap(blockIdx.x, grp.ntiles);
-  const int slot = bid;  // unique per tile of the (grouped) grid: split-K arrival counter
-  const bool second = bid >= grp.ntiles0;  // block-uniform
-  const GemmParams& p = second ? grp.q : p0;
-  if (second) bid -= grp.ntiles0;
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = p.N / BN;
   int tm, tn;
   tile_coords(bid, tiles_m, tiles_n, p.group_m, tm, tn);
@@ -580,6 +576,63 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
   // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
   __syncthreads();
   staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid, slot);
+}
+
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, GemmGroup grp) {
+  using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  int bid = xcd_remap(blockIdx.x, grp.ntiles);
+  const int slot = bid;  // unique per tile of the (grouped) grid: split-K arrival counter
+  const bool second = bid >= grp.ntiles0;  // block-uniform
+  const GemmParams& p = second ? grp.q : p0;
+  if (second) bid -= grp.ntiles0;
+  gemm_tile<BM, BN, AK, BKM, EPI, WM, WN, S>(p, bid, slot, smem);
+}
+
+// ---------------------------------------------------------------- all-layer weight gradients
+// Every weight gradient of a backward pass in ONE launch, at the end of the backward
+// (RunCtx.dw_batch, ops/functional.py): C_i[M_i][N_i] (+)= A_i^T B_i over the same token
+// dimension K, for up to DWB_MAXP problems (4 per transformer block).  The per-layer grouped
+// launches it replaces each fill the chip about once, so they need split-K (fp32 slabs + a
+// reduce) and, with Adam fused into the epilogue, every tile reaches the optimizer traffic
+// at the same moment (engine/optim.py: measured slower).  One launch over all layers has
+// ~20 rounds of 128x64 tiles: no split-K (each tile runs the full K loop -- deterministic, no
+// slabs), and tiles reach their epilogue -- plain store, or Adam (adam_epi4) -- staggered
+// while other tiles are on the MFMAs.  Problems are laid out back to back in the logical
+// tile order; after the XCD remap each XCD walks a contiguous range, i.e. 2-3 problems.
+constexpr int DWB_MAXP = 32;
+using DwProb = FdDwProb;  // adam_epi.h (shared with the host binding)
+struct DwBatch {
+  DwProb pr[DWB_MAXP];
+  int n, K, ntiles, group_m;
+  const int* step;
+  float lr, b1, b2, eps, wd;
+  int decoupled;
+};
+
+template <int BM, int BN, int WM, int WN, int S>
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch bt) {
+  using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S>;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  const int lid = xcd_remap(blockIdx.x, bt.ntiles);
+  int i = 0;
+  while (i + 1 < bt.n && lid >= bt.pr[i + 1].tile0) ++i;  // block-uniform
+  const DwProb& q = bt.pr[i];
+  GemmParams p{};
+  p.A = q.A; p.B = q.B; p.C = q.C;
+  p.M = q.M; p.N = q.N; p.K = bt.K;
+  p.lda = q.M; p.ldb = q.N; p.ldc = q.N;
+  p.k_split = bt.K;
+  p.group_m = bt.group_m;
+  p.out = q.C;
+  p.accumulate = q.accumulate;
+  if (q.p) {
+    p.adam.p = q.p; p.adam.m = q.m; p.adam.v = q.v; p.adam.sh = q.sh; p.adam.step = bt.step;
+    p.adam.lr = bt.lr; p.adam.b1 = bt.b1; p.adam.b2 = bt.b2; p.adam.eps = bt.eps; p.adam.wd = bt.wd;
+    p.adam.decoupled = bt.decoupled;
+  }
+  gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S>(p, lid - q.tile0, 0, smem);
 }
 
 // out[i] = (accumulate ? out[i] : 0) + sum_z slab[z][i]   (deterministic split-K reduce)
@@ -1011,6 +1064,69 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
   if (splits <= 0) return 6;
   return dw_launch(p, 2, id, splits, K, workspace, workspace_elems, accumulate, tile_cnt, ncnt, adams, defer,
                    splits_out, st);
+}
+
+// All-layer weight gradients in one launch (gemm_dw_batch_kernel).  probs[i] = {A, B, C, p, m,
+// v, sh, M, N, -, accumulate} (tile0 is filled here); adam != nullptr -> hyper-parameters of
+// the fused optimizer step for the problems with p != nullptr.  cfg < 0: FD_GEMM_DWB_CFG or
+// the default 128 x 64 (2 x 2 waves, 2-deep ring).  Returns 0, or nonzero on an unsupported
+// shape (nothing launched).
+bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
+  auto go = [&](auto kern, int bm, int bn, int threads) {
+    for (int i = 0; i < bt.n; ++i)
+      if (bt.pr[i].M % bm || bt.pr[i].N % bn) return false;
+    int t = 0;
+    for (int i = 0; i < bt.n; ++i) {
+      bt.pr[i].tile0 = t;
+      t += (bt.pr[i].M / bm) * (bt.pr[i].N / bn);
+    }
+    bt.ntiles = t;
+    if (!dry) hipLaunchKernelGGL(kern, dim3(t), dim3(threads), 0, st, bt);
+    return true;
+  };
+  switch (id) {
+    case 0: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 3>, 128, 64, 256);
+    case 1: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 2>, 128, 128, 256);
+    case 4: return go(gemm_dw_batch_kernel<256, 128, 4, 2, 3>, 256, 128, 512);
+    case 8: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 2>, 128, 64, 256);
+    case 10: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 3>, 128, 128, 256);
+    case 12: return go(gemm_dw_batch_kernel<256, 128, 4, 2, 2>, 256, 128, 512);
+    case 15: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 4>, 128, 64, 256);
+    case 21: return go(gemm_dw_batch_kernel<128, 128, 4, 2, 3>, 128, 128, 512);
+  }
+  return false;
+}
+
+int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const float* hyper, int cfg,
+                     hipStream_t st) {
+  if (n <= 0 || n > DWB_MAXP || K <= 0 || K % BKT) return 1;
+  DwBatch bt{};
+  bt.n = n;
+  bt.K = K;
+  for (int i = 0; i < n; ++i) {
+    bt.pr[i] = probs[i];
+    if (!probs[i].A || !probs[i].B || (!probs[i].C && !probs[i].p) || probs[i].M <= 0 || probs[i].N <= 0) return 2;
+    if (probs[i].p && (!probs[i].m || !probs[i].v || !step || !hyper)) return 3;
+  }
+  if (hyper) {
+    bt.step = step;
+    bt.lr = hyper[0]; bt.b1 = hyper[1]; bt.b2 = hyper[2]; bt.eps = hyper[3]; bt.wd = hyper[4];
+    bt.decoupled = hyper[5] != 0.f;
+  }
+  int id = cfg;
+  if (id < 0) {
+    static const int env = [] { const char* e = getenv("FD_GEMM_DWB_CFG"); return e ? atoi(e) : -1; }();
+    id = env >= 0 ? env : 8;
+  }
+  // Group height: A-panels of gm x BM rows x K (bf16) should take ~half of a 4 MiB L2.
+  const long long panel = 128ll * K * 2;
+  bt.group_m = (int)std::max(1ll, std::min(16ll, (2ll << 20) / panel));
+  if (!dwb_launch_cfg(id, bt, st, true)) {
+    id = 8;  // 128 x 64 fits every supported shape (M % 128, N % 64)
+    if (!dwb_launch_cfg(id, bt, st, true)) return 4;
+  }
+  dwb_launch_cfg(id, bt, st, false);
+  return 0;
 }
 
 // Reduce n deferred split-K weight gradients (slab layout of fd_gemm_dw2) in one launch.

@@ -20,7 +20,7 @@ Measured on MI355X (bs32 x seq128): overlap makes the step SLOWER (3.86 vs
 3.51 ms) -- the concurrent Adam blocks take CU slots from the one-round GEMM
 grids and HBM bandwidth from LayerNorm/colsum -- so it is off by default.
 
-Fused mode (``fuse_dw=True``; active inside a training step's
+Fused mode (``fuse_dw=True``, the default; active inside a training step's
 ``fused_adam_scope``): the encoder's 24 weight matrices (89 % of the dense
 parameters) are updated by the weight-gradient GEMMs themselves -- the epilogue
 applies Adam to the finished fp32 gradient tile (csrc/kernels/gemm.hip
@@ -30,12 +30,17 @@ while other tiles of the grid are still on the MFMAs.  ``step()`` then updates
 the rest (embeddings, biases, LayerNorms, head) in one launch over a run table.
 The W^T copies the backward's dX GEMMs read are taken before the step, so a
 block's later dX GEMMs still see the pre-update weights.  Bitwise identical to
-the unfused step (tests/test_fused_adam_gpu.py), but measured on MI355X at bs32 x
-seq128 it does not pay: the dW grids run as one round, so every tile reaches its
-Adam epilogue at the same time and the ~1.1 GB of optimizer traffic no longer
-overlaps anything (dW GEMMs +260 us vs Adam -180 us and the split-K reduces
--64 us; 2.39-2.42 vs 2.37-2.38 ms/step, profiles/r1_ab_fused_adam_fixup.txt).
-Off by default.
+the unfused step (tests/test_fused_adam_gpu.py, tests/test_dw_batch_gpu.py).
+
+With the per-layer grouped dW launches (round 1) it did not pay: each grid runs as
+one round, so every tile reached its Adam epilogue at the same time and the ~1.1 GB
+of optimizer traffic overlapped nothing (2.39-2.42 vs 2.37-2.38 ms/step,
+profiles/r1_ab_fused_adam_fixup.txt).  With all weight gradients of the step in ONE
+launch at the end of the backward (RunCtx.dw_batch: ~20 rounds of tiles, no split-K)
+the epilogues are staggered behind other tiles' MFMA work, and it does pay:
+2.034-2.039 (batched, unfused) vs 1.999-2.000 ms/step (batched + fused), against
+2.103 for the per-layer launches (profiles/r2_ab_dw_batch_fused_adam.txt).  On by
+default; ``fuse_dw=False`` for the unfused arm.
 """
 from __future__ import annotations
 
@@ -48,7 +53,7 @@ import torch
 class ArenaAdam:
     def __init__(self, model, lr: float = 2e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, decoupled: bool = False, overlap: bool = False,
-                 fuse_dw: bool = False):
+                 fuse_dw: bool = True):
         self.model = model
         self.overlap = overlap
         self.fuse_dw = fuse_dw

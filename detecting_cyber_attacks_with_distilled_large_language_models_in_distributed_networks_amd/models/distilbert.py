@@ -243,6 +243,9 @@ class DDoSClassifier(nn.Module):
         self._wgrad = None
         # HIP path: grouped weight-gradient GEMMs (RunCtx.group_dw)
         self.group_dw = True
+        # HIP path: every weight gradient of the step in one launch at the end of the backward
+        # (RunCtx.dw_batch; needs no per-block gradient hook / weight-gradient side stream)
+        self.batch_dw = os.environ.get("FD_BATCH_DW", "1") != "0"
         # HIP path: when the caller passes the batch's real-token count (DeviceLoader does,
         # from host-side lengths -- no sync), run the transformer blocks on the packed real
         # tokens only (~37 % of a seq128 CICIDS2017 batch is padding).  Rows are rounded up
@@ -451,6 +454,8 @@ class DDoSClassifier(nn.Module):
             rc.colsum_jobs = []  # (a per-block hook needs each block's grads final at once)
         if grad and self.defer_dw_reduce and self.layer_grads_hook is None:
             rc.dw_jobs = []
+        if grad and self.batch_dw and self.layer_grads_hook is None and not self.wgrad_stream:
+            rc.dw_batch = []
         rc.fuse_colsum = self.fuse_colsum
         rc.remat_gelu = self.remat_gelu
         if (grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None

@@ -67,6 +67,10 @@ class RunCtx:
     # optimizer whose Adam step the weight-gradient GEMMs apply in their epilogues
     # (engine/optim.py ArenaAdam.fused_args; set only inside a training step's scope)
     fused_adam: Optional[object] = None
+    # all-layer weight gradients: the blocks only record (dy, x, grad, accumulate) and the
+    # last backward node launches every weight gradient of the step as ONE grid
+    # (ops/kernels.py linear_dw_batch; with ``fused_adam`` the Adam step runs in its epilogue)
+    dw_batch: Optional[list] = None
 
 
 class _WGrad:
@@ -130,6 +134,11 @@ class EmbeddingFn(torch.autograd.Function):
             K.colsum_flush(ctx.rc.colsum_jobs)
         if ctx.rc.dw_jobs:
             K.dw_flush(ctx.rc.dw_jobs)
+        if ctx.rc.dw_batch:
+            fa = ctx.rc.fused_adam
+            acc_any = any(j[3] for j in ctx.rc.dw_batch)
+            K.linear_dw_batch(ctx.rc.dw_batch, adam=fa.fused_args if fa is not None and not acc_any else None)
+            ctx.rc.dw_batch.clear()
         return (None,) * 8
 
 
@@ -172,7 +181,8 @@ class LayerFn(torch.autograd.Function):
         wt = L.get("wT") or {}
         # Adam fused into the grouped dW epilogues: the weights are updated in the middle of
         # this backward, so every later reader must use the W^T copies taken before the step
-        fa = rc.fused_adam
+        batch = rc.dw_batch  # all-layer weight gradients: record now, one launch at the end
+        fa = rc.fused_adam if batch is None else None
         if fa is not None and (acc or not rc.group_dw or rc.wgrad is not None or wt.get("l1_w") is None
                                or wt.get("qkv_w") is None):
             fa = None
@@ -186,7 +196,9 @@ class LayerFn(torch.autograd.Function):
             g = g_out
         wg.fork(df, g, du, h)
         with wg.ctx():
-            if rc.group_dw:
+            if batch is not None:
+                batch += [(df, g, G["l2_w"].buf, acc), (du, h, G["l1_w"].buf, acc)]
+            elif rc.group_dw:
                 K.linear_dw2(df, g, G["l2_w"].buf, du, h, G["l1_w"].buf, acc,
                              adam=fa.fused_args([G["l2_w"].buf, G["l1_w"].buf]) if fa else None, jobs=rc.dw_jobs)
             else:
@@ -199,14 +211,16 @@ class LayerFn(torch.autograd.Function):
         dz1, _ = K.ln_bwd(dh, ao, x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf, G["o_b"].buf, rc.seed, 0,
                           0.0, acc, None, jobs)
         dcx = K.linear_dx(dz1, L["o_w"], wt=wt.get("o_w"))
-        if not rc.group_dw:
+        if not rc.group_dw and batch is None:
             wg.fork(dz1, cx)
             with wg.ctx():
                 K.linear_dw(dz1, cx, G["o_w"].buf, acc)
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu)
         wg.fork(dqkv, x, dz1, cx)
         with wg.ctx():
-            if rc.group_dw:
+            if batch is not None:
+                batch += [(dz1, cx, G["o_w"].buf, acc), (dqkv, x, G["qkv_w"].buf, acc)]
+            elif rc.group_dw:
                 K.linear_dw2(dz1, cx, G["o_w"].buf, dqkv, x, G["qkv_w"].buf, acc,
                              adam=fa.fused_args([G["o_w"].buf, G["qkv_w"].buf]) if fa else None, jobs=rc.dw_jobs)
             else:

@@ -154,6 +154,23 @@ def linear_dw2(dy0: torch.Tensor, x0: torch.Tensor, out0: torch.Tensor, dy1: tor
         jobs.append((ws[s0:s0 + splits * out1.numel()], out1, splits, accumulate))
 
 
+DW_BATCH_MAX = 32  # problems per all-layer weight-gradient launch (csrc/kernels/gemm.hip DWB_MAXP)
+
+
+def linear_dw_batch(jobs: list, adam=None, cfg: int = -1):
+    """Every weight gradient of a backward in one launch per 32 problems: for each job
+    (dy [K, M], x [K, N], out [M, N] fp32, accumulate) out (+)= dy^T x.  No split-K: each
+    output tile runs the whole token dimension (deterministic, no slabs, no reduce).
+    adam: a callable grads -> (state, hyper) (``ArenaAdam.fused_args``): apply the optimizer
+    step to each finished gradient tile instead of storing it."""
+    for i in range(0, len(jobs), DW_BATCH_MAX):
+        chunk = jobs[i:i + DW_BATCH_MAX]
+        outs = [j[2] for j in chunk]
+        st, hp = adam(outs) if adam is not None else ([], [])
+        ext().gemm_dw_batch([j[0] for j in chunk], [j[1] for j in chunk], outs, [int(j[3]) for j in chunk],
+                            st, hp, cfg)
+
+
 def dw_flush(jobs: list):
     """Reduce every deferred split-K weight gradient in one launch."""
     if jobs:

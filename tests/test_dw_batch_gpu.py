@@ -1,0 +1,101 @@
+"""All-layer weight gradients in one launch (csrc/kernels/gemm.hip gemm_dw_batch_kernel).
+
+* kernel: every problem of a batch == the fp32 product dy^T x (accumulate too), for the
+  DistilBERT shapes of a packed bs32 step and for several tile configurations;
+* model: the batched backward gives the per-layer (grouped, split-K) gradients up to fp32
+  summation order, and Adam fused into the batched epilogue reproduces gradient-then-Adam bit
+  for bit (training steps, eager and graph-replayed).
+"""
+import pytest
+import torch
+
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.engine import (
+    ArenaAdam, GraphedTrainStep, make_step_fn)
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.models import (
+    DDoSClassifier, DistilBertConfig)
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _frel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 4, 10, 12, 15, 21])
+def test_dw_batch_kernel_matches_fp32(cfg):
+    g = torch.Generator(device="cuda").manual_seed(cfg + 5)
+    T = 2688
+    shapes = [(768, 3072), (3072, 768), (768, 768), (2304, 768)] * 2
+    jobs, refs = [], []
+    for i, (M, N) in enumerate(shapes):
+        dy = (torch.randn(T, M, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+        x = torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16)
+        acc = i % 3 == 2
+        out = torch.randn(M, N, device="cuda", generator=g) if acc else torch.empty(M, N, device="cuda")
+        ref = dy.float().t() @ x.float() + (out.clone() if acc else 0.0)
+        jobs.append((dy, x, out, acc))
+        refs.append(ref)
+    K.linear_dw_batch(jobs, cfg=cfg)
+    torch.cuda.synchronize()
+    for (_, _, out, _), ref in zip(jobs, refs):
+        assert _frel(out, ref) < 1e-5, _frel(out, ref)
+
+
+def _batch(B, S, seed=0):
+    gen = torch.Generator().manual_seed(seed)
+    ids = torch.randint(1000, 2000, (B, S), generator=gen)
+    lens = torch.randint(S // 3, S + 1, (B,), generator=gen)
+    mask = (torch.arange(S)[None] < lens[:, None]).long()
+    ids = ids * mask
+    ids[:, 0] = 101
+    labels = torch.randint(0, 2, (B,), generator=gen)
+    return ids.cuda(), mask.cuda(), labels.cuda(), int(lens.sum())
+
+
+def test_batched_backward_matches_per_layer():
+    cfg = DistilBertConfig(n_layers=3)
+    grads = []
+    for batch in (True, False):
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=17)
+        m.batch_dw = batch
+        m.train()
+        ids, mask, labels, tokens = _batch(32, 128, seed=400)
+        for acc_step in range(2):  # the second backward accumulates into the gradients
+            if acc_step == 0:
+                m.zero_grad()
+            m.rng.fill_(acc_step)
+            loss, _ = m.forward_loss(ids, mask, labels, tokens=tokens)
+            loss.backward()
+        torch.cuda.synchronize()
+        grads.append({k: m.dense_grad(k).clone() for k in m.state_dict()})
+    for k in grads[0]:
+        if grads[1][k].norm() > 0:
+            assert _frel(grads[0][k], grads[1][k]) < 1e-4, k
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_adam_in_batched_dw_matches_unfused(graph):
+    cfg = DistilBertConfig(n_layers=2)
+    models, opts, steps = [], [], []
+    for fuse in (True, False):
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=19)
+        m.batch_dw = True
+        m.train()
+        opt = ArenaAdam(m, lr=1e-3, fuse_dw=fuse)
+        assert opt.can_fuse() == fuse
+        models.append(m)
+        opts.append(opt)
+        steps.append(GraphedTrainStep(make_step_fn(m, opt), warmup=1, enabled=graph, bucket=m.packed_rows))
+    for it in range(5):
+        ids, mask, labels, tokens = _batch(16, 128, seed=500 + it)
+        for st in steps:
+            st(ids, mask, labels, tokens)
+    torch.cuda.synchronize()
+    a, b = models[0].arena, models[1].arena
+    assert opts[0]._done == []
+    assert torch.equal(a.master, b.master)
+    assert torch.equal(opts[0].m, opts[1].m) and torch.equal(opts[0].v, opts[1].v)
+    assert torch.equal(a.shadow, b.shadow)
+    if graph:
+        assert all(st.graph is not None and st.failed is None for st in steps)

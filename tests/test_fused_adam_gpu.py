@@ -48,6 +48,7 @@ def test_fused_adam_training_matches_unfused(graph, fixup):
     models, opts, steps = [], [], []
     for fuse in (True, False):
         m = DDoSClassifier(config=cfg, device=DEV, impl="hip", seed=13)
+        m.batch_dw = False  # per-layer grouped dW with the split-K fixup (batched: test_dw_batch_gpu.py)
         m.train()
         opt = ArenaAdam(m, lr=1e-3, fuse_dw=fuse)
         assert opt.can_fuse() == fuse

@@ -156,7 +156,8 @@ def test_attention_skips_padded_key_tiles():
     assert torch.count_nonzero(dk) == 0
 
 
-@pytest.mark.parametrize("B,S,p", [(2, 128, 0.0), (3, 128, 0.1), (2, 256, 0.1), (1, 64, 0.0)])
+@pytest.mark.parametrize("B,S,p", [(2, 128, 0.0), (3, 128, 0.1), (2, 256, 0.1), (1, 64, 0.0), (2, 512, 0.1),
+                                   (1, 512, 0.0)])
 def test_attention_fwd(B, S, p):
     H = 12
     qkv = bf(B * S, 3 * H * 64, seed=14)
@@ -168,7 +169,7 @@ def test_attention_fwd(B, S, p):
     assert (lse - rlse).abs().max().item() < 1e-3
 
 
-@pytest.mark.parametrize("B,S,p", [(2, 128, 0.0), (2, 128, 0.1), (1, 256, 0.1)])
+@pytest.mark.parametrize("B,S,p", [(2, 128, 0.0), (2, 128, 0.1), (1, 256, 0.1), (2, 512, 0.1), (1, 512, 0.0)])
 def test_attention_bwd(B, S, p):
     H = 12
     qkv = bf(B * S, 3 * H * 64, seed=15)

@@ -131,6 +131,7 @@ def test_overlapped_adam_matches_single_pass(graph):
     for overlap in (True, False):
         m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=5)
         m.fuse_colsum = False  # (a per-block hook disables the deferred sums it needs)
+        m.batch_dw = False     # (... and the all-layer weight-gradient launch)
         m.train()
         opt = ArenaAdam(m, lr=1e-3, overlap=overlap, fuse_dw=False)
         assert (m.layer_grads_hook is not None) == overlap
@@ -180,6 +181,7 @@ def test_wgrad_side_stream_matches_serial(graph):
     for side in (True, False):
         m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=11)
         m.wgrad_stream = side
+        m.batch_dw = False  # (the side stream runs the per-layer weight-gradient launches)
         m.fuse_colsum = False  # (not combined with the side stream)
         m.train()
         models.append(m)
@@ -229,6 +231,7 @@ def test_deferred_dw_reduce_matches_immediate(tokens):
     grads = []
     for defer in (True, False):
         m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=12)
+        m.batch_dw = False  # the per-layer grouped launches are the path under test
         m.defer_dw_reduce = defer
         m.train()
         ids, mask, labels = _batch(16, 128, seed=301)

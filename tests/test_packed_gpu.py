@@ -32,11 +32,15 @@ def rel(a, b):
     return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-8)).item()
 
 
-@pytest.mark.parametrize("S", [128, 256])  # one-block-per-(b,h) kernels (S <= 128) and the 64-row tiles
+_LENS = {128: [128, 77, 64, 1, 100, 65, 17, 16], 256: [256, 77, 129, 1, 200, 65, 33, 192],
+         512: [512, 300, 129, 1, 450, 65, 511, 257]}
+
+
+@pytest.mark.parametrize("S", [128, 256, 512])  # one-block-per-(b,h) kernels (S <= 128) and the 64-row tiles
 def test_varlen_attention_matches_padded(S):
-    B, H = 6, 12
+    B, H = 8, 12
     g = torch.Generator(device="cuda").manual_seed(1)
-    lens = torch.tensor([S, 77, 64, 1, 100, 65]) if S == 128 else torch.tensor([256, 77, 129, 1, 200, 65])
+    lens = torch.tensor(_LENS[S])
     qkv_pad = (torch.randn(B * S, 3 * H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
     mask = (torch.arange(S)[None] < lens[:, None]).cuda()
     kb = K.mask_bias(mask.to(torch.int64))
@@ -132,3 +136,34 @@ def test_pack_kernel_matches_torch(B, S):
     # a row budget smaller than the real tokens never writes past it
     small_map, _, _ = K.pack(mask, ids, 64)
     assert torch.equal(small_map.long(), ref_map[:64])
+
+
+@pytest.mark.parametrize("S", [256, 512])
+def test_long_sequence_model_hip_vs_torch(S):
+    """the model at S = 256 / 512 (DistilBERT's position table caps S at 512),
+    padded and packed HIP paths against the fp32 torch path, dropout on with identical masks."""
+    cfg = DistilBertConfig(n_layers=2)
+    hip = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=6)
+    ref = DDoSClassifier(config=cfg, device="cuda", impl="torch", seed=6)
+    ids, mask, labels, tokens = _batch(4, S, S // 3, S, seed=S)
+    hip.train()
+    ref.train()
+    ref.rng.zero_() if hasattr(ref, "rng") else None
+    ref.torch_counter = 0
+    ref.zero_grad()
+    lr_, zr = ref.forward_loss(ids, mask, labels)
+    lr_.backward()
+    g_ref = ref.arena.grad.clone()
+    for tok in (None, tokens):
+        hip.rng.zero_()
+        hip.zero_grad()
+        lh, zh = hip.forward_loss(ids, mask, labels, tokens=tok)
+        lh.backward()
+        torch.cuda.synchronize()
+        assert rel(zh, zr) < 3e-2, (tok, rel(zh, zr))
+        for name in ("distilbert.transformer.layer.0.attention.q_lin.weight",
+                     "distilbert.transformer.layer.1.ffn.lin2.weight", "classifier.weight",
+                     "distilbert.embeddings.position_embeddings.weight"):
+            a, b = hip.dense_grad(name), ref.arena.gview(name)
+            err = ((a - b).norm() / b.norm()).item()
+            assert err < 3e-2, (tok, name, err)
