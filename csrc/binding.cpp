@@ -74,7 +74,8 @@ int fd_colsum_batched(int n, const float* const* parts, float* const* outs, cons
 int fd_rank_sort(const void* ids, int ids64, int T, long long* sorted, long long* perm, hipStream_t st);
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
-                float* logits, float* loss, float* dlogits, float* row_loss, const int* cls, int T, hipStream_t st);
+                float* logits, float* loss, float* dlogits, float* row_loss, const int* cls, int T,
+                const float* tlogits, float kd_T, float kd_alpha, hipStream_t st);
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
                 int accumulate, const int* cls, int T, const float* gscale, hipStream_t st);
@@ -700,8 +701,13 @@ void colsum_batched(const std::vector<at::Tensor>& parts, const std::vector<std:
 void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& W, const at::Tensor& bias,
               const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& labels,
               const at::Tensor& logits, const c10::optional<at::Tensor>& loss, const c10::optional<at::Tensor>& dlogits,
-              const c10::optional<at::Tensor>& row_loss, const c10::optional<at::Tensor>& cls) {
+              const c10::optional<at::Tensor>& row_loss, const c10::optional<at::Tensor>& cls,
+              const c10::optional<at::Tensor>& tlogits, double kd_T, double kd_alpha) {
   need_opt(row_loss, at::kFloat, "row_loss");
+  need_opt(tlogits, at::kFloat, "teacher logits");
+  if (tlogits.has_value() && tlogits->defined())
+    TORCH_CHECK(tlogits->numel() == 2 * B && labels.has_value() && labels->defined() && kd_T > 0.0,
+                "head_fwd: distillation needs teacher logits [B, 2], labels and a temperature > 0");
   need_opt(cls, at::kInt, "cls");
   need(hidden, at::kBFloat16, "hidden");
   need(W, at::kFloat, "W");
@@ -722,7 +728,8 @@ void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
   check_rc(fd_head_fwd(hidden.data_ptr(), (int)B, (int)S, (int)D, W.data_ptr<float>(), bias.data_ptr<float>(),
                        seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale,
                        ptr<const long long>(labels), logits.data_ptr<float>(), ptr<float>(loss), ptr<float>(dlogits),
-                       ptr<float>(row_loss), ptr<int>(cls), (int)(hidden.numel() / D), stream()),
+                       ptr<float>(row_loss), ptr<int>(cls), (int)(hidden.numel() / D), ptr<const float>(tlogits),
+                       (float)kd_T, (float)kd_alpha, stream()),
            "head_fwd");
 }
 
@@ -872,7 +879,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum_bf16", &colsum_bf16);
   m.def("colsum_batched", &colsum_batched);
   m.def("rank_sort", &rank_sort);
-  m.def("head_fwd", &head_fwd);
+  m.def("head_fwd", &head_fwd, py::arg("hidden"), py::arg("B"), py::arg("S"), py::arg("W"), py::arg("bias"),
+        py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("labels"), py::arg("logits"),
+        py::arg("loss"), py::arg("dlogits"), py::arg("row_loss"), py::arg("cls"), py::arg("tlogits") = py::none(),
+        py::arg("kd_T") = 1.0, py::arg("kd_alpha") = 1.0);
   m.def("head_bwd", &head_bwd);
   m.def("eval_metrics", &eval_metrics);
   m.def("adam", &adam);

@@ -43,6 +43,10 @@ struct HeadArgs {
   // padded layout, row b*S); rows are clamped to T-1
   const int* cls;
   int T;
+  // knowledge distillation (nullable): teacher logits [B, 2]; the row loss becomes
+  // kd_alpha * CE(z, y) + (1 - kd_alpha) * T^2 * KL(softmax(t / T) || softmax(z / T))
+  const float* tlogits;
+  float kd_T, kd_alpha;
 };
 
 DEV size_t cls_row(const HeadArgs& a, int b) {
@@ -80,10 +84,29 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
       const float mx = fmaxf(z0, z1);
       const float lse = mx + __logf(__expf(z0 - mx) + __expf(z1 - mx));
       const int y = (int)a.labels[b];
-      a.row_loss[b] = lse - (y ? z1 : z0);
       const float p1 = __expf(z1 - lse), p0 = __expf(z0 - lse);
-      a.dlogits[2 * b] = (p0 - (y == 0)) / a.B;
-      a.dlogits[2 * b + 1] = (p1 - (y == 1)) / a.B;
+      float loss = lse - (y ? z1 : z0);
+      float d0 = p0 - (y == 0), d1 = p1 - (y == 1);
+      if (a.tlogits) {
+        // soft term at temperature T (2 classes): log-softmax of z / T and t / T
+        const float iT = 1.f / a.kd_T;
+        const float s0 = z0 * iT, s1 = z1 * iT, t0 = a.tlogits[2 * b] * iT, t1 = a.tlogits[2 * b + 1] * iT;
+        const float ms = fmaxf(s0, s1), mt = fmaxf(t0, t1);
+        const float ls = ms + __logf(__expf(s0 - ms) + __expf(s1 - ms));
+        const float lt = mt + __logf(__expf(t0 - mt) + __expf(t1 - mt));
+        const float lq0 = s0 - ls, lq1 = s1 - ls;   // student log-probs
+        const float lp0 = t0 - lt, lp1 = t1 - lt;   // teacher log-probs
+        const float pt0 = __expf(lp0), pt1 = __expf(lp1);
+        const float kl = pt0 * (lp0 - lq0) + pt1 * (lp1 - lq1);
+        const float al = a.kd_alpha, T2 = a.kd_T * a.kd_T;
+        loss = al * loss + (1.f - al) * T2 * kl;
+        // d/dz of T^2 KL(p_t || softmax(z / T)) = T (q - p_t)
+        d0 = al * d0 + (1.f - al) * a.kd_T * (__expf(lq0) - pt0);
+        d1 = al * d1 + (1.f - al) * a.kd_T * (__expf(lq1) - pt1);
+      }
+      a.row_loss[b] = loss;
+      a.dlogits[2 * b] = d0 / a.B;
+      a.dlogits[2 * b + 1] = d1 / a.B;
     }
   }
 }
@@ -341,9 +364,12 @@ extern "C" {
 
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
-                float* logits, float* loss, float* dlogits, float* row_loss, const int* cls, int T, hipStream_t st) {
+                float* logits, float* loss, float* dlogits, float* row_loss, const int* cls, int T,
+                const float* tlogits, float kd_T, float kd_alpha, hipStream_t st) {
   if (B > 65536) return 1;
+  if (tlogits && (!labels || !(kd_T > 0.f))) return 3;
   HeadArgs a{};
+  a.tlogits = tlogits; a.kd_T = kd_T; a.kd_alpha = kd_alpha;
   a.cls = cls; a.T = T;
   a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W; a.bias = bias;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.labels = labels;

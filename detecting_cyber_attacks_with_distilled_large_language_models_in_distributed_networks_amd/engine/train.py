@@ -78,18 +78,17 @@ def make_step_fn(model, optimizer, criterion=None):
 
 
 def make_kd_step_fn(student, teacher, optimizer, temperature: float = 2.0, alpha: float = 0.5):
-    """Distillation step: frozen teacher forward (no grad, eval) -> student forward ->
-    alpha * CE + (1 - alpha) * T^2 * KL(teacher || student) -> backward -> Adam."""
-    from ..models.bert import kd_loss
+    """Distillation step: frozen teacher forward (no grad, eval) -> student forward with the
+    distillation loss alpha * CE + (1 - alpha) * T^2 * KL(teacher || student) fused into the
+    head kernel (HIP path; eager ``kd_loss`` on the torch path) -> backward -> Adam."""
 
     def step(ids, mask, labels, tokens=None):
         optimizer.zero_grad()
         with torch.no_grad():
             t_logits = teacher(ids, mask, tokens=tokens)
         with fused_adam_scope(student, optimizer):
-            s_logits = student(ids, mask, tokens=tokens)
-            loss = kd_loss(s_logits, t_logits, labels, temperature, alpha)
-            loss.backward()
+            loss, _ = student.forward_loss(ids, mask, labels, tokens=tokens, kd=(t_logits, temperature, alpha))
+            loss.backward(_one(loss.device) if loss.dtype == torch.float32 and loss.dim() == 0 else None)
         optimizer.step()
         return loss.detach()
 

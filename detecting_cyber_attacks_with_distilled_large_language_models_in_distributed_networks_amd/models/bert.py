@@ -9,7 +9,8 @@ Architecture = the DistilBERT block stack with BERT-base hyper-parameters
 (12 x [post-LN MHSA(12 heads) + GELU FFN 3072], hidden 768) plus BERT's
 token-type embedding, so every hot op runs on the same gfx950 kernels (the
 type-0 row is folded into the position table each forward: token_type_ids are
-all zero for single-sentence classification).  Parameters live in their own
+all zero for single-sentence classification; the table is an arena parameter and
+trains on the HIP path through the position gradient).  Parameters live in their own
 arena under the ``bert.`` prefix; ``load_hf_bert`` maps HuggingFace
 ``BertForSequenceClassification`` keys when a checkpoint is available offline.
 """
@@ -32,68 +33,37 @@ def bert_base_config(**kw) -> DistilBertConfig:
 
 
 class BertTeacherClassifier(DDoSClassifier):
-    """12-layer BERT-base + Dropout + Linear(768, 2) on the shared kernel path."""
+    """12-layer BERT-base + Dropout + Linear(768, 2) on the shared kernel path.
+
+    The token-type table lives in the parameter arena (``TOKEN_TYPES = 2``), so the
+    optimizer, FedAvg and checkpoints treat it like every other parameter; with
+    token_type_ids all 0 its row 0 is folded into the position table the kernels read and
+    its gradient is the column sum of the position gradient (ops/functional.py
+    EmbeddingFn) -- it trains on the HIP path too."""
 
     PREFIX = "bert."
+    TOKEN_TYPES = 2
 
     def __init__(self, local_model_path: Optional[str] = None, config: Optional[DistilBertConfig] = None,
                  device=None, impl: str = "auto", seed: int = 1, head_dropout: float = 0.1):
         cfg = config or bert_base_config()
         super().__init__(None, config=cfg, device="cpu", impl=impl, seed=seed, head_dropout=head_dropout)
-        # token-type table (2 x 768) kept outside the encoder arena (tiny, fp32)
-        g = torch.Generator().manual_seed(seed + 7)
-        self.token_type_embeddings = nn.Parameter(torch.randn(2, cfg.dim, generator=g) * cfg.initializer_range)
         if local_model_path and os.path.isdir(local_model_path):
             load_hf_bert(self, local_model_path)
         self.to(device or "cpu")
-
-    def _apply(self, fn, recurse=True):
-        out = super()._apply(fn, recurse)
-        if hasattr(self, "token_type_embeddings"):
-            self.token_type_embeddings.data = fn(self.token_type_embeddings.data)
-        return out
 
     def state_dict(self, *args, **kwargs):
         sd = super().state_dict(*args, **kwargs)
         out = type(sd)()
         for k, v in sd.items():
-            if k == "token_type_embeddings":
-                k = "distilbert.embeddings.token_type_embeddings.weight"
-            nk = self.PREFIX + k[len("distilbert."):] if k.startswith("distilbert.") else k
-            out[nk] = v
+            out[self.PREFIX + k[len("distilbert."):] if k.startswith("distilbert.") else k] = v
         return out
 
     def load_state_dict(self, sd, strict: bool = True, assign: bool = False):
         mapped = type(sd)() if hasattr(sd, "keys") else {}
         for k, v in sd.items():
-            nk = "distilbert." + k[len(self.PREFIX):] if k.startswith(self.PREFIX) else k
-            if nk == "distilbert.embeddings.token_type_embeddings.weight":
-                nk = "token_type_embeddings"
-            mapped[nk] = v
+            mapped["distilbert." + k[len(self.PREFIX):] if k.startswith(self.PREFIX) else k] = v
         return super().load_state_dict(mapped, strict=strict, assign=assign)
-
-    # position table with the type-0 row folded in (token_type_ids == 0)
-    def _hip_handles(self):
-        emb, layers, head = super()._hip_handles()
-        pos32 = self.arena.view("distilbert.embeddings.position_embeddings.weight")
-        emb = dict(emb)
-        emb["pos"] = (pos32 + self.token_type_embeddings[0].detach()).to(torch.bfloat16).contiguous()
-        return emb, layers, head
-
-    def _run_hip(self, ids, mask, labels, tokens=None):
-        self._hip_cache = None  # the folded table follows the (possibly updated) weights
-        return super()._run_hip(ids, mask, labels, tokens)
-
-    def _run_torch(self, ids, mask, labels):
-        with torch.no_grad():
-            pos = self.distilbert.embeddings.position_embeddings.weight
-            saved = pos.detach().clone()
-            pos.add_(self.token_type_embeddings[0].detach())
-        try:
-            return super()._run_torch(ids, mask, labels)
-        finally:
-            with torch.no_grad():
-                pos.copy_(saved)
 
 
 _HF_LAYER_MAP = {
@@ -121,10 +91,6 @@ def load_hf_bert(model: BertTeacherClassifier, path: str) -> int:
         k2 = k.removeprefix("bert.")
         tgt = None
         if k2.startswith("embeddings."):
-            if "token_type_embeddings" in k2:
-                model.token_type_embeddings.data.copy_(v.float())
-                n += 1
-                continue
             tgt = "distilbert." + k2
         elif k2.startswith("encoder.layer."):
             parts = k2.split(".")

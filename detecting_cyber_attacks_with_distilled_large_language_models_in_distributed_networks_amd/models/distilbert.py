@@ -80,12 +80,15 @@ _ARENA_LAYER_ORDER = [
 ]
 
 
-def encoder_specs(cfg: DistilBertConfig, prefix: str) -> List[Tuple[str, Tuple[int, ...]]]:
+def encoder_specs(cfg: DistilBertConfig, prefix: str, token_types: int = 0) -> List[Tuple[str, Tuple[int, ...]]]:
+    """token_types > 0: a BERT token-type table after the position table (models/bert.py)."""
     D = cfg.dim
     specs = [(f"{prefix}embeddings.word_embeddings.weight", (cfg.vocab_size, D)),
-             (f"{prefix}embeddings.position_embeddings.weight", (cfg.max_position_embeddings, D)),
-             (f"{prefix}embeddings.LayerNorm.weight", (D,)),
-             (f"{prefix}embeddings.LayerNorm.bias", (D,))]
+             (f"{prefix}embeddings.position_embeddings.weight", (cfg.max_position_embeddings, D))]
+    if token_types:
+        specs.append((f"{prefix}embeddings.token_type_embeddings.weight", (token_types, D)))
+    specs += [(f"{prefix}embeddings.LayerNorm.weight", (D,)),
+              (f"{prefix}embeddings.LayerNorm.bias", (D,))]
     shapes = _layer_shapes(cfg)
     for i in range(cfg.n_layers):
         for k in _ARENA_LAYER_ORDER:
@@ -116,6 +119,8 @@ class _Embeddings(nn.Module):
         super().__init__()
         self.word_embeddings = _P(arena, prefix + "word_embeddings.", ("weight",))
         self.position_embeddings = _P(arena, prefix + "position_embeddings.", ("weight",))
+        if prefix + "token_type_embeddings.weight" in arena.offsets:  # BERT teacher (HF registration order)
+            self.token_type_embeddings = _P(arena, prefix + "token_type_embeddings.", ("weight",))
         self.LayerNorm = _P(arena, prefix + "LayerNorm.")
         self.dropout = nn.Dropout(cfg.dropout)
 
@@ -207,13 +212,16 @@ def load_hf_weights(arena: ParamArena, prefix: str, path: str) -> int:
 class DDoSClassifier(nn.Module):
     """DistilBERT + Dropout(0.3) + Linear(768, 2) (client1.py:53-65)."""
 
+    TOKEN_TYPES = 0  # DistilBERT has no token-type embeddings (the BERT teacher: 2)
+
     def __init__(self, local_model_path: Optional[str] = None, config: Optional[DistilBertConfig] = None,
                  device=None, impl: str = "auto", seed: int = 0, head_dropout: float = 0.3):
         super().__init__()
         cfg = config or DistilBertConfig()
         self.config = cfg
         device = torch.device(device) if device is not None else torch.device("cpu")
-        specs = encoder_specs(cfg, "distilbert.") + [("classifier.weight", (2, cfg.dim)), ("classifier.bias", (2,))]
+        specs = encoder_specs(cfg, "distilbert.", self.TOKEN_TYPES) + [("classifier.weight", (2, cfg.dim)),
+                                                                        ("classifier.bias", (2,))]
         self.arena = ParamArena(specs, device="cpu", with_shadow=False)
         gen = torch.Generator().manual_seed(seed)
         init_encoder_(self.arena, "distilbert.", cfg, gen)
@@ -363,9 +371,17 @@ class DDoSClassifier(nn.Module):
         from ..ops.functional import GradSink
         A = self.arena
         pre = "distilbert."
+        tt_name = pre + "embeddings.token_type_embeddings.weight"
+        if tt_name in A.offsets:
+            # BERT teacher, token_type_ids all 0: type row 0 folded into the position table the
+            # kernels read (refreshed every forward, _run_hip); its gradient is the column sum
+            # of the position gradient (EmbeddingFn)
+            pos_tab = torch.empty_like(A.sview(pre + "embeddings.position_embeddings.weight"))
+        else:
+            pos_tab = A.sview(pre + "embeddings.position_embeddings.weight")
         emb = {
             "word": A.sview(pre + "embeddings.word_embeddings.weight"),
-            "pos": A.sview(pre + "embeddings.position_embeddings.weight"),
+            "pos": pos_tab,
             "ln_w": A.view(pre + "embeddings.LayerNorm.weight"),
             "ln_b": A.view(pre + "embeddings.LayerNorm.bias"),
             "sinks": {
@@ -376,6 +392,8 @@ class DDoSClassifier(nn.Module):
                 "flags": (self.emb_now, self.emb_ever) if self.sparse_word_grad else None,
             },
         }
+        if tt_name in A.offsets:
+            emb["sinks"]["type"] = GradSink(A, tt_name)
         layers = []
         for i in range(self.config.n_layers):
             lp = f"{pre}transformer.layer.{i}."
@@ -410,25 +428,31 @@ class DDoSClassifier(nn.Module):
         return self._run(input_ids, attention_mask, None, tokens)[1]
 
     def forward_loss(self, input_ids, attention_mask, labels,
-                     tokens: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                     tokens: Optional[int] = None, kd=None) -> Tuple[torch.Tensor, torch.Tensor]:
         """(mean CE loss, logits) with the head and the loss fused (one kernel).
 
         tokens: number of real (mask = 1) tokens in the batch, if the caller knows it
         without a device sync -- enables the unpadded HIP path (same math: padding
-        positions never reach a real token or the loss)."""
-        return self._run(input_ids, attention_mask, labels, tokens)
+        positions never reach a real token or the loss).
+        kd = (teacher logits [B, 2], temperature, alpha): the loss is the distillation loss
+        (models/bert.py ``kd_loss``), fused into the same head kernel on the HIP path."""
+        return self._run(input_ids, attention_mask, labels, tokens, kd)
 
-    def _run(self, input_ids, attention_mask, labels, tokens=None):
+    def _run(self, input_ids, attention_mask, labels, tokens=None, kd=None):
         if self.impl == "hip":
-            return self._run_hip(input_ids, attention_mask, labels, tokens)
-        return self._run_torch(input_ids, attention_mask, labels)
+            return self._run_hip(input_ids, attention_mask, labels, tokens, kd)
+        loss, logits = self._run_torch(input_ids, attention_mask, labels if kd is None else None)
+        if kd is not None and labels is not None:
+            from .bert import kd_loss
+            loss = kd_loss(logits, kd[0], labels, kd[1], kd[2])
+        return loss, logits
 
     def packed_rows(self, tokens: int, B: int, S: int) -> int:
         """Row count of the packed layout for a batch with ``tokens`` real tokens."""
         q = self.pack_quantum
         return min(B * S, (int(tokens) + q - 1) // q * q)
 
-    def _run_hip(self, ids, mask, labels, tokens=None):
+    def _run_hip(self, ids, mask, labels, tokens=None, kd=None):
         from ..ops import kernels as K
         from ..ops.functional import EmbeddingFn, HeadFn, LayerFn, RunCtx
         self.sync_shadow()
@@ -440,6 +464,10 @@ class DDoSClassifier(nn.Module):
             S += pad
         emb, layers, head = self._hip_handles()
         cfg = self.config
+        if self.TOKEN_TYPES:
+            A = self.arena
+            emb["pos"].copy_(A.view("distilbert.embeddings.position_embeddings.weight")
+                             + A.view("distilbert.embeddings.token_type_embeddings.weight")[0])
         grad = torch.is_grad_enabled()
         if grad and self.wgrad_stream and self._wgrad is None:
             self._wgrad = torch.cuda.Stream(device=self.arena.device)
@@ -493,7 +521,7 @@ class DDoSClassifier(nn.Module):
         for i, L in enumerate(layers):
             x = LayerFn.apply(x, L, rc, i)
         if labels is not None:
-            loss, logits = HeadFn.apply(x, head["w"], head["b"], head["sinks"], rc, labels.to(torch.int64))
+            loss, logits = HeadFn.apply(x, head["w"], head["b"], head["sinks"], rc, labels.to(torch.int64), kd)
             return loss, logits
         logits, _ = HeadFn.apply(x, head["w"], head["b"], head["sinks"], rc, None)
         return None, logits
@@ -515,7 +543,10 @@ class DDoSClassifier(nn.Module):
             counter = self.torch_counter
         B, S = ids.shape
         e = self.distilbert.embeddings
-        x = R.embedding_ref(ids, e.word_embeddings.weight, e.position_embeddings.weight, e.LayerNorm.weight,
+        pos = e.position_embeddings.weight
+        if hasattr(e, "token_type_embeddings"):  # BERT teacher: token_type_ids all 0
+            pos = pos + e.token_type_embeddings.weight[0]
+        x = R.embedding_ref(ids, e.word_embeddings.weight, pos, e.LayerNorm.weight,
                             e.LayerNorm.bias, cfg.layer_norm_eps, cfg.dropout if tr else 0.0, counter, 1)
         for i, blk in enumerate(self.distilbert.transformer.layer):
             a = blk.attention

@@ -128,6 +128,15 @@ class EmbeddingFn(torch.autograd.Function):
         now, ever = s.get("flags") or (None, None)
         K.emb_bwd(dy, ids, srt, perm, word, pos, gamma, mean, rstd, s["word"].buf, s["pos"].buf, s["ln_w"].buf,
                   s["ln_b"].buf, ctx.rc.S, ctx.rc.seed, 1, ctx.p, acc, now, ever, ctx.rc.row_map, ctx.rc.cu)
+        tt = s.get("type")
+        if tt is not None:
+            # BERT token-type row 0 is added at every position: d(type0) = sum_s d(pos_s).  The
+            # position gradient already holds the running total of an accumulating backward,
+            # so the type row is always re-derived from it (never added to).
+            tt.accumulate()
+            g = tt.buf
+            torch.sum(s["pos"].buf[:ctx.rc.S], 0, out=g[0])
+            g[1:].zero_()
         if ctx.rc.wgrad is not None:  # join the weight-gradient stream: every grad is final after this node
             torch.cuda.current_stream().wait_stream(ctx.rc.wgrad)
         if ctx.rc.colsum_jobs:
@@ -240,10 +249,11 @@ class HeadFn(torch.autograd.Function):
     """CLS -> Dropout(0.3) -> Linear(768, 2); optional fused CE (mean) loss."""
 
     @staticmethod
-    def forward(ctx, hidden, W, b, sinks, rc: RunCtx, labels: Optional[torch.Tensor]):
+    def forward(ctx, hidden, W, b, sinks, rc: RunCtx, labels: Optional[torch.Tensor], kd=None):
+        """kd = (teacher logits, T, alpha): the fused loss is the distillation loss."""
         p = rc.p_head if rc.training else 0.0
         cls = rc.cu[:-1] if rc.cu is not None else None  # packed: [CLS] = first row of each sequence
-        logits, loss, dlog = K.head_fwd(hidden, rc.B, rc.S, W, b, rc.seed, 2, p, labels, cls)
+        logits, loss, dlog = K.head_fwd(hidden, rc.B, rc.S, W, b, rc.seed, 2, p, labels, cls, kd)
         ctx.rc, ctx.sinks, ctx.p, ctx.W = rc, sinks, p, W
         ctx.save_for_backward(hidden)
         ctx.dlog = dlog
@@ -264,12 +274,12 @@ class HeadFn(torch.autograd.Function):
         gscale = None
         if ctx.fused_loss:
             if g0 is None:
-                return (None,) * 6
+                return (None,) * 7
             dlog = ctx.dlog
             gscale = g0.float().reshape(1)  # scaled inside the kernel (no elementwise launch)
         else:
             if g0 is None:
-                return (None,) * 6
+                return (None,) * 7
             dlog = g0.float().contiguous()
         s = ctx.sinks
         acc = s["w"].accumulate()
@@ -277,4 +287,4 @@ class HeadFn(torch.autograd.Function):
         cls = ctx.rc.cu[:-1] if ctx.rc.cu is not None else None
         dh = K.head_bwd(hidden, ctx.rc.B, ctx.rc.S, ctx.W, ctx.rc.seed, 2, ctx.p, dlog, s["w"].buf, s["b"].buf, acc,
                         cls, gscale)
-        return dh, None, None, None, None, None
+        return dh, None, None, None, None, None, None

@@ -320,8 +320,10 @@ def emb_bwd(dy, ids, sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos
 
 
 # ------------------------------------------------------------------ head / metrics / optimizer
-def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None, cls=None):
-    """cls (int32 [B]): packed layout -- sequence b's [CLS] is row cls[b] of hidden."""
+def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None, cls=None, kd=None):
+    """cls (int32 [B]): packed layout -- sequence b's [CLS] is row cls[b] of hidden.
+    kd = (teacher logits fp32 [B, 2], T, alpha): the fused loss is the distillation loss
+    alpha * CE + (1 - alpha) * T^2 * KL(softmax(t/T) || softmax(z/T)) (models/bert.py kd_loss)."""
     logits = torch.empty(B, 2, dtype=torch.float32, device=hidden.device)
     loss = dlogits = row_loss = None
     if labels is not None:
@@ -329,7 +331,11 @@ def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None, cls=None):
         dlogits = torch.empty(B, 2, dtype=torch.float32, device=hidden.device)
         row_loss = workspace(hidden.device, "head_row_loss", B)
     thr, sc = _drop(p)
-    ext().head_fwd(hidden, B, S, W, b, seed, site, thr, sc, labels, logits, loss, dlogits, row_loss, cls)
+    t, T, alpha = kd if kd is not None else (None, 1.0, 1.0)
+    if t is not None:
+        t = t.detach().float().contiguous()
+    ext().head_fwd(hidden, B, S, W, b, seed, site, thr, sc, labels, logits, loss, dlogits, row_loss, cls,
+                   t, float(T), float(alpha))
     return logits, loss, dlogits
 
 

@@ -207,9 +207,6 @@ def make_dp_step_fn(model, optimizer, sync: GradSync, teacher=None, temperature:
     the shard shares, sum to the client-batch KD loss exactly as the CE loss does."""
     if getattr(optimizer, "overlap", False):
         raise ValueError("data-parallel clients need ArenaAdam(overlap=False)")
-    if teacher is not None:
-        from ..models.bert import kd_loss
-
     def step(ids, mask, labels, tokens=None):  # shards run the padded path (no per-shard token count)
         optimizer.zero_grad()
         if teacher is None:
@@ -217,7 +214,7 @@ def make_dp_step_fn(model, optimizer, sync: GradSync, teacher=None, temperature:
         else:
             with torch.no_grad():
                 t_logits = teacher(ids, mask)
-            loss = kd_loss(model(ids, mask), t_logits, labels, temperature, alpha)
+            loss, _ = model.forward_loss(ids, mask, labels, kd=(t_logits, temperature, alpha))
         scaled = loss * sync.loss_scale
         scaled.backward()
         sync.finish()

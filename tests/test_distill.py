@@ -44,3 +44,35 @@ def test_kd_step_reduces_loss():
     student.train()
     losses = [float(step(ids, mask, y)) for _ in range(8)]
     assert losses[-1] < losses[0]
+
+
+def test_teacher_token_type_table_is_an_arena_parameter():
+    """The token-type table trains like every other weight (it used to sit outside the arena
+    and was folded in under detach(), so the HIP path never updated it)."""
+    t = BertTeacherClassifier(config=bert_base_config(n_layers=1))
+    names = [n for n, _ in t.named_parameters()]
+    assert "distilbert.embeddings.token_type_embeddings.weight" in names
+    off, shape = t.arena.offsets["distilbert.embeddings.token_type_embeddings.weight"]
+    assert shape == (2, 768)
+    ids, mask, y = _batch()
+    t.train()
+    t.zero_grad()
+    loss, _ = t.forward_loss(ids, mask, y)
+    loss.backward()
+    g = t.arena.gview("distilbert.embeddings.token_type_embeddings.weight")
+    gp = t.arena.gview("distilbert.embeddings.position_embeddings.weight")
+    assert g[0].abs().sum() > 0 and g[1].abs().sum() == 0
+    assert torch.allclose(g[0], gp[:ids.shape[1]].sum(0), rtol=1e-4, atol=1e-7)
+    before = t.arena.view("distilbert.embeddings.token_type_embeddings.weight").clone()
+    opt = ArenaAdam(t, lr=1e-3)
+    opt.step()
+    assert not torch.equal(before[0], t.arena.view("distilbert.embeddings.token_type_embeddings.weight")[0])
+
+
+def test_forward_loss_kd_equals_kd_loss():
+    student = DDoSClassifier(config=DistilBertConfig(n_layers=1))
+    ids, mask, y = _batch()
+    student.eval()
+    t_logits = torch.randn(ids.shape[0], 2)
+    loss, logits = student.forward_loss(ids, mask, y, kd=(t_logits, 2.0, 0.3))
+    assert torch.allclose(loss, kd_loss(logits, t_logits, y, 2.0, 0.3))
