@@ -4,9 +4,18 @@
 // kernel's grid assumes BEFORE launching (a mis-shaped launch of a hand-written
 // kernel can fault the GPU), then launches on the caller's current HIP stream so
 // the ops are stream-ordered and capturable into HIP graphs.
+#ifdef FD_HOST_VALIDATION
+// Host-only build of this validation layer (csrc/host_check/, tests/test_host_sanitizers.py):
+// compiled with g++ and ASan/UBSan against CPU ATen, launchers replaced by stubs that check
+// every extent the kernels would touch against the buffers the test registered.  Only the
+// device-placement check and the stream query differ; every shape/dtype rule is the same code.
+#include <ATen/ATen.h>
+typedef struct ihipStream_t* hipStream_t;
+#else
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
+#endif
 
 #include <cstdint>
 #include <vector>
@@ -92,12 +101,18 @@ int fd_axpby(float* dst, const float* x, const float* y, float a, float b, long 
 
 namespace {
 
+#ifdef FD_HOST_VALIDATION
+hipStream_t stream() { return nullptr; }
+bool on_device(const at::Tensor&) { return true; }  // CPU tensors stand in for device buffers
+#else
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+bool on_device(const at::Tensor& t) { return t.is_cuda(); }
+#endif
 
 void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, what, ": kernel launcher rejected arguments (rc=", rc, ")"); }
 
 void need(const at::Tensor& t, at::ScalarType dt, const char* name) {
-  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(on_device(t), name, " must be a GPU tensor");
   TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
@@ -109,7 +124,7 @@ T* ptr(const c10::optional<at::Tensor>& t) {
   return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
 }
 const uint32_t* seedp(const at::Tensor& s) {
-  TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kInt && s.numel() >= 1, "seed must be a GPU int32 tensor");
+  TORCH_CHECK(on_device(s) && s.scalar_type() == at::kInt && s.numel() >= 1, "seed must be a GPU int32 tensor");
   return reinterpret_cast<const uint32_t*>(s.data_ptr());
 }
 
@@ -357,7 +372,7 @@ void splitk_reduce_batched(const std::vector<at::Tensor>& slabs, const std::vect
 // Unpadded-step layout in one launch: row_map [rows] int32, cu [B+1] int32, ids_packed [rows] int64.
 void pack(const at::Tensor& mask, const at::Tensor& ids, const at::Tensor& row_map, const at::Tensor& cu,
           const at::Tensor& ids_packed) {
-  TORCH_CHECK(mask.is_cuda() && mask.is_contiguous() && ids.is_cuda() && ids.is_contiguous(), "pack: GPU inputs");
+  TORCH_CHECK(on_device(mask) && mask.is_contiguous() && on_device(ids) && ids.is_contiguous(), "pack: GPU inputs");
   TORCH_CHECK(mask.dim() == 2 && ids.sizes() == mask.sizes(), "pack: mask and ids must both be [B, S]");
   need(row_map, at::kInt, "row_map");
   need(cu, at::kInt, "cu");
@@ -401,7 +416,7 @@ int64_t comm_init(int64_t nranks, int64_t rank, const at::Tensor& id) {
 void comm_destroy(int64_t h) { comm_check(fd_comm_destroy(reinterpret_cast<void*>(h)), "ncclCommDestroy"); }
 void comm_allreduce(int64_t h, const at::Tensor& t, int64_t op) {
   TORCH_CHECK(h != 0, "comm_allreduce: communicator not initialised");
-  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "comm_allreduce: contiguous GPU tensor required");
+  TORCH_CHECK(on_device(t) && t.is_contiguous(), "comm_allreduce: contiguous GPU tensor required");
   TORCH_CHECK(op >= 0 && op <= 2, "comm_allreduce: op must be 0 (sum), 1 (avg) or 2 (max)");
   comm_check(fd_comm_allreduce(reinterpret_cast<void*>(h), t.data_ptr(), t.data_ptr(), t.numel(), comm_dtype(t),
                                (int)op, stream()),
@@ -409,14 +424,14 @@ void comm_allreduce(int64_t h, const at::Tensor& t, int64_t op) {
 }
 void comm_broadcast(int64_t h, const at::Tensor& t, int64_t root) {
   TORCH_CHECK(h != 0, "comm_broadcast: communicator not initialised");
-  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "comm_broadcast: contiguous GPU tensor required");
+  TORCH_CHECK(on_device(t) && t.is_contiguous(), "comm_broadcast: contiguous GPU tensor required");
   comm_check(fd_comm_broadcast(reinterpret_cast<void*>(h), t.data_ptr(), t.numel(), comm_dtype(t), (int)root,
                                stream()),
              "ncclBroadcast");
 }
 void comm_allgather(int64_t h, const at::Tensor& send, const at::Tensor& recv) {
   TORCH_CHECK(h != 0, "comm_allgather: communicator not initialised");
-  TORCH_CHECK(send.is_cuda() && recv.is_cuda() && send.is_contiguous() && recv.is_contiguous(),
+  TORCH_CHECK(on_device(send) && on_device(recv) && send.is_contiguous() && recv.is_contiguous(),
               "comm_allgather: contiguous GPU tensors required");
   TORCH_CHECK(send.scalar_type() == recv.scalar_type() && recv.numel() % send.numel() == 0,
               "comm_allgather: recv must hold nranks x send");
@@ -515,7 +530,7 @@ void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
 }
 
 void mask_to_bias(const at::Tensor& mask, const at::Tensor& bias) {
-  TORCH_CHECK(mask.is_cuda() && mask.is_contiguous(), "mask must be a contiguous GPU tensor");
+  TORCH_CHECK(on_device(mask) && mask.is_contiguous(), "mask must be a contiguous GPU tensor");
   need(bias, at::kFloat, "bias");
   TORCH_CHECK(mask.numel() == bias.numel(), "mask/bias size");
   check_rc(fd_mask_to_bias(mask.data_ptr(), (int)mask.element_size(), bias.data_ptr<float>(), (long)mask.numel(),
@@ -579,7 +594,7 @@ void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& po
              const at::Tensor& beta, const at::Tensor& y, const at::Tensor& mean, const at::Tensor& rstd, int64_t S,
              double eps, const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
              const c10::optional<at::Tensor>& row_map) {
-  TORCH_CHECK(ids.is_cuda() && ids.is_contiguous() && (ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt),
+  TORCH_CHECK(on_device(ids) && ids.is_contiguous() && (ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt),
               "ids must be contiguous GPU int64/int32");
   need(word, at::kBFloat16, "word");
   need(pos, at::kBFloat16, "pos");
@@ -639,7 +654,7 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
 }
 
 void rank_sort(const at::Tensor& ids, const at::Tensor& sorted, const at::Tensor& perm) {
-  TORCH_CHECK(ids.is_cuda() && ids.is_contiguous() && (ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt),
+  TORCH_CHECK(on_device(ids) && ids.is_contiguous() && (ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt),
               "ids must be contiguous GPU int64/int32");
   need(sorted, at::kLong, "sorted");
   need(perm, at::kLong, "perm");
@@ -844,6 +859,7 @@ void axpby(const at::Tensor& dst, const at::Tensor& x, const c10::optional<at::T
 
 }  // namespace
 
+#ifndef FD_HOST_VALIDATION
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the federated DistilBERT engine";
   m.def("gemm", &gemm, py::arg("kind"), py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"),
@@ -890,3 +906,4 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scale_cast", &scale_cast);
   m.def("axpby", &axpby);
 }
+#endif  // FD_HOST_VALIDATION

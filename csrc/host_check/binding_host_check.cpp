@@ -1,0 +1,522 @@
+// Host-only sanitizer harness for the launch-validation layer (csrc/binding.cpp).
+//
+// The binding is the only thing between Python and a hand-written kernel's grid: it must
+// reject every call whose shapes the kernel does not support, and pass every pointer with
+// the extent the kernel will touch.  Here it is compiled with g++ -fsanitize=address,undefined
+// against CPU ATen (FD_HOST_VALIDATION), with the fd_* launchers replaced by stubs that
+// (a) count calls and (b) check that every region the real kernel would read or write --
+// derived from the launch arguments exactly as the kernel derives it -- lies inside a buffer
+// the test registered.  The driver then makes valid calls (no exception, no violation) and
+// invalid ones (a c10::Error, and NO launcher call).  Run by tests/test_host_sanitizers.py.
+#define FD_HOST_VALIDATION 1
+#include "../binding.cpp"
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+namespace hc {
+struct Region { uintptr_t lo, hi; };
+std::vector<Region> regions;
+std::vector<std::string> violations;
+int calls = 0;
+
+void reg(const at::Tensor& t) {
+  const uintptr_t p = reinterpret_cast<uintptr_t>(t.data_ptr());
+  regions.push_back({p, p + (uintptr_t)(t.numel() * t.element_size())});
+}
+void span(const void* p, long long bytes, const char* what) {
+  if (bytes <= 0) return;
+  if (!p) { violations.push_back(std::string("null ") + what); return; }
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + (uintptr_t)bytes;
+  for (const Region& r : regions)
+    if (lo >= r.lo && hi <= r.hi) return;
+  violations.push_back(std::string("out of bounds: ") + what + " (" + std::to_string(bytes) + " B)");
+}
+void opt_span(const void* p, long long bytes, const char* what) { if (p) span(p, bytes, what); }
+}  // namespace hc
+
+// ------------------------------------------------------------------ stub launchers
+extern "C" {
+int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+               int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
+               long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+               float* colsum, int* colsum_blocks, void* aux_out, hipStream_t) {
+  ++hc::calls;
+  if (kind == 0) {  // A [M][lda] (K used), B [N][ldb], C [M][ldc] bf16
+    hc::span(A, ((long long)(M - 1) * lda + K) * 2, "gemm A");
+    hc::span(B, ((long long)(N - 1) * ldb + K) * 2, "gemm B");
+  } else if (kind == 1) {  // A [M][lda], B [K][ldb] (N used)
+    hc::span(A, ((long long)(M - 1) * lda + K) * 2, "gemm A");
+    hc::span(B, ((long long)(K - 1) * ldb + N) * 2, "gemm B");
+  } else {  // A [K][lda] (M used), B [K][ldb]
+    hc::span(A, ((long long)(K - 1) * lda + M) * 2, "gemm A");
+    hc::span(B, ((long long)(K - 1) * ldb + N) * 2, "gemm B");
+  }
+  hc::span(C, ((long long)(M - 1) * ldc + N) * (kind == 2 ? 4 : 2), "gemm C");
+  if (epi == 1 || epi == 2) hc::span(bias, (long long)N * 4, "gemm bias");
+  if (epi == 2 || epi == 3) hc::span(aux, ((long long)(M - 1) * ldaux + N) * 2, "gemm aux");
+  if (epi == 4) hc::span(res, ((long long)(M - 1) * ldres + N) * 2, "gemm res");
+  if (aux_out) hc::span(aux_out, ((long long)(M - 1) * ldaux + N) * 2, "gemm aux_out");
+  if (colsum && colsum_blocks) {
+    *colsum_blocks = (M + 127) / 128;
+    hc::span(colsum, (long long)*colsum_blocks * N * 4, "gemm colsum");
+  }
+  if (kind == 2 && workspace_elems > 0) hc::span(workspace, workspace_elems * 4, "gemm workspace");
+  if (adam && adam->p) {
+    hc::span(adam->p, (long long)M * N * 4, "adam p");
+    hc::span(adam->m, (long long)M * N * 4, "adam m");
+    hc::span(adam->v, (long long)M * N * 4, "adam v");
+    hc::opt_span(adam->sh, (long long)M * N * 2, "adam shadow");
+  }
+  (void)accumulate; (void)tile_cnt; (void)ncnt;
+  return 0;
+}
+int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+            const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
+            long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+            float* colsum, int* colsum_blocks, hipStream_t st) {
+  return fd_gemm_ex(kind, epi, A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, res, ldres, workspace,
+                    workspace_elems, accumulate, tile_cnt, ncnt, adam, colsum, colsum_blocks, nullptr, st);
+}
+int fd_gemm_set_cfg(int, int, int) { return 0; }
+int fd_gemm_set_fixup(int) { return 0; }
+int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
+                int M1, int N1, int K, float* workspace, long long workspace_elems, int, int*, long long,
+                const FdAdamEpi* adams, int, int* splits_out, hipStream_t) {
+  ++hc::calls;
+  hc::span(A0, (long long)K * M0 * 2, "dw2 A0");
+  hc::span(B0, (long long)K * N0 * 2, "dw2 B0");
+  hc::span(C0, (long long)M0 * N0 * 4, "dw2 C0");
+  hc::span(A1, (long long)K * M1 * 2, "dw2 A1");
+  hc::span(B1, (long long)K * N1 * 2, "dw2 B1");
+  hc::span(C1, (long long)M1 * N1 * 4, "dw2 C1");
+  hc::opt_span(workspace, workspace_elems * 4, "dw2 workspace");
+  (void)adams;
+  if (splits_out) *splits_out = 0;
+  return 0;
+}
+int fd_gemm_dw2_splits(int, int, int, int, int) { return 1; }
+int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg, hipStream_t) {
+  ++hc::calls;
+  if (n <= 0 || n > 32) hc::violations.push_back("dw_batch: problem count");
+  for (int i = 0; i < n; ++i) {
+    const FdDwProb& q = probs[i];
+    const long long mn = (long long)q.M * q.N;
+    hc::span(q.A, (long long)K * q.M * 2, "dw_batch A");
+    hc::span(q.B, (long long)K * q.N * 2, "dw_batch B");
+    if (q.p) {
+      hc::span(q.p, mn * 4, "dw_batch adam p");
+      hc::span(q.m, mn * 4, "dw_batch adam m");
+      hc::span(q.v, mn * 4, "dw_batch adam v");
+      hc::opt_span(q.sh, mn * 2, "dw_batch adam shadow");
+      hc::span(step, 4, "dw_batch step");
+      if (!hyper) hc::violations.push_back("dw_batch: fused Adam without hyper-parameters");
+    } else {
+      hc::span(q.C, mn * 4, "dw_batch C");
+    }
+  }
+  (void)cfg;
+  return 0;
+}
+int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
+                             const int* splits, const int*, hipStream_t) {
+  ++hc::calls;
+  for (int i = 0; i < n; ++i) {
+    hc::span(slabs[i], numel[i] * splits[i] * 4, "reduce slabs");
+    hc::span(outs[i], numel[i] * 4, "reduce out");
+  }
+  return 0;
+}
+int fd_transpose_batched(const void* const* srcs, void* const* dsts, const int* rows, const int* cols, int n,
+                         hipStream_t) {
+  ++hc::calls;
+  for (int i = 0; i < n; ++i) {
+    hc::span(srcs[i], (long long)rows[i] * cols[i] * 2, "transpose src");
+    hc::span(dsts[i], (long long)rows[i] * cols[i] * 2, "transpose dst");
+  }
+  return 0;
+}
+const char* fd_comm_last_error() { return ""; }
+int fd_comm_load(const char*) { return 0; }
+int fd_comm_unique_id_bytes() { return 128; }
+int fd_comm_get_unique_id(void*) { return 0; }
+int fd_comm_init(void**, int, int, const void*) { return 0; }
+int fd_comm_destroy(void*) { return 0; }
+int fd_comm_allreduce(void*, const void*, void*, long long, int, int, hipStream_t) { return 0; }
+int fd_comm_broadcast(void*, void*, long long, int, int, hipStream_t) { return 0; }
+int fd_comm_allgather(void*, const void*, void*, long long, int, hipStream_t) { return 0; }
+int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H, const uint32_t* seed,
+                uint32_t, uint32_t, float, const int* cu, int rows, hipStream_t) {
+  ++hc::calls;
+  const long long D = (long long)H * 64;
+  hc::span(qkv, rows * 3 * D * 2, "attn qkv");
+  hc::span(ctx, rows * D * 2, "attn ctx");
+  hc::span(lse, (long long)B * H * S * 4, "attn lse");
+  hc::span(seed, 4, "attn seed");
+  if (cu) hc::span(cu, (long long)(B + 1) * 4, "attn cu");
+  else hc::span(kbias, (long long)B * S * 4, "attn kbias");
+  return 0;
+}
+int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx, float* delta,
+                void* dqkv, int B, int S, int H, const uint32_t* seed, uint32_t, uint32_t, float, const int* cu,
+                int rows, hipStream_t) {
+  ++hc::calls;
+  const long long D = (long long)H * 64;
+  hc::span(qkv, rows * 3 * D * 2, "attn bwd qkv");
+  hc::span(dqkv, rows * 3 * D * 2, "attn bwd dqkv");
+  hc::span(ctx, rows * D * 2, "attn bwd ctx");
+  hc::span(dctx, rows * D * 2, "attn bwd dctx");
+  hc::span(lse, (long long)B * H * S * 4, "attn bwd lse");
+  hc::span(delta, (long long)B * H * S * 4, "attn bwd delta");
+  hc::span(seed, 4, "attn bwd seed");
+  if (cu) hc::span(cu, (long long)(B + 1) * 4, "attn bwd cu");
+  else hc::span(kbias, (long long)B * S * 4, "attn bwd kbias");
+  return 0;
+}
+int fd_mask_to_bias(const void*, int, float*, long, hipStream_t) { ++hc::calls; return 0; }
+int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, float* mean, float* rstd,
+              int T, int D, float, const uint32_t* seed, uint32_t, uint32_t, float, const int* row_map, hipStream_t) {
+  ++hc::calls;
+  const long long n = (long long)T * D;
+  hc::span(x, n * 2, "ln x");
+  hc::opt_span(r, n * 2, "ln r");
+  hc::span(y, n * 2, "ln y");
+  hc::span(gamma, (long long)D * 4, "ln gamma");
+  hc::span(beta, (long long)D * 4, "ln beta");
+  hc::span(mean, (long long)T * 4, "ln mean");
+  hc::span(rstd, (long long)T * 4, "ln rstd");
+  hc::span(seed, 4, "ln seed");
+  hc::opt_span(row_map, (long long)T * 4, "ln row_map");
+  return 0;
+}
+int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean, const float* rstd,
+              void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work, int T, int D,
+              const uint32_t* seed, uint32_t, uint32_t, float, int, const int* row_map, int, int* nblk_out,
+              hipStream_t) {
+  ++hc::calls;
+  const long long n = (long long)T * D;
+  hc::span(dy, n * 2, "ln bwd dy");
+  hc::span(x, n * 2, "ln bwd x");
+  hc::opt_span(r, n * 2, "ln bwd r");
+  hc::span(dz, n * 2, "ln bwd dz");
+  hc::opt_span(dx, n * 2, "ln bwd dx");
+  hc::span(gamma, (long long)D * 4, "ln bwd gamma");
+  hc::span(mean, (long long)T * 4, "ln bwd mean");
+  hc::span(rstd, (long long)T * 4, "ln bwd rstd");
+  hc::opt_span(dgamma, (long long)D * 4, "ln bwd dgamma");
+  hc::opt_span(dbeta, (long long)D * 4, "ln bwd dbeta");
+  hc::opt_span(dbias, (long long)D * 4, "ln bwd dbias");
+  const int blocks = std::min(512, (T + 7) / 8);  // the kernel's partial-sum grid (csrc/kernels/norm.hip)
+  hc::span(work, (long long)blocks * 3 * D * 4, "ln bwd work");
+  hc::span(seed, 4, "ln bwd seed");
+  hc::opt_span(row_map, (long long)T * 4, "ln bwd row_map");
+  if (nblk_out) *nblk_out = blocks;
+  return 0;
+}
+int fd_emb_fwd(const void*, int, const void*, const void*, const float*, const float*, void*, float*, float*, int, int,
+               int, float, const uint32_t*, uint32_t, uint32_t, float, const int*, hipStream_t) { ++hc::calls; return 0; }
+int fd_emb_bwd(const void*, const void*, int, const long long*, const long long*, const void*, const void*,
+               const float*, const float*, const float*, float*, float*, float*, float*, float*, float*, int, int, int,
+               int, int, int, const uint32_t*, uint32_t, uint32_t, float, int, unsigned char*, unsigned char*,
+               const int*, const int*, hipStream_t) { ++hc::calls; return 0; }
+int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
+            int* cu, long long* ids_packed, hipStream_t) {
+  ++hc::calls;
+  hc::span(mask, (long long)B * S * mask_bytes, "pack mask");
+  hc::span(ids, (long long)B * S * ids_bytes, "pack ids");
+  hc::span(row_map, (long long)rows * 4, "pack row_map");
+  hc::span(cu, (long long)(B + 1) * 4, "pack cu");
+  hc::span(ids_packed, (long long)rows * 8, "pack ids_packed");
+  return 0;
+}
+int fd_colsum_bf16(const void*, int, int, float*, float*, int, int, int* nblk_out, hipStream_t) {
+  ++hc::calls;
+  if (nblk_out) *nblk_out = 1;
+  return 0;
+}
+int fd_colsum_batched(int, const float* const*, float* const*, const int*, const int*, const int*, const int*,
+                      const int*, hipStream_t) { ++hc::calls; return 0; }
+int fd_rank_sort(const void*, int, int, long long*, long long*, hipStream_t) { ++hc::calls; return 0; }
+int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias, const uint32_t* seed,
+                uint32_t, uint32_t, float, const long long* labels, float* logits, float* loss, float* dlogits,
+                float* row_loss, const int* cls, int T, const float* tlogits, float, float, hipStream_t) {
+  ++hc::calls;
+  hc::span(hidden, (long long)T * D * 2, "head hidden");
+  hc::span(W, 2LL * D * 4, "head W");
+  hc::span(bias, 8, "head bias");
+  hc::span(logits, 2LL * B * 4, "head logits");
+  if (!cls && (long long)B * S > T) hc::violations.push_back("head: padded rows beyond hidden");
+  hc::opt_span(cls, (long long)B * 4, "head cls");
+  if (labels) {
+    hc::span(labels, (long long)B * 8, "head labels");
+    hc::span(loss, 4, "head loss");
+    hc::span(dlogits, 2LL * B * 4, "head dlogits");
+    hc::span(row_loss, (long long)B * 4, "head row_loss");
+  }
+  hc::opt_span(tlogits, 2LL * B * 4, "head teacher logits");
+  hc::span(seed, 4, "head seed");
+  return 0;
+}
+int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed, uint32_t, uint32_t,
+                float, const float* dlogits, float* dW, float* db, void* dhidden, int, const int* cls, int T,
+                const float* gscale, hipStream_t) {
+  ++hc::calls;
+  hc::span(hidden, (long long)T * D * 2, "head bwd hidden");
+  hc::span(dhidden, (long long)T * D * 2, "head bwd dhidden");
+  hc::span(W, 2LL * D * 4, "head bwd W");
+  hc::span(dlogits, 2LL * B * 4, "head bwd dlogits");
+  hc::span(dW, 2LL * D * 4, "head bwd dW");
+  hc::span(db, 8, "head bwd db");
+  hc::opt_span(cls, (long long)B * 4, "head bwd cls");
+  hc::opt_span(gscale, 4, "head bwd gscale");
+  hc::span(seed, 4, "head bwd seed");
+  (void)S;
+  return 0;
+}
+int fd_eval_metrics(const float*, const long long*, int, double*, long long*, float*, long long*, hipStream_t) {
+  ++hc::calls;
+  return 0;
+}
+int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float, float,
+            float, float, float, int, const unsigned char* touched, const unsigned char* now, long long skip_off,
+            long long skip_rows, int row_len, const long long* runs, int nruns, long long run_total4, hipStream_t) {
+  ++hc::calls;
+  hc::span(p, n * 4, "adam p");
+  hc::span(g, n * 4, "adam g");
+  hc::span(m, n * 4, "adam m");
+  hc::span(v, n * 4, "adam v");
+  hc::opt_span(shadow, n * 2, "adam shadow");
+  hc::span(step, 4, "adam step");
+  if (touched) {
+    hc::span(touched, skip_rows, "adam touched");
+    hc::opt_span(now, skip_rows, "adam now");
+    if (skip_off < 0 || skip_off + skip_rows * row_len > n) hc::violations.push_back("adam: skip range");
+  }
+  if (runs) {  // the kernel indexes [start4, start4 + count4) of every run (csrc/kernels/head_optim.hip)
+    hc::span(runs, (long long)nruns * 3 * 8, "adam runs");
+    long long pre = 0;
+    for (int i = 0; i < nruns; ++i) {
+      const long long s4 = runs[3 * i], c4 = runs[3 * i + 1], p4 = runs[3 * i + 2];
+      if (s4 < 0 || c4 <= 0 || (s4 + c4) * 4 > n) hc::violations.push_back("adam: run outside the arena");
+      if (p4 != pre) hc::violations.push_back("adam: run prefix");
+      pre += c4;
+    }
+    if (pre != run_total4) hc::violations.push_back("adam: run total");
+  }
+  return 0;
+}
+int fd_step(int*, uint32_t*, hipStream_t) { ++hc::calls; return 0; }
+int fd_scale_cast(float*, void*, long long, float, hipStream_t) { ++hc::calls; return 0; }
+int fd_axpby(float*, const float*, const float*, float, float, long long, hipStream_t) { ++hc::calls; return 0; }
+}  // extern "C"
+
+// ------------------------------------------------------------------ driver
+namespace {
+int failures = 0;
+
+at::Tensor T_(at::IntArrayRef shape, at::ScalarType dt) {
+  at::Tensor t = at::zeros(shape, at::TensorOptions().dtype(dt));
+  hc::reg(t);
+  return t;
+}
+
+template <typename F>
+void expect_ok(const char* name, F f) {
+  const size_t v0 = hc::violations.size();
+  const int c0 = hc::calls;
+  try {
+    f();
+  } catch (const c10::Error& e) {
+    std::printf("FAIL %s: unexpected rejection: %s\n", name, e.what_without_backtrace());
+    ++failures;
+    return;
+  }
+  if (hc::calls == c0) {
+    std::printf("FAIL %s: no launcher was called\n", name);
+    ++failures;
+  }
+  for (size_t i = v0; i < hc::violations.size(); ++i) {
+    std::printf("FAIL %s: %s\n", name, hc::violations[i].c_str());
+    ++failures;
+  }
+}
+
+template <typename F>
+void expect_reject(const char* name, F f) {
+  const int c0 = hc::calls;
+  bool threw = false;
+  try {
+    f();
+  } catch (const c10::Error&) {
+    threw = true;
+  }
+  if (!threw) {
+    std::printf("FAIL %s: accepted a call the kernels do not support\n", name);
+    ++failures;
+  } else if (hc::calls != c0) {
+    std::printf("FAIL %s: rejected only after launching\n", name);
+    ++failures;
+  }
+}
+
+const c10::optional<at::Tensor> none = c10::nullopt;
+}  // namespace
+
+int main() {
+  const auto bf = at::kBFloat16, f32 = at::kFloat, i32 = at::kInt, i64 = at::kLong;
+  // ---- GEMMs: y = x W^T + b (NT), dx = dy W (NN), dW (TN); the DistilBERT shapes at a packed bs32 step
+  {
+    auto x = T_({2688, 768}, bf), w = T_({2304, 768}, bf), y = T_({2688, 2304}, bf), b = T_({2304}, f32);
+    expect_ok("gemm NT bias", [&] { gemm(0, 1, x, w, y, b, none, none, none, false, none); });
+    auto w1 = T_({3072, 768}, bf), g = T_({2688, 3072}, bf), u = T_({2688, 3072}, bf), b1 = T_({3072}, f32);
+    expect_ok("gemm NT bias+gelu", [&] { gemm(0, 2, x, w1, g, b1, u, none, none, false, none); });
+    auto dy = T_({2688, 768}, bf), w2t = T_({3072, 768}, bf), du = T_({2688, 3072}, bf), gout = T_({2688, 3072}, bf);
+    expect_ok("gemm NT gelu' + remat", [&] { gemm(0, 3, dy, w2t, du, none, u, none, none, false, gout); });
+    auto res = T_({2688, 768}, bf), wt = T_({768, 3072}, bf), dx = T_({2688, 768}, bf);
+    expect_ok("gemm NT residual", [&] { gemm(0, 4, du, wt, dx, none, none, res, none, false, none); });
+    auto w2 = T_({768, 3072}, bf);
+    expect_ok("gemm NN", [&] { gemm(1, 0, dy, w2, du, none, none, none, none, false, none); });
+    auto dW = T_({2304, 768}, f32), dq = T_({2688, 2304}, bf), ws = T_({8 * 2304 * 768}, f32);
+    expect_ok("gemm TN", [&] { gemm(2, 5, dq, x, dW, none, none, none, ws, false, none); });
+    auto cs = T_({21 * 3072}, f32);
+    expect_ok("gemm colsum", [&] { gemm_colsum(3, dy, w2t, du, u, none, cs, gout); });
+    // rejections
+    auto xk = T_({2688, 700}, bf), wk = T_({2304, 700}, bf);
+    expect_reject("gemm K % 64", [&] { gemm(0, 1, xk, wk, y, b, none, none, none, false, none); });
+    expect_reject("gemm C shape", [&] { gemm(0, 1, x, w, dx, b, none, none, none, false, none); });
+    expect_reject("gemm bias size", [&] { gemm(0, 1, x, w, y, b1, none, none, none, false, none); });
+    auto xf = T_({2688, 768}, f32);
+    expect_reject("gemm dtype", [&] { gemm(0, 1, xf, w, y, b, none, none, none, false, none); });
+    expect_reject("gemm aux missing", [&] { gemm(0, 2, x, w1, g, b1, none, none, none, false, none); });
+    expect_reject("gemm aux_out epi", [&] { gemm(0, 1, x, w, y, b, none, none, none, false, gout); });
+    auto xt = x.t();
+    expect_reject("gemm non-contiguous", [&] { gemm(0, 1, xt, w, y, b, none, none, none, false, none); });
+    auto cs_small = T_({3072}, f32);
+    expect_reject("gemm colsum size", [&] { gemm_colsum(3, dy, w2t, du, u, none, cs_small, gout); });
+  }
+  // ---- all-layer weight gradients (with and without the fused Adam epilogue)
+  {
+    std::vector<at::Tensor> As, Bs, Cs, st;
+    const int64_t shapes[4][2] = {{2304, 768}, {768, 768}, {3072, 768}, {768, 3072}};
+    for (auto& sh : shapes) {
+      As.push_back(T_({2688, sh[0]}, bf));
+      Bs.push_back(T_({2688, sh[1]}, bf));
+      Cs.push_back(T_({sh[0], sh[1]}, f32));
+      st.push_back(T_({sh[0] * sh[1]}, f32));
+      st.push_back(T_({sh[0] * sh[1]}, f32));
+      st.push_back(T_({sh[0] * sh[1]}, f32));
+      st.push_back(T_({sh[0] * sh[1]}, bf));
+    }
+    st.push_back(T_({1}, i32));
+    const std::vector<double> hp = {2e-5, 0.9, 0.999, 1e-8, 0.0, 0.0};
+    std::vector<int64_t> acc(4, 0), acc1 = {0, 1, 0, 0};
+    expect_ok("dw_batch", [&] { gemm_dw_batch(As, Bs, Cs, acc, {}, {}, -1); });
+    expect_ok("dw_batch adam", [&] { gemm_dw_batch(As, Bs, Cs, acc, st, hp, -1); });
+    expect_reject("dw_batch adam+accumulate", [&] { gemm_dw_batch(As, Bs, Cs, acc1, st, hp, -1); });
+    auto Bbad = Bs;
+    Bbad[2] = T_({2000, 768}, bf);
+    expect_reject("dw_batch K mismatch", [&] { gemm_dw_batch(As, Bbad, Cs, acc, {}, {}, -1); });
+    auto Cbad = Cs;
+    Cbad[1] = T_({768, 3072}, f32);
+    expect_reject("dw_batch C shape", [&] { gemm_dw_batch(As, Bs, Cbad, acc, {}, {}, -1); });
+    auto stbad = st;
+    stbad[5] = T_({100}, f32);
+    expect_reject("dw_batch adam state size", [&] { gemm_dw_batch(As, Bs, Cs, acc, stbad, hp, -1); });
+    std::vector<at::Tensor> A33(33, As[1]), B33(33, Bs[1]), C33(33, Cs[1]);
+    expect_reject("dw_batch > 32 problems", [&] { gemm_dw_batch(A33, B33, C33, std::vector<int64_t>(33, 0), {}, {}, -1); });
+    auto A0 = T_({2688, 768}, bf), B0 = T_({2688, 3072}, bf), C0 = T_({768, 3072}, f32);
+    auto A1 = T_({2688, 3072}, bf), B1 = T_({2688, 768}, bf), C1 = T_({3072, 768}, f32), wsp = T_({8 * 2 * 2359296}, f32);
+    expect_ok("dw2", [&] { gemm_dw2(A0, B0, C0, A1, B1, C1, wsp, false, none, {}, {}, false); });
+  }
+  // ---- attention (padded and varlen), S up to 512
+  {
+    const int64_t B = 4, S = 128, H = 12, rows = B * S;
+    auto qkv = T_({rows, 3 * H * 64}, bf), kb = T_({B, S}, f32), ctx = T_({rows, H * 64}, bf);
+    auto lse = T_({B, H, S}, f32), seed = T_({1}, i32), dctx = T_({rows, H * 64}, bf), delta = T_({B * H * S}, f32);
+    auto dqkv = T_({rows, 3 * H * 64}, bf);
+    expect_ok("attn fwd", [&] { attn_fwd(qkv, kb, ctx, lse, B, S, H, seed, 16, 429496730, 1.1, none); });
+    expect_ok("attn bwd", [&] { attn_bwd(qkv, kb, ctx, lse, dctx, delta, dqkv, B, S, H, seed, 16, 0, 1.0, none); });
+    auto cu = T_({B + 1}, i32), qv = T_({300, 3 * H * 64}, bf), cv = T_({300, H * 64}, bf);
+    expect_ok("attn fwd varlen", [&] { attn_fwd(qv, kb, cv, lse, B, S, H, seed, 16, 0, 1.0, cu); });
+    const int64_t S5 = 512;
+    auto q5 = T_({2 * S5, 3 * H * 64}, bf), k5 = T_({2, S5}, f32), c5 = T_({2 * S5, H * 64}, bf), l5 = T_({2, H, S5}, f32);
+    expect_ok("attn fwd S=512", [&] { attn_fwd(q5, k5, c5, l5, 2, S5, H, seed, 16, 0, 1.0, none); });
+    expect_reject("attn S=576", [&] { attn_fwd(q5, k5, c5, l5, 2, 576, H, seed, 16, 0, 1.0, none); });
+    expect_reject("attn S % 64", [&] { attn_fwd(qkv, kb, ctx, lse, B, 100, H, seed, 16, 0, 1.0, none); });
+    expect_reject("attn lse size", [&] { attn_fwd(qkv, kb, ctx, l5, B, S, H, seed, 16, 0, 1.0, none); });
+    auto cu_bad = T_({B}, i32);
+    expect_reject("attn cu size", [&] { attn_fwd(qv, kb, cv, lse, B, S, H, seed, 16, 0, 1.0, cu_bad); });
+    expect_reject("attn bwd dqkv size", [&] { attn_bwd(qkv, kb, ctx, lse, dctx, delta, ctx, B, S, H, seed, 16, 0, 1.0, none); });
+  }
+  // ---- LayerNorm fwd / bwd
+  {
+    const int64_t Tn = 2688, D = 768;
+    auto x = T_({Tn, D}, bf), r = T_({Tn, D}, bf), ga = T_({D}, f32), be = T_({D}, f32), y = T_({Tn, D}, bf);
+    auto mean = T_({Tn}, f32), rstd = T_({Tn}, f32), seed = T_({1}, i32), rm = T_({Tn}, i32);
+    expect_ok("ln fwd", [&] { ln_fwd(x, r, ga, be, y, mean, rstd, 1e-12, seed, 17, 429496730, 1.1, rm); });
+    auto dz = T_({Tn, D}, bf), dx = T_({Tn, D}, bf), dg = T_({D}, f32), db = T_({D}, f32), dbias = T_({D}, f32);
+    auto work = T_({336 * 3 * D}, f32);
+    expect_ok("ln bwd", [&] { ln_bwd(x, x, r, ga, mean, rstd, dz, dx, dg, db, dbias, work, seed, 17, 429496730, 1.1,
+                                     false, rm, true); });
+    auto small = T_({100 * 3 * D}, f32);
+    expect_reject("ln bwd work", [&] { ln_bwd(x, x, r, ga, mean, rstd, dz, dx, dg, db, dbias, small, seed, 17, 0, 1.0,
+                                              false, none, false); });
+    expect_reject("ln bwd dx with dropout", [&] { ln_bwd(x, x, r, ga, mean, rstd, dz, none, dg, db, dbias, work, seed,
+                                                         17, 429496730, 1.1, false, none, false); });
+    auto g2 = T_({1024}, f32);
+    expect_reject("ln fwd D", [&] { ln_fwd(x, r, g2, g2, y, mean, rstd, 1e-12, seed, 17, 0, 1.0, none); });
+    auto rm_bad = T_({10}, i32);
+    expect_reject("ln fwd row_map", [&] { ln_fwd(x, r, ga, be, y, mean, rstd, 1e-12, seed, 17, 0, 1.0, rm_bad); });
+  }
+  // ---- head (+ fused distillation loss)
+  {
+    const int64_t B = 32, S = 128, D = 768;
+    auto hid = T_({B * S, D}, bf), W = T_({2, D}, f32), bias = T_({2}, f32), seed = T_({1}, i32);
+    auto lab = T_({B}, i64), logits = T_({B, 2}, f32), loss = T_({}, f32), dlog = T_({B, 2}, f32), rl = T_({B}, f32);
+    auto tl = T_({B, 2}, f32);
+    expect_ok("head fwd", [&] { head_fwd(hid, B, S, W, bias, seed, 2, 0, 1.0, lab, logits, loss, dlog, rl, none,
+                                         none, 1.0, 1.0); });
+    expect_ok("head fwd kd", [&] { head_fwd(hid, B, S, W, bias, seed, 2, 0, 1.0, lab, logits, loss, dlog, rl, none, tl,
+                                            2.0, 0.5); });
+    expect_reject("head kd without labels", [&] { head_fwd(hid, B, S, W, bias, seed, 2, 0, 1.0, none, logits, none,
+                                                           none, none, none, tl, 2.0, 0.5); });
+    expect_reject("head kd T <= 0", [&] { head_fwd(hid, B, S, W, bias, seed, 2, 0, 1.0, lab, logits, loss, dlog, rl,
+                                                   none, tl, 0.0, 0.5); });
+    auto dW = T_({2, D}, f32), db = T_({2}, f32), dh = T_({B * S, D}, bf);
+    expect_ok("head bwd", [&] { head_bwd(hid, B, S, W, seed, 2, 0, 1.0, dlog, dW, db, dh, false, none, none); });
+    auto hid_small = T_({B * S - 1, D}, bf);
+    expect_reject("head bwd hidden size", [&] { head_bwd(hid_small, B, S, W, seed, 2, 0, 1.0, dlog, dW, db, hid_small,
+                                                         false, none, none); });
+  }
+  // ---- Adam over an arena with a run table (the fused-step remainder)
+  {
+    const int64_t n = 4096;
+    auto p = T_({n}, f32), g = T_({n}, f32), m = T_({n}, f32), v = T_({n}, f32), sh = T_({n}, bf), step = T_({1}, i32);
+    auto runs = T_({2, 3}, i64);
+    auto rp = runs.data_ptr<int64_t>();
+    rp[0] = 0; rp[1] = 64; rp[2] = 0; rp[3] = 512; rp[4] = 256; rp[5] = 64;
+    expect_ok("adam runs", [&] { adam(p, g, m, v, sh, step, 2e-5, 0.9, 0.999, 1e-8, 0, false, none, none, 0, 0, 4,
+                                      runs, 320, 768); });
+    expect_reject("adam run end outside", [&] { adam(p, g, m, v, sh, step, 2e-5, 0.9, 0.999, 1e-8, 0, false, none,
+                                                     none, 0, 0, 4, runs, 320, 4096); });
+    auto g_small = T_({n - 4}, f32);
+    expect_reject("adam sizes", [&] { adam(p, g_small, m, v, sh, step, 2e-5, 0.9, 0.999, 1e-8, 0, false, none, none,
+                                           0, 0, 4, none, 0, 0); });
+  }
+  // ---- unpadded layout
+  {
+    auto mask = T_({32, 128}, i64), ids = T_({32, 128}, i64), rm = T_({2688}, i32), cu = T_({33}, i32);
+    auto ip = T_({2688}, i64);
+    expect_ok("pack", [&] { pack(mask, ids, rm, cu, ip); });
+    auto cu_bad = T_({32}, i32);
+    expect_reject("pack cu", [&] { pack(mask, ids, rm, cu_bad, ip); });
+  }
+  if (failures) {
+    std::printf("binding host check: %d failure(s)\n", failures);
+    return 1;
+  }
+  std::printf("binding host check: ok (%d launcher calls validated)\n", hc::calls);
+  return 0;
+}
