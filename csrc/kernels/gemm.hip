@@ -177,9 +177,12 @@ struct Operand {
 template <int EPI, int BM, int BN>
 struct EpiTraits {
   static constexpr bool ELEM = (EPI == EPI_ADD || EPI == EPI_GELU_BWD);
-  static constexpr bool F32S = EPI == EPI_F32 || (ELEM && BM * (BN * 4 + 16) <= LDS_MAX);
+  // fp32 weight-gradient tiles too large to stage in LDS (256 x 192, 256 x 256) are finished
+  // straight from the accumulators (direct_f32_epilogue): 16-byte stores per lane
+  static constexpr bool DIRECT = EPI == EPI_F32 && BM * (BN * 4 + 16) > LDS_MAX;
+  static constexpr bool F32S = (EPI == EPI_F32 && !DIRECT) || (ELEM && BM * (BN * 4 + 16) <= LDS_MAX);
   static constexpr int ES = F32S ? 4 : 2;
-  static constexpr int BYTES = BM * (BN * ES + 16);
+  static constexpr int BYTES = DIRECT ? 0 : BM * (BN * ES + 16);
 };
 
 DEV float4 ld_nt4(const float* p) {
@@ -286,6 +289,39 @@ DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0
     else *reinterpret_cast<float4*>(p.out + i) = g;
   }
   if (fix && tid == 0) p.tile_cnt[slot] = 0;  // ready for the next launch / graph replay
+}
+
+// fp32 epilogue from the accumulators (EpiTraits::DIRECT): lane (i, j) holds C[m][n..n+3] of
+// its wave tile.  Slab mode (out == nullptr: split z) or the final gradient (+= out when
+// accumulating), optionally with the fused Adam step; no split-K fixup (it needs the staged tile).
+template <int TM, int TN>
+DEV void direct_f32_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], int m0, int n0, int wr,
+                             int wc, int lane) {
+  const bool adam = p.adam.p != nullptr;
+  float step_size = 0.f, inv_sqrt_bc2 = 0.f;
+  if (adam) {
+    const int t = p.adam.step[0];
+    step_size = p.adam.lr / (1.f - powf(p.adam.b1, (float)t));
+    inv_sqrt_bc2 = 1.f / sqrtf(1.f - powf(p.adam.b2, (float)t));
+  }
+  float* C = p.out ? p.out : reinterpret_cast<float*>(p.C) + (size_t)blockIdx.z * p.slab_stride;
+#pragma unroll
+  for (int i = 0; i < TM / 16; ++i) {
+    const int m = m0 + wr * TM + i * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < TN / 16; ++j) {
+      const int n = n0 + wc * TN + j * 16 + 4 * (lane >> 4);
+      const size_t idx = (size_t)m * p.ldc + n;
+      float4 g = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      if (p.out && p.accumulate) {
+        const float4 o = *reinterpret_cast<const float4*>(p.out + idx);
+        g.x += o.x; g.y += o.y; g.z += o.z; g.w += o.w;
+      }
+      if (adam) adam_epi4(p.adam, idx, g, step_size, inv_sqrt_bc2);
+      else *reinterpret_cast<float4*>(C + idx) = g;
+    }
+  }
 }
 
 // aux_out[m][n..n+3] = gelu(aux[m][n..n+3]) from the 4 bf16 pre-activations already loaded
@@ -446,9 +482,13 @@ struct GemmCfg {
   using OA = Operand<BM, AK, NW>;
   using OB = Operand<BN, BKM, NW>;
   static constexpr int BUF = OA::BYTES + OB::BYTES;
-  static constexpr int EPI_BYTES = EpiTraits<EPI, BM, BN>::BYTES;
+  // DIRECT fp32 tiles are staged one wave-row band (BM / WM rows) at a time
+  static constexpr int EPI_BYTES = EpiTraits<EPI, BM, BN>::DIRECT ? (BM / WM) * (BN * 4 + 16)
+                                                                   : EpiTraits<EPI, BM, BN>::BYTES;
   static constexpr int SMEM = S * BUF > EPI_BYTES ? S * BUF : EPI_BYTES;
-  static constexpr bool VALID = SMEM <= LDS_MAX && (BKM || BN % 64 == 0) && (AK || BM % 64 == 0) &&
+  // (the accumulator-direct fp32 epilogue serves only the all-layer weight-gradient launch)
+  static constexpr bool VALID = SMEM <= LDS_MAX && !EpiTraits<EPI, BM, BN>::DIRECT && (BKM || BN % 64 == 0) &&
+                                (AK || BM % 64 == 0) &&
                                 (BM / WM) % 16 == 0 && (BN / WN) % 16 == 0 &&
                                 OA::PER_WAVE * NW * 1024 == OA::BYTES && OB::PER_WAVE * NW * 1024 == OB::BYTES;
 };
@@ -572,10 +612,35 @@ DEV void gemm_tile(const GemmParams& p, int bid, int slot, char* smem) {
       }
     }
   }
-  // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
-  // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
-  __syncthreads();
-  staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid, slot);
+  if constexpr (EpiTraits<EPI, BM, BN>::DIRECT) {
+    // fp32 tile too large for LDS: finish it one wave-row band (TM rows) at a time through the
+    // staged row-chunk epilogue (coalesced 16-byte rows for the gradient / Adam streams)
+    constexpr int LDC = BN * 4 + 16;
+#pragma unroll 1
+    for (int band = 0; band < WM; ++band) {
+      __syncthreads();  // ring slots (first band) / the previous band's staging are free
+      if (wr == band) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int r = i * 16 + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int c = wc * TN + j * 16 + 4 * (lane >> 4);
+            *reinterpret_cast<float4*>(smem + r * LDC + c * 4) =
+                make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+          }
+        }
+      }
+      __syncthreads();
+      f32_epilogue<TM, BN, 64 * NW>(p, smem, LDC, m0 + band * TM, n0, tid, slot);
+    }
+    (void)direct_f32_epilogue<TM, TN>;
+  } else {
+    // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
+    // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
+    __syncthreads();
+    staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid, slot);
+  }
 }
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
@@ -1069,7 +1134,9 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
 // All-layer weight gradients in one launch (gemm_dw_batch_kernel).  probs[i] = {A, B, C, p, m,
 // v, sh, M, N, -, accumulate} (tile0 is filled here); adam != nullptr -> hyper-parameters of
 // the fused optimizer step for the problems with p != nullptr.  cfg < 0: FD_GEMM_DWB_CFG or
-// the default 128 x 64 (2 x 2 waves, 2-deep ring).  Returns 0, or nonzero on an unsupported
+// the default 256 x 256 (2 x 4 waves, 2-deep ring, banded fp32 epilogue; falls back to 128 x 64
+// when a shape is not a multiple of 256).  Measured (profiles/r2_dw_batch_isolated_cfgs.txt,
+// all 24 dW of the bs32 step + Adam): 256^2 448 us, 128^2 470 us, 128 x 64 492 us.  Returns 0, or nonzero on an unsupported
 // shape (nothing launched).
 bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
   auto go = [&](auto kern, int bm, int bn, int threads) {
@@ -1093,6 +1160,9 @@ bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
     case 12: return go(gemm_dw_batch_kernel<256, 128, 4, 2, 2>, 256, 128, 512);
     case 15: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 4>, 128, 64, 256);
     case 21: return go(gemm_dw_batch_kernel<128, 128, 4, 2, 3>, 128, 128, 512);
+    case 3: return go(gemm_dw_batch_kernel<256, 192, 4, 2, 2>, 256, 192, 512);
+    case 6: return go(gemm_dw_batch_kernel<128, 192, 2, 4, 2>, 128, 192, 512);
+    case 11: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 2>, 256, 256, 512);
   }
   return false;
 }
@@ -1116,7 +1186,7 @@ int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const f
   int id = cfg;
   if (id < 0) {
     static const int env = [] { const char* e = getenv("FD_GEMM_DWB_CFG"); return e ? atoi(e) : -1; }();
-    id = env >= 0 ? env : 8;
+    id = env >= 0 ? env : 11;
   }
   // Group height: A-panels of gm x BM rows x K (bf16) should take ~half of a 4 MiB L2.
   const long long panel = 128ll * K * 2;
