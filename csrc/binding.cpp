@@ -39,6 +39,8 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
 int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K);
 int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg,
                      hipStream_t st);
+int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
+               const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t st);
 int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
                              const int* splits, const int* accumulate, hipStream_t st);
 int fd_transpose_batched(const void* const* srcs, void* const* dsts, const int* rows, const int* cols, int n,
@@ -65,7 +67,7 @@ int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* bet
 int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean,
               const float* rstd, void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work, int T,
               int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, int accumulate,
-              const int* row_map, int defer, int* nblk_out, hipStream_t st);
+              const int* row_map, int defer, int* nblk_out, int zin, hipStream_t st);
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const int* row_map, hipStream_t st);
@@ -345,6 +347,85 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
            "gemm_dw_batch");
 }
 
+// LayerNorm fused into the N = hidden NT GEMM C = A Bt^T (gemm.hip gemm_ln_kernel, FdLnEpi):
+//   bwd = false: C = LN(dropout(A Bt^T + bias) + res) (gamma, beta), z = the bf16 pre-LN sum,
+//                mean / rstd per row;
+//   bwd = true:  dy = A Bt^T + res; C = dz (LN input gradient) from z, mean, rstd, gamma;
+//                dx = dropout'(dz) (when thr); colpart[tiles_m][3][N] = dgamma, dbeta, dbias partials.
+// stats (int64, >= 2 (M + 128) N / 64, zeroed once) is the row-statistic exchange, cnt (int32 [2],
+// zeroed once, self-maintained) the launch epoch / done counter, err (int32) the timeout flag.
+// Returns the number of row blocks (colpart rows).
+int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::Tensor& C,
+                const c10::optional<at::Tensor>& bias, const at::Tensor& res, const at::Tensor& gamma,
+                const c10::optional<at::Tensor>& beta, const at::Tensor& mean, const at::Tensor& rstd,
+                const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& dx,
+                const c10::optional<at::Tensor>& colpart, const at::Tensor& stats, const at::Tensor& cnt,
+                const at::Tensor& err, double eps, const c10::optional<at::Tensor>& seed, int64_t site, int64_t thr,
+                double dscale, const c10::optional<at::Tensor>& row_map, int64_t cfg) {
+  need(A, at::kBFloat16, "A");
+  need(Bt, at::kBFloat16, "Bt");
+  need(C, at::kBFloat16, "C");
+  need(res, at::kBFloat16, "res");
+  need(gamma, at::kFloat, "gamma");
+  need(mean, at::kFloat, "mean");
+  need(rstd, at::kFloat, "rstd");
+  need(stats, at::kLong, "stats");
+  need(cnt, at::kInt, "cnt");
+  need(err, at::kInt, "err");
+  TORCH_CHECK(A.dim() == 2 && Bt.dim() == 2 && C.dim() == 2 && res.dim() == 2, "gemm_ln operands must be 2-D");
+  const int64_t M = A.size(0), K = A.size(1), N = Bt.size(0);
+  TORCH_CHECK(M > 0 && Bt.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_ln: shape mismatch");
+  TORCH_CHECK(res.size(0) == M && res.size(1) == N, "gemm_ln: res must be [M, N]");
+  TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && N <= 2048, "gemm_ln: K % 64, N % 64 and N <= 2048 required");
+  TORCH_CHECK(gamma.numel() == N, "gemm_ln: gamma of size N required");
+  TORCH_CHECK(mean.numel() >= M && rstd.numel() >= M, "gemm_ln: mean / rstd need M entries");
+  TORCH_CHECK(stats.numel() >= 2 * (M + 128) * (N / 64), "gemm_ln: stats too small");
+  TORCH_CHECK(cnt.numel() >= 2 && err.numel() >= 1, "gemm_ln: counters too small");
+  need_opt(bias, at::kFloat, "bias");
+  need_opt(beta, at::kFloat, "beta");
+  need_opt(z, at::kBFloat16, "z");
+  need_opt(dx, at::kBFloat16, "dx");
+  need_opt(colpart, at::kFloat, "colpart");
+  need_opt(row_map, at::kInt, "row_map");
+  const bool has_z = z.has_value() && z->defined();
+  if (has_z) TORCH_CHECK(z->size(0) == M && z->size(1) == N, "gemm_ln: z must be [M, N]");
+  if (!bwd) {
+    TORCH_CHECK(bias.has_value() && bias->defined() && bias->numel() == N, "gemm_ln: bias of size N required");
+    TORCH_CHECK(beta.has_value() && beta->defined() && beta->numel() == N, "gemm_ln: beta of size N required");
+  } else {
+    TORCH_CHECK(has_z, "gemm_ln backward needs the pre-LN sum z");
+    TORCH_CHECK(colpart.has_value() && colpart->defined() && colpart->numel() >= ((M + 63) / 64) * 3 * N,
+                "gemm_ln backward: colpart needs ceil(M/64) x 3N floats");
+    if (thr) TORCH_CHECK(dx.has_value() && dx->defined() && dx->size(0) == M && dx->size(1) == N,
+                         "gemm_ln backward with dropout needs dx [M, N]");
+  }
+  if (row_map.has_value() && row_map->defined()) TORCH_CHECK(row_map->numel() >= M, "gemm_ln: row_map needs M entries");
+  FdLnEpi ln{};
+  ln.gamma = gamma.data_ptr<float>();
+  ln.beta = ptr<float>(beta);
+  ln.mean = mean.data_ptr<float>();
+  ln.rstd = rstd.data_ptr<float>();
+  ln.z = ptr<uint16_t>(z);
+  ln.dx = ptr<uint16_t>(dx);
+  ln.colpart = ptr<float>(colpart);
+  ln.stats = reinterpret_cast<uint64_t*>(stats.data_ptr());
+  ln.cnt = cnt.data_ptr<int>();
+  ln.err = err.data_ptr<int>();
+  ln.eps = (float)eps;
+  ln.thr = (uint32_t)thr;
+  ln.site = (uint32_t)site;
+  ln.dscale = (float)dscale;
+  if (thr) {
+    TORCH_CHECK(seed.has_value() && seed->defined(), "gemm_ln: dropout needs the seed tensor");
+    ln.seed_ptr = seedp(*seed);
+    ln.row_map = ptr<int>(row_map);
+  }
+  const int rc = fd_gemm_ln(bwd ? 1 : 0, A.data_ptr(), Bt.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
+                            ptr<float>(bias), res.data_ptr(), (int)N, &ln, (int)cfg, stream());
+  TORCH_CHECK(rc > 0, "gemm_ln: kernel launcher rejected arguments (rc=", rc, ")");
+  return rc;
+}
+
 // Finish deferred split-K weight gradients: out_i (+)= sum_z slabs_i[z] (z order), one launch.
 void splitk_reduce_batched(const std::vector<at::Tensor>& slabs, const std::vector<at::Tensor>& outs,
                            const std::vector<int64_t>& splits, const std::vector<int64_t>& accumulate) {
@@ -562,8 +643,11 @@ int64_t ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at
             const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dz, const c10::optional<at::Tensor>& dx,
             const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
             const c10::optional<at::Tensor>& dbias, const at::Tensor& work, const at::Tensor& seed, int64_t site,
-            int64_t thr, double dscale, bool accumulate, const c10::optional<at::Tensor>& row_map, bool defer) {
-  // returns the number of [3][D] partial rows written to `work` (a deferred colsum job reduces them)
+            int64_t thr, double dscale, bool accumulate, const c10::optional<at::Tensor>& row_map, bool defer,
+            bool zin) {
+  // returns the number of [3][D] partial rows written to `work` (a deferred colsum job reduces them);
+  // zin: x is the saved pre-LN sum z (fused-LN forward), no residual
+  TORCH_CHECK(!zin || !(r.has_value() && r->defined()), "ln_bwd: zin takes no residual");
   need(dy, at::kBFloat16, "dy");
   need(x, at::kBFloat16, "x");
   need_opt(r, at::kBFloat16, "r");
@@ -585,7 +669,7 @@ int64_t ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at
                      rstd.data_ptr<float>(), dz.data_ptr(), ptr<void>(dx), ptr<float>(dgamma), ptr<float>(dbeta),
                      ptr<float>(dbias), work.data_ptr<float>(), (int)T, (int)D, seedp(seed), (uint32_t)site,
                      (uint32_t)thr, (float)dscale, accumulate ? 1 : 0, map_ptr(row_map, T), defer ? 1 : 0, &nblk,
-                     stream()),
+                     zin ? 1 : 0, stream()),
            "ln_bwd");
   return nblk;
 }
@@ -867,6 +951,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_dw2", &gemm_dw2);
   m.def("gemm_dw", &gemm_dw);
+  m.def("gemm_ln", &gemm_ln, py::arg("bwd"), py::arg("A"), py::arg("Bt"), py::arg("C"), py::arg("bias"),
+        py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("rstd"), py::arg("z"),
+        py::arg("dx"), py::arg("colpart"), py::arg("stats"), py::arg("cnt"), py::arg("err"), py::arg("eps"),
+        py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("row_map"),
+        py::arg("cfg") = -1);
   m.def("gemm_dw_batch", &gemm_dw_batch, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("accumulate"),
         py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1);
   m.def("gemm_colsum", &gemm_colsum, py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("aux"),

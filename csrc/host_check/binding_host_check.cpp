@@ -120,6 +120,36 @@ int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const
   (void)cfg;
   return 0;
 }
+int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
+               const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t) {
+  ++hc::calls;
+  const int bm = cfg == 13 ? 64 : 128;
+  const long long tm = (M + bm - 1) / bm, mn = (long long)M * N;
+  hc::span(A, (long long)M * K * 2, "gemm_ln A");
+  hc::span(Bt, (long long)N * K * 2, "gemm_ln Bt");
+  hc::span(C, mn * 2, "gemm_ln C");
+  hc::span(res, (long long)M * ldres * 2, "gemm_ln res");
+  hc::span(ln->gamma, (long long)N * 4, "gemm_ln gamma");
+  hc::span(ln->mean, (long long)M * 4, "gemm_ln mean");
+  hc::span(ln->rstd, (long long)M * 4, "gemm_ln rstd");
+  hc::span(ln->stats, tm * (N / 64) * 2 * bm * 8, "gemm_ln stats");
+  hc::span(ln->cnt, 2 * 4, "gemm_ln cnt");
+  hc::span(ln->err, 4, "gemm_ln err");
+  if (bwd) {
+    hc::span(ln->z, mn * 2, "gemm_ln z");
+    hc::span(ln->colpart, tm * 3 * N * 4, "gemm_ln colpart");
+    if (ln->thr) hc::span(ln->dx, mn * 2, "gemm_ln dx");
+  } else {
+    hc::span(bias, (long long)N * 4, "gemm_ln bias");
+    hc::span(ln->beta, (long long)N * 4, "gemm_ln beta");
+    hc::opt_span(ln->z, mn * 2, "gemm_ln z");
+  }
+  if (ln->thr) {
+    hc::span(ln->seed_ptr, 4, "gemm_ln seed");
+    hc::opt_span(ln->row_map, (long long)M * 4, "gemm_ln row_map");
+  }
+  return (int)tm;
+}
 int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
                              const int* splits, const int*, hipStream_t) {
   ++hc::calls;
@@ -194,7 +224,7 @@ int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* bet
 int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean, const float* rstd,
               void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work, int T, int D,
               const uint32_t* seed, uint32_t, uint32_t, float, int, const int* row_map, int, int* nblk_out,
-              hipStream_t) {
+              int, hipStream_t) {
   ++hc::calls;
   const long long n = (long long)T * D;
   hc::span(dy, n * 2, "ln bwd dy");
@@ -459,16 +489,41 @@ int main() {
     auto dz = T_({Tn, D}, bf), dx = T_({Tn, D}, bf), dg = T_({D}, f32), db = T_({D}, f32), dbias = T_({D}, f32);
     auto work = T_({336 * 3 * D}, f32);
     expect_ok("ln bwd", [&] { ln_bwd(x, x, r, ga, mean, rstd, dz, dx, dg, db, dbias, work, seed, 17, 429496730, 1.1,
-                                     false, rm, true); });
+                                     false, rm, true, false); });
     auto small = T_({100 * 3 * D}, f32);
     expect_reject("ln bwd work", [&] { ln_bwd(x, x, r, ga, mean, rstd, dz, dx, dg, db, dbias, small, seed, 17, 0, 1.0,
-                                              false, none, false); });
+                                              false, none, false, false); });
     expect_reject("ln bwd dx with dropout", [&] { ln_bwd(x, x, r, ga, mean, rstd, dz, none, dg, db, dbias, work, seed,
-                                                         17, 429496730, 1.1, false, none, false); });
+                                                         17, 429496730, 1.1, false, none, false, false); });
+    expect_ok("ln bwd from z", [&] { ln_bwd(x, x, none, ga, mean, rstd, dz, dx, dg, db, dbias, work, seed, 17, 429496730,
+                                            1.1, false, rm, true, true); });
+    expect_reject("ln bwd z + residual", [&] { ln_bwd(x, x, r, ga, mean, rstd, dz, dx, dg, db, dbias, work, seed, 17, 0,
+                                                      1.0, false, none, false, true); });
     auto g2 = T_({1024}, f32);
     expect_reject("ln fwd D", [&] { ln_fwd(x, r, g2, g2, y, mean, rstd, 1e-12, seed, 17, 0, 1.0, none); });
     auto rm_bad = T_({10}, i32);
     expect_reject("ln fwd row_map", [&] { ln_fwd(x, r, ga, be, y, mean, rstd, 1e-12, seed, 17, 0, 1.0, rm_bad); });
+    // LayerNorm fused into the N = 768 GEMM (forward: out_lin / lin2; backward: the dX GEMM)
+    auto a = T_({Tn, 3072}, bf), wt = T_({D, 3072}, bf), bias = T_({D}, f32), z = T_({Tn, D}, bf);
+    auto stats = T_({2 * (Tn + 128) * (D / 64)}, i64), cnt = T_({2}, i32), err = T_({1}, i32);
+    auto cp = T_({((Tn + 63) / 64) * 3 * D}, f32);
+    expect_ok("gemm_ln fwd", [&] { gemm_ln(false, a, wt, y, bias, r, ga, be, mean, rstd, z, none, none, stats, cnt, err,
+                                           1e-12, seed, 17, 429496730, 1.1, rm, -1); });
+    expect_ok("gemm_ln bwd", [&] { gemm_ln(true, a, wt, dz, none, r, ga, none, mean, rstd, z, dx, cp, stats, cnt, err,
+                                           1e-12, seed, 17, 429496730, 1.1, rm, -1); });
+    expect_reject("gemm_ln bwd without z", [&] { gemm_ln(true, a, wt, dz, none, r, ga, none, mean, rstd, none, dx, cp,
+                                                         stats, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1); });
+    expect_reject("gemm_ln bwd dropout without dx", [&] {
+      gemm_ln(true, a, wt, dz, none, r, ga, none, mean, rstd, z, none, cp, stats, cnt, err, 1e-12, seed, 17, 429496730,
+              1.1, rm, -1); });
+    auto stats_small = T_({100}, i64);
+    expect_reject("gemm_ln stats size", [&] { gemm_ln(false, a, wt, y, bias, r, ga, be, mean, rstd, z, none, none,
+                                                      stats_small, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1); });
+    expect_reject("gemm_ln fwd without beta", [&] { gemm_ln(false, a, wt, y, bias, r, ga, none, mean, rstd, z, none,
+                                                            none, stats, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1); });
+    auto cp_small = T_({3 * D}, f32);
+    expect_reject("gemm_ln colpart size", [&] { gemm_ln(true, a, wt, dz, none, r, ga, none, mean, rstd, z, dx, cp_small,
+                                                        stats, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1); });
   }
   // ---- head (+ fused distillation loss)
   {

@@ -32,3 +32,31 @@ struct FdDwProb {
   int tile0;          // filled by the launcher
   int accumulate;
 };
+
+// LayerNorm fused into an N = hidden GEMM (gemm.hip gemm_ln_kernel).  The column tiles of one
+// row block exchange per-row partial statistics through tagged granules in `stats`, so every
+// tile normalises its own slice from its accumulators.
+//   forward  (out_lin + sa_layer_norm, lin2 + output_layer_norm):
+//     z = dropout(acc + bias) + res  (bf16, kept for the backward);  C = LN(z) * gamma + beta
+//   backward (the dX GEMM that produces the LN output gradient dy = acc + res):
+//     C = dz = rstd * (gamma dy - mean(gamma dy) - xhat mean(gamma dy xhat)),  xhat from z;
+//     dx = dropout'(dz) (the producer's output gradient);  per-row-block column partials of
+//     dgamma = sum dy xhat, dbeta = sum dy, dbias = sum dx into colpart[tiles_m][3][N].
+struct FdLnEpi {
+  const float* gamma;
+  const float* beta;      // forward only
+  float* mean;            // [M] forward: out; backward: in
+  float* rstd;
+  uint16_t* z;            // [M][N] bf16 pre-LN sum: forward out (nullable), backward in
+  uint16_t* dx;           // backward: dropout-masked gradient (nullable without dropout)
+  float* colpart;         // backward: [tiles_m][3][N]
+  uint64_t* stats;        // [tiles_m][tiles_n][2][BM] {tag, value} granules (forward mean / M2,
+                          // backward s1 / s2 per row); zeroed once
+  int* cnt;               // [2]: launch epoch, done-block counter (zeroed once, self-maintained)
+  int* err;               // set nonzero if a row-block rendezvous timed out
+  const uint32_t* seed_ptr;
+  uint32_t site, thr;     // dropout (thr == 0: none), hashed like norm.hip's ln kernels
+  float dscale;
+  const int* row_map;     // packed row -> padded row (dropout hash only; nullable)
+  float eps;
+};

@@ -43,6 +43,8 @@ enum Epi : int {
   EPI_GELU_BWD = 3,   // C(bf16) = acc * gelu'(aux[m][n])
   EPI_ADD = 4,        // C(bf16) = acc + res[m][n]
   EPI_F32 = 5,        // C(fp32 slab z) = acc
+  EPI_LN = 6,         // C(bf16) = LN(dropout(acc + bias) + res)    (p.ln; gemm_ln_kernel only)
+  EPI_LN_BWD = 7,     // C(bf16) = LN backward of dy = acc + res    (p.ln; gemm_ln_kernel only)
 };
 
 struct GemmParams {
@@ -77,6 +79,7 @@ struct GemmParams {
   // the FFN activation g = gelu(u) next to its consumer (lin2's weight gradient) instead of
   // the forward keeping it: bitwise the forward's values (same bf16 u, same gelu_erf).
   bf16_t* aux_out;
+  FdLnEpi ln;            // EPI_LN / EPI_LN_BWD (adam_epi.h)
 };
 
 constexpr int BKT = 64;
@@ -177,10 +180,11 @@ struct Operand {
 template <int EPI, int BM, int BN>
 struct EpiTraits {
   static constexpr bool ELEM = (EPI == EPI_ADD || EPI == EPI_GELU_BWD);
+  static constexpr bool LN = (EPI == EPI_LN || EPI == EPI_LN_BWD);
   // fp32 weight-gradient tiles too large to stage in LDS (256 x 192, 256 x 256) are finished
   // straight from the accumulators (direct_f32_epilogue): 16-byte stores per lane
   static constexpr bool DIRECT = EPI == EPI_F32 && BM * (BN * 4 + 16) > LDS_MAX;
-  static constexpr bool F32S = (EPI == EPI_F32 && !DIRECT) || (ELEM && BM * (BN * 4 + 16) <= LDS_MAX);
+  static constexpr bool F32S = (EPI == EPI_F32 && !DIRECT) || ((ELEM || LN) && BM * (BN * 4 + 16) <= LDS_MAX);
   static constexpr int ES = F32S ? 4 : 2;
   static constexpr int BYTES = DIRECT ? 0 : BM * (BN * ES + 16);
 };
@@ -443,6 +447,269 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
   }
 }
 
+// ---------------------------------------------------------------- LayerNorm epilogues
+// EPI_LN / EPI_LN_BWD (FdLnEpi, adam_epi.h).  The tile is parked in LDS as fp32, then CPR
+// consecutive lanes own one tile row (8 columns each) for the element math; the row's two
+// partial statistics over this tile's BN columns reduce in a CPR-lane butterfly (every lane
+// ends with the same bits) and are published to stats[tm][tn][2][row].  Every tile of the row
+// block then reads all tiles_n partials and merges them in the same fixed order -- so each
+// normalises its slice with bitwise the same row mean / rstd.
+//
+// Exchange (no device-scope fence -- a full L2 writeback per block on the 8 non-coherent XCD
+// L2s; no arrival counter): each statistic is an 8-byte granule {tag, value} written by ONE
+// agent-scope relaxed atomic store (global store with the coherence bit, not kept in the XCD's
+// L2), and the readers poll the granules themselves with agent-scope atomic loads until every
+// tag is this launch's -- the data is the flag, so there is nothing to order.  The tag is the
+// launch epoch cnt[0] + 1, read at the start; the last block to finish (done counter cnt[1])
+// advances cnt[0], so stale granules of earlier launches never match (stats start zeroed).
+// Progress: a row block's tiles are consecutive logical tiles, walked in order per XCD
+// (xcd_remap); the poll is bounded regardless (ln.err flags a timeout, no hang).
+DEV void st_gran(uint64_t* p, uint32_t tag, float v) {
+  __hip_atomic_store(p, ((uint64_t)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV uint64_t ld_gran(uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV float gran_val(uint64_t g) { return __uint_as_float((uint32_t)g); }
+
+template <int CPR>
+DEV float row_sum(float v) {  // butterfly over the CPR lanes of a row: identical bits in each
+#pragma unroll
+  for (int o = 1; o < CPR; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// The last block of the launch to get here advances the epoch for the next launch.
+DEV void ln_done(const FdLnEpi& L, uint32_t tag, int tid) {
+  if (tid == 0 &&
+      __hip_atomic_fetch_add(L.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+    __hip_atomic_store(L.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(L.cnt, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+DEV void load8f(const float* p, float (&f)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+DEV void unpack8bf(const uint4& u, float (&f)[8]) {
+  f[0] = lo_bf(u.x); f[1] = hi_bf(u.x); f[2] = lo_bf(u.y); f[3] = hi_bf(u.y);
+  f[4] = lo_bf(u.z); f[5] = hi_bf(u.z); f[6] = lo_bf(u.w); f[7] = hi_bf(u.w);
+}
+DEV uint4 pack8bf(const float (&f)[8]) {
+  return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
+}
+
+constexpr int LN_MAXK = 4;  // column tiles per row block <= LN_MAXK * (BN / 8)
+
+template <int BM, int BN, int TM, int TN, bool BWD, int NT>
+DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int tm, int tn,
+                     int wr, int wc, int lane, int tid) {
+  constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int LDC = BN * 4 + 16;
+  constexpr int CPR = BN / 8;            // lanes per row (8 columns each)
+  constexpr int IT = BM * CPR / NT;      // rows per thread
+  static_assert(CPR >= 2 && CPR <= 64 && (CPR & (CPR - 1)) == 0 && NT % CPR == 0 && IT * NT == BM * CPR, "ln tile");
+  const FdLnEpi& L = p.ln;
+  const int m0 = tm * BM, n0 = tn * BN, tiles_n = p.N / BN, N = p.N;
+  const int cc = tid % CPR, n = n0 + 8 * cc;
+  // operands of the element math, issued before the tile is parked so their latency overlaps it
+  const uint32_t tag = (uint32_t)__hip_atomic_load(L.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  uint4 res_v[IT], z_v[IT];
+  float mrow[IT], rrow[IT];
+  int hrow_v[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int mc = min(m0 + (tid + it * NT) / CPR, p.M - 1);
+    res_v[it] = *reinterpret_cast<const uint4*>(p.res + (size_t)mc * p.ldres + n);
+    if constexpr (BWD) {
+      z_v[it] = *reinterpret_cast<const uint4*>(L.z + (size_t)mc * N + n);
+      mrow[it] = L.mean[mc];
+      rrow[it] = L.rstd[mc];
+    }
+    hrow_v[it] = (L.thr && L.row_map) ? L.row_map[mc] : mc;
+  }
+  float g[8];
+  load8f(L.gamma + n, g);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int r = wr * TM + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int c = wc * TN + j * 16 + 4 * (lane >> 4);
+      float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      if constexpr (!BWD) {
+        const float4 b = *reinterpret_cast<const float4*>(p.bias + n0 + c);
+        v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+      }
+      *reinterpret_cast<float4*>(smem + r * LDC + c * 4) = v;
+    }
+  }
+  __syncthreads();
+  const bool drop = L.thr != 0;
+  const uint32_t seed = drop ? hash32(L.seed_ptr[0], L.site) : 0u;
+  uint64_t* stats = L.stats + (size_t)(tm * tiles_n) * 2 * BM;  // [tn][2][BM] of this row block
+  float zv[IT][8], xv[IT][8];  // forward: z;  backward: gamma dy (zv) and xhat (xv)
+  float cg[8] = {}, cb[8] = {};  // backward column partials: dgamma, dbeta
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int r = (tid + it * NT) / CPR, m = m0 + r;
+    float v[8];
+    load8f(reinterpret_cast<const float*>(smem + r * LDC) + 8 * cc, v);
+    float rr[8];
+    unpack8bf(res_v[it], rr);
+    if constexpr (!BWD) {
+      if (drop) {
+        const size_t hrow = (size_t)(unsigned)hrow_v[it];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[e] = drop_keep(seed, (uint32_t)(hrow * N + n + e), L.thr) ? v[e] * L.dscale : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += rr[e];
+      // the normalisation runs on the bf16-rounded sum: exactly what the backward re-reads
+      // (stored after the rendezvous: the statistics publish drains only their own stores)
+      z_v[it] = pack8bf(v);
+      unpack8bf(z_v[it], zv[it]);
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += zv[it][e];
+      const float mt = row_sum<CPR>(s) * (1.f / BN);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = zv[it][e] - mt; q += d * d; }
+      q = row_sum<CPR>(q);
+      if (cc == 0) { st_gran(stats + (size_t)tn * 2 * BM + r, tag, mt); st_gran(stats + (size_t)(tn * 2 + 1) * BM + r, tag, q); }
+    } else {
+      float zz[8];
+      unpack8bf(z_v[it], zz);
+      const float mean = mrow[it], rstd = rrow[it];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dy = v[e] + rr[e];
+        const float xh = (zz[e] - mean) * rstd;
+        xv[it][e] = xh;
+        zv[it][e] = g[e] * dy;
+        s1 += zv[it][e];
+        s2 += zv[it][e] * xh;
+        if (m < p.M) { cg[e] += dy * xh; cb[e] += dy; }
+      }
+      s1 = row_sum<CPR>(s1);
+      s2 = row_sum<CPR>(s2);
+      if (cc == 0) { st_gran(stats + (size_t)tn * 2 * BM + r, tag, s1); st_gran(stats + (size_t)(tn * 2 + 1) * BM + r, tag, s2); }
+    }
+  }
+  // this lane's share of the tiles_n partials of its rows (tiles cc, cc + CPR, ...): poll the
+  // granules until every tag is this launch's (wave-uniform exit)
+  float2 st[IT][LN_MAXK];
+  {
+    int spins = 0;
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int r = (tid + it * NT) / CPR;
+#pragma unroll
+        for (int i = 0; i < LN_MAXK; ++i) {
+          const int t = cc + i * CPR;
+          if (t < tiles_n) {
+            const uint64_t a = ld_gran(stats + (size_t)t * 2 * BM + r);
+            const uint64_t b = ld_gran(stats + (size_t)(t * 2 + 1) * BM + r);
+            ok &= (uint32_t)(a >> 32) == tag && (uint32_t)(b >> 32) == tag;
+            st[it][i] = make_float2(gran_val(a), gran_val(b));
+          } else {
+            st[it][i] = make_float2(0.f, 0.f);
+          }
+        }
+      }
+      if (__all(ok) || (p.diag & 16)) break;  // (diag 16: timing only -- no wait, wrong statistics)
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 20)) {  // ~0.1 s: never in a healthy launch
+        if (lane == 0) __hip_atomic_fetch_or(L.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  float bt[8];
+  if constexpr (!BWD) load8f(L.beta + n, bt);
+  float cd[8] = {};  // backward: dbias partials
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int r = (tid + it * NT) / CPR, m = m0 + r;
+    // the row butterfly over the lanes' partials: a fixed order, the same in every tile
+    const float2 (&st_r)[LN_MAXK] = st[it];
+    const size_t off = (size_t)min(m, p.M - 1) * N + n;
+    if constexpr (!BWD) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < LN_MAXK; ++i) s += st_r[i].x;
+      const float mean = row_sum<CPR>(s) / tiles_n;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < LN_MAXK; ++i) {
+        const float d = st_r[i].x - mean;
+        if (cc + i * CPR < tiles_n) q += st_r[i].y + BN * d * d;
+      }
+      const float rstd = rsqrtf(row_sum<CPR>(q) / N + L.eps);
+      float y[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[e] = (zv[it][e] - mean) * rstd * g[e] + bt[e];
+      if (m < p.M) {
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + off) = pack8bf(y);
+        if (L.z) *reinterpret_cast<uint4*>(L.z + off) = z_v[it];
+        if (tn == 0 && cc == 0) { L.mean[m] = mean; L.rstd[m] = rstd; }
+      }
+    } else {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int i = 0; i < LN_MAXK; ++i) { a += st_r[i].x; b += st_r[i].y; }
+      const float s1 = row_sum<CPR>(a) / N, s2 = row_sum<CPR>(b) / N;
+      float dz[8], dx[8];
+      const size_t hrow = (size_t)(unsigned)hrow_v[it];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dz[e] = rrow[it] * (zv[it][e] - s1 - xv[it][e] * s2);
+        dx[e] = drop ? (drop_keep(seed, (uint32_t)(hrow * N + n + e), L.thr) ? dz[e] * L.dscale : 0.f) : dz[e];
+      }
+      if (m < p.M) {
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + off) = pack8bf(dz);
+        if (drop && L.dx) *reinterpret_cast<uint4*>(L.dx + off) = pack8bf(dx);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cd[e] += dx[e];
+      }
+    }
+  }
+  ln_done(L, tag, tid);
+  if constexpr (BWD) {
+    // column partials: lanes of a wave with the same column chunk (lane % CPR), then the waves
+    constexpr int NWV = NT / 64;
+    float* red = reinterpret_cast<float*>(smem);  // [3][NWV][BN]
+    __syncthreads();  // the staged tile is no longer read
+    auto park = [&](float (&a)[8], int w3) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+#pragma unroll
+        for (int o = CPR; o < 64; o <<= 1) a[e] += __shfl_xor(a[e], o, 64);
+      }
+      if (lane < CPR) {
+        float* dst = red + (w3 * NWV + (tid >> 6)) * BN + 8 * lane;
+        *reinterpret_cast<float4*>(dst) = make_float4(a[0], a[1], a[2], a[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(a[4], a[5], a[6], a[7]);
+      }
+    };
+    park(cg, 0);
+    park(cb, 1);
+    park(cd, 2);
+    __syncthreads();
+    for (int i = tid; i < 3 * BN; i += NT) {
+      const int w3 = i / BN, c = i % BN;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) v += red[(w3 * NWV + w) * BN + c];
+      L.colpart[((size_t)tm * 3 + w3) * N + n0 + c] = v;
+    }
+  }
+}
+
 // Scheduling hints for one K tile: the first 32-deep fragment set's ds_reads,
 // then each of its MFMAs followed by RPM of the second set's ds_reads (their
 // latency hides under the MFMA pipe), then the second set's MFMAs.
@@ -487,7 +754,9 @@ struct GemmCfg {
                                                                    : EpiTraits<EPI, BM, BN>::BYTES;
   static constexpr int SMEM = S * BUF > EPI_BYTES ? S * BUF : EPI_BYTES;
   // (the accumulator-direct fp32 epilogue serves only the all-layer weight-gradient launch)
-  static constexpr bool VALID = SMEM <= LDS_MAX && !EpiTraits<EPI, BM, BN>::DIRECT && (BKM || BN % 64 == 0) &&
+  static constexpr bool VALID = SMEM <= LDS_MAX && !EpiTraits<EPI, BM, BN>::DIRECT &&
+                                (!EpiTraits<EPI, BM, BN>::LN || EpiTraits<EPI, BM, BN>::F32S) &&
+                                (BKM || BN % 64 == 0) &&
                                 (AK || BM % 64 == 0) &&
                                 (BM / WM) % 16 == 0 && (BN / WN) % 16 == 0 &&
                                 OA::PER_WAVE * NW * 1024 == OA::BYTES && OB::PER_WAVE * NW * 1024 == OB::BYTES;
@@ -507,10 +776,10 @@ struct GemmGroup {
 #define FD_GEMM_SCHED 1
 #endif
 
-// One output tile of problem p: the K loop over the LDS-DMA ring, then the epilogue.
-// bid = the tile's index within p (walked in group-M order), slot = split-K arrival slot.
+// One output tile (tm, tn) of problem p: the K loop over the LDS-DMA ring, then the epilogue.
+// slot = split-K arrival slot.
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
-DEV void gemm_tile(const GemmParams& p, int bid, int slot, char* smem) {
+DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   using OA = typename G::OA;
   using OB = typename G::OB;
@@ -526,9 +795,6 @@ DEV void gemm_tile(const GemmParams& p, int bid, int slot, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / WN, wc = wid % WN;
-  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = p.N / BN;
-  int tm, tn;
-  tile_coords(bid, tiles_m, tiles_n, p.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = blockIdx.z * p.k_split;
   const int nk = p.k_split / BKT;
@@ -635,12 +901,23 @@ DEV void gemm_tile(const GemmParams& p, int bid, int slot, char* smem) {
       f32_epilogue<TM, BN, 64 * NW>(p, smem, LDC, m0 + band * TM, n0, tid, slot);
     }
     (void)direct_f32_epilogue<TM, TN>;
+  } else if constexpr (EpiTraits<EPI, BM, BN>::LN) {
+    __syncthreads();  // no wave still reads a ring slot
+    ln_epilogue<BM, BN, TM, TN, EPI == EPI_LN_BWD, 64 * NW>(p, acc, smem, tm, tn, wr, wc, lane, tid);
   } else {
     // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
     // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
     __syncthreads();
     staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid, slot);
   }
+}
+
+// bid = the tile's index within p, walked in group-M order
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+DEV void gemm_tile(const GemmParams& p, int bid, int slot, char* smem) {
+  int tm, tn;
+  tile_coords(bid, (p.M + BM - 1) / BM, p.N / BN, p.group_m, tm, tn);
+  gemm_tile_at<BM, BN, AK, BKM, EPI, WM, WN, S>(p, tm, tn, slot, smem);
 }
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
@@ -653,6 +930,17 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
   const GemmParams& p = second ? grp.q : p0;
   if (second) bid -= grp.ntiles0;
   gemm_tile<BM, BN, AK, BKM, EPI, WM, WN, S>(p, bid, slot, smem);
+}
+
+// LayerNorm-fused NT GEMM (EPI_LN / EPI_LN_BWD): the tiles of a row block are consecutive
+// logical tiles (row-major tile order), so after the XCD remap they run on one XCD, in order.
+template <int BM, int BN, int EPI, int WM, int WN, int S>
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_ln_kernel(GemmParams p) {
+  using G = GemmCfg<BM, BN, true, true, EPI, WM, WN, S>;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  const int tiles_n = p.N / BN;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  gemm_tile_at<BM, BN, true, true, EPI, WM, WN, S>(p, lid / tiles_n, lid % tiles_n, 0, smem);
 }
 
 // ---------------------------------------------------------------- all-layer weight gradients
@@ -999,7 +1287,7 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
                int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
                long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st) {
-  if (K % BKT != 0 || N % 64 != 0 || M <= 0 || kind < 0 || kind > 2) return 1;
+  if (K % BKT != 0 || N % 64 != 0 || M <= 0 || kind < 0 || kind > 2 || epi >= EPI_LN) return 1;
   if (aux_out && (epi != EPI_GELU_BWD || kind == 2)) return 7;
   GemmParams p{};
   p.aux_out = (bf16_t*)aux_out;
@@ -1217,6 +1505,51 @@ int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* out
     hipLaunchKernelGGL(splitk_reduce_batched_kernel, dim3(blocks), dim3(256), 0, st, rb);
   }
   return 0;
+}
+
+
+// LayerNorm-fused NT GEMM: C[M][N] = epilogue(A[M][K] Bt[N][K]^T) with N = the hidden size
+// (FdLnEpi, adam_epi.h).  bwd = 0: EPI_LN (bias + dropout + residual + LN), 1: EPI_LN_BWD.
+// cfg < 0: FD_GEMM_LN_CFG or 24 (128 x 64, 8 waves, two K tiles per barrier -- the N = 768
+// configuration of the plain GEMM).  Returns the number of row blocks (the colpart rows),
+// or a negative code on an unsupported shape (nothing launched).
+int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
+               const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t st) {
+  if (M <= 0 || K % BKT || N % 64 || !ln || !res || (!bwd && !bias)) return -1;
+  int id = cfg;
+  if (id < 0) {
+    static const int env = [] { const char* e = getenv("FD_GEMM_LN_CFG"); return e ? atoi(e) : -1; }();
+    id = env >= 0 ? env : 24;
+  }
+  const int bm = id == 13 ? 64 : 128, bn = 64;
+  if (N / bn > LN_MAXK * (bn / 8)) return -2;
+  GemmParams p{};
+  p.A = (const bf16_t*)A; p.B = (const bf16_t*)Bt; p.C = C;
+  p.M = M; p.N = N; p.K = K; p.lda = K; p.ldb = K; p.ldc = N;
+  p.bias = bias; p.res = (const bf16_t*)res; p.ldres = ldres;
+  p.k_split = K;
+  p.ln = *ln;
+  {
+    static const int diag = [] { const char* e = getenv("FD_GEMM_LN_DIAG"); return e ? atoi(e) : 0; }();
+    p.diag = diag;  // profiling only: 16 = no row-block rendezvous (wrong statistics)
+  }
+  const int tiles_m = (M + bm - 1) / bm;
+  const dim3 grid(tiles_m * (N / bn));
+  auto go = [&](auto kern, int threads) { hipLaunchKernelGGL(kern, grid, dim3(threads), 0, st, p); };
+#define FD_LN_CASE(ID, BM_, BN_, WM_, WN_, S_)                                              \
+  case ID:                                                                                 \
+    if (bwd) go(gemm_ln_kernel<BM_, BN_, EPI_LN_BWD, WM_, WN_, S_>, 64 * WM_ * WN_);       \
+    else go(gemm_ln_kernel<BM_, BN_, EPI_LN, WM_, WN_, S_>, 64 * WM_ * WN_);               \
+    break;
+  switch (id) {
+    FD_LN_CASE(24, 128, 64, 4, 2, 6)
+    FD_LN_CASE(0, 128, 64, 2, 2, 3)
+    FD_LN_CASE(18, 128, 64, 4, 2, 3)
+    FD_LN_CASE(13, 64, 64, 2, 2, 3)
+    default: return -3;
+  }
+#undef FD_LN_CASE
+  return tiles_m;
 }
 
 }  // extern "C"

@@ -38,6 +38,9 @@ struct LnArgs {
   // packed (unpadded) rows: row -> row of the padded [B*S] layout, used only to index the
   // dropout hash so a packed batch draws exactly the padded batch's masks (nullable)
   const int* row_map;
+  // backward: x already IS the pre-LN sum z (saved by the LayerNorm-fused GEMM), r unused;
+  // the dropout mask is still re-drawn for dx
+  int zin;
 };
 
 // Half-wave row layout for D = 768: 32 lanes own a row, lane hl holds columns
@@ -78,7 +81,7 @@ DEV void ln_load_sum(const LnArgs& a, int row, int hl, bool drop, uint32_t seed,
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const bool k = drop_keep(seed, (uint32_t)(off + e), a.thr);
-        z[c][e] = k ? z[c][e] * a.dscale : 0.f;
+        if (!a.zin) z[c][e] = k ? z[c][e] * a.dscale : 0.f;
         if (!k) keep &= ~(1u << (8 * c + e));
       }
     }
@@ -689,9 +692,10 @@ int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* bet
 int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, const float* mean,
               const float* rstd, void* dz, void* dx, float* dgamma, float* dbeta, float* dbias, float* work,
               int T, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
-              int accumulate, const int* row_map, int defer, int* nblk_out, hipStream_t st) {
-  if (D != 768) return 1;
+              int accumulate, const int* row_map, int defer, int* nblk_out, int zin, hipStream_t st) {
+  if (D != 768 || (zin && r)) return 1;
   LnArgs a{};
+  a.zin = zin;
   a.dy = (const bf16_t*)dy; a.x = (const bf16_t*)x; a.r = (const bf16_t*)r; a.gamma = gamma;
   a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = (bf16_t*)dz; a.dx = (bf16_t*)dx; a.part = work;
   a.T = T; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.row_map = row_map;

@@ -269,6 +269,9 @@ class DDoSClassifier(nn.Module):
         # HIP path: the backward re-creates the FFN activation gelu(u) in the GELU' dX epilogue
         # instead of the forward keeping it (FD_REMAT_GELU=0: keep it)
         self.remat_gelu = os.environ.get("FD_REMAT_GELU", "1") != "0"
+        # HIP path: LayerNorm fused into the N = 768 GEMMs (RunCtx.fuse_ln; FD_FUSE_LN=0: the
+        # separate LN kernels).  Hidden sizes the fused epilogue does not cover fall back.
+        self.fuse_ln = os.environ.get("FD_FUSE_LN", "1") != "0"
         # HIP path: build the per-step W^T copies on a side stream concurrently with the forward.
         # Measured SLOWER on MI355X (2.48 vs 2.36 ms/step, profiles/r1_ab_transpose_overlap_slower.txt):
         # the memory-bound transposes stretch the concurrent forward GEMMs.  Off by default.
@@ -486,6 +489,7 @@ class DDoSClassifier(nn.Module):
             rc.dw_batch = []
         rc.fuse_colsum = self.fuse_colsum
         rc.remat_gelu = self.remat_gelu
+        rc.fuse_ln = self.fuse_ln and cfg.dim % 64 == 0 and cfg.dim <= 2048
         if (grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None
                 and not self.wgrad_stream and self.transposed_dx):
             rc.fused_adam = self.fused_opt

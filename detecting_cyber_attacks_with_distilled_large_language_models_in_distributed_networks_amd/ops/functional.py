@@ -14,7 +14,7 @@ Reference call stack mirrored: DistilBertModel.forward -> Embeddings ->
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Callable, Optional
 
 import torch
@@ -64,6 +64,12 @@ class RunCtx:
     # side stream that produced data the backward reads (the W^T copies): joined at the
     # first backward node (the head)
     join_stream: Optional["torch.cuda.Stream"] = None
+    # LayerNorm fused into the N = hidden GEMMs (csrc/kernels/gemm.hip gemm_ln_kernel): forward
+    # out_lin + sa_layer_norm and lin2 + output_layer_norm; backward sa_layer_norm inside the
+    # lin1 dX GEMM and block i-1's output_layer_norm inside block i's qkv dX GEMM
+    fuse_ln: bool = False
+    ln2_saved: dict = field(default_factory=dict)    # block -> its output LN's saved state
+    ln2_pending: dict = field(default_factory=dict)  # block -> (dz2, df) computed by block + 1
     # optimizer whose Adam step the weight-gradient GEMMs apply in their epilogues
     # (engine/optim.py ArenaAdam.fused_args; set only inside a training step's scope)
     fused_adam: Optional[object] = None
@@ -160,17 +166,30 @@ class LayerFn(torch.autograd.Function):
         p_a = rc.p_attn if rc.training else 0.0
         p_h = rc.p_hidden if rc.training else 0.0
         attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
+        grad = ctx.needs_input_grad[0]
         qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
         cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu)
-        ao = K.linear_fwd(cx, L["o_w"], L["o_b"])
-        h, m1, r1 = K.ln_fwd(ao, x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0)
-        g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
-        f = K.linear_fwd(g, L["l2_w"], L["l2_b"])
-        y, m2, r2 = K.ln_fwd(f, h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed, ffn_site, p_h, rc.row_map)
-        if ctx.needs_input_grad[0]:
+        if rc.fuse_ln:
+            # bias + (dropout) + residual + LayerNorm in the N = 768 GEMMs' epilogues; the
+            # backward reads the saved bf16 pre-LN sums z1 / z2 instead of ao / f
+            h, ao, m1, r1 = K.linear_ln_fwd(cx, L["o_w"], L["o_b"], x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0,
+                                            0.0, keep_z=grad)
+            g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
+            y, f, m2, r2 = K.linear_ln_fwd(g, L["l2_w"], L["l2_b"], h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed,
+                                           ffn_site, p_h, rc.row_map, keep_z=grad)
+            if grad:
+                rc.ln2_saved[idx] = (f, m2, r2, L, ffn_site, p_h)
+        else:
+            ao = K.linear_fwd(cx, L["o_w"], L["o_b"])
+            h, m1, r1 = K.ln_fwd(ao, x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0)
+            g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
+            f = K.linear_fwd(g, L["l2_w"], L["l2_b"])
+            y, m2, r2 = K.ln_fwd(f, h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed, ffn_site, p_h, rc.row_map)
+        if grad:
             ctx.save_for_backward(x)
+            # (fused LN: ao / f hold the pre-LN sums z1 / z2)
             ctx.acts = (qkv, cx, lse, ao, h, m1, r1, u, None if rc.remat_gelu else g, f, m2, r2)
-        ctx.L, ctx.rc, ctx.sites, ctx.p = L, rc, (attn_site, ffn_site), (p_a, p_h)
+        ctx.L, ctx.rc, ctx.sites, ctx.p, ctx.fused_ln = L, rc, (attn_site, ffn_site), (p_a, p_h), rc.fuse_ln
         return y
 
     @staticmethod
@@ -185,8 +204,14 @@ class LayerFn(torch.autograd.Function):
         wg = _WGrad(rc)  # dW / bias-sum work -> side stream, dX chain stays on the main stream
         # output_layer_norm(dropout(lin2) + h): dz2 -> residual grad of h, df -> lin2 output grad
         jobs = rc.colsum_jobs
-        dz2, df = K.ln_bwd(dy, f, h, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, rc.seed,
-                           ffn_site, p_h, acc, rc.row_map, jobs)
+        fused = ctx.fused_ln
+        pend = rc.ln2_pending.pop(ctx.idx, None) if fused else None
+        if pend is not None and pend[0].data_ptr() == dy.data_ptr():
+            dz2, df = pend  # done by block idx + 1's qkv dX GEMM (its returned "dx" IS dz2)
+        else:
+            # fused forward: f holds z2 (the pre-LN sum), the residual is already in it
+            dz2, df = K.ln_bwd(dy, f, None if fused else h, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf,
+                               G["l2_b"].buf, rc.seed, ffn_site, p_h, acc, rc.row_map, jobs, zin=fused)
         wt = L.get("wT") or {}
         # Adam fused into the grouped dW epilogues: the weights are updated in the middle of
         # this backward, so every later reader must use the W^T copies taken before the step
@@ -215,10 +240,14 @@ class LayerFn(torch.autograd.Function):
                 K.linear_dw(du, h, G["l1_w"].buf, acc)
             if not fuse_cs:
                 K.colsum(du, G["l1_b"].buf, acc, jobs)
-        dh = K.linear_dx(du, L["l1_w"], res=dz2, wt=wt.get("l1_w"))    # du W1 + dz2
-        # sa_layer_norm(out_lin + x)
-        dz1, _ = K.ln_bwd(dh, ao, x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf, G["o_b"].buf, rc.seed, 0,
-                          0.0, acc, None, jobs)
+        # sa_layer_norm(out_lin + x): dh = du W1 + dz2, then its LayerNorm backward
+        if fused and wt.get("l1_w") is not None:
+            dz1, _ = K.linear_dx_ln_bwd(du, wt["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
+                                        G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs)
+        else:
+            dh = K.linear_dx(du, L["l1_w"], res=dz2, wt=wt.get("l1_w"))
+            dz1, _ = K.ln_bwd(dh, ao, None if fused else x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
+                              G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, zin=fused)
         dcx = K.linear_dx(dz1, L["o_w"], wt=wt.get("o_w"))
         if not rc.group_dw and batch is None:
             wg.fork(dz1, cx)
@@ -235,7 +264,22 @@ class LayerFn(torch.autograd.Function):
             else:
                 K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
             K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
-        dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt.get("qkv_w"))
+        prev = rc.ln2_saved.get(ctx.idx - 1) if fused and wt.get("qkv_w") is not None else None
+        if prev is not None:
+            # dx = dqkv Wqkv + dz1 is block idx-1's output-LN gradient: finish that LayerNorm
+            # backward in this GEMM's epilogue and hand (dz2, df) to block idx-1
+            z2p, m2p, r2p, Lp, site_p, p_p = prev
+            Gp = Lp["sinks"]
+            acc_p = [Gp[k].accumulate() for k in ("ln2_w", "ln2_b", "l2_b")]
+            if len(set(acc_p)) != 1:
+                raise RuntimeError("output-LN gradient sinks out of step")
+            acc_p = acc_p[0]
+            dx, df_p = K.linear_dx_ln_bwd(dqkv, wt["qkv_w"], dz1, z2p, Lp["ln2_w"], m2p, r2p, Gp["ln2_w"].buf,
+                                          Gp["ln2_b"].buf, Gp["l2_b"].buf, rc.seed, site_p, p_p, acc_p, rc.row_map,
+                                          jobs)
+            rc.ln2_pending[ctx.idx - 1] = (dx, df_p)
+        else:
+            dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt.get("qkv_w"))
         for k in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_w", "ln1_b", "l1_w", "l1_b", "l2_b", "ln2_w", "ln2_b"):
             G[k].accumulate()
         del ctx.acts

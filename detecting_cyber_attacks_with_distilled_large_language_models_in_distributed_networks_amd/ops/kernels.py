@@ -267,8 +267,10 @@ def ln_fwd(x, r, gamma, beta, eps, seed, site, p, row_map=None):
 
 
 def ln_bwd(dy, x, r, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False, row_map=None,
-           jobs: Optional[list] = None):
-    """jobs: deferred-colsum list -> the dgamma/dbeta/dbias partials wait for ``colsum_flush``."""
+           jobs: Optional[list] = None, zin: bool = False):
+    """jobs: deferred-colsum list -> the dgamma/dbeta/dbias partials wait for ``colsum_flush``.
+    zin: ``x`` is the saved pre-LN sum z of a LayerNorm-fused GEMM (``r`` must be None); dropout
+    only masks the returned dx."""
     D = gamma.numel()
     T = x.numel() // D
     dz = torch.empty_like(x)
@@ -277,9 +279,82 @@ def ln_bwd(dy, x, r, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, acc
     key = "ln_part" if jobs is None else f"ln_part_job{len(jobs)}"
     ws = workspace(x.device, key, LN_BWD_PARTS * 3 * D)
     nblk = ext().ln_bwd(dy.contiguous(), x, r, gamma, mean, rstd, dz, dx, dgamma, dbeta, dbias, ws, seed, site, thr,
-                        sc, accumulate, row_map if thr else None, jobs is not None)
+                        sc, accumulate, row_map if thr else None, jobs is not None, zin)
     if jobs is not None:
         jobs.append((ws, [dgamma, dbeta, dbias], nblk, 3 * D, D, accumulate))
+    return dz, (dx if dx is not None else dz)
+
+
+# ------------------------------------------------------------------ LayerNorm fused into a GEMM
+LN_STATE_ROWS = 32768  # row capacity of the exchange state (grown if a call needs more)
+
+
+def _ln_state(device, M: int, N: int):
+    """(stats, cnt, err) of the LayerNorm-fused GEMM (csrc/kernels/gemm.hip gemm_ln_kernel):
+    the tagged row-statistic granules and [launch epoch, done-block counter].  Zeroed once; the
+    kernel keeps them consistent itself (graph replays reuse them)."""
+    key = (_dev_key(device), "ln_state", N)
+    st = _WS.get(key)
+    rows = max(M, LN_STATE_ROWS)
+    if st is None or st[3] < M:
+        if st is not None:
+            _WS_RETIRED.append(st)
+        st = (torch.zeros(2 * (rows + 128) * (N // 64), dtype=torch.int64, device=device),
+              torch.zeros(2, dtype=torch.int32, device=device),
+              torch.zeros(1, dtype=torch.int32, device=device), rows)
+        _WS[key] = st
+    return st[:3]
+
+
+def ln_error_flag(device, N: int = 768) -> int:
+    """Nonzero if a fused-LN launch's row-block rendezvous ever timed out (never expected)."""
+    st = _WS.get((_dev_key(device), "ln_state", N))
+    return 0 if st is None else int(st[2].item())
+
+
+def _dev_key(device) -> str:
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return str(d)
+
+
+def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, keep_z: bool = True):
+    """y = LN(dropout(x w^T + b) + res) in ONE launch (the N = hidden GEMM's epilogue does the
+    bias, dropout, residual and LayerNorm).  Returns (y, z, mean, rstd): z = the bf16 pre-LN sum
+    (what the backward reads; None with keep_z=False), mean / rstd fp32 per row."""
+    M, N = x.shape[0], w.shape[0]
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    z = torch.empty_like(y) if keep_z else None
+    mean = torch.empty(M, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+    thr, sc = _drop(p)
+    stats, cnt, err = _ln_state(x.device, M, N)
+    ext().gemm_ln(False, x, w, y, b, res, gamma, beta, mean, rstd, z, None, None, stats, cnt, err, eps, seed, site,
+                  thr, sc, row_map if thr else None)
+    return y, z, mean, rstd
+
+
+def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False,
+                     row_map=None, jobs: Optional[list] = None):
+    """LayerNorm backward fused into the dX GEMM that produces its output gradient:
+    dy = a wt^T + res, then (dz, dx) of y = LN(dropout(f) + r) from the saved z = dropout(f) + r
+    (dz: gradient of the pre-LN sum, i.e. of the residual input r; dx: of f, = dz without dropout).
+    dgamma / dbeta / dbias (+)= the column sums (deferred to ``colsum_flush`` with ``jobs``)."""
+    M, N = a.shape[0], wt.shape[0]
+    dz = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    thr, sc = _drop(p)
+    dx = torch.empty_like(dz) if thr else None
+    key = "ln_colpart" if jobs is None else f"ln_colpart_job{len(jobs)}"
+    ws = workspace(a.device, key, ((M + 63) // 64) * 3 * N)
+    stats, cnt, err = _ln_state(a.device, M, N)
+    nblk = ext().gemm_ln(True, a, wt, dz, None, res, gamma, None, mean, rstd, z, dx, ws, stats, cnt, err, 0.0, seed,
+                         site, thr, sc, row_map if thr else None)
+    job = (ws, [dgamma, dbeta, dbias], nblk, 3 * N, N, accumulate)
+    if jobs is not None:
+        jobs.append(job)
+    else:
+        colsum_flush([job])
     return dz, (dx if dx is not None else dz)
 
 
