@@ -56,10 +56,10 @@ int fd_comm_broadcast(void* comm, void* buf, long long count, int dtype, int roo
 int fd_comm_allgather(void* comm, const void* send, void* recv, long long count, int dtype, hipStream_t st);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                int rows, hipStream_t st);
+                int rows, uint64_t* dmask, hipStream_t st);
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx,
                 float* delta, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site,
-                uint32_t thr, float drop_scale, const int* cu, int rows, hipStream_t st);
+                uint32_t thr, float drop_scale, const int* cu, int rows, const uint64_t* dmask, hipStream_t st);
 int fd_mask_to_bias(const void* mask, int mask_bytes, float* bias, long n, hipStream_t st);
 int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, float* mean,
               float* rstd, int T, int D, float eps, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
@@ -567,13 +567,22 @@ const int* map_ptr(const c10::optional<at::Tensor>& m, int64_t T) {
   return m->data_ptr<int>();
 }
 
+// Dropout keep bits handed from the S <= 128 attention forward to its backward: int64
+// [B * H * 128 * 2] (used only by the S <= 128 kernels with dropout; nullable).
+void check_dmask(const c10::optional<at::Tensor>& dmask, int64_t B, int64_t S, int64_t H) {
+  if (!dmask.has_value() || !dmask->defined()) return;
+  need(*dmask, at::kLong, "dmask");
+  TORCH_CHECK(S <= 128 && dmask->numel() == B * H * 256, "attention: dmask needs S <= 128 and B*H*256 words");
+}
+
 void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
               int64_t B, int64_t S, int64_t H, const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
-              const c10::optional<at::Tensor>& cu) {
+              const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask) {
   need(qkv, at::kBFloat16, "qkv");
   need(kbias, at::kFloat, "kbias");
   need(ctx, at::kBFloat16, "ctx");
   need(lse, at::kFloat, "lse");
+  check_dmask(dmask, B, S, H);
   TORCH_CHECK(S % 64 == 0 && S <= 512, "attention: S must be a multiple of 64 and <= 512");
   const bool varlen = cu.has_value() && cu->defined();
   const int64_t rows = varlen ? qkv.numel() / (3 * H * 64) : B * S;
@@ -582,13 +591,15 @@ void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
   check_cu(cu, B, rows, ctx.numel() / (H * 64));
   check_rc(fd_attn_fwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(), (int)B,
                        (int)S, (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu),
-                       (int)rows, stream()),
+                       (int)rows, ptr<uint64_t>(dmask), stream()),
            "attn_fwd");
 }
 
 void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
               const at::Tensor& dctx, const at::Tensor& delta, const at::Tensor& dqkv, int64_t B, int64_t S, int64_t H,
-              const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& cu) {
+              const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& cu,
+              const c10::optional<at::Tensor>& dmask) {
+  check_dmask(dmask, B, S, H);
   need(qkv, at::kBFloat16, "qkv");
   need(kbias, at::kFloat, "kbias");
   need(ctx, at::kBFloat16, "ctx");
@@ -606,7 +617,8 @@ void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
   check_cu(cu, B, rows, ctx.numel() / (H * 64));
   check_rc(fd_attn_bwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(),
                        dctx.data_ptr(), delta.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)S, (int)H,
-                       seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), (int)rows, stream()),
+                       seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), (int)rows,
+                       ptr<uint64_t>(dmask), stream()),
            "attn_bwd");
 }
 

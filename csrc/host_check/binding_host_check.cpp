@@ -178,9 +178,10 @@ int fd_comm_allreduce(void*, const void*, void*, long long, int, int, hipStream_
 int fd_comm_broadcast(void*, void*, long long, int, int, hipStream_t) { return 0; }
 int fd_comm_allgather(void*, const void*, void*, long long, int, hipStream_t) { return 0; }
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H, const uint32_t* seed,
-                uint32_t, uint32_t, float, const int* cu, int rows, hipStream_t) {
+                uint32_t, uint32_t, float, const int* cu, int rows, uint64_t* dmask, hipStream_t) {
   ++hc::calls;
   const long long D = (long long)H * 64;
+  hc::opt_span(dmask, (long long)B * H * 256 * 8, "attn dmask");
   hc::span(qkv, rows * 3 * D * 2, "attn qkv");
   hc::span(ctx, rows * D * 2, "attn ctx");
   hc::span(lse, (long long)B * H * S * 4, "attn lse");
@@ -191,9 +192,10 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
 }
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx, float* delta,
                 void* dqkv, int B, int S, int H, const uint32_t* seed, uint32_t, uint32_t, float, const int* cu,
-                int rows, hipStream_t) {
+                int rows, const uint64_t* dmask, hipStream_t) {
   ++hc::calls;
   const long long D = (long long)H * 64;
+  hc::opt_span(dmask, (long long)B * H * 256 * 8, "attn bwd dmask");
   hc::span(qkv, rows * 3 * D * 2, "attn bwd qkv");
   hc::span(dqkv, rows * 3 * D * 2, "attn bwd dqkv");
   hc::span(ctx, rows * D * 2, "attn bwd ctx");
@@ -466,19 +468,25 @@ int main() {
     auto qkv = T_({rows, 3 * H * 64}, bf), kb = T_({B, S}, f32), ctx = T_({rows, H * 64}, bf);
     auto lse = T_({B, H, S}, f32), seed = T_({1}, i32), dctx = T_({rows, H * 64}, bf), delta = T_({B * H * S}, f32);
     auto dqkv = T_({rows, 3 * H * 64}, bf);
-    expect_ok("attn fwd", [&] { attn_fwd(qkv, kb, ctx, lse, B, S, H, seed, 16, 429496730, 1.1, none); });
-    expect_ok("attn bwd", [&] { attn_bwd(qkv, kb, ctx, lse, dctx, delta, dqkv, B, S, H, seed, 16, 0, 1.0, none); });
+    expect_ok("attn fwd", [&] { attn_fwd(qkv, kb, ctx, lse, B, S, H, seed, 16, 429496730, 1.1, none, none); });
+    expect_ok("attn bwd", [&] { attn_bwd(qkv, kb, ctx, lse, dctx, delta, dqkv, B, S, H, seed, 16, 0, 1.0, none, none); });
     auto cu = T_({B + 1}, i32), qv = T_({300, 3 * H * 64}, bf), cv = T_({300, H * 64}, bf);
-    expect_ok("attn fwd varlen", [&] { attn_fwd(qv, kb, cv, lse, B, S, H, seed, 16, 0, 1.0, cu); });
+    expect_ok("attn fwd varlen", [&] { attn_fwd(qv, kb, cv, lse, B, S, H, seed, 16, 0, 1.0, cu, none); });
     const int64_t S5 = 512;
     auto q5 = T_({2 * S5, 3 * H * 64}, bf), k5 = T_({2, S5}, f32), c5 = T_({2 * S5, H * 64}, bf), l5 = T_({2, H, S5}, f32);
-    expect_ok("attn fwd S=512", [&] { attn_fwd(q5, k5, c5, l5, 2, S5, H, seed, 16, 0, 1.0, none); });
-    expect_reject("attn S=576", [&] { attn_fwd(q5, k5, c5, l5, 2, 576, H, seed, 16, 0, 1.0, none); });
-    expect_reject("attn S % 64", [&] { attn_fwd(qkv, kb, ctx, lse, B, 100, H, seed, 16, 0, 1.0, none); });
-    expect_reject("attn lse size", [&] { attn_fwd(qkv, kb, ctx, l5, B, S, H, seed, 16, 0, 1.0, none); });
+    expect_ok("attn fwd S=512", [&] { attn_fwd(q5, k5, c5, l5, 2, S5, H, seed, 16, 0, 1.0, none, none); });
+    expect_reject("attn S=576", [&] { attn_fwd(q5, k5, c5, l5, 2, 576, H, seed, 16, 0, 1.0, none, none); });
+    expect_reject("attn S % 64", [&] { attn_fwd(qkv, kb, ctx, lse, B, 100, H, seed, 16, 0, 1.0, none, none); });
+    expect_reject("attn lse size", [&] { attn_fwd(qkv, kb, ctx, l5, B, S, H, seed, 16, 0, 1.0, none, none); });
     auto cu_bad = T_({B}, i32);
-    expect_reject("attn cu size", [&] { attn_fwd(qv, kb, cv, lse, B, S, H, seed, 16, 0, 1.0, cu_bad); });
-    expect_reject("attn bwd dqkv size", [&] { attn_bwd(qkv, kb, ctx, lse, dctx, delta, ctx, B, S, H, seed, 16, 0, 1.0, none); });
+    expect_reject("attn cu size", [&] { attn_fwd(qv, kb, cv, lse, B, S, H, seed, 16, 0, 1.0, cu_bad, none); });
+    auto dm = T_({B * H * 256}, i64), dm_bad = T_({B * H * 100}, i64);
+    expect_ok("attn fwd + keep bits", [&] { attn_fwd(qkv, kb, ctx, lse, B, S, H, seed, 16, 429496730, 1.1, none, dm); });
+    expect_ok("attn bwd + keep bits", [&] { attn_bwd(qkv, kb, ctx, lse, dctx, delta, dqkv, B, S, H, seed, 16, 429496730,
+                                                     1.1, none, dm); });
+    expect_reject("attn dmask size", [&] { attn_fwd(qkv, kb, ctx, lse, B, S, H, seed, 16, 429496730, 1.1, none, dm_bad); });
+    expect_reject("attn dmask S=512", [&] { attn_fwd(q5, k5, c5, l5, 2, S5, H, seed, 16, 0, 1.0, none, dm); });
+    expect_reject("attn bwd dqkv size", [&] { attn_bwd(qkv, kb, ctx, lse, dctx, delta, ctx, B, S, H, seed, 16, 0, 1.0, none, none); });
   }
   // ---- LayerNorm fwd / bwd
   {

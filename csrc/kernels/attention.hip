@@ -113,6 +113,10 @@ struct AttnArgs {
   float scale;          // 1/sqrt(64)
   const int* cu;        // varlen: int32 [B+1] packed sequence starts (nullable = padded [B*S] layout)
   int rows;             // varlen: packed rows of qkv/ctx (rows cu[B] .. rows-1 are bucket filler)
+  // S <= 128 kernels with dropout (nullable): the forward leaves its keep bits here, the
+  // backward reads them instead of re-hashing (bitwise the same masks).  [B*H][128 q][2] u64,
+  // bit k of word (q, kt) = keep(q, key 64 kt + k)
+  uint64_t* dmask;
 };
 
 // Varlen: the extra grid slice z == B zeroes head h's columns of the filler rows
@@ -539,6 +543,7 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   // same result (a ~80-token sequence in a 128-row tile does 5/8 of the work).
   const uint64_t vk0 = __ballot(kb[lane] != -INFINITY);
   const uint64_t vk1 = __ballot(kb[64 + lane] != -INFINITY);
+  uint64_t* dmask = (drop && a.dmask) ? a.dmask + (((size_t)b * H + h) * 128 + q) * 2 : nullptr;
   for (int kt = 0; kt < nt; ++kt) {
     const uint64_t vk = kt ? vk1 : vk0;
     if (vk == 0) continue;  // fully masked key tile (exact skip)
@@ -548,6 +553,7 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
     const char* kst = ks + kt * 8192;
     const char* vst = vs + kt * 8192;
     const int k0 = kt * 64;
+    uint32_t kbits[2] = {0u, 0u};  // this lane's keep bits of the tile (keys 16 t + 4 g + r)
     f32x4 sc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -586,10 +592,20 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
         float pd = pv;
         if (drop) {
           const uint32_t key = k0 + 16 * t + 4 * g + r;
-          pd = drop_keep(seed, rowidx + key, a.drop_threshold) ? pv * a.drop_scale : 0.f;
+          const bool keep = drop_keep(seed, rowidx + key, a.drop_threshold);
+          pd = keep ? pv * a.drop_scale : 0.f;
+          kbits[t >> 1] |= (uint32_t)keep << (16 * (t & 1) + 4 * g + r);
         }
         sc[t][r] = pd;
       }
+    }
+    if (dmask) {  // the row's 64 keep bits: OR of the four lane groups' disjoint bits
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        kbits[i] |= __shfl_xor(kbits[i], 16, 64);
+        kbits[i] |= __shfl_xor(kbits[i], 32, 64);
+      }
+      if (g == 0) dmask[kt] = (uint64_t)kbits[0] | ((uint64_t)kbits[1] << 32);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -612,7 +628,7 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
 }
 
 __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[8 * 8192 + 3 * 512];
+  __shared__ __attribute__((aligned(16))) char smem[8 * 8192 + 3 * 512 + 2048];
   char* qs = smem;
   char* ks = smem + 2 * 8192;
   char* vs = smem + 4 * 8192;
@@ -620,6 +636,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   float* kb = reinterpret_cast<float*>(smem + 8 * 8192);
   float* lse_s = kb + 128;
   float* dl_s = lse_s + 128;
+  uint64_t* mk_s = reinterpret_cast<uint64_t*>(smem + 8 * 8192 + 3 * 512);  // [128 q][2] keep bits
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
@@ -651,9 +668,12 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
     lse_s[tid] = tid < len ? a.lse[st0 + tid] : INFINITY;
     dl_s[tid] = 0.f;
   }
+  const bool drop = a.drop_threshold != 0;
+  // the forward's keep bits (rows the forward did not write are past the sequence: P = 0 there)
+  const bool mk = drop && a.dmask != nullptr;
+  if (mk && tid < 256) mk_s[tid] = a.dmask[((size_t)b * H + h) * 256 + tid];
   __syncthreads();
   const uint32_t seed = site_seed(a);
-  const bool drop = a.drop_threshold != 0;
   const float sc_out = a.scale;
   // unmasked-key bits of the two 64-key tiles (see attn_fwd_s128_kernel): 16-key sub-tiles
   // with every key masked have P = dS = 0 exactly and are skipped in both phases
@@ -693,6 +713,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
       for (int t = 0; t < 4; ++t) tv[t] = ((vk >> (16 * t)) & 0xffffull) != 0;
       const char* kst = ks + kt * 8192;
       const char* vst = vs + kt * 8192;
+      const uint64_t mrow = mk ? mk_s[qr * 2 + kt] : 0ull;
       f32x4 sc[4], dp[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -713,7 +734,10 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
           const int kl = 16 * t + 4 * g + r;
           const float pv = __expf(sc[t][r] * a.scale + kb[kt * 64 + kl] - lse);
           float dpv = dp[t][r];
-          if (drop) dpv = drop_keep(seed, rowidx + kt * 64 + kl, a.drop_threshold) ? dpv * a.drop_scale : 0.f;
+          if (drop) {
+            const bool keep = mk ? ((mrow >> kl) & 1ull) != 0 : drop_keep(seed, rowidx + kt * 64 + kl, a.drop_threshold);
+            dpv = keep ? dpv * a.drop_scale : 0.f;
+          }
           sc[t][r] = pv * (dpv - dl);  // dS
         }
       }
@@ -795,7 +819,8 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
           const float pv = __expf(sc[t][r] * a.scale + kbias - lse_s[ql]);
           float dpv = dp[t][r], pdv = pv;
           if (drop) {
-            const bool keep = drop_keep(seed, (headidx + ql) * (uint32_t)S + key, a.drop_threshold);
+            const bool keep = mk ? ((mk_s[ql * 2 + (key >> 6)] >> (key & 63)) & 1ull) != 0
+                                 : drop_keep(seed, (headidx + ql) * (uint32_t)S + key, a.drop_threshold);
             dpv = keep ? dpv * a.drop_scale : 0.f;
             pdv = keep ? pv * a.drop_scale : 0.f;
           }
@@ -835,10 +860,11 @@ extern "C" {
 
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                int rows, hipStream_t st) {
+                int rows, uint64_t* dmask, hipStream_t st) {
   if (S % 64 != 0) return 1;
   AttnArgs a{};
   a.cu = cu;
+  a.dmask = use_s128(S) ? dmask : nullptr;
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
@@ -852,10 +878,11 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse,
                 const void* dctx, float* delta, void* dqkv, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                int rows, hipStream_t st) {
+                int rows, const uint64_t* dmask, hipStream_t st) {
   if (S % 64 != 0) return 1;
   AttnArgs a{};
   a.cu = cu;
+  a.dmask = use_s128(S) ? const_cast<uint64_t*>(dmask) : nullptr;
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = (float*)lse;
   a.dctx = (const bf16_t*)dctx; a.delta = delta; a.dqkv = (bf16_t*)dqkv;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;

@@ -168,7 +168,8 @@ class LayerFn(torch.autograd.Function):
         attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
         grad = ctx.needs_input_grad[0]
         qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
-        cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu)
+        dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
+        cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask)
         if rc.fuse_ln:
             # bias + (dropout) + residual + LayerNorm in the N = 768 GEMMs' epilogues; the
             # backward reads the saved bf16 pre-LN sums z1 / z2 instead of ao / f
@@ -189,6 +190,7 @@ class LayerFn(torch.autograd.Function):
             ctx.save_for_backward(x)
             # (fused LN: ao / f hold the pre-LN sums z1 / z2)
             ctx.acts = (qkv, cx, lse, ao, h, m1, r1, u, None if rc.remat_gelu else g, f, m2, r2)
+            ctx.dmask = dmask
         ctx.L, ctx.rc, ctx.sites, ctx.p, ctx.fused_ln = L, rc, (attn_site, ffn_site), (p_a, p_h), rc.fuse_ln
         return y
 
@@ -253,7 +255,7 @@ class LayerFn(torch.autograd.Function):
             wg.fork(dz1, cx)
             with wg.ctx():
                 K.linear_dw(dz1, cx, G["o_w"].buf, acc)
-        dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu)
+        dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask)
         wg.fork(dqkv, x, dz1, cx)
         with wg.ctx():
             if batch is not None:
@@ -282,7 +284,7 @@ class LayerFn(torch.autograd.Function):
             dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt.get("qkv_w"))
         for k in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_w", "ln1_b", "l1_w", "l1_b", "l2_b", "ln2_w", "ln2_b"):
             G[k].accumulate()
-        del ctx.acts
+        del ctx.acts, ctx.dmask
         if rc.on_layer_grads is not None:
             with wg.ctx():  # ordered after this block's dW work (and, via the forks, its LN grads)
                 rc.on_layer_grads(ctx.idx)

@@ -34,9 +34,10 @@ for B in (1, 4, 16, 32, 64, 128):
     qkv = (torch.randn(rows, 3 * H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
     kb = torch.zeros(B * S, device="cuda")
     dctx = (torch.randn(rows, H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
-    for p in (0.0, 0.1):
-        ctx, lse = K.attn_fwd(qkv, kb, B, S, H, seed, 5, p, cu=cu)
-        tf = timeit(lambda: K.attn_fwd(qkv, kb, B, S, H, seed, 5, p, cu=cu))
-        tb = timeit(lambda: K.attn_bwd(qkv, kb, ctx, lse, dctx, B, S, H, seed, 5, p, cu=cu))
-        print(f"S128={os.environ.get('FD_ATTN_S128', '1')} B={B:4d} p={p}: fwd {tf:7.1f} us  bwd {tb:7.1f} us",
-              flush=True)
+    for p, bits in ((0.0, False), (0.1, False), (0.1, True)):
+        dm = K.attn_keep_bits(B, S, H, p, "cuda") if bits else None
+        ctx, lse = K.attn_fwd(qkv, kb, B, S, H, seed, 5, p, cu=cu, dmask=dm)
+        tf = timeit(lambda: K.attn_fwd(qkv, kb, B, S, H, seed, 5, p, cu=cu, dmask=dm))
+        tb = timeit(lambda: K.attn_bwd(qkv, kb, ctx, lse, dctx, B, S, H, seed, 5, p, cu=cu, dmask=dm))
+        print(f"S128={os.environ.get('FD_ATTN_S128', '1')} B={B:4d} p={p} keep-bits={int(bits)}: fwd {tf:7.1f} us  "
+              f"bwd {tb:7.1f} us", flush=True)

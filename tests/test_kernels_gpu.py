@@ -156,6 +156,36 @@ def test_attention_skips_padded_key_tiles():
     assert torch.count_nonzero(dk) == 0
 
 
+@pytest.mark.parametrize("S,varlen", [(128, False), (64, False), (128, True)])
+def test_attention_keep_bits_match_hash(S, varlen):
+    """The S <= 128 forward records its dropout keep bits; the backward that reads them is
+    bitwise the backward that re-hashes every probability (and the forward is unchanged)."""
+    B, H, p = 5, 12, 0.1
+    g = torch.Generator().manual_seed(S)
+    lens = torch.randint(S // 3, S + 1, (B,), generator=g)
+    lens[0] = S
+    if varlen:
+        cu = torch.zeros(B + 1, dtype=torch.int32)
+        cu[1:] = torch.cumsum(lens, 0)
+        rows = (int(cu[-1]) + 127) // 128 * 128
+        cu, kb = cu.to(DEV), torch.zeros(1, device=DEV)
+    else:
+        cu, rows = None, B * S
+        kb = kn.mask_bias((torch.arange(S)[None, :] < lens[:, None]).long().to(DEV))
+    qkv = bf(rows, 3 * H * 64, seed=41)
+    dctx = bf(rows, H * 64, seed=42)
+    dm = kn.attn_keep_bits(B, S, H, p, DEV)
+    assert dm is not None and kn.attn_keep_bits(B, 256, H, p, DEV) is None and kn.attn_keep_bits(B, S, H, 0.0, DEV) is None
+    ctx0, lse0 = kn.attn_fwd(qkv, kb, B, S, H, seed_t(9), 21, p, cu=cu)
+    ctx1, lse1 = kn.attn_fwd(qkv, kb, B, S, H, seed_t(9), 21, p, cu=cu, dmask=dm)
+    valid = (torch.arange(S)[None, :] < lens[:, None]).to(DEV)[:, None, :].expand(B, H, S)  # (varlen: rows past a
+    assert torch.equal(ctx0, ctx1) and torch.equal(lse0[valid], lse1[valid])           # sequence are not written)
+    d0 = kn.attn_bwd(qkv, kb, ctx0, lse0, dctx, B, S, H, seed_t(9), 21, p, cu=cu)
+    d1 = kn.attn_bwd(qkv, kb, ctx1, lse1, dctx, B, S, H, seed_t(9), 21, p, cu=cu, dmask=dm)
+    torch.cuda.synchronize()
+    assert torch.equal(d0, d1)
+
+
 @pytest.mark.parametrize("B,S,p", [(2, 128, 0.0), (3, 128, 0.1), (2, 256, 0.1), (1, 64, 0.0), (2, 512, 0.1),
                                    (1, 512, 0.0)])
 def test_attention_fwd(B, S, p):
