@@ -578,6 +578,7 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
       for (int e = 0; e < 8; ++e) { const float d = zv[it][e] - mt; q += d * d; }
       q = row_sum<CPR>(q);
       if (cc == 0) { st_gran(stats + (size_t)tn * 2 * BM + r, tag, mt); st_gran(stats + (size_t)(tn * 2 + 1) * BM + r, tag, q); }
+      if (L.z && m < p.M) *reinterpret_cast<uint4*>(L.z + (size_t)m * N + n) = z_v[it];  // (before the wait)
     } else {
       float zz[8];
       unpack8bf(z_v[it], zz);
@@ -597,6 +598,39 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
       s2 = row_sum<CPR>(s2);
       if (cc == 0) { st_gran(stats + (size_t)tn * 2 * BM + r, tag, s1); st_gran(stats + (size_t)(tn * 2 + 1) * BM + r, tag, s2); }
     }
+  }
+  // backward column partials (lanes of a wave with the same column chunk, then the waves):
+  // dgamma / dbeta need no row statistics, so they are reduced and stored while the other
+  // tiles' granules are in flight; dbias follows the normalisation
+  constexpr int NWV = NT / 64;
+  float* red = reinterpret_cast<float*>(smem);  // [2][NWV][BN]
+  auto park = [&](float (&a)[8], int slot) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) a[e] += __shfl_xor(a[e], o, 64);
+    }
+    if (lane < CPR) {
+      float* dst = red + (slot * NWV + (tid >> 6)) * BN + 8 * lane;
+      *reinterpret_cast<float4*>(dst) = make_float4(a[0], a[1], a[2], a[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(a[4], a[5], a[6], a[7]);
+    }
+  };
+  auto flush = [&](int nslot, int w30) {  // colpart rows w30 .. w30 + nslot - 1 from slots 0 ..
+    for (int i = tid; i < nslot * BN; i += NT) {
+      const int sl = i / BN, c = i % BN;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) v += red[(sl * NWV + w) * BN + c];
+      L.colpart[((size_t)tm * 3 + w30 + sl) * N + n0 + c] = v;
+    }
+  };
+  if constexpr (BWD) {
+    __syncthreads();  // the staged tile has been read
+    park(cg, 0);
+    park(cb, 1);
+    __syncthreads();
+    flush(2, 0);
   }
   // this lane's share of the tiles_n partials of its rows (tiles cc, cc + CPR, ...): poll the
   // granules until every tag is this launch's (wave-uniform exit)
@@ -655,7 +689,6 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
       for (int e = 0; e < 8; ++e) y[e] = (zv[it][e] - mean) * rstd * g[e] + bt[e];
       if (m < p.M) {
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + off) = pack8bf(y);
-        if (L.z) *reinterpret_cast<uint4*>(L.z + off) = z_v[it];
         if (tn == 0 && cc == 0) { L.mean[m] = mean; L.rstd[m] = rstd; }
       }
     } else {
@@ -680,33 +713,10 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
   }
   ln_done(L, tag, tid);
   if constexpr (BWD) {
-    // column partials: lanes of a wave with the same column chunk (lane % CPR), then the waves
-    constexpr int NWV = NT / 64;
-    float* red = reinterpret_cast<float*>(smem);  // [3][NWV][BN]
-    __syncthreads();  // the staged tile is no longer read
-    auto park = [&](float (&a)[8], int w3) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-#pragma unroll
-        for (int o = CPR; o < 64; o <<= 1) a[e] += __shfl_xor(a[e], o, 64);
-      }
-      if (lane < CPR) {
-        float* dst = red + (w3 * NWV + (tid >> 6)) * BN + 8 * lane;
-        *reinterpret_cast<float4*>(dst) = make_float4(a[0], a[1], a[2], a[3]);
-        *reinterpret_cast<float4*>(dst + 4) = make_float4(a[4], a[5], a[6], a[7]);
-      }
-    };
-    park(cg, 0);
-    park(cb, 1);
-    park(cd, 2);
+    __syncthreads();  // slots 0 / 1 have been flushed
+    park(cd, 0);
     __syncthreads();
-    for (int i = tid; i < 3 * BN; i += NT) {
-      const int w3 = i / BN, c = i % BN;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < NWV; ++w) v += red[(w3 * NWV + w) * BN + c];
-      L.colpart[((size_t)tm * 3 + w3) * N + n0 + c] = v;
-    }
+    flush(1, 2);
   }
 }
 

@@ -132,8 +132,13 @@ DEV bool is_cls_row(const HeadArgs& a, int row) {
 
 // Blocks [0, ceil(D/256)): dW / db and the [CLS] rows of dhidden.  Blocks beyond: zero every
 // other row of dhidden (so the caller needs no separate fill launch).
+// Column blocks: 32 columns x 8 row groups per 256-thread block (D / 32 blocks), so every
+// thread has at most ceil(B / 8) [CLS] rows to load -- all issued before any use -- instead of
+// a serial walk over the batch; the 8 group partials of dW are summed through LDS in a fixed
+// order (deterministic).  The remaining blocks zero the non-[CLS] rows of dhidden.
+constexpr int HB_COLS = 32, HB_GROUPS = 8, HB_ROWS = 8;  // rows per thread held in flight (B <= 64)
 __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
-  const int nc = (a.D + 255) / 256;
+  const int nc = (a.D + HB_COLS - 1) / HB_COLS;
   if ((int)blockIdx.x >= nc) {
     const int per_row = a.D / 8;  // uint4 chunks
     const long long total = (long long)a.T * per_row;
@@ -144,43 +149,53 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
     }
     return;
   }
+  __shared__ float red[2][HB_GROUPS][HB_COLS];
+  const int c = threadIdx.x % HB_COLS, grp = threadIdx.x / HB_COLS;
+  const int col = blockIdx.x * HB_COLS + c;
+  const bool live = col < a.D;
+  const int colc = live ? col : 0;
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
-  for (int col = blockIdx.x * 256 + threadIdx.x; col < a.D; col += nc * 256) {
-    float g0 = 0.f, g1 = 0.f;
-    const float w0 = a.W[col], w1 = a.W[a.D + col];
-    for (int b0 = 0; b0 < a.B; b0 += 8) {
-      // 8 rows' loads in flight before any store (dhidden may alias nothing here, but the
-      // compiler cannot know: hoisting by hand)
-      float x[8];
-      size_t row[8];
+  const float gs = a.gscale ? a.gscale[0] : 1.f;
+  const float w0 = a.W[colc], w1 = a.W[a.D + colc];
+  float g0 = 0.f, g1 = 0.f;
+  for (int b0 = grp; b0 < a.B; b0 += HB_GROUPS * HB_ROWS) {
+    float x[HB_ROWS];
+    size_t row[HB_ROWS];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int b = min(b0 + u, a.B - 1);
-        row[u] = cls_row(a, b);
-        x[u] = bf2f(a.hidden[row[u] * a.D + col]);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int b = b0 + u;
-        if (b >= a.B) break;
-        const float gs = a.gscale ? a.gscale[0] : 1.f;
-        const float d0 = a.gscale ? a.dlog_in[2 * b] * gs : a.dlog_in[2 * b];
-        const float d1 = a.gscale ? a.dlog_in[2 * b + 1] * gs : a.dlog_in[2 * b + 1];
-        const bool keep = !drop || drop_keep(seed, (uint32_t)(b * a.D + col), a.thr);
-        const float sc = drop ? (keep ? a.dscale : 0.f) : 1.f;
-        const float xv = x[u] * sc;
-        g0 += d0 * xv;
-        g1 += d1 * xv;
-        a.dhidden[row[u] * a.D + col] = (bf16_t)f2bf((d0 * w0 + d1 * w1) * sc);
-      }
+    for (int u = 0; u < HB_ROWS; ++u) {  // every row's load in flight before the first use
+      const int b = min(b0 + u * HB_GROUPS, a.B - 1);
+      row[u] = cls_row(a, b);
+      x[u] = bf2f(a.hidden[row[u] * a.D + colc]);
     }
-    a.dW[col] = a.accumulate ? a.dW[col] + g0 : g0;
-    a.dW[a.D + col] = a.accumulate ? a.dW[a.D + col] + g1 : g1;
+#pragma unroll
+    for (int u = 0; u < HB_ROWS; ++u) {
+      const int b = b0 + u * HB_GROUPS;
+      if (b >= a.B) break;
+      const float d0 = a.dlog_in[2 * b] * gs, d1 = a.dlog_in[2 * b + 1] * gs;
+      const bool keep = !drop || drop_keep(seed, (uint32_t)(b * a.D + colc), a.thr);
+      const float sc = drop ? (keep ? a.dscale : 0.f) : 1.f;
+      const float xv = x[u] * sc;
+      g0 += d0 * xv;
+      g1 += d1 * xv;
+      // an empty sequence shares its [CLS] row with the next one: the later sequence writes it
+      const bool last_owner = b + 1 >= a.B || cls_row(a, b + 1) != row[u];
+      if (live && last_owner) a.dhidden[row[u] * a.D + col] = (bf16_t)f2bf((d0 * w0 + d1 * w1) * sc);
+    }
+  }
+  red[0][grp][c] = g0;
+  red[1][grp][c] = g1;
+  __syncthreads();
+  if (grp < 2 && live) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < HB_GROUPS; ++i) s += red[grp][i][c];
+    float* dst = a.dW + grp * a.D + col;
+    *dst = a.accumulate ? *dst + s : s;
   }
   if (blockIdx.x == 0 && threadIdx.x < 2) {
     float s = 0.f;
-    for (int b = 0; b < a.B; ++b) s += a.gscale ? a.dlog_in[2 * b + threadIdx.x] * a.gscale[0] : a.dlog_in[2 * b + threadIdx.x];
+    for (int b = 0; b < a.B; ++b) s += a.dlog_in[2 * b + threadIdx.x] * gs;
     a.db[threadIdx.x] = a.accumulate ? a.db[threadIdx.x] + s : s;
   }
 }
@@ -393,7 +408,7 @@ int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const u
   // compute blocks + zeroing blocks (~4 uint4 stores per thread over the non-[CLS] rows)
   const long long chunks = (long long)T * (D / 8);
   const int zb = (int)std::min<long long>((chunks + 1023) / 1024, 1024);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3((D + 255) / 256 + zb), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((D + HB_COLS - 1) / HB_COLS + zb), dim3(256), 0, st, a);
   return 0;
 }
 
