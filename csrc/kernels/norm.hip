@@ -390,10 +390,12 @@ __global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
 // back to back.  Rows s >= S are handled by a memset (first write) on the host side.
 // cu (packed rows): sequence b's position s is row cu[b] + s when s < its length; the
 // padded layout's extra terms are exact zeros, so both layouts give the same sums.
-// grid (S, ceil(D/256)): one thread per (position, column), 16 sequences' loads in flight.
+// grid (S, D/256): a block sums one position over the batch for 64 float4 columns, its 4
+// thread groups taking every 4th sequence (8 loads in flight each), combined in a fixed order.
 // Rows s < S: position gradient (sum over sequences).  Rows S <= s < gridDim.x (first write
 // only): zero -- those positions never occur.  Also clears the `now` row flags (V bytes) the
 // word-gradient kernels set next, so neither needs a memset launch of its own.
+constexpr int PG_GROUPS = 4, PG_COLS = 64;  // per block: 64 float4 columns x 4 sequence groups
 __global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* dpos, int B, int S, int D,
                                                        int accumulate, const int* cu, unsigned char* now, int V) {
   const int s = blockIdx.x;
@@ -406,22 +408,40 @@ __global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* d
     for (int col = blockIdx.y * 256 + threadIdx.x; col < D; col += gridDim.y * 256) dpos[(size_t)s * D + col] = 0.f;
     return;
   }
-  for (int col = blockIdx.y * 256 + threadIdx.x; col < D; col += gridDim.y * 256) {
-    float acc = accumulate ? dpos[(size_t)s * D + col] : 0.f;
-    for (int b0 = 0; b0 < B; b0 += 16) {
-      float v[16];
+  __shared__ int s_cu[257];
+  __shared__ float4 red[PG_GROUPS][PG_COLS];
+  if (cu)
+    for (int b = threadIdx.x; b <= B && b < 257; b += 256) s_cu[b] = cu[b];
+  __syncthreads();
+  const int c4 = blockIdx.y * PG_COLS + (threadIdx.x % PG_COLS), grp = threadIdx.x / PG_COLS;
+  const bool live = c4 < D / 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b0 = grp; b0 < B; b0 += PG_GROUPS * 8) {
+    float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int b = b0 + u;
-        if (cu)
-          v[u] = b < B && s < cu[b + 1] - cu[b] ? dz[((size_t)cu[b] + s) * D + col] : 0.f;
-        else
-          v[u] = b < B ? dz[((size_t)b * S + s) * D + col] : 0.f;
+    for (int u = 0; u < 8; ++u) {  // this group's sequences b0, b0 + 4, ...: loads in flight together
+      const int b = b0 + u * PG_GROUPS;
+      long long row = -1;
+      if (b < B) {
+        if (!cu) row = (long long)b * S + s;
+        else if (B < 257 && s < s_cu[b + 1] - s_cu[b]) row = (long long)s_cu[b] + s;
+        else if (B >= 257 && s < cu[b + 1] - cu[b]) row = (long long)cu[b] + s;
       }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) acc += v[u];
+      v[u] = (row >= 0 && live) ? reinterpret_cast<const float4*>(dz + (size_t)row * D)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    dpos[(size_t)s * D + col] = acc;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+  }
+  red[grp][threadIdx.x % PG_COLS] = acc;
+  __syncthreads();
+  if (grp == 0 && live) {
+    float4 t = accumulate ? reinterpret_cast<const float4*>(dpos + (size_t)s * D)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int g = 0; g < PG_GROUPS; ++g) {  // fixed order: deterministic
+      const float4 r = red[g][threadIdx.x];
+      t.x += r.x; t.y += r.y; t.z += r.z; t.w += r.w;
+    }
+    reinterpret_cast<float4*>(dpos + (size_t)s * D)[c4] = t;
   }
 }
 
@@ -468,13 +488,13 @@ __global__ __launch_bounds__(256) void rank_sort_kernel(const I* ids, int T, lon
 }
 
 // Word-embedding gradient over tokens grouped by id (rank sort above).  Pass 1:
-// one block per 32 sorted positions; every thread loads its 32 rows x 3 columns
+// one block per WCH (16) sorted positions; every thread loads its WCH rows x 3 columns
 // up front, then walks the runs: a run contained in the chunk is written
 // straight to dword, a piece of a run crossing a chunk boundary goes to
 // piece[start].  Pass 2: the chunk holding a crossing run's first position adds
 // that run's pieces in chunk order.  Every output row is written by exactly one
 // block -> deterministic, atomic-free.
-constexpr int WCH = 32;
+constexpr int WCH = 16;
 DEV void word_row_store(float* dword, long long id, int col, float acc, bool add) {
   float* dst = dword + (size_t)id * 768 + col;
   *dst = add ? *dst + acc : acc;
@@ -533,14 +553,26 @@ __global__ __launch_bounds__(256) void word_grad_combine_kernel(const long long*
   constexpr int D = 768;
   const int c0 = blockIdx.x * WCH, c1 = min(T, c0 + WCH);
   if (c1 >= T || sorted[c1] != sorted[c1 - 1]) return;  // no run crosses this chunk's end
-  // first position of the crossing run (within this chunk)
+  // The crossing run's first position in this chunk (the run is a suffix of the chunk) and its
+  // end, found by the whole block at once instead of walking the sorted ids one dependent load
+  // at a time (a template word's run spans many chunks).
   const long long id = sorted[c1 - 1];
-  int a = c1 - 1;
-  while (a > c0 && sorted[a - 1] == id) --a;
+  __shared__ int s_cnt, s_end;
+  if (threadIdx.x == 0) { s_cnt = 0; s_end = T; }
+  __syncthreads();
+  if ((int)threadIdx.x < c1 - c0 && sorted[c0 + threadIdx.x] == id) atomicAdd(&s_cnt, 1);
+  for (int base = c1;; base += 256) {
+    const int j = base + (int)threadIdx.x;
+    if (j < T && sorted[j] != id) atomicMin(&s_end, j);
+    __syncthreads();
+    const bool done = s_end < T || base + 256 >= T;
+    __syncthreads();
+    if (done) break;
+  }
+  const int a = c1 - s_cnt;
   if (a == c0 && c0 > 0 && sorted[c0 - 1] == id) return;  // run started in an earlier chunk
   const bool add = accumulate && (now ? now[id] != 0 : true);
-  int npieces = 0;  // chunk starts c1, c1+32, ... still inside the run
-  for (int j = c1; j < T && sorted[j] == id; j += WCH) ++npieces;
+  const int npieces = (s_end - c1 + WCH - 1) / WCH;  // chunk starts c1, c1 + WCH, ... inside the run
   for (int col = threadIdx.x; col < D; col += 256) {
     float acc = piece[(size_t)a * D + col];
     for (int p0 = 0; p0 < npieces; p0 += 16) {
@@ -741,7 +773,8 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                      st, a);
   hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 2), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
                      dbeta, (float*)nullptr, accumulate);
-  hipLaunchKernelGGL(pos_grad_kernel, dim3(!accumulate && P > S ? P : S, (D + 255) / 256), dim3(256), 0, st, dz_buf,
+  hipLaunchKernelGGL(pos_grad_kernel, dim3(!accumulate && P > S ? P : S, (D / 4 + PG_COLS - 1) / PG_COLS), dim3(256), 0,
+                     st, dz_buf,
                      dpos, B, S, D, accumulate, cu, !accumulate ? now : nullptr, V);
   if (!accumulate && !now) hipMemsetAsync(dword, 0, (size_t)V * D * sizeof(float), st);
   // piece sums reuse `work` (T*D floats)
