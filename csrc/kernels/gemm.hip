@@ -499,6 +499,12 @@ DEV uint4 pack8bf(const float (&f)[8]) {
 }
 
 constexpr int LN_MAXK = 4;  // column tiles per row block <= LN_MAXK * (BN / 8)
+// Largest LayerNorm-fused grid: one round of the 256 CUs, every tile resident at once (no row
+// block waits on a tile that cannot be dispatched yet).  Measured: at two rounds' worth of tiles
+// (bs64 x seq256 packed, 492 tiles) the fused GEMMs lose to GEMM + LN kernels even with two
+// 72 KiB blocks per CU (5.99 vs 5.78 ms/step, profiles/r2_ab_fused_ln_kd_seq256.txt), so
+// larger grids take the separate LayerNorm kernels (ops/kernels.py ln_fusable mirrors this).
+constexpr int LN_MAX_TILES = 256;
 
 template <int BM, int BN, int TM, int TN, bool BWD, int NT>
 DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int tm, int tn,
@@ -1533,6 +1539,7 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   }
   const int bm = id == 13 ? 64 : 128, bn = 64;
   if (N / bn > LN_MAXK * (bn / 8)) return -2;
+  if (((M + bm - 1) / bm) * (N / bn) > LN_MAX_TILES) return -4;  // caller: the unfused kernels
   GemmParams p{};
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)Bt; p.C = C;
   p.M = M; p.N = N; p.K = K; p.lda = K; p.ldb = K; p.ldc = N;

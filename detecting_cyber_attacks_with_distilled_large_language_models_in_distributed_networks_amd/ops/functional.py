@@ -170,7 +170,8 @@ class LayerFn(torch.autograd.Function):
         qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
         dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
         cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask)
-        if rc.fuse_ln:
+        fuse_ln = rc.fuse_ln and K.ln_fusable(x.shape[0], x.shape[1])
+        if fuse_ln:
             # bias + (dropout) + residual + LayerNorm in the N = 768 GEMMs' epilogues; the
             # backward reads the saved bf16 pre-LN sums z1 / z2 instead of ao / f
             h, ao, m1, r1 = K.linear_ln_fwd(cx, L["o_w"], L["o_b"], x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0,
@@ -191,7 +192,7 @@ class LayerFn(torch.autograd.Function):
             # (fused LN: ao / f hold the pre-LN sums z1 / z2)
             ctx.acts = (qkv, cx, lse, ao, h, m1, r1, u, None if rc.remat_gelu else g, f, m2, r2)
             ctx.dmask = dmask
-        ctx.L, ctx.rc, ctx.sites, ctx.p, ctx.fused_ln = L, rc, (attn_site, ffn_site), (p_a, p_h), rc.fuse_ln
+        ctx.L, ctx.rc, ctx.sites, ctx.p, ctx.fused_ln = L, rc, (attn_site, ffn_site), (p_a, p_h), fuse_ln
         return y
 
     @staticmethod

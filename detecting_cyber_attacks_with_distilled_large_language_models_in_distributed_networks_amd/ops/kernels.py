@@ -317,6 +317,16 @@ def _ln_state(device, M: int, N: int):
     return st[:3]
 
 
+LN_MAX_TILES = 256  # csrc/kernels/gemm.hip: the fused grid is one resident round of the CUs
+
+
+def ln_fusable(M: int, N: int) -> bool:
+    """Whether a LayerNorm-fused GEMM of M rows x N (= hidden) columns runs as one resident
+    round (its row blocks exchange statistics, so no tile may wait on an undispatched peer);
+    larger batches use the separate LayerNorm kernels."""
+    return N % 64 == 0 and N <= 2048 and ((M + 127) // 128) * (N // 64) <= LN_MAX_TILES
+
+
 def ln_error_flag(device, N: int = 768) -> int:
     """Nonzero if a fused-LN launch's row-block rendezvous ever timed out (never expected)."""
     st = _WS.get((_dev_key(device), "ln_state", N))

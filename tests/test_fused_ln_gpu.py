@@ -48,7 +48,7 @@ def state_clean(M):
     return int(err.item()) == 0 and int(cnt[1].item()) == 0 and int(cnt[0].item()) > 0
 
 
-@pytest.mark.parametrize("M,K,p", [(2688, 768, 0.0), (2600, 3072, 0.1), (300, 3072, 0.1), (4096, 768, 0.0),
+@pytest.mark.parametrize("M,K,p", [(2688, 768, 0.0), (2600, 3072, 0.1), (300, 3072, 0.1), (2000, 768, 0.0),
                                    (64, 768, 0.1)])
 def test_linear_ln_fwd(M, K, p):
     x, w, res = bf(M, K, seed=1), bf(D, K, scale=0.03, seed=2), bf(M, D, seed=3)
@@ -68,6 +68,18 @@ def test_linear_ln_fwd(M, K, p):
     y2, _, _ = kn.ln_fwd(kn.linear_fwd(x, w, b), res, gamma, beta, 1e-12, seed_t(9), 33, p)
     assert rel_err(y, y2) < 2e-2
     assert state_clean(M)
+
+
+def test_fused_grid_limited_to_one_resident_round():
+    """Row blocks wait on each other's statistics, so the fused grid must fit one round of the
+    CUs (21 row blocks x 12 column tiles at N = 768); a larger M is refused by the launcher and
+    the model takes the separate LayerNorm kernels (ln_fusable)."""
+    assert kn.ln_fusable(2688, D) and not kn.ln_fusable(2689, D) and not kn.ln_fusable(4096, D)
+    M, K = 4096, 768
+    x, w, res = bf(M, K, seed=1), bf(D, K, scale=0.03, seed=2), bf(M, D, seed=3)
+    gamma, beta = affine(5)
+    with pytest.raises(RuntimeError):
+        kn.linear_ln_fwd(x, w, torch.zeros(D, device=DEV), res, gamma, beta, 1e-12, seed_t(9), 33, 0.0)
 
 
 def test_linear_ln_fwd_packed_row_map():
