@@ -29,6 +29,8 @@ BUILD = os.path.join(REPO, "build", "native")
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# experiment builds only (e.g. "-DFD_GEMM_SCHED=0"); use with force=True / a clean build dir
+EXTRA = os.environ.get("FD_HIP_EXTRA_FLAGS", "").split()
 
 SO_DIR = os.path.join(REPO, "_so")
 HIP_OUT = os.path.join(SO_DIR, "_hip_kernels.so")
@@ -114,7 +116,7 @@ def build_hip(verbose=False, force=False, jobs=None) -> str:
         objs.append(o)
         if force or _newer(o, [s] + headers):
             jobs_list.append(([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                               "-munsafe-fp-atomics", "-I" + kdir, "-c", s, "-o", o], o))
+                               "-munsafe-fp-atomics", "-I" + kdir] + EXTRA + ["-c", s, "-o", o], o))
     for s in sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp"))):
         o = os.path.join(BUILD, "comm_" + os.path.basename(s) + ".o")
         objs.append(o)
