@@ -1539,7 +1539,18 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   }
   const int bm = id == 13 ? 64 : 128, bn = 64;
   if (N / bn > LN_MAXK * (bn / 8)) return -2;
-  if (((M + bm - 1) / bm) * (N / bn) > LN_MAX_TILES) return -4;  // caller: the unfused kernels
+  {
+    // one resident round: no more tiles than CUs (cfg 24: one 147 KiB block per CU)
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                   hipSuccess)
+        n = 0;
+      return n;
+    }();
+    const int max_tiles = std::min(LN_MAX_TILES, cus > 0 ? cus : LN_MAX_TILES);
+    if (((M + bm - 1) / bm) * (N / bn) > max_tiles) return -4;  // caller: the unfused kernels
+  }
   GemmParams p{};
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)Bt; p.C = C;
   p.M = M; p.N = N; p.K = K; p.lda = K; p.ldb = K; p.ldc = N;

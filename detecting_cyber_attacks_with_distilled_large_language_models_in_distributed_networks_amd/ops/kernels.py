@@ -320,11 +320,22 @@ def _ln_state(device, M: int, N: int):
 LN_MAX_TILES = 256  # csrc/kernels/gemm.hip: the fused grid is one resident round of the CUs
 
 
+_CUS = {}
+
+
+def _cu_count() -> int:
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else -1
+    if dev not in _CUS:
+        _CUS[dev] = torch.cuda.get_device_properties(dev).multi_processor_count if dev >= 0 else LN_MAX_TILES
+    return _CUS[dev]
+
+
 def ln_fusable(M: int, N: int) -> bool:
     """Whether a LayerNorm-fused GEMM of M rows x N (= hidden) columns runs as one resident
-    round (its row blocks exchange statistics, so no tile may wait on an undispatched peer);
-    larger batches use the separate LayerNorm kernels."""
-    return N % 64 == 0 and N <= 2048 and ((M + 127) // 128) * (N // 64) <= LN_MAX_TILES
+    round (its row blocks exchange statistics, so no tile may wait on an undispatched peer):
+    at most one 128 x 64 tile per CU; larger batches use the separate LayerNorm kernels."""
+    tiles = ((M + 127) // 128) * (N // 64)
+    return N % 64 == 0 and N <= 2048 and tiles <= min(LN_MAX_TILES, _cu_count())
 
 
 def ln_error_flag(device, N: int = 768) -> int:
