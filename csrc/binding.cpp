@@ -96,6 +96,9 @@ int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long lon
             float b1, float b2, float eps, float wd, int decoupled, const unsigned char* touched,
             const unsigned char* now, long long skip_off, long long skip_rows, int row_len, const long long* runs,
             int nruns, long long run_total4, hipStream_t st);
+int fd_adam_rows(float* p, const float* g, float* m, float* v, void* shadow, int rows, int row_len, const int* step,
+                 float lr, float b1, float b2, float eps, const unsigned char* ever, const unsigned char* now,
+                 hipStream_t st);
 int fd_step(int* step, uint32_t* seed, hipStream_t st);
 int fd_scale_cast(float* p, void* shadow, long long n, float scale, hipStream_t st);
 int fd_axpby(float* dst, const float* x, const float* y, float a, float b, long long n, hipStream_t st);
@@ -928,6 +931,33 @@ void adam(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const a
            "adam");
 }
 
+// Adam (weight decay 0) over the rows of a [rows][row_len] table whose `ever` flag is set
+// (gradient taken as 0 unless now[row]); p, g, m, v (and shadow) are that table's views.
+void adam_rows(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
+               const c10::optional<at::Tensor>& shadow, const at::Tensor& step, double lr, double b1, double b2,
+               double eps, const at::Tensor& ever, const c10::optional<at::Tensor>& now, int64_t row_len) {
+  need(p, at::kFloat, "p");
+  need(g, at::kFloat, "g");
+  need(m, at::kFloat, "m");
+  need(v, at::kFloat, "v");
+  need_opt(shadow, at::kBFloat16, "shadow");
+  need(step, at::kInt, "step");
+  need(ever, at::kByte, "ever");
+  need_opt(now, at::kByte, "now");
+  const int64_t n = p.numel();
+  TORCH_CHECK(row_len > 0 && row_len % 4 == 0 && n % row_len == 0, "adam_rows: rows of row_len (multiple of 4)");
+  const int64_t rows = n / row_len;
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam_rows: sizes");
+  if (shadow.has_value() && shadow->defined()) TORCH_CHECK(shadow->numel() == n, "adam_rows: shadow size");
+  TORCH_CHECK(ever.numel() >= rows, "adam_rows: ever flags");
+  if (now.has_value() && now->defined()) TORCH_CHECK(now->numel() >= rows, "adam_rows: now flags");
+  check_rc(fd_adam_rows(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                        ptr<void>(shadow), (int)rows, (int)row_len, step.data_ptr<int>(), (float)lr, (float)b1,
+                        (float)b2, (float)eps, ever.data_ptr<unsigned char>(), ptr<const unsigned char>(now),
+                        stream()),
+           "adam_rows");
+}
+
 void step_inc(const c10::optional<at::Tensor>& step, const c10::optional<at::Tensor>& seed) {
   need_opt(step, at::kInt, "step");
   need_opt(seed, at::kInt, "seed");
@@ -963,6 +993,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_dw2", &gemm_dw2);
   m.def("gemm_dw", &gemm_dw);
+  m.def("adam_rows", &adam_rows);
   m.def("gemm_ln", &gemm_ln, py::arg("bwd"), py::arg("A"), py::arg("Bt"), py::arg("C"), py::arg("bias"),
         py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("rstd"), py::arg("z"),
         py::arg("dx"), py::arg("colpart"), py::arg("stats"), py::arg("cnt"), py::arg("err"), py::arg("eps"),

@@ -120,6 +120,20 @@ int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const
   (void)cfg;
   return 0;
 }
+int fd_adam_rows(float* p, const float* g, float* m, float* v, void* shadow, int rows, int row_len, const int* step,
+                 float, float, float, float, const unsigned char* ever, const unsigned char* now, hipStream_t) {
+  ++hc::calls;
+  const long long n = (long long)rows * row_len;
+  hc::span(p, n * 4, "adam_rows p");
+  hc::span(g, n * 4, "adam_rows g");
+  hc::span(m, n * 4, "adam_rows m");
+  hc::span(v, n * 4, "adam_rows v");
+  hc::opt_span(shadow, n * 2, "adam_rows shadow");
+  hc::span(step, 4, "adam_rows step");
+  hc::span(ever, rows, "adam_rows ever");
+  hc::opt_span(now, rows, "adam_rows now");
+  return 0;
+}
 int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
                const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t) {
   ++hc::calls;
@@ -567,6 +581,12 @@ int main() {
     auto g_small = T_({n - 4}, f32);
     expect_reject("adam sizes", [&] { adam(p, g_small, m, v, sh, step, 2e-5, 0.9, 0.999, 1e-8, 0, false, none, none,
                                            0, 0, 4, none, 0, 0); });
+    // the sparse word-embedding rows (64 rows of 64)
+    auto ever = T_({64}, at::kByte), now = T_({64}, at::kByte), ever_small = T_({10}, at::kByte);
+    expect_ok("adam rows", [&] { adam_rows(p, g, m, v, sh, step, 2e-5, 0.9, 0.999, 1e-8, ever, now, 64); });
+    expect_reject("adam rows flags", [&] { adam_rows(p, g, m, v, sh, step, 2e-5, 0.9, 0.999, 1e-8, ever_small, now,
+                                                     64); });
+    expect_reject("adam rows row_len", [&] { adam_rows(p, g, m, v, sh, step, 2e-5, 0.9, 0.999, 1e-8, ever, now, 6); });
   }
   // ---- unpadded layout
   {

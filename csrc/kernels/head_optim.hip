@@ -282,6 +282,24 @@ DEV void st_nt(float4* p, float4 v) {
   __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
 }
 
+// The Adam update of 4 elements -- ONE copy of the arithmetic for every Adam kernel, so the
+// dense launch and the row-flag launch round identically (bitwise equal results).
+DEV void adam_math4(const AdamArgs& a, float (&pp)[4], const float (&gg)[4], float (&mm)[4], float (&vv)[4],
+                    float step_size, float inv_sqrt_bc2) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float gr = gg[e];
+    if (a.wd != 0.f) {
+      if (a.decoupled) pp[e] *= 1.f - a.lr * a.wd;
+      else gr += a.wd * pp[e];
+    }
+    mm[e] = a.b1 * mm[e] + (1.f - a.b1) * gr;
+    vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gr * gr;
+    const float denom = sqrtf(vv[e]) * inv_sqrt_bc2 + a.eps;
+    pp[e] -= step_size * mm[e] / denom;
+  }
+}
+
 template <bool NT, bool NTP = false>
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const int t = a.step[0];
@@ -312,18 +330,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
     }
     float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
     float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float gr = gg[e];
-      if (a.wd != 0.f) {
-        if (a.decoupled) pp[e] *= 1.f - a.lr * a.wd;
-        else gr += a.wd * pp[e];
-      }
-      mm[e] = a.b1 * mm[e] + (1.f - a.b1) * gr;
-      vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gr * gr;
-      const float denom = sqrtf(vv[e]) * inv_sqrt_bc2 + a.eps;
-      pp[e] -= step_size * mm[e] / denom;
-    }
+    adam_math4(a, pp, gg, mm, vv, step_size, inv_sqrt_bc2);
     if constexpr (NTP)
       st_nt(reinterpret_cast<float4*>(a.p) + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
     else
@@ -337,6 +344,37 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
     }
     if (a.shadow)
       reinterpret_cast<uint2*>(a.shadow)[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
+  }
+}
+
+// Adam over the rows of a table that have state (ever[row] != 0; weight decay 0): one wave per
+// row, which leaves at once unless the row is flagged, so every flagged row is updated in
+// parallel (row_len / 4 float4 per row, gradient 0 unless now[row]) with adam_kernel's
+// arithmetic (adam_math4: bitwise the dense launch's result).  The word-embedding table: ~30 k
+// rows, a few hundred of which a CICIDS2017 run ever touches; the dense launch walked all 23 M
+// parameters.
+__global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a, int rows, int row4) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows || !a.touched[row]) return;  // wave-uniform
+  const int t = a.step[0];
+  const float bc1 = 1.f - powf(a.b1, (float)t);
+  const float bc2 = 1.f - powf(a.b2, (float)t);
+  const float step_size = a.lr / bc1;
+  const float inv_sqrt_bc2 = 1.f / sqrtf(bc2);
+  const bool gvalid = a.now == nullptr || a.now[row] != 0;
+  for (int c = lane; c < row4; c += 64) {
+    const long long i = (long long)row * row4 + c;
+    const float4 p = ld_nt(reinterpret_cast<const float4*>(a.p) + i);
+    const float4 g = gvalid ? ld_nt(reinterpret_cast<const float4*>(a.g) + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 m = ld_nt(reinterpret_cast<const float4*>(a.m) + i);
+    const float4 v = ld_nt(reinterpret_cast<const float4*>(a.v) + i);
+    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
+    float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+    adam_math4(a, pp, gg, mm, vv, step_size, inv_sqrt_bc2);
+    st_nt(reinterpret_cast<float4*>(a.p) + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
+    st_nt(reinterpret_cast<float4*>(a.m) + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
+    st_nt(reinterpret_cast<float4*>(a.v) + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
+    if (a.shadow) reinterpret_cast<uint2*>(a.shadow)[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
   }
 }
 
@@ -436,6 +474,16 @@ int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long lon
     hipLaunchKernelGGL((adam_kernel<true, false>), dim3(grid_for(n / 4)), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((adam_kernel<false, false>), dim3(grid_for(n / 4)), dim3(256), 0, st, a);
+  return 0;
+}
+
+// Adam over the flagged rows of a [rows][row_len] table (weight decay 0; see adam_rows_kernel).
+int fd_adam_rows(float* p, const float* g, float* m, float* v, void* shadow, int rows, int row_len, const int* step,
+                 float lr, float b1, float b2, float eps, const unsigned char* ever, const unsigned char* now,
+                 hipStream_t st) {
+  if (row_len % 4 != 0 || rows <= 0 || !ever) return 1;
+  AdamArgs a{p, g, m, v, (bf16_t*)shadow, 0, step, lr, b1, b2, eps, 0.f, 0, 0, 0, row_len / 4, ever, now, nullptr, 0};
+  hipLaunchKernelGGL(adam_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, a, rows, row_len / 4);  // wave per row
   return 0;
 }
 

@@ -201,17 +201,39 @@ class ArenaAdam:
                 runs.append((pos, A.numel - pos))
             woff = self.model.word_embedding_span()[0] if sparse else -1
             table = self._runs_table(runs) if len(runs) > 1 else None
-            if table is not None:  # everything left (fused-GEMM spans excluded) in one launch
+            if table is not None and sparse:
+                # the word-embedding table by its row flags (one wave per 64 rows: only rows with
+                # Adam state are touched), everything else left in one run-table launch
+                from ..ops import kernels as K
+                _, rows, rl = self.model.word_embedding_span()
+                wend = woff + rows * rl
+                rest = []
+                for off, n in runs:
+                    a, b = off, off + n
+                    if b <= woff or a >= wend:
+                        rest.append((a, n))
+                        continue
+                    if not (a <= woff and wend <= b):
+                        raise RuntimeError("the word-embedding table must lie inside one Adam run")
+                    if woff > a:
+                        rest.append((a, woff - a))
+                    if b > wend:
+                        rest.append((wend, b - wend))
+                sl = slice(woff, wend)
+                K.adam_rows(A.master[sl], A.grad[sl], self.m[sl], self.v[sl], A.shadow[sl], self.step_t, self.lr, b1,
+                            b2, self.eps, self.model.emb_ever, self.model.emb_now, rl)
+                rest_table = self._runs_table(rest) if len(rest) > 1 else None
+                if rest_table is not None:
+                    K.adam(A.master, A.grad, self.m, self.v, A.shadow, self.step_t, self.lr, b1, b2, self.eps,
+                           self.weight_decay, self.decoupled, runs=rest_table)
+                else:
+                    for off, n in rest:
+                        self._update(off, n, False)
+            elif table is not None:  # everything left (fused-GEMM spans excluded) in one launch
                 from ..ops import kernels as K
                 b1, b2 = self.betas
-                if sparse:
-                    _, rows, rl = self.model.word_embedding_span()
-                    K.adam(A.master, A.grad, self.m, self.v, A.shadow, self.step_t, self.lr, b1, b2, self.eps,
-                           self.weight_decay, self.decoupled, self.model.emb_ever, self.model.emb_now, woff, rows,
-                           rl, runs=table)
-                else:
-                    K.adam(A.master, A.grad, self.m, self.v, A.shadow, self.step_t, self.lr, b1, b2, self.eps,
-                           self.weight_decay, self.decoupled, runs=table)
+                K.adam(A.master, A.grad, self.m, self.v, A.shadow, self.step_t, self.lr, b1, b2, self.eps,
+                       self.weight_decay, self.decoupled, runs=table)
             else:
                 for off, n in runs:
                     self._update(off, n, sparse and off <= woff < off + n)

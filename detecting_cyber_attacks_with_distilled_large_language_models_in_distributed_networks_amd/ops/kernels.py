@@ -470,6 +470,12 @@ def adam(p, g, m, v, shadow, step, lr, b1, b2, eps, wd, decoupled, touched=None,
                table, total4, end4)
 
 
+def adam_rows(p, g, m, v, shadow, step, lr, b1, b2, eps, ever, now, row_len):
+    """Adam (weight decay 0) over the rows of one [rows][row_len] table (views of the arenas)
+    whose ``ever`` flag is set -- the sparse word-embedding update, one wave per 64 row flags."""
+    ext().adam_rows(p, g, m, v, shadow, step, lr, b1, b2, eps, ever, now, row_len)
+
+
 def adam_runs(spans, device):
     """[(offset, numel)] element runs (multiples of 4, ascending, disjoint) -> the kernel's
     run table [start4, count4, prefix4] on ``device`` + its total and largest end (float4s)."""

@@ -200,3 +200,27 @@ def test_adam_run_table_matches_per_run_launches():
     for off, ln in runs:
         untouched[off:off + ln] = False
     assert torch.equal(a[0][untouched], base[0][untouched])
+
+
+def test_adam_rows_matches_flagged_dense_adam():
+    """The word-embedding update by row flags (adam_rows: one wave per 64 row flags) is bitwise
+    the dense launch that skips unflagged rows: rows with state but no gradient this step take
+    the g = 0 update, rows without state are left untouched."""
+    rows, rl = 1000, 768
+    n = rows * rl
+    g = torch.Generator(device=DEV).manual_seed(4)
+    base = [torch.randn(n, device=DEV, generator=g), torch.randn(n, device=DEV, generator=g),
+            torch.rand(n, device=DEV, generator=g) * 1e-3, torch.rand(n, device=DEV, generator=g) * 1e-6]
+    ever = (torch.rand(rows, device=DEV, generator=g) < 0.2).to(torch.uint8)
+    now = ((torch.rand(rows, device=DEV, generator=g) < 0.5).to(torch.uint8) * ever).contiguous()
+    a = [t.clone() for t in base]
+    b = [t.clone() for t in base]
+    sha, shb = a[0].to(torch.bfloat16), b[0].to(torch.bfloat16)
+    step = torch.tensor([3], dtype=torch.int32, device=DEV)
+    K.adam_rows(a[0], a[1], a[2], a[3], sha, step, 1e-3, 0.9, 0.999, 1e-8, ever, now, rl)
+    K.adam(b[0], b[1], b[2], b[3], shb, step, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, ever, now, 0, rows, rl)
+    torch.cuda.synchronize()
+    for x, y in zip(a + [sha], b + [shb]):
+        assert torch.equal(x, y)
+    untouched = ever.repeat_interleave(rl) == 0
+    assert torch.equal(a[0][untouched], base[0][untouched])
