@@ -399,32 +399,48 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
   } else if constexpr (EPI == EPI_F32) {
     f32_epilogue<BM, BN, NT>(p, smem, LDC, m0, n0, tid, slot);
   } else {
-    constexpr int CPR = BN / 4;  // 4 fp32 per chunk
+    // 8 fp32 per chunk: two float4 LDS reads, then one 16-byte load / store per global stream
+    constexpr int CPR = BN / 8;
     constexpr bool CS_OK = NT % CPR == 0;  // a thread keeps one column chunk for the whole tile
-    float cs[4] = {0.f, 0.f, 0.f, 0.f};  // column sums of this thread's rows (p.colsum)
-#pragma unroll 4
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums of this thread's rows (p.colsum)
+#pragma unroll 2
     for (int id = tid; id < BM * CPR; id += NT) {
       const int r = id / CPR, cc = id - r * CPR;
       const int m = m0 + r;
       if (m >= p.M) break;
-      const float4 v = *reinterpret_cast<const float4*>(smem + r * LDC + cc * 16);
-      const int n = n0 + cc * 4;
-      {
-        float v0 = v.x, v1 = v.y, v2 = v.z, v3 = v.w;
-        if constexpr (EPI == EPI_GELU_BWD) {
-          const uint2 u = *reinterpret_cast<const uint2*>(p.aux + (size_t)m * p.ldaux + n);
-          v0 *= gelu_erf_grad(lo_bf(u.x)); v1 *= gelu_erf_grad(hi_bf(u.x));
-          v2 *= gelu_erf_grad(lo_bf(u.y)); v3 *= gelu_erf_grad(hi_bf(u.y));
-          if (p.aux_out) gelu_remat(p, m, n, u);
-        } else {  // EPI_ADD
-          const uint2 r2 = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldres + n);
-          v0 += lo_bf(r2.x); v1 += hi_bf(r2.x); v2 += lo_bf(r2.y); v3 += hi_bf(r2.y);
+      const float4 va = *reinterpret_cast<const float4*>(smem + r * LDC + cc * 32);
+      const float4 vb = *reinterpret_cast<const float4*>(smem + r * LDC + cc * 32 + 16);
+      float v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+      const int n = n0 + cc * 8;
+      if constexpr (EPI == EPI_GELU_BWD) {
+        const uint4 u = *reinterpret_cast<const uint4*>(p.aux + (size_t)m * p.ldaux + n);
+        const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] *= gelu_erf_grad(lo_bf(uw[e]));
+          v[2 * e + 1] *= gelu_erf_grad(hi_bf(uw[e]));
         }
-        bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-        const uint2 o = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
-        *reinterpret_cast<uint2*>(C + (size_t)m * p.ldc + n) = o;
-        // the sums are of the stored (bf16) values: what a separate column sum would read
-        if constexpr (CS_OK) { cs[0] += lo_bf(o.x); cs[1] += hi_bf(o.x); cs[2] += lo_bf(o.y); cs[3] += hi_bf(o.y); }
+        if (p.aux_out) {
+          gelu_remat(p, m, n, make_uint2(u.x, u.y));
+          gelu_remat(p, m, n + 4, make_uint2(u.z, u.w));
+        }
+      } else {  // EPI_ADD
+        const uint4 r2 = *reinterpret_cast<const uint4*>(p.res + (size_t)m * p.ldres + n);
+        const uint32_t rw[4] = {r2.x, r2.y, r2.z, r2.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += lo_bf(rw[e]);
+          v[2 * e + 1] += hi_bf(rw[e]);
+        }
+      }
+      bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+      const uint4 o = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+      *reinterpret_cast<uint4*>(C + (size_t)m * p.ldc + n) = o;
+      // the sums are of the stored (bf16) values: what a separate column sum would read
+      if constexpr (CS_OK) {
+        const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { cs[2 * e] += lo_bf(ow[e]); cs[2 * e + 1] += hi_bf(ow[e]); }
       }
     }
     if (CS_OK && p.colsum) {
@@ -435,7 +451,7 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
       __syncthreads();  // every thread is done reading the staged tile
       const int cc = tid % CPR, g = tid / CPR;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) red[g * BN + cc * 4 + e] = cs[e];
+      for (int e = 0; e < 8; ++e) red[g * BN + cc * 8 + e] = cs[e];
       __syncthreads();
       for (int c = tid; c < BN; c += NT) {
         float s = 0.f;
