@@ -101,6 +101,29 @@ DEV void tile_coords(int lid, int tiles_m, int tiles_n, int gm, int& tm, int& tn
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void gbl_void;
 
+// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): 1 KiB to the wave-uniform LDS address
+// `lds`, each lane from its own `src`.  FD_GLDS_ASM (default): issued from inline asm, so hipcc
+// does not track it -- the ring's counted s_waitcnt vmcnt (wait_tiles) is the only wait.  With the
+// builtin, hipcc cannot tell the DMA's LDS write apart from the transposing ds_read_b64_tr_b16
+// fragment reads of MN-major operands and waits vmcnt(0) right after every K tile's DMA issue
+// (measured in the .s of every TN weight-gradient kernel): the next tile's DMA latency then sits
+// inside the K loop instead of behind the current tile's MFMAs.  Every path drains the ring
+// (vmcnt(0)) before the epilogue reuses the LDS, which __syncthreads() alone would not do.
+#ifndef FD_GLDS_ASM
+#define FD_GLDS_ASM 1
+#endif
+DEV void glds16(const void* src, char* lds) {
+#if FD_GLDS_ASM
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(lds_void*)lds);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+#else
+  __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds, 16, 0, 0);
+#endif
+}
+
 // Swizzle of 16-byte chunks for an MN-major ([k][mn]) sub-image of width W.
 template <int W>
 DEV int fk(int k) {
@@ -140,8 +163,28 @@ struct Operand {
         const int k = lp / SUB_CH, c = (lp % SUB_CH) ^ fk<SUB>(k);
         off = (uint32_t)(k * ld + sub * SUB + c * 8) * 2u;
       }
-      __builtin_amdgcn_global_load_lds((gbl_void*)(sbase + off), (lds_void*)(lds + piece * 1024), 16, 0, 0);
+      glds16(sbase + off, lds + piece * 1024);
     }
+  }
+
+  // One of stage()'s PER_WAVE pieces (i): the interleaved-DMA K loop spreads a tile's pieces
+  // over the MFMAs of the previous tile instead of issuing them in one burst.
+  DEV static void stage_one(const bf16_t* base, int ld, int row0, int k0, int lim, char* lds, int wid, int lane,
+                            int i) {
+    const char* sbase = reinterpret_cast<const char*>(KMAJ ? base + k0 : base + (size_t)k0 * ld + row0);
+    const int piece = wid * PER_WAVE + i;
+    const int pos = piece * 64 + lane;
+    uint32_t off;
+    if constexpr (KMAJ) {
+      const int r = pos >> 3, c = (pos & 7) ^ ksw(r);
+      const int gr = min(row0 + r, lim - 1);
+      off = (uint32_t)(gr * ld + c * 8) * 2u;
+    } else {
+      const int sub = pos / (SUB_BYTES / 16), lp = pos % (SUB_BYTES / 16);
+      const int k = lp / SUB_CH, c = (lp % SUB_CH) ^ fk<SUB>(k);
+      off = (uint32_t)(k * ld + sub * SUB + c * 8) * 2u;
+    }
+    glds16(sbase + off, lds + piece * 1024);
   }
 
   // MFMA fragment for rows [row0, row0+16) and k-step s (32 deep).
@@ -222,8 +265,12 @@ DEV void adam_epi4(const FdAdamEpi& a, size_t i, float4 g4, float step_size, flo
 }
 
 // Weight-gradient (fp32) epilogue; see GemmParams::out for the three modes.
+// flag: a 4-byte slot of the kernel's one LDS array (GemmCfg::FLAG).  A second __shared__ object
+// next to the LDS-DMA ring makes hipcc wait vmcnt(0) right after every K tile's DMA issue (the
+// DMA latency then sits in the K loop; gfx950 guide, 'three .s-level traps').
 template <int BM, int BN, int NT>
-DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0, int n0, int tid, int slot) {
+DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0, int n0, int tid, int slot,
+                      int* flag) {
   constexpr int CPR = BN / 4;  // 4 fp32 per chunk
   if (p.out == nullptr) {      // legacy: slab z, reduced by a separate launch
     float* C = reinterpret_cast<float*>(p.C) + (size_t)blockIdx.z * p.slab_stride;
@@ -249,12 +296,11 @@ DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0
           *reinterpret_cast<const float4*>(smem + r * ldc_lds + cc * 16);
     }
     // release this split's slab at device scope (other XCDs' L2s), then count the arrival
-    __shared__ int s_last;
     __threadfence();
     __syncthreads();
-    if (tid == 0) s_last = atomicAdd(p.tile_cnt + slot, 1) == (int)gridDim.z - 1;
+    if (tid == 0) *flag = atomicAdd(p.tile_cnt + slot, 1) == (int)gridDim.z - 1;
     __syncthreads();
-    if (!s_last) return;
+    if (!*flag) return;
     __threadfence();  // acquire: the other splits' slabs are visible
   }
   const bool adam = p.adam.p != nullptr;
@@ -337,7 +383,7 @@ DEV void gelu_remat(const GemmParams& p, int m, int n, const uint2& u) {
 
 template <int BM, int BN, int TM, int TN, int EPI, int NT>
 DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int m0, int n0,
-                         int wr, int wc, int lane, int tid, int slot) {
+                         int wr, int wc, int lane, int tid, int slot, int* flag) {
   using TR = EpiTraits<EPI, BM, BN>;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int LDC = BN * TR::ES + 16;
@@ -397,7 +443,7 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
       }
     }
   } else if constexpr (EPI == EPI_F32) {
-    f32_epilogue<BM, BN, NT>(p, smem, LDC, m0, n0, tid, slot);
+    f32_epilogue<BM, BN, NT>(p, smem, LDC, m0, n0, tid, slot, flag);
   } else {
     // 8 fp32 per chunk: two float4 LDS reads, then one 16-byte load / store per global stream
     constexpr int CPR = BN / 8;
@@ -760,6 +806,29 @@ DEV void sched_ktile() {
   __builtin_amdgcn_sched_group_barrier(0x008, M, 0);
 }
 
+// Interleaved-DMA variant: as sched_ktile for the first set (its reads, then its MFMAs each
+// followed by RPM of the second set's reads), then the second set's MFMAs in groups of G, each
+// followed by ONE LDS-DMA piece of the next K tile (V pieces).  An LDS-DMA wave-instruction
+// costs ~60-185 issue cycles; in one burst after the barrier it holds the wave off the MFMA
+// pipe, spread out it hides behind the MFMAs.  (The pieces write LDS, so they cannot move
+// above this tile's ds_reads: they go in the second half.)
+template <int V, int G>
+DEV void sched_vmem_groups() {
+  if constexpr (V > 0) {
+    __builtin_amdgcn_sched_group_barrier(0x008, G, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (the LDS-DMA piece)
+    sched_vmem_groups<V - 1, G>();
+  }
+}
+template <int R, int M, int V>
+DEV void sched_ktile_ilv() {
+  constexpr int G = M / V > 0 ? M / V : 1;
+  __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+  sched_interleave<M, (R + M - 1) / M>();
+  sched_vmem_groups<V, G>();
+  if constexpr (M - V * G > 0) __builtin_amdgcn_sched_group_barrier(0x008, M - V * G, 0);
+}
+
 template <int N>
 DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -784,7 +853,10 @@ struct GemmCfg {
   // DIRECT fp32 tiles are staged one wave-row band (BM / WM rows) at a time
   static constexpr int EPI_BYTES = EpiTraits<EPI, BM, BN>::DIRECT ? (BM / WM) * (BN * 4 + 16)
                                                                    : EpiTraits<EPI, BM, BN>::BYTES;
-  static constexpr int SMEM = S * BUF > EPI_BYTES ? S * BUF : EPI_BYTES;
+  static constexpr int SMEM0 = S * BUF > EPI_BYTES ? S * BUF : EPI_BYTES;
+  // fp32 epilogues keep their split-K "last arriver" flag in the same LDS array (f32_epilogue)
+  static constexpr int FLAG = SMEM0;
+  static constexpr int SMEM = SMEM0 + (EPI == EPI_F32 ? 16 : 0);
   // (the accumulator-direct fp32 epilogue serves only the all-layer weight-gradient launch)
   static constexpr bool VALID = SMEM <= LDS_MAX && !EpiTraits<EPI, BM, BN>::DIRECT &&
                                 (!EpiTraits<EPI, BM, BN>::LN || EpiTraits<EPI, BM, BN>::F32S) &&
@@ -810,7 +882,7 @@ struct GemmGroup {
 
 // One output tile (tm, tn) of problem p: the K loop over the LDS-DMA ring, then the epilogue.
 // slot = split-K arrival slot.
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool ILV = false>
 DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   using OA = typename G::OA;
@@ -866,7 +938,32 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
     if constexpr (!SCHED) __builtin_amdgcn_s_setprio(0);
   };
 
-  if constexpr (S < 6) {
+  if constexpr (ILV) {
+    static_assert(S < 6, "interleaved DMA: one K tile per barrier");
+    // Same ring protocol as below, but tile kt+S-1's pieces are issued one by one between
+    // tile kt's MFMAs (sched_ktile_ilv).  Branch-free body (a branch would end the scheduling
+    // region): past the last tile the pieces re-read the last tile into the free slot, and
+    // everything is drained before the epilogue touches the LDS.
+#pragma unroll
+    for (int t = 0; t < S - 1; ++t)
+      if (t < nk) issue(t);
+    for (int kt = 0; kt < nk; ++kt) {
+      wait_tiles<L, S - 2>(min(S - 2, nk - 1 - kt));
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int tn_ = kt + S - 1;
+      const int kload = kbeg + min(tn_, nk - 1) * BKT;
+      char* b = smem + (tn_ % S) * BUF;
+      read_frags(smem + (kt % S) * BUF);
+      mfmas();
+#pragma unroll
+      for (int j = 0; j < OA::PER_WAVE; ++j) OA::stage_one(p.A, p.lda, m0, kload, p.M, b, wid, lane, j);
+#pragma unroll
+      for (int j = 0; j < OB::PER_WAVE; ++j) OB::stage_one(p.B, p.ldb, n0, kload, p.N, b + OA::BYTES, wid, lane, j);
+      sched_ktile_ilv<MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2), MI * NI, L>();
+    }
+    wait_vm<0>();
+  } else if constexpr (S < 6) {
 #pragma unroll
     for (int t = 0; t < S - 1; ++t)
       if (t < nk) issue(t);
@@ -930,7 +1027,8 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
         }
       }
       __syncthreads();
-      f32_epilogue<TM, BN, 64 * NW>(p, smem, LDC, m0 + band * TM, n0, tid, slot);
+      f32_epilogue<TM, BN, 64 * NW>(p, smem, LDC, m0 + band * TM, n0, tid, slot,
+                                    reinterpret_cast<int*>(smem + G::FLAG));
     }
     (void)direct_f32_epilogue<TM, TN>;
   } else if constexpr (EpiTraits<EPI, BM, BN>::LN) {
@@ -940,16 +1038,17 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
     // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
     // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
     __syncthreads();
-    staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid, slot);
+    staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid, slot,
+                                                  reinterpret_cast<int*>(smem + G::FLAG));
   }
 }
 
 // bid = the tile's index within p, walked in group-M order
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool ILV = false>
 DEV void gemm_tile(const GemmParams& p, int bid, int slot, char* smem) {
   int tm, tn;
   tile_coords(bid, (p.M + BM - 1) / BM, p.N / BN, p.group_m, tm, tn);
-  gemm_tile_at<BM, BN, AK, BKM, EPI, WM, WN, S>(p, tm, tn, slot, smem);
+  gemm_tile_at<BM, BN, AK, BKM, EPI, WM, WN, S, ILV>(p, tm, tn, slot, smem);
 }
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
@@ -996,7 +1095,7 @@ struct DwBatch {
   int decoupled;
 };
 
-template <int BM, int BN, int WM, int WN, int S>
+template <int BM, int BN, int WM, int WN, int S, bool ILV = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch bt) {
   using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S>;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
@@ -1017,7 +1116,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch 
     p.adam.lr = bt.lr; p.adam.b1 = bt.b1; p.adam.b2 = bt.b2; p.adam.eps = bt.eps; p.adam.wd = bt.wd;
     p.adam.decoupled = bt.decoupled;
   }
-  gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S>(p, lid - q.tile0, 0, smem);
+  gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S, ILV>(p, lid - q.tile0, 0, smem);
 }
 
 // out[i] = (accumulate ? out[i] : 0) + sum_z slab[z][i]   (deterministic split-K reduce)
@@ -1483,6 +1582,11 @@ bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
     case 3: return go(gemm_dw_batch_kernel<256, 192, 4, 2, 2>, 256, 192, 512);
     case 6: return go(gemm_dw_batch_kernel<128, 192, 2, 4, 2>, 128, 192, 512);
     case 11: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 2>, 256, 256, 512);
+    // interleaved LDS-DMA issue (gemm_tile_at ILV)
+    case 31: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 2, true>, 256, 256, 512);
+    case 32: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 2, true>, 128, 128, 256);
+    case 33: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 3, true>, 128, 128, 256);
+    case 34: return go(gemm_dw_batch_kernel<256, 128, 4, 2, 2, true>, 256, 128, 512);
   }
   return false;
 }
