@@ -167,25 +167,6 @@ struct Operand {
     }
   }
 
-  // One of stage()'s PER_WAVE pieces (i): the interleaved-DMA K loop spreads a tile's pieces
-  // over the MFMAs of the previous tile instead of issuing them in one burst.
-  DEV static void stage_one(const bf16_t* base, int ld, int row0, int k0, int lim, char* lds, int wid, int lane,
-                            int i) {
-    const char* sbase = reinterpret_cast<const char*>(KMAJ ? base + k0 : base + (size_t)k0 * ld + row0);
-    const int piece = wid * PER_WAVE + i;
-    const int pos = piece * 64 + lane;
-    uint32_t off;
-    if constexpr (KMAJ) {
-      const int r = pos >> 3, c = (pos & 7) ^ ksw(r);
-      const int gr = min(row0 + r, lim - 1);
-      off = (uint32_t)(gr * ld + c * 8) * 2u;
-    } else {
-      const int sub = pos / (SUB_BYTES / 16), lp = pos % (SUB_BYTES / 16);
-      const int k = lp / SUB_CH, c = (lp % SUB_CH) ^ fk<SUB>(k);
-      off = (uint32_t)(k * ld + sub * SUB + c * 8) * 2u;
-    }
-    glds16(sbase + off, lds + piece * 1024);
-  }
 
   // MFMA fragment for rows [row0, row0+16) and k-step s (32 deep).
   DEV static bf16x8 frag(const char* lds, int row0, int s, int lane) {
@@ -806,29 +787,6 @@ DEV void sched_ktile() {
   __builtin_amdgcn_sched_group_barrier(0x008, M, 0);
 }
 
-// Interleaved-DMA variant: as sched_ktile for the first set (its reads, then its MFMAs each
-// followed by RPM of the second set's reads), then the second set's MFMAs in groups of G, each
-// followed by ONE LDS-DMA piece of the next K tile (V pieces).  An LDS-DMA wave-instruction
-// costs ~60-185 issue cycles; in one burst after the barrier it holds the wave off the MFMA
-// pipe, spread out it hides behind the MFMAs.  (The pieces write LDS, so they cannot move
-// above this tile's ds_reads: they go in the second half.)
-template <int V, int G>
-DEV void sched_vmem_groups() {
-  if constexpr (V > 0) {
-    __builtin_amdgcn_sched_group_barrier(0x008, G, 0);
-    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (the LDS-DMA piece)
-    sched_vmem_groups<V - 1, G>();
-  }
-}
-template <int R, int M, int V>
-DEV void sched_ktile_ilv() {
-  constexpr int G = M / V > 0 ? M / V : 1;
-  __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
-  sched_interleave<M, (R + M - 1) / M>();
-  sched_vmem_groups<V, G>();
-  if constexpr (M - V * G > 0) __builtin_amdgcn_sched_group_barrier(0x008, M - V * G, 0);
-}
-
 template <int N>
 DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -882,7 +840,7 @@ struct GemmGroup {
 
 // One output tile (tm, tn) of problem p: the K loop over the LDS-DMA ring, then the epilogue.
 // slot = split-K arrival slot.
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool ILV = false>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool PIPE = false>
 DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   using OA = typename G::OA;
@@ -938,30 +896,68 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
     if constexpr (!SCHED) __builtin_amdgcn_s_setprio(0);
   };
 
-  if constexpr (ILV) {
-    static_assert(S < 6, "interleaved DMA: one K tile per barrier");
-    // Same ring protocol as below, but tile kt+S-1's pieces are issued one by one between
-    // tile kt's MFMAs (sched_ktile_ilv).  Branch-free body (a branch would end the scheduling
-    // region): past the last tile the pieces re-read the last tile into the free slot, and
-    // everything is drained before the epilogue touches the LDS.
+  if constexpr (PIPE) {
+    // Register-pipelined ring (one K tile per barrier): the fragments of tile kt+1 are read
+    // while tile kt's MFMAs run from the other fragment buffer, so no wave waits on LDS latency
+    // inside the loop.  Every step issues exactly one tile group of LDS-DMA (past the last tile
+    // the sources are clamped to it and the data lands in a slot nobody reads), so the counted
+    // wait is a constant: at the top of step kt tiles 0 .. kt+S-2 are issued and tile kt+1 must
+    // have landed -> vmcnt((S-3) * L).  WAR: step kt refills the slot of tile kt-1, whose
+    // fragments were read in step kt-2 and consumed in step kt-1, before the barrier.
+    static_assert(S >= 3, "pipelined ring: at least one tile in flight");
+    static_assert((S - 2) * L <= 63, "vmcnt is 6 bits");
+    bf16x8 fa[2][2][MI], fb[2][2][NI];
+    auto issue_c = [&](int t) {
+      char* b = smem + (t % S) * BUF;
+      const int k0 = kbeg + min(t, nk - 1) * BKT;
+      OA::stage(p.A, p.lda, m0, k0, p.M, b, wid, lane);
+      OB::stage(p.B, p.ldb, n0, k0, p.N, b + OA::BYTES, wid, lane);
+    };
+    auto read_into = [&](auto bufc, int t) {
+      constexpr int q = decltype(bufc)::value;
+      const char* cur = smem + (t % S) * BUF;
 #pragma unroll
-    for (int t = 0; t < S - 1; ++t)
-      if (t < nk) issue(t);
-    for (int kt = 0; kt < nk; ++kt) {
-      wait_tiles<L, S - 2>(min(S - 2, nk - 1 - kt));
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) fa[q][h][i] = OA::frag(cur, wr * TM + i * 16, h, lane);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) fb[q][h][j] = OB::frag(cur + OA::BYTES, wc * TN + j * 16, h, lane);
+      }
+    };
+    auto mfma_from = [&](auto bufc) {
+      constexpr int q = decltype(bufc)::value;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(fb[q][h][j], fa[q][h][i], acc[i][j]);
+    };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    constexpr int RD = 2 * (MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2));  // ds_read instructions per tile
+    constexpr int MF = 2 * MI * NI;                                    // MFMAs per tile
+    auto step = [&](int kt, auto cur, auto nxt) {
+      wait_vm<(S - 3) * L>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      const int tn_ = kt + S - 1;
-      const int kload = kbeg + min(tn_, nk - 1) * BKT;
-      char* b = smem + (tn_ % S) * BUF;
-      read_frags(smem + (kt % S) * BUF);
-      mfmas();
+      issue_c(kt + S - 1);
+      read_into(nxt, kt + 1);
+      mfma_from(cur);
+      sched_interleave<MF, (RD + MF - 1) / MF>();
+    };
 #pragma unroll
-      for (int j = 0; j < OA::PER_WAVE; ++j) OA::stage_one(p.A, p.lda, m0, kload, p.M, b, wid, lane, j);
-#pragma unroll
-      for (int j = 0; j < OB::PER_WAVE; ++j) OB::stage_one(p.B, p.ldb, n0, kload, p.N, b + OA::BYTES, wid, lane, j);
-      sched_ktile_ilv<MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2), MI * NI, L>();
+    for (int t = 0; t < S - 1; ++t) issue_c(t);
+    wait_vm<(S - 2) * L>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read_into(B0{}, 0);
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      step(kt, B0{}, B1{});
+      step(kt + 1, B1{}, B0{});
     }
+    if (kt < nk) step(kt, B0{}, B1{});
     wait_vm<0>();
   } else if constexpr (S < 6) {
 #pragma unroll
@@ -1011,6 +1007,7 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
     // fp32 tile too large for LDS: finish it one wave-row band (TM rows) at a time through the
     // staged row-chunk epilogue (coalesced 16-byte rows for the gradient / Adam streams)
     constexpr int LDC = BN * 4 + 16;
+    if (p.diag & 4) return;
 #pragma unroll 1
     for (int band = 0; band < WM; ++band) {
       __syncthreads();  // ring slots (first band) / the previous band's staging are free
@@ -1044,14 +1041,14 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
 }
 
 // bid = the tile's index within p, walked in group-M order
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool ILV = false>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool PIPE = false>
 DEV void gemm_tile(const GemmParams& p, int bid, int slot, char* smem) {
   int tm, tn;
   tile_coords(bid, (p.M + BM - 1) / BM, p.N / BN, p.group_m, tm, tn);
-  gemm_tile_at<BM, BN, AK, BKM, EPI, WM, WN, S, ILV>(p, tm, tn, slot, smem);
+  gemm_tile_at<BM, BN, AK, BKM, EPI, WM, WN, S, PIPE>(p, tm, tn, slot, smem);
 }
 
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool PIPE = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, GemmGroup grp) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
@@ -1060,18 +1057,18 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
   const bool second = bid >= grp.ntiles0;  // block-uniform
   const GemmParams& p = second ? grp.q : p0;
   if (second) bid -= grp.ntiles0;
-  gemm_tile<BM, BN, AK, BKM, EPI, WM, WN, S>(p, bid, slot, smem);
+  gemm_tile<BM, BN, AK, BKM, EPI, WM, WN, S, PIPE>(p, bid, slot, smem);
 }
 
 // LayerNorm-fused NT GEMM (EPI_LN / EPI_LN_BWD): the tiles of a row block are consecutive
 // logical tiles (row-major tile order), so after the XCD remap they run on one XCD, in order.
-template <int BM, int BN, int EPI, int WM, int WN, int S>
+template <int BM, int BN, int EPI, int WM, int WN, int S, bool PIPE = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_ln_kernel(GemmParams p) {
   using G = GemmCfg<BM, BN, true, true, EPI, WM, WN, S>;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   const int tiles_n = p.N / BN;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  gemm_tile_at<BM, BN, true, true, EPI, WM, WN, S>(p, lid / tiles_n, lid % tiles_n, 0, smem);
+  gemm_tile_at<BM, BN, true, true, EPI, WM, WN, S, PIPE>(p, lid / tiles_n, lid % tiles_n, 0, smem);
 }
 
 // ---------------------------------------------------------------- all-layer weight gradients
@@ -1090,16 +1087,15 @@ using DwProb = FdDwProb;  // adam_epi.h (shared with the host binding)
 struct DwBatch {
   DwProb pr[DWB_MAXP];
   int n, K, ntiles, group_m;
+  int diag;  // FD_GEMM_DIAG (profiling only)
   const int* step;
   float lr, b1, b2, eps, wd;
   int decoupled;
 };
 
-template <int BM, int BN, int WM, int WN, int S, bool ILV = false>
-__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch bt) {
-  using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S>;
-  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
-  const int lid = xcd_remap(blockIdx.x, bt.ntiles);
+// One tile of the batch: logical tile id lid -> (problem, tile) -> K loop + epilogue.
+template <int BM, int BN, int WM, int WN, int S, bool PIPE>
+DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
   int i = 0;
   while (i + 1 < bt.n && lid >= bt.pr[i + 1].tile0) ++i;  // block-uniform
   const DwProb& q = bt.pr[i];
@@ -1109,6 +1105,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch 
   p.lda = q.M; p.ldb = q.N; p.ldc = q.N;
   p.k_split = bt.K;
   p.group_m = bt.group_m;
+  p.diag = bt.diag;
   p.out = q.C;
   p.accumulate = q.accumulate;
   if (q.p) {
@@ -1116,7 +1113,57 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch 
     p.adam.lr = bt.lr; p.adam.b1 = bt.b1; p.adam.b2 = bt.b2; p.adam.eps = bt.eps; p.adam.wd = bt.wd;
     p.adam.decoupled = bt.decoupled;
   }
-  gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S, ILV>(p, lid - q.tile0, 0, smem);
+  gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S, PIPE>(p, lid - q.tile0, 0, smem);
+}
+
+template <int BM, int BN, int WM, int WN, int S, bool PIPE = false>
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch bt) {
+  using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S>;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  dwb_tile<BM, BN, WM, WN, S, PIPE>(bt, xcd_remap(blockIdx.x, bt.ntiles), smem);
+}
+
+// Persistent, dynamically scheduled variant: a fixed grid (slots x CUs workgroups) pulls tiles from
+// per-XCD counters; XCD x (blocks b with b % 8 == x, the dispatcher's round robin) walks the same
+// contiguous range of logical tiles as xcd_remap gives it, so the L2 sharing of the static grid is
+// kept.  Why: in the static grid every tile of a round reaches its Adam epilogue (HBM-bound, ~26 B
+// per parameter) at the same moment and every CU then waits on HBM with its MFMAs idle; the
+// blocks of the second slot (blockIdx >= gridDim / 2) start `delay` ns late, so a CU's two blocks
+// alternate -- one streams its Adam epilogue while the other runs its K loop -- and a block that
+// finishes early simply takes the next tile.  Each tile is still computed whole by one block
+// (full K, fixed-order epilogue): the result does not depend on the schedule.  The counters live
+// in device memory (g_dwb_sched) and the last block to leave resets them, so graph replays need no
+// memset; at most one persistent dW launch may run at a time on a device.
+__device__ int g_dwb_sched[16];  // [0, 8): per-XCD tile counters, [8]: blocks finished
+
+template <int BM, int BN, int WM, int WN, int S>
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_persist_kernel(DwBatch bt, long long delay_ns) {
+  using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S>;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  int* s_tile = reinterpret_cast<int*>(smem + G::FLAG);
+  const int xcd = blockIdx.x % 8;
+  const int q = bt.ntiles / 8, r = bt.ntiles % 8;
+  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int cnt = q + (xcd < r ? 1 : 0);
+  if (delay_ns > 0 && blockIdx.x >= gridDim.x / 2) {
+    const unsigned long long t0 = wall_clock64();  // 100 MHz
+    while ((long long)(wall_clock64() - t0) * 10 < delay_ns) __builtin_amdgcn_s_sleep(32);
+  }
+  for (;;) {
+    __syncthreads();  // the previous tile's epilogue is done with the LDS (and with *s_tile)
+    if (threadIdx.x == 0) *s_tile = atomicAdd(g_dwb_sched + xcd, 1);
+    __syncthreads();
+    const int t = *s_tile;
+    if (t >= cnt) break;
+    dwb_tile<BM, BN, WM, WN, S, false>(bt, lo + t, smem);
+  }
+  if (threadIdx.x == 0) {
+    // every block that fetched from the counters has left its loop once all gridDim.x arrived
+    if (atomicAdd(g_dwb_sched + 8, 1) == (int)gridDim.x - 1) {
+      for (int x = 0; x < 8; ++x) atomicExch(g_dwb_sched + x, 0);
+      atomicExch(g_dwb_sched + 8, 0);
+    }
+  }
 }
 
 // out[i] = (accumulate ? out[i] : 0) + sum_z slab[z][i]   (deterministic split-K reduce)
@@ -1179,7 +1226,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_batched_kernel(ReduceBatch 
 // (A ping-pong variant -- the two 4-wave halves of an 8-wave block staggered by
 // one barrier phase so one half's LDS reads overlap the other's MFMAs -- was
 // correct but measured 1.5-3x slower on these shapes; not kept.)
-constexpr int NCFG = 25;
+// register-pipelined K loop (gemm_tile_at PIPE; fragments of tile kt+1 read under tile kt's MFMAs):
+// 25: 128 x 128, 2x2, S3    26: 128 x 128, 2x2, S4    27: 128 x 192, 2x4, S3
+// 28: 128 x  64, 4x2, S4    29: 128 x  64, 4x2, S6    30: 128 x 128, 4x2, S3
+constexpr int NCFG = 31;
 struct CfgDesc { int bm, bn, wm, wn, s; };
 constexpr CfgDesc CFGS[NCFG] = {{128, 64, 2, 2, 3}, {128, 128, 2, 2, 2}, {128, 96, 2, 2, 2}, {256, 192, 4, 2, 2},
                                 {256, 128, 4, 2, 3}, {64, 192, 1, 4, 3}, {128, 192, 2, 4, 2}, {256, 96, 4, 1, 3},
@@ -1187,9 +1237,10 @@ constexpr CfgDesc CFGS[NCFG] = {{128, 64, 2, 2, 3}, {128, 128, 2, 2, 2}, {128, 9
                                 {256, 128, 4, 2, 2}, {64, 64, 2, 2, 3},    {64, 128, 2, 2, 3},  {128, 64, 2, 2, 4},
                                 {128, 64, 2, 2, 5},  {128, 128, 2, 2, 4}, {128, 64, 4, 2, 3},  {128, 64, 4, 2, 2},
                                 {128, 64, 2, 4, 3},  {128, 128, 4, 2, 3}, {128, 64, 2, 2, 6},  {64, 64, 2, 2, 6},
-                                {128, 64, 4, 2, 6}};
+                                {128, 64, 4, 2, 6},  {128, 128, 2, 2, 3}, {128, 128, 2, 2, 4}, {128, 192, 2, 4, 3},
+                                {128, 64, 4, 2, 4},  {128, 64, 4, 2, 6},  {128, 128, 4, 2, 3}};
 
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool PIPE = false>
 bool launch_cfg(const GemmParams& p, int splits, hipStream_t st, const GemmParams* q) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   if constexpr (!G::VALID) {
@@ -1205,7 +1256,8 @@ bool launch_cfg(const GemmParams& p, int splits, hipStream_t st, const GemmParam
       grp.ntiles += (q->M / BM) * (q->N / BN);
     }
     const dim3 grid(grp.ntiles, 1, splits);
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKM, EPI, WM, WN, S>), grid, dim3(64 * WM * WN), 0, st, p, grp);
+    if constexpr (PIPE && EPI == EPI_F32) return false;  // (split-K weight gradients: the plain loops)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKM, EPI, WM, WN, S, PIPE>), grid, dim3(64 * WM * WN), 0, st, p, grp);
     return true;
   }
 }
@@ -1238,6 +1290,12 @@ bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st, const Ge
     case 22: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 6>(p, splits, st, q);
     case 23: return launch_cfg<64, 64, AK, BKM, EPI, 2, 2, 6>(p, splits, st, q);
     case 24: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 6>(p, splits, st, q);
+    case 25: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 3, true>(p, splits, st, q);
+    case 26: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 4, true>(p, splits, st, q);
+    case 27: return launch_cfg<128, 192, AK, BKM, EPI, 2, 4, 3, true>(p, splits, st, q);
+    case 28: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 4, true>(p, splits, st, q);
+    case 29: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 6, true>(p, splits, st, q);
+    case 30: return launch_cfg<128, 128, AK, BKM, EPI, 4, 2, 3, true>(p, splits, st, q);
   }
   return false;
 }
@@ -1278,6 +1336,9 @@ int pick_cfg(int kind, int M, int N, int K) {
   if (kind == 0) {  // NT forward (and dX on transposed weights)
     // FFN1 forward / FFN2 dX (N = 3072): 256x192 fills the chip at M = 4096 (padded bs32),
     // 128x128 wins at the packed M ~ 2.7 k (21.5 vs 25.7 us; profiles/r1_gemm_cfg_sweep_T2688_packed.txt)
+    // FD_GEMM_WIDE_CFG=<id>: configuration of the N >= 1536 NT GEMMs (QKV / FFN1 forward, FFN2 dX)
+    static const int wide = [] { const char* e = getenv("FD_GEMM_WIDE_CFG"); return e ? atoi(e) : -1; }();
+    if (wide >= 0 && wide < NCFG && N >= 1536 && M >= 1024 && M <= 4096 && tiles_of(wide, M, N) > 0) return wide;
     if (N % 192 == 0 && N >= 3072 && M >= 3584) return 3;
     if (N % 128 == 0 && N >= 3072 && M >= 2048) return 1;
     if (N % 192 == 0 && N >= 1536 && M >= 2048) return 6;
@@ -1570,7 +1631,31 @@ bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
     if (!dry) hipLaunchKernelGGL(kern, dim3(t), dim3(threads), 0, st, bt);
     return true;
   };
+  // persistent variants: slots x CUs blocks, the second slot delayed by FD_DWB_DELAY_NS
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  static const long long delay = [] { const char* e = getenv("FD_DWB_DELAY_NS"); return e ? atoll(e) : 20000ll; }();
+  auto persist = [&](auto kern, int bm, int bn, int threads, int slots) {
+    for (int i = 0; i < bt.n; ++i)
+      if (bt.pr[i].M % bm || bt.pr[i].N % bn) return false;
+    int t = 0;
+    for (int i = 0; i < bt.n; ++i) {
+      bt.pr[i].tile0 = t;
+      t += (bt.pr[i].M / bm) * (bt.pr[i].N / bn);
+    }
+    bt.ntiles = t;
+    if (!dry) hipLaunchKernelGGL(kern, dim3(slots * ncu), dim3(threads), 0, st, bt, slots > 1 ? delay : 0ll);
+    return true;
+  };
   switch (id) {
+    case 41: return persist(gemm_dw_batch_persist_kernel<256, 256, 2, 4, 2>, 256, 256, 512, 1);
+    case 42: return persist(gemm_dw_batch_persist_kernel<128, 128, 2, 2, 2>, 128, 128, 256, 2);
+    case 43: return persist(gemm_dw_batch_persist_kernel<128, 128, 2, 2, 3>, 128, 128, 256, 2);
+    case 44: return persist(gemm_dw_batch_persist_kernel<256, 128, 4, 2, 2>, 256, 128, 512, 1);
     case 0: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 3>, 128, 64, 256);
     case 1: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 2>, 128, 128, 256);
     case 4: return go(gemm_dw_batch_kernel<256, 128, 4, 2, 3>, 256, 128, 512);
@@ -1582,11 +1667,9 @@ bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
     case 3: return go(gemm_dw_batch_kernel<256, 192, 4, 2, 2>, 256, 192, 512);
     case 6: return go(gemm_dw_batch_kernel<128, 192, 2, 4, 2>, 128, 192, 512);
     case 11: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 2>, 256, 256, 512);
-    // interleaved LDS-DMA issue (gemm_tile_at ILV)
-    case 31: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 2, true>, 256, 256, 512);
-    case 32: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 2, true>, 128, 128, 256);
+    // register-pipelined K loop (gemm_tile_at PIPE)
     case 33: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 3, true>, 128, 128, 256);
-    case 34: return go(gemm_dw_batch_kernel<256, 128, 4, 2, 2, true>, 256, 128, 512);
+    case 34: return go(gemm_dw_batch_kernel<256, 128, 4, 2, 3, true>, 256, 128, 512);
   }
   return false;
 }
@@ -1597,6 +1680,8 @@ int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const f
   DwBatch bt{};
   bt.n = n;
   bt.K = K;
+  static const int diag = [] { const char* e = getenv("FD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
+  bt.diag = diag;
   for (int i = 0; i < n; ++i) {
     bt.pr[i] = probs[i];
     if (!probs[i].A || !probs[i].B || (!probs[i].C && !probs[i].p) || probs[i].M <= 0 || probs[i].N <= 0) return 2;
@@ -1684,16 +1769,22 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   const int tiles_m = (M + bm - 1) / bm;
   const dim3 grid(tiles_m * (N / bn));
   auto go = [&](auto kern, int threads) { hipLaunchKernelGGL(kern, grid, dim3(threads), 0, st, p); };
-#define FD_LN_CASE(ID, BM_, BN_, WM_, WN_, S_)                                              \
+#define FD_LN_CASE_P(ID, BM_, BN_, WM_, WN_, S_, P_)                                        \
   case ID:                                                                                 \
-    if (bwd) go(gemm_ln_kernel<BM_, BN_, EPI_LN_BWD, WM_, WN_, S_>, 64 * WM_ * WN_);       \
-    else go(gemm_ln_kernel<BM_, BN_, EPI_LN, WM_, WN_, S_>, 64 * WM_ * WN_);               \
+    if (bwd) go(gemm_ln_kernel<BM_, BN_, EPI_LN_BWD, WM_, WN_, S_, P_>, 64 * WM_ * WN_);   \
+    else go(gemm_ln_kernel<BM_, BN_, EPI_LN, WM_, WN_, S_, P_>, 64 * WM_ * WN_);           \
     break;
+#define FD_LN_CASE(ID, BM_, BN_, WM_, WN_, S_) FD_LN_CASE_P(ID, BM_, BN_, WM_, WN_, S_, false)
   switch (id) {
     FD_LN_CASE(24, 128, 64, 4, 2, 6)
     FD_LN_CASE(0, 128, 64, 2, 2, 3)
     FD_LN_CASE(18, 128, 64, 4, 2, 3)
     FD_LN_CASE(13, 64, 64, 2, 2, 3)
+    // register-pipelined K loop (gemm_tile_at PIPE)
+    FD_LN_CASE_P(30, 128, 64, 4, 2, 6, true)
+    FD_LN_CASE_P(31, 128, 64, 4, 2, 4, true)
+    FD_LN_CASE_P(32, 128, 64, 2, 2, 6, true)
+    FD_LN_CASE_P(33, 128, 64, 2, 2, 4, true)
     default: return -3;
   }
 #undef FD_LN_CASE

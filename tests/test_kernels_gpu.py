@@ -68,6 +68,32 @@ def test_gemm_identity_asymmetric():
     assert torch.equal(y.float(), w.float().t())
 
 
+@pytest.mark.parametrize("cfg", [25, 26, 27, 28, 29, 30])
+def test_gemm_pipelined_configs(cfg):
+    """The register-pipelined K loop (gemm.hip gemm_tile_at PIPE) on every fused epilogue of the
+    NT path, forced through the config override; odd and even K-tile counts, a partial row tile."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops._ext import ext
+    N = 768 if cfg in (28, 29) else 3072 if cfg != 27 else 2304
+    try:
+        ext().gemm_set_cfg(0, cfg, -1)
+        for M, K in ((2600, 768), (640, 704), (2688, 3072)):
+            x, w = bf(M, K, seed=31), bf(N, K, scale=0.05, seed=32)
+            b = torch.randn(N, device=DEV) * 0.1
+            ref = x.float() @ w.float().t()
+            assert rel_err(kn.linear_fwd(x, w, b), ref + b) < 1e-2
+            g, u = kn.linear_fwd(x, w, b, gelu=True)
+            assert rel_err(u, ref + b) < 1e-2
+            assert rel_err(g, torch.nn.functional.gelu((ref + b).float())) < 2e-2
+            res = bf(M, N, seed=33)
+            wt = w.t().contiguous()  # linear_dx on a transposed copy = the NT kernel
+            assert rel_err(kn.linear_dx(x, wt, res=res, wt=w), ref + res.float()) < 1e-2
+            uu = bf(M, N, seed=34).float().requires_grad_(True)
+            gref = torch.autograd.grad(torch.nn.functional.gelu(uu), uu, ref)[0]
+            assert rel_err(kn.linear_dx(x, wt, gelu_u=uu.detach().to(torch.bfloat16), wt=w), gref) < 1e-2
+    finally:
+        ext().gemm_set_cfg(0, -1, -1)
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 768, 768), (4096, 3072, 768), (320, 768, 2304)])
 def test_gemm_nn(M, N, K):
     dy, w = bf(M, K, seed=5), bf(K, N, scale=0.05, seed=6)
