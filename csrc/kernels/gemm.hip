@@ -1700,6 +1700,8 @@ int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const f
   // Group height: A-panels of gm x BM rows x K (bf16) should take ~half of a 4 MiB L2.
   const long long panel = 128ll * K * 2;
   bt.group_m = (int)std::max(1ll, std::min(16ll, (2ll << 20) / panel));
+  static const int gm_env = [] { const char* e = getenv("FD_DWB_GROUP_M"); return e ? atoi(e) : 0; }();
+  if (gm_env > 0) bt.group_m = gm_env;  // tuning override
   if (!dwb_launch_cfg(id, bt, st, true)) {
     id = 8;  // 128 x 64 fits every supported shape (M % 128, N % 64)
     if (!dwb_launch_cfg(id, bt, st, true)) return 4;

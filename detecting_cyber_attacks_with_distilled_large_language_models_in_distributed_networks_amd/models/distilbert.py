@@ -277,6 +277,12 @@ class DDoSClassifier(nn.Module):
         # the memory-bound transposes stretch the concurrent forward GEMMs.  Off by default.
         self.overlap_transpose = False
         self._tstream = None
+        # HIP path: at the end of the backward, run the embedding backward and the deferred
+        # column-sum flush on a side stream while the all-layer weight-gradient launch runs
+        # (RunCtx.tail_stream; FD_OVERLAP_TAIL=0: serial).  The dW grid's last round leaves
+        # ~half the CUs idle; the small, latency-bound tail kernels fill them.
+        self.overlap_tail = os.environ.get("FD_OVERLAP_TAIL", "0") != "0"
+        self._tail = None
         # optimizer that applies Adam inside the weight-gradient GEMM epilogues; set only for
         # the duration of a training step (engine/train.py fused_adam_scope)
         self.fused_opt = None
@@ -308,6 +314,7 @@ class DDoSClassifier(nn.Module):
         self._hip_cache = None
         self._wgrad = None
         self._tstream = None
+        self._tail = None
         self._synced_version = -1
         return self
 
@@ -487,6 +494,10 @@ class DDoSClassifier(nn.Module):
             rc.dw_jobs = []
         if grad and self.batch_dw and self.layer_grads_hook is None and not self.wgrad_stream:
             rc.dw_batch = []
+            if self.overlap_tail and ids.is_cuda:
+                if self._tail is None:
+                    self._tail = torch.cuda.Stream(device=self.arena.device)
+                rc.tail_stream = self._tail
         rc.fuse_colsum = self.fuse_colsum
         rc.remat_gelu = self.remat_gelu
         rc.fuse_ln = self.fuse_ln and cfg.dim % 64 == 0 and cfg.dim <= 2048

@@ -77,6 +77,9 @@ class RunCtx:
     # last backward node launches every weight gradient of the step as ONE grid
     # (ops/kernels.py linear_dw_batch; with ``fused_adam`` the Adam step runs in its epilogue)
     dw_batch: Optional[list] = None
+    # with dw_batch: side stream for the embedding backward + column-sum flush, concurrent with
+    # the all-layer weight-gradient launch (joined before the embedding node returns)
+    tail_stream: Optional["torch.cuda.Stream"] = None
 
 
 class _WGrad:
@@ -125,6 +128,36 @@ class EmbeddingFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        rc = ctx.rc
+        tail = rc.tail_stream if rc.dw_batch and rc.wgrad is None else None
+        if tail is None:
+            EmbeddingFn._tail(ctx, dy)
+            EmbeddingFn._weights(rc)
+            return (None,) * 8
+        # The all-layer weight gradients (one big grid) go first on the main stream; the
+        # embedding backward and the column-sum flush -- independent of them -- run on the side
+        # stream and take the CUs the dW grid's partial last round leaves idle.  Every tensor
+        # the side stream touches stays referenced until the join below.
+        cur = torch.cuda.current_stream()
+        tail.wait_stream(cur)
+        EmbeddingFn._weights(rc)
+        with torch.cuda.stream(tail):
+            EmbeddingFn._tail(ctx, dy)
+        cur.wait_stream(tail)
+        return (None,) * 8
+
+    @staticmethod
+    def _weights(rc):
+        if rc.dw_jobs:
+            K.dw_flush(rc.dw_jobs)
+        if rc.dw_batch:
+            fa = rc.fused_adam
+            acc_any = any(j[3] for j in rc.dw_batch)
+            K.linear_dw_batch(rc.dw_batch, adam=fa.fused_args if fa is not None and not acc_any else None)
+            rc.dw_batch.clear()
+
+    @staticmethod
+    def _tail(ctx, dy):
         ids, word, pos, gamma, mean, rstd = ctx.tensors
         s = ctx.sinks
         srt, perm = K.group_ids(ids)
@@ -147,14 +180,6 @@ class EmbeddingFn(torch.autograd.Function):
             torch.cuda.current_stream().wait_stream(ctx.rc.wgrad)
         if ctx.rc.colsum_jobs:
             K.colsum_flush(ctx.rc.colsum_jobs)
-        if ctx.rc.dw_jobs:
-            K.dw_flush(ctx.rc.dw_jobs)
-        if ctx.rc.dw_batch:
-            fa = ctx.rc.fused_adam
-            acc_any = any(j[3] for j in ctx.rc.dw_batch)
-            K.linear_dw_batch(ctx.rc.dw_batch, adam=fa.fused_args if fa is not None and not acc_any else None)
-            ctx.rc.dw_batch.clear()
-        return (None,) * 8
 
 
 class LayerFn(torch.autograd.Function):

@@ -119,3 +119,29 @@ def test_fused_adam_in_batched_dw_matches_unfused(graph):
     assert torch.equal(a.shadow, b.shadow)
     if graph:
         assert all(st.graph is not None and st.failed is None for st in steps)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_tail_overlap_bitwise(graph):
+    """Embedding backward + column-sum flush on a side stream concurrent with the all-layer dW
+    launch (model.overlap_tail): bitwise the serial order, eager and graph-replayed."""
+    cfg = DistilBertConfig(n_layers=2)
+    models, opts, steps = [], [], []
+    for overlap in (True, False):
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=23)
+        m.overlap_tail = overlap
+        m.train()
+        opt = ArenaAdam(m, lr=1e-3)
+        models.append(m)
+        opts.append(opt)
+        steps.append(GraphedTrainStep(make_step_fn(m, opt), warmup=1, enabled=graph, bucket=m.packed_rows))
+    for it in range(5):
+        ids, mask, labels, tokens = _batch(16, 128, seed=600 + it)
+        for st in steps:
+            st(ids, mask, labels, tokens)
+    torch.cuda.synchronize()
+    a, b = models[0].arena, models[1].arena
+    assert torch.equal(a.master, b.master) and torch.equal(a.shadow, b.shadow)
+    assert torch.equal(opts[0].m, opts[1].m) and torch.equal(opts[0].v, opts[1].v)
+    if graph:
+        assert all(st.graph is not None and st.failed is None for st in steps)
