@@ -78,6 +78,8 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                int accumulate, unsigned char* now, unsigned char* ever, const int* row_map, const int* cu, hipStream_t st);
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
             int* cu, long long* ids_packed, hipStream_t st);
+int fd_colsum_bf16_batched(int n, const void* const* xs, const int* T, const int* N, float* const* parts,
+                           hipStream_t st);
 int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, int defer, int* nblk_out,
                    hipStream_t st);
 int fd_colsum_batched(int n, const float* const* parts, float* const* outs, const int* nblk, const int* stride,
@@ -779,6 +781,34 @@ int64_t colsum_bf16(const at::Tensor& x, const at::Tensor& out, const at::Tensor
   return nblk;
 }
 
+// Partials of many bf16 column sums in one launch: parts[i] ([ceil(T_i / 32)][N_i] fp32) of xs[i]
+// ([T_i][N_i] bf16), bitwise colsum_bf16(defer=True) of each.  Returns the partial row counts.
+std::vector<int64_t> colsum_bf16_batched(const std::vector<at::Tensor>& xs, const std::vector<at::Tensor>& parts,
+                                         const std::vector<int64_t>& N) {
+  const size_t n = xs.size();
+  TORCH_CHECK(parts.size() == n && N.size() == n, "colsum_bf16_batched: ragged job lists");
+  std::vector<const void*> xp(n);
+  std::vector<float*> pp(n);
+  std::vector<int> tt(n), nn(n);
+  std::vector<int64_t> nblk(n);
+  for (size_t i = 0; i < n; ++i) {
+    need(xs[i], at::kBFloat16, "colsum x");
+    need(parts[i], at::kFloat, "colsum part");
+    TORCH_CHECK(N[i] > 0 && N[i] % 4 == 0 && xs[i].numel() % N[i] == 0, "colsum_bf16_batched: x is not [T][N]");
+    const int64_t T = xs[i].numel() / N[i];
+    TORCH_CHECK(T > 0 && parts[i].numel() >= ((T + 31) / 32) * N[i], "colsum_bf16_batched: partial buffer too small");
+    TORCH_CHECK(xs[i].device() == xs[0].device() && parts[i].device() == xs[0].device(), "colsum_bf16_batched: devices");
+    xp[i] = xs[i].data_ptr();
+    pp[i] = parts[i].data_ptr<float>();
+    tt[i] = (int)T;
+    nn[i] = (int)N[i];
+    nblk[i] = (T + 31) / 32;
+  }
+  if (n) check_rc(fd_colsum_bf16_batched((int)n, xp.data(), tt.data(), nn.data(), pp.data(), stream()),
+                  "colsum_bf16_batched");
+  return nblk;
+}
+
 // One launch finalising many deferred column sums: job i reduces parts[i] ([nblk][stride] fp32)
 // into outs[i][k] (k < 3, fp32 [D] or None) = sum over blocks of columns k*D .. k*D+D-1.
 void colsum_batched(const std::vector<at::Tensor>& parts, const std::vector<std::vector<c10::optional<at::Tensor>>>& outs,
@@ -1025,6 +1055,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("emb_fwd", &emb_fwd);
   m.def("emb_bwd", &emb_bwd);
   m.def("colsum_bf16", &colsum_bf16);
+  m.def("colsum_bf16_batched", &colsum_bf16_batched);
   m.def("colsum_batched", &colsum_batched);
   m.def("rank_sort", &rank_sort);
   m.def("head_fwd", &head_fwd, py::arg("hidden"), py::arg("B"), py::arg("S"), py::arg("W"), py::arg("bias"),

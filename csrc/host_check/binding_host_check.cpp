@@ -282,6 +282,15 @@ int fd_colsum_bf16(const void*, int, int, float*, float*, int, int, int* nblk_ou
   if (nblk_out) *nblk_out = 1;
   return 0;
 }
+int fd_colsum_bf16_batched(int n, const void* const* xs, const int* T, const int* N, float* const* parts,
+                           hipStream_t) {
+  ++hc::calls;
+  for (int i = 0; i < n; ++i) {
+    hc::span(xs[i], (long long)T[i] * N[i] * 2, "colsum_bf16_batched x");
+    hc::span(parts[i], (long long)((T[i] + 31) / 32) * N[i] * 4, "colsum_bf16_batched part");
+  }
+  return 0;
+}
 int fd_colsum_batched(int, const float* const*, float* const*, const int*, const int*, const int*, const int*,
                       const int*, hipStream_t) { ++hc::calls; return 0; }
 int fd_rank_sort(const void*, int, int, long long*, long long*, hipStream_t) { ++hc::calls; return 0; }
@@ -441,6 +450,12 @@ int main() {
     expect_reject("gemm non-contiguous", [&] { gemm(0, 1, xt, w, y, b, none, none, none, false, none); });
     auto cs_small = T_({3072}, f32);
     expect_reject("gemm colsum size", [&] { gemm_colsum(3, dy, w2t, du, u, none, cs_small, gout); });
+    // batched bf16 column-sum partials (per-layer qkv-bias partials at the end of the backward)
+    auto p1 = T_({84 * 2304}, f32), p2 = T_({84 * 3072}, f32), p_small = T_({83 * 2304}, f32);
+    expect_ok("colsum_bf16_batched", [&] { colsum_bf16_batched({dq, du}, {p1, p2}, {2304, 3072}); });
+    expect_reject("colsum_bf16_batched part size", [&] { colsum_bf16_batched({dq}, {p_small}, {2304}); });
+    expect_reject("colsum_bf16_batched N", [&] { colsum_bf16_batched({dq}, {p1}, {2303}); });
+    expect_reject("colsum_bf16_batched dtype", [&] { colsum_bf16_batched({p1}, {p1}, {2304}); });
   }
   // ---- all-layer weight gradients (with and without the fused Adam epilogue)
   {

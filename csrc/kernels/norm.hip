@@ -642,6 +642,43 @@ __global__ __launch_bounds__(256) void colsum_bf16_partial_kernel(const bf16_t* 
   *reinterpret_cast<float4*>(part + (size_t)blockIdx.x * N + c4) = make_float4(s0, s1, s2, s3);
 }
 
+// Many bf16 column-sum partial jobs in one launch (the per-layer qkv-bias partials of a whole
+// backward, computed at its end from the dqkv tensors the all-layer dW launch keeps alive anyway):
+// block b belongs to job j with start[j] <= b < start[j + 1]; within a job the blocks walk
+// (row block, column chunk) exactly as colsum_bf16_partial_kernel's grid, with the same per-block
+// arithmetic, so the partials -- and the finalised sums -- are bitwise the per-layer launches'.
+constexpr int CSB_MAXJ = 16;
+struct ColsumBf16Batch {
+  const bf16_t* x[CSB_MAXJ];
+  float* part[CSB_MAXJ];
+  int T[CSB_MAXJ], N[CSB_MAXJ], start[CSB_MAXJ + 1];
+  int n, rows;
+};
+__global__ __launch_bounds__(256) void colsum_bf16_partial_batched_kernel(ColsumBf16Batch cb) {
+  int j = 0;
+  while (j + 1 < cb.n && (int)blockIdx.x >= cb.start[j + 1]) ++j;  // block-uniform
+  const int local = blockIdx.x - cb.start[j];
+  const int N = cb.N[j], T = cb.T[j];
+  const int nchunk = (N / 4 + 255) / 256;
+  const int bx = local / nchunk, by = local % nchunk;
+  const int c4 = (by * 256 + threadIdx.x) * 4;
+  if (c4 >= N) return;
+  const bf16_t* x = cb.x[j];
+  const int r0 = bx * cb.rows, r1 = min(T, r0 + cb.rows);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (int rb = r0; rb < r1; rb += 16) {
+    uint2 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      v[u] = rb + u < r1 ? *reinterpret_cast<const uint2*>(x + (size_t)(rb + u) * N + c4) : make_uint2(0, 0);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      s0 += lo_bf(v[u].x); s1 += hi_bf(v[u].x); s2 += lo_bf(v[u].y); s3 += hi_bf(v[u].y);
+    }
+  }
+  *reinterpret_cast<float4*>(cb.part[j] + (size_t)bx * N + c4) = make_float4(s0, s1, s2, s3);
+}
+
 // Deferred column-sum finalisation: every bias / LayerNorm-affine gradient of the
 // backward leaves its per-block partials in a slot of its own, and ONE launch at the
 // end of the backward reduces all of them (instead of one small launch per producer).
@@ -813,6 +850,30 @@ int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int acc
   if (!defer)
     hipLaunchKernelGGL(colsum_kernel<16>, dim3((N + 63) / 64, 1), dim3(256), 0, st, work, nblk, N, N, out,
                        (float*)nullptr, (float*)nullptr, accumulate);
+  return 0;
+}
+
+// n bf16 [T_i][N_i] matrices -> per-32-row-block partials part_i [ceil(T_i / 32)][N_i], one launch.
+int fd_colsum_bf16_batched(int n, const void* const* xs, const int* T, const int* N, float* const* parts,
+                           hipStream_t st) {
+  for (int base = 0; base < n; base += CSB_MAXJ) {
+    ColsumBf16Batch cb{};
+    cb.n = std::min(CSB_MAXJ, n - base);
+    cb.rows = 32;
+    int blocks = 0;
+    for (int i = 0; i < cb.n; ++i) {
+      const int g = base + i;
+      if (N[g] <= 0 || N[g] % 4 != 0 || T[g] <= 0) return 1;
+      cb.x[i] = (const bf16_t*)xs[g];
+      cb.part[i] = parts[g];
+      cb.T[i] = T[g];
+      cb.N[i] = N[g];
+      cb.start[i] = blocks;
+      blocks += ((T[g] + 31) / 32) * ((N[g] / 4 + 255) / 256);
+    }
+    cb.start[cb.n] = blocks;
+    hipLaunchKernelGGL(colsum_bf16_partial_batched_kernel, dim3(blocks), dim3(256), 0, st, cb);
+  }
   return 0;
 }
 

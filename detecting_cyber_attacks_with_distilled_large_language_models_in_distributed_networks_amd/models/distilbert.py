@@ -282,6 +282,9 @@ class DDoSClassifier(nn.Module):
         # (RunCtx.tail_stream; FD_OVERLAP_TAIL=0: serial).  The dW grid's last round leaves
         # ~half the CUs idle; the small, latency-bound tail kernels fill them.
         self.overlap_tail = os.environ.get("FD_OVERLAP_TAIL", "0") != "0"
+        # HIP path (with batch_dw): the per-block qkv-bias column-sum partials in one launch at the
+        # end of the backward (RunCtx.colsum_pending; FD_BATCH_COLSUM=0: one launch per block)
+        self.batch_colsum = os.environ.get("FD_BATCH_COLSUM", "1") != "0"
         self._tail = None
         # optimizer that applies Adam inside the weight-gradient GEMM epilogues; set only for
         # the duration of a training step (engine/train.py fused_adam_scope)
@@ -494,6 +497,8 @@ class DDoSClassifier(nn.Module):
             rc.dw_jobs = []
         if grad and self.batch_dw and self.layer_grads_hook is None and not self.wgrad_stream:
             rc.dw_batch = []
+            if rc.colsum_jobs is not None and self.batch_colsum:
+                rc.colsum_pending = []
             if self.overlap_tail and ids.is_cuda:
                 if self._tail is None:
                     self._tail = torch.cuda.Stream(device=self.arena.device)

@@ -80,6 +80,10 @@ class RunCtx:
     # with dw_batch: side stream for the embedding backward + column-sum flush, concurrent with
     # the all-layer weight-gradient launch (joined before the embedding node returns)
     tail_stream: Optional["torch.cuda.Stream"] = None
+    # with dw_batch + colsum_jobs: bf16 column sums whose source stays alive to the end of the
+    # backward anyway (each block's dqkv, kept for the dW launch) -- their partials are computed
+    # in ONE launch at the end (ops/kernels.py colsum_partials_batched) instead of one per block
+    colsum_pending: Optional[list] = None
 
 
 class _WGrad:
@@ -178,6 +182,8 @@ class EmbeddingFn(torch.autograd.Function):
             g[1:].zero_()
         if ctx.rc.wgrad is not None:  # join the weight-gradient stream: every grad is final after this node
             torch.cuda.current_stream().wait_stream(ctx.rc.wgrad)
+        if ctx.rc.colsum_pending:
+            K.colsum_partials_batched(ctx.rc.colsum_pending, ctx.rc.colsum_jobs)
         if ctx.rc.colsum_jobs:
             K.colsum_flush(ctx.rc.colsum_jobs)
 
@@ -291,7 +297,10 @@ class LayerFn(torch.autograd.Function):
                              adam=fa.fused_args([G["o_w"].buf, G["qkv_w"].buf]) if fa else None, jobs=rc.dw_jobs)
             else:
                 K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
-            K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
+            if batch is not None and jobs is not None and rc.colsum_pending is not None:
+                rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))  # partials at the end, batched
+            else:
+                K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
         prev = rc.ln2_saved.get(ctx.idx - 1) if fused and wt.get("qkv_w") is not None else None
         if prev is not None:
             # dx = dqkv Wqkv + dz1 is block idx-1's output-LN gradient: finish that LayerNorm

@@ -204,6 +204,25 @@ def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = False, jobs: O
     return out
 
 
+def colsum_partials_batched(pending: list, jobs: list):
+    """Partials of several deferred bf16 column sums -- pending = [(x, out, accumulate)] -- in ONE
+    launch, each appended to ``jobs`` exactly as ``colsum(x, out, accumulate, jobs)`` would
+    (bitwise the same partials; ``colsum_flush`` finalises them)."""
+    if not pending:
+        return
+    xs, parts, ns = [], [], []
+    for x, out, acc in pending:
+        N = out.numel()
+        T = x.numel() // N
+        ws = workspace(x.device, f"colsum_job{len(jobs)}", ((T + 31) // 32) * N)
+        jobs.append((ws, [out], (T + 31) // 32, N, N, acc))
+        xs.append(x)
+        parts.append(ws)
+        ns.append(N)
+    ext().colsum_bf16_batched(xs, parts, ns)
+    pending.clear()
+
+
 def colsum_flush(jobs: list):
     """Finalise every deferred column sum in one launch (bitwise = the immediate path)."""
     if jobs:

@@ -145,3 +145,42 @@ def test_tail_overlap_bitwise(graph):
     assert torch.equal(opts[0].m, opts[1].m) and torch.equal(opts[0].v, opts[1].v)
     if graph:
         assert all(st.graph is not None and st.failed is None for st in steps)
+
+
+def test_batched_qkv_bias_partials_bitwise():
+    """The per-block qkv-bias column-sum partials computed in one launch at the end of the
+    backward (model.batch_colsum, ops/kernels.py colsum_partials_batched) give bitwise the
+    gradients of one partial launch per block -- including an accumulating second backward."""
+    cfg = DistilBertConfig(n_layers=3)
+    grads = []
+    for batched in (True, False):
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=29)
+        m.batch_colsum = batched
+        m.train()
+        ids, mask, labels, tokens = _batch(32, 128, seed=700)
+        for acc_step in range(2):
+            if acc_step == 0:
+                m.zero_grad()
+            m.rng.fill_(acc_step)
+            loss, _ = m.forward_loss(ids, mask, labels, tokens=tokens)
+            loss.backward()
+        torch.cuda.synchronize()
+        grads.append(m.arena.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+
+
+def test_colsum_partials_batched_kernel():
+    g = torch.Generator(device="cuda").manual_seed(3)
+    xs = [torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16) for T, N in ((2688, 2304), (700, 768), (33, 3072))]
+    outs_a = [torch.zeros(x.shape[1], device="cuda") for x in xs]
+    outs_b = [torch.ones(x.shape[1], device="cuda") for x in xs]
+    jobs_a, jobs_b = [], []
+    for x, o in zip(xs, outs_a):
+        K.colsum(x, o, False, jobs_a)
+    K.colsum_flush(jobs_a)
+    K.colsum_partials_batched([(x, o, True) for x, o in zip(xs, outs_b)], jobs_b)
+    K.colsum_flush(jobs_b)
+    torch.cuda.synchronize()
+    for x, a, b in zip(xs, outs_a, outs_b):
+        assert torch.equal(a + 1.0, b)
+        assert ((a - x.float().sum(0)).abs().max() / x.float().sum(0).abs().max()).item() < 1e-5
