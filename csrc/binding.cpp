@@ -77,7 +77,7 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
                int accumulate, unsigned char* now, unsigned char* ever, const int* row_map, const int* cu, hipStream_t st);
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
-            int* cu, long long* ids_packed, hipStream_t st);
+            int* cu, long long* ids_packed, int* step, uint32_t* seed, hipStream_t st);
 int fd_colsum_bf16_batched(int n, const void* const* xs, const int* T, const int* N, float* const* parts,
                            hipStream_t st);
 int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, int defer, int* nblk_out,
@@ -456,8 +456,11 @@ void splitk_reduce_batched(const std::vector<at::Tensor>& slabs, const std::vect
 }
 
 // Unpadded-step layout in one launch: row_map [rows] int32, cu [B+1] int32, ids_packed [rows] int64.
+// step / seed (optional int32 [1]): counters advanced by the same launch (the step counter kernel folded in)
 void pack(const at::Tensor& mask, const at::Tensor& ids, const at::Tensor& row_map, const at::Tensor& cu,
-          const at::Tensor& ids_packed) {
+          const at::Tensor& ids_packed, const c10::optional<at::Tensor>& step, const c10::optional<at::Tensor>& seed) {
+  need_opt(step, at::kInt, "step");
+  need_opt(seed, at::kInt, "seed");
   TORCH_CHECK(on_device(mask) && mask.is_contiguous() && on_device(ids) && ids.is_contiguous(), "pack: GPU inputs");
   TORCH_CHECK(mask.dim() == 2 && ids.sizes() == mask.sizes(), "pack: mask and ids must both be [B, S]");
   need(row_map, at::kInt, "row_map");
@@ -467,7 +470,7 @@ void pack(const at::Tensor& mask, const at::Tensor& ids, const at::Tensor& row_m
   TORCH_CHECK(cu.numel() == B + 1 && ids_packed.numel() == row_map.numel() && row_map.numel() >= 1, "pack: sizes");
   check_rc(fd_pack(mask.data_ptr(), (int)mask.element_size(), ids.data_ptr(), (int)ids.element_size(), (int)B, (int)S,
                    (int)row_map.numel(), row_map.data_ptr<int>(), cu.data_ptr<int>(),
-                   reinterpret_cast<long long*>(ids_packed.data_ptr()), stream()),
+                   reinterpret_cast<long long*>(ids_packed.data_ptr()), ptr<int>(step), ptr<uint32_t>(seed), stream()),
            "pack");
 }
 
@@ -1038,7 +1041,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return (int64_t)fd_gemm_dw2_splits((int)M0, (int)N0, (int)M1, (int)N1, (int)K);
   });
   m.def("gemm_set_fixup", [](bool on) { fd_gemm_set_fixup(on ? 1 : 0); });
-  m.def("pack", &pack);
+  m.def("pack", &pack, py::arg("mask"), py::arg("ids"), py::arg("row_map"), py::arg("cu"), py::arg("ids_packed"),
+        py::arg("step") = py::none(), py::arg("seed") = py::none());
   m.def("transpose_batched", &transpose_batched);
   m.def("comm_load", &comm_load);
   m.def("comm_unique_id", &comm_unique_id);

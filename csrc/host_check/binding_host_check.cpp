@@ -268,8 +268,10 @@ int fd_emb_bwd(const void*, const void*, int, const long long*, const long long*
                int, int, int, const uint32_t*, uint32_t, uint32_t, float, int, unsigned char*, unsigned char*,
                const int*, const int*, hipStream_t) { ++hc::calls; return 0; }
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
-            int* cu, long long* ids_packed, hipStream_t) {
+            int* cu, long long* ids_packed, int* step, uint32_t* seed, hipStream_t) {
   ++hc::calls;
+  hc::opt_span(step, 4, "pack step");
+  hc::opt_span(seed, 4, "pack seed");
   hc::span(mask, (long long)B * S * mask_bytes, "pack mask");
   hc::span(ids, (long long)B * S * ids_bytes, "pack ids");
   hc::span(row_map, (long long)rows * 4, "pack row_map");
@@ -607,9 +609,13 @@ int main() {
   {
     auto mask = T_({32, 128}, i64), ids = T_({32, 128}, i64), rm = T_({2688}, i32), cu = T_({33}, i32);
     auto ip = T_({2688}, i64);
-    expect_ok("pack", [&] { pack(mask, ids, rm, cu, ip); });
+    expect_ok("pack", [&] { pack(mask, ids, rm, cu, ip, none, none); });
+    auto st1 = T_({1}, i32);
+    expect_ok("pack + counters", [&] { pack(mask, ids, rm, cu, ip, st1, st1); });
+    auto stf = T_({1}, f32);
+    expect_reject("pack counter dtype", [&] { pack(mask, ids, rm, cu, ip, stf, none); });
     auto cu_bad = T_({32}, i32);
-    expect_reject("pack cu", [&] { pack(mask, ids, rm, cu_bad, ip); });
+    expect_reject("pack cu", [&] { pack(mask, ids, rm, cu_bad, ip, none, none); });
   }
   if (failures) {
     std::printf("binding host check: %d failure(s)\n", failures);

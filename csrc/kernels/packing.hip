@@ -15,7 +15,8 @@ namespace {
 
 template <typename M, typename I>
 __global__ __launch_bounds__(1024) void pack_kernel(const M* mask, const I* ids, int n, int S, int B, int rows,
-                                                    int* row_map, int* cu, long long* ids_packed) {
+                                                    int* row_map, int* cu, long long* ids_packed, int* step,
+                                                    uint32_t* seed) {
   __shared__ int wsum[16];
   __shared__ int carry_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -59,7 +60,13 @@ __global__ __launch_bounds__(1024) void pack_kernel(const M* mask, const I* ids,
     __syncthreads();
   }
   const int total = carry_s;
-  if (tid == 0) cu[B] = total;
+  if (tid == 0) {
+    cu[B] = total;
+    // the training step's counters (Adam step, dropout seed) ride on this launch instead of a
+    // kernel of their own; nothing in this kernel reads them
+    if (step) step[0] += 1;
+    if (seed) seed[0] += 1;
+  }
   const long long id0 = (long long)ids[0];
   for (int r = total + tid; r < rows; r += 1024) {
     row_map[r] = -1;
@@ -73,12 +80,12 @@ extern "C" {
 
 // mask_bytes / ids_bytes: 8 (int64) or 4 (int32) / 1 (uint8 mask).  n = B * S <= 1 << 20.
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
-            int* cu, long long* ids_packed, hipStream_t st) {
+            int* cu, long long* ids_packed, int* step, uint32_t* seed, hipStream_t st) {
   const int n = B * S;
   if (B <= 0 || S <= 0 || rows <= 0 || n > (1 << 20)) return 1;
 #define FD_PACK(MT, IT)                                                                                        \
   hipLaunchKernelGGL((pack_kernel<MT, IT>), dim3(1), dim3(1024), 0, st, (const MT*)mask, (const IT*)ids, n, S, B, \
-                     rows, row_map, cu, ids_packed)
+                     rows, row_map, cu, ids_packed, step, seed)
   if (mask_bytes == 8 && ids_bytes == 8) FD_PACK(long long, long long);
   else if (mask_bytes == 8 && ids_bytes == 4) FD_PACK(long long, int);
   else if (mask_bytes == 4 && ids_bytes == 8) FD_PACK(int, long long);

@@ -83,17 +83,25 @@ class ArenaAdam:
                 raise RuntimeError("ArenaAdam(overlap=True) cannot share the backward hook (data-parallel GradSync?)")
             self.model.layer_grads_hook = self._on_layer_grads
 
-    def _begin(self, seed: Optional[torch.Tensor] = None):
+    def _begin(self, seed: Optional[torch.Tensor] = None, defer: Optional[list] = None):
         """Advance the device step counter once per step, before the first update launch.
         ``seed``: the model's dropout counter, advanced by the same launch (the model's training
-        forward calls this inside a step scope: one tiny kernel instead of two)."""
+        forward calls this inside a step scope: one tiny kernel instead of two).  ``defer``: append
+        the (step, seed) counters to advance there instead of launching -- the caller folds them
+        into a launch it makes anyway before anything reads them (the packing kernel)."""
         from ..ops import kernels as K
         if not self._begun:
-            K.step_inc(self.step_t, seed)
+            if defer is not None:
+                defer.append((self.step_t, seed))
+            else:
+                K.step_inc(self.step_t, seed)
             self.host_step += 1
             self._begun = True
         elif seed is not None:
-            K.step_inc(None, seed)
+            if defer is not None:
+                defer.append((None, seed))
+            else:
+                K.step_inc(None, seed)
 
     def _update(self, off: int, n: int, sparse: bool):
         from ..ops import kernels as K

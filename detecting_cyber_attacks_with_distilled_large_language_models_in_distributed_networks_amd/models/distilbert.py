@@ -285,6 +285,9 @@ class DDoSClassifier(nn.Module):
         # HIP path (with batch_dw): the per-block qkv-bias column-sum partials in one launch at the
         # end of the backward (RunCtx.colsum_pending; FD_BATCH_COLSUM=0: one launch per block)
         self.batch_colsum = os.environ.get("FD_BATCH_COLSUM", "1") != "0"
+        # HIP path (packed step): the Adam step / dropout seed counters are advanced by the packing
+        # launch instead of a kernel of their own (FD_FOLD_STEP=0: separate launch)
+        self.fold_step_counters = os.environ.get("FD_FOLD_STEP", "1") != "0"
         self._tail = None
         # optimizer that applies Adam inside the weight-gradient GEMM epilogues; set only for
         # the duration of a training step (engine/train.py fused_adam_scope)
@@ -509,9 +512,13 @@ class DDoSClassifier(nn.Module):
         if (grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None
                 and not self.wgrad_stream and self.transposed_dx):
             rc.fused_adam = self.fused_opt
+        # packed step: the counters ride on the packing launch (no kernel of their own)
+        incs = [] if packed and self.fold_step_counters else None
         if self.training:
             if grad and self.step_opt is not None:
-                self.step_opt._begin(seed=self.rng)  # Adam step + dropout seed: one launch
+                self.step_opt._begin(seed=self.rng, defer=incs)  # Adam step + dropout seed: one launch
+            elif incs is not None:
+                incs.append((None, self.rng))
             else:
                 K.step_inc(None, self.rng)
         token = self._grad_token if torch.is_grad_enabled() else None
@@ -536,7 +543,12 @@ class DDoSClassifier(nn.Module):
             # row cu[b] for sequence b's [CLS].  Filler rows act as padded row 0: finite, and
             # their gradient is exactly 0 (they reach neither a real token nor the loss).
             # The layout (row map, sequence starts, packed ids) is one kernel (ops/packing).
-            rc.row_map, rc.cu, ids = K.pack(mask, ids, self.packed_rows(tokens, B, S))
+            incs = incs or []
+            st_inc = next((a for a, _ in incs if a is not None), None)
+            sd_inc = next((b for _, b in incs if b is not None), None)
+            if len([a for a, _ in incs if a is not None]) > 1 or len([b for _, b in incs if b is not None]) > 1:
+                raise RuntimeError("a counter deferred twice in one forward")
+            rc.row_map, rc.cu, ids = K.pack(mask, ids, self.packed_rows(tokens, B, S), step=st_inc, seed=sd_inc)
         x = EmbeddingFn.apply(token, ids, emb["word"], emb["pos"], emb["ln_w"], emb["ln_b"], emb["sinks"], rc)
         for i, L in enumerate(layers):
             x = LayerFn.apply(x, L, rc, i)
