@@ -304,7 +304,7 @@ int64_t gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C
 }
 
 // Every weight gradient of a backward in one launch (gemm.hip gemm_dw_batch_kernel):
-// Cs[i] (+)= As[i]^T Bs[i] (fp32), As[i] [K][M_i], Bs[i] [K][N_i] bf16 (one K for all).
+// Cs[i] (+)= As[i]^T Bs[i] (fp32), As[i] [K_i][M_i], Bs[i] [K_i][N_i] bf16 (K_i % 64 == 0).
 // adam: empty, or [p, m, v, shadow] per problem + the device step counter last (fused
 // optimizer step instead of storing the gradients; hp = [lr, b1, b2, eps, wd, decoupled]).
 void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tensor>& Bs,
@@ -314,7 +314,6 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
   TORCH_CHECK(n > 0 && n <= 32, "gemm_dw_batch: 1..32 problems, got ", n);
   TORCH_CHECK(Bs.size() == n && Cs.size() == n && accumulate.size() == n, "gemm_dw_batch: ragged problem lists");
   const int64_t K = As[0].size(0);
-  TORCH_CHECK(K > 0 && K % 64 == 0, "gemm_dw_batch: K (tokens) must be a positive multiple of 64, got ", K);
   std::vector<const at::Tensor*> cs(n);
   std::vector<FdDwProb> pr(n);
   for (size_t i = 0; i < n; ++i) {
@@ -322,7 +321,9 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
     need(Bs[i], at::kBFloat16, "B");
     need(Cs[i], at::kFloat, "C");
     TORCH_CHECK(As[i].dim() == 2 && Bs[i].dim() == 2 && Cs[i].dim() == 2, "gemm_dw_batch operands must be 2-D");
-    TORCH_CHECK(As[i].size(0) == K && Bs[i].size(0) == K, "gemm_dw_batch: every operand needs K = ", K, " rows");
+    const int64_t Ki = As[i].size(0);
+    TORCH_CHECK(Ki > 0 && Ki % 64 == 0, "gemm_dw_batch: K (rows) must be a positive multiple of 64, got ", Ki);
+    TORCH_CHECK(Bs[i].size(0) == Ki, "gemm_dw_batch: A and B of a problem need the same rows (", Ki, ")");
     TORCH_CHECK(Cs[i].size(0) == As[i].size(1) && Cs[i].size(1) == Bs[i].size(1), "gemm_dw_batch: C shape mismatch");
     TORCH_CHECK(As[i].size(1) % 128 == 0 && Bs[i].size(1) % 64 == 0, "gemm_dw_batch: M % 128 and N % 64 required");
     cs[i] = &Cs[i];
@@ -333,6 +334,7 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
     q.C = Cs[i].data_ptr<float>();
     q.M = (int)As[i].size(1);
     q.N = (int)Bs[i].size(1);
+    q.K = (int)Ki;
     q.accumulate = accumulate[i] ? 1 : 0;
   }
   std::vector<FdAdamEpi> ad(n);

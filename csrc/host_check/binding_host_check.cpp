@@ -104,8 +104,10 @@ int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const
   for (int i = 0; i < n; ++i) {
     const FdDwProb& q = probs[i];
     const long long mn = (long long)q.M * q.N;
-    hc::span(q.A, (long long)K * q.M * 2, "dw_batch A");
-    hc::span(q.B, (long long)K * q.N * 2, "dw_batch B");
+    const long long Kq = q.K > 0 ? q.K : K;
+    if (Kq % 64) hc::violations.push_back("dw_batch: K % 64");
+    hc::span(q.A, Kq * q.M * 2, "dw_batch A");
+    hc::span(q.B, Kq * q.N * 2, "dw_batch B");
     if (q.p) {
       hc::span(q.p, mn * 4, "dw_batch adam p");
       hc::span(q.m, mn * 4, "dw_batch adam m");
@@ -481,6 +483,16 @@ int main() {
     auto Bbad = Bs;
     Bbad[2] = T_({2000, 768}, bf);
     expect_reject("dw_batch K mismatch", [&] { gemm_dw_batch(As, Bbad, Cs, acc, {}, {}, -1); });
+    // per-problem rows (the pruned last block: padded [CLS] rows)
+    auto Amix = As, Bmix = Bs;
+    Amix[1] = T_({64, As[1].size(1)}, bf);
+    Bmix[1] = T_({64, Bs[1].size(1)}, bf);
+    expect_ok("dw_batch mixed K", [&] { gemm_dw_batch(Amix, Bmix, Cs, acc, st, hp, -1); });
+    auto Bodd = Bmix;
+    Bodd[1] = T_({96, Bs[1].size(1)}, bf);
+    auto Aodd = Amix;
+    Aodd[1] = T_({96, As[1].size(1)}, bf);
+    expect_reject("dw_batch K % 64", [&] { gemm_dw_batch(Aodd, Bodd, Cs, acc, {}, {}, -1); });
     auto Cbad = Cs;
     Cbad[1] = T_({768, 3072}, f32);
     expect_reject("dw_batch C shape", [&] { gemm_dw_batch(As, Bs, Cbad, acc, {}, {}, -1); });

@@ -18,8 +18,9 @@ struct FdAdamEpi {
 };
 
 // One weight-gradient problem of the all-layer launch (gemm.hip gemm_dw_batch_kernel):
-// C[M][N] (+)= A^T B with A [K][M], B [K][N] bf16 (same K for every problem).  p != nullptr:
-// apply Adam to the finished gradient tile (state laid out like C) instead of storing it.
+// C[M][N] (+)= A^T B with A [K][M], B [K][N] bf16 (K: this problem's rows, a multiple of 64 --
+// the pruned last block's problems run on the padded [CLS] rows only).  p != nullptr: apply Adam
+// to the finished gradient tile (state laid out like C) instead of storing it.
 struct FdDwProb {
   const uint16_t* A;
   const uint16_t* B;
@@ -31,6 +32,7 @@ struct FdDwProb {
   int M, N;
   int tile0;          // filled by the launcher
   int accumulate;
+  int K;              // rows of A and B (0: the launch's K)
 };
 
 // LayerNorm fused into an N = hidden GEMM (gemm.hip gemm_ln_kernel).  The column tiles of one

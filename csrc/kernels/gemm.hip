@@ -1101,9 +1101,10 @@ DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
   const DwProb& q = bt.pr[i];
   GemmParams p{};
   p.A = q.A; p.B = q.B; p.C = q.C;
-  p.M = q.M; p.N = q.N; p.K = bt.K;
+  const int K = q.K > 0 ? q.K : bt.K;
+  p.M = q.M; p.N = q.N; p.K = K;
   p.lda = q.M; p.ldb = q.N; p.ldc = q.N;
-  p.k_split = bt.K;
+  p.k_split = K;
   p.group_m = bt.group_m;
   p.diag = bt.diag;
   p.out = q.C;
@@ -1685,6 +1686,7 @@ int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const f
   for (int i = 0; i < n; ++i) {
     bt.pr[i] = probs[i];
     if (!probs[i].A || !probs[i].B || (!probs[i].C && !probs[i].p) || probs[i].M <= 0 || probs[i].N <= 0) return 2;
+    if (probs[i].K < 0 || probs[i].K % BKT) return 5;
     if (probs[i].p && (!probs[i].m || !probs[i].v || !step || !hyper)) return 3;
   }
   if (hyper) {

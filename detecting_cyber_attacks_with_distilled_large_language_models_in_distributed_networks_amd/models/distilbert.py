@@ -288,6 +288,9 @@ class DDoSClassifier(nn.Module):
         # HIP path (packed step): the Adam step / dropout seed counters are advanced by the packing
         # launch instead of a kernel of their own (FD_FOLD_STEP=0: separate launch)
         self.fold_step_counters = os.environ.get("FD_FOLD_STEP", "1") != "0"
+        # HIP path: the last block runs its out-proj / FFN / LayerNorms on the [CLS] rows only
+        # (exact: no other row of its output reaches the loss; FD_PRUNE_LAST=0: every row)
+        self.prune_last = os.environ.get("FD_PRUNE_LAST", "1") != "0"
         self._tail = None
         # optimizer that applies Adam inside the weight-gradient GEMM epilogues; set only for
         # the duration of a training step (engine/train.py fused_adam_scope)
@@ -550,6 +553,7 @@ class DDoSClassifier(nn.Module):
                 raise RuntimeError("a counter deferred twice in one forward")
             rc.row_map, rc.cu, ids = K.pack(mask, ids, self.packed_rows(tokens, B, S), step=st_inc, seed=sd_inc)
         x = EmbeddingFn.apply(token, ids, emb["word"], emb["pos"], emb["ln_w"], emb["ln_b"], emb["sinks"], rc)
+        self._setup_prune(rc, layers, grad, packed)
         for i, L in enumerate(layers):
             x = LayerFn.apply(x, L, rc, i)
         if labels is not None:
@@ -557,6 +561,36 @@ class DDoSClassifier(nn.Module):
             return loss, logits
         logits, _ = HeadFn.apply(x, head["w"], head["b"], head["sinks"], rc, None)
         return None, logits
+
+    def _setup_prune(self, rc, layers, grad: bool, packed: bool):
+        """Last-block [CLS] pruning (RunCtx.prune_idx; ops/functional.py LayerFn._forward_pruned):
+        exact -- the dropped rows reach neither the loss nor any gradient.  Needs the fused
+        LayerNorm path and, for a training step, the all-layer dW launch (the pruned block's
+        out-proj / FFN weight gradients join it with K = Bp rows) and the W^T copies."""
+        from ..ops import kernels as K
+        B, S, D = rc.B, rc.S, self.config.dim
+        Bp = (B + 63) // 64 * 64
+        if not (self.prune_last and rc.fuse_ln and layers and K.ln_fusable(Bp, D) and Bp <= rc.B * rc.S):
+            return
+        if grad and (rc.dw_batch is None or rc.wgrad is not None or rc.colsum_jobs is None or "wT" not in layers[-1]):
+            return
+        dev = self.arena.device
+        key = (B, S, Bp, str(dev))
+        cache = getattr(self, "_prune_cache", None)
+        if cache is None or cache[0] != key:
+            rmap = torch.zeros(Bp, dtype=torch.int32, device=dev)
+            rmap[:B] = torch.arange(B, dtype=torch.int32, device=dev) * S
+            padded_rows = rmap.to(torch.int64)  # padded layout: sequence b's [CLS] is row b * S
+            cache = (key, rmap, padded_rows, torch.arange(B, dtype=torch.int32, device=dev),
+                     torch.zeros(Bp, dtype=torch.int64, device=dev))
+            self._prune_cache = cache
+        _, rmap, padded_rows, head_rows, packed_rows = cache
+        if packed:
+            packed_rows[:B].copy_(rc.cu[:-1])  # row cu[b]; filler rows -> row 0 (a finite row)
+            rc.cls_rows = packed_rows
+        else:
+            rc.cls_rows = padded_rows
+        rc.cls_rmap, rc.head_rows, rc.prune_idx = rmap, head_rows, len(layers) - 1
 
     def _no_bias(self) -> torch.Tensor:
         """Placeholder key-bias tensor for the varlen path (the kernels do not read it)."""

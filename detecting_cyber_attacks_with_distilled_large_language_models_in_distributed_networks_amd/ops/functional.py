@@ -84,6 +84,19 @@ class RunCtx:
     # backward anyway (each block's dqkv, kept for the dW launch) -- their partials are computed
     # in ONE launch at the end (ops/kernels.py colsum_partials_batched) instead of one per block
     colsum_pending: Optional[list] = None
+    # Last-block [CLS] pruning: the loss reads only each sequence's [CLS] row of the last block's
+    # output, and every row of a block's FFN / out-proj / LayerNorms is computed independently of
+    # the others, so in the LAST block only the [CLS] rows of everything after the attention can
+    # reach the loss or any gradient (keys and values still need every row, so QKV and attention
+    # run on all rows).  prune_idx = index of the pruned block (-1: off); cls_rows = int64 [Bp]
+    # rows of the full layout to keep (the B [CLS] rows, then filler rows up to a multiple of 64 so
+    # the pruned weight-gradient problems keep K % 64 == 0; their upstream gradient is 0);
+    # cls_rmap = int32 [Bp] padded-row index of each kept row (dropout hash, same masks as the
+    # unpruned path); head_rows = int32 [B] = arange(B) (the head reads the pruned output).
+    prune_idx: int = -1
+    cls_rows: Optional[torch.Tensor] = None
+    cls_rmap: Optional[torch.Tensor] = None
+    head_rows: Optional[torch.Tensor] = None
 
 
 class _WGrad:
@@ -194,6 +207,9 @@ class LayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, L, rc: RunCtx, idx: int):
         ctx.idx = idx
+        ctx.pruned = idx == rc.prune_idx
+        if ctx.pruned:
+            return LayerFn._forward_pruned(ctx, x, L, rc, idx)
         p_a = rc.p_attn if rc.training else 0.0
         p_h = rc.p_hidden if rc.training else 0.0
         attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
@@ -227,7 +243,89 @@ class LayerFn(torch.autograd.Function):
         return y
 
     @staticmethod
+    def _forward_pruned(ctx, x, L, rc: RunCtx, idx: int):
+        """The last block on its [CLS] rows only (RunCtx.prune_idx): QKV + attention on every row
+        (keys / values), then out-proj + LN, FFN, LN on the gathered [CLS] rows.  Returns [Bp, D]."""
+        p_a = rc.p_attn if rc.training else 0.0
+        p_h = rc.p_hidden if rc.training else 0.0
+        attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
+        grad = ctx.needs_input_grad[0]
+        qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
+        dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
+        cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask)
+        ci, rm = rc.cls_rows, rc.cls_rmap
+        cxc, xc = cx.index_select(0, ci), x.index_select(0, ci)
+        h, ao, m1, r1 = K.linear_ln_fwd(cxc, L["o_w"], L["o_b"], xc, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0,
+                                        keep_z=grad)
+        g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
+        y, f, m2, r2 = K.linear_ln_fwd(g, L["l2_w"], L["l2_b"], h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed,
+                                       ffn_site, p_h, rm, keep_z=grad)
+        if grad:
+            ctx.save_for_backward(x)
+            ctx.acts = (qkv, cx, lse, cxc, ao, h, m1, r1, u, None if rc.remat_gelu else g, f, m2, r2)
+            ctx.dmask = dmask
+        ctx.L, ctx.rc, ctx.sites, ctx.p = L, rc, (attn_site, ffn_site), (p_a, p_h)
+        return y
+
+    @staticmethod
+    def _backward_pruned(ctx, dy):
+        """Backward of _forward_pruned: LayerNorm / FFN / out-proj on the Bp kept rows (their
+        weight gradients join the all-layer dW launch with K = Bp), the attention backward and the
+        QKV dX on every row with the [CLS] gradients scattered back (other rows' are exactly 0)."""
+        (x,) = ctx.saved_tensors
+        qkv, cx, lse, cxc, ao, h, m1, r1, u, g, f, m2, r2 = ctx.acts
+        L, rc = ctx.L, ctx.rc
+        G = L["sinks"]
+        attn_site, ffn_site = ctx.sites
+        p_a, p_h = ctx.p
+        acc = G["l2_w"].accumulate()
+        jobs = rc.colsum_jobs
+        batch = rc.dw_batch
+        wt = L["wT"]
+        ci, rm, B = rc.cls_rows, rc.cls_rmap, rc.B
+        dz2, df = K.ln_bwd(dy, f, None, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, rc.seed,
+                           ffn_site, p_h, acc, rm, jobs, zin=True)
+        g_out = torch.empty_like(u) if g is None else None
+        du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt["l2_w"], colsum=(jobs, G["l1_b"].buf, acc), aux_out=g_out)
+        if g is None:
+            g = g_out
+        batch += [(df, g, G["l2_w"].buf, acc), (du, h, G["l1_w"].buf, acc)]
+        dz1c, _ = K.linear_dx_ln_bwd(du, wt["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
+                                     G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs)
+        dcxc = K.linear_dx(dz1c, L["o_w"], wt=wt["o_w"])
+        # the [CLS] rows' gradients back into the full layout (filler rows carry exact zeros)
+        dcx = torch.zeros_like(cx)
+        dcx.index_copy_(0, ci[:B], dcxc[:B])
+        dz1 = torch.zeros_like(x)
+        dz1.index_copy_(0, ci[:B], dz1c[:B])
+        dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask)
+        batch += [(dz1c, cxc, G["o_w"].buf, acc), (dqkv, x, G["qkv_w"].buf, acc)]
+        if rc.colsum_pending is not None:
+            rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))
+        else:
+            K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
+        prev = rc.ln2_saved.get(ctx.idx - 1)
+        if prev is not None:
+            z2p, m2p, r2p, Lp, site_p, p_p = prev
+            Gp = Lp["sinks"]
+            acc_p = [Gp[k].accumulate() for k in ("ln2_w", "ln2_b", "l2_b")]
+            if len(set(acc_p)) != 1:
+                raise RuntimeError("output-LN gradient sinks out of step")
+            dx, df_p = K.linear_dx_ln_bwd(dqkv, wt["qkv_w"], dz1, z2p, Lp["ln2_w"], m2p, r2p, Gp["ln2_w"].buf,
+                                          Gp["ln2_b"].buf, Gp["l2_b"].buf, rc.seed, site_p, p_p, acc_p[0], rc.row_map,
+                                          jobs)
+            rc.ln2_pending[ctx.idx - 1] = (dx, df_p)
+        else:
+            dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt["qkv_w"])
+        for k in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_w", "ln1_b", "l1_w", "l1_b", "l2_b", "ln2_w", "ln2_b"):
+            G[k].accumulate()
+        del ctx.acts, ctx.dmask
+        return dx, None, None, None
+
+    @staticmethod
     def backward(ctx, dy):
+        if ctx.pruned:
+            return LayerFn._backward_pruned(ctx, dy)
         (x,) = ctx.saved_tensors
         qkv, cx, lse, ao, h, m1, r1, u, g, f, m2, r2 = ctx.acts
         L, rc = ctx.L, ctx.rc
@@ -333,7 +431,8 @@ class HeadFn(torch.autograd.Function):
     def forward(ctx, hidden, W, b, sinks, rc: RunCtx, labels: Optional[torch.Tensor], kd=None):
         """kd = (teacher logits, T, alpha): the fused loss is the distillation loss."""
         p = rc.p_head if rc.training else 0.0
-        cls = rc.cu[:-1] if rc.cu is not None else None  # packed: [CLS] = first row of each sequence
+        # packed: [CLS] = first row of each sequence; pruned last block: row b of its output
+        cls = rc.head_rows if rc.head_rows is not None else rc.cu[:-1] if rc.cu is not None else None
         logits, loss, dlog = K.head_fwd(hidden, rc.B, rc.S, W, b, rc.seed, 2, p, labels, cls, kd)
         ctx.rc, ctx.sinks, ctx.p, ctx.W = rc, sinks, p, W
         ctx.save_for_backward(hidden)
@@ -365,7 +464,8 @@ class HeadFn(torch.autograd.Function):
         s = ctx.sinks
         acc = s["w"].accumulate()
         s["b"].accumulate()
-        cls = ctx.rc.cu[:-1] if ctx.rc.cu is not None else None
+        rc = ctx.rc
+        cls = rc.head_rows if rc.head_rows is not None else rc.cu[:-1] if rc.cu is not None else None
         dh = K.head_bwd(hidden, ctx.rc.B, ctx.rc.S, ctx.W, ctx.rc.seed, 2, ctx.p, dlog, s["w"].buf, s["b"].buf, acc,
                         cls, gscale)
         return dh, None, None, None, None, None, None
