@@ -76,6 +76,10 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
                int accumulate, unsigned char* now, unsigned char* ever, const int* row_map, const int* cu, hipStream_t st);
+int fd_gather_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int n, int d_bytes,
+                    hipStream_t st);
+int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int nsrc, int T,
+                     int d_bytes, hipStream_t st);
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
             int* cu, long long* ids_packed, int* step, uint32_t* seed, hipStream_t st);
 int fd_colsum_bf16_batched(int n, const void* const* xs, const int* T, const int* N, float* const* parts,
@@ -474,6 +478,34 @@ void pack(const at::Tensor& mask, const at::Tensor& ids, const at::Tensor& row_m
                    (int)row_map.numel(), row_map.data_ptr<int>(), cu.data_ptr<int>(),
                    reinterpret_cast<long long*>(ids_packed.data_ptr()), ptr<int>(step), ptr<uint32_t>(seed), stream()),
            "pack");
+}
+
+// Pruned last block: (oa, ob)[k] = (a, b)[idx[k]] for k < n (same-shape bf16 [*, D] pairs), one launch.
+void gather_rows2(const at::Tensor& a, const at::Tensor& b, const at::Tensor& oa, const at::Tensor& ob,
+                  const at::Tensor& idx) {
+  for (const at::Tensor* t : {&a, &b, &oa, &ob}) need(*t, at::kBFloat16, "gather_rows2 operand");
+  need(idx, at::kLong, "idx");
+  TORCH_CHECK(a.dim() == 2 && a.sizes() == b.sizes() && oa.dim() == 2 && oa.sizes() == ob.sizes() &&
+                  oa.size(1) == a.size(1) && oa.size(0) == idx.numel(), "gather_rows2: shapes");
+  TORCH_CHECK((a.size(1) * 2) % 16 == 0, "gather_rows2: rows must be 16-byte multiples");
+  // (the indices are device data: the kernel trusts 0 <= idx < rows; the model builds them from cu)
+  check_rc(fd_gather_rows2(a.data_ptr(), b.data_ptr(), oa.data_ptr(), ob.data_ptr(),
+                           reinterpret_cast<const long long*>(idx.data_ptr()), (int)idx.numel(), (int)(a.size(1) * 2),
+                           stream()), "gather_rows2");
+}
+
+// Pruned last block: oa / ob [T, D] = 0 except rows idx[k] (k < nsrc, ascending) = a / b [k].
+void scatter_rows2(const at::Tensor& a, const at::Tensor& b, const at::Tensor& oa, const at::Tensor& ob,
+                   const at::Tensor& idx, int64_t nsrc) {
+  for (const at::Tensor* t : {&a, &b, &oa, &ob}) need(*t, at::kBFloat16, "scatter_rows2 operand");
+  need(idx, at::kLong, "idx");
+  TORCH_CHECK(a.dim() == 2 && a.sizes() == b.sizes() && oa.dim() == 2 && oa.sizes() == ob.sizes() &&
+                  oa.size(1) == a.size(1) && nsrc >= 0 && nsrc <= a.size(0) && nsrc <= idx.numel(),
+              "scatter_rows2: shapes");
+  TORCH_CHECK((a.size(1) * 2) % 16 == 0, "scatter_rows2: rows must be 16-byte multiples");
+  check_rc(fd_scatter_rows2(a.data_ptr(), b.data_ptr(), oa.data_ptr(), ob.data_ptr(),
+                            reinterpret_cast<const long long*>(idx.data_ptr()), (int)nsrc, (int)oa.size(0),
+                            (int)(a.size(1) * 2), stream()), "scatter_rows2");
 }
 
 // ---------------------------------------------------------------- native RCCL communicator
@@ -1043,6 +1075,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return (int64_t)fd_gemm_dw2_splits((int)M0, (int)N0, (int)M1, (int)N1, (int)K);
   });
   m.def("gemm_set_fixup", [](bool on) { fd_gemm_set_fixup(on ? 1 : 0); });
+  m.def("gather_rows2", &gather_rows2);
+  m.def("scatter_rows2", &scatter_rows2);
   m.def("pack", &pack, py::arg("mask"), py::arg("ids"), py::arg("row_map"), py::arg("cu"), py::arg("ids_packed"),
         py::arg("step") = py::none(), py::arg("seed") = py::none());
   m.def("transpose_batched", &transpose_batched);

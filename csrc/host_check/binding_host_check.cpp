@@ -269,6 +269,25 @@ int fd_emb_bwd(const void*, const void*, int, const long long*, const long long*
                const float*, const float*, const float*, float*, float*, float*, float*, float*, float*, int, int, int,
                int, int, int, const uint32_t*, uint32_t, uint32_t, float, int, unsigned char*, unsigned char*,
                const int*, const int*, hipStream_t) { ++hc::calls; return 0; }
+int fd_gather_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int n, int d_bytes,
+                    hipStream_t) {
+  ++hc::calls;
+  hc::span(oa, (long long)n * d_bytes, "gather_rows2 oa");
+  hc::span(ob, (long long)n * d_bytes, "gather_rows2 ob");
+  hc::span(idx, (long long)n * 8, "gather_rows2 idx");
+  (void)a; (void)b;  // rows named by device indices
+  return 0;
+}
+int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int nsrc, int T,
+                     int d_bytes, hipStream_t) {
+  ++hc::calls;
+  hc::span(a, (long long)nsrc * d_bytes, "scatter_rows2 a");
+  hc::span(b, (long long)nsrc * d_bytes, "scatter_rows2 b");
+  hc::span(oa, (long long)T * d_bytes, "scatter_rows2 oa");
+  hc::span(ob, (long long)T * d_bytes, "scatter_rows2 ob");
+  hc::span(idx, (long long)nsrc * 8, "scatter_rows2 idx");
+  return 0;
+}
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
             int* cu, long long* ids_packed, int* step, uint32_t* seed, hipStream_t) {
   ++hc::calls;
@@ -622,6 +641,15 @@ int main() {
     auto mask = T_({32, 128}, i64), ids = T_({32, 128}, i64), rm = T_({2688}, i32), cu = T_({33}, i32);
     auto ip = T_({2688}, i64);
     expect_ok("pack", [&] { pack(mask, ids, rm, cu, ip, none, none); });
+    {
+      auto ga = T_({300, 768}, bf), gb = T_({300, 768}, bf), go = T_({64, 768}, bf), go2 = T_({64, 768}, bf);
+      auto gi = T_({64}, i64);
+      expect_ok("gather_rows2", [&] { gather_rows2(ga, gb, go, go2, gi); });
+      expect_ok("scatter_rows2", [&] { scatter_rows2(go, go2, ga, gb, gi, 32); });
+      auto gbad = T_({63, 768}, bf);
+      expect_reject("gather_rows2 shapes", [&] { gather_rows2(ga, gb, gbad, go2, gi); });
+      expect_reject("scatter_rows2 nsrc", [&] { scatter_rows2(go, go2, ga, gb, gi, 65); });
+    }
     auto st1 = T_({1}, i32);
     expect_ok("pack + counters", [&] { pack(mask, ids, rm, cu, ip, st1, st1); });
     auto stf = T_({1}, f32);

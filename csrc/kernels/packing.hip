@@ -74,9 +74,58 @@ __global__ __launch_bounds__(1024) void pack_kernel(const M* mask, const I* ids,
   }
 }
 
+// Pruned last block (ops/functional.py LayerFn._forward_pruned): two [rows][D] bf16 matrices
+// gathered at the same row list in one launch (out_i[k] = in_i[idx[k]]), and the reverse: two
+// [n][D] matrices scattered into zero-filled [T][D] ones (out_i[idx[k]] = in_i[k] for k < nsrc,
+// every other row 0).  One thread moves 16 bytes; the scatter finds a row's source by binary
+// search over the ascending idx[0, nsrc) (the [CLS] rows), so each output row is written once.
+__global__ __launch_bounds__(256) void gather_rows2_kernel(const uint4* a, const uint4* b, uint4* oa, uint4* ob,
+                                                           const long long* idx, int n, int d16) {
+  const long long i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= (long long)n * d16) return;
+  const long long r = i / d16, c = i - r * d16;
+  const long long src = idx[r] * d16 + c;
+  oa[i] = a[src];
+  ob[i] = b[src];
+}
+__global__ __launch_bounds__(256) void scatter_rows2_kernel(const uint4* a, const uint4* b, uint4* oa, uint4* ob,
+                                                            const long long* idx, int nsrc, int T, int d16) {
+  const long long i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= (long long)T * d16) return;
+  const long long r = i / d16, c = i - r * d16;
+  int lo = 0, hi = nsrc;  // first k with idx[k] >= r
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (idx[mid] < r) lo = mid + 1; else hi = mid;
+  }
+  const bool hit = lo < nsrc && idx[lo] == r;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  oa[i] = hit ? a[(long long)lo * d16 + c] : z;
+  ob[i] = hit ? b[(long long)lo * d16 + c] : z;
+}
+
 }  // namespace
 
 extern "C" {
+
+int fd_gather_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int n, int d_bytes,
+                    hipStream_t st) {
+  if (n <= 0 || d_bytes <= 0 || d_bytes % 16) return 1;
+  const long long tot = (long long)n * (d_bytes / 16);
+  hipLaunchKernelGGL(gather_rows2_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const uint4*)a,
+                     (const uint4*)b, (uint4*)oa, (uint4*)ob, idx, n, d_bytes / 16);
+  return 0;
+}
+
+int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int nsrc, int T,
+                     int d_bytes, hipStream_t st) {
+  if (nsrc < 0 || T <= 0 || d_bytes <= 0 || d_bytes % 16) return 1;
+  const long long tot = (long long)T * (d_bytes / 16);
+  hipLaunchKernelGGL(scatter_rows2_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const uint4*)a,
+                     (const uint4*)b, (uint4*)oa, (uint4*)ob, idx, nsrc, T, d_bytes / 16);
+  return 0;
+}
+
 
 // mask_bytes / ids_bytes: 8 (int64) or 4 (int32) / 1 (uint8 mask).  n = B * S <= 1 << 20.
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,

@@ -572,7 +572,7 @@ class DDoSClassifier(nn.Module):
         Bp = (B + 63) // 64 * 64
         if not (self.prune_last and rc.fuse_ln and layers and K.ln_fusable(Bp, D) and Bp <= rc.B * rc.S):
             return
-        if grad and (rc.dw_batch is None or rc.wgrad is not None or rc.colsum_jobs is None or "wT" not in layers[-1]):
+        if grad and (rc.dw_batch is None or rc.wgrad is not None or "wT" not in layers[-1]):
             return
         dev = self.arena.device
         key = (B, S, Bp, str(dev))

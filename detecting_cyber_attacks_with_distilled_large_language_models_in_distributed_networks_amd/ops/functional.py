@@ -254,7 +254,7 @@ class LayerFn(torch.autograd.Function):
         dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
         cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask)
         ci, rm = rc.cls_rows, rc.cls_rmap
-        cxc, xc = cx.index_select(0, ci), x.index_select(0, ci)
+        cxc, xc = K.gather_rows2(cx, x, ci)
         h, ao, m1, r1 = K.linear_ln_fwd(cxc, L["o_w"], L["o_b"], xc, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0,
                                         keep_z=grad)
         g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
@@ -286,18 +286,19 @@ class LayerFn(torch.autograd.Function):
         dz2, df = K.ln_bwd(dy, f, None, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, rc.seed,
                            ffn_site, p_h, acc, rm, jobs, zin=True)
         g_out = torch.empty_like(u) if g is None else None
-        du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt["l2_w"], colsum=(jobs, G["l1_b"].buf, acc), aux_out=g_out)
+        fuse_cs = jobs is not None and rc.fuse_colsum
+        du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt["l2_w"], colsum=(jobs, G["l1_b"].buf, acc) if fuse_cs else None,
+                         aux_out=g_out)
+        if not fuse_cs:
+            K.colsum(du, G["l1_b"].buf, acc, jobs)
         if g is None:
             g = g_out
         batch += [(df, g, G["l2_w"].buf, acc), (du, h, G["l1_w"].buf, acc)]
         dz1c, _ = K.linear_dx_ln_bwd(du, wt["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
                                      G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs)
         dcxc = K.linear_dx(dz1c, L["o_w"], wt=wt["o_w"])
-        # the [CLS] rows' gradients back into the full layout (filler rows carry exact zeros)
-        dcx = torch.zeros_like(cx)
-        dcx.index_copy_(0, ci[:B], dcxc[:B])
-        dz1 = torch.zeros_like(x)
-        dz1.index_copy_(0, ci[:B], dz1c[:B])
+        # the [CLS] rows' gradients back into the full layout (every other row exactly 0)
+        dcx, dz1 = K.scatter_rows2(dcxc, dz1c, ci, B, cx.shape[0])
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask)
         batch += [(dz1c, cxc, G["o_w"].buf, acc), (dqkv, x, G["qkv_w"].buf, acc)]
         if rc.colsum_pending is not None:

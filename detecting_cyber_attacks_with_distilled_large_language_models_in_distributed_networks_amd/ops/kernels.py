@@ -204,6 +204,23 @@ def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = False, jobs: O
     return out
 
 
+def gather_rows2(a: torch.Tensor, b: torch.Tensor, idx: torch.Tensor):
+    """(a[idx], b[idx]) for two same-shape bf16 [T, D] matrices, one launch (idx int64, device)."""
+    oa = torch.empty(idx.numel(), a.shape[1], dtype=a.dtype, device=a.device)
+    ob = torch.empty_like(oa)
+    ext().gather_rows2(a, b, oa, ob, idx)
+    return oa, ob
+
+
+def scatter_rows2(a: torch.Tensor, b: torch.Tensor, idx: torch.Tensor, nsrc: int, T: int):
+    """Two zero-filled [T, D] matrices with rows idx[k] = a[k] / b[k] for k < nsrc (idx ascending
+    over those k), one launch."""
+    oa = torch.empty(T, a.shape[1], dtype=a.dtype, device=a.device)
+    ob = torch.empty_like(oa)
+    ext().scatter_rows2(a, b, oa, ob, idx, nsrc)
+    return oa, ob
+
+
 def colsum_partials_batched(pending: list, jobs: list):
     """Partials of several deferred bf16 column sums -- pending = [(x, out, accumulate)] -- in ONE
     launch, each appended to ``jobs`` exactly as ``colsum(x, out, accumulate, jobs)`` would

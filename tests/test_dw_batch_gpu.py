@@ -79,6 +79,7 @@ def test_batched_backward_matches_per_layer():
     for batch in (True, False):
         m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=17)
         m.batch_dw = batch
+        m.prune_last = False  # (pruning needs the batched launch; it is compared in test_prune_gpu.py)
         m.train()
         ids, mask, labels, tokens = _batch(32, 128, seed=400)
         for acc_step in range(2):  # the second backward accumulates into the gradients
