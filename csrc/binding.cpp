@@ -81,7 +81,7 @@ int fd_gather_rows2(const void* a, const void* b, void* oa, void* ob, const long
 int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int nsrc, int T,
                      int d_bytes, hipStream_t st);
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
-            int* cu, long long* ids_packed, int* step, uint32_t* seed, hipStream_t st);
+            int* cu, long long* ids_packed, int* step, uint32_t* seed, long long* cls_rows, hipStream_t st);
 int fd_colsum_bf16_batched(int n, const void* const* xs, const int* T, const int* N, float* const* parts,
                            hipStream_t st);
 int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, int defer, int* nblk_out,
@@ -464,9 +464,11 @@ void splitk_reduce_batched(const std::vector<at::Tensor>& slabs, const std::vect
 // Unpadded-step layout in one launch: row_map [rows] int32, cu [B+1] int32, ids_packed [rows] int64.
 // step / seed (optional int32 [1]): counters advanced by the same launch (the step counter kernel folded in)
 void pack(const at::Tensor& mask, const at::Tensor& ids, const at::Tensor& row_map, const at::Tensor& cu,
-          const at::Tensor& ids_packed, const c10::optional<at::Tensor>& step, const c10::optional<at::Tensor>& seed) {
+          const at::Tensor& ids_packed, const c10::optional<at::Tensor>& step, const c10::optional<at::Tensor>& seed,
+          const c10::optional<at::Tensor>& cls_rows) {
   need_opt(step, at::kInt, "step");
   need_opt(seed, at::kInt, "seed");
+  need_opt(cls_rows, at::kLong, "cls_rows");  // [>= B]: row cu[b] of sequence b (int64)
   TORCH_CHECK(on_device(mask) && mask.is_contiguous() && on_device(ids) && ids.is_contiguous(), "pack: GPU inputs");
   TORCH_CHECK(mask.dim() == 2 && ids.sizes() == mask.sizes(), "pack: mask and ids must both be [B, S]");
   need(row_map, at::kInt, "row_map");
@@ -474,9 +476,13 @@ void pack(const at::Tensor& mask, const at::Tensor& ids, const at::Tensor& row_m
   need(ids_packed, at::kLong, "ids_packed");
   const int64_t B = mask.size(0), S = mask.size(1);
   TORCH_CHECK(cu.numel() == B + 1 && ids_packed.numel() == row_map.numel() && row_map.numel() >= 1, "pack: sizes");
+  if (cls_rows.has_value() && cls_rows->defined()) TORCH_CHECK(cls_rows->numel() >= B, "pack: cls_rows needs B entries");
   check_rc(fd_pack(mask.data_ptr(), (int)mask.element_size(), ids.data_ptr(), (int)ids.element_size(), (int)B, (int)S,
                    (int)row_map.numel(), row_map.data_ptr<int>(), cu.data_ptr<int>(),
-                   reinterpret_cast<long long*>(ids_packed.data_ptr()), ptr<int>(step), ptr<uint32_t>(seed), stream()),
+                   reinterpret_cast<long long*>(ids_packed.data_ptr()), ptr<int>(step), ptr<uint32_t>(seed),
+                   cls_rows.has_value() && cls_rows->defined() ? reinterpret_cast<long long*>(cls_rows->data_ptr())
+                                                               : nullptr,
+                   stream()),
            "pack");
 }
 
@@ -1078,7 +1084,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gather_rows2", &gather_rows2);
   m.def("scatter_rows2", &scatter_rows2);
   m.def("pack", &pack, py::arg("mask"), py::arg("ids"), py::arg("row_map"), py::arg("cu"), py::arg("ids_packed"),
-        py::arg("step") = py::none(), py::arg("seed") = py::none());
+        py::arg("step") = py::none(), py::arg("seed") = py::none(), py::arg("cls_rows") = py::none());
   m.def("transpose_batched", &transpose_batched);
   m.def("comm_load", &comm_load);
   m.def("comm_unique_id", &comm_unique_id);

@@ -289,8 +289,9 @@ int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const lon
   return 0;
 }
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
-            int* cu, long long* ids_packed, int* step, uint32_t* seed, hipStream_t) {
+            int* cu, long long* ids_packed, int* step, uint32_t* seed, long long* cls_rows, hipStream_t) {
   ++hc::calls;
+  hc::opt_span(cls_rows, (long long)B * 8, "pack cls_rows");
   hc::opt_span(step, 4, "pack step");
   hc::opt_span(seed, 4, "pack seed");
   hc::span(mask, (long long)B * S * mask_bytes, "pack mask");
@@ -640,7 +641,7 @@ int main() {
   {
     auto mask = T_({32, 128}, i64), ids = T_({32, 128}, i64), rm = T_({2688}, i32), cu = T_({33}, i32);
     auto ip = T_({2688}, i64);
-    expect_ok("pack", [&] { pack(mask, ids, rm, cu, ip, none, none); });
+    expect_ok("pack", [&] { pack(mask, ids, rm, cu, ip, none, none, none); });
     {
       auto ga = T_({300, 768}, bf), gb = T_({300, 768}, bf), go = T_({64, 768}, bf), go2 = T_({64, 768}, bf);
       auto gi = T_({64}, i64);
@@ -651,11 +652,11 @@ int main() {
       expect_reject("scatter_rows2 nsrc", [&] { scatter_rows2(go, go2, ga, gb, gi, 65); });
     }
     auto st1 = T_({1}, i32);
-    expect_ok("pack + counters", [&] { pack(mask, ids, rm, cu, ip, st1, st1); });
+    expect_ok("pack + counters", [&] { pack(mask, ids, rm, cu, ip, st1, st1, none); });
     auto stf = T_({1}, f32);
-    expect_reject("pack counter dtype", [&] { pack(mask, ids, rm, cu, ip, stf, none); });
+    expect_reject("pack counter dtype", [&] { pack(mask, ids, rm, cu, ip, stf, none, none); });
     auto cu_bad = T_({32}, i32);
-    expect_reject("pack cu", [&] { pack(mask, ids, rm, cu_bad, ip, none, none); });
+    expect_reject("pack cu", [&] { pack(mask, ids, rm, cu_bad, ip, none, none, none); });
   }
   if (failures) {
     std::printf("binding host check: %d failure(s)\n", failures);

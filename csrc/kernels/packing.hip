@@ -16,7 +16,7 @@ namespace {
 template <typename M, typename I>
 __global__ __launch_bounds__(1024) void pack_kernel(const M* mask, const I* ids, int n, int S, int B, int rows,
                                                     int* row_map, int* cu, long long* ids_packed, int* step,
-                                                    uint32_t* seed) {
+                                                    uint32_t* seed, long long* cls_rows) {
   __shared__ int wsum[16];
   __shared__ int carry_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -46,7 +46,10 @@ __global__ __launch_bounds__(1024) void pack_kernel(const M* mask, const I* ids,
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int p = base + 4 * tid + j;
-      if (p < n && p % S == 0) cu[p / S] = off;  // tokens before sequence p / S
+      if (p < n && p % S == 0) {
+        cu[p / S] = off;  // tokens before sequence p / S
+        if (cls_rows) cls_rows[p / S] = off;  // (pruned last block: its [CLS] row, int64)
+      }
       if (f[j]) {
         if (off < rows) {
           row_map[off] = p;
@@ -129,12 +132,12 @@ int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const lon
 
 // mask_bytes / ids_bytes: 8 (int64) or 4 (int32) / 1 (uint8 mask).  n = B * S <= 1 << 20.
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
-            int* cu, long long* ids_packed, int* step, uint32_t* seed, hipStream_t st) {
+            int* cu, long long* ids_packed, int* step, uint32_t* seed, long long* cls_rows, hipStream_t st) {
   const int n = B * S;
   if (B <= 0 || S <= 0 || rows <= 0 || n > (1 << 20)) return 1;
 #define FD_PACK(MT, IT)                                                                                        \
   hipLaunchKernelGGL((pack_kernel<MT, IT>), dim3(1), dim3(1024), 0, st, (const MT*)mask, (const IT*)ids, n, S, B, \
-                     rows, row_map, cu, ids_packed, step, seed)
+                     rows, row_map, cu, ids_packed, step, seed, cls_rows)
   if (mask_bytes == 8 && ids_bytes == 8) FD_PACK(long long, long long);
   else if (mask_bytes == 8 && ids_bytes == 4) FD_PACK(long long, int);
   else if (mask_bytes == 4 && ids_bytes == 8) FD_PACK(int, long long);

@@ -515,6 +515,7 @@ class DDoSClassifier(nn.Module):
         if (grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None
                 and not self.wgrad_stream and self.transposed_dx):
             rc.fused_adam = self.fused_opt
+        plan = self._prune_plan(rc, layers, grad)
         # packed step: the counters ride on the packing launch (no kernel of their own)
         incs = [] if packed and self.fold_step_counters else None
         if self.training:
@@ -551,9 +552,10 @@ class DDoSClassifier(nn.Module):
             sd_inc = next((b for _, b in incs if b is not None), None)
             if len([a for a, _ in incs if a is not None]) > 1 or len([b for _, b in incs if b is not None]) > 1:
                 raise RuntimeError("a counter deferred twice in one forward")
-            rc.row_map, rc.cu, ids = K.pack(mask, ids, self.packed_rows(tokens, B, S), step=st_inc, seed=sd_inc)
+            rc.row_map, rc.cu, ids = K.pack(mask, ids, self.packed_rows(tokens, B, S), step=st_inc, seed=sd_inc,
+                                            cls_rows=plan[4] if plan is not None else None)
         x = EmbeddingFn.apply(token, ids, emb["word"], emb["pos"], emb["ln_w"], emb["ln_b"], emb["sinks"], rc)
-        self._setup_prune(rc, layers, grad, packed)
+        self._setup_prune(rc, plan, len(layers), packed)
         for i, L in enumerate(layers):
             x = LayerFn.apply(x, L, rc, i)
         if labels is not None:
@@ -562,18 +564,19 @@ class DDoSClassifier(nn.Module):
         logits, _ = HeadFn.apply(x, head["w"], head["b"], head["sinks"], rc, None)
         return None, logits
 
-    def _setup_prune(self, rc, layers, grad: bool, packed: bool):
+    def _prune_plan(self, rc, layers, grad: bool):
         """Last-block [CLS] pruning (RunCtx.prune_idx; ops/functional.py LayerFn._forward_pruned):
         exact -- the dropped rows reach neither the loss nor any gradient.  Needs the fused
         LayerNorm path and, for a training step, the all-layer dW launch (the pruned block's
-        out-proj / FFN weight gradients join it with K = Bp rows) and the W^T copies."""
+        out-proj / FFN weight gradients join it with K = Bp rows) and the W^T copies.  Returns the
+        per-shape index buffers (the packing launch fills the packed [CLS] rows), or None."""
         from ..ops import kernels as K
         B, S, D = rc.B, rc.S, self.config.dim
         Bp = (B + 63) // 64 * 64
         if not (self.prune_last and rc.fuse_ln and layers and K.ln_fusable(Bp, D) and Bp <= rc.B * rc.S):
-            return
+            return None
         if grad and (rc.dw_batch is None or rc.wgrad is not None or "wT" not in layers[-1]):
-            return
+            return None
         dev = self.arena.device
         key = (B, S, Bp, str(dev))
         cache = getattr(self, "_prune_cache", None)
@@ -584,13 +587,16 @@ class DDoSClassifier(nn.Module):
             cache = (key, rmap, padded_rows, torch.arange(B, dtype=torch.int32, device=dev),
                      torch.zeros(Bp, dtype=torch.int64, device=dev))
             self._prune_cache = cache
-        _, rmap, padded_rows, head_rows, packed_rows = cache
-        if packed:
-            packed_rows[:B].copy_(rc.cu[:-1])  # row cu[b]; filler rows -> row 0 (a finite row)
-            rc.cls_rows = packed_rows
-        else:
-            rc.cls_rows = padded_rows
-        rc.cls_rmap, rc.head_rows, rc.prune_idx = rmap, head_rows, len(layers) - 1
+        return cache
+
+    @staticmethod
+    def _setup_prune(rc, plan, n_layers: int, packed: bool):
+        if plan is None:
+            return
+        _, rmap, padded_rows, head_rows, packed_rows = plan
+        # packed: rows cu[b] (written by the packing launch); filler rows -> row 0 (a finite row)
+        rc.cls_rows = packed_rows if packed else padded_rows
+        rc.cls_rmap, rc.head_rows, rc.prune_idx = rmap, head_rows, n_layers - 1
 
     def _no_bias(self) -> torch.Tensor:
         """Placeholder key-bias tensor for the varlen path (the kernels do not read it)."""

@@ -249,16 +249,17 @@ def colsum_flush(jobs: list):
 
 
 # ------------------------------------------------------------------ unpadded layout
-def pack(mask: torch.Tensor, ids: torch.Tensor, rows: int, step=None, seed=None):
+def pack(mask: torch.Tensor, ids: torch.Tensor, rows: int, step=None, seed=None, cls_rows=None):
     """(row_map int32 [rows], cu int32 [B+1], ids_packed int64 [rows]) of a [B, S] batch: the
     real tokens in order (filler rows: row_map -1, id of position 0) -- one launch, which also
-    advances the optional int32 counters ``step`` / ``seed`` (what ``step_inc`` would launch)."""
+    advances the optional int32 counters ``step`` / ``seed`` (what ``step_inc`` would launch) and
+    writes cu[b] as int64 into ``cls_rows[b]`` when given (the pruned last block's row list)."""
     B = mask.shape[0]
     row_map = torch.empty(rows, dtype=torch.int32, device=mask.device)
     cu = torch.empty(B + 1, dtype=torch.int32, device=mask.device)
     ids_packed = torch.empty(rows, dtype=torch.int64, device=mask.device)
     m = mask if mask.dtype != torch.bool else mask.to(torch.uint8)
-    ext().pack(m.contiguous(), ids.contiguous(), row_map, cu, ids_packed, step, seed)
+    ext().pack(m.contiguous(), ids.contiguous(), row_map, cu, ids_packed, step, seed, cls_rows)
     return row_map, cu, ids_packed
 
 
