@@ -56,10 +56,11 @@ int fd_comm_broadcast(void* comm, void* buf, long long count, int dtype, int roo
 int fd_comm_allgather(void* comm, const void* send, void* recv, long long count, int dtype, hipStream_t st);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                int rows, uint64_t* dmask, hipStream_t st);
+                int rows, uint64_t* dmask, int q_live, hipStream_t st);
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx,
                 float* delta, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site,
-                uint32_t thr, float drop_scale, const int* cu, int rows, const uint64_t* dmask, hipStream_t st);
+                uint32_t thr, float drop_scale, const int* cu, int rows, const uint64_t* dmask, int q_live,
+                hipStream_t st);
 int fd_mask_to_bias(const void* mask, int mask_bytes, float* bias, long n, hipStream_t st);
 int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, float* mean,
               float* rstd, int T, int D, float eps, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
@@ -625,8 +626,9 @@ void check_dmask(const c10::optional<at::Tensor>& dmask, int64_t B, int64_t S, i
 
 void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
               int64_t B, int64_t S, int64_t H, const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
-              const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask) {
+              const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask, int64_t q_live = 0) {
   need(qkv, at::kBFloat16, "qkv");
+  TORCH_CHECK(q_live >= 0, "attention: q_live >= 0");
   need(kbias, at::kFloat, "kbias");
   need(ctx, at::kBFloat16, "ctx");
   need(lse, at::kFloat, "lse");
@@ -639,14 +641,15 @@ void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
   check_cu(cu, B, rows, ctx.numel() / (H * 64));
   check_rc(fd_attn_fwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(), (int)B,
                        (int)S, (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu),
-                       (int)rows, ptr<uint64_t>(dmask), stream()),
+                       (int)rows, ptr<uint64_t>(dmask), (int)q_live, stream()),
            "attn_fwd");
 }
 
 void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
               const at::Tensor& dctx, const at::Tensor& delta, const at::Tensor& dqkv, int64_t B, int64_t S, int64_t H,
               const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& cu,
-              const c10::optional<at::Tensor>& dmask) {
+              const c10::optional<at::Tensor>& dmask, int64_t q_live = 0) {
+  TORCH_CHECK(q_live >= 0, "attention: q_live >= 0");
   check_dmask(dmask, B, S, H);
   need(qkv, at::kBFloat16, "qkv");
   need(kbias, at::kFloat, "kbias");
@@ -666,7 +669,7 @@ void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
   check_rc(fd_attn_bwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(),
                        dctx.data_ptr(), delta.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)S, (int)H,
                        seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), (int)rows,
-                       ptr<uint64_t>(dmask), stream()),
+                       ptr<uint64_t>(dmask), (int)q_live, stream()),
            "attn_bwd");
 }
 
@@ -1093,8 +1096,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_allreduce", &comm_allreduce);
   m.def("comm_broadcast", &comm_broadcast);
   m.def("comm_allgather", &comm_allgather);
-  m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("B"),
+        py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"),
+        py::arg("dmask"), py::arg("q_live") = 0);
+  m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("dctx"),
+        py::arg("delta"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"),
+        py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("q_live") = 0);
   m.def("mask_to_bias", &mask_to_bias);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);

@@ -117,6 +117,11 @@ struct AttnArgs {
   // backward reads them instead of re-hashing (bitwise the same masks).  [B*H][128 q][2] u64,
   // bit k of word (q, kt) = keep(q, key 64 kt + k)
   uint64_t* dmask;
+  // S <= 128 kernels: only the first q_live query rows of each sequence are needed (0: all) --
+  // the pruned last block needs row 0 ([CLS]) only.  The forward leaves ctx / lse of the other
+  // rows unwritten; the backward treats them as rows with no gradient (lse = +inf -> P = 0,
+  // delta = 0, dQ = 0 written) -- the caller's dctx is 0 on them.
+  int q_live;
 };
 
 // Varlen: the extra grid slice z == B zeroes head h's columns of the filler rows
@@ -529,7 +534,8 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
   if (tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) : -INFINITY;
   __syncthreads();
-  if (q0 >= len) return;  // no barrier follows
+  const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows needed
+  if (q0 >= qlen) return;  // no barrier follows
   const uint32_t seed = site_seed(a);
   const bool drop = a.drop_threshold != 0;
   f32x4 o[4];
@@ -617,7 +623,7 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
-  if (q >= len) return;
+  if (q >= qlen) return;
   const float inv = 1.f / l;
   bf16_t* out = a.ctx + (tok0 + q) * D + h * DH;
 #pragma unroll
@@ -647,6 +653,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   int tok0i, len;
   seq_span(a, b, tok0i, len);
   const int nt = (len + 63) >> 6;
+  const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows with a gradient
   const size_t tok0 = (size_t)tok0i;
   const size_t st0 = ((size_t)b * H + h) * S;
   // phase 1's O rows (for delta) are fetched together with the staging loads: no second
@@ -665,7 +672,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   if (tid < 128) {
     kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) : -INFINITY;
     // query rows past the sequence: lse = +inf makes their P (and dS) exactly 0
-    lse_s[tid] = tid < len ? a.lse[st0 + tid] : INFINITY;
+    lse_s[tid] = tid < qlen ? a.lse[st0 + tid] : INFINITY;
     dl_s[tid] = 0.f;
   }
   const bool drop = a.drop_threshold != 0;
@@ -681,7 +688,15 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   const uint64_t vk1 = __ballot(kb[64 + lane] != -INFINITY);
 
   // ---- phase 1: dQ and delta; wave w owns queries 16w .. 16w+15
-  if (q0 < len) {
+  if (q0 >= qlen && q0 < len) {  // rows without a gradient (q_live): dQ = 0
+    const int q = q0 + (lane & 15);
+    if (q < len) {
+      bf16_t* out = a.dqkv + (tok0 + q) * ld3 + h * DH;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) = make_uint2(0u, 0u);
+    }
+  }
+  if (q0 < qlen) {
     const int q = q0 + (lane & 15);
     const int qr = min(q, len - 1);
     const char* qst = qs + (q0 >> 6) * 8192;
@@ -700,6 +715,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
       for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)of[s2][j]) * bf2f((uint16_t)dof[s2][j]);
     dl += __shfl_xor(dl, 16, 64);
     dl += __shfl_xor(dl, 32, 64);
+    if (q >= qlen) dl = 0.f;  // (q_live: this row's O was never written -- it has no gradient)
     if (g == 0 && q < len) dl_s[q] = dl;
     const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
     f32x4 dq[4];
@@ -787,7 +803,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
     // 16-query sub-tiles past the sequence (varlen) have lse = +inf: P = dS = 0, skipped
     bool tv[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) tv[t] = qt * 64 + 16 * t < len;
+    for (int t = 0; t < 4; ++t) tv[t] = qt * 64 + 16 * t < qlen;
     f32x4 sc[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -860,9 +876,10 @@ extern "C" {
 
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                int rows, uint64_t* dmask, hipStream_t st) {
+                int rows, uint64_t* dmask, int q_live, hipStream_t st) {
   if (S % 64 != 0) return 1;
   AttnArgs a{};
+  a.q_live = q_live;
   a.cu = cu;
   a.dmask = use_s128(S) ? dmask : nullptr;
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
@@ -878,9 +895,10 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse,
                 const void* dctx, float* delta, void* dqkv, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                int rows, const uint64_t* dmask, hipStream_t st) {
+                int rows, const uint64_t* dmask, int q_live, hipStream_t st) {
   if (S % 64 != 0) return 1;
   AttnArgs a{};
+  a.q_live = q_live;
   a.cu = cu;
   a.dmask = use_s128(S) ? const_cast<uint64_t*>(dmask) : nullptr;
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = (float*)lse;

@@ -252,7 +252,8 @@ class LayerFn(torch.autograd.Function):
         grad = ctx.needs_input_grad[0]
         qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
         dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
-        cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask)
+        # only each sequence's first query row ([CLS]) is needed: the other rows' context is never read
+        cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask, q_live=1)
         ci, rm = rc.cls_rows, rc.cls_rmap
         cxc, xc = K.gather_rows2(cx, x, ci)
         h, ao, m1, r1 = K.linear_ln_fwd(cxc, L["o_w"], L["o_b"], xc, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0,
@@ -299,7 +300,8 @@ class LayerFn(torch.autograd.Function):
         dcxc = K.linear_dx(dz1c, L["o_w"], wt=wt["o_w"])
         # the [CLS] rows' gradients back into the full layout (every other row exactly 0)
         dcx, dz1 = K.scatter_rows2(dcxc, dz1c, ci, B, cx.shape[0])
-        dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask)
+        dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask,
+                          q_live=1)
         batch += [(dz1c, cxc, G["o_w"].buf, acc), (dqkv, x, G["qkv_w"].buf, acc)]
         if rc.colsum_pending is not None:
             rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))

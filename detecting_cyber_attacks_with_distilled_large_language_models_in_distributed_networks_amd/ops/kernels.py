@@ -281,7 +281,7 @@ def attn_keep_bits(B, S, H, p, device) -> Optional[torch.Tensor]:
     return torch.empty(B * H * 256, dtype=torch.int64, device=device)
 
 
-def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None) -> Tuple[torch.Tensor, torch.Tensor]:
+def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """cu (int32 [B+1]): varlen mode -- qkv/ctx hold packed sequences (rows cu[b]..cu[b+1]-1);
     the kernel zeroes ctx's filler rows past cu[B] itself.  dmask (``attn_keep_bits``): also
     record the dropout keep bits for ``attn_bwd``."""
@@ -289,17 +289,18 @@ def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None) -> Tuple[t
     ctx = torch.empty(rows, H * 64, dtype=torch.bfloat16, device=qkv.device)
     lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
     thr, sc = _drop(p)
-    ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None)
+    # q_live > 0 (S <= 128): only the first q_live query rows of each sequence are computed
+    ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None, q_live)
     return ctx, lse
 
 
-def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=None) -> torch.Tensor:
+def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0) -> torch.Tensor:
     """dmask: the keep bits recorded by the matching ``attn_fwd`` (same seed / site / p)."""
     dqkv = torch.empty_like(qkv)  # varlen: filler rows zeroed by the dQ kernel
     delta = workspace(qkv.device, "attn_delta", B * H * S)
     thr, sc = _drop(p)
     ext().attn_bwd(qkv, kbias, ctx, lse, dctx.contiguous(), delta, dqkv, B, S, H, seed, site, thr, sc, cu,
-                   dmask if thr else None)
+                   dmask if thr else None, q_live)
     return dqkv
 
 

@@ -88,3 +88,37 @@ def test_pruned_graph_training_tracks_full():
     for a, b in zip(*losses):
         assert abs(a - b) < 1e-3 * max(1.0, abs(b))
     assert _frel(models[0].arena.master, models[1].arena.master) < 1e-6
+
+
+def test_attention_q_live_matches_full_and_ignores_garbage():
+    """q_live = 1 (the pruned block's attention): only each sequence's first query row is computed;
+    with dO non-zero on those rows only, dQ / dK / dV equal the full kernels' and stay finite even
+    when the unwritten context rows hold NaN (the caching allocator is primed with NaN memory)."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import (
+        kernels as K)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    B, S, H = 8, 128, 12
+    lens = torch.tensor([70, 84, 60, 77, 81, 65, 83, 72])
+    cu = torch.zeros(B + 1, dtype=torch.int32)
+    cu[1:] = torch.cumsum(lens, 0)
+    rows = (int(lens.sum()) + 127) // 128 * 128
+    cu = cu.cuda()
+    qkv = (torch.randn(rows, 3 * H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    kb = torch.zeros(1, device="cuda")
+    seed = torch.tensor([3], dtype=torch.int32, device="cuda")
+    for p in (0.0, 0.1):
+        dm = K.attn_keep_bits(B, S, H, p, "cuda")
+        ctx_full, lse_full = K.attn_fwd(qkv, kb, B, S, H, seed, 5, p, cu=cu, dmask=dm)
+        junk = torch.full((rows * H * 64 * 4,), float("nan"), device="cuda")
+        del junk
+        dm2 = K.attn_keep_bits(B, S, H, p, "cuda")
+        ctx_q, lse_q = K.attn_fwd(qkv, kb, B, S, H, seed, 5, p, cu=cu, dmask=dm2, q_live=1)
+        cls = cu[:-1].long()
+        assert torch.equal(ctx_q[cls], ctx_full[cls])
+        dctx = torch.zeros(rows, H * 64, device="cuda", dtype=torch.bfloat16)
+        dctx[cls] = (torch.randn(B, H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+        d_full = K.attn_bwd(qkv, kb, ctx_full, lse_full, dctx, B, S, H, seed, 5, p, cu=cu, dmask=dm)
+        d_q = K.attn_bwd(qkv, kb, ctx_q, lse_q, dctx, B, S, H, seed, 5, p, cu=cu, dmask=dm2, q_live=1)
+        torch.cuda.synchronize()
+        assert torch.isfinite(d_q.float()).all()
+        assert _frel(d_q, d_full) < 1e-2
