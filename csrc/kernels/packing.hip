@@ -91,17 +91,25 @@ __global__ __launch_bounds__(256) void gather_rows2_kernel(const uint4* a, const
   oa[i] = a[src];
   ob[i] = b[src];
 }
+constexpr int SCATTER_LDS_IDX = 512;
 __global__ __launch_bounds__(256) void scatter_rows2_kernel(const uint4* a, const uint4* b, uint4* oa, uint4* ob,
                                                             const long long* idx, int nsrc, int T, int d16) {
+  // the (short, ascending) source row list staged in LDS once per block: the per-element binary
+  // search then costs LDS latency instead of dependent global loads
+  __shared__ long long sidx[SCATTER_LDS_IDX];
+  const bool lds = nsrc <= SCATTER_LDS_IDX;
+  if (lds)
+    for (int k = threadIdx.x; k < nsrc; k += 256) sidx[k] = idx[k];
+  __syncthreads();
   const long long i = blockIdx.x * 256ll + threadIdx.x;
   if (i >= (long long)T * d16) return;
   const long long r = i / d16, c = i - r * d16;
   int lo = 0, hi = nsrc;  // first k with idx[k] >= r
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    if (idx[mid] < r) lo = mid + 1; else hi = mid;
+    if ((lds ? sidx[mid] : idx[mid]) < r) lo = mid + 1; else hi = mid;
   }
-  const bool hit = lo < nsrc && idx[lo] == r;
+  const bool hit = lo < nsrc && (lds ? sidx[lo] : idx[lo]) == r;
   const uint4 z = make_uint4(0, 0, 0, 0);
   oa[i] = hit ? a[(long long)lo * d16 + c] : z;
   ob[i] = hit ? b[(long long)lo * d16 + c] : z;
