@@ -1333,7 +1333,15 @@ long long tiles_of(int id, int M, int N) {
 // Occupancy wins over ring depth: the 2-3 blocks/CU configs (S2) beat the
 // 1 block/CU S3 rings at every shape; 8-wave 256x192 / 128x192 only where they
 // make one full round of tiles.
+// M <= 64 (the pruned last block's [CLS] rows): 64 x 64 tiles -- a 128-row tile would be half
+// empty, and a one-round grid's time is its per-tile K loop (FD_SMALLM_TILES=0: off)
+bool smallm_tiles() {
+  static const bool on = [] { const char* e = getenv("FD_SMALLM_TILES"); return !e || atoi(e) != 0; }();
+  return on;
+}
+
 int pick_cfg(int kind, int M, int N, int K) {
+  if (kind == 0 && M <= 64 && N % 64 == 0 && smallm_tiles()) return 13;
   if (kind == 0) {  // NT forward (and dX on transposed weights)
     // FFN1 forward / FFN2 dX (N = 3072): 256x192 fills the chip at M = 4096 (padded bs32),
     // 128x128 wins at the packed M ~ 2.7 k (21.5 vs 25.7 us; profiles/r1_gemm_cfg_sweep_T2688_packed.txt)
@@ -1505,6 +1513,7 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
   if (colsum) {
     // only the staged-fp32 epilogues sum columns: 128 x {128, 64} tiles (never 256-row ones)
     if (kind != 0 || (epi != EPI_GELU_BWD && epi != EPI_ADD)) return 2;
+    if (CFGS[id].bm != 128 && cfg_override(kind) < 0) id = 8;  // (small-M 64-row tiles: 128 x 64)
     if (CFGS[id].bm != 128 || (CFGS[id].bn != 128 && CFGS[id].bn != 64) || N % CFGS[id].bn) {
       // the shape's tile has no staged-fp32 epilogue (e.g. 256 x 192 at M >= 3.5 k): launch
       // nothing, report 0 blocks -- the caller runs the plain GEMM + a column-sum pass
@@ -1744,7 +1753,7 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   int id = cfg;
   if (id < 0) {
     static const int env = [] { const char* e = getenv("FD_GEMM_LN_CFG"); return e ? atoi(e) : -1; }();
-    id = env >= 0 ? env : 24;
+    id = env >= 0 ? env : (M <= 64 && smallm_tiles() ? 13 : 24);
   }
   const int bm = id == 13 ? 64 : 128, bn = 64;
   if (N / bn > LN_MAXK * (bn / 8)) return -2;
