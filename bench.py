@@ -105,11 +105,48 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _visible_gpus(nodes_dir: str = KFD_NODES) -> int:
+    """GPUs this process may use, counted WITHOUT any GPU library: the KFD topology nodes with a
+    nonzero ``gpu_id`` (CPU nodes have 0), capped by ``ROCR_VISIBLE_DEVICES`` /
+    ``HIP_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES`` (an empty list hides every GPU).  The
+    launcher parent must not initialise the GPU runtime before it starts the rank processes
+    (torch.cuda.device_count() can fall back to hipGetDeviceCount).  0 = unknown / none."""
+    n = 0
+    try:
+        for node in os.listdir(nodes_dir):
+            try:
+                with open(os.path.join(nodes_dir, node, "gpu_id")) as f:
+                    n += int(f.read().strip() or 0) != 0
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
+def _gpu_runtime_mapped() -> bool:
+    """Whether this process has opened the GPU (the KFD device is mapped once HSA initialises)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return any("/dev/kfd" in ln for ln in f)
+    except OSError:
+        return False
+
+
 def _spawn(args) -> int:
     """--gpus N > 1 without a torch.distributed environment: run N ranks as a child
     ``torch.distributed.run`` (one process per GPU, rendezvous on 127.0.0.1) and return its
-    exit status.  Nothing here initialises the GPU (device_count() does not, on this image)."""
-    ngpu = torch.cuda.device_count()
+    exit status.  Nothing here initialises the GPU: the GPUs are counted from sysfs, and the
+    children learn (FEDDDOS_PARENT_GPU_INIT) whether the parent's address space held the GPU
+    device at the moment of the spawn -- rank 0 reports it as ``parent_gpu_initialized``."""
+    ngpu = _visible_gpus()
     shared = os.environ.get("FEDDDOS_BACKEND") == "gloo"  # functional runs: ranks may share a device
     if ngpu and ngpu < args.gpus and not shared:
         print(f"bench: --gpus {args.gpus} needs {args.gpus} GPUs (one rank per GPU over RCCL), "
@@ -120,6 +157,7 @@ def _spawn(args) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
+    env["FEDDDOS_PARENT_GPU_INIT"] = "1" if _gpu_runtime_mapped() else "0"
     return subprocess.call(cmd, env=env)
 
 
@@ -329,6 +367,8 @@ def main():
             "fused_adam": fused,
             "graph_error": graph_err,
             "host_submit_ms": round(1000.0 * host_s, 2),
+            **({"parent_gpu_initialized": os.environ["FEDDDOS_PARENT_GPU_INIT"] == "1"}
+               if "FEDDDOS_PARENT_GPU_INIT" in os.environ else {}),
             **({"step_ms": [round(evs[i].elapsed_time(evs[i + 1]), 3) for i in range(len(evs) - 1)]} if evs else {}),
             "mean_loss": round(loss, 5),
             **comm_stats,
@@ -362,7 +402,7 @@ def _fedavg_timing(model, di, fedavg, comm, ncomm, k, sync):
         comm.barrier()
         t = time.perf_counter()
         if ncomm is not None and scratch.is_cuda:
-            ncomm.all_reduce_(scratch, "sum")
+            ncomm.all_reduce_(scratch, "sum", wait=False)  # (timed to the sync below)
         else:
             dist.all_reduce(scratch)
         sync()

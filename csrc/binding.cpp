@@ -39,6 +39,7 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
 int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K);
 int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg,
                      hipStream_t st);
+int fd_gemm_ln_set_diag(int diag);
 int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
                const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t st);
 int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
@@ -51,6 +52,9 @@ int fd_comm_unique_id_bytes();
 int fd_comm_get_unique_id(void* out);
 int fd_comm_init(void** comm, int nranks, int rank, const void* id_bytes);
 int fd_comm_destroy(void* comm);
+int fd_comm_async_error(void* comm);
+int fd_comm_wait(void* comm, hipStream_t st, long long timeout_ms);
+int fd_comm_abort(void* comm);
 int fd_comm_allreduce(void* comm, const void* send, void* recv, long long count, int dtype, int op, hipStream_t st);
 int fd_comm_broadcast(void* comm, void* buf, long long count, int dtype, int root, hipStream_t st);
 int fd_comm_allgather(void* comm, const void* send, void* recv, long long count, int dtype, hipStream_t st);
@@ -71,7 +75,8 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
               const int* row_map, int defer, int* nblk_out, int zin, hipStream_t st);
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
-               const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const int* row_map, hipStream_t st);
+               const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const int* row_map, int* ln_epoch,
+               hipStream_t st);
 int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sorted, const long long* perm,
                const void* word, const void* pos, const float* gamma, const float* mean, const float* rstd,
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
@@ -82,7 +87,8 @@ int fd_gather_rows2(const void* a, const void* b, void* oa, void* ob, const long
 int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int nsrc, int T,
                      int d_bytes, hipStream_t st);
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
-            int* cu, long long* ids_packed, int* step, uint32_t* seed, long long* cls_rows, hipStream_t st);
+            int* cu, long long* ids_packed, int* step, uint32_t* seed, long long* cls_rows, int* cls_rmap,
+            hipStream_t st);
 int fd_colsum_bf16_batched(int n, const void* const* xs, const int* T, const int* N, float* const* parts,
                            hipStream_t st);
 int fd_colsum_bf16(const void* x, int T, int N, float* out, float* work, int accumulate, int defer, int* nblk_out,
@@ -96,7 +102,7 @@ int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const f
                 const float* tlogits, float kd_T, float kd_alpha, hipStream_t st);
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
-                int accumulate, const int* cls, int T, const float* gscale, hipStream_t st);
+                int accumulate, const int* cls, int T, const float* gscale, const int* own, hipStream_t st);
 int fd_eval_metrics(const float* logits, const long long* labels, int B, double* acc, long long* counts,
                     float* prob1, long long* preds, hipStream_t st);
 int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float lr,
@@ -365,7 +371,8 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
 //   bwd = true:  dy = A Bt^T + res; C = dz (LN input gradient) from z, mean, rstd, gamma;
 //                dx = dropout'(dz) (when thr); colpart[tiles_m][3][N] = dgamma, dbeta, dbias partials.
 // stats (int64, >= 2 (M + 128) N / 64, zeroed once) is the row-statistic exchange, cnt (int32 [2],
-// zeroed once, self-maintained) the launch epoch / done counter, err (int32) the timeout flag.
+// zeroed once) the exchange epoch (advanced per model forward by emb_fwd, or by the caller),
+// err (int32) the timeout flag; xsite the launch's exchange call site (unique per epoch).
 // Returns the number of row blocks (colpart rows).
 int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::Tensor& C,
                 const c10::optional<at::Tensor>& bias, const at::Tensor& res, const at::Tensor& gamma,
@@ -373,7 +380,7 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
                 const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& dx,
                 const c10::optional<at::Tensor>& colpart, const at::Tensor& stats, const at::Tensor& cnt,
                 const at::Tensor& err, double eps, const c10::optional<at::Tensor>& seed, int64_t site, int64_t thr,
-                double dscale, const c10::optional<at::Tensor>& row_map, int64_t cfg) {
+                double dscale, const c10::optional<at::Tensor>& row_map, int64_t cfg, int64_t xsite) {
   need(A, at::kBFloat16, "A");
   need(Bt, at::kBFloat16, "Bt");
   need(C, at::kBFloat16, "C");
@@ -392,7 +399,8 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
   TORCH_CHECK(gamma.numel() == N, "gemm_ln: gamma of size N required");
   TORCH_CHECK(mean.numel() >= M && rstd.numel() >= M, "gemm_ln: mean / rstd need M entries");
   TORCH_CHECK(stats.numel() >= 2 * (M + 128) * (N / 64), "gemm_ln: stats too small");
-  TORCH_CHECK(cnt.numel() >= 2 && err.numel() >= 1, "gemm_ln: counters too small");
+  TORCH_CHECK(cnt.numel() >= 1 && err.numel() >= 1, "gemm_ln: counters too small");
+  TORCH_CHECK(xsite >= 0 && xsite < FD_LN_XSITES, "gemm_ln: exchange call site out of range");
   need_opt(bias, at::kFloat, "bias");
   need_opt(beta, at::kFloat, "beta");
   need_opt(z, at::kBFloat16, "z");
@@ -427,6 +435,7 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
   ln.thr = (uint32_t)thr;
   ln.site = (uint32_t)site;
   ln.dscale = (float)dscale;
+  ln.xsite = (uint32_t)xsite;
   if (thr) {
     TORCH_CHECK(seed.has_value() && seed->defined(), "gemm_ln: dropout needs the seed tensor");
     ln.seed_ptr = seedp(*seed);
@@ -466,7 +475,8 @@ void splitk_reduce_batched(const std::vector<at::Tensor>& slabs, const std::vect
 // step / seed (optional int32 [1]): counters advanced by the same launch (the step counter kernel folded in)
 void pack(const at::Tensor& mask, const at::Tensor& ids, const at::Tensor& row_map, const at::Tensor& cu,
           const at::Tensor& ids_packed, const c10::optional<at::Tensor>& step, const c10::optional<at::Tensor>& seed,
-          const c10::optional<at::Tensor>& cls_rows) {
+          const c10::optional<at::Tensor>& cls_rows, const c10::optional<at::Tensor>& cls_rmap) {
+  need_opt(cls_rmap, at::kInt, "cls_rmap");  // [>= B]: padded row of packed row cu[b] (int32)
   need_opt(step, at::kInt, "step");
   need_opt(seed, at::kInt, "seed");
   need_opt(cls_rows, at::kLong, "cls_rows");  // [>= B]: row cu[b] of sequence b (int64)
@@ -478,12 +488,13 @@ void pack(const at::Tensor& mask, const at::Tensor& ids, const at::Tensor& row_m
   const int64_t B = mask.size(0), S = mask.size(1);
   TORCH_CHECK(cu.numel() == B + 1 && ids_packed.numel() == row_map.numel() && row_map.numel() >= 1, "pack: sizes");
   if (cls_rows.has_value() && cls_rows->defined()) TORCH_CHECK(cls_rows->numel() >= B, "pack: cls_rows needs B entries");
+  if (cls_rmap.has_value() && cls_rmap->defined()) TORCH_CHECK(cls_rmap->numel() >= B, "pack: cls_rmap needs B entries");
   check_rc(fd_pack(mask.data_ptr(), (int)mask.element_size(), ids.data_ptr(), (int)ids.element_size(), (int)B, (int)S,
                    (int)row_map.numel(), row_map.data_ptr<int>(), cu.data_ptr<int>(),
                    reinterpret_cast<long long*>(ids_packed.data_ptr()), ptr<int>(step), ptr<uint32_t>(seed),
                    cls_rows.has_value() && cls_rows->defined() ? reinterpret_cast<long long*>(cls_rows->data_ptr())
                                                                : nullptr,
-                   stream()),
+                   ptr<int>(cls_rmap), stream()),
            "pack");
 }
 
@@ -544,6 +555,24 @@ int64_t comm_init(int64_t nranks, int64_t rank, const at::Tensor& id) {
   return reinterpret_cast<int64_t>(c);
 }
 void comm_destroy(int64_t h) { comm_check(fd_comm_destroy(reinterpret_cast<void*>(h)), "ncclCommDestroy"); }
+void comm_abort(int64_t h) { comm_check(fd_comm_abort(reinterpret_cast<void*>(h)), "ncclCommAbort"); }
+// (code, message): 0 = healthy; else the RCCL error of the communicator's async state
+std::tuple<int64_t, std::string> comm_async_error(int64_t h) {
+  const int rc = fd_comm_async_error(reinterpret_cast<void*>(h));
+  return {rc, rc ? std::string(fd_comm_last_error()) : std::string()};
+}
+// Bounded wait for the current stream (the collective just issued on it): (code, message) with
+// code 0 = done, 1001 = timeout, 1002 = HIP error, else the RCCL async error.  Releases the GIL.
+std::tuple<int64_t, std::string> comm_wait(int64_t h, int64_t timeout_ms) {
+  TORCH_CHECK(h != 0, "comm_wait: communicator not initialised");
+  const hipStream_t st = stream();
+  int rc;
+  {
+    py::gil_scoped_release nogil;
+    rc = fd_comm_wait(reinterpret_cast<void*>(h), st, (long long)timeout_ms);
+  }
+  return {rc, rc ? std::string(fd_comm_last_error()) : std::string()};
+}
 void comm_allreduce(int64_t h, const at::Tensor& t, int64_t op) {
   TORCH_CHECK(h != 0, "comm_allreduce: communicator not initialised");
   TORCH_CHECK(on_device(t) && t.is_contiguous(), "comm_allreduce: contiguous GPU tensor required");
@@ -740,9 +769,10 @@ int64_t ln_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at
 void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& pos, const at::Tensor& gamma,
              const at::Tensor& beta, const at::Tensor& y, const at::Tensor& mean, const at::Tensor& rstd, int64_t S,
              double eps, const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
-             const c10::optional<at::Tensor>& row_map) {
+             const c10::optional<at::Tensor>& row_map, const c10::optional<at::Tensor>& ln_epoch) {
   TORCH_CHECK(on_device(ids) && ids.is_contiguous() && (ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt),
               "ids must be contiguous GPU int64/int32");
+  need_opt(ln_epoch, at::kInt, "ln_epoch");
   need(word, at::kBFloat16, "word");
   need(pos, at::kBFloat16, "pos");
   need(gamma, at::kFloat, "gamma");
@@ -755,7 +785,7 @@ void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& po
   check_rc(fd_emb_fwd(ids.data_ptr(), ids.scalar_type() == at::kLong, word.data_ptr(), pos.data_ptr(),
                       gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(), mean.data_ptr<float>(),
                       rstd.data_ptr<float>(), (int)T, (int)S, (int)D, (float)eps, seedp(seed), (uint32_t)site,
-                      (uint32_t)thr, (float)dscale, map_ptr(row_map, T), stream()),
+                      (uint32_t)thr, (float)dscale, map_ptr(row_map, T), ptr<int>(ln_epoch), stream()),
            "emb_fwd");
 }
 
@@ -926,9 +956,11 @@ void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
 void head_bwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& W, const at::Tensor& seed, int64_t site,
               int64_t thr, double dscale, const at::Tensor& dlogits, const at::Tensor& dW, const at::Tensor& db,
               const at::Tensor& dhidden, bool accumulate, const c10::optional<at::Tensor>& cls,
-              const c10::optional<at::Tensor>& gscale) {
+              const c10::optional<at::Tensor>& gscale, const c10::optional<at::Tensor>& own) {
   need_opt(cls, at::kInt, "cls");
   need_opt(gscale, at::kFloat, "gscale");
+  need_opt(own, at::kInt, "own");
+  if (own.has_value() && own->defined()) TORCH_CHECK(own->numel() == B + 1, "head_bwd: own must be [B + 1]");
   if (gscale.has_value() && gscale->defined()) TORCH_CHECK(gscale->numel() == 1, "head_bwd: gscale is a scalar");
   need(hidden, at::kBFloat16, "hidden");
   need(W, at::kFloat, "W");
@@ -945,7 +977,7 @@ void head_bwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
   check_rc(fd_head_bwd(hidden.data_ptr(), (int)B, (int)S, (int)D, W.data_ptr<float>(), seedp(seed), (uint32_t)site,
                        (uint32_t)thr, (float)dscale, dlogits.data_ptr<float>(), dW.data_ptr<float>(),
                        db.data_ptr<float>(), dhidden.data_ptr(), accumulate ? 1 : 0, ptr<int>(cls),
-                       (int)(hidden.numel() / D), ptr<float>(gscale), stream()),
+                       (int)(hidden.numel() / D), ptr<float>(gscale), ptr<int>(own), stream()),
            "head_bwd");
 }
 
@@ -1074,7 +1106,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("rstd"), py::arg("z"),
         py::arg("dx"), py::arg("colpart"), py::arg("stats"), py::arg("cnt"), py::arg("err"), py::arg("eps"),
         py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("row_map"),
-        py::arg("cfg") = -1);
+        py::arg("cfg") = -1, py::arg("xsite") = 0);
   m.def("gemm_dw_batch", &gemm_dw_batch, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("accumulate"),
         py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1);
   m.def("gemm_colsum", &gemm_colsum, py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("aux"),
@@ -1087,12 +1119,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gather_rows2", &gather_rows2);
   m.def("scatter_rows2", &scatter_rows2);
   m.def("pack", &pack, py::arg("mask"), py::arg("ids"), py::arg("row_map"), py::arg("cu"), py::arg("ids_packed"),
-        py::arg("step") = py::none(), py::arg("seed") = py::none(), py::arg("cls_rows") = py::none());
+        py::arg("step") = py::none(), py::arg("seed") = py::none(), py::arg("cls_rows") = py::none(),
+        py::arg("cls_rmap") = py::none());
   m.def("transpose_batched", &transpose_batched);
   m.def("comm_load", &comm_load);
   m.def("comm_unique_id", &comm_unique_id);
   m.def("comm_init", &comm_init);
   m.def("comm_destroy", &comm_destroy);
+  m.def("comm_abort", &comm_abort);
+  m.def("comm_async_error", &comm_async_error);
+  m.def("comm_wait", &comm_wait);
   m.def("comm_allreduce", &comm_allreduce);
   m.def("comm_broadcast", &comm_broadcast);
   m.def("comm_allgather", &comm_allgather);
@@ -1105,7 +1141,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mask_to_bias", &mask_to_bias);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
-  m.def("emb_fwd", &emb_fwd);
+  m.def("emb_fwd", &emb_fwd, py::arg("ids"), py::arg("word"), py::arg("pos"), py::arg("gamma"), py::arg("beta"),
+        py::arg("y"), py::arg("mean"), py::arg("rstd"), py::arg("S"), py::arg("eps"), py::arg("seed"), py::arg("site"),
+        py::arg("thr"), py::arg("dscale"), py::arg("row_map") = py::none(), py::arg("ln_epoch") = py::none());
+  m.def("gemm_ln_set_diag", [](int64_t d) { fd_gemm_ln_set_diag((int)d); });
   m.def("emb_bwd", &emb_bwd);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("colsum_bf16_batched", &colsum_bf16_batched);
@@ -1115,7 +1154,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("labels"), py::arg("logits"),
         py::arg("loss"), py::arg("dlogits"), py::arg("row_loss"), py::arg("cls"), py::arg("tlogits") = py::none(),
         py::arg("kd_T") = 1.0, py::arg("kd_alpha") = 1.0);
-  m.def("head_bwd", &head_bwd);
+  m.def("head_bwd", &head_bwd, py::arg("hidden"), py::arg("B"), py::arg("S"), py::arg("W"), py::arg("seed"),
+        py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("dlogits"), py::arg("dW"), py::arg("db"),
+        py::arg("dhidden"), py::arg("accumulate"), py::arg("cls") = py::none(), py::arg("gscale") = py::none(),
+        py::arg("own") = py::none());
   m.def("eval_metrics", &eval_metrics);
   m.def("adam", &adam);
   m.def("step_inc", &step_inc);

@@ -12,6 +12,14 @@
 // group, so the framework's collectives do not depend on torch's NCCL wrapper
 // (its watchdog, work objects, stream bookkeeping).
 //
+// Failure semantics (the reference bounds every socket with a 300 s timeout and retries,
+// client1.py:22,280,323, server.py:10,92-112): a collective whose peer died never completes on
+// its own.  fd_comm_wait polls the stream the collective was issued on together with
+// ncclCommGetAsyncError, so the host learns of an RCCL-reported failure (a peer's broken
+// connection) or of a timeout instead of blocking forever; the caller then aborts the
+// communicator (fd_comm_abort = ncclCommAbort: it tears down the proxy threads and unblocks the
+// kernels of the pending collective) and raises.
+//
 // RCCL itself is bound at run time (fd_comm_load): the process already holds
 // the librccl that torch was built against, and linking a second copy from
 // /opt/rocm would put two RCCL instances (two sets of proxy threads / IPC
@@ -20,9 +28,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 
 namespace {
 
@@ -39,6 +49,8 @@ struct Rccl {
   decltype(&ncclGroupStart) GroupStart = nullptr;
   decltype(&ncclGroupEnd) GroupEnd = nullptr;
   decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+  decltype(&ncclCommAbort) CommAbort = nullptr;
 } R;
 
 #define ncclGetUniqueId R.GetUniqueId
@@ -50,6 +62,8 @@ struct Rccl {
 #define ncclGroupStart R.GroupStart
 #define ncclGroupEnd R.GroupEnd
 #define ncclGetErrorString R.GetErrorString
+#define ncclCommGetAsyncError R.CommGetAsyncError
+#define ncclCommAbort R.CommAbort
 
 int fail(const char* what, ncclResult_t r) {
   g_err = std::string(what) + ": " + ncclGetErrorString(r);
@@ -90,8 +104,10 @@ int fd_comm_load(const char* path) {
   R.GroupStart = (decltype(R.GroupStart))sym("ncclGroupStart");
   R.GroupEnd = (decltype(R.GroupEnd))sym("ncclGroupEnd");
   R.GetErrorString = (decltype(R.GetErrorString))sym("ncclGetErrorString");
+  R.CommGetAsyncError = (decltype(R.CommGetAsyncError))sym("ncclCommGetAsyncError");
+  R.CommAbort = (decltype(R.CommAbort))sym("ncclCommAbort");
   if (!R.GetUniqueId || !R.CommInitRank || !R.CommDestroy || !R.AllReduce || !R.Broadcast || !R.AllGather ||
-      !R.GroupStart || !R.GroupEnd || !R.GetErrorString) {
+      !R.GroupStart || !R.GroupEnd || !R.GetErrorString || !R.CommGetAsyncError || !R.CommAbort) {
     g_err = std::string("missing RCCL symbols in ") + path;
     R = Rccl{};
     return 2;
@@ -123,6 +139,54 @@ int fd_comm_init(void** comm, int nranks, int rank, const void* id_bytes) {
   if (r != ncclSuccess) return fail("ncclCommInitRank", r);
   *comm = c;
   return 0;
+}
+
+// The communicator's asynchronous error state (ncclCommGetAsyncError): 0 = healthy,
+// otherwise the ncclResult_t RCCL recorded (the message is left in fd_comm_last_error).
+int fd_comm_async_error(void* comm) {
+  if (!R.lib || !comm) { g_err = "communicator not initialised"; return 1; }
+  ncclResult_t async = ncclSuccess;
+  const ncclResult_t r = ncclCommGetAsyncError((ncclComm_t)comm, &async);
+  if (r != ncclSuccess) return fail("ncclCommGetAsyncError", r);
+  if (async != ncclSuccess && async != ncclInProgress) return fail("RCCL asynchronous error", async);
+  return 0;
+}
+
+// Wait until everything issued on `st` (the collective last among it) has completed, checking the
+// communicator's async error every poll.  Returns 0 when done, FD_COMM_TIMEOUT after timeout_ms,
+// or the RCCL error code; a HIP error of the stream returns FD_COMM_HIP_ERROR.  Never aborts by
+// itself: the caller decides (fd_comm_abort) -- the stream's pending work then stays queued.
+#define FD_COMM_TIMEOUT 1001
+#define FD_COMM_HIP_ERROR 1002
+int fd_comm_wait(void* comm, hipStream_t st, long long timeout_ms) {
+  const auto t0 = std::chrono::steady_clock::now();
+  int sleep_us = 20;
+  for (;;) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) {
+      g_err = std::string("hipStreamQuery: ") + hipGetErrorString(q);
+      return FD_COMM_HIP_ERROR;
+    }
+    const int a = fd_comm_async_error(comm);
+    if (a) return a;
+    const long long ms =
+        std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_ms >= 0 && ms >= timeout_ms) {
+      g_err = "collective did not complete within " + std::to_string(timeout_ms) + " ms (peer lost?)";
+      return FD_COMM_TIMEOUT;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
+    if (sleep_us < 2000) sleep_us *= 2;
+  }
+}
+
+// ncclCommAbort: frees the communicator without the collective handshake of ncclCommDestroy
+// (which would wait for the dead peer) and makes its pending kernels return.
+int fd_comm_abort(void* comm) {
+  if (!R.lib || !comm) return 0;
+  const ncclResult_t r = ncclCommAbort((ncclComm_t)comm);
+  return r == ncclSuccess ? 0 : fail("ncclCommAbort", r);
 }
 
 int fd_comm_destroy(void* comm) {

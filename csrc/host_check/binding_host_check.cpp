@@ -149,7 +149,7 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   hc::span(ln->mean, (long long)M * 4, "gemm_ln mean");
   hc::span(ln->rstd, (long long)M * 4, "gemm_ln rstd");
   hc::span(ln->stats, tm * (N / 64) * 2 * bm * 8, "gemm_ln stats");
-  hc::span(ln->cnt, 2 * 4, "gemm_ln cnt");
+  hc::span(ln->cnt, 4, "gemm_ln cnt");
   hc::span(ln->err, 4, "gemm_ln err");
   if (bwd) {
     hc::span(ln->z, mn * 2, "gemm_ln z");
@@ -190,6 +190,9 @@ int fd_comm_unique_id_bytes() { return 128; }
 int fd_comm_get_unique_id(void*) { return 0; }
 int fd_comm_init(void**, int, int, const void*) { return 0; }
 int fd_comm_destroy(void*) { return 0; }
+int fd_comm_async_error(void*) { return 0; }
+int fd_comm_wait(void*, hipStream_t, long long) { return 0; }
+int fd_comm_abort(void*) { return 0; }
 int fd_comm_allreduce(void*, const void*, void*, long long, int, int, hipStream_t) { return 0; }
 int fd_comm_broadcast(void*, void*, long long, int, int, hipStream_t) { return 0; }
 int fd_comm_allgather(void*, const void*, void*, long long, int, hipStream_t) { return 0; }
@@ -264,7 +267,11 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
   return 0;
 }
 int fd_emb_fwd(const void*, int, const void*, const void*, const float*, const float*, void*, float*, float*, int, int,
-               int, float, const uint32_t*, uint32_t, uint32_t, float, const int*, hipStream_t) { ++hc::calls; return 0; }
+               int, float, const uint32_t*, uint32_t, uint32_t, float, const int*, int* ln_epoch, hipStream_t) {
+  ++hc::calls;
+  hc::opt_span(ln_epoch, 4, "emb ln_epoch");
+  return 0;
+}
 int fd_emb_bwd(const void*, const void*, int, const long long*, const long long*, const void*, const void*,
                const float*, const float*, const float*, float*, float*, float*, float*, float*, float*, int, int, int,
                int, int, int, const uint32_t*, uint32_t, uint32_t, float, int, unsigned char*, unsigned char*,
@@ -289,7 +296,9 @@ int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const lon
   return 0;
 }
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
-            int* cu, long long* ids_packed, int* step, uint32_t* seed, long long* cls_rows, hipStream_t) {
+            int* cu, long long* ids_packed, int* step, uint32_t* seed, long long* cls_rows, int* cls_rmap,
+            hipStream_t) {
+  hc::opt_span(cls_rmap, (long long)B * 4, "pack cls_rmap");
   ++hc::calls;
   hc::opt_span(cls_rows, (long long)B * 8, "pack cls_rows");
   hc::opt_span(step, 4, "pack step");
@@ -340,8 +349,9 @@ int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const f
 }
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed, uint32_t, uint32_t,
                 float, const float* dlogits, float* dW, float* db, void* dhidden, int, const int* cls, int T,
-                const float* gscale, hipStream_t) {
+                const float* gscale, const int* own, hipStream_t) {
   ++hc::calls;
+  hc::opt_span(own, (B + 1LL) * 4, "head bwd own");
   hc::span(hidden, (long long)T * D * 2, "head bwd hidden");
   hc::span(dhidden, (long long)T * D * 2, "head bwd dhidden");
   hc::span(W, 2LL * D * 4, "head bwd W");
@@ -579,22 +589,24 @@ int main() {
     auto stats = T_({2 * (Tn + 128) * (D / 64)}, i64), cnt = T_({2}, i32), err = T_({1}, i32);
     auto cp = T_({((Tn + 63) / 64) * 3 * D}, f32);
     expect_ok("gemm_ln fwd", [&] { gemm_ln(false, a, wt, y, bias, r, ga, be, mean, rstd, z, none, none, stats, cnt, err,
-                                           1e-12, seed, 17, 429496730, 1.1, rm, -1); });
+                                           1e-12, seed, 17, 429496730, 1.1, rm, -1, 0); });
     expect_ok("gemm_ln bwd", [&] { gemm_ln(true, a, wt, dz, none, r, ga, none, mean, rstd, z, dx, cp, stats, cnt, err,
-                                           1e-12, seed, 17, 429496730, 1.1, rm, -1); });
+                                           1e-12, seed, 17, 429496730, 1.1, rm, -1, 0); });
     expect_reject("gemm_ln bwd without z", [&] { gemm_ln(true, a, wt, dz, none, r, ga, none, mean, rstd, none, dx, cp,
-                                                         stats, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1); });
+                                                         stats, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1, 0); });
     expect_reject("gemm_ln bwd dropout without dx", [&] {
       gemm_ln(true, a, wt, dz, none, r, ga, none, mean, rstd, z, none, cp, stats, cnt, err, 1e-12, seed, 17, 429496730,
-              1.1, rm, -1); });
+              1.1, rm, -1, 0); });
     auto stats_small = T_({100}, i64);
     expect_reject("gemm_ln stats size", [&] { gemm_ln(false, a, wt, y, bias, r, ga, be, mean, rstd, z, none, none,
-                                                      stats_small, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1); });
+                                                      stats_small, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1, 0); });
     expect_reject("gemm_ln fwd without beta", [&] { gemm_ln(false, a, wt, y, bias, r, ga, none, mean, rstd, z, none,
-                                                            none, stats, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1); });
+                                                            none, stats, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1, 0); });
+    expect_reject("gemm_ln xsite range", [&] { gemm_ln(false, a, wt, y, bias, r, ga, be, mean, rstd, z, none, none,
+                                                       stats, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1, 128); });
     auto cp_small = T_({3 * D}, f32);
     expect_reject("gemm_ln colpart size", [&] { gemm_ln(true, a, wt, dz, none, r, ga, none, mean, rstd, z, dx, cp_small,
-                                                        stats, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1); });
+                                                        stats, cnt, err, 1e-12, seed, 17, 0, 1.0, none, -1, 0); });
   }
   // ---- head (+ fused distillation loss)
   {
@@ -611,10 +623,10 @@ int main() {
     expect_reject("head kd T <= 0", [&] { head_fwd(hid, B, S, W, bias, seed, 2, 0, 1.0, lab, logits, loss, dlog, rl,
                                                    none, tl, 0.0, 0.5); });
     auto dW = T_({2, D}, f32), db = T_({2}, f32), dh = T_({B * S, D}, bf);
-    expect_ok("head bwd", [&] { head_bwd(hid, B, S, W, seed, 2, 0, 1.0, dlog, dW, db, dh, false, none, none); });
+    expect_ok("head bwd", [&] { head_bwd(hid, B, S, W, seed, 2, 0, 1.0, dlog, dW, db, dh, false, none, none, none); });
     auto hid_small = T_({B * S - 1, D}, bf);
     expect_reject("head bwd hidden size", [&] { head_bwd(hid_small, B, S, W, seed, 2, 0, 1.0, dlog, dW, db, hid_small,
-                                                         false, none, none); });
+                                                         false, none, none, none); });
   }
   // ---- Adam over an arena with a run table (the fused-step remainder)
   {

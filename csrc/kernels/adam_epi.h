@@ -35,6 +35,8 @@ struct FdDwProb {
   int K;              // rows of A and B (0: the launch's K)
 };
 
+#define FD_LN_XSITES 128
+
 // LayerNorm fused into an N = hidden GEMM (gemm.hip gemm_ln_kernel).  The column tiles of one
 // row block exchange per-row partial statistics through tagged granules in `stats`, so every
 // tile normalises its own slice from its accumulators.
@@ -54,8 +56,12 @@ struct FdLnEpi {
   float* colpart;         // backward: [tiles_m][3][N]
   uint64_t* stats;        // [tiles_m][tiles_n][2][BM] {tag, value} granules (forward mean / M2,
                           // backward s1 / s2 per row); zeroed once
-  int* cnt;               // [2]: launch epoch, done-block counter (zeroed once, self-maintained)
-  int* err;               // set nonzero if a row-block rendezvous timed out
+  int* cnt;               // [1]: exchange epoch, advanced once per model forward (norm.hip
+                          // emb_fwd_kernel) or by the caller (ops/kernels.py ln_epoch_advance)
+  int* err;               // set nonzero if a row-block rendezvous timed out (fatal: the host
+                          // raises at its next check, ops/kernels.py check_ln_error)
+  uint32_t xsite;         // exchange call site, unique per LN launch between two epoch advances
+                          // (< FD_LN_XSITES): granule tag = epoch * FD_LN_XSITES + xsite + 1
   const uint32_t* seed_ptr;
   uint32_t site, thr;     // dropout (thr == 0: none), hashed like norm.hip's ln kernels
   float dscale;

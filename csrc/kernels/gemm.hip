@@ -502,11 +502,15 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
 // L2s; no arrival counter): each statistic is an 8-byte granule {tag, value} written by ONE
 // agent-scope relaxed atomic store (global store with the coherence bit, not kept in the XCD's
 // L2), and the readers poll the granules themselves with agent-scope atomic loads until every
-// tag is this launch's -- the data is the flag, so there is nothing to order.  The tag is the
-// launch epoch cnt[0] + 1, read at the start; the last block to finish (done counter cnt[1])
-// advances cnt[0], so stale granules of earlier launches never match (stats start zeroed).
+// tag is this launch's -- the data is the flag, so there is nothing to order.  The tag is
+// epoch * FD_LN_XSITES + xsite + 1: the epoch is advanced once per model forward by an earlier
+// launch (norm.hip emb_fwd_kernel) and every LN launch of that forward / backward passes its own
+// call site, so stale granules of earlier launches never match and no launch needs a "last
+// block" fan-in to advance anything (the old per-launch done counter cost ~2 us per call).
 // Progress: a row block's tiles are consecutive logical tiles, walked in order per XCD
-// (xcd_remap); the poll is bounded regardless (ln.err flags a timeout, no hang).
+// (xcd_remap), and the grid is one resident round.  The poll is bounded by the wall clock
+// (0.25 s, never reached in a healthy launch): a timeout sets ln.err, which the host treats as
+// fatal (ops/kernels.py check_ln_error) -- the tile's statistics are then wrong.
 DEV void st_gran(uint64_t* p, uint32_t tag, float v) {
   __hip_atomic_store(p, ((uint64_t)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -518,15 +522,6 @@ DEV float row_sum(float v) {  // butterfly over the CPR lanes of a row: identica
 #pragma unroll
   for (int o = 1; o < CPR; o <<= 1) v += __shfl_xor(v, o, 64);
   return v;
-}
-
-// The last block of the launch to get here advances the epoch for the next launch.
-DEV void ln_done(const FdLnEpi& L, uint32_t tag, int tid) {
-  if (tid == 0 &&
-      __hip_atomic_fetch_add(L.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-    __hip_atomic_store(L.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(L.cnt, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 DEV void load8f(const float* p, float (&f)[8]) {
@@ -561,7 +556,8 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
   const int m0 = tm * BM, n0 = tn * BN, tiles_n = p.N / BN, N = p.N;
   const int cc = tid % CPR, n = n0 + 8 * cc;
   // operands of the element math, issued before the tile is parked so their latency overlaps it
-  const uint32_t tag = (uint32_t)__hip_atomic_load(L.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const uint32_t tag = (uint32_t)__hip_atomic_load(L.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * FD_LN_XSITES +
+                       L.xsite + 1u;
   uint4 res_v[IT], z_v[IT];
   float mrow[IT], rrow[IT];
   int hrow_v[IT];
@@ -685,7 +681,9 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
   // granules until every tag is this launch's (wave-uniform exit)
   float2 st[IT][LN_MAXK];
   {
-    int spins = 0;
+    // diag 64 (tests only): wait for a tag no launch writes -> the timeout path
+    const uint32_t want = (p.diag & 64) ? tag + 1u : tag;
+    const uint64_t t0 = wall_clock64();  // 100 MHz
     for (;;) {
       bool ok = true;
 #pragma unroll
@@ -697,7 +695,7 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
           if (t < tiles_n) {
             const uint64_t a = ld_gran(stats + (size_t)t * 2 * BM + r);
             const uint64_t b = ld_gran(stats + (size_t)(t * 2 + 1) * BM + r);
-            ok &= (uint32_t)(a >> 32) == tag && (uint32_t)(b >> 32) == tag;
+            ok &= (uint32_t)(a >> 32) == want && (uint32_t)(b >> 32) == want;
             st[it][i] = make_float2(gran_val(a), gran_val(b));
           } else {
             st[it][i] = make_float2(0.f, 0.f);
@@ -706,7 +704,7 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
       }
       if (__all(ok) || (p.diag & 16)) break;  // (diag 16: timing only -- no wait, wrong statistics)
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1 << 20)) {  // ~0.1 s: never in a healthy launch
+      if (wall_clock64() - t0 > 25000000ull) {  // 0.25 s: never in a healthy launch
         if (lane == 0) __hip_atomic_fetch_or(L.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -760,7 +758,6 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
       }
     }
   }
-  ln_done(L, tag, tid);
   if constexpr (BWD) {
     __syncthreads();  // slots 0 / 1 have been flushed
     park(cd, 0);
@@ -1304,6 +1301,7 @@ bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st, const Ge
 // Tuning overrides: per GEMM kind a forced config id / split count (-1 = auto),
 // set from FD_GEMM_CFG_{NT,NN,TN} / FD_GEMM_SPLITS or at run time (fd_gemm_set_cfg).
 int g_cfg_override[3] = {-2, -2, -2};
+int g_ln_diag = -1;  // FD_GEMM_LN_DIAG / fd_gemm_ln_set_diag
 int g_splits_override = -2;
 
 int cfg_override(int kind) {
@@ -1747,9 +1745,15 @@ int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* out
 // cfg < 0: FD_GEMM_LN_CFG or 24 (128 x 64, 8 waves, two K tiles per barrier -- the N = 768
 // configuration of the plain GEMM).  Returns the number of row blocks (the colpart rows),
 // or a negative code on an unsupported shape (nothing launched).
+int fd_gemm_ln_set_diag(int diag) {
+  g_ln_diag = diag;
+  return 0;
+}
+
 int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
                const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t st) {
   if (M <= 0 || K % BKT || N % 64 || !ln || !res || (!bwd && !bias)) return -1;
+  if (ln->xsite >= FD_LN_XSITES) return -5;
   int id = cfg;
   if (id < 0) {
     static const int env = [] { const char* e = getenv("FD_GEMM_LN_CFG"); return e ? atoi(e) : -1; }();
@@ -1775,10 +1779,13 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   p.bias = bias; p.res = (const bf16_t*)res; p.ldres = ldres;
   p.k_split = K;
   p.ln = *ln;
-  {
-    static const int diag = [] { const char* e = getenv("FD_GEMM_LN_DIAG"); return e ? atoi(e) : 0; }();
-    p.diag = diag;  // profiling only: 16 = no row-block rendezvous (wrong statistics)
+  if (g_ln_diag < 0) {
+    const char* e = getenv("FD_GEMM_LN_DIAG");
+    g_ln_diag = e ? atoi(e) : 0;
   }
+  // profiling / tests only: 16 = no row-block rendezvous (wrong statistics), 64 = force the
+  // rendezvous timeout (fd_gemm_ln_set_diag; tests/test_fused_ln_gpu.py)
+  p.diag = g_ln_diag;
   const int tiles_m = (M + bm - 1) / bm;
   const dim3 grid(tiles_m * (N / bn));
   auto go = [&](auto kern, int threads) { hipLaunchKernelGGL(kern, grid, dim3(threads), 0, st, p); };

@@ -43,6 +43,11 @@ struct HeadArgs {
   // padded layout, row b*S); rows are clamped to T-1
   const int* cls;
   int T;
+  // packed sequence starts (int32 [B+1], nullable): sequence b is EMPTY (all-zero mask row) when
+  // own[b] == own[b+1]; its [CLS] row is not its own (the next sequence's, or a filler row), so
+  // the backward gives it no hidden-state gradient -- the same in the pruned layout (distinct
+  // rows) as in the packed one (shared rows), ADVICE r2
+  const int* own;
   // knowledge distillation (nullable): teacher logits [B, 2]; the row loss becomes
   // kd_alpha * CE(z, y) + (1 - kd_alpha) * T^2 * KL(softmax(t / T) || softmax(z / T))
   const float* tlogits;
@@ -118,16 +123,19 @@ __global__ __launch_bounds__(64) void head_loss_mean_kernel(const float* row_los
   if (threadIdx.x == 0) loss[0] = s / B;
 }
 
-// Is `row` some sequence's [CLS] row (the rows the compute blocks write)?
+DEV bool empty_seq(const HeadArgs& a, int b) { return a.own && a.own[b] == a.own[b + 1]; }
+
+// Is `row` the [CLS] row of some non-empty sequence (the rows the compute blocks write)?
 DEV bool is_cls_row(const HeadArgs& a, int row) {
   if (!a.cls) return row % a.S == 0 && row / a.S < a.B;
-  int lo = 0, hi = a.B - 1;  // cls = sequence starts: ascending
+  int lo = 0, hi = a.B;  // cls = sequence starts: non-decreasing; first b with cls_row(b) > row
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    if ((int)cls_row(a, mid) < row) lo = mid + 1;
+    if ((int)cls_row(a, mid) <= row) lo = mid + 1;
     else hi = mid;
   }
-  return (int)cls_row(a, lo) == row;
+  const int b = lo - 1;  // the last sequence claiming `row` (duplicates: the later one owns it)
+  return b >= 0 && (int)cls_row(a, b) == row && !empty_seq(a, b);
 }
 
 // Blocks [0, ceil(D/256)): dW / db and the [CLS] rows of dhidden.  Blocks beyond: zero every
@@ -180,7 +188,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
       g1 += d1 * xv;
       // an empty sequence shares its [CLS] row with the next one: the later sequence writes it
       const bool last_owner = b + 1 >= a.B || cls_row(a, b + 1) != row[u];
-      if (live && last_owner) a.dhidden[row[u] * a.D + col] = (bf16_t)f2bf((d0 * w0 + d1 * w1) * sc);
+      if (live && last_owner && !empty_seq(a, b)) a.dhidden[row[u] * a.D + col] = (bf16_t)f2bf((d0 * w0 + d1 * w1) * sc);
     }
   }
   red[0][grp][c] = g0;
@@ -435,10 +443,10 @@ int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const f
 
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
-                int accumulate, const int* cls, int T, const float* gscale, hipStream_t st) {
+                int accumulate, const int* cls, int T, const float* gscale, const int* own, hipStream_t st) {
   HeadArgs a{};
   a.gscale = gscale;
-  a.cls = cls; a.T = T;
+  a.cls = cls; a.T = T; a.own = own;
   a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.dlog_in = dlogits;
   a.dW = dW; a.db = db; a.dhidden = (bf16_t*)dhidden; a.accumulate = accumulate;

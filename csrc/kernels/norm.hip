@@ -272,6 +272,10 @@ struct EmbArgs {
   // packed rows (unpadded step): row -> padded row (position = padded row % S, dropout
   // hashed by the padded row; -1 = bucket filler, treated as padded row 0)
   const int* row_map;
+  // forward only (nullable): the LayerNorm-fused GEMMs' exchange epoch (gemm.hip ln_epilogue),
+  // advanced once per model forward here -- the first kernel of every forward -- so the fused
+  // LayerNorm launches of this forward / backward tag their row statistics with a fresh epoch
+  int* ln_epoch;
 };
 
 DEV int padded_row(const EmbArgs& a, int row) { return a.row_map ? max(a.row_map[row], 0) : row; }
@@ -284,6 +288,7 @@ template <int NC>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbArgs a) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (a.ln_epoch && blockIdx.x == 0 && threadIdx.x == 0) a.ln_epoch[0] += 1;  // (read by later launches only)
   if (row >= a.T) return;
   const int D = a.D;
   const long id = load_id(a, row);
@@ -781,9 +786,10 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const int* row_map,
-               hipStream_t st) {
+               int* ln_epoch, hipStream_t st) {
   if (D != 768) return 1;
   EmbArgs a{};
+  a.ln_epoch = ln_epoch;
   a.ids = ids; a.ids64 = ids64; a.word = (const bf16_t*)word; a.pos = (const bf16_t*)pos; a.gamma = gamma;
   a.beta = beta; a.y = (bf16_t*)y; a.mean = mean; a.rstd = rstd; a.T = T; a.S = S; a.D = D; a.eps = eps;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.row_map = row_map;

@@ -16,7 +16,7 @@ namespace {
 template <typename M, typename I>
 __global__ __launch_bounds__(1024) void pack_kernel(const M* mask, const I* ids, int n, int S, int B, int rows,
                                                     int* row_map, int* cu, long long* ids_packed, int* step,
-                                                    uint32_t* seed, long long* cls_rows) {
+                                                    uint32_t* seed, long long* cls_rows, int* cls_rmap) {
   __shared__ int wsum[16];
   __shared__ int carry_s;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -75,13 +75,23 @@ __global__ __launch_bounds__(1024) void pack_kernel(const M* mask, const I* ids,
     row_map[r] = -1;
     ids_packed[r] = id0;
   }
+  if (cls_rmap) {
+    // pruned last block: the padded row whose dropout masks the kept row of sequence b uses --
+    // that of packed row cu[b] (b * S, or, for an empty sequence, the row its [CLS] row belongs
+    // to), exactly what the unpruned LayerNorms hash it by; filler rows act as padded row 0
+    __syncthreads();  // row_map / cu of this block are written
+    for (int b = tid; b < B; b += 1024) {
+      const int r = cu[b];
+      cls_rmap[b] = r < total && r < rows ? max(row_map[r], 0) : 0;
+    }
+  }
 }
 
 // Pruned last block (ops/functional.py LayerFn._forward_pruned): two [rows][D] bf16 matrices
 // gathered at the same row list in one launch (out_i[k] = in_i[idx[k]]), and the reverse: two
 // [n][D] matrices scattered into zero-filled [T][D] ones (out_i[idx[k]] = in_i[k] for k < nsrc,
 // every other row 0).  One thread moves 16 bytes; the scatter finds a row's source by binary
-// search over the ascending idx[0, nsrc) (the [CLS] rows), so each output row is written once.
+// search over the non-decreasing idx[0, nsrc) (the [CLS] rows), so each output row is written once.
 __global__ __launch_bounds__(256) void gather_rows2_kernel(const uint4* a, const uint4* b, uint4* oa, uint4* ob,
                                                            const long long* idx, int n, int d16) {
   const long long i = blockIdx.x * 256ll + threadIdx.x;
@@ -104,15 +114,19 @@ __global__ __launch_bounds__(256) void scatter_rows2_kernel(const uint4* a, cons
   const long long i = blockIdx.x * 256ll + threadIdx.x;
   if (i >= (long long)T * d16) return;
   const long long r = i / d16, c = i - r * d16;
-  int lo = 0, hi = nsrc;  // first k with idx[k] >= r
+  // LAST k with idx[k] == r: an empty sequence (all-zero mask row) repeats its successor's [CLS]
+  // row cu[b] == cu[b+1], and -- as in head_bwd's last-owner rule -- the later sequence (the one
+  // that actually owns the row) wins
+  int lo = 0, hi = nsrc;  // first k with idx[k] > r
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    if ((lds ? sidx[mid] : idx[mid]) < r) lo = mid + 1; else hi = mid;
+    if ((lds ? sidx[mid] : idx[mid]) <= r) lo = mid + 1; else hi = mid;
   }
-  const bool hit = lo < nsrc && (lds ? sidx[lo] : idx[lo]) == r;
+  const int k = lo - 1;
+  const bool hit = k >= 0 && (lds ? sidx[k] : idx[k]) == r;
   const uint4 z = make_uint4(0, 0, 0, 0);
-  oa[i] = hit ? a[(long long)lo * d16 + c] : z;
-  ob[i] = hit ? b[(long long)lo * d16 + c] : z;
+  oa[i] = hit ? a[(long long)k * d16 + c] : z;
+  ob[i] = hit ? b[(long long)k * d16 + c] : z;
 }
 
 }  // namespace
@@ -140,12 +154,13 @@ int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const lon
 
 // mask_bytes / ids_bytes: 8 (int64) or 4 (int32) / 1 (uint8 mask).  n = B * S <= 1 << 20.
 int fd_pack(const void* mask, int mask_bytes, const void* ids, int ids_bytes, int B, int S, int rows, int* row_map,
-            int* cu, long long* ids_packed, int* step, uint32_t* seed, long long* cls_rows, hipStream_t st) {
+            int* cu, long long* ids_packed, int* step, uint32_t* seed, long long* cls_rows, int* cls_rmap,
+            hipStream_t st) {
   const int n = B * S;
   if (B <= 0 || S <= 0 || rows <= 0 || n > (1 << 20)) return 1;
 #define FD_PACK(MT, IT)                                                                                        \
   hipLaunchKernelGGL((pack_kernel<MT, IT>), dim3(1), dim3(1024), 0, st, (const MT*)mask, (const IT*)ids, n, S, B, \
-                     rows, row_map, cu, ids_packed, step, seed, cls_rows)
+                     rows, row_map, cu, ids_packed, step, seed, cls_rows, cls_rmap)
   if (mask_bytes == 8 && ids_bytes == 8) FD_PACK(long long, long long);
   else if (mask_bytes == 8 && ids_bytes == 4) FD_PACK(long long, int);
   else if (mask_bytes == 4 && ids_bytes == 8) FD_PACK(int, long long);

@@ -141,21 +141,22 @@ def _bench(argv):
 
 
 def _scaling(argv):
+    """bench.py at each GPU count, back to back (bench.py starts its own ranks for N > 1, on a
+    free rendezvous port); unknown arguments are passed to every bench run."""
     ap = argparse.ArgumentParser(prog="scaling")
     ap.add_argument("--gpus", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--out", default="scaling.json")
-    ns = ap.parse_args(argv)
+    ns, extra = ap.parse_known_args(argv)
     results = []
-    for i, n in enumerate(int(x) for x in ns.gpus.split(",")):
-        base = [os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", str(ns.steps), "--warmup", str(ns.warmup)]
-        if n == 1:
-            cmd = [sys.executable] + base
-        else:
-            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-                   "--master-addr", "127.0.0.1", "--master-port", str(29600 + i)] + base
-        out = subprocess.run(cmd, capture_output=True, text=True)
+    for n in (int(x) for x in ns.gpus.split(",")):
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", str(ns.steps),
+               "--warmup", str(ns.warmup)] + extra
+        env = dict(os.environ)
+        for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):  # bench.py launches its own ranks
+            env.pop(k, None)
+        out = subprocess.run(cmd, capture_output=True, text=True, env=env)
         line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
         if not line:
             print(out.stdout[-2000:], out.stderr[-2000:], file=sys.stderr)

@@ -56,6 +56,8 @@ def evaluate_model(model, loader, criterion=None, device=None, log=None, name: s
             nb += 1
         loss_sum = acc.item()
         correct, tp, fp, fn, tn = counts.tolist()
+        if packed and getattr(model, "fuse_ln", False):
+            K.check_ln_error(dev, model.config.dim)  # a timed-out LayerNorm rendezvous is fatal
     else:
         loss_sum = 0.0
         correct = tp = fp = fn = tn = 0

@@ -95,6 +95,14 @@ def make_kd_step_fn(student, teacher, optimizer, temperature: float = 2.0, alpha
     return step
 
 
+def _check_native(model):
+    """Fatal-error flags of the HIP kernels (the fused LayerNorm rendezvous timeout), read at the
+    epoch's one host sync."""
+    if getattr(model, "impl", None) == "hip" and getattr(model, "fuse_ln", False):
+        from ..ops import kernels as K
+        K.check_ln_error(model.device, model.config.dim)
+
+
 def train_model(model, train_loader, criterion=None, optimizer=None, num_epochs: int = 3, device=None,
                 log=None, use_graph: bool = True, max_steps: Optional[int] = None,
                 on_epoch: Optional[Callable] = None, teacher=None, kd_temperature: float = 2.0,
@@ -142,6 +150,7 @@ def train_model(model, train_loader, criterion=None, optimizer=None, num_epochs:
             import torch.distributed as dist
             dist.all_reduce(loss_sum, group=grad_sync.group)
         avg = loss_sum.item() / max(nb, 1)  # the one sync per epoch
+        _check_native(model)
         dt = time.perf_counter() - te
         epoch_losses.append(avg)
         if log:

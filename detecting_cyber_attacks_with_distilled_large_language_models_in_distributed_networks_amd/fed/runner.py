@@ -133,16 +133,31 @@ class FederatedClient:
         writes right after FedAvg and before any client records the round in its fed_state.
         Rank 0 can tag round r+1 only after every client has finished round r, so after a crash
         the tag is the last round whose aggregate exists, whatever each client's own sidecar
-        says.  The tag is MIN-reduced over the world so every rank agrees even if one cannot
-        see the file; rank 0 loads the aggregate and broadcasts it.  A client's own
-        ``clientN_model.pth`` is never the resume point of a collective run: after a crash
-        inside a round it holds that round's LOCAL model (fed/runner.py run_round saves it
-        before FedAvg).  Single-process runs with no sidecar keep the reference behaviour of
-        loading it (client1.py:375-377: re-running the script is the next round)."""
+        says.  Rank 0 -- the rank that loads and broadcasts the aggregate -- decides, and its
+        round is broadcast, so a rank that cannot see the file (a per-node out_dir) follows
+        rank 0 instead of restarting the world from scratch.  An out_dir written before the
+        tag existed (aggregate on disk, no tag) resumes from rank 0's sidecar
+        ``completed_rounds``, with a warning.  A client's own ``clientN_model.pth`` is never the
+        resume point of a collective run: after a crash inside a round it holds that round's
+        LOCAL model (fed/runner.py run_round saves it before FedAvg).  Single-process runs with
+        no sidecar keep the reference behaviour of loading it (client1.py:375-377: re-running
+        the script is the next round)."""
         cfg, log = self.cfg, self.log
         st = ck.load_fed_state(cfg.out_dir, self.client_id)
-        tagged = ck.load_global_round(cfg.out_dir)
-        start = int(comm.all_reduce_min(float(tagged))) if self.di.distributed else tagged
+        start = 0
+        if self.di.is_main or not self.di.distributed:
+            start = ck.load_global_round(cfg.out_dir)
+            legacy = int((st or {}).get("completed_rounds", 0))
+            if start == 0 and os.path.exists(ck.global_ckpt_path(cfg.out_dir)):
+                if legacy > 0:
+                    log.info(f"[WARN] {ck.global_ckpt_path(cfg.out_dir)} has no round tag (written by an older "
+                             f"version): resuming from the client sidecar's {legacy} completed round(s)")
+                    start = legacy
+                else:
+                    log.info(f"[WARN] {ck.global_ckpt_path(cfg.out_dir)} has no round tag and no sidecar "
+                             f"records a completed round: starting from round 1")
+        if self.di.distributed:
+            start = int(comm.broadcast_float(float(start), src=0))
         if start > 0:
             path = ck.global_ckpt_path(cfg.out_dir)
             if self.di.is_main or not self.di.distributed:

@@ -55,6 +55,15 @@ LAYER_KEYS = [  # HF registration (= state_dict) order inside a TransformerBlock
 ]
 
 
+def gpu_shared() -> bool:
+    """Whether this process shares its GPU with other ranks of the job (more local ranks than
+    visible GPUs, e.g. ``FEDDDOS_BACKEND=gloo`` clients on a 1-GPU box)."""
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
+    if local <= 1 or not torch.cuda.is_available():
+        return False
+    return local > torch.cuda.device_count()
+
+
 def _layer_shapes(cfg: DistilBertConfig) -> Dict[str, Tuple[int, ...]]:
     D, F = cfg.dim, cfg.hidden_dim
     return {
@@ -271,7 +280,10 @@ class DDoSClassifier(nn.Module):
         self.remat_gelu = os.environ.get("FD_REMAT_GELU", "1") != "0"
         # HIP path: LayerNorm fused into the N = 768 GEMMs (RunCtx.fuse_ln; FD_FUSE_LN=0: the
         # separate LN kernels).  Hidden sizes the fused epilogue does not cover fall back.
-        self.fuse_ln = os.environ.get("FD_FUSE_LN", "1") != "0"
+        # Its row blocks wait on each other's statistics, so every tile of a launch must be resident
+        # at once: off when other processes share this GPU (e.g. several gloo clients on one card),
+        # whose kernels could hold CUs through a rendezvous (a timeout is fatal: check_ln_error).
+        self.fuse_ln = os.environ.get("FD_FUSE_LN", "1") != "0" and not gpu_shared()
         # HIP path: build the per-step W^T copies on a side stream concurrently with the forward.
         # Measured SLOWER on MI355X (2.48 vs 2.36 ms/step, profiles/r1_ab_transpose_overlap_slower.txt):
         # the memory-bound transposes stretch the concurrent forward GEMMs.  Off by default.
@@ -553,7 +565,8 @@ class DDoSClassifier(nn.Module):
             if len([a for a, _ in incs if a is not None]) > 1 or len([b for _, b in incs if b is not None]) > 1:
                 raise RuntimeError("a counter deferred twice in one forward")
             rc.row_map, rc.cu, ids = K.pack(mask, ids, self.packed_rows(tokens, B, S), step=st_inc, seed=sd_inc,
-                                            cls_rows=plan[4] if plan is not None else None)
+                                            cls_rows=plan[4] if plan is not None else None,
+                                            cls_rmap=plan[5] if plan is not None else None)
         x = EmbeddingFn.apply(token, ids, emb["word"], emb["pos"], emb["ln_w"], emb["ln_b"], emb["sinks"], rc)
         self._setup_prune(rc, plan, len(layers), packed)
         for i, L in enumerate(layers):
@@ -584,8 +597,9 @@ class DDoSClassifier(nn.Module):
             rmap = torch.zeros(Bp, dtype=torch.int32, device=dev)
             rmap[:B] = torch.arange(B, dtype=torch.int32, device=dev) * S
             padded_rows = rmap.to(torch.int64)  # padded layout: sequence b's [CLS] is row b * S
+            # (packed: the packing launch fills the kept rows and their dropout-hash rows)
             cache = (key, rmap, padded_rows, torch.arange(B, dtype=torch.int32, device=dev),
-                     torch.zeros(Bp, dtype=torch.int64, device=dev))
+                     torch.zeros(Bp, dtype=torch.int64, device=dev), torch.zeros(Bp, dtype=torch.int32, device=dev))
             self._prune_cache = cache
         return cache
 
@@ -593,10 +607,12 @@ class DDoSClassifier(nn.Module):
     def _setup_prune(rc, plan, n_layers: int, packed: bool):
         if plan is None:
             return
-        _, rmap, padded_rows, head_rows, packed_rows = plan
-        # packed: rows cu[b] (written by the packing launch); filler rows -> row 0 (a finite row)
+        _, rmap, padded_rows, head_rows, packed_rows, packed_rmap = plan
+        # packed: rows cu[b] and their padded rows (written by the packing launch); filler rows ->
+        # row 0 (a finite row)
         rc.cls_rows = packed_rows if packed else padded_rows
-        rc.cls_rmap, rc.head_rows, rc.prune_idx = rmap, head_rows, n_layers - 1
+        rc.cls_rmap = packed_rmap if packed else rmap
+        rc.head_rows, rc.prune_idx = head_rows, n_layers - 1
 
     def _no_bias(self) -> torch.Tensor:
         """Placeholder key-bias tensor for the varlen path (the kernels do not read it)."""

@@ -138,7 +138,9 @@ class EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, token, ids, word, pos, gamma, beta, sinks, rc: RunCtx):
         p = rc.p_hidden if rc.training else 0.0
-        y, mean, rstd = K.emb_fwd(ids, word, pos, gamma, beta, rc.S, rc.eps, rc.seed, 1, p, rc.row_map)
+        # (the first launch of the forward also starts the fused LayerNorms' exchange epoch)
+        y, mean, rstd = K.emb_fwd(ids, word, pos, gamma, beta, rc.S, rc.eps, rc.seed, 1, p, rc.row_map,
+                                  ln_epoch=K.ln_epoch(ids.device, gamma.numel()) if rc.fuse_ln else None)
         ctx.rc, ctx.sinks, ctx.p = rc, sinks, p
         ctx.tensors = (ids, word, pos, gamma, mean, rstd)
         return y
@@ -188,10 +190,12 @@ class EmbeddingFn(torch.autograd.Function):
         if tt is not None:
             # BERT token-type row 0 is added at every position: d(type0) = sum_s d(pos_s).  The
             # position gradient already holds the running total of an accumulating backward,
-            # so the type row is always re-derived from it (never added to).
+            # so the type row is always re-derived from it (never added to) -- over EVERY
+            # position row: an earlier micro-batch with a longer padded S accumulated into rows
+            # this one does not reach (rows never reached are zero: pos_grad_kernel clears them)
             tt.accumulate()
             g = tt.buf
-            torch.sum(s["pos"].buf[:ctx.rc.S], 0, out=g[0])
+            torch.sum(s["pos"].buf, 0, out=g[0])
             g[1:].zero_()
         if ctx.rc.wgrad is not None:  # join the weight-gradient stream: every grad is final after this node
             torch.cuda.current_stream().wait_stream(ctx.rc.wgrad)
@@ -222,10 +226,10 @@ class LayerFn(torch.autograd.Function):
             # bias + (dropout) + residual + LayerNorm in the N = 768 GEMMs' epilogues; the
             # backward reads the saved bf16 pre-LN sums z1 / z2 instead of ao / f
             h, ao, m1, r1 = K.linear_ln_fwd(cx, L["o_w"], L["o_b"], x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0,
-                                            0.0, keep_z=grad)
+                                            0.0, keep_z=grad, xsite=K.ln_xsite(idx, 0, False))
             g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
             y, f, m2, r2 = K.linear_ln_fwd(g, L["l2_w"], L["l2_b"], h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed,
-                                           ffn_site, p_h, rc.row_map, keep_z=grad)
+                                           ffn_site, p_h, rc.row_map, keep_z=grad, xsite=K.ln_xsite(idx, 1, False))
             if grad:
                 rc.ln2_saved[idx] = (f, m2, r2, L, ffn_site, p_h)
         else:
@@ -257,10 +261,10 @@ class LayerFn(torch.autograd.Function):
         ci, rm = rc.cls_rows, rc.cls_rmap
         cxc, xc = K.gather_rows2(cx, x, ci)
         h, ao, m1, r1 = K.linear_ln_fwd(cxc, L["o_w"], L["o_b"], xc, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0,
-                                        keep_z=grad)
+                                        keep_z=grad, xsite=K.ln_xsite(idx, 0, False))
         g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
         y, f, m2, r2 = K.linear_ln_fwd(g, L["l2_w"], L["l2_b"], h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed,
-                                       ffn_site, p_h, rm, keep_z=grad)
+                                       ffn_site, p_h, rm, keep_z=grad, xsite=K.ln_xsite(idx, 1, False))
         if grad:
             ctx.save_for_backward(x)
             ctx.acts = (qkv, cx, lse, cxc, ao, h, m1, r1, u, None if rc.remat_gelu else g, f, m2, r2)
@@ -296,7 +300,7 @@ class LayerFn(torch.autograd.Function):
             g = g_out
         batch += [(df, g, G["l2_w"].buf, acc), (du, h, G["l1_w"].buf, acc)]
         dz1c, _ = K.linear_dx_ln_bwd(du, wt["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
-                                     G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs)
+                                     G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, xsite=K.ln_xsite(ctx.idx, 0, True))
         dcxc = K.linear_dx(dz1c, L["o_w"], wt=wt["o_w"])
         # the [CLS] rows' gradients back into the full layout (every other row exactly 0)
         dcx, dz1 = K.scatter_rows2(dcxc, dz1c, ci, B, cx.shape[0])
@@ -316,7 +320,7 @@ class LayerFn(torch.autograd.Function):
                 raise RuntimeError("output-LN gradient sinks out of step")
             dx, df_p = K.linear_dx_ln_bwd(dqkv, wt["qkv_w"], dz1, z2p, Lp["ln2_w"], m2p, r2p, Gp["ln2_w"].buf,
                                           Gp["ln2_b"].buf, Gp["l2_b"].buf, rc.seed, site_p, p_p, acc_p[0], rc.row_map,
-                                          jobs)
+                                          jobs, xsite=K.ln_xsite(ctx.idx, 1, True))
             rc.ln2_pending[ctx.idx - 1] = (dx, df_p)
         else:
             dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt["qkv_w"])
@@ -378,7 +382,8 @@ class LayerFn(torch.autograd.Function):
         # sa_layer_norm(out_lin + x): dh = du W1 + dz2, then its LayerNorm backward
         if fused and wt.get("l1_w") is not None:
             dz1, _ = K.linear_dx_ln_bwd(du, wt["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
-                                        G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs)
+                                        G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs,
+                                        xsite=K.ln_xsite(ctx.idx, 0, True))
         else:
             dh = K.linear_dx(du, L["l1_w"], res=dz2, wt=wt.get("l1_w"))
             dz1, _ = K.ln_bwd(dh, ao, None if fused else x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
@@ -414,7 +419,7 @@ class LayerFn(torch.autograd.Function):
             acc_p = acc_p[0]
             dx, df_p = K.linear_dx_ln_bwd(dqkv, wt["qkv_w"], dz1, z2p, Lp["ln2_w"], m2p, r2p, Gp["ln2_w"].buf,
                                           Gp["ln2_b"].buf, Gp["l2_b"].buf, rc.seed, site_p, p_p, acc_p, rc.row_map,
-                                          jobs)
+                                          jobs, xsite=K.ln_xsite(ctx.idx, 1, True))
             rc.ln2_pending[ctx.idx - 1] = (dx, df_p)
         else:
             dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt.get("qkv_w"))
@@ -470,5 +475,5 @@ class HeadFn(torch.autograd.Function):
         rc = ctx.rc
         cls = rc.head_rows if rc.head_rows is not None else rc.cu[:-1] if rc.cu is not None else None
         dh = K.head_bwd(hidden, ctx.rc.B, ctx.rc.S, ctx.W, ctx.rc.seed, 2, ctx.p, dlog, s["w"].buf, s["b"].buf, acc,
-                        cls, gscale)
+                        cls, gscale, own=rc.cu)
         return dh, None, None, None, None, None, None

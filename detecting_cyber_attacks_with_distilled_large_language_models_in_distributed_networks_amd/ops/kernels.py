@@ -249,17 +249,18 @@ def colsum_flush(jobs: list):
 
 
 # ------------------------------------------------------------------ unpadded layout
-def pack(mask: torch.Tensor, ids: torch.Tensor, rows: int, step=None, seed=None, cls_rows=None):
+def pack(mask: torch.Tensor, ids: torch.Tensor, rows: int, step=None, seed=None, cls_rows=None, cls_rmap=None):
     """(row_map int32 [rows], cu int32 [B+1], ids_packed int64 [rows]) of a [B, S] batch: the
     real tokens in order (filler rows: row_map -1, id of position 0) -- one launch, which also
     advances the optional int32 counters ``step`` / ``seed`` (what ``step_inc`` would launch) and
-    writes cu[b] as int64 into ``cls_rows[b]`` when given (the pruned last block's row list)."""
+    writes cu[b] as int64 into ``cls_rows[b]`` when given (the pruned last block's row list) and the
+    padded row of packed row cu[b] into ``cls_rmap[b]`` (int32; its dropout-hash rows)."""
     B = mask.shape[0]
     row_map = torch.empty(rows, dtype=torch.int32, device=mask.device)
     cu = torch.empty(B + 1, dtype=torch.int32, device=mask.device)
     ids_packed = torch.empty(rows, dtype=torch.int64, device=mask.device)
     m = mask if mask.dtype != torch.bool else mask.to(torch.uint8)
-    ext().pack(m.contiguous(), ids.contiguous(), row_map, cu, ids_packed, step, seed, cls_rows)
+    ext().pack(m.contiguous(), ids.contiguous(), row_map, cu, ids_packed, step, seed, cls_rows, cls_rmap)
     return row_map, cu, ids_packed
 
 
@@ -341,19 +342,60 @@ LN_STATE_ROWS = 32768  # row capacity of the exchange state (grown if a call nee
 
 def _ln_state(device, M: int, N: int):
     """(stats, cnt, err) of the LayerNorm-fused GEMM (csrc/kernels/gemm.hip gemm_ln_kernel):
-    the tagged row-statistic granules and [launch epoch, done-block counter].  Zeroed once; the
-    kernel keeps them consistent itself (graph replays reuse them)."""
+    the tagged row-statistic granules, the exchange epoch and the timeout flag.  Zeroed once;
+    the epoch is advanced by ``emb_fwd`` (the first launch of every model forward) or by
+    ``ln_epoch_advance`` (graph replays reuse the same state)."""
     key = (_dev_key(device), "ln_state", N)
     st = _WS.get(key)
     rows = max(M, LN_STATE_ROWS)
     if st is None or st[3] < M:
         if st is not None:
             _WS_RETIRED.append(st)
-        st = (torch.zeros(2 * (rows + 128) * (N // 64), dtype=torch.int64, device=device),
-              torch.zeros(2, dtype=torch.int32, device=device),
-              torch.zeros(1, dtype=torch.int32, device=device), rows)
+        # the epoch survives a regrow: a granule tag must never repeat on the same state
+        epoch = st[1] if st is not None else torch.zeros(2, dtype=torch.int32, device=device)
+        err = st[2] if st is not None else torch.zeros(1, dtype=torch.int32, device=device)
+        st = (torch.zeros(2 * (rows + 128) * (N // 64), dtype=torch.int64, device=device), epoch, err, rows)
         _WS[key] = st
     return st[:3]
+
+
+LN_XSITES = 128  # csrc/kernels/adam_epi.h FD_LN_XSITES: exchange call sites per epoch
+
+
+def ln_xsite(layer: int, which: int, backward: bool) -> int:
+    """Exchange call site of a model's LayerNorm-fused launch: forward out_lin / lin2 of block
+    ``layer`` -> 2 * layer + which; the backward ones (lin1 dX / qkv dX) 64 + 2 * layer + which.
+    Unique within one forward + backward (the epoch advances once per forward)."""
+    if not 0 <= layer < 32 or which not in (0, 1):
+        raise ValueError(f"no LayerNorm exchange site for block {layer} / {which}")
+    return (64 if backward else 0) + 2 * layer + which
+
+
+def ln_epoch(device, N: int = D_MODEL) -> torch.Tensor:
+    """The exchange epoch tensor (int32), for ``emb_fwd(ln_epoch=...)``."""
+    return _ln_state(device, 1, N)[1]
+
+
+def ln_epoch_advance(device, N: int = D_MODEL):
+    """Start a new exchange epoch (one small launch): callers of ``linear_ln_fwd`` /
+    ``linear_dx_ln_bwd`` that do not run a model forward (tests, scripts) use this."""
+    ln_epoch(device, N)[:1].add_(1)
+
+
+def check_ln_error(device, N: int = D_MODEL):
+    """Raise if a LayerNorm-fused launch's row-block rendezvous ever timed out: its statistics
+    (and every output after it) are wrong.  One host sync; call it at epoch / eval boundaries."""
+    if ln_error_flag(device, N):
+        raise RuntimeError("a LayerNorm-fused GEMM timed out waiting for its row block's statistics "
+                           "(other work held the GPU's CUs?): the results of this run are invalid; "
+                           "rerun with FD_FUSE_LN=0 if the GPU is shared")
+
+
+def _xsite(device, N, xsite):
+    if xsite is None:  # a standalone call: a fresh epoch of its own
+        ln_epoch_advance(device, N)
+        return 0
+    return int(xsite)
 
 
 LN_MAX_TILES = 256  # csrc/kernels/gemm.hip: the fused grid is one resident round of the CUs
@@ -377,6 +419,11 @@ def ln_fusable(M: int, N: int) -> bool:
     return N % 64 == 0 and N <= 2048 and tiles <= min(LN_MAX_TILES, _cu_count())
 
 
+def ln_set_diag(diag: int):
+    """Tests / profiling only: FD_GEMM_LN_DIAG at run time (64 forces the rendezvous timeout)."""
+    ext().gemm_ln_set_diag(int(diag))
+
+
 def ln_error_flag(device, N: int = 768) -> int:
     """Nonzero if a fused-LN launch's row-block rendezvous ever timed out (never expected)."""
     st = _WS.get((_dev_key(device), "ln_state", N))
@@ -390,10 +437,11 @@ def _dev_key(device) -> str:
     return str(d)
 
 
-def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, keep_z: bool = True):
+def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, keep_z: bool = True, xsite=None):
     """y = LN(dropout(x w^T + b) + res) in ONE launch (the N = hidden GEMM's epilogue does the
     bias, dropout, residual and LayerNorm).  Returns (y, z, mean, rstd): z = the bf16 pre-LN sum
-    (what the backward reads; None with keep_z=False), mean / rstd fp32 per row."""
+    (what the backward reads; None with keep_z=False), mean / rstd fp32 per row.  xsite: the
+    launch's exchange call site (``ln_xsite``) within the current epoch; None = a new epoch."""
     M, N = x.shape[0], w.shape[0]
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
     z = torch.empty_like(y) if keep_z else None
@@ -401,13 +449,14 @@ def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, k
     rstd = torch.empty(M, dtype=torch.float32, device=x.device)
     thr, sc = _drop(p)
     stats, cnt, err = _ln_state(x.device, M, N)
+    xs = _xsite(x.device, N, xsite)
     ext().gemm_ln(False, x, w, y, b, res, gamma, beta, mean, rstd, z, None, None, stats, cnt, err, eps, seed, site,
-                  thr, sc, row_map if thr else None)
+                  thr, sc, row_map if thr else None, -1, xs)
     return y, z, mean, rstd
 
 
 def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False,
-                     row_map=None, jobs: Optional[list] = None):
+                     row_map=None, jobs: Optional[list] = None, xsite=None):
     """LayerNorm backward fused into the dX GEMM that produces its output gradient:
     dy = a wt^T + res, then (dz, dx) of y = LN(dropout(f) + r) from the saved z = dropout(f) + r
     (dz: gradient of the pre-LN sum, i.e. of the residual input r; dx: of f, = dz without dropout).
@@ -419,8 +468,9 @@ def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, see
     key = "ln_colpart" if jobs is None else f"ln_colpart_job{len(jobs)}"
     ws = workspace(a.device, key, ((M + 63) // 64) * 3 * N)
     stats, cnt, err = _ln_state(a.device, M, N)
+    xs = _xsite(a.device, N, xsite)
     nblk = ext().gemm_ln(True, a, wt, dz, None, res, gamma, None, mean, rstd, z, dx, ws, stats, cnt, err, 0.0, seed,
-                         site, thr, sc, row_map if thr else None)
+                         site, thr, sc, row_map if thr else None, -1, xs)
     job = (ws, [dgamma, dbeta, dbias], nblk, 3 * N, N, accumulate)
     if jobs is not None:
         jobs.append(job)
@@ -440,15 +490,17 @@ def group_ids(ids: torch.Tensor):
     return srt, perm
 
 
-def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p, row_map=None):
-    """row_map (int32 [T]): ``ids`` are packed real tokens; positions and dropout follow the padded row."""
+def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p, row_map=None, ln_epoch=None):
+    """row_map (int32 [T]): ``ids`` are packed real tokens; positions and dropout follow the padded row.
+    ln_epoch (``ln_epoch(device)``): also advance the LayerNorm-fused GEMMs' exchange epoch."""
     T = ids.numel()
     D = gamma.numel()
     y = torch.empty(T, D, dtype=torch.bfloat16, device=ids.device)
     mean = torch.empty(T, dtype=torch.float32, device=ids.device)
     rstd = torch.empty(T, dtype=torch.float32, device=ids.device)
     thr, sc = _drop(p)
-    ext().emb_fwd(ids.contiguous(), word, pos, gamma, beta, y, mean, rstd, S, eps, seed, site, thr, sc, row_map)
+    ext().emb_fwd(ids.contiguous(), word, pos, gamma, beta, y, mean, rstd, S, eps, seed, site, thr, sc, row_map,
+                  ln_epoch)
     return y, mean, rstd
 
 
@@ -485,12 +537,14 @@ def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None, cls=None, kd=None):
     return logits, loss, dlogits
 
 
-def head_bwd(hidden, B, S, W, seed, site, p, dlogits, dW, db, accumulate=False, cls=None, gscale=None):
-    """gscale: optional fp32 scalar tensor multiplying dlogits (a fused loss's upstream grad)."""
+def head_bwd(hidden, B, S, W, seed, site, p, dlogits, dW, db, accumulate=False, cls=None, gscale=None, own=None):
+    """gscale: optional fp32 scalar tensor multiplying dlogits (a fused loss's upstream grad).
+    own: packed sequence starts (int32 [B+1]); an empty sequence (own[b] == own[b+1]) gets no
+    hidden-state gradient (its [CLS] row belongs to another sequence)."""
     dhidden = torch.empty_like(hidden)  # the kernel writes every row ([CLS] rows: gradient, others: 0)
     thr, sc = _drop(p)
     ext().head_bwd(hidden, B, S, W, seed, site, thr, sc, dlogits.contiguous(), dW, db, dhidden, accumulate, cls,
-                   gscale)
+                   gscale, own)
     return dhidden
 
 

@@ -110,6 +110,15 @@ def all_reduce_min(x: float) -> float:
     return float(t.item())
 
 
+def broadcast_float(x: float, src: int = 0) -> float:
+    """Rank ``src``'s value on every rank (identity when not distributed)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=info().device)
+    dist.broadcast(t, src=src)
+    return float(t.item())
+
+
 def all_gather_floats(vals: List[float]) -> List[List[float]]:
     """Gather a small per-rank float vector (metrics) to every rank."""
     if not (dist.is_available() and dist.is_initialized()):

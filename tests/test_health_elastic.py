@@ -109,3 +109,44 @@ def test_elastic_restart_after_fedavg_first_round(tmp_path):
     for cid in (1, 2):
         c = torch.load(tmp_path / f"client{cid}_model.pth", weights_only=True)
         assert all(torch.equal(g[k], c[k]) for k in g)
+
+
+def _tiny_client(tmp_path):
+    from importlib import import_module
+    config = import_module(f"{PKG}.config")
+    runner = import_module(f"{PKG}.fed.runner")
+    models = import_module(f"{PKG}.models")
+    cfg = config.FedConfig(out_dir=str(tmp_path), synthetic_rows=400, data_fraction=0.25, max_len=32, epochs=1,
+                           batch_size=8, eval_batch_size=32, plots=False, impl="torch", use_graph=False,
+                           heartbeat_s=0.0, verbose=False)
+    return runner.FederatedClient(cfg, model_config=models.DistilBertConfig(n_layers=1)), models
+
+
+def test_resume_legacy_untagged_out_dir(tmp_path):
+    """an out_dir written before the round tag existed (aggregate on disk, sidecar
+    completed_rounds > 0, no ddos_distilbert_model.json) must resume at the sidecar's round from
+    the aggregate -- not silently restart at round 1 and overwrite it."""
+    import torch
+    from importlib import import_module
+    ck = import_module(f"{PKG}.utils.checkpoint")
+    client, models = _tiny_client(tmp_path)
+    donor = models.DDoSClassifier(config=models.DistilBertConfig(n_layers=1), impl="torch", seed=123)
+    ck.save_model(donor, ck.global_ckpt_path(str(tmp_path)))
+    ck.save_fed_state(str(tmp_path), 1, {"completed_rounds": 1, "history": [{"round": 1}]})
+    assert not os.path.exists(ck.global_tag_path(str(tmp_path)))
+    client.setup()
+    assert client.start_round == 1
+    assert [h["round"] for h in client.history] == [1]
+    got, want = client.model.state_dict(), donor.state_dict()
+    assert all(torch.equal(got[k].cpu(), want[k].cpu()) for k in want)
+
+
+def test_resume_untagged_without_sidecar_starts_fresh(tmp_path):
+    """An aggregate with neither a tag nor a sidecar round: start at round 1 (logged)."""
+    from importlib import import_module
+    ck = import_module(f"{PKG}.utils.checkpoint")
+    client, models = _tiny_client(tmp_path)
+    donor = models.DDoSClassifier(config=models.DistilBertConfig(n_layers=1), impl="torch", seed=123)
+    ck.save_model(donor, ck.global_ckpt_path(str(tmp_path)))
+    client.setup()
+    assert client.start_round == 0

@@ -13,15 +13,22 @@ from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed
 pytestmark = pytest.mark.gpu
 
 
-def _batch(B, S, seed=0):
+def _batch(B, S, seed=0, empty=None):
     # CICIDS2017-like lengths (<= 84 tokens): the full model's LayerNorm-fused GEMMs stay fused
-    # (<= 2,688 rows), so both arms run the same LayerNorm kernels and the forward is bitwise equal
+    # (<= 2,688 rows), so both arms run the same LayerNorm kernels and the forward is bitwise equal.
+    # empty: index of a sequence with an all-zero mask (its [CLS] row cu[b] == cu[b+1] is the next
+    # sequence's; the pruned scatter and the unpruned head backward must both give that row to the
+    # later sequence -- ADVICE r2)
     gen = torch.Generator().manual_seed(seed)
     ids = torch.randint(1000, 2000, (B, S), generator=gen)
     lens = torch.randint(60, 85, (B,), generator=gen)
+    if empty is not None:
+        lens[empty] = 0
     mask = (torch.arange(S)[None] < lens[:, None]).long()
     ids = ids * mask
     ids[:, 0] = 101
+    if empty is not None:
+        ids[empty] = 0
     labels = torch.randint(0, 2, (B,), generator=gen)
     return ids.cuda(), mask.cuda(), labels.cuda(), int(lens.sum())
 
@@ -30,15 +37,15 @@ def _frel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("packed,B", [(True, 32), (False, 16), (True, 20)])
-def test_pruned_last_block_matches_full(packed, B):
+@pytest.mark.parametrize("packed,B,empty", [(True, 32, None), (False, 16, None), (True, 20, None), (True, 20, 3)])
+def test_pruned_last_block_matches_full(packed, B, empty):
     cfg = DistilBertConfig(n_layers=3)
     outs = []
     for prune in (True, False):
         m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=31)
         m.prune_last = prune
         m.train()
-        ids, mask, labels, tokens = _batch(B, 128, seed=800)
+        ids, mask, labels, tokens = _batch(B, 128, seed=800, empty=empty)
         m.zero_grad()
         m.rng.fill_(5)
         loss, logits = m.forward_loss(ids, mask, labels, tokens=tokens if packed else None)

@@ -9,7 +9,10 @@ it).  What the first multi-GPU run must prove before any scaling number means an
   bit-exact mean of two different arenas (server.py:67-79 semantics: unweighted mean), and the
   bf16 compute shadow is refreshed from it;
 * a data-parallel client (2 GPUs, ``GradSync``: per-block async all-reduces from the backward
-  hook + the compacted sparse word-row exchange) gives the full-batch gradient.
+  hook + the compacted sparse word-row exchange) gives the full-batch gradient;
+* a peer that dies inside FedAvg: the survivor's ``NativeComm`` collective does not hang -- its
+  bounded wait (ncclCommGetAsyncError polling) aborts the communicator (ncclCommAbort) and raises
+  ``PeerFailure`` within the timeout (reference: 300 s socket timeouts, server.py:10).
 """
 import os
 import socket
@@ -123,6 +126,30 @@ def _dp_worker(rank, world, port, outdir):
     comm.shutdown()
 
 
+def _abort_worker(rank, world, port, outdir):
+    import time
+    comm, di = _init(rank, world, port)
+    from importlib import import_module
+    rccl = import_module(f"{PKG}.parallel.rccl")
+    health = import_module(f"{PKG}.parallel.health")
+    c = rccl.NativeComm(timeout_s=20.0)
+    x = torch.ones(1 << 24, dtype=torch.float32, device="cuda")
+    c.all_reduce_(x, "sum")  # healthy round first: both ranks present
+    ok = torch.equal(x, torch.full_like(x, 2.0))
+    comm.barrier()
+    if rank == 1:
+        os._exit(0)  # dies "mid-FedAvg": the next collective has one participant only
+    t0 = time.monotonic()
+    try:
+        c.all_reduce_(x, "sum")
+        res = "no failure detected"
+    except health.PeerFailure as e:
+        res = f"raised after {time.monotonic() - t0:.1f}s: {e}"
+    with open(os.path.join(outdir, "abort.txt"), "w") as f:
+        f.write(f"{ok}|{res}|{c.handle}")
+    os._exit(0)  # (the process group's peer is gone: no collective shutdown)
+
+
 def _spawn(fn, *args, world=2, timeout=180):
     port = _free_port()
     ctx = mp.get_context("spawn")
@@ -184,3 +211,12 @@ def test_dp_gradsync_matches_full_batch_over_rccl(tmp_path):
     # replicas hold the same summed gradient (word rows outside the batch are never written)
     assert torch.equal(r0["grad"][woff + V * D:], r1["grad"][woff + V * D:])
     assert torch.equal(r0["grad"][:woff], r1["grad"][:woff])
+
+
+def test_dead_peer_in_fedavg_aborts_instead_of_hanging(tmp_path):
+    _spawn(_abort_worker, str(tmp_path), timeout=150)
+    ok, res, handle = (tmp_path / "abort.txt").read_text().split("|")
+    assert ok == "True"
+    assert res.startswith("raised after"), res
+    assert float(res.split("after ")[1].split("s")[0]) < 60, res
+    assert handle == "0"  # aborted
