@@ -62,7 +62,6 @@ def _args(argv=None):
     ap.add_argument("--impl", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-group-dw", action="store_true", help="one launch per weight gradient (A/B)")
-    ap.add_argument("--overlap-transpose", action="store_true", help="W^T copies on a side stream (A/B; slower)")
     ap.add_argument("--spinup-seconds", type=float, default=1.0,
                     help="busy the GPU with a plain matmul loop before the warmup steps (a GPU that was idle "
                          "runs the first ~100 ms of work measurably slower); no model state is touched")
@@ -83,8 +82,6 @@ def _args(argv=None):
                          "all-layer weight-gradient GEMM's epilogue (A/B)")
     ap.add_argument("--padded", action="store_true",
                     help="run the blocks on all B*S positions instead of the packed real tokens (A/B)")
-    ap.add_argument("--wgrad-stream", action="store_true",
-                    help="run the backward's weight-gradient work on a side stream (A/B; measured slower)")
     ap.add_argument("--layers", type=int, default=6)
     ap.add_argument("--comm", default="torch", choices=["torch", "rccl"],
                     help="FedAvg collective: torch.distributed (RCCL) or the framework's NativeComm (RCCL)")
@@ -208,7 +205,6 @@ def main():
     # ---- the throughput model (same architecture and init; discarded after the timed window)
     cfg = models.DistilBertConfig(n_layers=args.layers)
     model = models.DDoSClassifier(config=cfg, device=dev, impl=args.impl, seed=0)
-    model.wgrad_stream = args.wgrad_stream
     model.group_dw = not args.no_group_dw
     model.defer_dw_reduce = not args.no_defer_dw
     model.fuse_colsum = not args.no_fuse_colsum
@@ -232,7 +228,6 @@ def main():
     else:
         fn = engine.make_step_fn(model, opt)
     model.unpad = not args.padded
-    model.overlap_transpose = args.overlap_transpose
     step = engine.GraphedTrainStep(fn, warmup=2, enabled=(not args.no_graph) and args.impl == "hip"
                                    and on_gpu and gsync is None,
                                    bucket=getattr(model, "packed_rows", None))

@@ -11,6 +11,7 @@
 // device-placement check and the stream query differ; every shape/dtype rule is the same code.
 #include <ATen/ATen.h>
 typedef struct ihipStream_t* hipStream_t;
+namespace py { struct gil_scoped_release {}; }  // (no Python in the host-only build)
 #else
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
@@ -25,21 +26,24 @@ typedef struct ihipStream_t* hipStream_t;
 extern "C" {
 int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
             int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
-            long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+            long long workspace_elems, int accumulate, const FdAdamEpi* adam,
             float* colsum, int* colsum_blocks, hipStream_t st);
 int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
-               long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+               long long workspace_elems, int accumulate, const FdAdamEpi* adam,
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
-int fd_gemm_set_fixup(int on);
+int fd_gemm_stamps(unsigned long long* host, int nblocks);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
-                int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, int* tile_cnt,
-                long long ncnt, const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st);
+                int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate,
+                const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st);
 int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K);
 int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg,
                      hipStream_t st);
 int fd_gemm_ln_set_diag(int diag);
+int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, float* workspace,
+                   long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
+                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, hipStream_t st);
 int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
                const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t st);
 int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
@@ -182,8 +186,8 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
   const long long ws = (workspace.has_value() && workspace->defined()) ? workspace->numel() : 0;
   check_rc(fd_gemm_ex((int)kind, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
                       (int)A.size(1), (int)B.size(1), (int)N, ptr<float>(bias), ptr<void>(aux), (int)N,
-                      ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, nullptr, 0, nullptr,
-                      nullptr, nullptr, ptr<void>(aux_out), stream()),
+                      ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, nullptr, nullptr,
+                      nullptr, ptr<void>(aux_out), stream()),
            "gemm");
 }
 
@@ -213,7 +217,7 @@ int64_t gemm_colsum(int64_t epi, const at::Tensor& A, const at::Tensor& B, const
   int blocks = 0;
   check_rc(fd_gemm_ex(0, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K, (int)K,
                       (int)K, (int)N, nullptr, ptr<void>(aux), (int)N, ptr<void>(res), (int)N, nullptr, 0, 0,
-                      nullptr, 0, nullptr, colsum.data_ptr<float>(), &blocks, ptr<void>(aux_out), stream()),
+                      nullptr, colsum.data_ptr<float>(), &blocks, ptr<void>(aux_out), stream()),
            "gemm_colsum");
   return blocks;
 }
@@ -249,19 +253,10 @@ void adam_descs(const std::vector<at::Tensor>& st, const std::vector<double>& hp
   }
 }
 
-int* counters_ptr(const c10::optional<at::Tensor>& c, long long* n) {
-  *n = 0;
-  if (!c.has_value() || !c->defined()) return nullptr;
-  need(*c, at::kInt, "tile counters");
-  *n = c->numel();
-  return c->data_ptr<int>();
-}
-
-// Weight gradient C[M][N] (+)= A^T B (fp32), split-K reduced in-kernel through `counters`
-// (int32, zero-initialised, self-resetting), optionally with Adam fused into the epilogue.
+// Weight gradient C[M][N] (+)= A^T B (fp32; split-K slabs in `workspace`, reduced by a second
+// launch), optionally with Adam fused into the epilogue (one K split).
 void gemm_dw(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, const at::Tensor& workspace,
-             bool accumulate, const c10::optional<at::Tensor>& counters, const std::vector<at::Tensor>& adam,
-             const std::vector<double>& hp) {
+             bool accumulate, const std::vector<at::Tensor>& adam, const std::vector<double>& hp) {
   need(A, at::kBFloat16, "A");
   need(B, at::kBFloat16, "B");
   need(C, at::kFloat, "C");
@@ -273,19 +268,16 @@ void gemm_dw(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, cons
   FdAdamEpi ad{};
   const at::Tensor* gs[1] = {&C};
   if (!adam.empty()) adam_descs(adam, hp, gs, 1, &ad);
-  long long ncnt;
-  int* cnt = counters_ptr(counters, &ncnt);
   check_rc(fd_gemm(2, 5, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K, (int)M, (int)N, (int)N,
                    nullptr, nullptr, 0, nullptr, 0, workspace.data_ptr<float>(), workspace.numel(),
-                   accumulate ? 1 : 0, cnt, ncnt, adam.empty() ? nullptr : &ad, nullptr, nullptr, stream()),
+                   accumulate ? 1 : 0, adam.empty() ? nullptr : &ad, nullptr, nullptr, stream()),
            "gemm_dw");
 }
 
 // Grouped weight gradients: C0 (+)= A0^T B0 and C1 (+)= A1^T B1 in one launch (shared K = tokens).
 int64_t gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C0, const at::Tensor& A1,
                  const at::Tensor& B1, const at::Tensor& C1, const at::Tensor& workspace, bool accumulate,
-                 const c10::optional<at::Tensor>& counters, const std::vector<at::Tensor>& adam,
-                 const std::vector<double>& hp, bool defer) {
+                 const std::vector<at::Tensor>& adam, const std::vector<double>& hp, bool defer) {
   const at::Tensor* As[2] = {&A0, &A1};
   const at::Tensor* Bs[2] = {&B0, &B1};
   const at::Tensor* Cs[2] = {&C0, &C1};
@@ -303,12 +295,10 @@ int64_t gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C
   need(workspace, at::kFloat, "workspace");
   FdAdamEpi ad[2]{};
   if (!adam.empty()) adam_descs(adam, hp, Cs, 2, ad);
-  long long ncnt;
-  int* cnt = counters_ptr(counters, &ncnt);
   int splits = 0;
   check_rc(fd_gemm_dw2(A0.data_ptr(), B0.data_ptr(), C0.data_ptr<float>(), (int)A0.size(1), (int)B0.size(1),
                        A1.data_ptr(), B1.data_ptr(), C1.data_ptr<float>(), (int)A1.size(1), (int)B1.size(1), (int)K,
-                       workspace.data_ptr<float>(), workspace.numel(), accumulate ? 1 : 0, cnt, ncnt,
+                       workspace.data_ptr<float>(), workspace.numel(), accumulate ? 1 : 0,
                        adam.empty() ? nullptr : ad, defer ? 1 : 0, &splits, stream()),
            "gemm_dw2");
   return splits;  // > 0: slabs left in `workspace` (problem 0 then 1) for splitk_reduce_batched
@@ -445,6 +435,89 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
                             ptr<float>(bias), res.data_ptr(), (int)N, &ln, (int)cfg, stream());
   TORCH_CHECK(rc > 0, "gemm_ln: kernel launcher rejected arguments (rc=", rc, ")");
   return rc;
+}
+
+// Split-K NT GEMM + fused epilogue (splitk.hip): C = epi(A Bt^T) through fp32 slabs in `workspace`.
+// epi: 0 bf16, 1 bias, 2 bias+GELU (aux = u out), 3 GELU' (aux = u in, aux_out = gelu(u)), 4 residual,
+// 6 LayerNorm forward, 7 LayerNorm backward (the ln_* arguments as for gemm_ln; colpart: M rows of
+// [3][N]).  colsum (epi 3 / 4): ceil(M / 32) x N column partials of C.  Returns (splits, colsum
+// partial rows).
+std::vector<int64_t> gemm_splitk(int64_t epi, const at::Tensor& A, const at::Tensor& Bt, const at::Tensor& C,
+                                 const at::Tensor& workspace, int64_t splits, const c10::optional<at::Tensor>& bias,
+                                 const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& aux_out,
+                                 const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& colsum,
+                                 const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                                 const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor>& rstd,
+                                 const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& dx,
+                                 const c10::optional<at::Tensor>& colpart, double eps,
+                                 const c10::optional<at::Tensor>& seed, int64_t site, int64_t thr, double dscale,
+                                 const c10::optional<at::Tensor>& row_map) {
+  need(A, at::kBFloat16, "A");
+  need(Bt, at::kBFloat16, "Bt");
+  need(C, at::kBFloat16, "C");
+  need(workspace, at::kFloat, "workspace");
+  TORCH_CHECK(A.dim() == 2 && Bt.dim() == 2 && C.dim() == 2, "gemm_splitk operands must be 2-D");
+  const int64_t M = A.size(0), K = A.size(1), N = Bt.size(0);
+  TORCH_CHECK(M > 0 && Bt.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_splitk: shape mismatch");
+  TORCH_CHECK(K % 64 == 0 && N % 64 == 0, "gemm_splitk: K % 64 and N % 64 required");
+  TORCH_CHECK(epi >= 0 && epi <= 7 && epi != 5, "gemm_splitk: epilogue code");
+  for (const auto* t : {&aux, &aux_out, &res, &z, &dx}) {
+    need_opt(*t, at::kBFloat16, "gemm_splitk bf16 operand");
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->dim() == 2 && (*t)->size(0) == M && (*t)->size(1) == N, "gemm_splitk: [M, N] operand");
+  }
+  for (const auto* t : {&bias, &gamma, &beta}) {
+    need_opt(*t, at::kFloat, "gemm_splitk fp32 vector");
+    if (t->has_value() && (*t)->defined()) TORCH_CHECK((*t)->numel() == N, "gemm_splitk: vector of size N");
+  }
+  need_opt(mean, at::kFloat, "mean");
+  need_opt(rstd, at::kFloat, "rstd");
+  need_opt(colsum, at::kFloat, "colsum");
+  need_opt(colpart, at::kFloat, "colpart");
+  need_opt(row_map, at::kInt, "row_map");
+  auto has = [](const c10::optional<at::Tensor>& t) { return t.has_value() && t->defined(); };
+  if (epi == 1 || epi == 2 || epi == 6) TORCH_CHECK(has(bias), "gemm_splitk: bias required");
+  if (epi == 2 || epi == 3) TORCH_CHECK(has(aux), "gemm_splitk: aux [M, N] required");
+  if (epi == 4 || epi >= 6) TORCH_CHECK(has(res), "gemm_splitk: res [M, N] required");
+  if (has(colsum)) {
+    TORCH_CHECK(epi == 3 || epi == 4, "gemm_splitk: column sums only with the GELU' / residual epilogues");
+    TORCH_CHECK(colsum->numel() >= ((M + 31) / 32) * N, "gemm_splitk: colsum needs ceil(M/32) x N floats");
+  }
+  FdLnEpi ln{};
+  if (epi >= 6) {
+    TORCH_CHECK(has(gamma) && has(mean) && has(rstd) && mean->numel() >= M && rstd->numel() >= M,
+                "gemm_splitk LayerNorm: gamma, mean / rstd of M entries required");
+    if (epi == 6) TORCH_CHECK(has(beta), "gemm_splitk LayerNorm forward: beta required");
+    if (epi == 7) {
+      TORCH_CHECK(has(z), "gemm_splitk LayerNorm backward: z required");
+      TORCH_CHECK(has(colpart) && colpart->numel() >= M * 3 * N, "gemm_splitk LayerNorm backward: colpart M x 3N");
+      if (thr) TORCH_CHECK(has(dx), "gemm_splitk LayerNorm backward with dropout: dx required");
+    }
+    ln.gamma = gamma->data_ptr<float>();
+    ln.beta = ptr<float>(beta);
+    ln.mean = mean->data_ptr<float>();
+    ln.rstd = rstd->data_ptr<float>();
+    ln.z = ptr<uint16_t>(z);
+    ln.dx = ptr<uint16_t>(dx);
+    ln.colpart = ptr<float>(colpart);
+    ln.eps = (float)eps;
+    ln.thr = (uint32_t)thr;
+    ln.site = (uint32_t)site;
+    ln.dscale = (float)dscale;
+    if (thr) {
+      TORCH_CHECK(seed.has_value() && seed->defined(), "gemm_splitk: dropout needs the seed tensor");
+      ln.seed_ptr = seedp(*seed);
+      ln.row_map = ptr<int>(row_map);
+      if (has(row_map)) TORCH_CHECK(row_map->numel() >= M, "gemm_splitk: row_map needs M entries");
+    }
+  }
+  int blocks = 0;
+  const int rc = fd_gemm_splitk((int)epi, A.data_ptr(), Bt.data_ptr(), (int)M, (int)N, (int)K,
+                                workspace.data_ptr<float>(), workspace.numel(), (int)splits, ptr<float>(bias),
+                                C.data_ptr(), ptr<void>(aux), ptr<void>(aux_out), ptr<void>(res), ptr<float>(colsum),
+                                &blocks, epi >= 6 ? &ln : nullptr, stream());
+  TORCH_CHECK(rc > 0, "gemm_splitk: launcher rejected arguments (rc=", rc, ")");
+  return {rc, blocks};
 }
 
 // Finish deferred split-K weight gradients: out_i (+)= sum_z slabs_i[z] (z order), one launch.
@@ -619,6 +692,14 @@ void transpose_batched(const std::vector<at::Tensor>& srcs, const std::vector<at
   }
   check_rc(fd_transpose_batched(sp.data(), dp.data(), rows.data(), cols.data(), (int)sp.size(), stream()),
            "transpose_batched");
+}
+
+// Diagnostic builds (FD_GEMM_STAMPS): per-block phase stamps of the last one-round GEMM launch
+// into `out` (CPU int64 [nblocks][8]); returns the blocks copied (-1: a normal build).
+int64_t gemm_stamps(at::Tensor out) {
+  TORCH_CHECK(!out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous() && out.dim() == 2 &&
+                  out.size(1) == 8, "gemm_stamps: CPU int64 [n][8]");
+  return fd_gemm_stamps(reinterpret_cast<unsigned long long*>(out.data_ptr()), (int)out.size(0));
 }
 
 // Tuning hook: force GEMM configuration `cfg` (-1 = measured default) for a kind.
@@ -1099,6 +1180,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, py::arg("kind"), py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"),
         py::arg("aux"), py::arg("res"), py::arg("workspace"), py::arg("accumulate"), py::arg("aux_out") = py::none());
   m.def("gemm_set_cfg", &gemm_set_cfg);
+  m.def("gemm_stamps", &gemm_stamps);
+  m.def("gemm_splitk", &gemm_splitk, py::arg("epi"), py::arg("A"), py::arg("Bt"), py::arg("C"), py::arg("workspace"),
+        py::arg("splits") = 0, py::arg("bias") = py::none(), py::arg("aux") = py::none(),
+        py::arg("aux_out") = py::none(), py::arg("res") = py::none(), py::arg("colsum") = py::none(),
+        py::arg("gamma") = py::none(), py::arg("beta") = py::none(), py::arg("mean") = py::none(),
+        py::arg("rstd") = py::none(), py::arg("z") = py::none(), py::arg("dx") = py::none(),
+        py::arg("colpart") = py::none(), py::arg("eps") = 1e-12, py::arg("seed") = py::none(),
+        py::arg("site") = 0, py::arg("thr") = 0, py::arg("dscale") = 1.0, py::arg("row_map") = py::none());
   m.def("gemm_dw2", &gemm_dw2);
   m.def("gemm_dw", &gemm_dw);
   m.def("adam_rows", &adam_rows);
@@ -1115,7 +1204,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_dw2_splits", [](int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K) {
     return (int64_t)fd_gemm_dw2_splits((int)M0, (int)N0, (int)M1, (int)N1, (int)K);
   });
-  m.def("gemm_set_fixup", [](bool on) { fd_gemm_set_fixup(on ? 1 : 0); });
   m.def("gather_rows2", &gather_rows2);
   m.def("scatter_rows2", &scatter_rows2);
   m.def("pack", &pack, py::arg("mask"), py::arg("ids"), py::arg("row_map"), py::arg("cu"), py::arg("ids_packed"),

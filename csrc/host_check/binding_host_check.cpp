@@ -9,6 +9,7 @@
 // the test registered.  The driver then makes valid calls (no exception, no violation) and
 // invalid ones (a c10::Error, and NO launcher call).  Run by tests/test_host_sanitizers.py.
 #define FD_HOST_VALIDATION 1
+#include <algorithm>
 #include "../binding.cpp"
 
 #include <cstdio>
@@ -41,7 +42,7 @@ void opt_span(const void* p, long long bytes, const char* what) { if (p) span(p,
 extern "C" {
 int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
-               long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+               long long workspace_elems, int accumulate, const FdAdamEpi* adam,
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t) {
   ++hc::calls;
   if (kind == 0) {  // A [M][lda] (K used), B [N][ldb], C [M][ldc] bf16
@@ -70,20 +71,20 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
     hc::span(adam->v, (long long)M * N * 4, "adam v");
     hc::opt_span(adam->sh, (long long)M * N * 2, "adam shadow");
   }
-  (void)accumulate; (void)tile_cnt; (void)ncnt;
+  (void)accumulate;
   return 0;
 }
 int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
             const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
-            long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+            long long workspace_elems, int accumulate, const FdAdamEpi* adam,
             float* colsum, int* colsum_blocks, hipStream_t st) {
   return fd_gemm_ex(kind, epi, A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, res, ldres, workspace,
-                    workspace_elems, accumulate, tile_cnt, ncnt, adam, colsum, colsum_blocks, nullptr, st);
+                    workspace_elems, accumulate, adam, colsum, colsum_blocks, nullptr, st);
 }
 int fd_gemm_set_cfg(int, int, int) { return 0; }
-int fd_gemm_set_fixup(int) { return 0; }
+int fd_gemm_stamps(unsigned long long*, int) { return -1; }
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
-                int M1, int N1, int K, float* workspace, long long workspace_elems, int, int*, long long,
+                int M1, int N1, int K, float* workspace, long long workspace_elems, int,
                 const FdAdamEpi* adams, int, int* splits_out, hipStream_t) {
   ++hc::calls;
   hc::span(A0, (long long)K * M0 * 2, "dw2 A0");
@@ -135,6 +136,43 @@ int fd_adam_rows(float* p, const float* g, float* m, float* v, void* shadow, int
   hc::span(ever, rows, "adam_rows ever");
   hc::opt_span(now, rows, "adam_rows now");
   return 0;
+}
+int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, float* workspace,
+                   long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
+                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, hipStream_t) {
+  ++hc::calls;
+  const long long mn = (long long)M * N;
+  if (splits <= 0) splits = 1;
+  hc::span(A, (long long)M * K * 2, "splitk A");
+  hc::span(Bt, (long long)N * K * 2, "splitk Bt");
+  hc::span(C, mn * 2, "splitk C");
+  hc::span(workspace, std::min(workspace_elems, (long long)splits * mn) * 4, "splitk workspace");
+  if (epi == 1 || epi == 2 || epi == 6) hc::span(bias, (long long)N * 4, "splitk bias");
+  if (epi == 2 || epi == 3) hc::span(aux, mn * 2, "splitk aux");
+  hc::opt_span(aux_out, mn * 2, "splitk aux_out");
+  if (epi == 4 || epi >= 6) hc::span(res, mn * 2, "splitk res");
+  if (colsum) {
+    if (colsum_blocks) *colsum_blocks = (M + 31) / 32;
+    hc::span(colsum, (long long)((M + 31) / 32) * N * 4, "splitk colsum");
+  }
+  if (ln) {
+    hc::span(ln->gamma, (long long)N * 4, "splitk gamma");
+    hc::span(ln->mean, (long long)M * 4, "splitk mean");
+    hc::span(ln->rstd, (long long)M * 4, "splitk rstd");
+    if (epi == 7) {
+      hc::span(ln->z, mn * 2, "splitk z");
+      hc::span(ln->colpart, mn * 3 * 4, "splitk colpart");
+      if (ln->thr) hc::span(ln->dx, mn * 2, "splitk dx");
+    } else {
+      hc::span(ln->beta, (long long)N * 4, "splitk beta");
+      hc::opt_span(ln->z, mn * 2, "splitk z");
+    }
+    if (ln->thr) {
+      hc::span(ln->seed_ptr, 4, "splitk seed");
+      hc::opt_span(ln->row_map, (long long)M * 4, "splitk row_map");
+    }
+  }
+  return splits;
 }
 int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
                const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t) {
@@ -533,7 +571,29 @@ int main() {
     expect_reject("dw_batch > 32 problems", [&] { gemm_dw_batch(A33, B33, C33, std::vector<int64_t>(33, 0), {}, {}, -1); });
     auto A0 = T_({2688, 768}, bf), B0 = T_({2688, 3072}, bf), C0 = T_({768, 3072}, f32);
     auto A1 = T_({2688, 3072}, bf), B1 = T_({2688, 768}, bf), C1 = T_({3072, 768}, f32), wsp = T_({8 * 2 * 2359296}, f32);
-    expect_ok("dw2", [&] { gemm_dw2(A0, B0, C0, A1, B1, C1, wsp, false, none, {}, {}, false); });
+    expect_ok("dw2", [&] { gemm_dw2(A0, B0, C0, A1, B1, C1, wsp, false, {}, {}, false); });
+  }
+  // ---- split-K small-M GEMM + fused epilogues (splitk.hip)
+  {
+    auto A = T_({64, 3072}, bf), Bt = T_({768, 3072}, bf), C = T_({64, 768}, bf), ws = T_({256 * 64 * 64 + 64 * 768}, f32);
+    auto res = T_({64, 768}, bf), g = T_({768}, f32), b = T_({768}, f32), mean = T_({64}, f32), rstd = T_({64}, f32);
+    auto z = T_({64, 768}, bf), dx = T_({64, 768}, bf), cp = T_({64 * 3 * 768}, f32), sd = T_({1}, i32);
+    const c10::optional<at::Tensor> o_b = b, o_res = res, o_g = g, o_m = mean, o_r = rstd, o_z = z, o_dx = dx, o_cp = cp,
+                                    o_sd = sd;
+    expect_ok("splitk bf16", [&] { gemm_splitk(0, A, Bt, C, ws, 0, none, none, none, none, none, none, none, none, none,
+                                               none, none, none, 1e-12, none, 0, 0, 1.0, none); });
+    expect_ok("splitk ln fwd", [&] { gemm_splitk(6, A, Bt, C, ws, 0, o_b, none, none, o_res, none, o_g, o_b, o_m, o_r,
+                                                 o_z, none, none, 1e-12, o_sd, 9, 1000, 1.1, none); });
+    expect_ok("splitk ln bwd", [&] { gemm_splitk(7, A, Bt, C, ws, 0, none, none, none, o_res, none, o_g, none, o_m, o_r,
+                                                 o_z, o_dx, o_cp, 1e-12, o_sd, 9, 1000, 1.1, none); });
+    expect_reject("splitk ln bwd colpart", [&] {
+      gemm_splitk(7, A, Bt, C, ws, 0, none, none, none, o_res, none, o_g, none, o_m, o_r, o_z, o_dx,
+                  c10::optional<at::Tensor>(T_({64 * 768}, f32)), 1e-12, o_sd, 9, 1000, 1.1, none); });
+    expect_reject("splitk K mismatch", [&] { gemm_splitk(0, A, T_({768, 768}, bf), C, ws, 0, none, none, none, none,
+                                                         none, none, none, none, none, none, none, none, 1e-12, none,
+                                                         0, 0, 1.0, none); });
+    expect_reject("splitk bias missing", [&] { gemm_splitk(1, A, Bt, C, ws, 0, none, none, none, none, none, none, none,
+                                                           none, none, none, none, none, 1e-12, none, 0, 0, 1.0, none); });
   }
   // ---- attention (padded and varlen), S up to 512
   {
@@ -653,7 +713,7 @@ int main() {
   {
     auto mask = T_({32, 128}, i64), ids = T_({32, 128}, i64), rm = T_({2688}, i32), cu = T_({33}, i32);
     auto ip = T_({2688}, i64);
-    expect_ok("pack", [&] { pack(mask, ids, rm, cu, ip, none, none, none); });
+    expect_ok("pack", [&] { pack(mask, ids, rm, cu, ip, none, none, none, none); });
     {
       auto ga = T_({300, 768}, bf), gb = T_({300, 768}, bf), go = T_({64, 768}, bf), go2 = T_({64, 768}, bf);
       auto gi = T_({64}, i64);
@@ -664,11 +724,11 @@ int main() {
       expect_reject("scatter_rows2 nsrc", [&] { scatter_rows2(go, go2, ga, gb, gi, 65); });
     }
     auto st1 = T_({1}, i32);
-    expect_ok("pack + counters", [&] { pack(mask, ids, rm, cu, ip, st1, st1, none); });
+    expect_ok("pack + counters", [&] { pack(mask, ids, rm, cu, ip, st1, st1, none, none); });
     auto stf = T_({1}, f32);
-    expect_reject("pack counter dtype", [&] { pack(mask, ids, rm, cu, ip, stf, none, none); });
+    expect_reject("pack counter dtype", [&] { pack(mask, ids, rm, cu, ip, stf, none, none, none); });
     auto cu_bad = T_({32}, i32);
-    expect_reject("pack cu", [&] { pack(mask, ids, rm, cu_bad, ip, none, none, none); });
+    expect_reject("pack cu", [&] { pack(mask, ids, rm, cu_bad, ip, none, none, none, none); });
   }
   if (failures) {
     std::printf("binding host check: %d failure(s)\n", failures);

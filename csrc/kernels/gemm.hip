@@ -62,14 +62,10 @@ struct GemmParams {
   long long slab_stride; // elements between fp32 slabs
   int group_m;           // tile-walk group height (L2 working-set control)
   int diag;              // FD_GEMM_DIAG bits (profiling only): 1 no in-loop DMA, 4 no stores
-  // EPI_F32 destinations (weight gradients).  out == nullptr: legacy slab mode (slab z of C,
-  // reduced by splitk_reduce_kernel).  Otherwise the final [M][N] fp32 gradient:
-  //   tile_cnt == nullptr -> one K split, the tile goes straight to out (+= out if accumulate);
-  //   tile_cnt != nullptr -> split-K fixup: every split stores its slab into C, the last split
-  //   of a tile to arrive sums the slabs in z order (bitwise what splitk_reduce computes) and
-  //   finishes the tile; the per-tile arrival counters reset themselves for the next launch.
+  // EPI_F32 destinations (weight gradients).  out == nullptr: slab mode (slab z of C, reduced
+  // by splitk_reduce_kernel).  Otherwise one K split: the tile goes straight to the final [M][N]
+  // fp32 gradient out (+= out if accumulate).
   float* out;
-  int* tile_cnt;
   int accumulate;
   FdAdamEpi adam;        // adam.p != nullptr: apply Adam to the finished tile instead of storing it
   // EPI_GELU_BWD / EPI_ADD with a staged fp32 tile: column sums of the stored output per M
@@ -84,6 +80,33 @@ struct GemmParams {
 
 constexpr int BKT = 64;
 constexpr int LDS_MAX = 163840;
+
+// Diagnostic build only (FD_HIP_EXTRA_FLAGS=-DFD_GEMM_STAMPS=1): per-block wall-clock stamps
+// (100 MHz) at the phase boundaries of the one-round GEMMs, read back with fd_gemm_stamps
+// (scripts/gemm_stamps.py).  Slot 7 holds the hardware id (XCC << 16 | HW_ID).  Nothing of the
+// normal build executes or reads them.
+#ifndef FD_GEMM_STAMPS
+#define FD_GEMM_STAMPS 0
+#endif
+constexpr int STAMP_MAXB = 2048;
+#if FD_GEMM_STAMPS
+__device__ unsigned long long g_stamps[STAMP_MAXB * 8];
+DEV int stamp_bid() { return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); }
+#define FD_STAMP(i)                                                                                \
+  do {                                                                                             \
+    if (threadIdx.x == 0 && stamp_bid() < STAMP_MAXB) g_stamps[stamp_bid() * 8 + (i)] = wall_clock64(); \
+  } while (0)
+DEV void stamp_hwid() {
+  if (threadIdx.x == 0 && stamp_bid() < STAMP_MAXB) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
+    g_stamps[stamp_bid() * 8 + 7] = ((unsigned long long)(xcc & 0xf) << 32) | hw;
+  }
+}
+#else
+#define FD_STAMP(i) do {} while (0)
+DEV void stamp_hwid() {}
+#endif
 
 // Logical tile id -> (tm, tn).  After the XCD remap each XCD owns a contiguous
 // range of logical ids; walking them in groups of `gm` M-tiles x all N-tiles
@@ -245,13 +268,9 @@ DEV void adam_epi4(const FdAdamEpi& a, size_t i, float4 g4, float step_size, flo
   if (a.sh) *reinterpret_cast<uint2*>(a.sh + i) = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
 }
 
-// Weight-gradient (fp32) epilogue; see GemmParams::out for the three modes.
-// flag: a 4-byte slot of the kernel's one LDS array (GemmCfg::FLAG).  A second __shared__ object
-// next to the LDS-DMA ring makes hipcc wait vmcnt(0) right after every K tile's DMA issue (the
-// DMA latency then sits in the K loop; gfx950 guide, 'three .s-level traps').
+// Weight-gradient (fp32) epilogue; see GemmParams::out for the two modes.
 template <int BM, int BN, int NT>
-DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0, int n0, int tid, int slot,
-                      int* flag) {
+DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0, int n0, int tid) {
   constexpr int CPR = BN / 4;  // 4 fp32 per chunk
   if (p.out == nullptr) {      // legacy: slab z, reduced by a separate launch
     float* C = reinterpret_cast<float*>(p.C) + (size_t)blockIdx.z * p.slab_stride;
@@ -265,25 +284,6 @@ DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0
     }
     return;
   }
-  const bool fix = p.tile_cnt != nullptr;
-  if (fix) {
-    float* C = reinterpret_cast<float*>(p.C) + (size_t)blockIdx.z * p.slab_stride;
-#pragma unroll 4
-    for (int id = tid; id < BM * CPR; id += NT) {
-      const int r = id / CPR, cc = id - r * CPR;
-      const int m = m0 + r;
-      if (m >= p.M) break;
-      *reinterpret_cast<float4*>(C + (size_t)m * p.ldc + n0 + cc * 4) =
-          *reinterpret_cast<const float4*>(smem + r * ldc_lds + cc * 16);
-    }
-    // release this split's slab at device scope (other XCDs' L2s), then count the arrival
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) *flag = atomicAdd(p.tile_cnt + slot, 1) == (int)gridDim.z - 1;
-    __syncthreads();
-    if (!*flag) return;
-    __threadfence();  // acquire: the other splits' slabs are visible
-  }
   const bool adam = p.adam.p != nullptr;
   float step_size = 0.f, inv_sqrt_bc2 = 0.f;
   if (adam) {
@@ -293,65 +293,19 @@ DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0
     step_size = p.adam.lr / bc1;
     inv_sqrt_bc2 = 1.f / sqrtf(bc2);
   }
-  const float* slabs = reinterpret_cast<const float*>(p.C);
 #pragma unroll 2
   for (int id = tid; id < BM * CPR; id += NT) {
     const int r = id / CPR, cc = id - r * CPR;
     const int m = m0 + r;
     if (m >= p.M) break;
     const size_t i = (size_t)m * p.ldc + n0 + cc * 4;
-    float4 g;
-    if (fix) {
-      g = p.accumulate ? *reinterpret_cast<const float4*>(p.out + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int z = 0; z < (int)gridDim.z; ++z) {
-        const float4 s = ld_nt4(slabs + z * p.slab_stride + i);
-        g.x += s.x; g.y += s.y; g.z += s.z; g.w += s.w;
-      }
-    } else {
-      const float4 t = *reinterpret_cast<const float4*>(smem + r * ldc_lds + cc * 16);
-      if (p.accumulate) {
-        g = *reinterpret_cast<const float4*>(p.out + i);
-        g.x += t.x; g.y += t.y; g.z += t.z; g.w += t.w;
-      } else {
-        g = t;
-      }
+    float4 g = *reinterpret_cast<const float4*>(smem + r * ldc_lds + cc * 16);
+    if (p.accumulate) {
+      const float4 o = *reinterpret_cast<const float4*>(p.out + i);
+      g.x += o.x; g.y += o.y; g.z += o.z; g.w += o.w;
     }
     if (adam) adam_epi4(p.adam, i, g, step_size, inv_sqrt_bc2);
     else *reinterpret_cast<float4*>(p.out + i) = g;
-  }
-  if (fix && tid == 0) p.tile_cnt[slot] = 0;  // ready for the next launch / graph replay
-}
-
-// fp32 epilogue from the accumulators (EpiTraits::DIRECT): lane (i, j) holds C[m][n..n+3] of
-// its wave tile.  Slab mode (out == nullptr: split z) or the final gradient (+= out when
-// accumulating), optionally with the fused Adam step; no split-K fixup (it needs the staged tile).
-template <int TM, int TN>
-DEV void direct_f32_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], int m0, int n0, int wr,
-                             int wc, int lane) {
-  const bool adam = p.adam.p != nullptr;
-  float step_size = 0.f, inv_sqrt_bc2 = 0.f;
-  if (adam) {
-    const int t = p.adam.step[0];
-    step_size = p.adam.lr / (1.f - powf(p.adam.b1, (float)t));
-    inv_sqrt_bc2 = 1.f / sqrtf(1.f - powf(p.adam.b2, (float)t));
-  }
-  float* C = p.out ? p.out : reinterpret_cast<float*>(p.C) + (size_t)blockIdx.z * p.slab_stride;
-#pragma unroll
-  for (int i = 0; i < TM / 16; ++i) {
-    const int m = m0 + wr * TM + i * 16 + (lane & 15);
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < TN / 16; ++j) {
-      const int n = n0 + wc * TN + j * 16 + 4 * (lane >> 4);
-      const size_t idx = (size_t)m * p.ldc + n;
-      float4 g = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      if (p.out && p.accumulate) {
-        const float4 o = *reinterpret_cast<const float4*>(p.out + idx);
-        g.x += o.x; g.y += o.y; g.z += o.z; g.w += o.w;
-      }
-      if (adam) adam_epi4(p.adam, idx, g, step_size, inv_sqrt_bc2);
-      else *reinterpret_cast<float4*>(C + idx) = g;
-    }
   }
 }
 
@@ -364,7 +318,7 @@ DEV void gelu_remat(const GemmParams& p, int m, int n, const uint2& u) {
 
 template <int BM, int BN, int TM, int TN, int EPI, int NT>
 DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int m0, int n0,
-                         int wr, int wc, int lane, int tid, int slot, int* flag) {
+                         int wr, int wc, int lane, int tid) {
   using TR = EpiTraits<EPI, BM, BN>;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int LDC = BN * TR::ES + 16;
@@ -424,7 +378,7 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
       }
     }
   } else if constexpr (EPI == EPI_F32) {
-    f32_epilogue<BM, BN, NT>(p, smem, LDC, m0, n0, tid, slot, flag);
+    f32_epilogue<BM, BN, NT>(p, smem, LDC, m0, n0, tid);
   } else {
     // 8 fp32 per chunk: two float4 LDS reads, then one 16-byte load / store per global stream
     constexpr int CPR = BN / 8;
@@ -680,6 +634,7 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
   // this lane's share of the tiles_n partials of its rows (tiles cc, cc + CPR, ...): poll the
   // granules until every tag is this launch's (wave-uniform exit)
   float2 st[IT][LN_MAXK];
+  FD_STAMP(3);
   {
     // diag 64 (tests only): wait for a tag no launch writes -> the timeout path
     const uint32_t want = (p.diag & 64) ? tag + 1u : tag;
@@ -710,6 +665,7 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
       }
     }
   }
+  FD_STAMP(4);
   float bt[8];
   if constexpr (!BWD) load8f(L.beta + n, bt);
   float cd[8] = {};  // backward: dbias partials
@@ -808,10 +764,7 @@ struct GemmCfg {
   // DIRECT fp32 tiles are staged one wave-row band (BM / WM rows) at a time
   static constexpr int EPI_BYTES = EpiTraits<EPI, BM, BN>::DIRECT ? (BM / WM) * (BN * 4 + 16)
                                                                    : EpiTraits<EPI, BM, BN>::BYTES;
-  static constexpr int SMEM0 = S * BUF > EPI_BYTES ? S * BUF : EPI_BYTES;
-  // fp32 epilogues keep their split-K "last arriver" flag in the same LDS array (f32_epilogue)
-  static constexpr int FLAG = SMEM0;
-  static constexpr int SMEM = SMEM0 + (EPI == EPI_F32 ? 16 : 0);
+  static constexpr int SMEM = S * BUF > EPI_BYTES ? S * BUF : EPI_BYTES;
   // (the accumulator-direct fp32 epilogue serves only the all-layer weight-gradient launch)
   static constexpr bool VALID = SMEM <= LDS_MAX && !EpiTraits<EPI, BM, BN>::DIRECT &&
                                 (!EpiTraits<EPI, BM, BN>::LN || EpiTraits<EPI, BM, BN>::F32S) &&
@@ -836,9 +789,8 @@ struct GemmGroup {
 #endif
 
 // One output tile (tm, tn) of problem p: the K loop over the LDS-DMA ring, then the epilogue.
-// slot = split-K arrival slot.
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool PIPE = false>
-DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem) {
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   using OA = typename G::OA;
   using OB = typename G::OB;
@@ -893,70 +845,7 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
     if constexpr (!SCHED) __builtin_amdgcn_s_setprio(0);
   };
 
-  if constexpr (PIPE) {
-    // Register-pipelined ring (one K tile per barrier): the fragments of tile kt+1 are read
-    // while tile kt's MFMAs run from the other fragment buffer, so no wave waits on LDS latency
-    // inside the loop.  Every step issues exactly one tile group of LDS-DMA (past the last tile
-    // the sources are clamped to it and the data lands in a slot nobody reads), so the counted
-    // wait is a constant: at the top of step kt tiles 0 .. kt+S-2 are issued and tile kt+1 must
-    // have landed -> vmcnt((S-3) * L).  WAR: step kt refills the slot of tile kt-1, whose
-    // fragments were read in step kt-2 and consumed in step kt-1, before the barrier.
-    static_assert(S >= 3, "pipelined ring: at least one tile in flight");
-    static_assert((S - 2) * L <= 63, "vmcnt is 6 bits");
-    bf16x8 fa[2][2][MI], fb[2][2][NI];
-    auto issue_c = [&](int t) {
-      char* b = smem + (t % S) * BUF;
-      const int k0 = kbeg + min(t, nk - 1) * BKT;
-      OA::stage(p.A, p.lda, m0, k0, p.M, b, wid, lane);
-      OB::stage(p.B, p.ldb, n0, k0, p.N, b + OA::BYTES, wid, lane);
-    };
-    auto read_into = [&](auto bufc, int t) {
-      constexpr int q = decltype(bufc)::value;
-      const char* cur = smem + (t % S) * BUF;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i) fa[q][h][i] = OA::frag(cur, wr * TM + i * 16, h, lane);
-#pragma unroll
-        for (int j = 0; j < NI; ++j) fb[q][h][j] = OB::frag(cur + OA::BYTES, wc * TN + j * 16, h, lane);
-      }
-    };
-    auto mfma_from = [&](auto bufc) {
-      constexpr int q = decltype(bufc)::value;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(fb[q][h][j], fa[q][h][i], acc[i][j]);
-    };
-    using B0 = std::integral_constant<int, 0>;
-    using B1 = std::integral_constant<int, 1>;
-    constexpr int RD = 2 * (MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2));  // ds_read instructions per tile
-    constexpr int MF = 2 * MI * NI;                                    // MFMAs per tile
-    auto step = [&](int kt, auto cur, auto nxt) {
-      wait_vm<(S - 3) * L>();
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      issue_c(kt + S - 1);
-      read_into(nxt, kt + 1);
-      mfma_from(cur);
-      sched_interleave<MF, (RD + MF - 1) / MF>();
-    };
-#pragma unroll
-    for (int t = 0; t < S - 1; ++t) issue_c(t);
-    wait_vm<(S - 2) * L>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    read_into(B0{}, 0);
-    int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {
-      step(kt, B0{}, B1{});
-      step(kt + 1, B1{}, B0{});
-    }
-    if (kt < nk) step(kt, B0{}, B1{});
-    wait_vm<0>();
-  } else if constexpr (S < 6) {
+  if constexpr (S < 6) {
 #pragma unroll
     for (int t = 0; t < S - 1; ++t)
       if (t < nk) issue(t);
@@ -967,6 +856,7 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
       // ... and everyone's has; everyone is also done reading tile kt-1's slot.
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      if (FD_GEMM_STAMPS && kt == 0) FD_STAMP(1);
       if (kt + S - 1 < nk && !(p.diag & 1)) issue(kt + S - 1);
       read_frags(smem + (kt % S) * BUF);
       mfmas();
@@ -986,6 +876,7 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
       wait_tiles<L, S - 4>(min(S - 4, max(0, issued - need)));
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      if (FD_GEMM_STAMPS && kt == 0) FD_STAMP(1);
       if (!(p.diag & 1)) {
         if (kt + S - 2 < nk) issue(kt + S - 2);  // slot of tile kt-2
         if (kt + S - 1 < nk) issue(kt + S - 1);  // slot of tile kt-1
@@ -1000,6 +891,7 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
       }
     }
   }
+  FD_STAMP(2);
   if constexpr (EpiTraits<EPI, BM, BN>::DIRECT) {
     // fp32 tile too large for LDS: finish it one wave-row band (TM rows) at a time through the
     // staged row-chunk epilogue (coalesced 16-byte rows for the gradient / Adam streams)
@@ -1021,10 +913,8 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
         }
       }
       __syncthreads();
-      f32_epilogue<TM, BN, 64 * NW>(p, smem, LDC, m0 + band * TM, n0, tid, slot,
-                                    reinterpret_cast<int*>(smem + G::FLAG));
+      f32_epilogue<TM, BN, 64 * NW>(p, smem, LDC, m0 + band * TM, n0, tid);
     }
-    (void)direct_f32_epilogue<TM, TN>;
   } else if constexpr (EpiTraits<EPI, BM, BN>::LN) {
     __syncthreads();  // no wave still reads a ring slot
     ln_epilogue<BM, BN, TM, TN, EPI == EPI_LN_BWD, 64 * NW>(p, acc, smem, tm, tn, wr, wc, lane, tid);
@@ -1032,40 +922,46 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, int slot, char* smem)
     // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
     // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
     __syncthreads();
-    staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid, slot,
-                                                  reinterpret_cast<int*>(smem + G::FLAG));
+    staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid);
   }
 }
 
 // bid = the tile's index within p, walked in group-M order
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool PIPE = false>
-DEV void gemm_tile(const GemmParams& p, int bid, int slot, char* smem) {
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+DEV void gemm_tile(const GemmParams& p, int bid, char* smem) {
   int tm, tn;
   tile_coords(bid, (p.M + BM - 1) / BM, p.N / BN, p.group_m, tm, tn);
-  gemm_tile_at<BM, BN, AK, BKM, EPI, WM, WN, S, PIPE>(p, tm, tn, slot, smem);
+  gemm_tile_at<BM, BN, AK, BKM, EPI, WM, WN, S>(p, tm, tn, smem);
 }
 
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool PIPE = false>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, GemmGroup grp) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  FD_STAMP(0);
+  stamp_hwid();
   int bid = xcd_remap(blockIdx.x, grp.ntiles);
-  const int slot = bid;  // unique per tile of the (grouped) grid: split-K arrival counter
   const bool second = bid >= grp.ntiles0;  // block-uniform
   const GemmParams& p = second ? grp.q : p0;
   if (second) bid -= grp.ntiles0;
-  gemm_tile<BM, BN, AK, BKM, EPI, WM, WN, S, PIPE>(p, bid, slot, smem);
+  gemm_tile<BM, BN, AK, BKM, EPI, WM, WN, S>(p, bid, smem);
+  __syncthreads();
+  FD_STAMP(5);
 }
 
 // LayerNorm-fused NT GEMM (EPI_LN / EPI_LN_BWD): the tiles of a row block are consecutive
 // logical tiles (row-major tile order), so after the XCD remap they run on one XCD, in order.
-template <int BM, int BN, int EPI, int WM, int WN, int S, bool PIPE = false>
+template <int BM, int BN, int EPI, int WM, int WN, int S>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_ln_kernel(GemmParams p) {
   using G = GemmCfg<BM, BN, true, true, EPI, WM, WN, S>;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  FD_STAMP(0);
+  stamp_hwid();
   const int tiles_n = p.N / BN;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  gemm_tile_at<BM, BN, true, true, EPI, WM, WN, S, PIPE>(p, lid / tiles_n, lid % tiles_n, 0, smem);
+  gemm_tile_at<BM, BN, true, true, EPI, WM, WN, S>(p, lid / tiles_n, lid % tiles_n, smem);
+  __syncthreads();
+  FD_STAMP(5);
 }
 
 // ---------------------------------------------------------------- all-layer weight gradients
@@ -1091,7 +987,7 @@ struct DwBatch {
 };
 
 // One tile of the batch: logical tile id lid -> (problem, tile) -> K loop + epilogue.
-template <int BM, int BN, int WM, int WN, int S, bool PIPE>
+template <int BM, int BN, int WM, int WN, int S>
 DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
   int i = 0;
   while (i + 1 < bt.n && lid >= bt.pr[i + 1].tile0) ++i;  // block-uniform
@@ -1111,57 +1007,14 @@ DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
     p.adam.lr = bt.lr; p.adam.b1 = bt.b1; p.adam.b2 = bt.b2; p.adam.eps = bt.eps; p.adam.wd = bt.wd;
     p.adam.decoupled = bt.decoupled;
   }
-  gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S, PIPE>(p, lid - q.tile0, 0, smem);
+  gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S>(p, lid - q.tile0, smem);
 }
 
-template <int BM, int BN, int WM, int WN, int S, bool PIPE = false>
+template <int BM, int BN, int WM, int WN, int S>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch bt) {
   using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S>;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
-  dwb_tile<BM, BN, WM, WN, S, PIPE>(bt, xcd_remap(blockIdx.x, bt.ntiles), smem);
-}
-
-// Persistent, dynamically scheduled variant: a fixed grid (slots x CUs workgroups) pulls tiles from
-// per-XCD counters; XCD x (blocks b with b % 8 == x, the dispatcher's round robin) walks the same
-// contiguous range of logical tiles as xcd_remap gives it, so the L2 sharing of the static grid is
-// kept.  Why: in the static grid every tile of a round reaches its Adam epilogue (HBM-bound, ~26 B
-// per parameter) at the same moment and every CU then waits on HBM with its MFMAs idle; the
-// blocks of the second slot (blockIdx >= gridDim / 2) start `delay` ns late, so a CU's two blocks
-// alternate -- one streams its Adam epilogue while the other runs its K loop -- and a block that
-// finishes early simply takes the next tile.  Each tile is still computed whole by one block
-// (full K, fixed-order epilogue): the result does not depend on the schedule.  The counters live
-// in device memory (g_dwb_sched) and the last block to leave resets them, so graph replays need no
-// memset; at most one persistent dW launch may run at a time on a device.
-__device__ int g_dwb_sched[16];  // [0, 8): per-XCD tile counters, [8]: blocks finished
-
-template <int BM, int BN, int WM, int WN, int S>
-__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_persist_kernel(DwBatch bt, long long delay_ns) {
-  using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S>;
-  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
-  int* s_tile = reinterpret_cast<int*>(smem + G::FLAG);
-  const int xcd = blockIdx.x % 8;
-  const int q = bt.ntiles / 8, r = bt.ntiles % 8;
-  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  const int cnt = q + (xcd < r ? 1 : 0);
-  if (delay_ns > 0 && blockIdx.x >= gridDim.x / 2) {
-    const unsigned long long t0 = wall_clock64();  // 100 MHz
-    while ((long long)(wall_clock64() - t0) * 10 < delay_ns) __builtin_amdgcn_s_sleep(32);
-  }
-  for (;;) {
-    __syncthreads();  // the previous tile's epilogue is done with the LDS (and with *s_tile)
-    if (threadIdx.x == 0) *s_tile = atomicAdd(g_dwb_sched + xcd, 1);
-    __syncthreads();
-    const int t = *s_tile;
-    if (t >= cnt) break;
-    dwb_tile<BM, BN, WM, WN, S, false>(bt, lo + t, smem);
-  }
-  if (threadIdx.x == 0) {
-    // every block that fetched from the counters has left its loop once all gridDim.x arrived
-    if (atomicAdd(g_dwb_sched + 8, 1) == (int)gridDim.x - 1) {
-      for (int x = 0; x < 8; ++x) atomicExch(g_dwb_sched + x, 0);
-      atomicExch(g_dwb_sched + 8, 0);
-    }
-  }
+  dwb_tile<BM, BN, WM, WN, S>(bt, xcd_remap(blockIdx.x, bt.ntiles), smem);
 }
 
 // out[i] = (accumulate ? out[i] : 0) + sum_z slab[z][i]   (deterministic split-K reduce)
@@ -1221,13 +1074,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_batched_kernel(ReduceBatch 
 // 18: 128 x  64, 4x2, S3     19: 128 x  64, 4x2, S2     20: 128 x  64, 2x4, S3
 // 21: 128 x 128, 4x2, S3  (8-wave blocks: two waves per SIMD where the grid is one block per CU)
 // 22: 128 x  64, 2x2, S6     23:  64 x  64, 2x2, S6     24: 128 x  64, 4x2, S6  (two K tiles per barrier)
-// (A ping-pong variant -- the two 4-wave halves of an 8-wave block staggered by
-// one barrier phase so one half's LDS reads overlap the other's MFMAs -- was
-// correct but measured 1.5-3x slower on these shapes; not kept.)
-// register-pipelined K loop (gemm_tile_at PIPE; fragments of tile kt+1 read under tile kt's MFMAs):
-// 25: 128 x 128, 2x2, S3    26: 128 x 128, 2x2, S4    27: 128 x 192, 2x4, S3
-// 28: 128 x  64, 4x2, S4    29: 128 x  64, 4x2, S6    30: 128 x 128, 4x2, S3
-constexpr int NCFG = 31;
+// Only the configurations some shape picks (pick_cfg / dw2_cfg / the LayerNorm-fused and all-layer
+// dW launchers) are instantiated; the others were measured and lost (profiles/r1_gemm_cfg_sweep*,
+// r1_ab_small_tiles.txt) and launch nothing (the caller falls back to cfg 0 / 8).  Removed after
+// losing their A/B in the step: a ping-pong 8-wave variant (1.5-3x slower), a register-pipelined
+// K loop (cfg 25-34; faster isolated, 1.911 vs 1.895-1.904 ms/step), a persistent per-XCD dW
+// grid (cfg 41-44; neutral) and an in-kernel split-K fixup (2.89 vs 2.38 ms/step)
+// (profiles/r2_ab_pipelined_gemm_persistent_dw.txt, r1_ab_fused_adam_fixup.txt).
+constexpr int NCFG = 25;
 struct CfgDesc { int bm, bn, wm, wn, s; };
 constexpr CfgDesc CFGS[NCFG] = {{128, 64, 2, 2, 3}, {128, 128, 2, 2, 2}, {128, 96, 2, 2, 2}, {256, 192, 4, 2, 2},
                                 {256, 128, 4, 2, 3}, {64, 192, 1, 4, 3}, {128, 192, 2, 4, 2}, {256, 96, 4, 1, 3},
@@ -1235,10 +1089,9 @@ constexpr CfgDesc CFGS[NCFG] = {{128, 64, 2, 2, 3}, {128, 128, 2, 2, 2}, {128, 9
                                 {256, 128, 4, 2, 2}, {64, 64, 2, 2, 3},    {64, 128, 2, 2, 3},  {128, 64, 2, 2, 4},
                                 {128, 64, 2, 2, 5},  {128, 128, 2, 2, 4}, {128, 64, 4, 2, 3},  {128, 64, 4, 2, 2},
                                 {128, 64, 2, 4, 3},  {128, 128, 4, 2, 3}, {128, 64, 2, 2, 6},  {64, 64, 2, 2, 6},
-                                {128, 64, 4, 2, 6},  {128, 128, 2, 2, 3}, {128, 128, 2, 2, 4}, {128, 192, 2, 4, 3},
-                                {128, 64, 4, 2, 4},  {128, 64, 4, 2, 6},  {128, 128, 4, 2, 3}};
+                                {128, 64, 4, 2, 6}};
 
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, bool PIPE = false>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
 bool launch_cfg(const GemmParams& p, int splits, hipStream_t st, const GemmParams* q) {
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   if constexpr (!G::VALID) {
@@ -1254,8 +1107,7 @@ bool launch_cfg(const GemmParams& p, int splits, hipStream_t st, const GemmParam
       grp.ntiles += (q->M / BM) * (q->N / BN);
     }
     const dim3 grid(grp.ntiles, 1, splits);
-    if constexpr (PIPE && EPI == EPI_F32) return false;  // (split-K weight gradients: the plain loops)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKM, EPI, WM, WN, S, PIPE>), grid, dim3(64 * WM * WN), 0, st, p, grp);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKM, EPI, WM, WN, S>), grid, dim3(64 * WM * WN), 0, st, p, grp);
     return true;
   }
 }
@@ -1265,35 +1117,15 @@ bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st, const Ge
   switch (id) {
     case 0: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
     case 1: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 2>(p, splits, st, q);
-    case 2: return launch_cfg<128, 96, AK, BKM, EPI, 2, 2, 2>(p, splits, st, q);
     case 3: return launch_cfg<256, 192, AK, BKM, EPI, 4, 2, 2>(p, splits, st, q);
-    case 4: return launch_cfg<256, 128, AK, BKM, EPI, 4, 2, 3>(p, splits, st, q);
-    case 5: return launch_cfg<64, 192, AK, BKM, EPI, 1, 4, 3>(p, splits, st, q);
     case 6: return launch_cfg<128, 192, AK, BKM, EPI, 2, 4, 2>(p, splits, st, q);
-    case 7: return launch_cfg<256, 96, AK, BKM, EPI, 4, 1, 3>(p, splits, st, q);
     case 8: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 2>(p, splits, st, q);
-    case 9: return launch_cfg<128, 96, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
     case 10: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
     case 11: return launch_cfg<256, 256, AK, BKM, EPI, 2, 4, 2>(p, splits, st, q);
-    case 12: return launch_cfg<256, 128, AK, BKM, EPI, 4, 2, 2>(p, splits, st, q);
     case 13: return launch_cfg<64, 64, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
-    case 14: return launch_cfg<64, 128, AK, BKM, EPI, 2, 2, 3>(p, splits, st, q);
-    case 15: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 4>(p, splits, st, q);
-    case 16: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 5>(p, splits, st, q);
-    case 17: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 4>(p, splits, st, q);
     case 18: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 3>(p, splits, st, q);
-    case 19: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 2>(p, splits, st, q);
-    case 20: return launch_cfg<128, 64, AK, BKM, EPI, 2, 4, 3>(p, splits, st, q);
     case 21: return launch_cfg<128, 128, AK, BKM, EPI, 4, 2, 3>(p, splits, st, q);
-    case 22: return launch_cfg<128, 64, AK, BKM, EPI, 2, 2, 6>(p, splits, st, q);
-    case 23: return launch_cfg<64, 64, AK, BKM, EPI, 2, 2, 6>(p, splits, st, q);
     case 24: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 6>(p, splits, st, q);
-    case 25: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 3, true>(p, splits, st, q);
-    case 26: return launch_cfg<128, 128, AK, BKM, EPI, 2, 2, 4, true>(p, splits, st, q);
-    case 27: return launch_cfg<128, 192, AK, BKM, EPI, 2, 4, 3, true>(p, splits, st, q);
-    case 28: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 4, true>(p, splits, st, q);
-    case 29: return launch_cfg<128, 64, AK, BKM, EPI, 4, 2, 6, true>(p, splits, st, q);
-    case 30: return launch_cfg<128, 128, AK, BKM, EPI, 4, 2, 3, true>(p, splits, st, q);
   }
   return false;
 }
@@ -1384,38 +1216,20 @@ bool launch_epi(int epi, const GemmParams& p, int id, int splits, hipStream_t st
   return false;
 }
 
-// Split-K weight gradients: 0 = slabs + a separate reduce launch (default), 1 = in-kernel
-// fixup by the last-arriving split (FD_GEMM_FIXUP=1 / fd_gemm_set_fixup).  The fixup needs a
-// device-scope release/acquire pair per block (L2 writeback + invalidate across the 8 XCDs'
-// L2s); measured on MI355X at bs32 x seq128 that costs ~40 us per launch, far more than the
-// 5 us reduce launch it saves (2.89 vs 2.38 ms/step, profiles/r1_ab_fused_adam_fixup.txt).
-int g_fixup = -1;
-bool fixup_enabled() {
-  if (g_fixup < 0) {
-    const char* e = getenv("FD_GEMM_FIXUP");
-    g_fixup = (e && atoi(e) != 0) ? 1 : 0;
-  }
-  return g_fixup == 1;
-}
-
 // Launch the weight-gradient GEMM(s) ps[0..nprob) (ps[i].C = final fp32 gradient, k_split
-// unset) with `splits` K splits: direct (one split), in-kernel split-K fixup (arrival
-// counters), or legacy slabs + reduce.  adams[i].p != nullptr fuses Adam into the epilogue
-// (direct / fixup only: the legacy path falls back to one split).
+// unset) with `splits` K splits: direct (one split) or fp32 slabs + a deterministic reduce.
+// adams[i].p != nullptr fuses Adam into the epilogue (one split only).
 int dw_launch(GemmParams* ps, int nprob, int id, int splits, int K, float* workspace, long long workspace_elems,
-              int accumulate, int* cnt, long long ncnt, const FdAdamEpi* adams, int defer, int* splits_out,
-              hipStream_t st) {
+              int accumulate, const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st) {
   if (splits_out) *splits_out = 0;
-  long long tiles = 0, slab_total = 0;
+  long long slab_total = 0;
   bool fused = false;
   for (int i = 0; i < nprob; ++i) {
-    tiles += tiles_of(id, ps[i].M, ps[i].N);
     slab_total += (long long)ps[i].M * ps[i].N;
     if (adams && adams[i].p) fused = true;
   }
   if (splits > 1 && workspace_elems < slab_total * splits) splits = 1;
-  const bool fix = splits > 1 && cnt != nullptr && ncnt >= tiles && fixup_enabled();
-  if (splits > 1 && !fix && fused) splits = 1;
+  if (splits > 1 && fused) splits = 1;
   float* finals[2] = {(float*)ps[0].C, nprob > 1 ? (float*)ps[1].C : nullptr};
   long long off = 0;
   for (int i = 0; i < nprob; ++i) {
@@ -1424,20 +1238,19 @@ int dw_launch(GemmParams* ps, int nprob, int id, int splits, int K, float* works
     p.accumulate = accumulate;
     if (adams) p.adam = adams[i];
     if (splits == 1) {
-      p.out = finals[i]; p.tile_cnt = nullptr; p.slab_stride = 0;
+      p.out = finals[i]; p.slab_stride = 0;
     } else {
       p.C = workspace + off; p.slab_stride = (long long)p.M * p.N; p.ldc = p.N;
       off += p.slab_stride * splits;
-      p.out = fix ? finals[i] : nullptr;
-      p.tile_cnt = fix ? cnt : nullptr;
+      p.out = nullptr;
     }
   }
   if (!launch_id<false, false, EPI_F32>(ps[0], id, splits, st, nprob > 1 ? &ps[1] : nullptr)) return 7;
-  if (splits > 1 && !fix && defer) {  // the caller reduces the slabs later (fd_splitk_reduce_batched)
+  if (splits > 1 && defer) {  // the caller reduces the slabs later (fd_splitk_reduce_batched)
     if (splits_out) *splits_out = splits;
     return 0;
   }
-  if (splits > 1 && !fix) {
+  if (splits > 1) {
     for (int i = 0; i < nprob; ++i) {
       const long long n4 = ps[i].slab_stride / 4;
       const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
@@ -1453,9 +1266,17 @@ int dw_launch(GemmParams* ps, int nprob, int id, int splits, int K, float* works
 // ---------------------------------------------------------------- C ABI
 extern "C" {
 
-int fd_gemm_set_fixup(int on) {
-  g_fixup = on ? 1 : 0;
-  return 0;
+// Copy the diagnostic stamps (FD_GEMM_STAMPS builds) of blocks [0, nblocks) to host memory
+// [nblocks][8]; -1 in a normal build.
+int fd_gemm_stamps(unsigned long long* host, int nblocks) {
+#if FD_GEMM_STAMPS
+  if (nblocks > STAMP_MAXB) nblocks = STAMP_MAXB;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * nblocks, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? nblocks : -2;
+#else
+  (void)host; (void)nblocks;
+  return -1;
+#endif
 }
 
 // Force a configuration id / split count for a GEMM kind (tuning; -1 = auto).
@@ -1470,21 +1291,21 @@ int fd_gemm_set_cfg(int kind, int cfg, int splits) {
 // Returns 0 on success, nonzero on unsupported shape.
 int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
-               long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+               long long workspace_elems, int accumulate, const FdAdamEpi* adam,
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st);
 
 int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
             const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
-            long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+            long long workspace_elems, int accumulate, const FdAdamEpi* adam,
             float* colsum, int* colsum_blocks, hipStream_t st) {
   return fd_gemm_ex(kind, epi, A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, res, ldres, workspace,
-                    workspace_elems, accumulate, tile_cnt, ncnt, adam, colsum, colsum_blocks, nullptr, st);
+                    workspace_elems, accumulate, adam, colsum, colsum_blocks, nullptr, st);
 }
 
 // fd_gemm + aux_out: the GELU' epilogue also re-creates gelu(aux) (nullable; EPI_GELU_BWD only).
 int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
-               long long workspace_elems, int accumulate, int* tile_cnt, long long ncnt, const FdAdamEpi* adam,
+               long long workspace_elems, int accumulate, const FdAdamEpi* adam,
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st) {
   if (K % BKT != 0 || N % 64 != 0 || M <= 0 || kind < 0 || kind > 2 || epi >= EPI_LN) return 1;
   if (aux_out && (epi != EPI_GELU_BWD || kind == 2)) return 7;
@@ -1521,16 +1342,6 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
     p.colsum = colsum;
     if (colsum_blocks) *colsum_blocks = (M + CFGS[id].bm - 1) / CFGS[id].bm;
   }
-  if (kind == 0 && epi == EPI_F32) {
-    // fp32 split-K partials of an NT product into workspace slabs [splits][M][N] (no reduce:
-    // the caller reduces and applies the epilogue); splits from FD_GEMM_SPLITS (default 2)
-    const int so = splits_override();
-    const int splits = so > 0 ? so : 2;
-    if (K % (splits * BKT) != 0 || workspace_elems < (long long)splits * M * N) return 6;
-    p.k_split = K / splits;
-    p.C = workspace; p.ldc = N; p.slab_stride = (long long)M * N;
-    return launch_epi<true, true>(EPI_F32, p, id, splits, st) ? 0 : 2;
-  }
   if (kind == 0) {  // also dX = dy (W^T)^T with a transposed weight copy: GELU' / residual epilogues
     if (epi == EPI_F32) return 2;
     if (launch_epi<true, true>(epi, p, id, 1, st)) return 0;
@@ -1555,8 +1366,34 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
     while (tiles * splits < 400 && (K / (splits * 2)) % BKT == 0 && K / (splits * 2) >= 512) splits *= 2;
   }
   if (ldc != N) return 4;
-  return dw_launch(&p, 1, id, splits, K, workspace, workspace_elems, accumulate, tile_cnt, ncnt, adam, 0, nullptr,
-                   st);
+  return dw_launch(&p, 1, id, splits, K, workspace, workspace_elems, accumulate, adam, 0, nullptr, st);
+}
+
+// Split-K NT product into fp32 slabs: slabs[z][M][N] = A[M][k in split z] Bt[N][k in split z]^T
+// (A [M][lda], Bt [N][ldb] bf16, K % (64 * splits) == 0), one launch of splits x tiles blocks --
+// the small-M GEMMs (the pruned block's [CLS] rows) on the whole chip instead of a dozen CUs.
+// The caller reduces the slabs and applies the epilogue (splitk.hip fd_splitk_epilogue).
+// splits <= 0: picked here (largest divisor of K / 64 that keeps >= 2 K tiles per block and the
+// grid within one round of 256 blocks); returns the split count used, or a negative error.
+int fd_gemm_f32_splits(const void* A, const void* Bt, float* slabs, long long slab_elems, int M, int N, int K,
+                       int lda, int ldb, int splits, hipStream_t st) {
+  if (M <= 0 || K % BKT || N % 64 || !A || !Bt || !slabs) return -1;
+  const int id = M <= 64 ? 13 : 8;
+  const long long tiles = tiles_of(id, M, N);
+  const int nkt = K / BKT;
+  if (splits <= 0) {
+    splits = 1;
+    for (int s = 1; s <= nkt; ++s)
+      if (nkt % s == 0 && tiles * s <= 256 && nkt / s >= 2) splits = s;
+  }
+  if (nkt % splits || slab_elems < (long long)splits * M * N) return -2;
+  GemmParams p{};
+  p.A = (const bf16_t*)A; p.B = (const bf16_t*)Bt; p.C = slabs;
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = N;
+  p.k_split = K / splits;
+  p.slab_stride = (long long)M * N;
+  p.group_m = 1;
+  return launch_id<true, true, EPI_F32>(p, id, splits, st) ? splits : -3;
 }
 
 // Two weight-gradient GEMMs over the same token dimension in ONE launch:
@@ -1596,8 +1433,8 @@ int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K) {
 }
 
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
-                int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate, int* tile_cnt,
-                long long ncnt, const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st) {
+                int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate,
+                const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st) {
   if (K % BKT != 0 || M0 % 128 || M1 % 128 || N0 % 64 || N1 % 64 || M0 <= 0 || M1 <= 0) return 1;
   const int id = dw2_cfg(M0, N0, M1, N1);
   static const int diag = [] { const char* e = getenv("FD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
@@ -1615,8 +1452,7 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
   }
   const int splits = fd_gemm_dw2_splits(M0, N0, M1, N1, K);
   if (splits <= 0) return 6;
-  return dw_launch(p, 2, id, splits, K, workspace, workspace_elems, accumulate, tile_cnt, ncnt, adams, defer,
-                   splits_out, st);
+  return dw_launch(p, 2, id, splits, K, workspace, workspace_elems, accumulate, adams, defer, splits_out, st);
 }
 
 // All-layer weight gradients in one launch (gemm_dw_batch_kernel).  probs[i] = {A, B, C, p, m,
@@ -1639,45 +1475,10 @@ bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
     if (!dry) hipLaunchKernelGGL(kern, dim3(t), dim3(threads), 0, st, bt);
     return true;
   };
-  // persistent variants: slots x CUs blocks, the second slot delayed by FD_DWB_DELAY_NS
-  static const int ncu = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    return n > 0 ? n : 256;
-  }();
-  static const long long delay = [] { const char* e = getenv("FD_DWB_DELAY_NS"); return e ? atoll(e) : 20000ll; }();
-  auto persist = [&](auto kern, int bm, int bn, int threads, int slots) {
-    for (int i = 0; i < bt.n; ++i)
-      if (bt.pr[i].M % bm || bt.pr[i].N % bn) return false;
-    int t = 0;
-    for (int i = 0; i < bt.n; ++i) {
-      bt.pr[i].tile0 = t;
-      t += (bt.pr[i].M / bm) * (bt.pr[i].N / bn);
-    }
-    bt.ntiles = t;
-    if (!dry) hipLaunchKernelGGL(kern, dim3(slots * ncu), dim3(threads), 0, st, bt, slots > 1 ? delay : 0ll);
-    return true;
-  };
   switch (id) {
-    case 41: return persist(gemm_dw_batch_persist_kernel<256, 256, 2, 4, 2>, 256, 256, 512, 1);
-    case 42: return persist(gemm_dw_batch_persist_kernel<128, 128, 2, 2, 2>, 128, 128, 256, 2);
-    case 43: return persist(gemm_dw_batch_persist_kernel<128, 128, 2, 2, 3>, 128, 128, 256, 2);
-    case 44: return persist(gemm_dw_batch_persist_kernel<256, 128, 4, 2, 2>, 256, 128, 512, 1);
-    case 0: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 3>, 128, 64, 256);
     case 1: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 2>, 128, 128, 256);
-    case 4: return go(gemm_dw_batch_kernel<256, 128, 4, 2, 3>, 256, 128, 512);
     case 8: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 2>, 128, 64, 256);
-    case 10: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 3>, 128, 128, 256);
-    case 12: return go(gemm_dw_batch_kernel<256, 128, 4, 2, 2>, 256, 128, 512);
-    case 15: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 4>, 128, 64, 256);
-    case 21: return go(gemm_dw_batch_kernel<128, 128, 4, 2, 3>, 128, 128, 512);
-    case 3: return go(gemm_dw_batch_kernel<256, 192, 4, 2, 2>, 256, 192, 512);
-    case 6: return go(gemm_dw_batch_kernel<128, 192, 2, 4, 2>, 128, 192, 512);
     case 11: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 2>, 256, 256, 512);
-    // register-pipelined K loop (gemm_tile_at PIPE)
-    case 33: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 3, true>, 128, 128, 256);
-    case 34: return go(gemm_dw_batch_kernel<256, 128, 4, 2, 3, true>, 256, 128, 512);
   }
   return false;
 }
@@ -1789,22 +1590,16 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   const int tiles_m = (M + bm - 1) / bm;
   const dim3 grid(tiles_m * (N / bn));
   auto go = [&](auto kern, int threads) { hipLaunchKernelGGL(kern, grid, dim3(threads), 0, st, p); };
-#define FD_LN_CASE_P(ID, BM_, BN_, WM_, WN_, S_, P_)                                        \
-  case ID:                                                                                 \
-    if (bwd) go(gemm_ln_kernel<BM_, BN_, EPI_LN_BWD, WM_, WN_, S_, P_>, 64 * WM_ * WN_);   \
-    else go(gemm_ln_kernel<BM_, BN_, EPI_LN, WM_, WN_, S_, P_>, 64 * WM_ * WN_);           \
+#define FD_LN_CASE(ID, BM_, BN_, WM_, WN_, S_)                                          \
+  case ID:                                                                             \
+    if (bwd) go(gemm_ln_kernel<BM_, BN_, EPI_LN_BWD, WM_, WN_, S_>, 64 * WM_ * WN_);   \
+    else go(gemm_ln_kernel<BM_, BN_, EPI_LN, WM_, WN_, S_>, 64 * WM_ * WN_);           \
     break;
-#define FD_LN_CASE(ID, BM_, BN_, WM_, WN_, S_) FD_LN_CASE_P(ID, BM_, BN_, WM_, WN_, S_, false)
   switch (id) {
     FD_LN_CASE(24, 128, 64, 4, 2, 6)
     FD_LN_CASE(0, 128, 64, 2, 2, 3)
     FD_LN_CASE(18, 128, 64, 4, 2, 3)
     FD_LN_CASE(13, 64, 64, 2, 2, 3)
-    // register-pipelined K loop (gemm_tile_at PIPE)
-    FD_LN_CASE_P(30, 128, 64, 4, 2, 6, true)
-    FD_LN_CASE_P(31, 128, 64, 4, 2, 4, true)
-    FD_LN_CASE_P(32, 128, 64, 2, 2, 6, true)
-    FD_LN_CASE_P(33, 128, 64, 2, 2, 4, true)
     default: return -3;
   }
 #undef FD_LN_CASE

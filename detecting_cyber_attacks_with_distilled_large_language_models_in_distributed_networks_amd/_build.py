@@ -25,7 +25,8 @@ from concurrent.futures import ThreadPoolExecutor
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(REPO, "csrc")
-BUILD = os.path.join(REPO, "build", "native")
+# experiment builds keep their objects apart (FD_BUILD_TAG=stamps -> build/native_stamps)
+BUILD = os.path.join(REPO, "build", "native" + ("_" + os.environ["FD_BUILD_TAG"] if os.environ.get("FD_BUILD_TAG") else ""))
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -33,7 +34,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 EXTRA = os.environ.get("FD_HIP_EXTRA_FLAGS", "").split()
 
 SO_DIR = os.path.join(REPO, "_so")
-HIP_OUT = os.path.join(SO_DIR, "_hip_kernels.so")
+# FD_SO_OUT: write (and load) the kernel library elsewhere, e.g. ab/stamps.so for a diagnostic build
+HIP_OUT = os.environ.get("FD_SO_OUT") or os.path.join(SO_DIR, "_hip_kernels.so")
 TEXT_OUT = os.path.join(SO_DIR, "_text_native_impl.so")
 
 
@@ -133,7 +135,7 @@ def build_hip(verbose=False, force=False, jobs=None) -> str:
         with ThreadPoolExecutor(n) as ex:
             list(ex.map(lambda j: _run(j[0], verbose), jobs_list))
     if force or jobs_list or _newer(HIP_OUT, objs):
-        os.makedirs(SO_DIR, exist_ok=True)
+        os.makedirs(os.path.dirname(HIP_OUT), exist_ok=True)
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + [
             "-L" + libdir, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
             "-ldl",  # RCCL is bound at run time from torch's copy (csrc/comm/rccl_comm.cpp)

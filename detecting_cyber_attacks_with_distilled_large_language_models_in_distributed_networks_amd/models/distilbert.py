@@ -252,12 +252,11 @@ class DDoSClassifier(nn.Module):
         # HIP path: backward dX GEMMs read W^T copies (K-major staging is ~30% faster than
         # reading W MN-major; the per-step transpose of the encoder weights is ~85 MB r+w)
         self.transposed_dx = True
-        # HIP path: weight-gradient work of the backward on a side stream (ops/functional.py).
-        # Bitwise identical either way; measured on MI355X at bs32 x seq128 (scripts/gpu_ab.sh,
-        # 3 A/B pairs): 3.24 ms/step with vs 3.20 without -- the concurrent dW and dX grids slow
-        # each other ~30 % (LDS-bound co-residency), so the gain is eaten.  Off by default.
-        self.wgrad_stream = False
-        self._wgrad = None
+        # (Removed after losing their A/B, logs in profiles/: the weight-gradient GEMMs on a side
+        # stream -- 3.24 vs 3.20 ms/step, r1_ab_wgrad_side_stream.txt; the W^T copies on a side
+        # stream during the forward -- 2.48 vs 2.36, r1_ab_transpose_overlap_slower.txt; the
+        # embedding backward + column-sum flush beside the dW launch -- neutral,
+        # r2_ab_tail_overlap_groupm.txt.)
         # HIP path: grouped weight-gradient GEMMs (RunCtx.group_dw)
         self.group_dw = True
         # HIP path: every weight gradient of the step in one launch at the end of the backward
@@ -284,16 +283,6 @@ class DDoSClassifier(nn.Module):
         # at once: off when other processes share this GPU (e.g. several gloo clients on one card),
         # whose kernels could hold CUs through a rendezvous (a timeout is fatal: check_ln_error).
         self.fuse_ln = os.environ.get("FD_FUSE_LN", "1") != "0" and not gpu_shared()
-        # HIP path: build the per-step W^T copies on a side stream concurrently with the forward.
-        # Measured SLOWER on MI355X (2.48 vs 2.36 ms/step, profiles/r1_ab_transpose_overlap_slower.txt):
-        # the memory-bound transposes stretch the concurrent forward GEMMs.  Off by default.
-        self.overlap_transpose = False
-        self._tstream = None
-        # HIP path: at the end of the backward, run the embedding backward and the deferred
-        # column-sum flush on a side stream while the all-layer weight-gradient launch runs
-        # (RunCtx.tail_stream; FD_OVERLAP_TAIL=0: serial).  The dW grid's last round leaves
-        # ~half the CUs idle; the small, latency-bound tail kernels fill them.
-        self.overlap_tail = os.environ.get("FD_OVERLAP_TAIL", "0") != "0"
         # HIP path (with batch_dw): the per-block qkv-bias column-sum partials in one launch at the
         # end of the backward (RunCtx.colsum_pending; FD_BATCH_COLSUM=0: one launch per block)
         self.batch_colsum = os.environ.get("FD_BATCH_COLSUM", "1") != "0"
@@ -303,7 +292,6 @@ class DDoSClassifier(nn.Module):
         # HIP path: the last block runs its out-proj / FFN / LayerNorms on the [CLS] rows only
         # (exact: no other row of its output reaches the loss; FD_PRUNE_LAST=0: every row)
         self.prune_last = os.environ.get("FD_PRUNE_LAST", "1") != "0"
-        self._tail = None
         # optimizer that applies Adam inside the weight-gradient GEMM epilogues; set only for
         # the duration of a training step (engine/train.py fused_adam_scope)
         self.fused_opt = None
@@ -333,9 +321,6 @@ class DDoSClassifier(nn.Module):
         self.emb_ever = torch.zeros(V, dtype=torch.uint8, device=dev) if dev.type == "cuda" else None
         self._grad_token = torch.zeros((), device=dev, requires_grad=True)
         self._hip_cache = None
-        self._wgrad = None
-        self._tstream = None
-        self._tail = None
         self._synced_version = -1
         return self
 
@@ -500,32 +485,25 @@ class DDoSClassifier(nn.Module):
             emb["pos"].copy_(A.view("distilbert.embeddings.position_embeddings.weight")
                              + A.view("distilbert.embeddings.token_type_embeddings.weight")[0])
         grad = torch.is_grad_enabled()
-        if grad and self.wgrad_stream and self._wgrad is None:
-            self._wgrad = torch.cuda.Stream(device=self.arena.device)
         packed = tokens is not None and self.unpad and self.packed_rows(tokens, B, S) < B * S
         # varlen attention masks keys by sequence length; the padded path needs the additive bias
         kbias = self._no_bias() if packed else K.mask_bias(mask)
         rc = RunCtx(B=B, S=S, H=cfg.n_heads, kbias=kbias, seed=self.rng, training=self.training,
                     eps=cfg.layer_norm_eps, p_hidden=cfg.dropout, p_attn=cfg.attention_dropout, p_head=self.dropout.p,
-                    on_layer_grads=self.layer_grads_hook if grad else None,
-                    wgrad=self._wgrad if grad and self.wgrad_stream else None, group_dw=self.group_dw)
+                    on_layer_grads=self.layer_grads_hook if grad else None, group_dw=self.group_dw)
         if grad and self.defer_colsum and self.layer_grads_hook is None:
             rc.colsum_jobs = []  # (a per-block hook needs each block's grads final at once)
         if grad and self.defer_dw_reduce and self.layer_grads_hook is None:
             rc.dw_jobs = []
-        if grad and self.batch_dw and self.layer_grads_hook is None and not self.wgrad_stream:
+        if grad and self.batch_dw and self.layer_grads_hook is None:
             rc.dw_batch = []
             if rc.colsum_jobs is not None and self.batch_colsum:
                 rc.colsum_pending = []
-            if self.overlap_tail and ids.is_cuda:
-                if self._tail is None:
-                    self._tail = torch.cuda.Stream(device=self.arena.device)
-                rc.tail_stream = self._tail
         rc.fuse_colsum = self.fuse_colsum
         rc.remat_gelu = self.remat_gelu
         rc.fuse_ln = self.fuse_ln and cfg.dim % 64 == 0 and cfg.dim <= 2048
         if (grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None
-                and not self.wgrad_stream and self.transposed_dx):
+                and self.transposed_dx):
             rc.fused_adam = self.fused_opt
         plan = self._prune_plan(rc, layers, grad)
         # packed step: the counters ride on the packing launch (no kernel of their own)
@@ -541,17 +519,7 @@ class DDoSClassifier(nn.Module):
         if token is not None and self.transposed_dx:
             srcs = [L[k] for L in layers for k in L["wT"]]
             dsts = [L["wT"][k] for L in layers for k in L["wT"]]
-            if self.overlap_transpose:
-                # the W^T copies are first read by the backward: build them on a side stream
-                # while the forward runs (joined at the head's backward, the first backward node)
-                if self._tstream is None:
-                    self._tstream = torch.cuda.Stream(device=self.arena.device)
-                self._tstream.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(self._tstream):
-                    K.transpose_many(srcs, dsts)
-                rc.join_stream = self._tstream
-            else:
-                K.transpose_many(srcs, dsts)
+            K.transpose_many(srcs, dsts)
         if packed:
             # Unpadded step: only the real tokens (sequence-contiguous, filler rows at the end)
             # are embedded and run through the blocks; varlen attention over cu; positions and
@@ -588,7 +556,7 @@ class DDoSClassifier(nn.Module):
         Bp = (B + 63) // 64 * 64
         if not (self.prune_last and rc.fuse_ln and layers and K.ln_fusable(Bp, D) and Bp <= rc.B * rc.S):
             return None
-        if grad and (rc.dw_batch is None or rc.wgrad is not None or "wT" not in layers[-1]):
+        if grad and (rc.dw_batch is None or "wT" not in layers[-1]):
             return None
         dev = self.arena.device
         key = (B, S, Bp, str(dev))

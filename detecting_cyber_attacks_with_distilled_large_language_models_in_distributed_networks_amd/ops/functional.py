@@ -38,11 +38,6 @@ class RunCtx:
     # called with the layer index once a block's parameter gradients are final
     # (lets the optimizer update that block on a side stream during the rest of backward)
     on_layer_grads: Optional[Callable[[int], None]] = None
-    # side stream for the weight-gradient work (dW GEMMs, split-K reduces, bias column
-    # sums): it is off the backward's critical path (dX -> LN bwd -> attention bwd ->
-    # dX ...), so it runs concurrently with it and fills the CUs the one-round dX grids
-    # leave idle.  Joined at the end of the embedding backward (the last node).
-    wgrad: Optional["torch.cuda.Stream"] = None
     # launch the weight gradients that become ready together (lin2 + lin1, out_lin + qkv)
     # as one grouped GEMM grid (fewer split-K slab round trips; csrc/kernels/gemm.hip)
     group_dw: bool = True
@@ -61,9 +56,6 @@ class RunCtx:
     # FFN activation g = gelu(u) not kept by the forward: the backward's GELU' dX GEMM re-creates
     # it next to its consumer (lin2's dW), so ~16.5 MB/layer less stays live across the step
     remat_gelu: bool = True
-    # side stream that produced data the backward reads (the W^T copies): joined at the
-    # first backward node (the head)
-    join_stream: Optional["torch.cuda.Stream"] = None
     # LayerNorm fused into the N = hidden GEMMs (csrc/kernels/gemm.hip gemm_ln_kernel): forward
     # out_lin + sa_layer_norm and lin2 + output_layer_norm; backward sa_layer_norm inside the
     # lin1 dX GEMM and block i-1's output_layer_norm inside block i's qkv dX GEMM
@@ -77,9 +69,6 @@ class RunCtx:
     # last backward node launches every weight gradient of the step as ONE grid
     # (ops/kernels.py linear_dw_batch; with ``fused_adam`` the Adam step runs in its epilogue)
     dw_batch: Optional[list] = None
-    # with dw_batch: side stream for the embedding backward + column-sum flush, concurrent with
-    # the all-layer weight-gradient launch (joined before the embedding node returns)
-    tail_stream: Optional["torch.cuda.Stream"] = None
     # with dw_batch + colsum_jobs: bf16 column sums whose source stays alive to the end of the
     # backward anyway (each block's dqkv, kept for the dW launch) -- their partials are computed
     # in ONE launch at the end (ops/kernels.py colsum_partials_batched) instead of one per block
@@ -97,27 +86,6 @@ class RunCtx:
     cls_rows: Optional[torch.Tensor] = None
     cls_rmap: Optional[torch.Tensor] = None
     head_rows: Optional[torch.Tensor] = None
-
-
-class _WGrad:
-    """Fork weight-gradient work onto ``rc.wgrad`` (no-op without a side stream)."""
-
-    def __init__(self, rc: RunCtx):
-        self.side = rc.wgrad
-        self.cur = torch.cuda.current_stream() if self.side is not None else None
-
-    def fork(self, *tensors):
-        """Side stream waits for everything issued so far; ``tensors`` may be freed by
-        the main stream while the side stream still reads them -> record the use."""
-        if self.side is None:
-            return
-        self.side.wait_stream(self.cur)
-        for t in tensors:
-            t.record_stream(self.side)
-
-    def ctx(self):
-        import contextlib
-        return torch.cuda.stream(self.side) if self.side is not None else contextlib.nullcontext()
 
 
 class GradSink:
@@ -147,22 +115,8 @@ class EmbeddingFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        rc = ctx.rc
-        tail = rc.tail_stream if rc.dw_batch and rc.wgrad is None else None
-        if tail is None:
-            EmbeddingFn._tail(ctx, dy)
-            EmbeddingFn._weights(rc)
-            return (None,) * 8
-        # The all-layer weight gradients (one big grid) go first on the main stream; the
-        # embedding backward and the column-sum flush -- independent of them -- run on the side
-        # stream and take the CUs the dW grid's partial last round leaves idle.  Every tensor
-        # the side stream touches stays referenced until the join below.
-        cur = torch.cuda.current_stream()
-        tail.wait_stream(cur)
-        EmbeddingFn._weights(rc)
-        with torch.cuda.stream(tail):
-            EmbeddingFn._tail(ctx, dy)
-        cur.wait_stream(tail)
+        EmbeddingFn._tail(ctx, dy)
+        EmbeddingFn._weights(ctx.rc)
         return (None,) * 8
 
     @staticmethod
@@ -197,8 +151,6 @@ class EmbeddingFn(torch.autograd.Function):
             g = tt.buf
             torch.sum(s["pos"].buf, 0, out=g[0])
             g[1:].zero_()
-        if ctx.rc.wgrad is not None:  # join the weight-gradient stream: every grad is final after this node
-            torch.cuda.current_stream().wait_stream(ctx.rc.wgrad)
         if ctx.rc.colsum_pending:
             K.colsum_partials_batched(ctx.rc.colsum_pending, ctx.rc.colsum_jobs)
         if ctx.rc.colsum_jobs:
@@ -340,7 +292,6 @@ class LayerFn(torch.autograd.Function):
         attn_site, ffn_site = ctx.sites
         p_a, p_h = ctx.p
         acc = G["l2_w"].accumulate()
-        wg = _WGrad(rc)  # dW / bias-sum work -> side stream, dX chain stays on the main stream
         # output_layer_norm(dropout(lin2) + h): dz2 -> residual grad of h, df -> lin2 output grad
         jobs = rc.colsum_jobs
         fused = ctx.fused_ln
@@ -356,29 +307,26 @@ class LayerFn(torch.autograd.Function):
         # this backward, so every later reader must use the W^T copies taken before the step
         batch = rc.dw_batch  # all-layer weight gradients: record now, one launch at the end
         fa = rc.fused_adam if batch is None else None
-        if fa is not None and (acc or not rc.group_dw or rc.wgrad is not None or wt.get("l1_w") is None
-                               or wt.get("qkv_w") is None):
+        if fa is not None and (acc or not rc.group_dw or wt.get("l1_w") is None or wt.get("qkv_w") is None):
             fa = None
-        # dg W2 * gelu'(u); with deferred column sums and no weight-gradient side stream the
-        # epilogue also leaves lin1's bias-gradient partials (no separate pass over du)
-        fuse_cs = jobs is not None and rc.wgrad is None and rc.fuse_colsum and wt.get("l2_w") is not None
+        # dg W2 * gelu'(u); with deferred column sums the epilogue also leaves lin1's bias-gradient
+        # partials (no separate pass over du)
+        fuse_cs = jobs is not None and rc.fuse_colsum and wt.get("l2_w") is not None
         g_out = torch.empty_like(u) if g is None else None  # re-created gelu(u) (RunCtx.remat_gelu)
         du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"),
                          colsum=(jobs, G["l1_b"].buf, acc) if fuse_cs else None, aux_out=g_out)
         if g is None:
             g = g_out
-        wg.fork(df, g, du, h)
-        with wg.ctx():
-            if batch is not None:
-                batch += [(df, g, G["l2_w"].buf, acc), (du, h, G["l1_w"].buf, acc)]
-            elif rc.group_dw:
-                K.linear_dw2(df, g, G["l2_w"].buf, du, h, G["l1_w"].buf, acc,
-                             adam=fa.fused_args([G["l2_w"].buf, G["l1_w"].buf]) if fa else None, jobs=rc.dw_jobs)
-            else:
-                K.linear_dw(df, g, G["l2_w"].buf, acc)
-                K.linear_dw(du, h, G["l1_w"].buf, acc)
-            if not fuse_cs:
-                K.colsum(du, G["l1_b"].buf, acc, jobs)
+        if batch is not None:
+            batch += [(df, g, G["l2_w"].buf, acc), (du, h, G["l1_w"].buf, acc)]
+        elif rc.group_dw:
+            K.linear_dw2(df, g, G["l2_w"].buf, du, h, G["l1_w"].buf, acc,
+                         adam=fa.fused_args([G["l2_w"].buf, G["l1_w"].buf]) if fa else None, jobs=rc.dw_jobs)
+        else:
+            K.linear_dw(df, g, G["l2_w"].buf, acc)
+            K.linear_dw(du, h, G["l1_w"].buf, acc)
+        if not fuse_cs:
+            K.colsum(du, G["l1_b"].buf, acc, jobs)
         # sa_layer_norm(out_lin + x): dh = du W1 + dz2, then its LayerNorm backward
         if fused and wt.get("l1_w") is not None:
             dz1, _ = K.linear_dx_ln_bwd(du, wt["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
@@ -390,23 +338,19 @@ class LayerFn(torch.autograd.Function):
                               G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, zin=fused)
         dcx = K.linear_dx(dz1, L["o_w"], wt=wt.get("o_w"))
         if not rc.group_dw and batch is None:
-            wg.fork(dz1, cx)
-            with wg.ctx():
-                K.linear_dw(dz1, cx, G["o_w"].buf, acc)
+            K.linear_dw(dz1, cx, G["o_w"].buf, acc)
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask)
-        wg.fork(dqkv, x, dz1, cx)
-        with wg.ctx():
-            if batch is not None:
-                batch += [(dz1, cx, G["o_w"].buf, acc), (dqkv, x, G["qkv_w"].buf, acc)]
-            elif rc.group_dw:
-                K.linear_dw2(dz1, cx, G["o_w"].buf, dqkv, x, G["qkv_w"].buf, acc,
-                             adam=fa.fused_args([G["o_w"].buf, G["qkv_w"].buf]) if fa else None, jobs=rc.dw_jobs)
-            else:
-                K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
-            if batch is not None and jobs is not None and rc.colsum_pending is not None:
-                rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))  # partials at the end, batched
-            else:
-                K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
+        if batch is not None:
+            batch += [(dz1, cx, G["o_w"].buf, acc), (dqkv, x, G["qkv_w"].buf, acc)]
+        elif rc.group_dw:
+            K.linear_dw2(dz1, cx, G["o_w"].buf, dqkv, x, G["qkv_w"].buf, acc,
+                         adam=fa.fused_args([G["o_w"].buf, G["qkv_w"].buf]) if fa else None, jobs=rc.dw_jobs)
+        else:
+            K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
+        if batch is not None and jobs is not None and rc.colsum_pending is not None:
+            rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))  # partials at the end, batched
+        else:
+            K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
         prev = rc.ln2_saved.get(ctx.idx - 1) if fused and wt.get("qkv_w") is not None else None
         if prev is not None:
             # dx = dqkv Wqkv + dz1 is block idx-1's output-LN gradient: finish that LayerNorm
@@ -427,8 +371,7 @@ class LayerFn(torch.autograd.Function):
             G[k].accumulate()
         del ctx.acts, ctx.dmask
         if rc.on_layer_grads is not None:
-            with wg.ctx():  # ordered after this block's dW work (and, via the forks, its LN grads)
-                rc.on_layer_grads(ctx.idx)
+            rc.on_layer_grads(ctx.idx)  # (stream-ordered after this block's dW work and LN grads)
         return dx, None, None, None
 
 
@@ -456,8 +399,6 @@ class HeadFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g0, g1):
-        if ctx.rc.join_stream is not None:
-            torch.cuda.current_stream().wait_stream(ctx.rc.join_stream)
         (hidden,) = ctx.saved_tensors
         gscale = None
         if ctx.fused_loss:

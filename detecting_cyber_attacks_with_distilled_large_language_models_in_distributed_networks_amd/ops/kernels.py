@@ -46,12 +46,38 @@ def _drop(p: float):
 
 # ------------------------------------------------------------------ GEMMs
 EPI_BF16, EPI_BIAS, EPI_BIAS_GELU, EPI_GELU_BWD, EPI_ADD = 0, 1, 2, 3, 4
+EPI_LN, EPI_LN_BWD = 6, 7
+
+# Small-M GEMMs (the pruned last block's [CLS] rows, M = 64): split over K into fp32 slabs and
+# reduced by one epilogue launch (csrc/kernels/splitk.hip) -- the single-pass kernels would run
+# the whole K loop on the dozen CUs its 64 x 64 tiles cover.  FD_SPLITK_SMALLM=0: off.
+import os as _os
+SPLITK_MAX_M = 64 if _os.environ.get("FD_SPLITK_SMALLM", "1") != "0" else 0
+
+
+def _splitk_ok(M: int, N: int, K: int) -> bool:
+    return 0 < M <= SPLITK_MAX_M and N % 64 == 0 and K % 64 == 0
+
+
+def _splitk(epi, x, wt, y, **kw):
+    """One split-K GEMM + epilogue (``ext().gemm_splitk``) on the shared slab workspace (slabs
+    are consumed by the epilogue launch right behind the GEMM on the same stream)."""
+    M, N = x.shape[0], wt.shape[0]
+    ws = workspace(x.device, "splitk_small", 256 * M * N // max(1, ((M + 63) // 64) * (N // 64)) + M * N)
+    return ext().gemm_splitk(epi, x, wt, y, ws, **kw)
 
 
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu: bool = False):
     """y = x w^T + b (bf16), optionally also returning u (pre-GELU) with y = gelu(u)."""
     M, N = x.shape[0], w.shape[0]
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    if _splitk_ok(M, N, x.shape[1]):
+        if gelu:
+            u = torch.empty_like(y)
+            _splitk(EPI_BIAS_GELU, x, w, y, bias=b, aux=u)
+            return y, u
+        _splitk(EPI_BIAS if b is not None else EPI_BF16, x, w, y, bias=b)
+        return y
     if gelu:
         u = torch.empty_like(y)
         ext().gemm(0, EPI_BIAS_GELU, x, w, y, b, u, None, None, False)
@@ -73,6 +99,19 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] 
     gelu(gelu_u) there -- the forward's activation, bitwise.  Returns dx."""
     M, N = dy.shape[0], w.shape[1]
     dx = torch.empty(M, N, dtype=torch.bfloat16, device=dy.device)
+    if wt is not None and _splitk_ok(M, N, dy.shape[1]):
+        epi = EPI_GELU_BWD if gelu_u is not None else (EPI_ADD if res is not None else EPI_BF16)
+        if colsum is not None:
+            if epi == EPI_BF16:
+                raise ValueError("fused column sums need a GELU' / residual epilogue")
+            jobs, out, acc = colsum
+            cs = workspace(dy.device, f"colsum_job{len(jobs)}", ((M + 31) // 32) * N)
+            _, nblk = _splitk(epi, dy, wt, dx, aux=gelu_u, aux_out=aux_out if gelu_u is not None else None, res=res,
+                              colsum=cs)
+            jobs.append((cs, [out], nblk, N, N, acc))
+            return dx
+        _splitk(epi, dy, wt, dx, aux=gelu_u, aux_out=aux_out if gelu_u is not None else None, res=res)
+        return dx
     if colsum is not None and wt is not None and (gelu_u is not None or res is not None):
         jobs, out, acc = colsum
         ws = workspace(dy.device, f"colsum_job{len(jobs)}", ((M + 127) // 128) * N)
@@ -100,35 +139,15 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] 
     return dx
 
 
-TILE_COUNTERS = 8192
-
-
-def tile_counters(device) -> torch.Tensor:
-    """Split-K arrival counters of the weight-gradient GEMMs (zeroed once; every launch
-    leaves them at zero again).  Fixed size, never reallocated: graphs keep the pointer."""
-    key = (str(device), "tile_cnt", torch.int32)
-    t = _WS.get(key)
-    if t is None:
-        t = torch.zeros(TILE_COUNTERS, dtype=torch.int32, device=device)
-        _WS[key] = t
-    return t
-
-
-def set_splitk_fixup(on: bool):
-    """Split-K weight gradients reduced inside the GEMM by the last-arriving split (True) or by a
-    separate reduce launch (False, the measured-faster default; csrc/kernels/gemm.hip)."""
-    ext().gemm_set_fixup(bool(on))
-
-
 def linear_dw(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
               adam=None) -> torch.Tensor:
-    """out[N_out, N_in] (fp32) (+)= dy^T x; split-K partials are reduced inside the GEMM.
+    """out[N_out, N_in] (fp32) (+)= dy^T x (split-K fp32 slabs + a deterministic reduce launch).
     adam = (state, hyper) from ``ArenaAdam.fused_args``: apply Adam to the finished gradient
     instead of storing it."""
     M, N = dy.shape[1], x.shape[1]
     ws = workspace(dy.device, "splitk", 8 * M * N)
     st, hp = adam if adam is not None else ([], [])
-    ext().gemm_dw(dy, x, out, ws, accumulate, tile_counters(dy.device), st, hp)
+    ext().gemm_dw(dy, x, out, ws, accumulate, st, hp)
     return out
 
 
@@ -147,7 +166,7 @@ def linear_dw2(dy0: torch.Tensor, x0: torch.Tensor, out0: torch.Tensor, dy1: tor
     ws = workspace(dy0.device, f"splitk_def{len(jobs)}", planned * n) if defer else \
         workspace(dy0.device, "splitk", 8 * n)
     st, hp = adam if adam is not None else ([], [])
-    splits = ext().gemm_dw2(dy0, x0, out0, dy1, x1, out1, ws, accumulate, tile_counters(dy0.device), st, hp, defer)
+    splits = ext().gemm_dw2(dy0, x0, out0, dy1, x1, out1, ws, accumulate, st, hp, defer)
     if splits:
         s0 = splits * out0.numel()
         jobs.append((ws[:s0], out0, splits, accumulate))
@@ -448,6 +467,10 @@ def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, k
     mean = torch.empty(M, dtype=torch.float32, device=x.device)
     rstd = torch.empty(M, dtype=torch.float32, device=x.device)
     thr, sc = _drop(p)
+    if _splitk_ok(M, N, x.shape[1]):
+        _splitk(EPI_LN, x, w, y, bias=b, res=res, gamma=gamma, beta=beta, mean=mean, rstd=rstd, z=z, eps=eps,
+                seed=seed, site=site, thr=thr, dscale=sc, row_map=row_map if thr else None)
+        return y, z, mean, rstd
     stats, cnt, err = _ln_state(x.device, M, N)
     xs = _xsite(x.device, N, xsite)
     ext().gemm_ln(False, x, w, y, b, res, gamma, beta, mean, rstd, z, None, None, stats, cnt, err, eps, seed, site,
@@ -465,6 +488,17 @@ def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, see
     dz = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
     thr, sc = _drop(p)
     dx = torch.empty_like(dz) if thr else None
+    if _splitk_ok(M, N, a.shape[1]):
+        key = "ln_colpart" if jobs is None else f"ln_colpart_job{len(jobs)}"
+        ws = workspace(a.device, key, M * 3 * N)
+        _splitk(EPI_LN_BWD, a, wt, dz, res=res, gamma=gamma, mean=mean, rstd=rstd, z=z, dx=dx, colpart=ws,
+                seed=seed, site=site, thr=thr, dscale=sc, row_map=row_map if thr else None)
+        job = (ws, [dgamma, dbeta, dbias], M, 3 * N, N, accumulate)
+        if jobs is not None:
+            jobs.append(job)
+        else:
+            colsum_flush([job])
+        return dz, (dx if dx is not None else dz)
     key = "ln_colpart" if jobs is None else f"ln_colpart_job{len(jobs)}"
     ws = workspace(a.device, key, ((M + 63) // 64) * 3 * N)
     stats, cnt, err = _ln_state(a.device, M, N)

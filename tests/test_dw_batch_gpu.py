@@ -22,7 +22,7 @@ def _frel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 3, 4, 6, 10, 11, 12, 15, 21, 33, 41, 42, 43, 44])
+@pytest.mark.parametrize("cfg", [-1, 1, 8, 11])
 def test_dw_batch_kernel_matches_fp32(cfg):
     g = torch.Generator(device="cuda").manual_seed(cfg + 5)
     T = 2688
@@ -40,26 +40,6 @@ def test_dw_batch_kernel_matches_fp32(cfg):
     torch.cuda.synchronize()
     for (_, _, out, _), ref in zip(jobs, refs):
         assert _frel(out, ref) < 1e-5, _frel(out, ref)
-
-
-@pytest.mark.parametrize("persist,static", [(41, 11), (42, 1), (43, 10), (44, 12)])
-def test_persistent_dw_batch_bitwise_static(persist, static):
-    """The persistent, dynamically scheduled launch computes every tile whole (full K, same
-    epilogue) whatever block takes it: bitwise the static grid of the same tile, on every one of
-    several back-to-back launches (the per-XCD counters reset themselves)."""
-    g = torch.Generator(device="cuda").manual_seed(7)
-    T = 1344
-    shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072)] * 3
-    ins = [((torch.randn(T, M, device="cuda", generator=g) * 0.1).to(torch.bfloat16),
-            torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16)) for M, N in shapes]
-    ref = [torch.empty(M, N, device="cuda") for M, N in shapes]
-    K.linear_dw_batch([(dy, x, o, False) for (dy, x), o in zip(ins, ref)], cfg=static)
-    for _ in range(4):
-        outs = [torch.full((M, N), float("nan"), device="cuda") for M, N in shapes]
-        K.linear_dw_batch([(dy, x, o, False) for (dy, x), o in zip(ins, outs)], cfg=persist)
-        torch.cuda.synchronize()
-        for o, r in zip(outs, ref):
-            assert torch.equal(o, r)
 
 
 def _batch(B, S, seed=0):
@@ -118,32 +98,6 @@ def test_fused_adam_in_batched_dw_matches_unfused(graph):
     assert torch.equal(a.master, b.master)
     assert torch.equal(opts[0].m, opts[1].m) and torch.equal(opts[0].v, opts[1].v)
     assert torch.equal(a.shadow, b.shadow)
-    if graph:
-        assert all(st.graph is not None and st.failed is None for st in steps)
-
-
-@pytest.mark.parametrize("graph", [False, True])
-def test_tail_overlap_bitwise(graph):
-    """Embedding backward + column-sum flush on a side stream concurrent with the all-layer dW
-    launch (model.overlap_tail): bitwise the serial order, eager and graph-replayed."""
-    cfg = DistilBertConfig(n_layers=2)
-    models, opts, steps = [], [], []
-    for overlap in (True, False):
-        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=23)
-        m.overlap_tail = overlap
-        m.train()
-        opt = ArenaAdam(m, lr=1e-3)
-        models.append(m)
-        opts.append(opt)
-        steps.append(GraphedTrainStep(make_step_fn(m, opt), warmup=1, enabled=graph, bucket=m.packed_rows))
-    for it in range(5):
-        ids, mask, labels, tokens = _batch(16, 128, seed=600 + it)
-        for st in steps:
-            st(ids, mask, labels, tokens)
-    torch.cuda.synchronize()
-    a, b = models[0].arena, models[1].arena
-    assert torch.equal(a.master, b.master) and torch.equal(a.shadow, b.shadow)
-    assert torch.equal(opts[0].m, opts[1].m) and torch.equal(opts[0].v, opts[1].v)
     if graph:
         assert all(st.graph is not None and st.failed is None for st in steps)
 

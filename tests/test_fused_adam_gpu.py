@@ -1,9 +1,9 @@
 """Adam fused into the weight-gradient GEMM epilogues == gradient, then Adam kernel.
 
 The fused epilogue (csrc/kernels/gemm.hip ``adam_epi4``) runs the Adam kernel's
-arithmetic on the finished fp32 gradient tile; the split-K tiles are summed in
-z order by the last-arriving split (the same order as the separate reduce
-kernel).  So a fused training step should reproduce the unfused one bit for bit.
+arithmetic on the finished fp32 gradient tile (a fused launch never splits K).  So a
+fused training step reproduces the unfused one bit for bit when the unfused one does
+not split K either.
 """
 import pytest
 import torch
@@ -34,21 +34,21 @@ def rel(a, b):
 
 
 @pytest.fixture
-def fixup():
-    K.set_splitk_fixup(True)
+def nosplit():
+    """Weight-gradient GEMMs unsplit in both arms (a fused launch never splits K; a split
+    unfused one would sum in another fp32 order)."""
+    K.ext().gemm_set_cfg(2, -1, 1)
     yield
-    K.set_splitk_fixup(False)
+    K.ext().gemm_set_cfg(2, -1, -1)
 
 
 @pytest.mark.parametrize("graph", [False, True])
-def test_fused_adam_training_matches_unfused(graph, fixup):
-    """(With the in-kernel split-K fixup both arms split the out_lin + qkv weight gradient the
-    same way; without it the fused arm runs that GEMM unsplit -- a different fp32 sum order.)"""
+def test_fused_adam_training_matches_unfused(graph, nosplit):
     cfg = DistilBertConfig(n_layers=2)
     models, opts, steps = [], [], []
     for fuse in (True, False):
         m = DDoSClassifier(config=cfg, device=DEV, impl="hip", seed=13)
-        m.batch_dw = False  # per-layer grouped dW with the split-K fixup (batched: test_dw_batch_gpu.py)
+        m.batch_dw = False  # per-layer grouped dW launches (batched: test_dw_batch_gpu.py)
         m.train()
         opt = ArenaAdam(m, lr=1e-3, fuse_dw=fuse)
         assert opt.can_fuse() == fuse
@@ -139,18 +139,17 @@ def _check_fused_dw(shapes, T):
     assert (junk == 7.0).all()  # the gradient itself is never stored
     for a, b in zip(state[0], state[1]):
         assert torch.equal(a, b), rel(a, b)
-    assert not K.tile_counters(DEV).any()  # split-K arrival counters reset themselves
 
 
 @pytest.mark.parametrize("shapes,T", [(((768, 768), (2304, 768)), 2688)])
-def test_dw_fused_adam_with_splitk_fixup(shapes, T, fixup):
-    """Split-K shape: with the in-kernel fixup the fused launch splits K like the reference."""
+def test_dw_fused_adam_splitk_shape(shapes, T, nosplit):
+    """A shape the unfused launch would split K on: the fused launch runs it unsplit."""
     _check_fused_dw(shapes, T)
 
 
-def test_splitk_fixup_graph_replays_and_accumulates(fixup):
-    """In-kernel split-K reduction: repeated launches (and graph replays) reuse the
-    self-resetting counters; accumulate adds onto the existing gradient."""
+def test_splitk_graph_replays_and_accumulates():
+    """Split-K weight gradient (fp32 slabs + the reduce launch): repeated launches and graph
+    replays give bitwise the same result; accumulate adds onto the existing gradient."""
     T, M, N = 4096, 768, 768  # 72 tiles -> split K
     g = torch.Generator(device=DEV).manual_seed(9)
     dy = (torch.randn(T, M, device=DEV, generator=g)).to(torch.bfloat16)
@@ -175,7 +174,6 @@ def test_splitk_fixup_graph_replays_and_accumulates(fixup):
         gr.replay()
         torch.cuda.synchronize()
         assert torch.equal(out, first)
-    assert not K.tile_counters(DEV).any()
 
 
 def test_adam_run_table_matches_per_run_launches():

@@ -68,12 +68,12 @@ def test_gemm_identity_asymmetric():
     assert torch.equal(y.float(), w.float().t())
 
 
-@pytest.mark.parametrize("cfg", [25, 26, 27, 28, 29, 30])
-def test_gemm_pipelined_configs(cfg):
-    """The register-pipelined K loop (gemm.hip gemm_tile_at PIPE) on every fused epilogue of the
+@pytest.mark.parametrize("cfg", [0, 1, 6, 10, 13, 18, 21, 24])
+def test_gemm_forced_configs(cfg):
+    """Every instantiated NT tile configuration (gemm.hip launch_id) on every fused epilogue of the
     NT path, forced through the config override; odd and even K-tile counts, a partial row tile."""
     from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops._ext import ext
-    N = 768 if cfg in (28, 29) else 3072 if cfg != 27 else 2304
+    N = 2304 if cfg == 6 else 3072 if cfg in (1, 10, 21) else 768
     try:
         ext().gemm_set_cfg(0, cfg, -1)
         for M, K in ((2600, 768), (640, 704), (2688, 3072)):

@@ -1,7 +1,9 @@
 """Last-block [CLS] pruning (RunCtx.prune_idx, ops/functional.py LayerFn._forward_pruned): the
 last block runs out-proj / FFN / LayerNorms on the [CLS] rows only.  Exact by construction (no
-other row of its output reaches the loss), so the logits and loss match the unpruned model and
-every gradient matches up to fp32 summation order; a few graph-replayed Adam steps stay together."""
+other row of its output reaches the loss): with the pruned GEMMs on the same one-pass kernels as
+the full model (split-K off) the logits and loss are bitwise the unpruned model's; with the default
+split-K small-M GEMMs (ops/kernels.py SPLITK_MAX_M) they agree to fp32 summation order.  Every
+gradient matches up to fp32 summation order; a few graph-replayed Adam steps stay together."""
 import pytest
 import torch
 
@@ -37,8 +39,12 @@ def _frel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
 
 
+@pytest.mark.parametrize("splitk", [False, True])
 @pytest.mark.parametrize("packed,B,empty", [(True, 32, None), (False, 16, None), (True, 20, None), (True, 20, 3)])
-def test_pruned_last_block_matches_full(packed, B, empty):
+def test_pruned_last_block_matches_full(packed, B, empty, splitk, monkeypatch):
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+    if not splitk:
+        monkeypatch.setattr(K, "SPLITK_MAX_M", 0)
     cfg = DistilBertConfig(n_layers=3)
     outs = []
     for prune in (True, False):
@@ -54,15 +60,25 @@ def test_pruned_last_block_matches_full(packed, B, empty):
         outs.append((loss.detach().clone(), logits.detach().clone(), m.arena.grad.clone(),
                      {k: m.dense_grad(k).clone() for k in m.state_dict()}))
     (l0, z0, g0, d0), (l1, z1, g1, d1) = outs
-    assert torch.equal(z0, z1), (z0 - z1).abs().max()
-    assert l0.item() == l1.item()
-    assert _frel(g0, g1) < 1e-5
+    if not splitk:
+        assert torch.equal(z0, z1), (z0 - z1).abs().max()
+        assert l0.item() == l1.item()
+        assert _frel(g0, g1) < 1e-5
+    else:
+        assert _frel(z0, z1) < 2e-2, (z0 - z1).abs().max()
+        assert abs(l0.item() - l1.item()) < 2e-2 * max(1.0, abs(l1.item()))
+        assert _frel(g0, g1) < 2e-2
     for k in d1:
         if d1[k].norm() > 0:
-            assert _frel(d0[k], d1[k]) < 1e-4, k
+            if not splitk:
+                assert _frel(d0[k], d1[k]) < 1e-4, k
+            else:  # (+ an absolute floor: k_lin.bias's gradient is zero up to rounding noise, ~1e-7)
+                assert (d0[k] - d1[k]).norm().item() <= 3e-2 * d1[k].norm().item() + 1e-5, k
 
 
-def test_pruned_eval_logits_match():
+def test_pruned_eval_logits_match(monkeypatch):
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+    monkeypatch.setattr(K, "SPLITK_MAX_M", 0)  # (bitwise: the same one-pass kernels in both arms)
     cfg = DistilBertConfig(n_layers=2)
     res = []
     for prune in (True, False):
@@ -75,7 +91,11 @@ def test_pruned_eval_logits_match():
     assert torch.equal(res[0], res[1])
 
 
-def test_pruned_graph_training_tracks_full():
+@pytest.mark.parametrize("splitk", [False, True])
+def test_pruned_graph_training_tracks_full(splitk, monkeypatch):
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+    if not splitk:
+        monkeypatch.setattr(K, "SPLITK_MAX_M", 0)
     cfg = DistilBertConfig(n_layers=2)
     models, steps = [], []
     for prune in (True, False):
@@ -94,7 +114,9 @@ def test_pruned_graph_training_tracks_full():
     assert all(st.graph is not None and st.failed is None for st in steps)
     for a, b in zip(*losses):
         assert abs(a - b) < 1e-3 * max(1.0, abs(b))
-    assert _frel(models[0].arena.master, models[1].arena.master) < 1e-6
+    # (split-K: gradients agree to fp32 order only; Adam turns rounding-level differences of
+    # near-zero gradient components into lr-sized steps)
+    assert _frel(models[0].arena.master, models[1].arena.master) < (1e-6 if not splitk else 5e-4)
 
 
 def test_attention_q_live_matches_full_and_ignores_garbage():
