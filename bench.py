@@ -220,7 +220,7 @@ def main():
     if topo.dp:
         dp = import_module(f"{PKG}.parallel.dp")
         dp.dp_seed_offset(model, topo.dp_rank)
-        gsync = dp.GradSync(model, topo.dp_group, k, max_rows=B * S)
+        gsync = dp.GradSync(model, topo.dp_group, k, max_rows=B * S, ncomm=client.dp_comm)
         gsync.set_loss_scale(1.0 / k)
         fn = dp.make_dp_step_fn(model, opt, gsync, teacher, 2.0, 0.5)
     elif args.teacher:
@@ -228,8 +228,10 @@ def main():
     else:
         fn = engine.make_step_fn(model, opt)
     model.unpad = not args.padded
+    # (a data-parallel client's step is captured too when its exchange runs over the client's own
+    # NativeComm -- fed/runner.py dp_comm; torch.distributed's collectives are not capturable)
     step = engine.GraphedTrainStep(fn, warmup=2, enabled=(not args.no_graph) and args.impl == "hip"
-                                   and on_gpu and gsync is None,
+                                   and on_gpu and (gsync is None or gsync.capturable),
                                    bucket=getattr(model, "packed_rows", None))
     model.train()
 
@@ -323,8 +325,11 @@ def main():
     per_client = args.steps / dt
     if di.is_main:
         default_cfg = (S == 128 and B == 32 and args.layers == 6 and not args.teacher)
+        # a non-default config names its real workload: the rows are padded to S, but the packed
+        # step runs on the real tokens only (CICIDS2017 text is ~80 WordPiece tokens a row)
         metric = HEADLINE_METRIC if default_cfg else (
             f"batches/sec/client (DistilBERT{'' if args.layers == 6 else f' {args.layers}-layer'} seq{S} bs{B}"
+            + (f", mean {real_frac * S:.0f} real tokens/row" if real_frac < 1.0 else "")
             + (" KD from BERT-base teacher" if args.teacher else "") + ") + aggregated F1 after 1 FedAvg round")
         out = {
             "metric": metric,
@@ -351,6 +356,7 @@ def main():
             "per_rank_ms_per_step": per_rank_ms,
             "backend": di.backend,
             "real_token_fraction": round(real_frac, 4),
+            "mean_real_tokens_per_row": round(real_frac * S, 1),
             "packed_row_fraction": round(rows_frac, 4),
             "impl": args.impl,
             "comm": args.comm,

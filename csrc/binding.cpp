@@ -34,6 +34,7 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
 int fd_gemm_stamps(unsigned long long* host, int nblocks);
+int fd_attn_stamps(unsigned long long* host, int nblocks);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
                 int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate,
                 const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st);
@@ -606,6 +607,7 @@ int comm_dtype(const at::Tensor& t) {
     case at::kBFloat16: return 1;
     case at::kDouble: return 2;
     case at::kLong: return 3;
+    case at::kInt: return 4;
     default: TORCH_CHECK(false, "comm: unsupported dtype ", t.scalar_type());
   }
   return 0;
@@ -700,6 +702,13 @@ int64_t gemm_stamps(at::Tensor out) {
   TORCH_CHECK(!out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous() && out.dim() == 2 &&
                   out.size(1) == 8, "gemm_stamps: CPU int64 [n][8]");
   return fd_gemm_stamps(reinterpret_cast<unsigned long long*>(out.data_ptr()), (int)out.size(0));
+}
+
+// Diagnostic builds (FD_ATTN_STAMPS): per-block phase stamps of the last S <= 128 attention launch.
+int64_t attn_stamps(at::Tensor out) {
+  TORCH_CHECK(!out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous() && out.dim() == 2 &&
+                  out.size(1) == 8, "attn_stamps: CPU int64 [n][8]");
+  return fd_attn_stamps(reinterpret_cast<unsigned long long*>(out.data_ptr()), (int)out.size(0));
 }
 
 // Tuning hook: force GEMM configuration `cfg` (-1 = measured default) for a kind.
@@ -1181,6 +1190,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("aux"), py::arg("res"), py::arg("workspace"), py::arg("accumulate"), py::arg("aux_out") = py::none());
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_stamps", &gemm_stamps);
+  m.def("attn_stamps", &attn_stamps);
   m.def("gemm_splitk", &gemm_splitk, py::arg("epi"), py::arg("A"), py::arg("Bt"), py::arg("C"), py::arg("workspace"),
         py::arg("splits") = 0, py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("aux_out") = py::none(), py::arg("res") = py::none(), py::arg("colsum") = py::none(),

@@ -76,6 +76,7 @@ ncclDataType_t dtype_of(int dtype) {
     case 1: return ncclBfloat16;
     case 2: return ncclFloat64;
     case 3: return ncclInt64;
+    case 4: return ncclInt32;
     default: return ncclFloat32;
   }
 }

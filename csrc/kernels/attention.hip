@@ -158,6 +158,32 @@ DEV float key_bias(const AttnArgs& a, int tok0, int len, int k) {
 
 DEV uint32_t site_seed(const AttnArgs& a) { return hash32(a.seed_ptr ? a.seed_ptr[0] : 0u, a.site); }
 
+// Diagnostic build only (FD_HIP_EXTRA_FLAGS=-DFD_ATTN_STAMPS=1): wall-clock stamps (100 MHz) of
+// wave 0 of every block at the phase boundaries of the S <= 128 kernels, read back with
+// fd_attn_stamps (scripts/attn_stamps.py).  Slot 7: XCC << 32 | HW_ID.  The normal build has none.
+#ifndef FD_ATTN_STAMPS
+#define FD_ATTN_STAMPS 0
+#endif
+constexpr int ASTAMP_MAXB = 8192;
+#if FD_ATTN_STAMPS
+__device__ unsigned long long g_astamps[ASTAMP_MAXB * 8];
+DEV int astamp_bid() { return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); }
+#define ASTAMP(i)                                                                                  \
+  do {                                                                                             \
+    if (threadIdx.x == 0 && astamp_bid() < ASTAMP_MAXB) g_astamps[astamp_bid() * 8 + (i)] = wall_clock64(); \
+  } while (0)
+DEV void astamp_hwid() {
+  if (threadIdx.x == 0 && astamp_bid() < ASTAMP_MAXB) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));
+    g_astamps[astamp_bid() * 8 + 7] = ((unsigned long long)(xcc & 0xf) << 32) | hw;
+  }
+}
+#else
+#define ASTAMP(i) do {} while (0)
+DEV void astamp_hwid() {}
+#endif
+
 // ------------------------------------------------------------------ forward
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 8192 + 256];
@@ -474,6 +500,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
     *reinterpret_cast<uint2*>(outv + 16 * dt + 4 * g) =
         make_uint2(pack_bf2(dv[dt][0], dv[dt][1]), pack_bf2(dv[dt][2], dv[dt][3]));
   }
+  ASTAMP(4);
 }
 
 template <typename M>
@@ -516,6 +543,8 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  ASTAMP(0);
+  astamp_hwid();
   if (b == a.B) {
     zero_filler(a, a.ctx, D, 1, h);
     return;
@@ -534,6 +563,7 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
   if (tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) : -INFINITY;
   __syncthreads();
+  ASTAMP(1);
   const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows needed
   if (q0 >= qlen) return;  // no barrier follows
   const uint32_t seed = site_seed(a);
@@ -623,6 +653,7 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
+  ASTAMP(2);
   if (q >= qlen) return;
   const float inv = 1.f / l;
   bf16_t* out = a.ctx + (tok0 + q) * D + h * DH;
@@ -631,6 +662,7 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
     *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) =
         make_uint2(pack_bf2(o[dt][0] * inv, o[dt][1] * inv), pack_bf2(o[dt][2] * inv, o[dt][3] * inv));
   if (g == 0) a.lse[((size_t)b * H + h) * S + q] = m + __logf(l);
+  ASTAMP(3);
 }
 
 __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
@@ -646,6 +678,8 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  ASTAMP(0);
+  astamp_hwid();
   if (b == a.B) {
     zero_filler(a, a.dqkv, ld3, 3, h);
     return;
@@ -680,6 +714,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   const bool mk = drop && a.dmask != nullptr;
   if (mk && tid < 256) mk_s[tid] = a.dmask[((size_t)b * H + h) * 256 + tid];
   __syncthreads();
+  ASTAMP(1);
   const uint32_t seed = site_seed(a);
   const float sc_out = a.scale;
   // unmasked-key bits of the two 64-key tiles (see attn_fwd_s128_kernel): 16-key sub-tiles
@@ -773,7 +808,9 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
             pack_bf2(dq[dt][0] * sc_out, dq[dt][1] * sc_out), pack_bf2(dq[dt][2] * sc_out, dq[dt][3] * sc_out));
     }
   }
+  ASTAMP(2);
   __syncthreads();  // delta of every query row is in LDS
+  ASTAMP(3);
 
   // ---- phase 2: dK and dV; wave w owns keys 16w .. 16w+15
   const int key0 = w * 16;
@@ -912,6 +949,19 @@ int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const floa
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
   return 0;
+}
+
+// Copy the diagnostic stamps (FD_ATTN_STAMPS builds) of blocks [0, nblocks) to host memory
+// [nblocks][8]; -1 in a normal build.
+int fd_attn_stamps(unsigned long long* host, int nblocks) {
+#if FD_ATTN_STAMPS
+  if (nblocks > ASTAMP_MAXB) nblocks = ASTAMP_MAXB;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_astamps), sizeof(unsigned long long) * 8 * nblocks, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? nblocks : -2;
+#else
+  (void)host; (void)nblocks;
+  return -1;
+#endif
 }
 
 int fd_mask_to_bias(const void* mask, int mask_bytes, float* bias, long n, hipStream_t st) {

@@ -94,10 +94,16 @@ class FederatedClient:
         # Identical start for every client: rank 0's weights win.
         broadcast_model(self.model, comm=self.comm)
         self.grad_sync = None
+        self.dp_comm = None
         if self.topo.dp:
             dp_seed_offset(self.model, self.topo.dp_rank)
+            if dev.type == "cuda" and self.di.backend == "nccl" and os.environ.get("FEDDDOS_DP_NATIVE", "1") != "0":
+                # the client's replicas exchange over a framework RCCL communicator of their own
+                # group: stream-ordered collectives, so the data-parallel step is graph-captured
+                from ..parallel.rccl import NativeComm
+                self.dp_comm = NativeComm(group=self.topo.dp_group)
             self.grad_sync = GradSync(self.model, self.topo.dp_group, self.topo.gpus_per_client,
-                                      max_rows=cfg.batch_size * cfg.max_len)
+                                      max_rows=cfg.batch_size * cfg.max_len, ncomm=self.dp_comm)
             log.info(f"data-parallel client: replica {self.topo.dp_rank + 1}/{self.topo.gpus_per_client}")
         self.teacher = None
         if cfg.teacher:
@@ -110,7 +116,7 @@ class FederatedClient:
             # the teacher fine-tune is data-parallel too, so every replica distils from the same teacher
             dp_seed_offset(self.teacher, self.topo.dp_rank)
             self.teacher_sync = GradSync(self.teacher, self.topo.dp_group, self.topo.gpus_per_client,
-                                         max_rows=cfg.batch_size * cfg.max_len)
+                                         max_rows=cfg.batch_size * cfg.max_len, ncomm=self.dp_comm)
         self.start_round = 0
         self.history: List[Dict] = []
         if cfg.resume:
@@ -189,10 +195,11 @@ class FederatedClient:
             t_opt = ArenaAdam(self.teacher, lr=cfg.lr)
             with self.timer("teacher"):
                 train_model(self.teacher, self.train_loader, None, t_opt, int(cfg.extra.get("teacher_epochs", cfg.epochs)),
-                            log=log, use_graph=cfg.use_graph and (self.teacher_sync is None or cfg.dp_graph),
+                            log=log, use_graph=cfg.use_graph and (self.teacher_sync is None or cfg.dp_graph
+                                                                  or self.teacher_sync.capturable),
                             grad_sync=self.teacher_sync)
         with self.timer("train"):
-            use_graph = cfg.use_graph and (self.grad_sync is None or cfg.dp_graph)
+            use_graph = cfg.use_graph and (self.grad_sync is None or cfg.dp_graph or self.grad_sync.capturable)
             tr = train_model(model, self.train_loader, None, opt, cfg.epochs, log=log, use_graph=use_graph,
                              teacher=self.teacher, kd_temperature=cfg.kd_temperature, kd_alpha=cfg.kd_alpha,
                              grad_sync=self.grad_sync)

@@ -430,10 +430,29 @@ def _cu_count() -> int:
     return _CUS[dev]
 
 
+# Tile configuration of the LayerNorm-fused GEMMs (csrc/kernels/gemm.hip fd_gemm_ln): -1 = the
+# launcher's default (FD_GEMM_LN_CFG or its measured pick); tests pin the others.
+LN_CFG = -1
+
+# Several processes on one GPU (gloo functional runs, FEDDDOS_BACKEND=gloo): another process's
+# kernels can hold the CUs a fused-LN tile's peers need, and two such grids then block each other
+# until the rendezvous times out (measured: tests/test_dp_gpu.py, two replicas on one MI355X).  Set
+# by parallel/comm.py init_distributed; the separate LayerNorm kernels run instead.
+_SHARED_DEVICE = False
+
+
+def set_shared_device(shared: bool) -> None:
+    global _SHARED_DEVICE
+    _SHARED_DEVICE = bool(shared)
+
+
 def ln_fusable(M: int, N: int) -> bool:
     """Whether a LayerNorm-fused GEMM of M rows x N (= hidden) columns runs as one resident
     round (its row blocks exchange statistics, so no tile may wait on an undispatched peer):
-    at most one 128 x 64 tile per CU; larger batches use the separate LayerNorm kernels."""
+    at most one 128 x 64 tile per CU, and no other process on the device; larger batches use
+    the separate LayerNorm kernels."""
+    if _SHARED_DEVICE:
+        return False
     tiles = ((M + 127) // 128) * (N // 64)
     return N % 64 == 0 and N <= 2048 and tiles <= min(LN_MAX_TILES, _cu_count())
 
@@ -474,7 +493,7 @@ def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, k
     stats, cnt, err = _ln_state(x.device, M, N)
     xs = _xsite(x.device, N, xsite)
     ext().gemm_ln(False, x, w, y, b, res, gamma, beta, mean, rstd, z, None, None, stats, cnt, err, eps, seed, site,
-                  thr, sc, row_map if thr else None, -1, xs)
+                  thr, sc, row_map if thr else None, LN_CFG, xs)
     return y, z, mean, rstd
 
 
@@ -504,7 +523,7 @@ def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, see
     stats, cnt, err = _ln_state(a.device, M, N)
     xs = _xsite(a.device, N, xsite)
     nblk = ext().gemm_ln(True, a, wt, dz, None, res, gamma, None, mean, rstd, z, dx, ws, stats, cnt, err, 0.0, seed,
-                         site, thr, sc, row_map if thr else None, -1, xs)
+                         site, thr, sc, row_map if thr else None, LN_CFG, xs)
     job = (ws, [dgamma, dbeta, dbias], nblk, 3 * N, N, accumulate)
     if jobs is not None:
         jobs.append(job)

@@ -49,6 +49,10 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 300.0, de
         n = torch.cuda.device_count()
         torch.cuda.set_device(local % max(n, 1))
         dev = torch.device("cuda", local % max(n, 1))
+        if world > 1 and int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) > n:
+            # ranks share a GPU (gloo functional runs): no kernel may assume it owns every CU
+            from ..ops import kernels as _K
+            _K.set_shared_device(True)
     else:
         dev = torch.device("cpu")
     be = "none"

@@ -26,6 +26,12 @@ is C federated clients of k GPUs each:
   (<= one row per token of the client batch) and scatter them back.
 * FedAvg across clients stays ONE all-reduce over the whole world: replicas of
   a client are identical, so giving each weight w/k yields the client average.
+* With a framework communicator over the client's group (``NativeComm(group=...)``, RCCL) every
+  collective of the exchange is issued on a side stream forked from the compute stream and joined
+  back in ``finish()`` -- nothing synchronises the host -- so the whole data-parallel step (forward,
+  backward with the overlapped block all-reduces, the sparse row exchange, Adam) is captured into
+  ONE HIP graph (``capturable``); torch.distributed's work objects are not capturable, so without
+  it the step stays eager.
 """
 from __future__ import annotations
 
@@ -114,7 +120,8 @@ class DPShardLoader:
 class GradSync:
     """Sum a client's gradients over its k data-parallel replicas (see module doc)."""
 
-    def __init__(self, model, group, k: int, max_rows: Optional[int] = None, overlap: bool = True):
+    def __init__(self, model, group, k: int, max_rows: Optional[int] = None, overlap: bool = True,
+                 ncomm=None):
         self.model, self.group, self.k = model, group, k
         self.overlap = overlap
         self.arena = model.arena
@@ -123,12 +130,32 @@ class GradSync:
         self.works: List = []
         self.done: List[Tuple[int, int]] = []
         self.loss_scale = torch.ones((), dtype=torch.float32, device=self.arena.device)
+        # ncomm: NativeComm over this client's group -> stream-ordered, graph-capturable exchange
+        self.ncomm = ncomm if (ncomm is not None and self.arena.device.type == "cuda") else None
+        self.side = torch.cuda.Stream(device=self.arena.device) if self.ncomm is not None else None
+        self._forked = False
         self._prev_hook = model.layer_grads_hook
         if overlap:
             model.layer_grads_hook = self._on_layer
 
+    @property
+    def capturable(self) -> bool:
+        """Whether a step using this exchange may be captured into a HIP graph."""
+        return self.ncomm is not None
+
     # -------------------------------------------------------------- pieces
+    def _fork(self):
+        """Side stream waits for everything the compute stream issued so far (the gradients the
+        next collective reads are final in stream order)."""
+        self.side.wait_stream(torch.cuda.current_stream(self.arena.device))
+        self._forked = True
+
     def _allreduce(self, t: torch.Tensor, op=None):
+        if self.ncomm is not None:
+            self._fork()
+            with torch.cuda.stream(self.side):
+                self.ncomm.all_reduce_(t, "max" if op == dist.ReduceOp.MAX else "sum", wait=False)
+            return
         w = dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.works.append(w)
 
@@ -152,18 +179,29 @@ class GradSync:
         woff, V, D = m.word_embedding_span()
         g = self.arena.grad[woff:woff + V * D].view(V, D)
         now = m.emb_now
-        union = now.to(torch.int32)
-        dist.all_reduce(union, op=dist.ReduceOp.MAX, group=self.group)
-        rows = torch.nonzero_static(union, size=self.max_rows, fill_value=-1).squeeze(1)
-        # filler slots repeat the first real row (the [CLS] id is always present), so the
-        # duplicate index_copy_ writes below all carry the same, correct value
-        rows = torch.where(rows >= 0, rows, rows[:1])
-        keep = now.index_select(0, rows).to(g.dtype)
-        buf = g.index_select(0, rows) * keep[:, None]  # zero where only another replica has the row
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
-        g.index_copy_(0, rows, buf)
-        now.copy_(union.clamp_(max=1).to(now.dtype))
-        m.emb_ever.bitwise_or_(now)
+        native = self.ncomm is not None
+        if native:  # the whole exchange on the side stream, after everything computed so far
+            self._fork()
+        import contextlib
+        with torch.cuda.stream(self.side) if native else contextlib.nullcontext():
+            union = now.to(torch.int32)
+            if native:
+                self.ncomm.all_reduce_(union, "max", wait=False)
+            else:
+                dist.all_reduce(union, op=dist.ReduceOp.MAX, group=self.group)
+            rows = torch.nonzero_static(union, size=self.max_rows, fill_value=-1).squeeze(1)
+            # filler slots repeat the first real row (the [CLS] id is always present), so the
+            # duplicate index_copy_ writes below all carry the same, correct value
+            rows = torch.where(rows >= 0, rows, rows[:1])
+            keep = now.index_select(0, rows).to(g.dtype)
+            buf = g.index_select(0, rows) * keep[:, None]  # zero where only another replica has the row
+            if native:
+                self.ncomm.all_reduce_(buf, "sum", wait=False)
+            else:
+                dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+            g.index_copy_(0, rows, buf)
+            now.copy_(union.clamp_(max=1).to(now.dtype))
+            m.emb_ever.bitwise_or_(now)
 
     # -------------------------------------------------------------- step API
     def set_loss_scale(self, s: float):
@@ -189,6 +227,13 @@ class GradSync:
             self._word_rows()
         for w in self.works:
             w.wait()
+        if self.ncomm is not None and self._forked:
+            # join: Adam (next on the compute stream) reads the summed gradients; no host sync --
+            # an RCCL-reported failure still surfaces here (async error poll, outside capture)
+            torch.cuda.current_stream(self.arena.device).wait_stream(self.side)
+            self._forked = False
+            if not torch.cuda.is_current_stream_capturing():
+                self.ncomm.check()
         self.works, self.done = [], []
 
     def detach(self):

@@ -48,15 +48,27 @@ class CommAborted(PeerFailure):
 
 
 class NativeComm:
+    """group: a torch.distributed sub-group (e.g. one data-parallel client's replicas): the
+    communicator then spans that group only, ranked by group rank; its unique id travels over the
+    group from the group's first rank.  Every rank of the WORLD must construct the communicators of
+    the groups it belongs to in the same order (as with ``dist.new_group``)."""
+
     def __init__(self, rank: Optional[int] = None, world_size: Optional[int] = None,
-                 timeout_s: Optional[float] = None):
+                 timeout_s: Optional[float] = None, group=None):
         from ..ops._ext import ext
         self._ext = ext()
         # bounded wait per eager collective (FEDDDOS_COMM_TIMEOUT_S; reference socket timeout 300 s)
         self.timeout_s = float(timeout_s if timeout_s is not None else os.environ.get("FEDDDOS_COMM_TIMEOUT_S", 300.0))
         on = dist.is_available() and dist.is_initialized()
-        self.rank = rank if rank is not None else (dist.get_rank() if on else 0)
-        self.world_size = world_size if world_size is not None else (dist.get_world_size() if on else 1)
+        src = 0
+        if group is not None:
+            if not on:
+                raise RuntimeError("NativeComm(group=...) needs an initialised torch.distributed")
+            self.rank, self.world_size = dist.get_rank(group), dist.get_world_size(group)
+            src = dist.get_global_rank(group, 0)
+        else:
+            self.rank = rank if rank is not None else (dist.get_rank() if on else 0)
+            self.world_size = world_size if world_size is not None else (dist.get_world_size() if on else 1)
         self._ext.comm_load(_torch_rccl_path())
         uid = self._ext.comm_unique_id() if self.rank == 0 else None
         if self.world_size > 1:
@@ -64,7 +76,7 @@ class NativeComm:
                 raise RuntimeError("NativeComm with world_size > 1 needs an initialised torch.distributed "
                                    "group for the unique-id rendezvous")
             box = [bytes(uid.numpy()) if uid is not None else None]
-            dist.broadcast_object_list(box, src=0)
+            dist.broadcast_object_list(box, src=src, group=group)
             uid = torch.frombuffer(bytearray(box[0]), dtype=torch.uint8).clone()
         self.handle = self._ext.comm_init(self.world_size, self.rank, uid)
 

@@ -48,9 +48,17 @@ def state_clean(M):
     return int(err.item()) == 0 and int(cnt[0].item()) > 0
 
 
+@pytest.fixture(params=[-1, 0, 18])
+def ln_cfg(request, monkeypatch):
+    """Every instantiated LayerNorm-fused tile configuration (gemm.hip fd_gemm_ln): the default
+    (8-wave 128 x 64, two K tiles per barrier) and the 4- / 8-wave 3-slot rings."""
+    monkeypatch.setattr(kn, "LN_CFG", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("M,K,p", [(2688, 768, 0.0), (2600, 3072, 0.1), (300, 3072, 0.1), (2000, 768, 0.0),
-                                   (64, 768, 0.1)])
-def test_linear_ln_fwd(M, K, p):
+                                   (64, 768, 0.1), (640, 128, 0.0)])
+def test_linear_ln_fwd(M, K, p, ln_cfg):
     x, w, res = bf(M, K, seed=1), bf(D, K, scale=0.03, seed=2), bf(M, D, seed=3)
     b = (torch.randn(D, generator=torch.Generator().manual_seed(4)) * 0.1).to(DEV)
     gamma, beta = affine(5)
@@ -99,8 +107,8 @@ def test_linear_ln_fwd_packed_row_map():
 
 
 @pytest.mark.parametrize("M,K,p,defer", [(2688, 3072, 0.0, False), (2600, 2304, 0.1, True), (300, 2304, 0.1, False),
-                                         (130, 3072, 0.0, True)])
-def test_linear_dx_ln_bwd(M, K, p, defer):
+                                         (130, 3072, 0.0, True), (700, 128, 0.1, False)])
+def test_linear_dx_ln_bwd(M, K, p, defer, ln_cfg):
     gamma, beta = affine(21)
     x2, w2, r2 = bf(M, D, seed=22), bf(D, D, scale=0.03, seed=23), bf(M, D, seed=24)
     b2 = torch.zeros(D, device=DEV)

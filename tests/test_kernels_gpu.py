@@ -71,12 +71,13 @@ def test_gemm_identity_asymmetric():
 @pytest.mark.parametrize("cfg", [0, 1, 6, 10, 13, 18, 21, 24])
 def test_gemm_forced_configs(cfg):
     """Every instantiated NT tile configuration (gemm.hip launch_id) on every fused epilogue of the
-    NT path, forced through the config override; odd and even K-tile counts, a partial row tile."""
+    NT path, forced through the config override; odd and even K-tile counts, a partial row tile,
+    and fewer K tiles than ring slots."""
     from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops._ext import ext
     N = 2304 if cfg == 6 else 3072 if cfg in (1, 10, 21) else 768
     try:
         ext().gemm_set_cfg(0, cfg, -1)
-        for M, K in ((2600, 768), (640, 704), (2688, 3072)):
+        for M, K in ((2600, 768), (640, 704), (2688, 3072), (300, 128), (200, 64)):
             x, w = bf(M, K, seed=31), bf(N, K, scale=0.05, seed=32)
             b = torch.randn(N, device=DEV) * 0.1
             ref = x.float() @ w.float().t()

@@ -10,6 +10,8 @@ it).  What the first multi-GPU run must prove before any scaling number means an
   bf16 compute shadow is refreshed from it;
 * a data-parallel client (2 GPUs, ``GradSync``: per-block async all-reduces from the backward
   hook + the compacted sparse word-row exchange) gives the full-batch gradient;
+* the data-parallel step over a group ``NativeComm`` replays from a HIP graph bitwise equal to
+  the eager step (the collectives are side-stream ordered and captured with the step);
 * a peer that dies inside FedAvg: the survivor's ``NativeComm`` collective does not hang -- its
   bounded wait (ncclCommGetAsyncError polling) aborts the communicator (ncclCommAbort) and raises
   ``PeerFailure`` within the timeout (reference: 300 s socket timeouts, server.py:10).
@@ -126,6 +128,37 @@ def _dp_worker(rank, world, port, outdir):
     comm.shutdown()
 
 
+def _dp_graph_worker(rank, world, port, outdir):
+    """The same data-parallel training steps eager and replayed from a HIP graph: GradSync over a
+    NativeComm of the client's group (side-stream collectives, no host sync) is capturable."""
+    comm, di = _init(rank, world, port)
+    from importlib import import_module
+    dp = import_module(f"{PKG}.parallel.dp")
+    rccl = import_module(f"{PKG}.parallel.rccl")
+    engine = import_module(f"{PKG}.engine")
+    topo = dp.make_topology(2)
+    nc = rccl.NativeComm(group=topo.dp_group)
+    ids, mask, labels = _batch(di.device)
+    sl = slice(8 * rank, 8 * rank + 8)
+    out = {}
+    for graphed in (False, True):
+        m = _model(di.device)
+        opt = engine.ArenaAdam(m, lr=1e-3)
+        sync = dp.GradSync(m, topo.dp_group, 2, max_rows=16 * 64, ncomm=nc)
+        assert sync.capturable
+        sync.set_loss_scale(0.5)
+        step = engine.GraphedTrainStep(dp.make_dp_step_fn(m, opt, sync), warmup=2, enabled=graphed)
+        losses = [step(ids[sl], mask[sl], labels[sl]).clone() for _ in range(5)]
+        torch.cuda.synchronize()
+        out["graph" if graphed else "eager"] = {"master": m.arena.master.cpu(), "loss": torch.stack(losses).cpu(),
+                                                "captured": step.graph is not None, "failed": str(step.failed)}
+        sync.detach()
+        del step, opt, m
+    nc.close()
+    torch.save(out, os.path.join(outdir, f"dpg{rank}.pt"))
+    comm.shutdown()
+
+
 def _abort_worker(rank, world, port, outdir):
     import time
     comm, di = _init(rank, world, port)
@@ -211,6 +244,19 @@ def test_dp_gradsync_matches_full_batch_over_rccl(tmp_path):
     # replicas hold the same summed gradient (word rows outside the batch are never written)
     assert torch.equal(r0["grad"][woff + V * D:], r1["grad"][woff + V * D:])
     assert torch.equal(r0["grad"][:woff], r1["grad"][:woff])
+
+
+def test_dp_step_graphed_equals_eager_over_native_comm(tmp_path):
+    _spawn(_dp_graph_worker, str(tmp_path))
+    r = [torch.load(tmp_path / f"dpg{i}.pt", weights_only=True) for i in range(2)]
+    for x in r:
+        assert x["graph"]["captured"] and x["graph"]["failed"] == "None", x["graph"]["failed"]
+        assert not x["eager"]["captured"]
+        # same kernels in the same order on the same inputs: the replayed step is the eager step
+        assert torch.equal(x["graph"]["master"], x["eager"]["master"])
+        assert torch.equal(x["graph"]["loss"], x["eager"]["loss"])
+    # the replicas stay identical (summed gradients, identical Adam)
+    assert torch.equal(r[0]["graph"]["master"], r[1]["graph"]["master"])
 
 
 def test_dead_peer_in_fedavg_aborts_instead_of_hanging(tmp_path):
