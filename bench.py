@@ -92,6 +92,11 @@ def _args(argv=None):
                     help="infer: serving throughput of the HIP-graph forward (reference evaluate_model rate)")
     ap.add_argument("--teacher", action="store_true",
                     help="distillation step (BASELINE.json config 5): BERT-base teacher fwd + DistilBERT student")
+    ap.add_argument("--lr", type=float, default=2e-5, help="Adam learning rate of the quality protocol "
+                    "(reference client1.py:380: 2e-5)")
+    ap.add_argument("--kd-alpha", type=float, default=0.9,
+                    help="distillation loss weight of the CE term: alpha CE + (1 - alpha) T^2 KL")
+    ap.add_argument("--kd-temperature", type=float, default=2.0)
     return ap.parse_args(argv)
 
 
@@ -190,7 +195,8 @@ def main():
                           max_len=S, impl=args.impl, gpus_per_client=args.gpus_per_client, comm=args.comm,
                           out_dir=os.path.join(os.environ.get("TMPDIR", "/tmp"), f"fedddos_bench_{os.getpid()}"),
                           plots=False, resume=False, save_checkpoints=False, heartbeat_s=0.0, verbose=False,
-                          teacher="bert-base" if args.teacher else None)
+                          teacher="bert-base" if args.teacher else None, lr=args.lr, kd_alpha=args.kd_alpha,
+                          kd_temperature=args.kd_temperature)
     client = runner.FederatedClient(fc, model_config=models.DistilBertConfig(n_layers=args.layers))
     topo = client.topo
     k = topo.gpus_per_client
@@ -222,9 +228,9 @@ def main():
         dp.dp_seed_offset(model, topo.dp_rank)
         gsync = dp.GradSync(model, topo.dp_group, k, max_rows=B * S, ncomm=client.dp_comm)
         gsync.set_loss_scale(1.0 / k)
-        fn = dp.make_dp_step_fn(model, opt, gsync, teacher, 2.0, 0.5)
+        fn = dp.make_dp_step_fn(model, opt, gsync, teacher, args.kd_temperature, args.kd_alpha)
     elif args.teacher:
-        fn = engine.make_kd_step_fn(model, teacher, opt, 2.0, 0.5)
+        fn = engine.make_kd_step_fn(model, teacher, opt, args.kd_temperature, args.kd_alpha)
     else:
         fn = engine.make_step_fn(model, opt)
     model.unpad = not args.padded
@@ -447,7 +453,12 @@ def _quality(client, di, comm, rows, epochs, on_gpu):
             "fedavg_rounds": 1, "local_epochs": epochs, "quality_file_rows": rows,
             "quality_epoch_losses": [round(x, 5) for x in tr["epoch_losses"]],
             "quality_train_steps": tr["steps"], "quality_train_batches_per_sec": round(tr["batches_per_sec"], 2),
-            "quality_fedavg_ms": round(rec["fedavg_ms"], 3), "quality_wall_s": round(wall, 2)}
+            "quality_fedavg_ms": round(rec["fedavg_ms"], 3), "quality_wall_s": round(wall, 2),
+            "quality_lr": client.cfg.lr,
+            **({"kd_alpha": client.cfg.kd_alpha, "kd_temperature": client.cfg.kd_temperature}
+               if client.teacher is not None else {}),
+            **({"teacher_test_accuracy_pct": round(rec["teacher_test"]["accuracy"], 3),
+                "teacher_test_f1": round(rec["teacher_test"]["f1"], 5)} if "teacher_test" in rec else {})}
 
 
 def _bench_infer(args, model, it, di, comm, B, S):

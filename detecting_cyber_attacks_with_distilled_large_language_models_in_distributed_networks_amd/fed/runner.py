@@ -189,6 +189,7 @@ class FederatedClient:
         opt_path = os.path.join(cfg.out_dir, f"client{self.client_id}_optim.pth")
         if cfg.save_optimizer and r == self.start_round:
             ck.load_optimizer(opt, opt_path)
+        teacher_test = None
         if self.teacher is not None and r == self.start_round:
             # Local teacher fine-tune (BERT-base, same kernels), then distil into the student.
             log.info("training BERT-base teacher")
@@ -198,6 +199,10 @@ class FederatedClient:
                             log=log, use_graph=cfg.use_graph and (self.teacher_sync is None or cfg.dp_graph
                                                                   or self.teacher_sync.capturable),
                             grad_sync=self.teacher_sync)
+            with self.timer("eval"):
+                teacher_test = _metrics_record(evaluate_model(self.teacher, self.test_loader, log=log,
+                                                              name="Teacher test"))
+            self.teacher.eval()
         with self.timer("train"):
             use_graph = cfg.use_graph and (self.grad_sync is None or cfg.dp_graph or self.grad_sync.capturable)
             tr = train_model(model, self.train_loader, None, opt, cfg.epochs, log=log, use_graph=use_graph,
@@ -264,6 +269,8 @@ class FederatedClient:
         rec = {"round": r + 1, "train": tr, "fedavg_ms": t_fed * 1e3, "participated": contributes,
                "local_val": _metrics_record(val_local), "local_test": _metrics_record(local),
                "aggregated_val": _metrics_record(val_agg), "aggregated_test": _metrics_record(agg)}
+        if teacher_test is not None:
+            rec["teacher_test"] = teacher_test
         self.history.append(rec)
         if self.writer:
             ck.save_fed_state(cfg.out_dir, self.client_id, {"completed_rounds": r + 1, "history": self.history})

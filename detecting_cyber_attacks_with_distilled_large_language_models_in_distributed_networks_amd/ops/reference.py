@@ -17,6 +17,16 @@ import torch.nn.functional as F
 from .dropout import keep_mask
 
 
+# Numerics experiments only (scripts/curve_bisect.py): round every tensor the HIP path stores in
+# bf16 (activations between kernels, the pre-LN sums, attention probabilities before P.V) to bf16
+# here too -- in the forward and, through the casts' autograd, in the backward.
+BF16_STORAGE = False
+
+
+def _st(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.bfloat16).to(t.dtype) if BF16_STORAGE and t.dtype == torch.float32 else t
+
+
 def dropout_ref(x: torch.Tensor, p: float, counter: Optional[int], site: int) -> torch.Tensor:
     if p <= 0.0 or counter is None:
         return x
@@ -25,11 +35,11 @@ def dropout_ref(x: torch.Tensor, p: float, counter: Optional[int], site: int) ->
 
 
 def linear_ref(x, w, b=None):
-    return F.linear(x, w, b)
+    return _st(F.linear(x, w, b))
 
 
 def gelu_ref(x):
-    return F.gelu(x)  # exact erf form (HF GELUActivation)
+    return _st(F.gelu(x))  # exact erf form (HF GELUActivation)
 
 
 def add_ln_ref(x, r, gamma, beta, eps=1e-12, p=0.0, counter=None, site=0):
@@ -37,7 +47,7 @@ def add_ln_ref(x, r, gamma, beta, eps=1e-12, p=0.0, counter=None, site=0):
     z = dropout_ref(x, p, counter, site)
     if r is not None:
         z = z + r
-    return F.layer_norm(z, (z.shape[-1],), gamma, beta, eps)
+    return _st(F.layer_norm(_st(z), (z.shape[-1],), gamma, beta, eps))
 
 
 def embedding_ref(ids, word, pos, gamma, beta, eps=1e-12, p=0.0, counter=None, site=0):
@@ -45,7 +55,7 @@ def embedding_ref(ids, word, pos, gamma, beta, eps=1e-12, p=0.0, counter=None, s
     B, S = ids.shape
     z = word[ids.reshape(-1)] + pos[:S].repeat(B, 1)
     y = F.layer_norm(z, (z.shape[-1],), gamma, beta, eps)
-    return dropout_ref(y, p, counter, site)
+    return _st(dropout_ref(y, p, counter, site))
 
 
 def attention_ref(qkv: torch.Tensor, mask: torch.Tensor, B: int, S: int, H: int, p: float = 0.0,
@@ -58,8 +68,8 @@ def attention_ref(qkv: torch.Tensor, mask: torch.Tensor, B: int, S: int, H: int,
     scores = scores.masked_fill(keymask, float("-inf"))
     lse = torch.logsumexp(scores, dim=-1)
     probs = torch.softmax(scores, dim=-1)
-    probs = dropout_ref(probs, p, counter, site)
-    ctx = (probs @ v).permute(0, 2, 1, 3).reshape(B * S, D)
+    probs = _st(dropout_ref(probs, p, counter, site))
+    ctx = _st((probs @ v).permute(0, 2, 1, 3).reshape(B * S, D))
     return ctx, lse
 
 
