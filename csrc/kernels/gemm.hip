@@ -1181,13 +1181,8 @@ int pick_cfg(int kind, int M, int N, int K) {
     if (N % 192 == 0 && N >= 3072 && M >= 3584) return 3;
     if (N % 128 == 0 && N >= 3072 && M >= 2048) return 1;
     if (N % 192 == 0 && N >= 1536 && M >= 2048) return 6;
-    // N = 768 (out_lin fwd, FFN2 fwd, every dX back to the hidden size): 64x64 tiles give
-    // 2x the blocks of 128x64, so each CU runs 2-3 of them.  Faster in isolation (7.6 vs
-    // 7.8-8.1 us at K = 768, 17.9 vs 19.5 us at K = 2304; profiles/r1_gemm_cfg_sweep_T2688_
-    // small_tiles.txt) but not in the step (2.370 vs 2.367 ms, 3 A/B pairs,
-    // profiles/r1_ab_small_tiles.txt): opt-in with FD_GEMM_SMALL_TILES=1.
-    static const bool small = [] { const char* e = getenv("FD_GEMM_SMALL_TILES"); return e && atoi(e) != 0; }();
-    if (small && N < 1536 && M >= 1024) return 13;
+    // (N = 768 on 64 x 64 tiles -- 2-3 blocks per CU -- was faster in isolation but not in the
+    // step, 2.370 vs 2.367 ms, profiles/r1_ab_small_tiles.txt: removed)
     // N = 768 at M <= 4 k (the packed / padded bs32 step): 8-wave 128 x 64 tiles with two K
     // tiles per barrier (cfg 24) -- one block per CU still gets two waves per SIMD, and the
     // loop pays half the barriers.  2.21-2.25 vs 2.28 ms/step in the model (3 A/B pairs,

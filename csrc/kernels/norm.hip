@@ -736,14 +736,11 @@ __global__ __launch_bounds__(256) void colsum_batched_kernel(ColsumBatch cb) {
 
 constexpr int LN_GRID = 256;
 constexpr int LN_BWD_THREADS = 512;
-// LayerNorm backward: 512-thread blocks (16 rows per pass) on up to 256 blocks.  FD_LN_BWD_WIDE=1
-// selects 256-thread blocks on up to 512 (spreads a packed ~2.7 k-row batch over every CU) --
-// measured SLOWER, 2.476 vs 2.448 ms/step (more partial rows for the batched colsum).
+// LayerNorm backward: 512-thread blocks (16 rows per pass) on up to 256 blocks.  (256-thread
+// blocks on up to 512 -- every CU for a packed ~2.7 k-row batch -- measured slower, 2.476 vs
+// 2.448 ms/step: more partial rows for the batched colsum; removed, profiles/r1_ab_ln_bwd_wide_slower.txt.)
 constexpr int LN_BWD_GRID_MAX = 512;
-int ln_bwd_threads() {
-  static const int t = [] { const char* e = getenv("FD_LN_BWD_WIDE"); return (e && atoi(e) == 1) ? 256 : 512; }();
-  return t;
-}
+int ln_bwd_threads() { return LN_BWD_THREADS; }
 
 }  // namespace
 
