@@ -88,11 +88,11 @@ DEV bf16x8 tr_frag(const char* lds, int col0, int ks, int lane) {
 
 // Pack accumulator tiles 2ks, 2ks+1 (4 regs each) into a bf16x8 operand in the
 // permuted k order matching tr_frag.
+// (v_cvt_pk_bf16_f32: round-to-nearest-even like f2bf for every finite value -- P and dS are finite)
 DEV bf16x8 pack_acc(const f32x4& a, const f32x4& b) {
-  bf16x8 o;
-  o[0] = (short)f2bf(a[0]); o[1] = (short)f2bf(a[1]); o[2] = (short)f2bf(a[2]); o[3] = (short)f2bf(a[3]);
-  o[4] = (short)f2bf(b[0]); o[5] = (short)f2bf(b[1]); o[6] = (short)f2bf(b[2]); o[7] = (short)f2bf(b[3]);
-  return o;
+  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  const u32x4_t w = {pack_bf2(a[0], a[1]), pack_bf2(a[2], a[3]), pack_bf2(b[0], b[1]), pack_bf2(b[2], b[3])};
+  return __builtin_bit_cast(bf16x8, w);
 }
 
 DEV bf16x8 load_frag_global(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -535,6 +535,14 @@ DEV void stage_rows(char* lds, const bf16_t* src, long ld, int tid, int nt, int 
   }
 }
 
+// Forward, S <= 128: every key of the row at once.  The whole row (<= 128 keys, two 64-key
+// tiles) fits one wave's registers, so there is no online-softmax rescale: all score MFMAs issue
+// back to back (their K fragments read together), ONE row-max reduction, then exp / dropout and
+// all P.V MFMAs -- the earlier tile-by-tile loop paid two dependent cross-lane reductions, the
+// rescale and a keep-bit OR-reduction per tile, and the kernel spent 60 % of its wave-cycles
+// waiting (PMC, profiles/r3_rejected_register_staging.txt).  Varlen key masks are arithmetic
+// (k < len), not an LDS table.  Keep bits go out lane-major: u16 [q][kt * 4 + g], bit 4 t + r =
+// key 64 kt + 16 t + 4 g + r -- each lane stores its own bits, no cross-lane OR.
 __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 512];
   char* ks = smem;
@@ -556,100 +564,100 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   const int q0 = w * 16;
   const int q = q0 + (lane & 15);
   const int qr = min(q, len - 1);
+  const bool varlen = a.cu != nullptr;
   bf16x8 qf[2];  // this wave's Q rows, fetched together with the K/V staging loads
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) qf[s2] = load_frag_global(a.qkv + (tok0 + qr) * ld3 + h * DH + 32 * s2 + 8 * g);
   stage_rows(ks, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
   stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
-  if (tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) : -INFINITY;
+  if (!varlen && tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) : -INFINITY;
   __syncthreads();
   ASTAMP(1);
   const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows needed
   if (q0 >= qlen) return;  // no barrier follows
   const uint32_t seed = site_seed(a);
   const bool drop = a.drop_threshold != 0;
-  f32x4 o[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
-  const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
-  // Unmasked-key bits of the two 64-key tiles (wave-uniform).  A 16-key sub-tile whose keys
-  // are all masked has probabilities exactly 0: its score MFMAs, exp / dropout hashes and,
-  // when both halves of a 32-key step are empty, its PV MFMAs are skipped -- bitwise the
-  // same result (a ~80-token sequence in a 128-row tile does 5/8 of the work).
-  const uint64_t vk0 = __ballot(kb[lane] != -INFINITY);
-  const uint64_t vk1 = __ballot(kb[64 + lane] != -INFINITY);
-  uint64_t* dmask = (drop && a.dmask) ? a.dmask + (((size_t)b * H + h) * 128 + q) * 2 : nullptr;
-  for (int kt = 0; kt < nt; ++kt) {
-    const uint64_t vk = kt ? vk1 : vk0;
-    if (vk == 0) continue;  // fully masked key tile (exact skip)
-    bool tv[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) tv[t] = ((vk >> (16 * t)) & 0xffffull) != 0;
-    const char* kst = ks + kt * 8192;
-    const char* vst = vs + kt * 8192;
-    const int k0 = kt * 64;
-    uint32_t kbits[2] = {0u, 0u};  // this lane's keep bits of the tile (keys 16 t + 4 g + r)
-    f32x4 sc[4];
+  // live 16-key sub-tiles (wave-uniform), bit 4 kt + t: at least one unmasked key.  A sub-tile
+  // whose keys are all masked has probabilities exactly 0: its MFMAs and exp / hashes are skipped.
+  uint32_t live;
+  if (varlen) {
+    live = (1u << ((len + 15) >> 4)) - 1u;
+  } else {
+    const uint64_t vk0 = __ballot(kb[lane] != -INFINITY), vk1 = __ballot(kb[64 + lane] != -INFINITY);
+    live = 0u;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (!tv[t]) continue;  // score stays 0; the -inf key bias below masks it
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) sc[t] = mfma16(row_frag(kst, 16 * t, s2, lane), qf[s2], sc[t]);
+      live |= (((vk0 >> (16 * t)) & 0xffffull) != 0 ? 1u : 0u) << t;
+      live |= (((vk1 >> (16 * t)) & 0xffffull) != 0 ? 1u : 0u) << (4 + t);
     }
-    float mx = -INFINITY;
+  }
+  // ---- scores of every key of the row
+  f32x4 sc[2][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        sc[t][r] = sc[t][r] * a.scale + kb[k0 + 16 * t + 4 * g + r];
-        mx = fmaxf(mx, sc[t][r]);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float mref = mn == -INFINITY ? 0.f : mn;
-    const float alpha = __expf(m - mref);
-    m = mn;
-    l *= alpha;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] *= alpha;
+  for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      if (!tv[t]) {  // exp(-inf) = 0: nothing to add, nothing to hash
-        sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        continue;
-      }
+      sc[kt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!((live >> (4 * kt + t)) & 1u)) continue;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) sc[kt][t] = mfma16(row_frag(ks + kt * 8192, 16 * t, s2, lane), qf[s2], sc[kt][t]);
+    }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (!((live >> (4 * kt + t)) & 1u)) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = __expf(sc[t][r] - mref);
+        const int k = 64 * kt + 16 * t + 4 * g + r;
+        const float bias = varlen ? (k < len ? 0.f : -INFINITY) : kb[k];
+        sc[kt][t][r] = sc[kt][t][r] * a.scale + bias;
+        mx = fmaxf(mx, sc[kt][t][r]);
+      }
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float mref = mx == -INFINITY ? 0.f : mx;
+  const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
+  float l = 0.f;
+  uint32_t kw[2] = {0u, 0u};  // this lane's keep bits per key tile (bit 4 t + r)
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (!((live >> (4 * kt + t)) & 1u)) continue;  // stays 0: exp(-inf) = 0, nothing to hash
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = __expf(sc[kt][t][r] - mref);
         l += pv;
         float pd = pv;
         if (drop) {
-          const uint32_t key = k0 + 16 * t + 4 * g + r;
-          const bool keep = drop_keep(seed, rowidx + key, a.drop_threshold);
+          const bool keep = drop_keep(seed, rowidx + 64 * kt + 16 * t + 4 * g + r, a.drop_threshold);
           pd = keep ? pv * a.drop_scale : 0.f;
-          kbits[t >> 1] |= (uint32_t)keep << (16 * (t & 1) + 4 * g + r);
+          kw[kt] |= (uint32_t)keep << (4 * t + r);
         }
-        sc[t][r] = pd;
+        sc[kt][t][r] = pd;
       }
     }
-    if (dmask) {  // the row's 64 keep bits: OR of the four lane groups' disjoint bits
+  // ---- P . V over every live 32-key half
+  f32x4 o[4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        kbits[i] |= __shfl_xor(kbits[i], 16, 64);
-        kbits[i] |= __shfl_xor(kbits[i], 32, 64);
-      }
-      if (g == 0) dmask[kt] = (uint64_t)kbits[0] | ((uint64_t)kbits[1] << 32);
-    }
+  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      if (!(tv[2 * kk] || tv[2 * kk + 1])) continue;
-      const bf16x8 pf = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
+      if (!((live >> (4 * kt + 2 * kk)) & 3u)) continue;
+      const bf16x8 pf = pack_acc(sc[kt][2 * kk], sc[kt][2 * kk + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(tr_frag(vst, 16 * dt, kk, lane), pf, o[dt]);
+      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(tr_frag(vs + kt * 8192, 16 * dt, kk, lane), pf, o[dt]);
     }
+  if (drop && a.dmask) {
+    uint16_t* dm = reinterpret_cast<uint16_t*>(a.dmask) + (((size_t)b * H + h) * 128 + q) * 8 + g;
+    dm[0] = (uint16_t)kw[0];
+    dm[4] = (uint16_t)kw[1];
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -661,7 +669,7 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   for (int dt = 0; dt < 4; ++dt)
     *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) =
         make_uint2(pack_bf2(o[dt][0] * inv, o[dt][1] * inv), pack_bf2(o[dt][2] * inv, o[dt][3] * inv));
-  if (g == 0) a.lse[((size_t)b * H + h) * S + q] = m + __logf(l);
+  if (g == 0) a.lse[((size_t)b * H + h) * S + q] = mref + __logf(l);
   ASTAMP(3);
 }
 
@@ -674,7 +682,8 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   float* kb = reinterpret_cast<float*>(smem + 8 * 8192);
   float* lse_s = kb + 128;
   float* dl_s = lse_s + 128;
-  uint64_t* mk_s = reinterpret_cast<uint64_t*>(smem + 8 * 8192 + 3 * 512);  // [128 q][2] keep bits
+  uint64_t* mk_s = reinterpret_cast<uint64_t*>(smem + 8 * 8192 + 3 * 512);  // the forward's keep bits
+  const uint16_t* mk16 = reinterpret_cast<const uint16_t*>(mk_s);  // [128 q][kt * 4 + g], bit 4 t + r
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
@@ -764,7 +773,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
       for (int t = 0; t < 4; ++t) tv[t] = ((vk >> (16 * t)) & 0xffffull) != 0;
       const char* kst = ks + kt * 8192;
       const char* vst = vs + kt * 8192;
-      const uint64_t mrow = mk ? mk_s[qr * 2 + kt] : 0ull;
+      const uint32_t mrow = mk ? mk16[qr * 8 + kt * 4 + g] : 0u;  // this lane's keys 16 t + 4 g + r
       f32x4 sc[4], dp[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -786,7 +795,8 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
           const float pv = __expf(sc[t][r] * a.scale + kb[kt * 64 + kl] - lse);
           float dpv = dp[t][r];
           if (drop) {
-            const bool keep = mk ? ((mrow >> kl) & 1ull) != 0 : drop_keep(seed, rowidx + kt * 64 + kl, a.drop_threshold);
+            const bool keep = mk ? ((mrow >> (4 * t + r)) & 1u) != 0
+                                 : drop_keep(seed, rowidx + kt * 64 + kl, a.drop_threshold);
             dpv = keep ? dpv * a.drop_scale : 0.f;
           }
           sc[t][r] = pv * (dpv - dl);  // dS
@@ -826,6 +836,8 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   }
   const float kbias = kb[key];
   const uint32_t headidx = (uint32_t)(b * H + h) * S;
+  // this lane's key in the forward's lane-major keep bits: word kt * 4 + g', bit 4 t' + r'
+  const int kword = (key >> 6) * 4 + ((key >> 2) & 3), kbit = 4 * ((key >> 4) & 3) + (key & 3);
   f32x4 dk[4], dv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -872,7 +884,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
           const float pv = __expf(sc[t][r] * a.scale + kbias - lse_s[ql]);
           float dpv = dp[t][r], pdv = pv;
           if (drop) {
-            const bool keep = mk ? ((mk_s[ql * 2 + (key >> 6)] >> (key & 63)) & 1ull) != 0
+            const bool keep = mk ? ((mk16[ql * 8 + kword] >> kbit) & 1u) != 0
                                  : drop_keep(seed, (headidx + ql) * (uint32_t)S + key, a.drop_threshold);
             dpv = keep ? dpv * a.drop_scale : 0.f;
             pdv = keep ? pv * a.drop_scale : 0.f;
