@@ -500,7 +500,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
     *reinterpret_cast<uint2*>(outv + 16 * dt + 4 * g) =
         make_uint2(pack_bf2(dv[dt][0], dv[dt][1]), pack_bf2(dv[dt][2], dv[dt][3]));
   }
-  ASTAMP(4);
 }
 
 template <typename M>
@@ -726,6 +725,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   ASTAMP(1);
   const uint32_t seed = site_seed(a);
   const float sc_out = a.scale;
+  const bool varlen = a.cu != nullptr;  // key masks are arithmetic (k < len)
   // unmasked-key bits of the two 64-key tiles (see attn_fwd_s128_kernel): 16-key sub-tiles
   // with every key masked have P = dS = 0 exactly and are skipped in both phases
   const uint64_t vk0 = __ballot(kb[lane] != -INFINITY);
@@ -765,9 +765,10 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
     f32x4 dq[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nt; ++kt) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
       const uint64_t vk = kt ? vk1 : vk0;
-      if (vk == 0) continue;  // fully masked key tile: dS = 0
+      if (kt >= nt || vk == 0) continue;  // fully masked key tile: dS = 0
       bool tv[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) tv[t] = ((vk >> (16 * t)) & 0xffffull) != 0;
@@ -792,7 +793,8 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int kl = 16 * t + 4 * g + r;
-          const float pv = __expf(sc[t][r] * a.scale + kb[kt * 64 + kl] - lse);
+          const float bias = varlen ? (kt * 64 + kl < len ? 0.f : -INFINITY) : kb[kt * 64 + kl];
+          const float pv = __expf(sc[t][r] * a.scale + bias - lse);
           float dpv = dp[t][r];
           if (drop) {
             const bool keep = mk ? ((mrow >> (4 * t + r)) & 1u) != 0
@@ -846,7 +848,9 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   }
   // this wave's 16 keys all masked (padded layout): P and dS columns are 0, dK = dV = 0
   const bool keys_live = (((key0 < 64 ? vk0 >> key0 : vk1 >> (key0 - 64))) & 0xffffull) != 0;
-  for (int qt = 0; qt < (keys_live ? nt : 0); ++qt) {
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    if (!keys_live || qt >= nt) continue;
     const char* qst = qs + qt * 8192;
     const char* ost = os + qt * 8192;
     // 16-query sub-tiles past the sequence (varlen) have lse = +inf: P = dS = 0, skipped
@@ -878,10 +882,14 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
           pd[u] = f32x4{0.f, 0.f, 0.f, 0.f};
           continue;  // sc[t] = 0 already
         }
+        // the 4 query rows of this lane: one 16-byte LDS read each for their lse and delta
+        const float4 lse4 = *reinterpret_cast<const float4*>(lse_s + qt * 64 + 16 * t + 4 * g);
+        const float4 dl4 = *reinterpret_cast<const float4*>(dl_s + qt * 64 + 16 * t + 4 * g);
+        const float lsev[4] = {lse4.x, lse4.y, lse4.z, lse4.w}, dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ql = qt * 64 + 16 * t + 4 * g + r;
-          const float pv = __expf(sc[t][r] * a.scale + kbias - lse_s[ql]);
+          const float pv = __expf(sc[t][r] * a.scale + kbias - lsev[r]);
           float dpv = dp[t][r], pdv = pv;
           if (drop) {
             const bool keep = mk ? ((mk16[ql * 8 + kword] >> kbit) & 1u) != 0
@@ -890,7 +898,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
             pdv = keep ? pv * a.drop_scale : 0.f;
           }
           pd[u][r] = pdv;
-          sc[t][r] = pv * (dpv - dl_s[ql]);  // dS
+          sc[t][r] = pv * (dpv - dlv[r]);  // dS
         }
       }
       const bf16x8 pf = pack_acc(pd[0], pd[1]);
@@ -912,6 +920,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
     *reinterpret_cast<uint2*>(outv + 16 * dt + 4 * g) =
         make_uint2(pack_bf2(dv[dt][0], dv[dt][1]), pack_bf2(dv[dt][2], dv[dt][3]));
   }
+  ASTAMP(4);
 }
 
 bool use_s128(int S) {
