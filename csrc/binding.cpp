@@ -104,7 +104,7 @@ int fd_rank_sort(const void* ids, int ids64, int T, long long* sorted, long long
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
                 float* logits, float* loss, float* dlogits, float* row_loss, const int* cls, int T,
-                const float* tlogits, float kd_T, float kd_alpha, hipStream_t st);
+                const float* tlogits, float kd_T, float kd_alpha, float* loss_acc, hipStream_t st);
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
                 int accumulate, const int* cls, int T, const float* gscale, const int* own, hipStream_t st);
@@ -1012,7 +1012,10 @@ void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
               const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& labels,
               const at::Tensor& logits, const c10::optional<at::Tensor>& loss, const c10::optional<at::Tensor>& dlogits,
               const c10::optional<at::Tensor>& row_loss, const c10::optional<at::Tensor>& cls,
-              const c10::optional<at::Tensor>& tlogits, double kd_T, double kd_alpha) {
+              const c10::optional<at::Tensor>& tlogits, double kd_T, double kd_alpha,
+              const c10::optional<at::Tensor>& loss_acc) {
+  need_opt(loss_acc, at::kFloat, "loss_acc");
+  if (loss_acc.has_value() && loss_acc->defined()) TORCH_CHECK(loss_acc->numel() >= 1, "head_fwd: loss_acc [1]");
   need_opt(row_loss, at::kFloat, "row_loss");
   need_opt(tlogits, at::kFloat, "teacher logits");
   if (tlogits.has_value() && tlogits->defined())
@@ -1039,7 +1042,7 @@ void head_fwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
                        seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale,
                        ptr<const long long>(labels), logits.data_ptr<float>(), ptr<float>(loss), ptr<float>(dlogits),
                        ptr<float>(row_loss), ptr<int>(cls), (int)(hidden.numel() / D), ptr<const float>(tlogits),
-                       (float)kd_T, (float)kd_alpha, stream()),
+                       (float)kd_T, (float)kd_alpha, ptr<float>(loss_acc), stream()),
            "head_fwd");
 }
 
@@ -1251,7 +1254,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_fwd", &head_fwd, py::arg("hidden"), py::arg("B"), py::arg("S"), py::arg("W"), py::arg("bias"),
         py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("labels"), py::arg("logits"),
         py::arg("loss"), py::arg("dlogits"), py::arg("row_loss"), py::arg("cls"), py::arg("tlogits") = py::none(),
-        py::arg("kd_T") = 1.0, py::arg("kd_alpha") = 1.0);
+        py::arg("kd_T") = 1.0, py::arg("kd_alpha") = 1.0, py::arg("loss_acc") = py::none());
   m.def("head_bwd", &head_bwd, py::arg("hidden"), py::arg("B"), py::arg("S"), py::arg("W"), py::arg("seed"),
         py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("dlogits"), py::arg("dW"), py::arg("db"),
         py::arg("dhidden"), py::arg("accumulate"), py::arg("cls") = py::none(), py::arg("gscale") = py::none(),

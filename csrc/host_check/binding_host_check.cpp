@@ -368,8 +368,10 @@ int fd_colsum_batched(int, const float* const*, float* const*, const int*, const
 int fd_rank_sort(const void*, int, int, long long*, long long*, hipStream_t) { ++hc::calls; return 0; }
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias, const uint32_t* seed,
                 uint32_t, uint32_t, float, const long long* labels, float* logits, float* loss, float* dlogits,
-                float* row_loss, const int* cls, int T, const float* tlogits, float, float, hipStream_t) {
+                float* row_loss, const int* cls, int T, const float* tlogits, float, float, float* loss_acc,
+                hipStream_t) {
   ++hc::calls;
+  hc::opt_span(loss_acc, 4, "head loss_acc");
   hc::span(hidden, (long long)T * D * 2, "head hidden");
   hc::span(W, 2LL * D * 4, "head W");
   hc::span(bias, 8, "head bias");
@@ -676,13 +678,16 @@ int main() {
     auto lab = T_({B}, i64), logits = T_({B, 2}, f32), loss = T_({}, f32), dlog = T_({B, 2}, f32), rl = T_({B}, f32);
     auto tl = T_({B, 2}, f32);
     expect_ok("head fwd", [&] { head_fwd(hid, B, S, W, bias, seed, 2, 0, 1.0, lab, logits, loss, dlog, rl, none,
-                                         none, 1.0, 1.0); });
+                                         none, 1.0, 1.0, none); });
+    const c10::optional<at::Tensor> lacc = T_({1}, f32);
+    expect_ok("head fwd loss_acc", [&] { head_fwd(hid, B, S, W, bias, seed, 2, 0, 1.0, lab, logits, loss, dlog, rl,
+                                                  none, none, 1.0, 1.0, lacc); });
     expect_ok("head fwd kd", [&] { head_fwd(hid, B, S, W, bias, seed, 2, 0, 1.0, lab, logits, loss, dlog, rl, none, tl,
-                                            2.0, 0.5); });
+                                            2.0, 0.5, none); });
     expect_reject("head kd without labels", [&] { head_fwd(hid, B, S, W, bias, seed, 2, 0, 1.0, none, logits, none,
-                                                           none, none, none, tl, 2.0, 0.5); });
+                                                           none, none, none, tl, 2.0, 0.5, none); });
     expect_reject("head kd T <= 0", [&] { head_fwd(hid, B, S, W, bias, seed, 2, 0, 1.0, lab, logits, loss, dlog, rl,
-                                                   none, tl, 0.0, 0.5); });
+                                                   none, tl, 0.0, 0.5, none); });
     auto dW = T_({2, D}, f32), db = T_({2}, f32), dh = T_({B * S, D}, bf);
     expect_ok("head bwd", [&] { head_bwd(hid, B, S, W, seed, 2, 0, 1.0, dlog, dW, db, dh, false, none, none, none); });
     auto hid_small = T_({B * S - 1, D}, bf);

@@ -52,18 +52,17 @@ struct HeadArgs {
   // kd_alpha * CE(z, y) + (1 - kd_alpha) * T^2 * KL(softmax(t / T) || softmax(z / T))
   const float* tlogits;
   float kd_T, kd_alpha;
+  // nullable: the mean loss is also added here (a device-side running sum, e.g. a benchmark's
+  // loss over a graph-replayed loop, with no separate add launch per step)
+  float* loss_acc;
 };
 
 DEV size_t cls_row(const HeadArgs& a, int b) {
   return a.cls ? (size_t)min(max(a.cls[b], 0), a.T - 1) : (size_t)b * a.S;
 }
 
-// One wave per batch row (grid = ceil(B/4) blocks); per-row loss to row_loss,
-// reduced in a fixed order by head_loss_mean_kernel.
-__global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= a.B) return;
+// Row b of the head (one wave): logits, and with labels the row loss and dlogits.
+DEV void head_row(const HeadArgs& a, int b, int lane) {
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
   const bf16_t* x = a.hidden + cls_row(a, b) * a.D;
@@ -116,11 +115,34 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
   }
 }
 
-__global__ __launch_bounds__(64) void head_loss_mean_kernel(const float* row_loss, int B, float* loss) {
+// One wave per batch row (grid = ceil(B/4) blocks): logits only (no labels), or the rows of a
+// batch too large for head_fwd_mean_kernel (their loss reduced by head_loss_mean_kernel).
+__global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b < a.B) head_row(a, b, threadIdx.x & 63);
+}
+
+DEV void loss_mean(const HeadArgs& a, int lane) {  // one wave; fixed order
   float s = 0.f;
-  for (int b = threadIdx.x; b < B; b += 64) s += row_loss[b];
+  for (int b = lane; b < a.B; b += 64) s += a.row_loss[b];
   s = wave_sum(s);
-  if (threadIdx.x == 0) loss[0] = s / B;
+  if (lane == 0) {
+    a.loss[0] = s / a.B;
+    if (a.loss_acc) a.loss_acc[0] += s / a.B;
+  }
+}
+
+__global__ __launch_bounds__(64) void head_loss_mean_kernel(HeadArgs a) { loss_mean(a, threadIdx.x); }
+
+// With labels and B <= HEAD_MEAN_MAXB: ONE block of 16 waves takes every row (wave w: rows w,
+// w + 16, ...), then its first wave reduces the row losses -- the same sums in the same order as
+// head_fwd_kernel + head_loss_mean_kernel, one launch instead of two.
+constexpr int HEAD_MEAN_MAXB = 1024;
+__global__ __launch_bounds__(1024) void head_fwd_mean_kernel(HeadArgs a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int b = w; b < a.B; b += 16) head_row(a, b, lane);
+  __syncthreads();  // (every row loss written; workgroup-visible)
+  if (w == 0) loss_mean(a, lane);
 }
 
 DEV bool empty_seq(const HeadArgs& a, int b) { return a.own && a.own[b] == a.own[b + 1]; }
@@ -426,7 +448,7 @@ extern "C" {
 int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const float* bias,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const long long* labels,
                 float* logits, float* loss, float* dlogits, float* row_loss, const int* cls, int T,
-                const float* tlogits, float kd_T, float kd_alpha, hipStream_t st) {
+                const float* tlogits, float kd_T, float kd_alpha, float* loss_acc, hipStream_t st) {
   if (B > 65536) return 1;
   if (tlogits && (!labels || !(kd_T > 0.f))) return 3;
   HeadArgs a{};
@@ -435,9 +457,14 @@ int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const f
   a.hidden = (const bf16_t*)hidden; a.B = B; a.S = S; a.D = D; a.W = W; a.bias = bias;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.labels = labels;
   a.logits = logits; a.loss = loss; a.dlogits = dlogits; a.row_loss = row_loss;
+  a.loss_acc = labels ? loss_acc : nullptr;
   if (labels && !row_loss) return 2;
+  if (labels && B <= HEAD_MEAN_MAXB) {
+    hipLaunchKernelGGL(head_fwd_mean_kernel, dim3(1), dim3(1024), 0, st, a);
+    return 0;
+  }
   hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st, a);
-  if (labels) hipLaunchKernelGGL(head_loss_mean_kernel, dim3(1), dim3(64), 0, st, row_loss, B, loss);
+  if (labels) hipLaunchKernelGGL(head_loss_mean_kernel, dim3(1), dim3(64), 0, st, a);
   return 0;
 }
 

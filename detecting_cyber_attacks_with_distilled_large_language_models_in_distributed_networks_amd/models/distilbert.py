@@ -262,6 +262,10 @@ class DDoSClassifier(nn.Module):
         # HIP path: every weight gradient of the step in one launch at the end of the backward
         # (RunCtx.dw_batch; needs no per-block gradient hook / weight-gradient side stream)
         self.batch_dw = os.environ.get("FD_BATCH_DW", "1") != "0"
+        # optional fp32 [1] device tensor: the HIP head kernel adds every training step's mean
+        # loss to it (RunCtx.loss_acc; bench.py reads one sum after a graph-replayed loop).  A
+        # captured graph holds its address: keep it alive as long as that graph is replayed.
+        self.loss_acc = None
         # HIP path: when the caller passes the batch's real-token count (DeviceLoader does,
         # from host-side lengths -- no sync), run the transformer blocks on the packed real
         # tokens only (~37 % of a seq128 CICIDS2017 batch is padding).  Rows are rounded up
@@ -490,7 +494,8 @@ class DDoSClassifier(nn.Module):
         kbias = self._no_bias() if packed else K.mask_bias(mask)
         rc = RunCtx(B=B, S=S, H=cfg.n_heads, kbias=kbias, seed=self.rng, training=self.training,
                     eps=cfg.layer_norm_eps, p_hidden=cfg.dropout, p_attn=cfg.attention_dropout, p_head=self.dropout.p,
-                    on_layer_grads=self.layer_grads_hook if grad else None, group_dw=self.group_dw)
+                    on_layer_grads=self.layer_grads_hook if grad else None, group_dw=self.group_dw,
+                    loss_acc=getattr(self, "loss_acc", None))
         if grad and self.defer_colsum and self.layer_grads_hook is None:
             rc.colsum_jobs = []  # (a per-block hook needs each block's grads final at once)
         if grad and self.defer_dw_reduce and self.layer_grads_hook is None:

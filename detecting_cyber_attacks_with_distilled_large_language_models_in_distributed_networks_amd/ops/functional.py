@@ -73,6 +73,9 @@ class RunCtx:
     # backward anyway (each block's dqkv, kept for the dW launch) -- their partials are computed
     # in ONE launch at the end (ops/kernels.py colsum_partials_batched) instead of one per block
     colsum_pending: Optional[list] = None
+    # fp32 [1] device running sum of the fused loss (the model's ``loss_acc``): the head kernel
+    # adds each step's mean loss, so a graph-replayed loop needs no add launch of its own
+    loss_acc: Optional[torch.Tensor] = None
     # Last-block [CLS] pruning: the loss reads only each sequence's [CLS] row of the last block's
     # output, and every row of a block's FFN / out-proj / LayerNorms is computed independently of
     # the others, so in the LAST block only the [CLS] rows of everything after the attention can
@@ -384,7 +387,8 @@ class HeadFn(torch.autograd.Function):
         p = rc.p_head if rc.training else 0.0
         # packed: [CLS] = first row of each sequence; pruned last block: row b of its output
         cls = rc.head_rows if rc.head_rows is not None else rc.cu[:-1] if rc.cu is not None else None
-        logits, loss, dlog = K.head_fwd(hidden, rc.B, rc.S, W, b, rc.seed, 2, p, labels, cls, kd)
+        logits, loss, dlog = K.head_fwd(hidden, rc.B, rc.S, W, b, rc.seed, 2, p, labels, cls, kd,
+                                        loss_acc=rc.loss_acc if rc.training else None)
         ctx.rc, ctx.sinks, ctx.p, ctx.W = rc, sinks, p, W
         ctx.save_for_backward(hidden)
         ctx.dlog = dlog

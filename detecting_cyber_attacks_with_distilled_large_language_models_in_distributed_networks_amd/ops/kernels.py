@@ -571,10 +571,11 @@ def emb_bwd(dy, ids, sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos
 
 
 # ------------------------------------------------------------------ head / metrics / optimizer
-def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None, cls=None, kd=None):
+def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None, cls=None, kd=None, loss_acc=None):
     """cls (int32 [B]): packed layout -- sequence b's [CLS] is row cls[b] of hidden.
     kd = (teacher logits fp32 [B, 2], T, alpha): the fused loss is the distillation loss
-    alpha * CE + (1 - alpha) * T^2 * KL(softmax(t/T) || softmax(z/T)) (models/bert.py kd_loss)."""
+    alpha * CE + (1 - alpha) * T^2 * KL(softmax(t/T) || softmax(z/T)) (models/bert.py kd_loss).
+    loss_acc (fp32 [1], optional): the mean loss is also added to it on the device."""
     logits = torch.empty(B, 2, dtype=torch.float32, device=hidden.device)
     loss = dlogits = row_loss = None
     if labels is not None:
@@ -586,7 +587,7 @@ def head_fwd(hidden, B, S, W, b, seed, site, p, labels=None, cls=None, kd=None):
     if t is not None:
         t = t.detach().float().contiguous()
     ext().head_fwd(hidden, B, S, W, b, seed, site, thr, sc, labels, logits, loss, dlogits, row_loss, cls,
-                   t, float(T), float(alpha))
+                   t, float(T), float(alpha), loss_acc if labels is not None else None)
     return logits, loss, dlogits
 
 

@@ -1,12 +1,11 @@
 #!/bin/bash
-# Targeted GPU tests + headline bench + kernel stats (round 3 iteration loop).
+# Targeted GPU tests, then N headline benches (no quality protocol) and a kernel-stats profile.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/${1:-r3chk}; mkdir -p $O
-shift
-TESTS=${@:-tests/}
-timeout -k 10 900 python -u -m pytest $TESTS -x -q -m gpu --timeout 300 --timeout-method thread > $O/tests.log 2>&1
-rc=$?; tail -5 $O/tests.log
-if [ $rc -ne 0 ]; then echo "tests rc=$rc: stopping"; exit $rc; fi
-timeout -k 10 300 python bench.py --steps 50 --warmup 10 > $O/bench.log 2>&1 && tail -1 $O/bench.log | cut -c1-400 &&
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/raw -- python3 bench.py --steps 20 --warmup 3 --spinup-seconds 0 --no-quality > $O/prof_bench.log 2>&1 &&
-f=$(find $O/raw -name "*kernel_stats.csv" | head -1) && python scripts/kstats.py "$f" auto 40 > $O/kernel_stats.txt && head -24 $O/kernel_stats.txt
+O=gpurun_out/${1:-check}; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_model_gpu.py tests/test_dw_batch_gpu.py tests/test_fused_adam_gpu.py tests/test_prune_gpu.py tests/test_packed_gpu.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; tail -3 $O/tests.log; [ $rc -ne 0 ] && { grep -B3 -A25 "Error\|assert" $O/tests.log | head -50; exit $rc; }
+for i in 1 2 3; do
+  timeout -k 10 300 python bench.py --steps 200 --warmup 10 --no-quality > $O/bench_$i.log 2>&1 || { tail -5 $O/bench_$i.log; exit 1; }
+  python -c "import json; d=json.loads(open('$O/bench_$i.log').read().splitlines()[-1]); print('bench', d['ms_per_step'], d['value'], d['mean_loss'])"
+done
+bash scripts/gpu_prof_quick.sh $(basename $O)_prof

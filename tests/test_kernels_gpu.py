@@ -313,6 +313,30 @@ def test_head():
     assert rel_err(dh, gh) < 1e-2
 
 
+@pytest.mark.parametrize("B", [32, 1500])
+def test_head_loss_mean_and_device_accumulator(B):
+    """With labels the head forward's mean loss comes from one launch for B <= 1024 (16 waves take
+    every row, wave 0 reduces -- head_fwd_mean_kernel) and from head_fwd + head_loss_mean beyond;
+    both add it to an optional device running sum (bench.py's graph-replayed loop)."""
+    S, D = 1, 768
+    hidden = bf(B * S, D, seed=29)
+    W = torch.randn(2, D, device=DEV) * 0.05
+    b = torch.randn(2, device=DEV)
+    labels = torch.randint(0, 2, (B,), device=DEV)
+    acc = torch.full((1,), 0.5, device=DEV)
+    losses = []
+    for _ in range(3):
+        logits, loss, _ = kn.head_fwd(hidden, B, S, W, b, seed_t(2), 2, 0.0, labels, loss_acc=acc)
+        losses.append(loss.clone())
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.cross_entropy(hidden.float() @ W.t() + b, labels)
+    assert abs(losses[0].item() - ref.item()) < 1e-4
+    assert all(torch.equal(losses[0], x) for x in losses)
+    assert abs(acc.item() - (0.5 + 3 * losses[0].item())) < 1e-5
+    _, loss_plain, _ = kn.head_fwd(hidden, B, S, W, b, seed_t(2), 2, 0.0, labels)
+    assert torch.equal(loss_plain, losses[0])
+
+
 def test_adam_matches_torch():
     n = 4096 + 64
     p0 = torch.randn(n, device=DEV)
