@@ -276,6 +276,11 @@ struct EmbArgs {
   // advanced once per model forward here -- the first kernel of every forward -- so the fused
   // LayerNorm launches of this forward / backward tag their row statistics with a fresh epoch
   int* ln_epoch;
+  // forward only (nullable): the word-gradient grouping of the backward (rank sort of ids) is
+  // computed by extra blocks of the forward launch (sort_blocks of them, after the rows' blocks)
+  long long* sorted;
+  long long* perm;
+  int sort_blocks;
 };
 
 DEV int padded_row(const EmbArgs& a, int row) { return a.row_map ? max(a.row_map[row], 0) : row; }
@@ -284,8 +289,62 @@ DEV long load_id(const EmbArgs& a, int t) {
   return a.ids64 ? reinterpret_cast<const long long*>(a.ids)[t] : reinterpret_cast<const int*>(a.ids)[t];
 }
 
+// Deterministic token grouping without a library sort: the sorted position of
+// token t is the number of tokens with key (id, index) smaller than its own
+// (a rank sort; O(T^2) compares but T <= 16k and every compare is an LDS
+// broadcast).  4 threads per token each scan a quarter of the keys.
+template <typename I>
+DEV void rank_sort_block(const I* ids, int T, long long* sorted, long long* perm, int* keys, int blk) {
+  for (int i = threadIdx.x; i < T; i += 256) keys[i] = (int)ids[i];
+  __syncthreads();
+  // 16 tokens per block, 16 threads per token (grid = T/16 blocks: ~256 for a bs32 batch,
+  // one per CU, instead of T/64 blocks that left 3/4 of the chip idle)
+  const int t = blk * 16 + (threadIdx.x >> 4);
+  const int part = threadIdx.x & 15;
+  int cnt = 0;
+  int my = 0;
+  if (t < T) {
+    my = keys[t];
+    // the 16 threads of a token read adjacent 16-byte groups: one ds_read_b128 each,
+    // 256 contiguous bytes per token (the wave's 4 tokens read the same bytes: broadcast)
+    const int T4 = T & ~63;
+    for (int j = 4 * part; j < T4; j += 64) {
+      const int4 k = *reinterpret_cast<const int4*>(keys + j);
+      cnt += (k.x < my) | ((k.x == my) & (j < t));
+      cnt += (k.y < my) | ((k.y == my) & (j + 1 < t));
+      cnt += (k.z < my) | ((k.z == my) & (j + 2 < t));
+      cnt += (k.w < my) | ((k.w == my) & (j + 3 < t));
+    }
+    for (int j = T4 + part; j < T; j += 16) {
+      const int k = keys[j];
+      cnt += (k < my) | ((k == my) & (j < t));
+    }
+  }
+  cnt += __shfl_xor(cnt, 1, 64);
+  cnt += __shfl_xor(cnt, 2, 64);
+  cnt += __shfl_xor(cnt, 4, 64);
+  cnt += __shfl_xor(cnt, 8, 64);
+  if (t < T && part == 0) {
+    sorted[cnt] = my;
+    perm[cnt] = t;
+  }
+}
+
+template <typename I>
+__global__ __launch_bounds__(256) void rank_sort_kernel(const I* ids, int T, long long* sorted, long long* perm) {
+  extern __shared__ __attribute__((aligned(16))) int keys[];  // T ids
+  rank_sort_block<I>(ids, T, sorted, perm, keys, blockIdx.x);
+}
+
 template <int NC>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbArgs a) {
+  if (a.sort_blocks && (int)blockIdx.x >= (int)gridDim.x - a.sort_blocks) {  // block-uniform
+    extern __shared__ __attribute__((aligned(16))) int keys[];  // T ids
+    const int blk = blockIdx.x - (gridDim.x - a.sort_blocks);
+    if (a.ids64) rank_sort_block<long long>(reinterpret_cast<const long long*>(a.ids), a.T, a.sorted, a.perm, keys, blk);
+    else rank_sort_block<int>(reinterpret_cast<const int*>(a.ids), a.T, a.sorted, a.perm, keys, blk);
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (a.ln_epoch && blockIdx.x == 0 && threadIdx.x == 0) a.ln_epoch[0] += 1;  // (read by later launches only)
@@ -447,48 +506,6 @@ __global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* d
       t.x += r.x; t.y += r.y; t.z += r.z; t.w += r.w;
     }
     reinterpret_cast<float4*>(dpos + (size_t)s * D)[c4] = t;
-  }
-}
-
-// Deterministic token grouping without a library sort: the sorted position of
-// token t is the number of tokens with key (id, index) smaller than its own
-// (a rank sort; O(T^2) compares but T <= 16k and every compare is an LDS
-// broadcast).  4 threads per token each scan a quarter of the keys.
-template <typename I>
-__global__ __launch_bounds__(256) void rank_sort_kernel(const I* ids, int T, long long* sorted, long long* perm) {
-  extern __shared__ __attribute__((aligned(16))) int keys[];  // T ids
-  for (int i = threadIdx.x; i < T; i += 256) keys[i] = (int)ids[i];
-  __syncthreads();
-  // 16 tokens per block, 16 threads per token (grid = T/16 blocks: ~256 for a bs32 batch,
-  // one per CU, instead of T/64 blocks that left 3/4 of the chip idle)
-  const int t = blockIdx.x * 16 + (threadIdx.x >> 4);
-  const int part = threadIdx.x & 15;
-  int cnt = 0;
-  int my = 0;
-  if (t < T) {
-    my = keys[t];
-    // the 16 threads of a token read adjacent 16-byte groups: one ds_read_b128 each,
-    // 256 contiguous bytes per token (the wave's 4 tokens read the same bytes: broadcast)
-    const int T4 = T & ~63;
-    for (int j = 4 * part; j < T4; j += 64) {
-      const int4 k = *reinterpret_cast<const int4*>(keys + j);
-      cnt += (k.x < my) | ((k.x == my) & (j < t));
-      cnt += (k.y < my) | ((k.y == my) & (j + 1 < t));
-      cnt += (k.z < my) | ((k.z == my) & (j + 2 < t));
-      cnt += (k.w < my) | ((k.w == my) & (j + 3 < t));
-    }
-    for (int j = T4 + part; j < T; j += 16) {
-      const int k = keys[j];
-      cnt += (k < my) | ((k == my) & (j < t));
-    }
-  }
-  cnt += __shfl_xor(cnt, 1, 64);
-  cnt += __shfl_xor(cnt, 2, 64);
-  cnt += __shfl_xor(cnt, 4, 64);
-  cnt += __shfl_xor(cnt, 8, 64);
-  if (t < T && part == 0) {
-    sorted[cnt] = my;
-    perm[cnt] = t;
   }
 }
 
@@ -783,14 +800,18 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const int* row_map,
-               int* ln_epoch, hipStream_t st) {
+               int* ln_epoch, long long* sorted, long long* perm, hipStream_t st) {
   if (D != 768) return 1;
+  if ((sorted == nullptr) != (perm == nullptr) || (sorted && T > 16384)) return 2;
   EmbArgs a{};
   a.ln_epoch = ln_epoch;
+  a.sorted = sorted; a.perm = perm;
+  a.sort_blocks = sorted ? (T + 15) / 16 : 0;
   a.ids = ids; a.ids64 = ids64; a.word = (const bf16_t*)word; a.pos = (const bf16_t*)pos; a.gamma = gamma;
   a.beta = beta; a.y = (bf16_t*)y; a.mean = mean; a.rstd = rstd; a.T = T; a.S = S; a.D = D; a.eps = eps;
   a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.row_map = row_map;
-  hipLaunchKernelGGL(emb_fwd_kernel<3>, dim3((T + 3) / 4), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(emb_fwd_kernel<3>, dim3((T + 3) / 4 + a.sort_blocks), dim3(256),
+                     sorted ? (size_t)T * sizeof(int) : 0, st, a);
   return 0;
 }
 

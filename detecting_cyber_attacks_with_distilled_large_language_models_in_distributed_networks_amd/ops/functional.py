@@ -110,8 +110,12 @@ class EmbeddingFn(torch.autograd.Function):
     def forward(ctx, token, ids, word, pos, gamma, beta, sinks, rc: RunCtx):
         p = rc.p_hidden if rc.training else 0.0
         # (the first launch of the forward also starts the fused LayerNorms' exchange epoch)
-        y, mean, rstd = K.emb_fwd(ids, word, pos, gamma, beta, rc.S, rc.eps, rc.seed, 1, p, rc.row_map,
-                                  ln_epoch=K.ln_epoch(ids.device, gamma.numel()) if rc.fuse_ln else None)
+        # (a training forward's launch also groups the ids for the word gradient: no sort in the tail)
+        group = bool(ctx.needs_input_grad[0])
+        out = K.emb_fwd(ids, word, pos, gamma, beta, rc.S, rc.eps, rc.seed, 1, p, rc.row_map,
+                        ln_epoch=K.ln_epoch(ids.device, gamma.numel()) if rc.fuse_ln else None, group=group)
+        y, mean, rstd = out[:3]
+        ctx.grouped = out[3] if group else None
         ctx.rc, ctx.sinks, ctx.p = rc, sinks, p
         ctx.tensors = (ids, word, pos, gamma, mean, rstd)
         return y
@@ -136,7 +140,7 @@ class EmbeddingFn(torch.autograd.Function):
     def _tail(ctx, dy):
         ids, word, pos, gamma, mean, rstd = ctx.tensors
         s = ctx.sinks
-        srt, perm = K.group_ids(ids)
+        srt, perm = ctx.grouped if ctx.grouped is not None else K.group_ids(ids)
         acc = s["word"].accumulate()
         for k in ("pos", "ln_w", "ln_b"):
             assert s[k].accumulate() == acc

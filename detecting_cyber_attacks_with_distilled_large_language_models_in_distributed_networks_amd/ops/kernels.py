@@ -535,7 +535,7 @@ def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, see
 def group_ids(ids: torch.Tensor):
     """(sorted ids, positions) grouping equal ids -- deterministic rank sort on device."""
     flat = ids.reshape(-1).contiguous()
-    if flat.numel() > 16384:
+    if flat.numel() > RANK_SORT_MAX:
         return torch.sort(flat, stable=True)
     srt = torch.empty(flat.numel(), dtype=torch.int64, device=flat.device)
     perm = torch.empty_like(srt)
@@ -543,17 +543,28 @@ def group_ids(ids: torch.Tensor):
     return srt, perm
 
 
-def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p, row_map=None, ln_epoch=None):
+RANK_SORT_MAX = 16384  # csrc/kernels/norm.hip rank sort: T ids in LDS
+
+
+def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p, row_map=None, ln_epoch=None, group=False):
     """row_map (int32 [T]): ``ids`` are packed real tokens; positions and dropout follow the padded row.
-    ln_epoch (``ln_epoch(device)``): also advance the LayerNorm-fused GEMMs' exchange epoch."""
+    ln_epoch (``ln_epoch(device)``): also advance the LayerNorm-fused GEMMs' exchange epoch.
+    group: also return the backward's id grouping (``group_ids``), computed by extra blocks of
+    the same launch (T <= RANK_SORT_MAX; None beyond) -- the backward tail then has no sort launch."""
     T = ids.numel()
     D = gamma.numel()
     y = torch.empty(T, D, dtype=torch.bfloat16, device=ids.device)
     mean = torch.empty(T, dtype=torch.float32, device=ids.device)
     rstd = torch.empty(T, dtype=torch.float32, device=ids.device)
     thr, sc = _drop(p)
+    srt = perm = None
+    if group and T <= RANK_SORT_MAX:
+        srt = torch.empty(T, dtype=torch.int64, device=ids.device)
+        perm = torch.empty_like(srt)
     ext().emb_fwd(ids.contiguous(), word, pos, gamma, beta, y, mean, rstd, S, eps, seed, site, thr, sc, row_map,
-                  ln_epoch)
+                  ln_epoch, srt, perm)
+    if group:
+        return y, mean, rstd, ((srt, perm) if srt is not None else None)
     return y, mean, rstd
 
 

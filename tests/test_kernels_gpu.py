@@ -313,6 +313,29 @@ def test_head():
     assert rel_err(dh, gh) < 1e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
+def test_emb_fwd_groups_ids_like_rank_sort(dtype):
+    """The embedding forward's extra blocks group the ids for the word gradient exactly as the
+    standalone rank sort does (same sorted ids, same stable permutation), and the rows' outputs
+    do not change."""
+    T, S, D = 2688, 128, 768
+    g = torch.Generator(device=DEV).manual_seed(41)
+    ids = torch.randint(0, 30522, (T,), device=DEV, generator=g)
+    ids[::7] = 101  # heavy duplicates (a template word per row)
+    ids = ids.to(dtype)
+    word = bf(30522, D, seed=42)
+    pos = bf(512, D, seed=43)
+    gamma, beta = torch.randn(D, device=DEV), torch.randn(D, device=DEV)
+    y0, m0, r0 = kn.emb_fwd(ids, word, pos, gamma, beta, S, 1e-12, seed_t(4), 1, 0.1)
+    y1, m1, r1, grp = kn.emb_fwd(ids, word, pos, gamma, beta, S, 1e-12, seed_t(4), 1, 0.1, group=True)
+    srt, perm = kn.group_ids(ids)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1) and torch.equal(m0, m1) and torch.equal(r0, r1)
+    assert torch.equal(grp[0], srt) and torch.equal(grp[1], perm)
+    ref_s, ref_p = torch.sort(ids.long(), stable=True)
+    assert torch.equal(grp[0], ref_s) and torch.equal(grp[1], ref_p)
+
+
 @pytest.mark.parametrize("B", [32, 1500])
 def test_head_loss_mean_and_device_accumulator(B):
     """With labels the head forward's mean loss comes from one launch for B <= 1024 (16 waves take
