@@ -97,6 +97,10 @@ def _args(argv=None):
     ap.add_argument("--kd-alpha", type=float, default=0.9,
                     help="distillation loss weight of the CE term: alpha CE + (1 - alpha) T^2 KL")
     ap.add_argument("--kd-temperature", type=float, default=2.0)
+    ap.add_argument("--virtual-clients", type=int, default=2,
+                    help="one-GPU job: the quality protocol trains this many federated clients in turn on the "
+                         "GPU (seeds 42, 43, ...) and averages them -- the reference's 2-client FedAvg round "
+                         "(1: a single client, whose FedAvg is an identity)")
     return ap.parse_args(argv)
 
 
@@ -315,6 +319,10 @@ def main():
     comm.barrier()
     sync()
     dt_rank = time.perf_counter() - t0
+    if args.impl == "hip" and on_gpu and getattr(model, "fuse_ln", False):
+        # a LayerNorm-fused GEMM whose row-block rendezvous timed out inside the timed window
+        # produced wrong statistics: fail loudly instead of reporting its throughput
+        import_module(f"{PKG}.ops.kernels").check_ln_error(dev, cfg.dim)
     per_rank_ms = [round(1000.0 * v[0] / args.steps, 4) for v in comm.all_gather_floats([dt_rank])]
     dt = comm.all_reduce_max(dt_rank)
     loss = float((model.loss_acc if dev_acc else loss_acc).sum().item()) / args.steps
@@ -335,7 +343,8 @@ def main():
         torch.cuda.empty_cache()
 
     # ---- quality: 3 local epochs + 1 FedAvg round through the federated client (untimed)
-    quality = {} if args.no_quality else _quality(client, di, comm, q_rows, q_epochs, on_gpu)
+    quality = {} if args.no_quality else _quality(client, di, comm, q_rows, q_epochs, on_gpu,
+                                                  n_virtual=args.virtual_clients)
     n = di.world_size
     clients = topo.num_clients
     per_client = args.steps / dt
@@ -432,9 +441,56 @@ def _fedavg_timing(model, di, fedavg, comm, ncomm, k, sync):
             "allreduce_busbw_GBps": round(2.0 * (n - 1) / n * nbytes / r / 1e9, 2)}
 
 
-def _quality(client, di, comm, rows, epochs, on_gpu):
+def _quality_virtual(client, rows, epochs, on_gpu, n_virtual):
+    """1-GPU job: the reference's 2-client round with both clients trained one after the other on
+    this GPU (fed/runner.py run_virtual_clients): seeds 42 / 43, the same init, 3 local epochs each,
+    the FedAvg sum + scale_cast, each client's test split evaluated on its local model and on the
+    aggregate (client1_local_metrics.csv / client1_aggregated_metrics.csv)."""
+    from importlib import import_module
+    runner = import_module(f"{PKG}.fed.runner")
+    t0 = time.perf_counter()
+    res = runner.run_virtual_clients(client, n_virtual)
+    if on_gpu:
+        torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    (tn, fp), (fn, tp) = res["aggregated_confusion"]
+    prec = tp / (tp + fp) if tp + fp else 0.0
+    rec_ = tp / (tp + fn) if tp + fn else 0.0
+    f1 = 2 * prec * rec_ / (prec + rec_) if prec + rec_ else 0.0
+    total = tp + fp + fn + tn
+    cl = res["clients"]
+    return {"aggregated_f1": round(f1, 5),
+            "aggregated_accuracy_pct": round(100.0 * (tp + tn) / max(total, 1), 3),
+            "aggregated_confusion": [[int(tn), int(fp)], [int(fn), int(tp)]],
+            "min_client_aggregated_accuracy_pct": round(min(c["aggregated_test"]["accuracy"] for c in cl), 3),
+            "min_client_aggregated_f1": round(min(c["aggregated_test"]["f1"] for c in cl), 5),
+            "mean_client_local_accuracy_pct": round(float(np.mean([c["local_test"]["accuracy"] for c in cl])), 3),
+            "mean_client_local_f1": round(float(np.mean([c["local_test"]["f1"] for c in cl])), 5),
+            "quality_virtual_clients": n_virtual,
+            "quality_clients": n_virtual,
+            "per_client": [{"client": c["client"], "seed": client.cfg.client_seed(c["client"] - 1),
+                            "train_rows": c["train_rows"], "test_rows": c["test_rows"],
+                            "local_accuracy_pct": round(c["local_test"]["accuracy"], 3),
+                            "local_f1": round(c["local_test"]["f1"], 5),
+                            "aggregated_accuracy_pct": round(c["aggregated_test"]["accuracy"], 3),
+                            "aggregated_f1": round(c["aggregated_test"]["f1"], 5),
+                            "aggregated_confusion": c["aggregated_test"]["confusion_matrix"],
+                            "rel_l2_local_to_aggregate": float(f"{c['rel_l2_local_to_aggregate']:.4e}"),
+                            "epoch_losses": [round(x, 5) for x in c["train"]["epoch_losses"]],
+                            "train_steps": c["train"]["steps"]} for c in cl],
+            "eval_rows": int(total), "eval_rows_per_client": int(total) // max(len(cl), 1),
+            "train_rows_per_client": cl[0]["train_rows"], "fedavg_rounds": 1, "local_epochs": epochs,
+            "quality_file_rows": rows, "quality_fedavg_ms": round(res["fedavg_ms"], 3),
+            "quality_train_batches_per_sec": round(float(np.mean([c["train"]["batches_per_sec"] for c in cl])), 2),
+            "quality_wall_s": round(wall, 2), "quality_lr": client.cfg.lr}
+
+
+def _quality(client, di, comm, rows, epochs, on_gpu, n_virtual=1):
     """Run round 1 of the federated client (fed/runner.py run_round: local train -> local eval
-    -> FedAvg -> aggregated eval) and pool the aggregated test confusion matrices of all clients."""
+    -> FedAvg -> aggregated eval) and pool the aggregated test confusion matrices of all clients.
+    n_virtual > 1 (a one-process job): that many clients trained in turn on this device instead."""
+    if n_virtual > 1 and not di.distributed and client.teacher is None:
+        return _quality_virtual(client, rows, epochs, on_gpu, n_virtual)
     t0 = time.perf_counter()
     rec = client.run_round(0)
     if on_gpu:

@@ -81,7 +81,7 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const int* row_map, int* ln_epoch,
-               long long* sorted, long long* perm, hipStream_t st);
+               unsigned long long* ln_stats, long long ln_stats_n, long long* sorted, long long* perm, hipStream_t st);
 int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sorted, const long long* perm,
                const void* word, const void* pos, const float* gamma, const float* mean, const float* rstd,
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
@@ -860,7 +860,8 @@ void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& po
              const at::Tensor& beta, const at::Tensor& y, const at::Tensor& mean, const at::Tensor& rstd, int64_t S,
              double eps, const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
              const c10::optional<at::Tensor>& row_map, const c10::optional<at::Tensor>& ln_epoch,
-             const c10::optional<at::Tensor>& sorted, const c10::optional<at::Tensor>& perm) {
+             const c10::optional<at::Tensor>& sorted, const c10::optional<at::Tensor>& perm,
+             const c10::optional<at::Tensor>& ln_stats) {
   TORCH_CHECK(on_device(ids) && ids.is_contiguous() && (ids.scalar_type() == at::kLong || ids.scalar_type() == at::kInt),
               "ids must be contiguous GPU int64/int32");
   // optional: the backward's id grouping (rank sort) computed by extra blocks of this launch
@@ -872,6 +873,10 @@ void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& po
     TORCH_CHECK(sorted->numel() == ids.numel() && perm->numel() == ids.numel() && ids.numel() <= 16384,
                 "emb_fwd: sorted / perm need ids.numel() (<= 16384) elements");
   need_opt(ln_epoch, at::kInt, "ln_epoch");
+  need_opt(ln_stats, at::kLong, "ln_stats");
+  const bool has_stats = ln_stats.has_value() && ln_stats->defined();
+  TORCH_CHECK(!has_stats || (ln_epoch.has_value() && ln_epoch->defined() && ln_stats->numel() > 0),
+              "emb_fwd: ln_stats needs ln_epoch");
   need(word, at::kBFloat16, "word");
   need(pos, at::kBFloat16, "pos");
   need(gamma, at::kFloat, "gamma");
@@ -884,7 +889,9 @@ void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& po
   check_rc(fd_emb_fwd(ids.data_ptr(), ids.scalar_type() == at::kLong, word.data_ptr(), pos.data_ptr(),
                       gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(), mean.data_ptr<float>(),
                       rstd.data_ptr<float>(), (int)T, (int)S, (int)D, (float)eps, seedp(seed), (uint32_t)site,
-                      (uint32_t)thr, (float)dscale, map_ptr(row_map, T), ptr<int>(ln_epoch), ptr<long long>(sorted),
+                      (uint32_t)thr, (float)dscale, map_ptr(row_map, T), ptr<int>(ln_epoch),
+                      reinterpret_cast<unsigned long long*>(ptr<long long>(ln_stats)),
+                      has_stats ? (long long)ln_stats->numel() : 0ll, ptr<long long>(sorted),
                       ptr<long long>(perm), stream()),
            "emb_fwd");
 }
@@ -1255,7 +1262,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("emb_fwd", &emb_fwd, py::arg("ids"), py::arg("word"), py::arg("pos"), py::arg("gamma"), py::arg("beta"),
         py::arg("y"), py::arg("mean"), py::arg("rstd"), py::arg("S"), py::arg("eps"), py::arg("seed"), py::arg("site"),
         py::arg("thr"), py::arg("dscale"), py::arg("row_map") = py::none(), py::arg("ln_epoch") = py::none(),
-        py::arg("sorted") = py::none(), py::arg("perm") = py::none());
+        py::arg("sorted") = py::none(), py::arg("perm") = py::none(), py::arg("ln_stats") = py::none());
   m.def("gemm_ln_set_diag", [](int64_t d) { fd_gemm_ln_set_diag((int)d); });
   m.def("emb_bwd", &emb_bwd);
   m.def("colsum_bf16", &colsum_bf16);

@@ -306,10 +306,11 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
   return 0;
 }
 int fd_emb_fwd(const void*, int, const void*, const void*, const float*, const float*, void*, float*, float*, int, int,
-               int, float, const uint32_t*, uint32_t, uint32_t, float, const int*, int* ln_epoch, long long* sorted,
-               long long* perm, hipStream_t) {
+               int, float, const uint32_t*, uint32_t, uint32_t, float, const int*, int* ln_epoch,
+               unsigned long long* ln_stats, long long ln_stats_n, long long* sorted, long long* perm, hipStream_t) {
   ++hc::calls;
   hc::opt_span(ln_epoch, 4, "emb ln_epoch");
+  hc::opt_span(ln_stats, ln_stats_n * 8, "emb ln_stats");
   if ((sorted == nullptr) != (perm == nullptr)) hc::violations.push_back("emb_fwd: sorted without perm");
   return 0;
 }

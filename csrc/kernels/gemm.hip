@@ -945,8 +945,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
   const GemmParams& p = second ? grp.q : p0;
   if (second) bid -= grp.ntiles0;
   gemm_tile<BM, BN, AK, BKM, EPI, WM, WN, S>(p, bid, smem);
+#if FD_GEMM_STAMPS
   __syncthreads();
   FD_STAMP(5);
+#endif
 }
 
 // LayerNorm-fused NT GEMM (EPI_LN / EPI_LN_BWD): the tiles of a row block are consecutive
@@ -960,8 +962,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_ln_kernel(GemmParams p) 
   const int tiles_n = p.N / BN;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   gemm_tile_at<BM, BN, true, true, EPI, WM, WN, S>(p, lid / tiles_n, lid % tiles_n, smem);
+#if FD_GEMM_STAMPS
   __syncthreads();
   FD_STAMP(5);
+#endif
 }
 
 // ---------------------------------------------------------------- all-layer weight gradients
@@ -1130,6 +1134,15 @@ bool launch_id(const GemmParams& p, int id, int splits, hipStream_t st, const Ge
   return false;
 }
 
+// The configuration ids launch_id instantiates; an override naming any other id (measured and
+// removed, see the table above) falls back to the automatic pick instead of failing the launch.
+constexpr int INSTANTIATED[] = {0, 1, 3, 6, 8, 10, 11, 13, 18, 21, 24};
+bool cfg_instantiated(int id) {
+  for (int v : INSTANTIATED)
+    if (v == id) return true;
+  return false;
+}
+
 // Tuning overrides: per GEMM kind a forced config id / split count (-1 = auto),
 // set from FD_GEMM_CFG_{NT,NN,TN} / FD_GEMM_SPLITS or at run time (fd_gemm_set_cfg).
 int g_cfg_override[3] = {-2, -2, -2};
@@ -1140,7 +1153,7 @@ int cfg_override(int kind) {
   if (g_cfg_override[kind] == -2) {
     const char* names[3] = {"FD_GEMM_CFG_NT", "FD_GEMM_CFG_NN", "FD_GEMM_CFG_TN"};
     const char* e = getenv(names[kind]);
-    g_cfg_override[kind] = e ? atoi(e) : -1;
+    g_cfg_override[kind] = e && cfg_instantiated(atoi(e)) ? atoi(e) : -1;
   }
   return g_cfg_override[kind];
 }
@@ -1177,7 +1190,7 @@ int pick_cfg(int kind, int M, int N, int K) {
     // 128x128 wins at the packed M ~ 2.7 k (21.5 vs 25.7 us; profiles/r1_gemm_cfg_sweep_T2688_packed.txt)
     // FD_GEMM_WIDE_CFG=<id>: configuration of the N >= 1536 NT GEMMs (QKV / FFN1 forward, FFN2 dX)
     static const int wide = [] { const char* e = getenv("FD_GEMM_WIDE_CFG"); return e ? atoi(e) : -1; }();
-    if (wide >= 0 && wide < NCFG && N >= 1536 && M >= 1024 && M <= 4096 && tiles_of(wide, M, N) > 0) return wide;
+    if (cfg_instantiated(wide) && N >= 1536 && M >= 1024 && M <= 4096 && tiles_of(wide, M, N) > 0) return wide;
     if (N % 192 == 0 && N >= 3072 && M >= 3584) return 3;
     if (N % 128 == 0 && N >= 3072 && M >= 2048) return 1;
     if (N % 192 == 0 && N >= 1536 && M >= 2048) return 6;
@@ -1188,7 +1201,7 @@ int pick_cfg(int kind, int M, int N, int K) {
     // loop pays half the barriers.  2.21-2.25 vs 2.28 ms/step in the model (3 A/B pairs,
     // profiles/r1_ab_narrow_cfg24.txt).  FD_GEMM_NARROW_CFG=<id> overrides (-1: the rule below).
     static const int narrow = [] { const char* e = getenv("FD_GEMM_NARROW_CFG"); return e ? atoi(e) : 24; }();
-    if (narrow >= 0 && narrow < NCFG && N < 1536 && M >= 1024 && M <= 4096) return narrow;
+    if (cfg_instantiated(narrow) && N < 1536 && M >= 1024 && M <= 4096) return narrow;
     return K >= 2048 ? 0 : 8;
   }
   if (kind == 1) {  // NN dX
@@ -1276,7 +1289,7 @@ int fd_gemm_stamps(unsigned long long* host, int nblocks) {
 
 // Force a configuration id / split count for a GEMM kind (tuning; -1 = auto).
 int fd_gemm_set_cfg(int kind, int cfg, int splits) {
-  if (kind < 0 || kind > 2 || cfg < -1 || cfg >= NCFG) return 1;
+  if (kind < 0 || kind > 2 || cfg < -1 || cfg >= NCFG || (cfg >= 0 && !cfg_instantiated(cfg))) return 1;
   g_cfg_override[kind] = cfg;
   if (kind == 2) g_splits_override = splits;
   return 0;
@@ -1407,7 +1420,7 @@ int dw2_cfg(int M0, int N0, int M1, int N1) {
     static const int big_cfg = [] { const char* e = getenv("FD_GEMM_DW_BIG_CFG"); return e ? atoi(e) : -1; }();
     const bool small = tiles_of(8, M0, N0) + tiles_of(8, M1, N1) < 400;
     id = small ? small_cfg : big_cfg;
-    if (id < 0 || id >= NCFG) id = 8;
+    if (!cfg_instantiated(id)) id = 8;
   }
   if (M0 % CFGS[id].bm || M1 % CFGS[id].bm || N0 % CFGS[id].bn || N1 % CFGS[id].bn) id = 8;
   return id;

@@ -276,6 +276,13 @@ struct EmbArgs {
   // advanced once per model forward here -- the first kernel of every forward -- so the fused
   // LayerNorm launches of this forward / backward tag their row statistics with a fresh epoch
   int* ln_epoch;
+  // with ln_epoch (nullable): the exchange's granule buffer ([ln_stats_n] 8-byte {tag, value}).
+  // A granule tag is (epoch * FD_LN_XSITES + xsite + 1) mod 2^32, so it repeats every 2^25
+  // epochs: when the epoch crosses such a multiple, block 0 zeroes every granule first (tag 0
+  // matches no launch), so a row block's statistics left untouched since then can never pass
+  // for fresh ones
+  unsigned long long* ln_stats;
+  long long ln_stats_n;
   // forward only (nullable): the word-gradient grouping of the backward (rank sort of ids) is
   // computed by extra blocks of the forward launch (sort_blocks of them, after the rows' blocks)
   long long* sorted;
@@ -347,7 +354,13 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbArgs a) {
   }
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (a.ln_epoch && blockIdx.x == 0 && threadIdx.x == 0) a.ln_epoch[0] += 1;  // (read by later launches only)
+  if (a.ln_epoch && blockIdx.x == 0) {  // (read by later launches only)
+    const unsigned e = (unsigned)a.ln_epoch[0] + 1u;
+    __syncthreads();  // every thread has read the old epoch before thread 0 replaces it
+    if (a.ln_stats && (e & ((1u << 25) - 1u)) == 0u)
+      for (long long i = threadIdx.x; i < a.ln_stats_n; i += 256) a.ln_stats[i] = 0ull;
+    if (threadIdx.x == 0) a.ln_epoch[0] = (int)e;
+  }
   if (row >= a.T) return;
   const int D = a.D;
   const long id = load_id(a, row);
@@ -800,11 +813,15 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const int* row_map,
-               int* ln_epoch, long long* sorted, long long* perm, hipStream_t st) {
+               int* ln_epoch, unsigned long long* ln_stats, long long ln_stats_n, long long* sorted,
+               long long* perm, hipStream_t st) {
   if (D != 768) return 1;
   if ((sorted == nullptr) != (perm == nullptr) || (sorted && T > 16384)) return 2;
+  if (ln_stats && (!ln_epoch || ln_stats_n <= 0)) return 3;
   EmbArgs a{};
   a.ln_epoch = ln_epoch;
+  a.ln_stats = ln_stats;
+  a.ln_stats_n = ln_stats_n;
   a.sorted = sorted; a.perm = perm;
   a.sort_blocks = sorted ? (T + 15) / 16 : 0;
   a.ids = ids; a.ids64 = ids64; a.word = (const bf16_t*)word; a.pos = (const bf16_t*)pos; a.gamma = gamma;

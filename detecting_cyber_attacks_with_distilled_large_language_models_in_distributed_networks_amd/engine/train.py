@@ -146,6 +146,11 @@ def train_model(model, train_loader, criterion=None, optimizer=None, num_epochs:
             steps += 1
             if max_steps is not None and steps >= max_steps:
                 break
+        if grad_sync is not None and getattr(grad_sync, "ncomm", None) is not None:
+            # the epoch's replays issued their exchanges without a host wait: a bounded native wait
+            # here (RCCL async error or timeout -> ncclCommAbort + PeerFailure) instead of blocking
+            # forever in the loss all-reduce / .item() below when a replica died
+            grad_sync.ncomm.wait("data-parallel epoch")
         if grad_sync is not None:  # replica shares of each client-batch mean -> the mean
             import torch.distributed as dist
             dist.all_reduce(loss_sum, group=grad_sync.group)

@@ -97,7 +97,9 @@ class FederatedClient:
         self.dp_comm = None
         if self.topo.dp:
             dp_seed_offset(self.model, self.topo.dp_rank)
-            if dev.type == "cuda" and self.di.backend == "nccl" and os.environ.get("FEDDDOS_DP_NATIVE", "1") != "0":
+            # opt-in (FEDDDOS_DP_NATIVE=1) until the graph-captured exchange has run on >= 2 GPUs
+            # (ADVICE r3); the default is torch.distributed's eager async all-reduces
+            if dev.type == "cuda" and self.di.backend == "nccl" and os.environ.get("FEDDDOS_DP_NATIVE", "0") == "1":
                 # the client's replicas exchange over a framework RCCL communicator of their own
                 # group: stream-ordered collectives, so the data-parallel step is graph-captured
                 from ..parallel.rccl import NativeComm
@@ -338,6 +340,78 @@ class FederatedClient:
                 json.dump(rep, f, indent=1)
             self.log.info(f"federated report written to {path}")
         return rep
+
+
+@torch.no_grad()
+def _average_masters(model, states: List[torch.Tensor]) -> None:
+    """``fedavg_``'s arithmetic in one process: the SUM of the clients' fp32 masters (what the
+    all-reduce computes; for two clients a + b is exact in any order), then the fused 1/N scale +
+    bf16 shadow refresh (``scale_cast``) on GPU."""
+    A = model.arena
+    A.master.copy_(states[0])
+    for s in states[1:]:
+        A.master.add_(s)
+    if A.master.is_cuda:
+        from ..ops import kernels as K
+        K.scale_cast(A.master, A.shadow, 1.0 / len(states))
+        model.mark_shadow_synced()
+    else:
+        A.master.mul_(1.0 / len(states))
+        model.sync_shadow(force=True)
+
+
+def run_virtual_clients(client: "FederatedClient", n_clients: int = 2) -> Dict:
+    """One FedAvg round of ``n_clients`` federated clients on THIS process's device, trained one
+    after another (a 1-GPU job: ``bench.py`` quality half, ``cli launch --virtual-clients``).
+
+    Reference protocol (client1.py / client2.py + server.py:67-79): client k samples its own 10 %
+    of the file with seed 42 + k (client1.py:89, client2.py:84), every client starts from the same
+    weights (here: the model's broadcast init), trains ``cfg.epochs`` local epochs with
+    a fresh Adam, is evaluated on its test split, the server averages the fp32 state dicts
+    (unweighted mean; ``_average_masters`` = fedavg_'s sum + ``scale_cast``) and every client then
+    evaluates the aggregate on its own test split (client1_aggregated_metrics.csv).  Returns the
+    per-client local / aggregated metrics, the pooled aggregated confusion matrix and each local
+    model's relative L2 distance to the aggregate (0 would mean the "average" was an identity)."""
+    cfg, model = client.cfg, client.model
+    if client.di.distributed:
+        raise RuntimeError("virtual clients run in a single-process job (world size 1)")
+    if client.teacher is not None:
+        raise RuntimeError("virtual clients: the distillation extension runs one client per process")
+    dev = model.device
+    A = model.arena
+    init = A.master.detach().clone()
+    locals_, recs = [], []
+    for v in range(n_clients):
+        data = build_client_data(client.frame, v, cfg.data_fraction, cfg.base_seed, cfg.max_len, client.tokenizer,
+                                 cfg.partition, n_clients)
+        loader = DeviceLoader(data.train, cfg.batch_size, shuffle=True, device=dev, seed=cfg.client_seed(v))
+        test = DeviceLoader(data.test, cfg.eval_batch_size, device=dev)
+        with torch.no_grad():
+            A.master.copy_(init)
+        model.sync_shadow(force=True)
+        opt = ArenaAdam(model, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
+                        decoupled=cfg.decoupled_weight_decay)
+        opt.reset_state()  # (also clears the sparse word rows' "has Adam state" flags)
+        t0 = time.perf_counter()
+        tr = train_model(model, loader, None, opt, cfg.epochs, log=client.log, use_graph=cfg.use_graph)
+        local = _metrics_record(evaluate_model(model, test, name=f"Client {v + 1} local test"))
+        locals_.append(A.master.detach().clone())
+        recs.append({"client": v + 1, "train_rows": len(data.train), "test_rows": len(data.test),
+                     "train": tr, "train_wall_s": time.perf_counter() - t0, "local_test": local, "test": test})
+        del opt, loader
+    t0 = time.perf_counter()
+    _average_masters(model, locals_)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    fed_ms = 1e3 * (time.perf_counter() - t0)
+    agg = A.master.detach()
+    for r, loc in zip(recs, locals_):
+        r["aggregated_test"] = _metrics_record(evaluate_model(model, r.pop("test"), name=f"Client {r['client']} "
+                                                                                          "aggregated test"))
+        r["rel_l2_local_to_aggregate"] = float((loc - agg).norm() / loc.norm().clamp_min(1e-30))
+    pooled = [[sum(r["aggregated_test"]["confusion_matrix"][i][j] for r in recs
+                   if len(r["aggregated_test"]["confusion_matrix"]) == 2) for j in range(2)] for i in range(2)]
+    return {"clients": recs, "fedavg_ms": fed_ms, "aggregated_confusion": pooled}
 
 
 def run_federated(cfg: FedConfig, frame=None, model_config: Optional[DistilBertConfig] = None) -> Dict:

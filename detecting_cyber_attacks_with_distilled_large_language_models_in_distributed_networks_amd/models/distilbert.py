@@ -507,6 +507,10 @@ class DDoSClassifier(nn.Module):
         rc.fuse_colsum = self.fuse_colsum
         rc.remat_gelu = self.remat_gelu
         rc.fuse_ln = self.fuse_ln and cfg.dim % 64 == 0 and cfg.dim <= 2048
+        # a data-parallel client's gradient exchange overlaps the backward (parallel/dp.py GradSync
+        # sets collectives_in_backward): no LayerNorm-fused backward GEMM beside RCCL's kernels
+        rc.fuse_ln_bwd = rc.fuse_ln and K.ln_fusable(
+            1, cfg.dim, concurrent_collectives=bool(grad and getattr(self, "collectives_in_backward", False)))
         if (grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None
                 and self.transposed_dx):
             rc.fused_adam = self.fused_opt

@@ -60,6 +60,11 @@ class RunCtx:
     # out_lin + sa_layer_norm and lin2 + output_layer_norm; backward sa_layer_norm inside the
     # lin1 dX GEMM and block i-1's output_layer_norm inside block i's qkv dX GEMM
     fuse_ln: bool = False
+    # the backward's LayerNorm-fused dX GEMMs (lin1 dX + sa_layer_norm, qkv dX + the previous
+    # block's output_layer_norm); False while collectives run beside the backward (a data-parallel
+    # client's overlapped gradient all-reduces: RCCL kernels hold CUs a row block's peers may
+    # need -- ops/kernels.py ln_fusable) -> the plain dX GEMMs + separate LayerNorm backward
+    fuse_ln_bwd: bool = True
     ln2_saved: dict = field(default_factory=dict)    # block -> its output LN's saved state
     ln2_pending: dict = field(default_factory=dict)  # block -> (dz2, df) computed by block + 1
     # optimizer whose Adam step the weight-gradient GEMMs apply in their epilogues
@@ -113,7 +118,8 @@ class EmbeddingFn(torch.autograd.Function):
         # (a training forward's launch also groups the ids for the word gradient: no sort in the tail)
         group = bool(ctx.needs_input_grad[0])
         out = K.emb_fwd(ids, word, pos, gamma, beta, rc.S, rc.eps, rc.seed, 1, p, rc.row_map,
-                        ln_epoch=K.ln_epoch(ids.device, gamma.numel()) if rc.fuse_ln else None, group=group)
+                        ln_epoch=K.ln_epoch(ids.device, gamma.numel()) if rc.fuse_ln else None, group=group,
+                        ln_stats=K.ln_stats(ids.device, gamma.numel()) if rc.fuse_ln else None)
         y, mean, rstd = out[:3]
         ctx.grouped = out[3] if group else None
         ctx.rc, ctx.sinks, ctx.p = rc, sinks, p
@@ -270,7 +276,7 @@ class LayerFn(torch.autograd.Function):
             rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))
         else:
             K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
-        prev = rc.ln2_saved.get(ctx.idx - 1)
+        prev = rc.ln2_saved.get(ctx.idx - 1) if rc.fuse_ln_bwd else None
         if prev is not None:
             z2p, m2p, r2p, Lp, site_p, p_p = prev
             Gp = Lp["sinks"]
@@ -302,6 +308,7 @@ class LayerFn(torch.autograd.Function):
         # output_layer_norm(dropout(lin2) + h): dz2 -> residual grad of h, df -> lin2 output grad
         jobs = rc.colsum_jobs
         fused = ctx.fused_ln
+        fused_bwd = fused and rc.fuse_ln_bwd
         pend = rc.ln2_pending.pop(ctx.idx, None) if fused else None
         if pend is not None and pend[0].data_ptr() == dy.data_ptr():
             dz2, df = pend  # done by block idx + 1's qkv dX GEMM (its returned "dx" IS dz2)
@@ -335,7 +342,7 @@ class LayerFn(torch.autograd.Function):
         if not fuse_cs:
             K.colsum(du, G["l1_b"].buf, acc, jobs)
         # sa_layer_norm(out_lin + x): dh = du W1 + dz2, then its LayerNorm backward
-        if fused and wt.get("l1_w") is not None:
+        if fused_bwd and wt.get("l1_w") is not None:
             dz1, _ = K.linear_dx_ln_bwd(du, wt["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
                                         G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs,
                                         xsite=K.ln_xsite(ctx.idx, 0, True))
@@ -358,7 +365,7 @@ class LayerFn(torch.autograd.Function):
             rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))  # partials at the end, batched
         else:
             K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
-        prev = rc.ln2_saved.get(ctx.idx - 1) if fused and wt.get("qkv_w") is not None else None
+        prev = rc.ln2_saved.get(ctx.idx - 1) if fused_bwd and wt.get("qkv_w") is not None else None
         if prev is not None:
             # dx = dqkv Wqkv + dz1 is block idx-1's output-LN gradient: finish that LayerNorm
             # backward in this GEMM's epilogue and hand (dz2, df) to block idx-1

@@ -395,6 +395,12 @@ def ln_epoch(device, N: int = D_MODEL) -> torch.Tensor:
     return _ln_state(device, 1, N)[1]
 
 
+def ln_stats(device, N: int = D_MODEL) -> torch.Tensor:
+    """The exchange's granule buffer (int64), for ``emb_fwd(ln_stats=...)``: the epoch launch
+    zeroes it whenever the 32-bit granule tags are about to repeat (every 2^25 epochs)."""
+    return _ln_state(device, 1, N)[0]
+
+
 def ln_epoch_advance(device, N: int = D_MODEL):
     """Start a new exchange epoch (one small launch): callers of ``linear_ln_fwd`` /
     ``linear_dx_ln_bwd`` that do not run a model forward (tests, scripts) use this."""
@@ -446,12 +452,15 @@ def set_shared_device(shared: bool) -> None:
     _SHARED_DEVICE = bool(shared)
 
 
-def ln_fusable(M: int, N: int) -> bool:
+def ln_fusable(M: int, N: int, concurrent_collectives: bool = False) -> bool:
     """Whether a LayerNorm-fused GEMM of M rows x N (= hidden) columns runs as one resident
     round (its row blocks exchange statistics, so no tile may wait on an undispatched peer):
-    at most one 128 x 64 tile per CU, and no other process on the device; larger batches use
-    the separate LayerNorm kernels."""
-    if _SHARED_DEVICE:
+    at most one 128 x 64 tile per CU, no other process on the device, and no collective of this
+    process in flight beside it (``concurrent_collectives``: a data-parallel client's gradient
+    all-reduces overlapping the backward -- RCCL's kernels hold CUs and LDS while they wait on a
+    slower replica, so a fused tile's row-block peers might not get a CU until the 0.25 s
+    rendezvous timeout).  Otherwise the plain GEMMs + separate LayerNorm kernels."""
+    if _SHARED_DEVICE or concurrent_collectives:
         return False
     tiles = ((M + 127) // 128) * (N // 64)
     return N % 64 == 0 and N <= 2048 and tiles <= min(LN_MAX_TILES, _cu_count())
@@ -546,9 +555,11 @@ def group_ids(ids: torch.Tensor):
 RANK_SORT_MAX = 16384  # csrc/kernels/norm.hip rank sort: T ids in LDS
 
 
-def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p, row_map=None, ln_epoch=None, group=False):
+def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p, row_map=None, ln_epoch=None, group=False,
+            ln_stats=None):
     """row_map (int32 [T]): ``ids`` are packed real tokens; positions and dropout follow the padded row.
-    ln_epoch (``ln_epoch(device)``): also advance the LayerNorm-fused GEMMs' exchange epoch.
+    ln_epoch (``ln_epoch(device)``): also advance the LayerNorm-fused GEMMs' exchange epoch;
+    ln_stats (``ln_stats(device)``, with ln_epoch): the granules it zeroes when the tags wrap.
     group: also return the backward's id grouping (``group_ids``), computed by extra blocks of
     the same launch (T <= RANK_SORT_MAX; None beyond) -- the backward tail then has no sort launch."""
     T = ids.numel()
@@ -562,7 +573,7 @@ def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p, row_map=None, ln
         srt = torch.empty(T, dtype=torch.int64, device=ids.device)
         perm = torch.empty_like(srt)
     ext().emb_fwd(ids.contiguous(), word, pos, gamma, beta, y, mean, rstd, S, eps, seed, site, thr, sc, row_map,
-                  ln_epoch, srt, perm)
+                  ln_epoch, srt, perm, ln_stats)
     if group:
         return y, mean, rstd, ((srt, perm) if srt is not None else None)
     return y, mean, rstd

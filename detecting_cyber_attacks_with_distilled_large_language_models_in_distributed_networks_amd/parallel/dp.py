@@ -137,6 +137,9 @@ class GradSync:
         self._prev_hook = model.layer_grads_hook
         if overlap:
             model.layer_grads_hook = self._on_layer
+            # collectives now run beside the backward: the model keeps its LayerNorm-fused backward
+            # GEMMs off (their row-block rendezvous needs every tile resident; ops/kernels.py ln_fusable)
+            model.collectives_in_backward = True
 
     @property
     def capturable(self) -> bool:
@@ -239,6 +242,7 @@ class GradSync:
     def detach(self):
         if self.overlap and self.model.layer_grads_hook == self._on_layer:
             self.model.layer_grads_hook = self._prev_hook
+            self.model.collectives_in_backward = False
 
 
 def make_dp_step_fn(model, optimizer, sync: GradSync, teacher=None, temperature: float = 2.0,

@@ -20,6 +20,13 @@ def test_bench_json_line():
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["higher_is_better"] is True
     assert d["config"]["seq_len"] == 64
+    # one process: the quality half still runs the reference's 2-client round (virtual clients
+    # trained in turn, seeds 42 / 43), and the average is not an identity
+    assert d["quality_virtual_clients"] == 2 and d["quality_clients"] == 2
+    pc = d["per_client"]
+    assert [c["seed"] for c in pc] == [42, 43]
+    assert all(c["rel_l2_local_to_aggregate"] > 0 for c in pc)
+    assert d["eval_rows"] == sum(c["test_rows"] for c in pc)
 
 
 def test_bench_spawns_ranks_itself():

@@ -247,3 +247,24 @@ def test_two_dp_clients_over_the_reference_tcp_protocol(tmp_path):
     for m in ms[1:]:
         assert torch.equal(ms[0], m)  # every replica of both clients holds the server's mean
     assert res.get("agg") is not None and len(srv.received) == 2
+
+
+def test_fused_ln_backward_off_beside_collectives():
+    """while a data-parallel client's gradient all-reduces overlap the backward, the
+    LayerNorm-fused backward GEMMs (whose row blocks wait for every tile to be resident) are not
+    used: RCCL's kernels may hold the CUs a peer tile needs.  The rule (ops/kernels.py
+    ln_fusable) and its trigger (GradSync attaching its per-block hook) are checked on CPU; the
+    GPU side (no gemm_ln backward launch, same gradients) in tests/test_model_gpu.py."""
+    from importlib import import_module
+    K = import_module(f"{PKG}.ops.kernels")
+    dp = import_module(f"{PKG}.parallel.dp")
+    assert K.ln_fusable(2688, 768)
+    assert not K.ln_fusable(2688, 768, concurrent_collectives=True)
+    m = _model()
+    assert not getattr(m, "collectives_in_backward", False)
+    sync = dp.GradSync(m, None, 2)
+    assert m.collectives_in_backward
+    sync.detach()
+    assert not m.collectives_in_backward
+    dp.GradSync(m, None, 2, overlap=False)  # no per-block hook: nothing runs beside the backward
+    assert not m.collectives_in_backward

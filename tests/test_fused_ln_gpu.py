@@ -269,3 +269,46 @@ def test_rendezvous_timeout_is_detected_and_fatal():
     kn.linear_ln_fwd(x, w, torch.zeros(D, device=DEV), res, gamma, beta, 1e-12, seed_t(3), 7, 0.0)
     torch.cuda.synchronize()
     kn.check_ln_error(DEV)
+
+
+def test_granule_tags_wrap_clears_stats():
+    """a granule tag is (epoch * 128 + site + 1) mod 2^32, so tags repeat every 2^25
+    epochs.  The epoch launch (emb_fwd) zeroes every granule when the epoch crosses such a
+    multiple -- a row block's statistics untouched since then can never pass for fresh ones --
+    and the fused LayerNorm still matches the unfused kernels right after the wrap."""
+    dev = torch.device(DEV)
+    M, K = 2688, 768
+    stats, cnt, err = kn._ln_state(dev, M, D)
+    T, S = 256, 128
+    ids = torch.randint(0, 1000, (T,), device=DEV)
+    word, pos = bf(1000, D, seed=11), bf(512, D, seed=12)
+    gamma, beta = affine(13)
+    # one epoch short of a multiple of 2^25: the next epoch launch must not clear anything
+    cnt[0] = (1 << 25) - 2
+    stats.fill_(0x1234567800000000)
+    kn.emb_fwd(ids, word, pos, gamma, beta, S, 1e-12, seed_t(1), 1, 0.0, ln_epoch=cnt, ln_stats=stats)
+    torch.cuda.synchronize()
+    assert int(cnt[0].item()) == (1 << 25) - 1 and bool((stats == 0x1234567800000000).all())
+    kn.emb_fwd(ids, word, pos, gamma, beta, S, 1e-12, seed_t(1), 1, 0.0, ln_epoch=cnt, ln_stats=stats)
+    torch.cuda.synchronize()
+    assert int(cnt[0].item()) == 1 << 25 and int(stats.count_nonzero().item()) == 0
+    # the exchange works at the wrapped epoch (tags 1..128 again)
+    x, w, res = bf(M, K, seed=1), bf(D, K, scale=0.03, seed=2), bf(M, D, seed=3)
+    b = (torch.randn(D, generator=torch.Generator().manual_seed(4)) * 0.1).to(DEV)
+    y, _, _, _ = kn.linear_ln_fwd(x, w, b, res, gamma, beta, 1e-12, seed_t(9), 33, 0.0, xsite=5)
+    y2, _, _ = kn.ln_fwd(kn.linear_fwd(x, w, b), res, gamma, beta, 1e-12, seed_t(9), 33, 0.0)
+    assert rel_err(y, y2) < 2e-2
+    assert int(err.item()) == 0
+
+
+def test_gemm_override_rejects_uninstantiated_cfg():
+    """a tuning override naming a configuration that is not compiled in is refused
+    (fd_gemm_set_cfg) instead of making later launches fail."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops._ext import ext
+    with pytest.raises(RuntimeError):
+        ext().gemm_set_cfg(0, 2, -1)   # cfg 2 was measured and removed
+    ext().gemm_set_cfg(0, 8, -1)       # an instantiated one is accepted
+    x, w = bf(256, 768, seed=1), bf(768, 768, scale=0.03, seed=2)
+    y = kn.linear_fwd(x, w, None)
+    ext().gemm_set_cfg(0, -1, -1)
+    assert rel_err(y, x.float() @ w.float().t()) < 1e-2

@@ -304,3 +304,35 @@ def test_teacher_token_type_grad_hip_matches_torch():
     a, b = th.arena.gview(name), tt.arena.gview(name)
     assert b[0].norm() > 0 and a[1].abs().sum() == 0
     assert ((a[0] - b[0]).norm() / b[0].norm()).item() < 3e-2
+
+
+def test_no_fused_ln_backward_beside_collectives(monkeypatch):
+    """With collectives overlapping the backward (parallel/dp.py GradSync sets
+    ``collectives_in_backward``) the model runs no LayerNorm-fused dX GEMM (their
+    row-block rendezvous needs every tile resident, RCCL kernels could hold the CUs), and the
+    gradients equal the fused path's to bf16 accuracy."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as kn
+    ids, mask, labels = _batch(B=32, S=128)
+    grads = []
+    for beside in (False, True):
+        model = DDoSClassifier(config=DistilBertConfig(n_layers=2), device=DEV, impl="hip", seed=3)
+        model.train()
+        model.collectives_in_backward = beside
+        calls = []
+        real = kn.linear_dx_ln_bwd
+
+        def spy(*a, **k):
+            calls.append(a[0].shape[0])
+            return real(*a, **k)
+
+        monkeypatch.setattr(kn, "linear_dx_ln_bwd", spy)
+        model.zero_grad()
+        loss, _ = model.forward_loss(ids, mask, labels)
+        loss.backward()
+        torch.cuda.synchronize()
+        monkeypatch.setattr(kn, "linear_dx_ln_bwd", real)
+        full = [m for m in calls if m > 64]  # (the pruned block's M = 64 split-K call has no rendezvous)
+        assert (len(full) == 0) == beside, calls
+        grads.append(model.arena.grad.clone())
+    g0, g1 = grads
+    assert ((g0 - g1).norm() / g0.norm()).item() < 2e-2
