@@ -193,9 +193,15 @@ class ArenaAdam:
         b1, b2 = self.betas
         if A.master.is_cuda:
             self._begin()
-            sparse = (getattr(self.model, "sparse_word_grad", False) and self.weight_decay == 0.0
+            # Only the HIP path leaves a sparse word gradient (and sets the emb_now / emb_ever row
+            # flags, in its embedding backward): the torch path's autograd writes the dense table
+            # and sets no flag, so the row-flag Adam would skip every word row there.  (Round 3's
+            # "HIP learns faster than fp32" loss-curve bias was exactly that: the fp32 reference
+            # arm on the GPU never updated its word embeddings -- results/numerics_r4/.)
+            hip_sparse = getattr(self.model, "impl", None) == "hip" and getattr(self.model, "sparse_word_grad", False)
+            sparse = (hip_sparse and self.weight_decay == 0.0
                       and getattr(self.model, "emb_ever", None) is not None)
-            if not sparse and getattr(self.model, "emb_now", None) is not None and self.model.sparse_word_grad:
+            if hip_sparse and not sparse and getattr(self.model, "emb_now", None) is not None:
                 raise RuntimeError("sparse word-embedding grads need weight_decay == 0 "
                                    "(set model.sparse_word_grad = False for AdamW)")
             # everything not already updated by the per-block hook, in contiguous runs

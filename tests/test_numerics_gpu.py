@@ -89,14 +89,6 @@ def _curve(impl, batches, test, counter0=0):
     return curve, acc
 
 
-@pytest.mark.xfail(strict=False, reason=(
-    "open finding (round 3): the HIP curve runs 1.3 % below fp32 on average, below in 18 of 20 windows "
-    "of both dropout streams, so the strict per-window band fails at the flat end of the curve.  "
-    "scripts/curve_bisect.py (results/numerics_r3/): the bias is unchanged with every fast path off "
-    "(graph, packing, [CLS] pruning, fused LN, fused Adam) and with dropout off, and the fp32 torch path "
-    "under bf16 autocast plus bf16 rounding of every tensor the HIP path stores tracks fp32 within "
-    "+0.0005 -- so it is neither a fast path nor bf16 precision; one-step gradients agree to <= 0.8 % "
-    "per tensor and parameter drift after 50 steps is ~1.5x the bf16 control's.  Root cause not found."))
 def test_loss_curve_parity_200_steps():
     """HIP (bf16 compute) vs fp32 torch on identical batches and dropout masks, measured against
     the run-to-run spread of EACH path (same batches, a second dropout stream, counter0 = 1 << 16):
@@ -104,7 +96,9 @@ def test_loss_curve_parity_200_steps():
     from the fp32 curve than either path is from itself under another dropout stream (plus a 3 %
     relative band; no absolute slack).  A systematic bias (e.g. in the packed / pruned / fused-Adam
     paths) would show as HIP-vs-torch differences of one sign in both stream pairs: the mean signed
-    difference over the 20 windows of both pairs must stay inside the self-spread."""
+    difference over the 20 windows of both pairs must stay inside the self-spread.  (Round 3 had this
+    test xfail on a -0.013 bias: the fp32 arm never updated its word embeddings on the GPU --
+    engine/optim.py; scripts/curve_bisect.py, results/numerics_r4/.)"""
     frame = generate_cicids2017(8000, seed=5, hard=True)
     cd = build_client_data(frame, 0, data_fraction=1.0, max_len=128)
     loader = DeviceLoader(cd.train, 32, shuffle=True, device="cuda", seed=3, drop_last=True)
@@ -141,3 +135,26 @@ def test_loss_curve_parity_200_steps():
     assert acc_r < 99.5, acc_r                   # hard profile: not saturated
     self_acc = max(abs(acc_r2 - acc_r), abs(acc_h2 - acc_h))
     assert abs(acc_h - acc_r) <= max(2.0 * self_acc, 1.0) + 1.0, (acc_h, acc_r, acc_h2, acc_r2)
+
+
+def test_torch_path_on_gpu_trains_word_embeddings(client_batch):
+    """The fp32 torch path on a GPU arena writes a DENSE word gradient and sets none of the HIP
+    path's row flags, so ArenaAdam must update its word table densely (round 4 fix: the row-flag
+    Adam skipped every word row -- the round-3 loss-curve bias); the HIP path updates exactly the
+    rows it flagged."""
+    b = client_batch
+    for impl in ("torch", "hip"):
+        m = DDoSClassifier(device="cuda", impl=impl, seed=21)
+        opt = ArenaAdam(m, lr=2e-5)
+        m.train()
+        woff, V, D = m.word_embedding_span()
+        w0 = m.arena.master[woff:woff + V * D].view(V, D).clone()
+        step = make_step_fn(m, opt)
+        step(b["input_ids"], b["attention_mask"], b["labels"], b["n_tokens"] if impl == "hip" else None)
+        torch.cuda.synchronize()
+        w1 = m.arena.master[woff:woff + V * D].view(V, D)
+        moved = (w1 != w0).any(1)
+        used = torch.zeros(V, dtype=torch.bool, device="cuda")
+        used[b["input_ids"][b["attention_mask"] != 0]] = True
+        assert bool(moved[used].all()), (impl, int(moved[used].sum()), int(used.sum()))
+        assert not bool(moved[~used].any()), impl  # untouched rows: zero gradient, zero state
