@@ -309,9 +309,12 @@ int64_t gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C
 // Cs[i] (+)= As[i]^T Bs[i] (fp32), As[i] [K_i][M_i], Bs[i] [K_i][N_i] bf16 (K_i % 64 == 0).
 // adam: empty, or [p, m, v, shadow] per problem + the device step counter last (fused
 // optimizer step instead of storing the gradients; hp = [lr, b1, b2, eps, wd, decoupled]).
+// wts: empty, or per problem the bf16 transposed shadow W^T [N][M] the fused Adam epilogue also
+// refreshes (an empty tensor: none for that problem).
 void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tensor>& Bs,
                    const std::vector<at::Tensor>& Cs, const std::vector<int64_t>& accumulate,
-                   const std::vector<at::Tensor>& adam, const std::vector<double>& hp, int64_t cfg) {
+                   const std::vector<at::Tensor>& adam, const std::vector<double>& hp, int64_t cfg,
+                   const std::vector<at::Tensor>& wts = {}) {
   const size_t n = As.size();
   TORCH_CHECK(n > 0 && n <= 32, "gemm_dw_batch: 1..32 problems, got ", n);
   TORCH_CHECK(Bs.size() == n && Cs.size() == n && accumulate.size() == n, "gemm_dw_batch: ragged problem lists");
@@ -347,6 +350,15 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
     for (size_t i = 0; i < n; ++i) {
       TORCH_CHECK(!accumulate[i], "gemm_dw_batch: a fused Adam step cannot accumulate into a gradient");
       pr[i].p = ad[i].p; pr[i].m = ad[i].m; pr[i].v = ad[i].v; pr[i].sh = ad[i].sh;
+    }
+    TORCH_CHECK(wts.empty() || wts.size() == n, "gemm_dw_batch: one W^T entry per problem");
+    for (size_t i = 0; i < wts.size(); ++i) {
+      if (!wts[i].defined() || wts[i].numel() == 0) continue;
+      need(wts[i], at::kBFloat16, "W^T");
+      TORCH_CHECK(wts[i].dim() == 2 && wts[i].size(0) == Cs[i].size(1) && wts[i].size(1) == Cs[i].size(0),
+                  "gemm_dw_batch: W^T must be [N][M] of its problem's [M][N] gradient");
+      TORCH_CHECK(pr[i].sh != nullptr, "gemm_dw_batch: W^T needs the problem's bf16 shadow");
+      pr[i].shT = reinterpret_cast<uint16_t*>(wts[i].data_ptr());
     }
     step = ad[0].step;
     hyper[0] = ad[0].lr; hyper[1] = ad[0].b1; hyper[2] = ad[0].b2; hyper[3] = ad[0].eps; hyper[4] = ad[0].wd;
@@ -1227,7 +1239,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("row_map"),
         py::arg("cfg") = -1, py::arg("xsite") = 0);
   m.def("gemm_dw_batch", &gemm_dw_batch, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("accumulate"),
-        py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1);
+        py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1, py::arg("wts") = std::vector<at::Tensor>{});
   m.def("gemm_colsum", &gemm_colsum, py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("aux"),
         py::arg("res"), py::arg("colsum"), py::arg("aux_out") = py::none());
   m.def("splitk_reduce_batched", &splitk_reduce_batched);

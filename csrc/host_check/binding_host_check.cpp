@@ -110,6 +110,10 @@ int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const
     if (Kq % 64) hc::violations.push_back("dw_batch: K % 64");
     hc::span(q.A, Kq * q.M * 2, "dw_batch A");
     hc::span(q.B, Kq * q.N * 2, "dw_batch B");
+    if (q.shT) {
+      if (!q.p || !q.sh || q.M % 8) hc::violations.push_back("dw_batch: W^T without its shadow's Adam");
+      hc::span(q.shT, mn * 2, "dw_batch W^T");
+    }
     if (q.p) {
       hc::span(q.p, mn * 4, "dw_batch adam p");
       hc::span(q.m, mn * 4, "dw_batch adam m");
@@ -554,6 +558,14 @@ int main() {
     expect_ok("dw_batch", [&] { gemm_dw_batch(As, Bs, Cs, acc, {}, {}, -1); });
     expect_ok("dw_batch adam", [&] { gemm_dw_batch(As, Bs, Cs, acc, st, hp, -1); });
     expect_reject("dw_batch adam+accumulate", [&] { gemm_dw_batch(As, Bs, Cs, acc1, st, hp, -1); });
+    std::vector<at::Tensor> wts;
+    for (auto& sh : shapes) wts.push_back(T_({sh[1], sh[0]}, bf));
+    wts[1] = at::Tensor();  // a problem without W^T
+    expect_ok("dw_batch adam + W^T", [&] { gemm_dw_batch(As, Bs, Cs, acc, st, hp, -1, wts); });
+    auto wbad = wts;
+    wbad[0] = T_({2304, 768}, bf);  // not transposed
+    expect_reject("dw_batch W^T shape", [&] { gemm_dw_batch(As, Bs, Cs, acc, st, hp, -1, wbad); });
+    expect_reject("dw_batch W^T ragged", [&] { gemm_dw_batch(As, Bs, Cs, acc, st, hp, -1, {wts[0]}); });
     auto Bbad = Bs;
     Bbad[2] = T_({2000, 768}, bf);
     expect_reject("dw_batch K mismatch", [&] { gemm_dw_batch(As, Bbad, Cs, acc, {}, {}, -1); });

@@ -246,7 +246,7 @@ DEV void st_nt4(float* p, float4 v) {
 
 // Adam on 4 consecutive elements of a finished gradient tile: the same arithmetic, in the
 // same order, as adam_kernel (head_optim.hip), so a fused step matches the unfused one.
-DEV void adam_epi4(const FdAdamEpi& a, size_t i, float4 g4, float step_size, float inv_sqrt_bc2) {
+DEV float4 adam_epi4(const FdAdamEpi& a, size_t i, float4 g4, float step_size, float inv_sqrt_bc2) {
   const float4 p4 = ld_nt4(a.p + i), m4 = ld_nt4(a.m + i), v4 = ld_nt4(a.v + i);
   float pp[4] = {p4.x, p4.y, p4.z, p4.w}, gg[4] = {g4.x, g4.y, g4.z, g4.w};
   float mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
@@ -266,6 +266,7 @@ DEV void adam_epi4(const FdAdamEpi& a, size_t i, float4 g4, float step_size, flo
   st_nt4(a.m + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
   st_nt4(a.v + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
   if (a.sh) *reinterpret_cast<uint2*>(a.sh + i) = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
+  return make_float4(pp[0], pp[1], pp[2], pp[3]);
 }
 
 // Weight-gradient (fp32) epilogue; see GemmParams::out for the two modes.
@@ -293,19 +294,53 @@ DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0
     step_size = p.adam.lr / bc1;
     inv_sqrt_bc2 = 1.f / sqrtf(bc2);
   }
+  const bool wt = adam && p.adam.shT != nullptr;
 #pragma unroll 2
   for (int id = tid; id < BM * CPR; id += NT) {
     const int r = id / CPR, cc = id - r * CPR;
     const int m = m0 + r;
     if (m >= p.M) break;
     const size_t i = (size_t)m * p.ldc + n0 + cc * 4;
-    float4 g = *reinterpret_cast<const float4*>(smem + r * ldc_lds + cc * 16);
+    char* slot = const_cast<char*>(smem) + r * ldc_lds + cc * 16;
+    float4 g = *reinterpret_cast<const float4*>(slot);
     if (p.accumulate) {
       const float4 o = *reinterpret_cast<const float4*>(p.out + i);
       g.x += o.x; g.y += o.y; g.z += o.z; g.w += o.w;
     }
-    if (adam) adam_epi4(p.adam, i, g, step_size, inv_sqrt_bc2);
-    else *reinterpret_cast<float4*>(p.out + i) = g;
+    if (adam) {
+      const float4 np = adam_epi4(p.adam, i, g, step_size, inv_sqrt_bc2);
+      // the updated bf16 weights back into this thread's own staging slot (it read g from there):
+      // the transposed copy is written from LDS below
+      if (wt) *reinterpret_cast<uint2*>(slot) = make_uint2(pack_bf2(np.x, np.y), pack_bf2(np.z, np.w));
+    } else {
+      *reinterpret_cast<float4*>(p.out + i) = g;
+    }
+  }
+  if (wt) {
+    // W^T [N][M] (row pitch p.M): 8 consecutive rows m of one column n are 16 contiguous bytes of
+    // W^T row n.  A thread takes TWO adjacent columns (one 4-byte LDS word holds both bf16) and 8
+    // rows: 8 ds_read_b32, two 16-byte stores.  Lanes of a wave walk adjacent column pairs of the
+    // same 8 rows (conflict-free: one 16-byte slot per two lanes).
+    __syncthreads();
+    const int rows = min(BM, p.M - m0);
+    constexpr int PAIRS = BN / 2;
+    for (int id = tid; id < (BM / 8) * PAIRS; id += NT) {
+      const int r8 = id / PAIRS, pr = id - r8 * PAIRS;
+      if (r8 * 8 >= rows) break;  // rows ascend with id
+      const int c = 2 * pr;       // first of the two columns (tile-local)
+      uint32_t w[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        w[j] = *reinterpret_cast<const uint32_t*>(smem + (r8 * 8 + j) * ldc_lds + (c >> 2) * 16 + (c & 3) * 2);
+      uint4 lo, hi;  // column c: low halves, column c + 1: high halves
+      lo.x = (w[0] & 0xffffu) | (w[1] << 16); lo.y = (w[2] & 0xffffu) | (w[3] << 16);
+      lo.z = (w[4] & 0xffffu) | (w[5] << 16); lo.w = (w[6] & 0xffffu) | (w[7] << 16);
+      hi.x = (w[0] >> 16) | (w[1] & 0xffff0000u); hi.y = (w[2] >> 16) | (w[3] & 0xffff0000u);
+      hi.z = (w[4] >> 16) | (w[5] & 0xffff0000u); hi.w = (w[6] >> 16) | (w[7] & 0xffff0000u);
+      uint16_t* dst = p.adam.shT + (size_t)(n0 + c) * p.M + m0 + r8 * 8;
+      *reinterpret_cast<uint4*>(dst) = lo;
+      *reinterpret_cast<uint4*>(dst + p.M) = hi;
+    }
   }
 }
 
@@ -1007,7 +1042,7 @@ DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
   p.out = q.C;
   p.accumulate = q.accumulate;
   if (q.p) {
-    p.adam.p = q.p; p.adam.m = q.m; p.adam.v = q.v; p.adam.sh = q.sh; p.adam.step = bt.step;
+    p.adam.p = q.p; p.adam.m = q.m; p.adam.v = q.v; p.adam.sh = q.sh; p.adam.shT = q.shT; p.adam.step = bt.step;
     p.adam.lr = bt.lr; p.adam.b1 = bt.b1; p.adam.b2 = bt.b2; p.adam.eps = bt.eps; p.adam.wd = bt.wd;
     p.adam.decoupled = bt.decoupled;
   }
@@ -1504,6 +1539,7 @@ int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const f
     if (!probs[i].A || !probs[i].B || (!probs[i].C && !probs[i].p) || probs[i].M <= 0 || probs[i].N <= 0) return 2;
     if (probs[i].K < 0 || probs[i].K % BKT) return 5;
     if (probs[i].p && (!probs[i].m || !probs[i].v || !step || !hyper)) return 3;
+    if (probs[i].shT && (!probs[i].p || probs[i].M % 8)) return 6;
   }
   if (hyper) {
     bt.step = step;

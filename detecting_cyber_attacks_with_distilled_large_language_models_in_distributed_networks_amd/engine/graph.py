@@ -12,6 +12,11 @@ call captures, then replays the capture for its own batch.  Batches whose shape
 differs from the captured one (the last partial batch, drop_last=False) run
 eagerly.
 
+``step_fn.prepare`` (optional): called eagerly before every replay and before the capture, for
+state a replay does not refresh by itself -- the model's W^T copies after an out-of-band weight
+change (FedAvg, checkpoint load): the fused Adam epilogue keeps them current, so the graphs hold
+no transpose launch (models/distilbert.py refresh_wT).
+
 Unpadded model path: a batch also carries its real-token count; ``bucket(tokens,
 B, S)`` (the model's ``packed_rows``) maps it to the packed row count the step
 is shaped by, and one graph is captured per (batch shape, bucket) -- a handful
@@ -88,7 +93,10 @@ class GraphedTrainStep:
             return self.step_fn(ids, mask, labels, tokens)
         key = self._key(ids, tokens)
         hit = self.graphs.get(key)
+        prepare = getattr(self.step_fn, "prepare", None)
         if hit is not None:
+            if prepare is not None:
+                prepare()  # eager state the graph does not refresh itself (the model's W^T copies)
             g, static, loss = hit
             blk = contiguous_block(ids, mask, labels) if static["flat"] is not None else None
             if blk is not None:
@@ -111,6 +119,8 @@ class GraphedTrainStep:
         (s_ids, s_mask, s_lab), flat = static_block(ids, mask, labels)
         static = {"ids": s_ids, "mask": s_mask, "labels": s_lab, "flat": flat}
         g = torch.cuda.CUDAGraph()
+        if prepare is not None:
+            prepare()
         try:
             torch.cuda.synchronize()
             with torch.cuda.graph(g):

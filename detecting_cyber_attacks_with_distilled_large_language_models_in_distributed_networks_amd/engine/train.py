@@ -74,6 +74,7 @@ def make_step_fn(model, optimizer, criterion=None):
         optimizer.step()
         return loss.detach()
 
+    step.prepare = getattr(model, "refresh_wT", None)
     return step
 
 
@@ -92,6 +93,7 @@ def make_kd_step_fn(student, teacher, optimizer, temperature: float = 2.0, alpha
         optimizer.step()
         return loss.detach()
 
+    step.prepare = getattr(student, "refresh_wT", None)
     return step
 
 

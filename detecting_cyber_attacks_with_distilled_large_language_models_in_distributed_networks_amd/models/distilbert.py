@@ -306,6 +306,10 @@ class DDoSClassifier(nn.Module):
         self._grad_token = None
         self._synced_version = -1
         self._hip_cache = None
+        # W^T copies of the backward's dX GEMMs: stale until taken; kept current by the fused Adam
+        # epilogue (refresh_wT)
+        self._wT_dirty = True
+        self._wT_kept_by_step = False
         self.to(device)
 
     # -------------------------------------------------------------- device management
@@ -326,6 +330,7 @@ class DDoSClassifier(nn.Module):
         self._grad_token = torch.zeros((), device=dev, requires_grad=True)
         self._hip_cache = None
         self._synced_version = -1
+        self._wT_dirty = True
         return self
 
     @property
@@ -380,9 +385,40 @@ class DDoSClassifier(nn.Module):
         if force or v != self._synced_version:
             self.arena.sync_shadow()
             self._synced_version = self._param_version()
+            self._wT_dirty = True
 
-    def mark_shadow_synced(self):
+    def mark_shadow_synced(self, wT_kept: bool = False):
+        """The shadow was rewritten outside ``sync_shadow`` (an Adam step, FedAvg's scale_cast).
+        wT_kept: the writer also rewrote the W^T copies (the fused Adam epilogue of the all-layer
+        weight-gradient launch) -- otherwise they are stale until ``refresh_wT``."""
         self._synced_version = self._param_version()
+        self._wT_kept_by_step = bool(wT_kept)
+        if not wT_kept:
+            self._wT_dirty = True
+
+    @property
+    def n_transposed(self) -> int:
+        """Weight matrices with a W^T copy (4 per block on the HIP path, 0 otherwise)."""
+        return 4 * self.config.n_layers if self.transposed_dx else 0
+
+    def wT_stale(self) -> bool:
+        return self.transposed_dx and (self._wT_dirty or not self._wT_kept_by_step)
+
+    def refresh_wT(self, force: bool = False) -> bool:
+        """Re-derive the backward's W^T copies from the bf16 shadow (one transpose launch) if
+        anything but the fused Adam epilogue -- which rewrites them itself -- changed the weights
+        since they were taken: a FedAvg / broadcast / checkpoint load / an unfused optimizer step.
+        Called by a training forward, and before a graph replay (``GraphedTrainStep``: the graphs
+        hold no transpose launch of their own while the fused epilogue keeps W^T current).
+        Returns whether it launched."""
+        if not (self.transposed_dx and self.impl == "hip") or not (force or self.wT_stale()):
+            return False
+        from ..ops import kernels as K
+        self.sync_shadow()
+        _, layers, _ = self._hip_handles()
+        K.transpose_many([L[k] for L in layers for k in L["wT"]], [L["wT"][k] for L in layers for k in L["wT"]])
+        self._wT_dirty = False
+        return True
 
     # -------------------------------------------------------------- HIP handles
     def _hip_handles(self):
@@ -525,10 +561,10 @@ class DDoSClassifier(nn.Module):
             else:
                 K.step_inc(None, self.rng)
         token = self._grad_token if torch.is_grad_enabled() else None
-        if token is not None and self.transposed_dx:
-            srcs = [L[k] for L in layers for k in L["wT"]]
-            dsts = [L["wT"][k] for L in layers for k in L["wT"]]
-            K.transpose_many(srcs, dsts)
+        if token is not None:
+            # the W^T copies the backward's dX GEMMs read: current unless something other than the
+            # fused Adam epilogue (which rewrites them) changed the weights
+            self.refresh_wT()
         if packed:
             # Unpadded step: only the real tokens (sequence-contiguous, filler rows at the end)
             # are embedded and run through the blocks; varlen attention over cu; positions and
@@ -569,15 +605,20 @@ class DDoSClassifier(nn.Module):
             return None
         dev = self.arena.device
         key = (B, S, Bp, str(dev))
-        cache = getattr(self, "_prune_cache", None)
-        if cache is None or cache[0] != key:
+        # One buffer set per batch shape, kept for the model's lifetime: HIP graphs captured for one
+        # shape (the bs16 eval forward) hold these addresses while another shape (the bs32 train
+        # step) runs -- replacing the set would free memory a later replay reads and writes
+        # (round 4: a second client's eval replay faulted on the first client's freed buffers).
+        caches = self.__dict__.setdefault("_prune_caches", {})
+        cache = caches.get(key)
+        if cache is None:
             rmap = torch.zeros(Bp, dtype=torch.int32, device=dev)
             rmap[:B] = torch.arange(B, dtype=torch.int32, device=dev) * S
             padded_rows = rmap.to(torch.int64)  # padded layout: sequence b's [CLS] is row b * S
             # (packed: the packing launch fills the kept rows and their dropout-hash rows)
             cache = (key, rmap, padded_rows, torch.arange(B, dtype=torch.int32, device=dev),
                      torch.zeros(Bp, dtype=torch.int64, device=dev), torch.zeros(Bp, dtype=torch.int32, device=dev))
-            self._prune_cache = cache
+            caches[key] = cache
         return cache
 
     @staticmethod

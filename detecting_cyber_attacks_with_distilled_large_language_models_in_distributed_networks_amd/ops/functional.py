@@ -263,7 +263,7 @@ class LayerFn(torch.autograd.Function):
             K.colsum(du, G["l1_b"].buf, acc, jobs)
         if g is None:
             g = g_out
-        batch += [(df, g, G["l2_w"].buf, acc), (du, h, G["l1_w"].buf, acc)]
+        batch += [(df, g, G["l2_w"].buf, acc, wt["l2_w"]), (du, h, G["l1_w"].buf, acc, wt["l1_w"])]
         dz1c, _ = K.linear_dx_ln_bwd(du, wt["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
                                      G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, xsite=K.ln_xsite(ctx.idx, 0, True))
         dcxc = K.linear_dx(dz1c, L["o_w"], wt=wt["o_w"])
@@ -271,7 +271,7 @@ class LayerFn(torch.autograd.Function):
         dcx, dz1 = K.scatter_rows2(dcxc, dz1c, ci, B, cx.shape[0])
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask,
                           q_live=1)
-        batch += [(dz1c, cxc, G["o_w"].buf, acc), (dqkv, x, G["qkv_w"].buf, acc)]
+        batch += [(dz1c, cxc, G["o_w"].buf, acc, wt["o_w"]), (dqkv, x, G["qkv_w"].buf, acc, wt["qkv_w"])]
         if rc.colsum_pending is not None:
             rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))
         else:
@@ -332,7 +332,7 @@ class LayerFn(torch.autograd.Function):
         if g is None:
             g = g_out
         if batch is not None:
-            batch += [(df, g, G["l2_w"].buf, acc), (du, h, G["l1_w"].buf, acc)]
+            batch += [(df, g, G["l2_w"].buf, acc, wt.get("l2_w")), (du, h, G["l1_w"].buf, acc, wt.get("l1_w"))]
         elif rc.group_dw:
             K.linear_dw2(df, g, G["l2_w"].buf, du, h, G["l1_w"].buf, acc,
                          adam=fa.fused_args([G["l2_w"].buf, G["l1_w"].buf]) if fa else None, jobs=rc.dw_jobs)
@@ -355,7 +355,7 @@ class LayerFn(torch.autograd.Function):
             K.linear_dw(dz1, cx, G["o_w"].buf, acc)
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask)
         if batch is not None:
-            batch += [(dz1, cx, G["o_w"].buf, acc), (dqkv, x, G["qkv_w"].buf, acc)]
+            batch += [(dz1, cx, G["o_w"].buf, acc, wt.get("o_w")), (dqkv, x, G["qkv_w"].buf, acc, wt.get("qkv_w"))]
         elif rc.group_dw:
             K.linear_dw2(dz1, cx, G["o_w"].buf, dqkv, x, G["qkv_w"].buf, acc,
                          adam=fa.fused_args([G["o_w"].buf, G["qkv_w"].buf]) if fa else None, jobs=rc.dw_jobs)

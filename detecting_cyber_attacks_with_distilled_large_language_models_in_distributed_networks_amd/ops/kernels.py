@@ -178,16 +178,23 @@ DW_BATCH_MAX = 32  # problems per all-layer weight-gradient launch (csrc/kernels
 
 def linear_dw_batch(jobs: list, adam=None, cfg: int = -1):
     """Every weight gradient of a backward in one launch per 32 problems: for each job
-    (dy [K, M], x [K, N], out [M, N] fp32, accumulate) out (+)= dy^T x.  No split-K: each
+    (dy [K, M], x [K, N], out [M, N] fp32, accumulate[, wT]) out (+)= dy^T x.  No split-K: each
     output tile runs the whole token dimension (deterministic, no slabs, no reduce).
-    adam: a callable grads -> (state, hyper) (``ArenaAdam.fused_args``): apply the optimizer
-    step to each finished gradient tile instead of storing it."""
+    adam: a callable (grads, n_with_wT) -> (state, hyper) (``ArenaAdam.fused_args``): apply the
+    optimizer step to each finished gradient tile instead of storing it; a job's optional wT
+    (bf16 [N, M]) is then refreshed by the same epilogue with the updated weights transposed (the
+    next step's dX GEMMs read it: no transpose launch)."""
     for i in range(0, len(jobs), DW_BATCH_MAX):
         chunk = jobs[i:i + DW_BATCH_MAX]
         outs = [j[2] for j in chunk]
-        st, hp = adam(outs) if adam is not None else ([], [])
+        wts = [j[4] if len(j) > 4 else None for j in chunk] if adam is not None else []
+        nwt = sum(w is not None for w in wts)
+        st, hp = adam(outs, nwt) if adam is not None else ([], [])
+        empty = None
+        if nwt:
+            empty = torch.empty(0, dtype=torch.bfloat16, device=outs[0].device)
         ext().gemm_dw_batch([j[0] for j in chunk], [j[1] for j in chunk], outs, [int(j[3]) for j in chunk],
-                            st, hp, cfg)
+                            st, hp, cfg, [w if w is not None else empty for w in wts] if nwt else [])
 
 
 def dw_flush(jobs: list):

@@ -26,7 +26,7 @@ for M, N in shapes:
 step = torch.ones(1, dtype=torch.int32, device="cuda")
 
 
-def adam(outs):
+def adam(outs, n_wT=0):
     st = []
     for s in states[:len(outs)]:
         st += s

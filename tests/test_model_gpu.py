@@ -315,7 +315,7 @@ def test_no_fused_ln_backward_beside_collectives(monkeypatch):
     ids, mask, labels = _batch(B=32, S=128)
     grads = []
     for beside in (False, True):
-        model = DDoSClassifier(config=DistilBertConfig(n_layers=2), device=DEV, impl="hip", seed=3)
+        model = DDoSClassifier(config=DistilBertConfig(n_layers=2), device="cuda", impl="hip", seed=3)
         model.train()
         model.collectives_in_backward = beside
         calls = []
@@ -336,3 +336,30 @@ def test_no_fused_ln_backward_beside_collectives(monkeypatch):
         grads.append(model.arena.grad.clone())
     g0, g1 = grads
     assert ((g0 - g1).norm() / g0.norm()).item() < 2e-2
+
+
+def test_eval_graphs_survive_interleaved_training():
+    """Round 4 regression: the bs16 eval forward's HIP graphs keep valid buffers while bs32 training
+    steps run between their replays (a per-shape buffer set of the pruned last block used to be
+    replaced -- freed -- by the other shape; a second virtual client's eval then faulted).  The
+    replayed logits equal an eager forward's bit for bit."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.engine import (
+        make_step_fn)
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.engine.infer import (
+        GraphedForward)
+    model = DDoSClassifier(config=DistilBertConfig(n_layers=2), device="cuda", impl="hip", seed=3)
+    opt = ArenaAdam(model, lr=1e-4)
+    fn = make_step_fn(model, opt)
+    ids32, mask32, lab32 = _batch(32, 128)
+    ids16, mask16, _ = _batch(16, 128, seed=5)
+    tok32, tok16 = int(mask32.sum()), int(mask16.sum())
+    fwd = GraphedForward(model)
+    for _ in range(3):
+        model.train()
+        fn(ids32, mask32, lab32, tok32)
+        out = fwd(ids16, mask16, tok16).clone()  # capture on the first pass, replays after
+        with torch.no_grad():
+            model.eval()
+            ref = model(ids16, mask16, tokens=tok16)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
