@@ -33,6 +33,7 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
                long long workspace_elems, int accumulate, const FdAdamEpi* adam,
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
+int fd_gemm_set_da(int id);
 int fd_gemm_stamps(unsigned long long* host, int nblocks);
 int fd_attn_stamps(unsigned long long* host, int nblocks);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
@@ -46,7 +47,7 @@ int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, 
                    long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
                    const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, hipStream_t st);
 int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
-               const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t st);
+               const void* res, int ldres, const FdLnEpi* ln, int cfg, int b_mn, hipStream_t st);
 int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
                              const int* splits, const int* accumulate, hipStream_t st);
 int fd_transpose_batched(const void* const* srcs, void* const* dsts, const int* rows, const int* cols, int n,
@@ -195,16 +196,19 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
 // NT dX GEMM (GELU' or residual epilogue) that also leaves per-M-tile column sums of its bf16
 // output in `colsum` ([ceil(M / 128)][N] fp32; returns the tile count) for a deferred
 // producer-bias gradient.
+// kind 0: B = W^T [N][K] (NT); kind 1: B = W [K][N] (NN; direct-A kernels only, else 0 tiles).
 int64_t gemm_colsum(int64_t epi, const at::Tensor& A, const at::Tensor& B, const at::Tensor& C,
                     const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& res,
-                    const at::Tensor& colsum, const c10::optional<at::Tensor>& aux_out) {
+                    const at::Tensor& colsum, const c10::optional<at::Tensor>& aux_out, int64_t kind = 0) {
   need(A, at::kBFloat16, "A");
   need(B, at::kBFloat16, "B");
   need(C, at::kBFloat16, "C");
   need(colsum, at::kFloat, "colsum");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm_colsum operands must be 2-D");
-  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
-  TORCH_CHECK(B.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_colsum: shape mismatch");
+  TORCH_CHECK(kind == 0 || kind == 1, "gemm_colsum: kind 0 (NT) or 1 (NN)");
+  const int64_t M = A.size(0), K = A.size(1), N = kind == 0 ? B.size(0) : B.size(1);
+  TORCH_CHECK((kind == 0 ? B.size(1) : B.size(0)) == K && C.size(0) == M && C.size(1) == N,
+              "gemm_colsum: shape mismatch");
   TORCH_CHECK(K % 64 == 0 && N % 64 == 0, "gemm_colsum: K % 64 and N % 64 required");
   TORCH_CHECK(epi == 3 || epi == 4, "gemm_colsum: GELU' (3) or residual (4) epilogue");
   need_opt(aux, at::kBFloat16, "aux");
@@ -216,9 +220,9 @@ int64_t gemm_colsum(int64_t epi, const at::Tensor& A, const at::Tensor& B, const
   if (aux_out.has_value() && aux_out->defined())
     TORCH_CHECK(epi == 3 && aux_out->size(0) == M && aux_out->size(1) == N, "aux_out [M,N] only with GELU'");
   int blocks = 0;
-  check_rc(fd_gemm_ex(0, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K, (int)K,
-                      (int)K, (int)N, nullptr, ptr<void>(aux), (int)N, ptr<void>(res), (int)N, nullptr, 0, 0,
-                      nullptr, colsum.data_ptr<float>(), &blocks, ptr<void>(aux_out), stream()),
+  check_rc(fd_gemm_ex((int)kind, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
+                      (int)K, (int)B.size(1), (int)N, nullptr, ptr<void>(aux), (int)N, ptr<void>(res), (int)N,
+                      nullptr, 0, 0, nullptr, colsum.data_ptr<float>(), &blocks, ptr<void>(aux_out), stream()),
            "gemm_colsum");
   return blocks;
 }
@@ -383,7 +387,9 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
                 const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& dx,
                 const c10::optional<at::Tensor>& colpart, const at::Tensor& stats, const at::Tensor& cnt,
                 const at::Tensor& err, double eps, const c10::optional<at::Tensor>& seed, int64_t site, int64_t thr,
-                double dscale, const c10::optional<at::Tensor>& row_map, int64_t cfg, int64_t xsite) {
+                double dscale, const c10::optional<at::Tensor>& row_map, int64_t cfg, int64_t xsite,
+                bool b_mn = false) {
+  // b_mn: Bt is the weight itself, W [K][N] (MN-major B, a dX GEMM without a W^T copy; direct-A only)
   need(A, at::kBFloat16, "A");
   need(Bt, at::kBFloat16, "Bt");
   need(C, at::kBFloat16, "C");
@@ -395,8 +401,9 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
   need(cnt, at::kInt, "cnt");
   need(err, at::kInt, "err");
   TORCH_CHECK(A.dim() == 2 && Bt.dim() == 2 && C.dim() == 2 && res.dim() == 2, "gemm_ln operands must be 2-D");
-  const int64_t M = A.size(0), K = A.size(1), N = Bt.size(0);
-  TORCH_CHECK(M > 0 && Bt.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_ln: shape mismatch");
+  const int64_t M = A.size(0), K = A.size(1), N = b_mn ? Bt.size(1) : Bt.size(0);
+  TORCH_CHECK(M > 0 && (b_mn ? Bt.size(0) : Bt.size(1)) == K && C.size(0) == M && C.size(1) == N,
+              "gemm_ln: shape mismatch");
   TORCH_CHECK(res.size(0) == M && res.size(1) == N, "gemm_ln: res must be [M, N]");
   TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && N <= 2048, "gemm_ln: K % 64, N % 64 and N <= 2048 required");
   TORCH_CHECK(gamma.numel() == N, "gemm_ln: gamma of size N required");
@@ -445,7 +452,7 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
     ln.row_map = ptr<int>(row_map);
   }
   const int rc = fd_gemm_ln(bwd ? 1 : 0, A.data_ptr(), Bt.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
-                            ptr<float>(bias), res.data_ptr(), (int)N, &ln, (int)cfg, stream());
+                            ptr<float>(bias), res.data_ptr(), (int)N, &ln, (int)cfg, b_mn ? 1 : 0, stream());
   TORCH_CHECK(rc > 0, "gemm_ln: kernel launcher rejected arguments (rc=", rc, ")");
   return rc;
 }
@@ -1221,6 +1228,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, py::arg("kind"), py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"),
         py::arg("aux"), py::arg("res"), py::arg("workspace"), py::arg("accumulate"), py::arg("aux_out") = py::none());
   m.def("gemm_set_cfg", &gemm_set_cfg);
+  m.def("gemm_set_da", [](int64_t id) { check_rc(fd_gemm_set_da((int)id), "gemm_set_da"); });
   m.def("gemm_stamps", &gemm_stamps);
   m.def("attn_stamps", &attn_stamps);
   m.def("gemm_splitk", &gemm_splitk, py::arg("epi"), py::arg("A"), py::arg("Bt"), py::arg("C"), py::arg("workspace"),
@@ -1237,11 +1245,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("rstd"), py::arg("z"),
         py::arg("dx"), py::arg("colpart"), py::arg("stats"), py::arg("cnt"), py::arg("err"), py::arg("eps"),
         py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("row_map"),
-        py::arg("cfg") = -1, py::arg("xsite") = 0);
+        py::arg("cfg") = -1, py::arg("xsite") = 0, py::arg("b_mn") = false);
   m.def("gemm_dw_batch", &gemm_dw_batch, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("accumulate"),
         py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1, py::arg("wts") = std::vector<at::Tensor>{});
   m.def("gemm_colsum", &gemm_colsum, py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("aux"),
-        py::arg("res"), py::arg("colsum"), py::arg("aux_out") = py::none());
+        py::arg("res"), py::arg("colsum"), py::arg("aux_out") = py::none(), py::arg("kind") = 0);
   m.def("splitk_reduce_batched", &splitk_reduce_batched);
   m.def("gemm_dw2_splits", [](int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K) {
     return (int64_t)fd_gemm_dw2_splits((int)M0, (int)N0, (int)M1, (int)N1, (int)K);

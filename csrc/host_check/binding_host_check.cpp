@@ -100,6 +100,7 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
   return 0;
 }
 int fd_gemm_dw2_splits(int, int, int, int, int) { return 1; }
+int fd_gemm_set_da(int) { return 0; }
 int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg, hipStream_t) {
   ++hc::calls;
   if (n <= 0 || n > 32) hc::violations.push_back("dw_batch: problem count");
@@ -180,8 +181,9 @@ int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, 
   return splits;
 }
 int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
-               const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t) {
+               const void* res, int ldres, const FdLnEpi* ln, int cfg, int b_mn, hipStream_t) {
   ++hc::calls;
+  (void)b_mn;  // (W [K][N] or W^T [N][K]: the same N * K elements)
   const int bm = cfg == 13 ? 64 : 128;
   const long long tm = (M + bm - 1) / bm, mn = (long long)M * N;
   hc::span(A, (long long)M * K * 2, "gemm_ln A");

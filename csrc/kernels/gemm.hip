@@ -533,9 +533,45 @@ constexpr int LN_MAXK = 4;  // column tiles per row block <= LN_MAXK * (BN / 8)
 // larger grids take the separate LayerNorm kernels (ops/kernels.py ln_fusable mirrors this).
 constexpr int LN_MAX_TILES = 256;
 
+// The per-thread operands of the LayerNorm epilogue's element math (a thread owns IT rows x 8
+// columns): residual, backward z / mean / rstd, dropout-hash rows, gamma, the exchange tag.  The
+// direct-A kernels load them during their last K tiles (gemm_ln_da_kernel), the LDS-DMA kernels
+// right after their K loop (their inline-asm ring waits would count these loads as ring tiles).
+template <int IT>
+struct LnPre {
+  uint4 res_v[IT], z_v[IT];
+  float mrow[IT], rrow[IT];
+  int hrow_v[IT];
+  float g[8];
+  uint32_t tag;
+};
+
+template <int BM, int BN, bool BWD, int NT>
+DEV LnPre<BM * (BN / 8) / NT> ln_prefetch(const GemmParams& p, int tm, int tn, int tid) {
+  constexpr int CPR = BN / 8, IT = BM * CPR / NT;
+  const FdLnEpi& L = p.ln;
+  const int m0 = tm * BM, N = p.N;
+  const int n = tn * BN + 8 * (tid % CPR);
+  LnPre<IT> pre;
+  pre.tag = (uint32_t)__hip_atomic_load(L.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * FD_LN_XSITES + L.xsite + 1u;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int mc = min(m0 + (tid + it * NT) / CPR, p.M - 1);
+    pre.res_v[it] = *reinterpret_cast<const uint4*>(p.res + (size_t)mc * p.ldres + n);
+    if constexpr (BWD) {
+      pre.z_v[it] = *reinterpret_cast<const uint4*>(L.z + (size_t)mc * N + n);
+      pre.mrow[it] = L.mean[mc];
+      pre.rrow[it] = L.rstd[mc];
+    }
+    pre.hrow_v[it] = (L.thr && L.row_map) ? L.row_map[mc] : mc;
+  }
+  load8f(L.gamma + n, pre.g);
+  return pre;
+}
+
 template <int BM, int BN, int TM, int TN, bool BWD, int NT>
 DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int tm, int tn,
-                     int wr, int wc, int lane, int tid) {
+                     int wr, int wc, int lane, int tid, const LnPre<BM * (BN / 8) / NT>& pre) {
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int LDC = BN * 4 + 16;
   constexpr int CPR = BN / 8;            // lanes per row (8 columns each)
@@ -544,25 +580,15 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
   const FdLnEpi& L = p.ln;
   const int m0 = tm * BM, n0 = tn * BN, tiles_n = p.N / BN, N = p.N;
   const int cc = tid % CPR, n = n0 + 8 * cc;
-  // operands of the element math, issued before the tile is parked so their latency overlaps it
-  const uint32_t tag = (uint32_t)__hip_atomic_load(L.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * FD_LN_XSITES +
-                       L.xsite + 1u;
-  uint4 res_v[IT], z_v[IT];
-  float mrow[IT], rrow[IT];
-  int hrow_v[IT];
+  const uint32_t tag = pre.tag;
+  uint4 z_v[IT];
+  const uint4* res_v = pre.res_v;
+  const float* mrow = pre.mrow;
+  const float* rrow = pre.rrow;
+  const int* hrow_v = pre.hrow_v;
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int mc = min(m0 + (tid + it * NT) / CPR, p.M - 1);
-    res_v[it] = *reinterpret_cast<const uint4*>(p.res + (size_t)mc * p.ldres + n);
-    if constexpr (BWD) {
-      z_v[it] = *reinterpret_cast<const uint4*>(L.z + (size_t)mc * N + n);
-      mrow[it] = L.mean[mc];
-      rrow[it] = L.rstd[mc];
-    }
-    hrow_v[it] = (L.thr && L.row_map) ? L.row_map[mc] : mc;
-  }
-  float g[8];
-  load8f(L.gamma + n, g);
+  for (int it = 0; it < IT; ++it) z_v[it] = pre.z_v[it];
+  const float* g = pre.g;
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int r = wr * TM + i * 16 + (lane & 15);
@@ -951,8 +977,9 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
       f32_epilogue<TM, BN, 64 * NW>(p, smem, LDC, m0 + band * TM, n0, tid);
     }
   } else if constexpr (EpiTraits<EPI, BM, BN>::LN) {
+    const auto pre = ln_prefetch<BM, BN, EPI == EPI_LN_BWD, 64 * NW>(p, tm, tn, tid);
     __syncthreads();  // no wave still reads a ring slot
-    ln_epilogue<BM, BN, TM, TN, EPI == EPI_LN_BWD, 64 * NW>(p, acc, smem, tm, tn, wr, wc, lane, tid);
+    ln_epilogue<BM, BN, TM, TN, EPI == EPI_LN_BWD, 64 * NW>(p, acc, smem, tm, tn, wr, wc, lane, tid, pre);
   } else {
     // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
     // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
@@ -988,15 +1015,186 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
 
 // LayerNorm-fused NT GEMM (EPI_LN / EPI_LN_BWD): the tiles of a row block are consecutive
 // logical tiles (row-major tile order), so after the XCD remap they run on one XCD, in order.
-template <int BM, int BN, int EPI, int WM, int WN, int S>
+// BKM = false: B is the weight W [K][N] itself (MN-major; the backward dX GEMMs without W^T).
+template <int BM, int BN, int EPI, int WM, int WN, int S, bool BKM = true>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_ln_kernel(GemmParams p) {
-  using G = GemmCfg<BM, BN, true, true, EPI, WM, WN, S>;
+  using G = GemmCfg<BM, BN, true, BKM, EPI, WM, WN, S>;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   FD_STAMP(0);
   stamp_hwid();
   const int tiles_n = p.N / BN;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  gemm_tile_at<BM, BN, true, true, EPI, WM, WN, S>(p, lid / tiles_n, lid % tiles_n, smem);
+  gemm_tile_at<BM, BN, true, BKM, EPI, WM, WN, S>(p, lid / tiles_n, lid % tiles_n, smem);
+#if FD_GEMM_STAMPS
+  __syncthreads();
+  FD_STAMP(5);
+#endif
+}
+
+// ---------------------------------------------------------------- direct-A K loop (round 4)
+// The one-round NT GEMMs (M ~ 2.7 k packed tokens) were bound by getting operand bytes into the
+// CU: 24 KiB per 64-deep K tile of a 128 x 64 tile, and LDS-DMA fills only 77-88 GB/s per CU with
+// 8 waves against ~108 GB/s for plain global loads into VGPRs (profiles/r3_l2_fill.txt); the K
+// loop ran at ~64 GB/s.  Here a block of WM waves (WN = 1) owns BM x BN; wave w owns TM = BM / WM
+// rows and all BN columns, so no two waves share an A row:
+//  * A (the activations, 2/3 of the bytes) goes global -> VGPRs straight in MFMA fragment layout
+//    (lane l: row l & 15, 8 consecutive k = 16 contiguous bytes) -- no LDS write, no LDS read;
+//  * B (BN weight rows x 64 k) goes global -> VGPRs -> one ds_write_b128 per thread into a
+//    double-buffered swizzled LDS slot (the K-major image of Operand<.., true, ..>) and is read
+//    as fragments by every wave;
+//  * both through a D-deep register ring: tile t + D is requested while tile t computes, every
+//    load compiler-visible, so hipcc's counted vmcnt waits are exact (no inline-asm DMA whose
+//    waits it cannot see); one barrier per K tile.
+// nk % D == 0 and nk >= D (the host falls back to the LDS-DMA kernels otherwise).
+template <int BM, int BN, int WM, int D>
+struct DaCfg {
+  static constexpr int NW = WM;
+  static constexpr int TM = BM / WM;
+  static constexpr int MI = TM / 16, NI = BN / 16;
+  static constexpr int BSLOT = BN * BKT * 2;                // one B slot: BN rows x 128 B
+  static constexpr int BCH = BN * (BKT / 8) / (64 * NW);    // 16-byte B chunks per thread per tile
+  static constexpr int KBYTES = 2 * BSLOT;
+  static_assert(TM % 16 == 0 && BN % 16 == 0 && BCH >= 1 && BCH * 64 * NW * 8 == BN * BKT && D % 2 == 0,
+                "direct-A tile");
+};
+
+// BKM: B K-major (B(k, n) = B[n * ldb + k]: a W^T copy / the NT weight) or MN-major (B(k, n) =
+// B[k * ldb + n]: the dX GEMMs reading the weight W itself -- its LDS image is the [64 k][SUB n]
+// swizzled one of Operand<.., false, ..>, read with the transposing ds_read_b64_tr_b16).
+// before_tail(): called once every load of the K loop has been issued, before the last D tiles
+// compute -- the epilogue's own global loads go there, so their latency hides under those tiles.
+struct NoTail {
+  DEV void operator()() const {}
+};
+
+template <int BM, int BN, int WM, int D, bool BKM = true, typename Tail = NoTail>
+DEV void da_kloop(const GemmParams& p, int m0, int n0, char* smem, f32x4 (&acc)[BM / WM / 16][BN / 16],
+                  Tail before_tail = Tail()) {
+  using C = DaCfg<BM, BN, WM, D>;
+  using OB = Operand<BN, BKM, WM>;
+  constexpr int MI = C::MI, NI = C::NI, TM = C::TM, BCH = C::BCH;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nk = p.K / BKT;
+  const bf16_t* pa[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int r = min(m0 + wid * TM + i * 16 + (lane & 15), p.M - 1);  // (clamped rows are never stored)
+    pa[i] = p.A + (size_t)r * p.lda + 8 * (lane >> 4);
+  }
+  const bf16_t* pb[BCH];
+  int bo[BCH];
+#pragma unroll
+  for (int c = 0; c < BCH; ++c) {
+    const int id = tid + c * 64 * C::NW;
+    if constexpr (BKM) {  // 8 lanes = one weight row's 128 contiguous bytes of the K tile
+      const int n = id >> 3, ch = id & 7;
+      pb[c] = p.B + (size_t)(n0 + n) * p.ldb + ch * 8;
+      bo[c] = n * 128 + ((ch ^ ksw(n)) << 4);
+    } else {              // BN / 8 lanes = one k row's BN contiguous columns
+      constexpr int CPRB = BN / 8;
+      const int k = id / CPRB, n = (id % CPRB) * 8;
+      pb[c] = p.B + (size_t)k * p.ldb + n0 + n;
+      bo[c] = (n / OB::SUB) * OB::SUB_BYTES + k * OB::SUB * 2 + ((((n % OB::SUB) >> 3) ^ fk<OB::SUB>(k)) << 4);
+    }
+  }
+  const size_t bstep = BKM ? (size_t)BKT : (size_t)BKT * p.ldb;  // B elements per K tile
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // One register ring for both operands (slots 0 .. 2 MI - 1: A fragments [i][s], then BCH B
+  // chunks): kept as ONE ext-vector array so hipcc promotes it to VGPRs (a separate small B ring
+  // went to scratch).
+  constexpr int RS = 2 * MI + BCH;
+  bf16x8 ring[D][RS];
+  auto load = [&](int t, bf16x8 (&r)[RS]) {
+#pragma unroll
+    for (int c = 0; c < BCH; ++c) r[2 * MI + c] = *reinterpret_cast<const bf16x8*>(pb[c] + t * bstep);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) r[2 * i + s] = *reinterpret_cast<const bf16x8*>(pa[i] + t * BKT + s * 32);
+  };
+  // tile in ring slot d (LDS slot d & 1: tiles alternate parity since D is even)
+  auto compute = [&](int d, const bf16x8 (&r)[RS]) {
+    char* slot = smem + (d & 1) * C::BSLOT;
+#pragma unroll
+    for (int c = 0; c < BCH; ++c) *reinterpret_cast<bf16x8*>(slot + bo[c]) = r[2 * MI + c];
+    // this tile's B is in LDS for every wave; every wave is done reading this slot's previous
+    // tile (two tiles ago: it passed the previous tile's barrier after its fragment reads)
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 bf[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) bf[j] = OB::frag(slot, j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(bf[j], r[2 * i + s], acc[i][j]);
+    }
+  };
+#pragma unroll
+  for (int d = 0; d < D; ++d) load(d, ring[d]);
+  for (int t0 = 0; t0 < nk - D; t0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      compute(d, ring[d]);
+      load(t0 + d + D, ring[d]);
+    }
+  }
+  before_tail();
+#pragma unroll
+  for (int d = 0; d < D; ++d) compute(d, ring[d]);
+  __syncthreads();  // every wave is done with the B slots: the epilogue may reuse the LDS
+}
+
+template <int BM, int BN, int EPI, int WM, int D>
+struct DaKern {
+  using TR = EpiTraits<EPI, BM, BN>;
+  static constexpr int SMEM = DaCfg<BM, BN, WM, D>::KBYTES > TR::BYTES ? DaCfg<BM, BN, WM, D>::KBYTES : TR::BYTES;
+  static constexpr bool VALID = SMEM <= LDS_MAX && !TR::DIRECT && EPI != EPI_F32 && (!TR::LN || TR::F32S);
+};
+
+// Plain NT / NN GEMM (y = x W^T, dx = dy W; + epilogue) on the direct-A K loop.
+template <int BM, int BN, int EPI, int WM, int D, bool BKM = true>
+__global__ __launch_bounds__(64 * WM, 2) void gemm_da_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(1024))) char smem[DaKern<BM, BN, EPI, WM, D>::SMEM];
+  FD_STAMP(0);
+  stamp_hwid();
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = p.N / BN;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, p.group_m, tm, tn);
+  f32x4 acc[BM / WM / 16][BN / 16];
+  da_kloop<BM, BN, WM, D, BKM>(p, tm * BM, tn * BN, smem, acc);
+  FD_STAMP(2);
+  const int tid = threadIdx.x;
+  staged_epilogue<BM, BN, BM / WM, BN, EPI, 64 * WM>(p, acc, smem, tm * BM, tn * BN, tid >> 6, 0, tid & 63, tid);
+#if FD_GEMM_STAMPS
+  __syncthreads();
+  FD_STAMP(5);
+#endif
+}
+
+// LayerNorm-fused NT GEMM on the direct-A K loop (row-major tile order: a row block's tiles are
+// consecutive logical tiles, so after the XCD remap they run on one XCD, in order).
+template <int BM, int BN, int EPI, int WM, int D, bool BKM = true>
+__global__ __launch_bounds__(64 * WM, 2) void gemm_ln_da_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(1024))) char smem[DaKern<BM, BN, EPI, WM, D>::SMEM];
+  FD_STAMP(0);
+  stamp_hwid();
+  const int tiles_n = p.N / BN;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lid / tiles_n, tn = lid % tiles_n;
+  f32x4 acc[BM / WM / 16][BN / 16];
+  const int tid = threadIdx.x;
+  LnPre<BM * (BN / 8) / (64 * WM)> pre;
+  // the epilogue's residual / z / mean / rstd / gamma loads are issued under the last K tiles
+  da_kloop<BM, BN, WM, D, BKM>(p, tm * BM, tn * BN, smem, acc,
+                               [&] { pre = ln_prefetch<BM, BN, EPI == EPI_LN_BWD, 64 * WM>(p, tm, tn, tid); });
+  FD_STAMP(2);
+  ln_epilogue<BM, BN, BM / WM, BN, EPI == EPI_LN_BWD, 64 * WM>(p, acc, smem, tm, tn, tid >> 6, 0, tid & 63, tid, pre);
 #if FD_GEMM_STAMPS
   __syncthreads();
   FD_STAMP(5);
@@ -1246,6 +1444,61 @@ int pick_cfg(int kind, int M, int N, int K) {
   return (N % 128 == 0 && M > 1024 && M < 3072 && N < 3072) ? 1 : 8;  // TN dW
 }
 
+// Direct-A NT GEMMs (gemm_da_kernel): FD_GEMM_DA=<id> selects them for the kind-0 launches
+// (50: 128 x 64 on 8 waves, 52: 128 x 128 on 8 waves -- 16 rows x all columns per wave);
+// unset / -1 = off.  K / 64 must be a multiple of the ring depth (4).
+int g_da = -2;  // FD_GEMM_DA / fd_gemm_set_da
+int da_cfg(int M, int N, int K) {
+  if (g_da == -2) {
+    const char* e = getenv("FD_GEMM_DA");
+    g_da = e ? atoi(e) : -1;
+  }
+  if (g_da < 0 || (K / BKT) % 4 || K / BKT < 4 || M < 128) return -1;
+  if (g_da == 52 && N % 128 == 0) return 52;
+  return N % 64 == 0 ? 50 : -1;
+}
+
+template <int BM, int BN, int EPI, int WM, int D, bool BKM>
+bool launch_da_cfg(const GemmParams& p, hipStream_t st) {
+  if constexpr (!DaKern<BM, BN, EPI, WM, D>::VALID) {
+    return false;
+  } else {
+    if (p.N % BN) return false;
+    const int tiles = ((p.M + BM - 1) / BM) * (p.N / BN);
+    hipLaunchKernelGGL((gemm_da_kernel<BM, BN, EPI, WM, D, BKM>), dim3(tiles), dim3(64 * WM), 0, st, p);
+    return true;
+  }
+}
+
+template <int EPI, bool BKM>
+bool launch_da_id(const GemmParams& p, int id, hipStream_t st) {
+  switch (id) {
+    case 50: return launch_da_cfg<128, 64, EPI, 8, 4, BKM>(p, st);
+    case 52: return launch_da_cfg<128, 128, EPI, 8, 4, BKM>(p, st);
+  }
+  return false;
+}
+
+// bkm: B K-major (kind 0, NT) or MN-major (kind 1, NN: the dX GEMMs on the weight itself)
+bool launch_da(int epi, const GemmParams& p, int id, bool bkm, hipStream_t st) {
+  if (bkm) {
+    switch (epi) {
+      case EPI_BF16: return launch_da_id<EPI_BF16, true>(p, id, st);
+      case EPI_BIAS: return launch_da_id<EPI_BIAS, true>(p, id, st);
+      case EPI_BIAS_GELU: return launch_da_id<EPI_BIAS_GELU, true>(p, id, st);
+      case EPI_GELU_BWD: return launch_da_id<EPI_GELU_BWD, true>(p, id, st);
+      case EPI_ADD: return launch_da_id<EPI_ADD, true>(p, id, st);
+    }
+    return false;
+  }
+  switch (epi) {
+    case EPI_BF16: return launch_da_id<EPI_BF16, false>(p, id, st);
+    case EPI_GELU_BWD: return launch_da_id<EPI_GELU_BWD, false>(p, id, st);
+    case EPI_ADD: return launch_da_id<EPI_ADD, false>(p, id, st);
+  }
+  return false;
+}
+
 template <bool AK, bool BKM>
 bool launch_epi(int epi, const GemmParams& p, int id, int splits, hipStream_t st) {
   switch (epi) {
@@ -1322,6 +1575,13 @@ int fd_gemm_stamps(unsigned long long* host, int nblocks) {
 #endif
 }
 
+// Direct-A NT GEMMs for the kind-0 launches: 50 / 52 (see da_cfg), -1 = off (tests / A/B).
+int fd_gemm_set_da(int id) {
+  if (id != -1 && id != 50 && id != 52) return 1;
+  g_da = id;
+  return 0;
+}
+
 // Force a configuration id / split count for a GEMM kind (tuning; -1 = auto).
 int fd_gemm_set_cfg(int kind, int cfg, int splits) {
   if (kind < 0 || kind > 2 || cfg < -1 || cfg >= NCFG || (cfg >= 0 && !cfg_instantiated(cfg))) return 1;
@@ -1372,9 +1632,21 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
     if (e) gm = atoi(e);
     p.group_m = std::max(1, gm);
   }
+  // direct-A kernels (da_cfg; 128-row tiles with the staged-fp32 epilogue, so column sums too)
+  const int da = (kind == 0 || kind == 1) ? da_cfg(M, N, K) : -1;
+  if (colsum && da >= 0 && (epi == EPI_GELU_BWD || epi == EPI_ADD)) {
+    p.colsum = colsum;
+    if (colsum_blocks) *colsum_blocks = (M + 127) / 128;
+    if (launch_da(epi, p, da, kind == 0, st)) return 0;
+    p.colsum = nullptr;
+  }
   if (colsum) {
     // only the staged-fp32 epilogues sum columns: 128 x {128, 64} tiles (never 256-row ones)
-    if (kind != 0 || (epi != EPI_GELU_BWD && epi != EPI_ADD)) return 2;
+    if (epi != EPI_GELU_BWD && epi != EPI_ADD) return 2;
+    if (kind != 0) {  // (NN: the direct-A kernels only) launch nothing: plain GEMM + column-sum pass
+      if (colsum_blocks) *colsum_blocks = 0;
+      return kind == 1 ? 0 : 2;
+    }
     if (CFGS[id].bm != 128 && cfg_override(kind) < 0) id = 8;  // (small-M 64-row tiles: 128 x 64)
     if (CFGS[id].bm != 128 || (CFGS[id].bn != 128 && CFGS[id].bn != 64) || N % CFGS[id].bn) {
       // the shape's tile has no staged-fp32 epilogue (e.g. 256 x 192 at M >= 3.5 k): launch
@@ -1387,11 +1659,13 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
   }
   if (kind == 0) {  // also dX = dy (W^T)^T with a transposed weight copy: GELU' / residual epilogues
     if (epi == EPI_F32) return 2;
+    if (da >= 0 && !colsum && launch_da(epi, p, da, true, st)) return 0;
     if (launch_epi<true, true>(epi, p, id, 1, st)) return 0;
     return launch_epi<true, true>(epi, p, 0, 1, st) ? 0 : 2;  // 128x64 fits any N % 64 == 0
   }
   if (kind == 1) {
     if (epi != EPI_BF16 && epi != EPI_GELU_BWD && epi != EPI_ADD) return 2;
+    if (da >= 0 && !colsum && launch_da(epi, p, da, false, st)) return 0;
     if (launch_epi<true, false>(epi, p, id, 1, st)) return 0;
     return launch_epi<true, false>(epi, p, 0, 1, st) ? 0 : 2;
   }
@@ -1596,14 +1870,19 @@ int fd_gemm_ln_set_diag(int diag) {
 }
 
 int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
-               const void* res, int ldres, const FdLnEpi* ln, int cfg, hipStream_t st) {
+               const void* res, int ldres, const FdLnEpi* ln, int cfg, int b_mn, hipStream_t st) {
   if (M <= 0 || K % BKT || N % 64 || !ln || !res || (!bwd && !bias)) return -1;
+  // b_mn: B is the weight W [K][N] itself (MN-major; LayerNorm backward only)
+  if (b_mn && !bwd) return -6;
   if (ln->xsite >= FD_LN_XSITES) return -5;
   int id = cfg;
   if (id < 0) {
     static const int env = [] { const char* e = getenv("FD_GEMM_LN_CFG"); return e ? atoi(e) : -1; }();
     id = env >= 0 ? env : (M <= 64 && smallm_tiles() ? 13 : 24);
   }
+  // direct-A K loop (cfg 50: 8 waves x 16 rows, 51: 4 waves x 32 rows; 4-deep register ring) needs
+  // K / 64 to be a multiple of the ring depth; otherwise the LDS-DMA configuration
+  if (id >= 50 && ((K / BKT) % 4 || K / BKT < 4)) id = 24;
   const int bm = id == 13 ? 64 : 128, bn = 64;
   if (N / bn > LN_MAXK * (bn / 8)) return -2;
   {
@@ -1620,7 +1899,7 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   }
   GemmParams p{};
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)Bt; p.C = C;
-  p.M = M; p.N = N; p.K = K; p.lda = K; p.ldb = K; p.ldc = N;
+  p.M = M; p.N = N; p.K = K; p.lda = K; p.ldb = b_mn ? N : K; p.ldc = N;
   p.bias = bias; p.res = (const bf16_t*)res; p.ldres = ldres;
   p.k_split = K;
   p.ln = *ln;
@@ -1636,10 +1915,31 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   auto go = [&](auto kern, int threads) { hipLaunchKernelGGL(kern, grid, dim3(threads), 0, st, p); };
 #define FD_LN_CASE(ID, BM_, BN_, WM_, WN_, S_)                                          \
   case ID:                                                                             \
-    if (bwd) go(gemm_ln_kernel<BM_, BN_, EPI_LN_BWD, WM_, WN_, S_>, 64 * WM_ * WN_);   \
+    if (b_mn) go(gemm_ln_kernel<BM_, BN_, EPI_LN_BWD, WM_, WN_, S_, false>, 64 * WM_ * WN_); \
+    else if (bwd) go(gemm_ln_kernel<BM_, BN_, EPI_LN_BWD, WM_, WN_, S_>, 64 * WM_ * WN_);   \
     else go(gemm_ln_kernel<BM_, BN_, EPI_LN, WM_, WN_, S_>, 64 * WM_ * WN_);           \
     break;
   switch (id) {
+    case 50:
+      if (b_mn) {  // (the dX GEMMs only: LayerNorm backward)
+        if (!bwd) return -6;
+        go(gemm_ln_da_kernel<128, 64, EPI_LN_BWD, 8, 4, false>, 512);
+      } else if (bwd) {
+        go(gemm_ln_da_kernel<128, 64, EPI_LN_BWD, 8, 4>, 512);
+      } else {
+        go(gemm_ln_da_kernel<128, 64, EPI_LN, 8, 4>, 512);
+      }
+      break;
+    case 51:
+      if (b_mn) {
+        if (!bwd) return -6;
+        go(gemm_ln_da_kernel<128, 64, EPI_LN_BWD, 4, 4, false>, 256);
+      } else if (bwd) {
+        go(gemm_ln_da_kernel<128, 64, EPI_LN_BWD, 4, 4>, 256);
+      } else {
+        go(gemm_ln_da_kernel<128, 64, EPI_LN, 4, 4>, 256);
+      }
+      break;
     FD_LN_CASE(24, 128, 64, 4, 2, 6)
     FD_LN_CASE(0, 128, 64, 2, 2, 3)
     FD_LN_CASE(18, 128, 64, 4, 2, 3)

@@ -26,9 +26,28 @@ from the mask, so any batch of the same bucket replays it.
 """
 from __future__ import annotations
 
+import gc
 from typing import Callable, Dict, Optional
 
 import torch
+
+
+class no_gc:
+    """Python's cyclic GC paused over a graph capture: a collection that runs mid-capture can free
+    an unreachable model's HIP graphs / tensors (a model and its cached eval GraphedForward
+    reference each other), and the resulting hipGraphExecDestroy / hipFree is not permitted while
+    the stream captures (measured: scripts/curve_bisect.py's 8th model, round 4)."""
+
+    def __enter__(self):
+        self.was = gc.isenabled()
+        gc.collect()
+        gc.disable()
+        return self
+
+    def __exit__(self, *exc):
+        if self.was:
+            gc.enable()
+        return False
 
 
 def contiguous_block(*ts: torch.Tensor) -> Optional[torch.Tensor]:
@@ -123,7 +142,7 @@ class GraphedTrainStep:
             prepare()
         try:
             torch.cuda.synchronize()
-            with torch.cuda.graph(g):
+            with no_gc(), torch.cuda.graph(g):
                 loss = self.step_fn(static["ids"], static["mask"], static["labels"], key[1])
         except Exception as e:  # pragma: no cover - capture support varies by op
             self.failed = f"{type(e).__name__}: {e}"

@@ -15,7 +15,7 @@ from typing import Dict, Optional, Tuple
 import numpy as np
 import torch
 
-from .graph import contiguous_block, static_block
+from .graph import contiguous_block, no_gc, static_block
 
 
 class GraphedForward:
@@ -69,7 +69,7 @@ class GraphedForward:
         g = torch.cuda.CUDAGraph()
         try:
             torch.cuda.synchronize()
-            with torch.cuda.graph(g):
+            with no_gc(), torch.cuda.graph(g):
                 out = m(static["ids"], static["mask"], tokens=key[1])
         except Exception as e:  # pragma: no cover - capture support varies by op
             self.failed = f"{type(e).__name__}: {e}"

@@ -12,6 +12,7 @@ update on (fixed) or frozen (the round-3 reference arm's behaviour, emulated by 
 table after every step), two dropout streams each, and prints the 20-step window means, the mean
 signed HIP - torch difference and the self-spread.  Usage: python scripts/curve_bisect.py
 (BISECT_STEPS=200)."""
+import gc
 import os
 import sys
 
@@ -53,6 +54,7 @@ def curve(impl, batches, test, counter0=0, freeze_word=False):
     c = torch.stack(out).float().cpu().numpy()
     acc = evaluate_model(m, DeviceLoader(test, 64, device="cuda"))[0]
     del step, opt, m
+    gc.collect()
     torch.cuda.empty_cache()
     return c, acc, moved
 
