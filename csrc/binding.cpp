@@ -45,7 +45,7 @@ int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const
 int fd_gemm_ln_set_diag(int diag);
 int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, float* workspace,
                    long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
-                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, hipStream_t st);
+                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, int b_mn, hipStream_t st);
 int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
                const void* res, int ldres, const FdLnEpi* ln, int cfg, int b_mn, hipStream_t st);
 int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
@@ -471,14 +471,16 @@ std::vector<int64_t> gemm_splitk(int64_t epi, const at::Tensor& A, const at::Ten
                                  const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& dx,
                                  const c10::optional<at::Tensor>& colpart, double eps,
                                  const c10::optional<at::Tensor>& seed, int64_t site, int64_t thr, double dscale,
-                                 const c10::optional<at::Tensor>& row_map) {
+                                 const c10::optional<at::Tensor>& row_map, bool b_mn = false) {
+  // b_mn: Bt is the weight W [K][N] itself (C = epi(A W); a dX GEMM without a W^T copy)
   need(A, at::kBFloat16, "A");
   need(Bt, at::kBFloat16, "Bt");
   need(C, at::kBFloat16, "C");
   need(workspace, at::kFloat, "workspace");
   TORCH_CHECK(A.dim() == 2 && Bt.dim() == 2 && C.dim() == 2, "gemm_splitk operands must be 2-D");
-  const int64_t M = A.size(0), K = A.size(1), N = Bt.size(0);
-  TORCH_CHECK(M > 0 && Bt.size(1) == K && C.size(0) == M && C.size(1) == N, "gemm_splitk: shape mismatch");
+  const int64_t M = A.size(0), K = A.size(1), N = b_mn ? Bt.size(1) : Bt.size(0);
+  TORCH_CHECK(M > 0 && (b_mn ? Bt.size(0) : Bt.size(1)) == K && C.size(0) == M && C.size(1) == N,
+              "gemm_splitk: shape mismatch");
   TORCH_CHECK(K % 64 == 0 && N % 64 == 0, "gemm_splitk: K % 64 and N % 64 required");
   TORCH_CHECK(epi >= 0 && epi <= 7 && epi != 5, "gemm_splitk: epilogue code");
   for (const auto* t : {&aux, &aux_out, &res, &z, &dx}) {
@@ -535,7 +537,7 @@ std::vector<int64_t> gemm_splitk(int64_t epi, const at::Tensor& A, const at::Ten
   const int rc = fd_gemm_splitk((int)epi, A.data_ptr(), Bt.data_ptr(), (int)M, (int)N, (int)K,
                                 workspace.data_ptr<float>(), workspace.numel(), (int)splits, ptr<float>(bias),
                                 C.data_ptr(), ptr<void>(aux), ptr<void>(aux_out), ptr<void>(res), ptr<float>(colsum),
-                                &blocks, epi >= 6 ? &ln : nullptr, stream());
+                                &blocks, epi >= 6 ? &ln : nullptr, b_mn ? 1 : 0, stream());
   TORCH_CHECK(rc > 0, "gemm_splitk: launcher rejected arguments (rc=", rc, ")");
   return {rc, blocks};
 }
@@ -1237,7 +1239,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gamma") = py::none(), py::arg("beta") = py::none(), py::arg("mean") = py::none(),
         py::arg("rstd") = py::none(), py::arg("z") = py::none(), py::arg("dx") = py::none(),
         py::arg("colpart") = py::none(), py::arg("eps") = 1e-12, py::arg("seed") = py::none(),
-        py::arg("site") = 0, py::arg("thr") = 0, py::arg("dscale") = 1.0, py::arg("row_map") = py::none());
+        py::arg("site") = 0, py::arg("thr") = 0, py::arg("dscale") = 1.0, py::arg("row_map") = py::none(),
+        py::arg("b_mn") = false);
   m.def("gemm_dw2", &gemm_dw2);
   m.def("gemm_dw", &gemm_dw);
   m.def("adam_rows", &adam_rows);

@@ -145,8 +145,9 @@ int fd_adam_rows(float* p, const float* g, float* m, float* v, void* shadow, int
 }
 int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, float* workspace,
                    long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
-                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, hipStream_t) {
+                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, int b_mn, hipStream_t) {
   ++hc::calls;
+  (void)b_mn;  // (W [K][N] or W^T [N][K]: the same N * K elements)
   const long long mn = (long long)M * N;
   if (splits <= 0) splits = 1;
   hc::span(A, (long long)M * K * 2, "splitk A");

@@ -251,18 +251,15 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] *= alpha;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      const uint32_t kb = drop ? drop_keep_bits<4>(seed, rowidx + k0 + 16 * t + 4 * g, a.drop_threshold) : 0xfu;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float pv = __expf(sc[t][r] - mref);
         l += pv;
-        float pd = pv;
-        if (drop) {
-          const uint32_t key = k0 + 16 * t + 4 * g + r;
-          pd = drop_keep(seed, rowidx + key, a.drop_threshold) ? pv * a.drop_scale : 0.f;
-        }
-        sc[t][r] = pd;
+        sc[t][r] = drop ? ((kb >> r) & 1u ? pv * a.drop_scale : 0.f) : pv;
       }
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const bf16x8 pf = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
@@ -371,16 +368,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
       }
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      const uint32_t kw = drop ? drop_keep_bits<4>(seed, rowidx + k0 + 16 * t + 4 * g, a.drop_threshold) : 0xfu;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int kl = 16 * t + 4 * g + r;
         const float pv = __expf(sc[t][r] * a.scale + kb[kl] - lse);
         float dpv = dp[t][r];
-        if (drop)
-          dpv = drop_keep(seed, rowidx + k0 + kl, a.drop_threshold) ? dpv * a.drop_scale : 0.f;
+        if (drop) dpv = (kw >> r) & 1u ? dpv * a.drop_scale : 0.f;
         sc[t][r] = pv * (dpv - dl);  // dS
       }
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const bf16x8 df = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
@@ -627,17 +625,13 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       if (!((live >> (4 * kt + t)) & 1u)) continue;  // stays 0: exp(-inf) = 0, nothing to hash
+      const uint32_t kb = drop ? drop_keep_bits<4>(seed, rowidx + 64 * kt + 16 * t + 4 * g, a.drop_threshold) : 0xfu;
+      if (drop) kw[kt] |= kb << (4 * t);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float pv = __expf(sc[kt][t][r] - mref);
         l += pv;
-        float pd = pv;
-        if (drop) {
-          const bool keep = drop_keep(seed, rowidx + 64 * kt + 16 * t + 4 * g + r, a.drop_threshold);
-          pd = keep ? pv * a.drop_scale : 0.f;
-          kw[kt] |= (uint32_t)keep << (4 * t + r);
-        }
-        sc[kt][t][r] = pd;
+        sc[kt][t][r] = drop ? ((kb >> r) & 1u ? pv * a.drop_scale : 0.f) : pv;
       }
     }
   // ---- P . V over every live 32-key half
@@ -790,17 +784,16 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if (!tv[t]) continue;  // sc[t] = 0 = dS of a fully masked sub-tile
+        const uint32_t kw = !drop ? 0xfu
+                            : mk  ? (mrow >> (4 * t)) & 0xfu
+                                  : drop_keep_bits<4>(seed, rowidx + kt * 64 + 16 * t + 4 * g, a.drop_threshold);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int kl = 16 * t + 4 * g + r;
           const float bias = varlen ? (kt * 64 + kl < len ? 0.f : -INFINITY) : kb[kt * 64 + kl];
           const float pv = __expf(sc[t][r] * a.scale + bias - lse);
           float dpv = dp[t][r];
-          if (drop) {
-            const bool keep = mk ? ((mrow >> (4 * t + r)) & 1u) != 0
-                                 : drop_keep(seed, rowidx + kt * 64 + kl, a.drop_threshold);
-            dpv = keep ? dpv * a.drop_scale : 0.f;
-          }
+          if (drop) dpv = (kw >> r) & 1u ? dpv * a.drop_scale : 0.f;
           sc[t][r] = pv * (dpv - dl);  // dS
         }
       }

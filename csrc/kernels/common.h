@@ -8,7 +8,7 @@
 //      B frag, lane l: B[k = 8*(l>>4) + j][col = l&15]
 //      C/D,   lane l: D[row = 4*(l>>4) + r][col = l&15], r = 0..3
 //  * Dropout masks come from a stateless counter hash (`drop_keep`) of
-//    (seed, element index) so the backward pass regenerates them instead of
+//    (seed, element index / 2) so the backward pass regenerates them instead of
 //    storing them; the same hash is reproduced in torch for the CPU reference.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -59,9 +59,26 @@ DEV uint32_t hash32(uint32_t seed, uint32_t idx) {
   x ^= x >> 16;
   return x;
 }
-// keep iff hash >= threshold, threshold = round(p * 2^32) (0 => always keep).
+// One hash serves an element pair: element idx keeps iff its 16-bit half of
+// hash32(seed, idx >> 1) (low half: even idx, high half: odd) >= threshold, threshold =
+// round(p * 2^16) (0 => always keep).  Half the integer multiplies of a hash per element --
+// the attention forward's softmax phase and the LN epilogues are VALU-bound on them.
 DEV bool drop_keep(uint32_t seed, uint32_t idx, uint32_t threshold) {
-  return hash32(seed, idx) >= threshold;
+  const uint32_t h = hash32(seed, idx >> 1);
+  return ((idx & 1u) ? (h >> 16) : (h & 0xffffu)) >= threshold;
+}
+// Keep bits (bit e) of the NE elements idx0 .. idx0 + NE - 1; idx0 even, NE even: NE / 2 hashes.
+template <int NE>
+DEV uint32_t drop_keep_bits(uint32_t seed, uint32_t idx0, uint32_t threshold) {
+  static_assert(NE % 2 == 0 && NE <= 32, "element pairs");
+  uint32_t bits = 0u;
+#pragma unroll
+  for (int e = 0; e < NE; e += 2) {
+    const uint32_t h = hash32(seed, (idx0 >> 1) + (uint32_t)(e >> 1));
+    bits |= ((h & 0xffffu) >= threshold ? 1u : 0u) << e;
+    bits |= ((h >> 16) >= threshold ? 1u : 0u) << (e + 1);
+  }
+  return bits;
 }
 
 // Exact-erf GELU (HF DistilBERT's activation) evaluated with Abramowitz-Stegun

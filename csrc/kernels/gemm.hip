@@ -61,7 +61,8 @@ struct GemmParams {
   int k_split;           // K elements per split (multiple of 64)
   long long slab_stride; // elements between fp32 slabs
   int group_m;           // tile-walk group height (L2 working-set control)
-  int diag;              // FD_GEMM_DIAG bits (profiling only): 1 no in-loop DMA, 4 no stores
+  int diag;              // FD_GEMM_DIAG bits (profiling only): 1 no in-loop DMA, 4 no stores,
+                         // 128 LN epilogue operands loaded after the K loop (no ln_dma A/B)
   // EPI_F32 destinations (weight gradients).  out == nullptr: slab mode (slab z of C, reduced
   // by splitk_reduce_kernel).  Otherwise one K split: the tile goes straight to the final [M][N]
   // fp32 gradient out (+= out if accumulate).
@@ -542,7 +543,7 @@ struct LnPre {
   uint4 res_v[IT], z_v[IT];
   float mrow[IT], rrow[IT];
   int hrow_v[IT];
-  float g[8];
+  float g[8], bt[8];  // gamma / beta (forward) of this thread's 8 columns
   uint32_t tag;
 };
 
@@ -566,6 +567,74 @@ DEV LnPre<BM * (BN / 8) / NT> ln_prefetch(const GemmParams& p, int tm, int tn, i
     pre.hrow_v[it] = (L.thr && L.row_map) ? L.row_map[mc] : mc;
   }
   load8f(L.gamma + n, pre.g);
+  if constexpr (!BWD) load8f(L.beta + n, pre.bt);
+  return pre;
+}
+
+// The same operands LDS-DMA'd by the LDS-DMA kernels into the two ring slots their last K-tile
+// pair leaves free (gemm_tile_at, EPI_LN / EPI_LN_BWD, S >= 6): the loads land under that pair's
+// MFMAs instead of stalling the epilogue (round 3 stamps: 2-4 us of epilogue before the
+// rendezvous, mostly this latency).  Region layout (dst): [0, 16 K) the residual tile, [16 K, 32 K)
+// z (backward), then 1 KiB pieces: gamma | beta, mean | rstd (backward), the dropout-hash rows.
+// Rows past M re-read row M - 1 (never stored); per-row scalars need M % 4 == 0 (caller).  Each
+// wave issues ln_dma_ops() DMAs (vmcnt is per wave).
+constexpr int LN_DMA_MISC = 32768;
+DEV bool ln_dma_rowmap(const FdLnEpi& L) { return L.thr != 0 && L.row_map != nullptr; }
+
+template <bool BWD>
+DEV int ln_dma_ops(const FdLnEpi& L, int wid, int ppw) {
+  return ppw * (BWD ? 2 : 1) + (wid == 0) + (BWD && wid == 1) + (wid == 2 && ln_dma_rowmap(L));
+}
+
+template <int BM, int BN, bool BWD, int NW>
+DEV void ln_dma(const GemmParams& p, int tm, int tn, char* dst, int wid, int lane) {
+  constexpr int PIECES = BM * BN * 2 / 1024, PPW = PIECES / NW;
+  static_assert(BN * 2 == 128 && PIECES % NW == 0, "ln prefetch tile");
+  const FdLnEpi& L = p.ln;
+  const int m0 = tm * BM, n0 = tn * BN;
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int piece = wid * PPW + i;
+    const int mc = min(m0 + piece * 8 + (lane >> 3), p.M - 1), c = lane & 7;
+    glds16(p.res + (size_t)mc * p.ldres + n0 + c * 8, dst + piece * 1024);
+    if constexpr (BWD) glds16(L.z + (size_t)mc * p.N + n0 + c * 8, dst + 16384 + piece * 1024);
+  }
+  char* misc = dst + LN_DMA_MISC;
+  if (wid == 0) {  // lanes 0-15 gamma, 16-31 beta (forward)
+    if (lane < 16) glds16(L.gamma + n0 + 4 * lane, misc);
+    else if (!BWD && lane < 32) glds16(L.beta + n0 + 4 * (lane - 16), misc);
+  }
+  if (BWD && wid == 1) {  // lanes 0-31 mean, 32-63 rstd: 4 rows per lane
+    const int r = m0 + 4 * (lane & 31);
+    if (r < p.M) glds16((lane < 32 ? L.mean : L.rstd) + r, misc + 1024);
+  }
+  if (wid == 2 && ln_dma_rowmap(L)) {
+    const int r = m0 + 4 * lane;
+    if (lane < BM / 4 && r < p.M) glds16(L.row_map + r, misc + 2048);
+  }
+}
+
+template <int BM, int BN, bool BWD, int NT>
+DEV LnPre<BM * (BN / 8) / NT> ln_from_lds(const GemmParams& p, int tm, int tn, int tid, const char* src) {
+  constexpr int CPR = BN / 8, IT = BM * CPR / NT;
+  const FdLnEpi& L = p.ln;
+  const int m0 = tm * BM, cc = tid % CPR;
+  const char* misc = src + LN_DMA_MISC;
+  LnPre<IT> pre;
+  pre.tag = (uint32_t)__hip_atomic_load(L.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * FD_LN_XSITES + L.xsite + 1u;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int r = (tid + it * NT) / CPR;
+    pre.res_v[it] = *reinterpret_cast<const uint4*>(src + r * 128 + cc * 16);
+    if constexpr (BWD) {
+      pre.z_v[it] = *reinterpret_cast<const uint4*>(src + 16384 + r * 128 + cc * 16);
+      pre.mrow[it] = reinterpret_cast<const float*>(misc + 1024)[r];
+      pre.rrow[it] = reinterpret_cast<const float*>(misc + 1536)[r];
+    }
+    pre.hrow_v[it] = ln_dma_rowmap(L) ? reinterpret_cast<const int*>(misc + 2048)[r] : min(m0 + r, p.M - 1);
+  }
+  load8f(reinterpret_cast<const float*>(misc) + 8 * cc, pre.g);
+  if constexpr (!BWD) load8f(reinterpret_cast<const float*>(misc + 256) + 8 * cc, pre.bt);
   return pre;
 }
 
@@ -619,9 +688,9 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
     if constexpr (!BWD) {
       if (drop) {
         const size_t hrow = (size_t)(unsigned)hrow_v[it];
+        const uint32_t kb = drop_keep_bits<8>(seed, (uint32_t)(hrow * N + n), L.thr);
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          v[e] = drop_keep(seed, (uint32_t)(hrow * N + n + e), L.thr) ? v[e] * L.dscale : 0.f;
+        for (int e = 0; e < 8; ++e) v[e] = (kb >> e) & 1u ? v[e] * L.dscale : 0.f;
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += rr[e];
@@ -727,8 +796,7 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
     }
   }
   FD_STAMP(4);
-  float bt[8];
-  if constexpr (!BWD) load8f(L.beta + n, bt);
+  const float* bt = pre.bt;
   float cd[8] = {};  // backward: dbias partials
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
@@ -762,10 +830,11 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
       const float s1 = row_sum<CPR>(a) / N, s2 = row_sum<CPR>(b) / N;
       float dz[8], dx[8];
       const size_t hrow = (size_t)(unsigned)hrow_v[it];
+      const uint32_t kb = drop ? drop_keep_bits<8>(seed, (uint32_t)(hrow * N + n), L.thr) : 0xffu;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         dz[e] = rrow[it] * (zv[it][e] - s1 - xv[it][e] * s2);
-        dx[e] = drop ? (drop_keep(seed, (uint32_t)(hrow * N + n + e), L.thr) ? dz[e] * L.dscale : 0.f) : dz[e];
+        dx[e] = drop ? ((kb >> e) & 1u ? dz[e] * L.dscale : 0.f) : dz[e];
       }
       if (m < p.M) {
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + off) = pack8bf(dz);
@@ -804,6 +873,20 @@ DEV void sched_ktile() {
 template <int N>
 DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Runtime count of ops allowed in flight (vmcnt needs an immediate): 0 .. 7.
+DEV void wait_ops(int n) {
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<1>(); break;
+    case 2: wait_vm<2>(); break;
+    case 3: wait_vm<3>(); break;
+    case 4: wait_vm<4>(); break;
+    case 5: wait_vm<5>(); break;
+    case 6: wait_vm<6>(); break;
+    default: wait_vm<7>(); break;
+  }
 }
 
 // Counted wait for "all but the youngest n*L LDS-DMA ops" (n = tiles still allowed in flight).
@@ -852,6 +935,7 @@ struct GemmGroup {
 // One output tile (tm, tn) of problem p: the K loop over the LDS-DMA ring, then the epilogue.
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
 DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
+  const int tm_ = tm, tn_ = tn;
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
   using OA = typename G::OA;
   using OB = typename G::OB;
@@ -906,6 +990,12 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
     if constexpr (!SCHED) __builtin_amdgcn_s_setprio(0);
   };
 
+  // LayerNorm epilogue operands LDS-DMA'd under the last two K-tile pairs (ln_dma): S >= 6 rings
+  // whose K tiles are a whole number of rings, so the pair before last frees slots 0 and 1
+  constexpr bool LNPF = EpiTraits<EPI, BM, BN>::LN && S >= 6 && BN == 64 && (BM * BN * 2 / 1024) % NW == 0 &&
+                        2 * BUF >= LN_DMA_MISC + 3072;
+  const bool lnpf = LNPF && nk % S == 0 && nk >= S && p.M % 4 == 0 && !(p.diag & (1 | 128));
+  int e_ops = 0;  // this wave's epilogue DMAs in flight (younger than every ring tile)
   if constexpr (S < 6) {
 #pragma unroll
     for (int t = 0; t < S - 1; ++t)
@@ -934,13 +1024,23 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
     for (int kt = 0; kt < nk; kt += 2) {
       const int issued = min(nk, S - 2 + kt);
       const int need = min(kt + 2, nk);
-      wait_tiles<L, S - 4>(min(S - 4, max(0, issued - need)));
+      if (LNPF && lnpf && kt == nk - 2) {
+        wait_ops(e_ops);  // the last pair's tiles; only the epilogue DMAs stay in flight
+      } else {
+        wait_tiles<L, S - 4>(min(S - 4, max(0, issued - need)));
+      }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (FD_GEMM_STAMPS && kt == 0) FD_STAMP(1);
       if (!(p.diag & 1)) {
         if (kt + S - 2 < nk) issue(kt + S - 2);  // slot of tile kt-2
         if (kt + S - 1 < nk) issue(kt + S - 1);  // slot of tile kt-1
+      }
+      if constexpr (LNPF) {
+        if (lnpf && kt == nk - 4) {  // slots 0 / 1 (tiles nk - 6, nk - 5) were read last pair; no refill
+          ln_dma<BM, BN, EPI == EPI_LN_BWD, NW>(p, tm_, tn_, smem, wid, lane);
+          e_ops = ln_dma_ops<EPI == EPI_LN_BWD>(p.ln, wid, (BM * BN * 2 / 1024) / NW);
+        }
       }
       read_frags(smem + (kt % S) * BUF);
       mfmas();
@@ -977,9 +1077,17 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
       f32_epilogue<TM, BN, 64 * NW>(p, smem, LDC, m0 + band * TM, n0, tid);
     }
   } else if constexpr (EpiTraits<EPI, BM, BN>::LN) {
-    const auto pre = ln_prefetch<BM, BN, EPI == EPI_LN_BWD, 64 * NW>(p, tm, tn, tid);
-    __syncthreads();  // no wave still reads a ring slot
-    ln_epilogue<BM, BN, TM, TN, EPI == EPI_LN_BWD, 64 * NW>(p, acc, smem, tm, tn, wr, wc, lane, tid, pre);
+    if (LNPF && lnpf) {
+      wait_vm<0>();     // this wave's epilogue DMAs have landed ...
+      __syncthreads();  // ... and every wave's; no wave still reads a ring slot
+      const auto pre = ln_from_lds<BM, BN, EPI == EPI_LN_BWD, 64 * NW>(p, tm, tn, tid, smem);
+      // (the tile is parked behind the prefetched operands: slots 2.. of the ring)
+      ln_epilogue<BM, BN, TM, TN, EPI == EPI_LN_BWD, 64 * NW>(p, acc, smem + 2 * BUF, tm, tn, wr, wc, lane, tid, pre);
+    } else {
+      const auto pre = ln_prefetch<BM, BN, EPI == EPI_LN_BWD, 64 * NW>(p, tm, tn, tid);
+      __syncthreads();  // no wave still reads a ring slot
+      ln_epilogue<BM, BN, TM, TN, EPI == EPI_LN_BWD, 64 * NW>(p, acc, smem, tm, tn, wr, wc, lane, tid, pre);
+    }
   } else {
     // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
     // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
@@ -1437,8 +1545,14 @@ int pick_cfg(int kind, int M, int N, int K) {
     if (cfg_instantiated(narrow) && N < 1536 && M >= 1024 && M <= 4096) return narrow;
     return K >= 2048 ? 0 : 8;
   }
-  if (kind == 1) {  // NN dX
-    if (N % 192 == 0 && N >= 3072 && M >= 2048) return 3;
+  if (kind == 1) {  // NN dX (on the weight W itself: MN-major B through the transposing LDS reads)
+    // the NT rules above, measured equal per configuration (round 4, scripts/da_bench.py
+    // DX_LAYOUTS: the LayerNorm-fused dX reads W as fast as W^T on cfg 24)
+    if (N % 192 == 0 && N >= 3072 && M >= 3584) return 3;
+    if (N % 128 == 0 && N >= 3072 && M >= 2048) return 1;
+    if (N % 192 == 0 && N >= 1536 && M >= 2048) return 6;
+    static const int narrow = [] { const char* e = getenv("FD_GEMM_NARROW_CFG"); return e ? atoi(e) : 24; }();
+    if (cfg_instantiated(narrow) && N < 1536 && M >= 1024 && M <= 4096) return narrow;
     return 8;
   }
   return (N % 128 == 0 && M > 1024 && M < 3072 && N < 3072) ? 1 : 8;  // TN dW
@@ -1643,10 +1757,7 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
   if (colsum) {
     // only the staged-fp32 epilogues sum columns: 128 x {128, 64} tiles (never 256-row ones)
     if (epi != EPI_GELU_BWD && epi != EPI_ADD) return 2;
-    if (kind != 0) {  // (NN: the direct-A kernels only) launch nothing: plain GEMM + column-sum pass
-      if (colsum_blocks) *colsum_blocks = 0;
-      return kind == 1 ? 0 : 2;
-    }
+    if (kind != 0 && kind != 1) return 2;
     if (CFGS[id].bm != 128 && cfg_override(kind) < 0) id = 8;  // (small-M 64-row tiles: 128 x 64)
     if (CFGS[id].bm != 128 || (CFGS[id].bn != 128 && CFGS[id].bn != 64) || N % CFGS[id].bn) {
       // the shape's tile has no staged-fp32 epilogue (e.g. 256 x 192 at M >= 3.5 k): launch
@@ -1657,6 +1768,7 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
     p.colsum = colsum;
     if (colsum_blocks) *colsum_blocks = (M + CFGS[id].bm - 1) / CFGS[id].bm;
   }
+  // (NN launches fall back to cfg 8 below when the picked tile does not fit; that keeps 128 x 64)
   if (kind == 0) {  // also dX = dy (W^T)^T with a transposed weight copy: GELU' / residual epilogues
     if (epi == EPI_F32) return 2;
     if (da >= 0 && !colsum && launch_da(epi, p, da, true, st)) return 0;
@@ -1693,7 +1805,8 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
 // splits <= 0: picked here (largest divisor of K / 64 that keeps >= 2 K tiles per block and the
 // grid within one round of 256 blocks); returns the split count used, or a negative error.
 int fd_gemm_f32_splits(const void* A, const void* Bt, float* slabs, long long slab_elems, int M, int N, int K,
-                       int lda, int ldb, int splits, hipStream_t st) {
+                       int lda, int ldb, int splits, int b_mn, hipStream_t st) {
+  // b_mn: Bt is the weight W [K][N] itself (MN-major B, ldb = its row pitch)
   if (M <= 0 || K % BKT || N % 64 || !A || !Bt || !slabs) return -1;
   const int id = M <= 64 ? 13 : 8;
   const long long tiles = tiles_of(id, M, N);
@@ -1710,6 +1823,7 @@ int fd_gemm_f32_splits(const void* A, const void* Bt, float* slabs, long long sl
   p.k_split = K / splits;
   p.slab_stride = (long long)M * N;
   p.group_m = 1;
+  if (b_mn) return launch_id<true, false, EPI_F32>(p, id, splits, st) ? splits : -3;
   return launch_id<true, true, EPI_F32>(p, id, splits, st) ? splits : -3;
 }
 

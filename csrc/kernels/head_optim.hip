@@ -73,8 +73,9 @@ DEV void head_row(const HeadArgs& a, int b, int lane) {
     const float4 w0 = *reinterpret_cast<const float4*>(a.W + col);
     const float4 w1 = *reinterpret_cast<const float4*>(a.W + a.D + col);
     if (drop) {
+      const uint32_t kb = drop_keep_bits<4>(seed, (uint32_t)(b * a.D + col), a.thr);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = drop_keep(seed, (uint32_t)(b * a.D + col + e), a.thr) ? v[e] * a.dscale : 0.f;
+      for (int e = 0; e < 4; ++e) v[e] = (kb >> e) & 1u ? v[e] * a.dscale : 0.f;
     }
     z0 += v[0] * w0.x + v[1] * w0.y + v[2] * w0.z + v[3] * w0.w;
     z1 += v[0] * w1.x + v[1] * w1.y + v[2] * w1.z + v[3] * w1.w;

@@ -78,9 +78,10 @@ DEV void ln_load_sum(const LnArgs& a, int row, int hl, bool drop, uint32_t seed,
     const size_t off = hrow * a.D + 8 * (hl + HL * c);
     unpack8(xv[c], z[c]);
     if (drop) {
+      const uint32_t kb = drop_keep_bits<8>(seed, (uint32_t)off, a.thr);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const bool k = drop_keep(seed, (uint32_t)(off + e), a.thr);
+        const bool k = (kb >> e) & 1u;
         if (!a.zin) z[c][e] = k ? z[c][e] * a.dscale : 0.f;
         if (!k) keep &= ~(1u << (8 * c + e));
       }
@@ -394,9 +395,9 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbArgs a) {
     float y[4] = {(z[c][0] - mean) * rstd * g.x + b.x, (z[c][1] - mean) * rstd * g.y + b.y,
                   (z[c][2] - mean) * rstd * g.z + b.z, (z[c][3] - mean) * rstd * g.w + b.w};
     if (drop) {
-      const size_t hoff = (size_t)prow * D + col;
+      const uint32_t kb = drop_keep_bits<4>(seed, (uint32_t)((size_t)prow * D + col), a.thr);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = drop_keep(seed, (uint32_t)(hoff + e), a.thr) ? y[e] * a.dscale : 0.f;
+      for (int e = 0; e < 4; ++e) y[e] = (kb >> e) & 1u ? y[e] * a.dscale : 0.f;
     }
     *reinterpret_cast<uint2*>(a.y + off) = make_uint2(pack_bf2(y[0], y[1]), pack_bf2(y[2], y[3]));
   }
@@ -429,9 +430,9 @@ __global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
       const uint2 dv = *reinterpret_cast<const uint2*>(a.dy + off);
       float d4[4] = {lo_bf(dv.x), hi_bf(dv.x), lo_bf(dv.y), hi_bf(dv.y)};
       if (drop) {
-        const size_t hoff = (size_t)prow * D + col;
+        const uint32_t kb = drop_keep_bits<4>(seed, (uint32_t)((size_t)prow * D + col), a.thr);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) d4[e] = drop_keep(seed, (uint32_t)(hoff + e), a.thr) ? d4[e] * a.dscale : 0.f;
+        for (int e = 0; e < 4; ++e) d4[e] = (kb >> e) & 1u ? d4[e] * a.dscale : 0.f;
       }
       const float4 g = *reinterpret_cast<const float4*>(a.gamma + col);
       const float g4[4] = {g.x, g.y, g.z, g.w};

@@ -171,10 +171,11 @@ __global__ __launch_bounds__(256) void sk_ln_kernel(SkArgs a) {
     if (act) {
       const float4 b0 = *reinterpret_cast<const float4*>(a.bias + n), b1 = *reinterpret_cast<const float4*>(a.bias + n + 4);
       const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      const uint32_t kb = drop ? drop_keep_bits<8>(seed, (uint32_t)(hrow * N + n), L.thr) : 0xffu;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float x = v[e] + b[e];
-        if (drop) x = drop_keep(seed, (uint32_t)(hrow * N + n + e), L.thr) ? x * L.dscale : 0.f;
+        if (drop) x = (kb >> e) & 1u ? x * L.dscale : 0.f;
         v[e] = x + r[e];
       }
       const uint4 zb = pack8bf(v);
@@ -223,10 +224,11 @@ __global__ __launch_bounds__(256) void sk_ln_kernel(SkArgs a) {
     s2 = block_sum4(s2, lds) / N;
     if (act) {
       float dz[8], dx[8];
+      const uint32_t kb = drop ? drop_keep_bits<8>(seed, (uint32_t)(hrow * N + n), L.thr) : 0xffu;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         dz[e] = rstd * (gd[e] - s1 - xh[e] * s2);
-        dx[e] = drop ? (drop_keep(seed, (uint32_t)(hrow * N + n + e), L.thr) ? dz[e] * L.dscale : 0.f) : dz[e];
+        dx[e] = drop ? ((kb >> e) & 1u ? dz[e] * L.dscale : 0.f) : dz[e];
       }
       *reinterpret_cast<uint4*>(a.C + i) = pack8bf(dz);
       if (drop && L.dx) *reinterpret_cast<uint4*>(L.dx + i) = pack8bf(dx);
@@ -301,14 +303,15 @@ int fd_splitk_epilogue(int epi, const float* slabs, long long sstride, int split
 
 extern "C" {
 int fd_gemm_f32_splits(const void* A, const void* Bt, float* slabs, long long slab_elems, int M, int N, int K,
-                       int lda, int ldb, int splits, hipStream_t st);
+                       int lda, int ldb, int splits, int b_mn, hipStream_t st);
 
 // Split-K NT GEMM with a fused epilogue: C = epi(A Bt^T) via fp32 slabs (workspace, >= splits x
 // M x N floats; splits <= 0: auto).  Two launches.  Returns the split count, or a negative code.
+// b_mn: Bt is the weight W [K][N] itself (C = epi(A W)), read MN-major.
 int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, float* workspace,
                    long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
-                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, hipStream_t st) {
-  const int s = fd_gemm_f32_splits(A, Bt, workspace, workspace_elems, M, N, K, K, K, splits, st);
+                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, int b_mn, hipStream_t st) {
+  const int s = fd_gemm_f32_splits(A, Bt, workspace, workspace_elems, M, N, K, K, b_mn ? N : K, splits, b_mn, st);
   if (s <= 0) return s == 0 ? -9 : s;
   const int rc = fd_splitk_epilogue(epi, workspace, (long long)M * N, s, M, N, bias, C, aux, aux_out, res, colsum,
                                     colsum_blocks, ln, st);

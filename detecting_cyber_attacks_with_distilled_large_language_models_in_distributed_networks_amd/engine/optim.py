@@ -136,8 +136,11 @@ class ArenaAdam:
     def can_fuse(self) -> bool:
         """Whether the model's weight-gradient GEMMs may apply this optimizer's step."""
         m = self.model
+        # the fused step updates weights inside the backward: safe when the dX GEMMs read W^T copies
+        # taken before it, or when every weight gradient runs in the all-layer launch at the end
         return (self.fuse_dw and not self.overlap and self.arena.device.type == "cuda"
-                and getattr(m, "impl", "") == "hip" and getattr(m, "transposed_dx", False)
+                and getattr(m, "impl", "") == "hip"
+                and (getattr(m, "transposed_dx", False) or getattr(m, "batch_dw", False))
                 and getattr(m, "group_dw", False) and getattr(m, "layer_grads_hook", None) is None
                 and self.arena.shadow is not None)
 

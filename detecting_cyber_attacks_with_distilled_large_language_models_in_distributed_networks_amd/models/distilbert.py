@@ -251,7 +251,7 @@ class DDoSClassifier(nn.Module):
         self.layer_grads_hook = None
         # HIP path: backward dX GEMMs read W^T copies (K-major staging is ~30% faster than
         # reading W MN-major; the per-step transpose of the encoder weights is ~85 MB r+w)
-        self.transposed_dx = True
+        self.transposed_dx = os.environ.get("FD_TRANSPOSED_DX", "0") == "1"
         # (Removed after losing their A/B, logs in profiles/: the weight-gradient GEMMs on a side
         # stream -- 3.24 vs 3.20 ms/step, r1_ab_wgrad_side_stream.txt; the W^T copies on a side
         # stream during the forward -- 2.48 vs 2.36, r1_ab_transpose_overlap_slower.txt; the
@@ -547,8 +547,9 @@ class DDoSClassifier(nn.Module):
         # sets collectives_in_backward): no LayerNorm-fused backward GEMM beside RCCL's kernels
         rc.fuse_ln_bwd = rc.fuse_ln and K.ln_fusable(
             1, cfg.dim, concurrent_collectives=bool(grad and getattr(self, "collectives_in_backward", False)))
-        if (grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None
-                and self.transposed_dx):
+        if grad and self.training and self.fused_opt is not None and self.layer_grads_hook is None:
+            # (the per-layer grouped dW path applies it only where the dX GEMMs read W^T copies taken
+            # before the step; the all-layer dW launch runs after every dX GEMM of the backward)
             rc.fused_adam = self.fused_opt
         plan = self._prune_plan(rc, layers, grad)
         # packed step: the counters ride on the packing launch (no kernel of their own)
@@ -601,7 +602,7 @@ class DDoSClassifier(nn.Module):
         Bp = (B + 63) // 64 * 64
         if not (self.prune_last and rc.fuse_ln and layers and K.ln_fusable(Bp, D) and Bp <= rc.B * rc.S):
             return None
-        if grad and (rc.dw_batch is None or "wT" not in layers[-1]):
+        if grad and rc.dw_batch is None:
             return None
         dev = self.arena.device
         key = (B, S, Bp, str(dev))

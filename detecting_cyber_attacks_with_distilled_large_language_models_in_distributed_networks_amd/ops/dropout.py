@@ -2,9 +2,11 @@
 
 The reference uses ATen's Philox dropout at 14 sites (hidden/attention p=0.1,
 classifier p=0.3; client1.py:57,63 and HF DistilBERT).  Our kernels instead
-derive every keep bit from ``hash32(site_seed, element_index)`` so the backward
-regenerates masks instead of storing them, and the torch reference path (CPU)
-produces the *same* masks for parity tests.
+derive every keep bit from ``hash32(site_seed, element_index >> 1)`` -- one hash per
+even/odd element pair, each element comparing its own 16-bit half (low: even, high:
+odd) against ``threshold(p) = round(p * 2^16)`` -- so the backward regenerates masks
+instead of storing them, and the torch reference path (CPU) produces the *same* masks
+for parity tests.
 
 site_seed = hash32(counter, site) where ``counter`` is a device int32 that the
 train step increments (graph-replay safe) and ``site`` identifies the dropout
@@ -50,10 +52,17 @@ def hash32(seed: int, idx: int) -> int:
 
 
 def threshold(p: float) -> int:
-    """Keep iff hash >= threshold; p=0 -> 0 (always keep)."""
+    """Keep iff the element's 16-bit hash half >= threshold; p=0 -> 0 (always keep)."""
     if p <= 0.0:
         return 0
-    return min(int(round(p * 4294967296.0)), M32)
+    return min(int(round(p * 65536.0)), 0xFFFF)
+
+
+def keep_t(seed, idx: torch.Tensor, thr: int) -> torch.Tensor:
+    """Keep bits of int64 element indices ``idx`` (common.h drop_keep)."""
+    h = hash32_t(seed, idx >> 1)
+    half = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
+    return half >= thr
 
 
 def site_seed(counter: int, site: int) -> int:
@@ -67,7 +76,7 @@ def keep_mask(counter: int, site: int, numel: int, p: float, device=None, offset
         return torch.ones(numel, dtype=torch.bool, device=device)
     s = site_seed(counter, site)
     idx = torch.arange(offset, offset + numel, dtype=torch.int64, device=device)
-    return hash32_t(s, idx) >= thr
+    return keep_t(s, idx, thr)
 
 
 class Sites:

@@ -170,6 +170,13 @@ class EmbeddingFn(torch.autograd.Function):
             K.colsum_flush(ctx.rc.colsum_jobs)
 
 
+def _wsel(L, wt: dict, k: str):
+    """(B operand, b_mn) of a dX GEMM on weight ``k``: its W^T copy when the model keeps one
+    (K-major B), else the weight itself (MN-major B; the default, models/distilbert.py transposed_dx)."""
+    t = wt.get(k)
+    return (t, False) if t is not None else (L[k], True)
+
+
 class LayerFn(torch.autograd.Function):
     """One post-LN TransformerBlock: 7 kernels forward, 13 backward."""
 
@@ -251,27 +258,29 @@ class LayerFn(torch.autograd.Function):
         acc = G["l2_w"].accumulate()
         jobs = rc.colsum_jobs
         batch = rc.dw_batch
-        wt = L["wT"]
+        wt = L.get("wT") or {}
         ci, rm, B = rc.cls_rows, rc.cls_rmap, rc.B
         dz2, df = K.ln_bwd(dy, f, None, L["ln2_w"], m2, r2, G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, rc.seed,
                            ffn_site, p_h, acc, rm, jobs, zin=True)
         g_out = torch.empty_like(u) if g is None else None
         fuse_cs = jobs is not None and rc.fuse_colsum
-        du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt["l2_w"], colsum=(jobs, G["l1_b"].buf, acc) if fuse_cs else None,
-                         aux_out=g_out)
+        du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"),
+                         colsum=(jobs, G["l1_b"].buf, acc) if fuse_cs else None, aux_out=g_out)
         if not fuse_cs:
             K.colsum(du, G["l1_b"].buf, acc, jobs)
         if g is None:
             g = g_out
-        batch += [(df, g, G["l2_w"].buf, acc, wt["l2_w"]), (du, h, G["l1_w"].buf, acc, wt["l1_w"])]
-        dz1c, _ = K.linear_dx_ln_bwd(du, wt["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
-                                     G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, xsite=K.ln_xsite(ctx.idx, 0, True))
-        dcxc = K.linear_dx(dz1c, L["o_w"], wt=wt["o_w"])
+        batch += [(df, g, G["l2_w"].buf, acc, wt.get("l2_w")), (du, h, G["l1_w"].buf, acc, wt.get("l1_w"))]
+        b1, mn1 = _wsel(L, wt, "l1_w")
+        dz1c, _ = K.linear_dx_ln_bwd(du, b1, dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
+                                     G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, xsite=K.ln_xsite(ctx.idx, 0, True),
+                                     b_mn=mn1)
+        dcxc = K.linear_dx(dz1c, L["o_w"], wt=wt.get("o_w"))
         # the [CLS] rows' gradients back into the full layout (every other row exactly 0)
         dcx, dz1 = K.scatter_rows2(dcxc, dz1c, ci, B, cx.shape[0])
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask,
                           q_live=1)
-        batch += [(dz1c, cxc, G["o_w"].buf, acc, wt["o_w"]), (dqkv, x, G["qkv_w"].buf, acc, wt["qkv_w"])]
+        batch += [(dz1c, cxc, G["o_w"].buf, acc, wt.get("o_w")), (dqkv, x, G["qkv_w"].buf, acc, wt.get("qkv_w"))]
         if rc.colsum_pending is not None:
             rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))
         else:
@@ -283,12 +292,13 @@ class LayerFn(torch.autograd.Function):
             acc_p = [Gp[k].accumulate() for k in ("ln2_w", "ln2_b", "l2_b")]
             if len(set(acc_p)) != 1:
                 raise RuntimeError("output-LN gradient sinks out of step")
-            dx, df_p = K.linear_dx_ln_bwd(dqkv, wt["qkv_w"], dz1, z2p, Lp["ln2_w"], m2p, r2p, Gp["ln2_w"].buf,
+            bq, mnq = _wsel(L, wt, "qkv_w")
+            dx, df_p = K.linear_dx_ln_bwd(dqkv, bq, dz1, z2p, Lp["ln2_w"], m2p, r2p, Gp["ln2_w"].buf,
                                           Gp["ln2_b"].buf, Gp["l2_b"].buf, rc.seed, site_p, p_p, acc_p[0], rc.row_map,
-                                          jobs, xsite=K.ln_xsite(ctx.idx, 1, True))
+                                          jobs, xsite=K.ln_xsite(ctx.idx, 1, True), b_mn=mnq)
             rc.ln2_pending[ctx.idx - 1] = (dx, df_p)
         else:
-            dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt["qkv_w"])
+            dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt.get("qkv_w"))
         for k in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_w", "ln1_b", "l1_w", "l1_b", "l2_b", "ln2_w", "ln2_b"):
             G[k].accumulate()
         del ctx.acts, ctx.dmask
@@ -325,7 +335,7 @@ class LayerFn(torch.autograd.Function):
             fa = None
         # dg W2 * gelu'(u); with deferred column sums the epilogue also leaves lin1's bias-gradient
         # partials (no separate pass over du)
-        fuse_cs = jobs is not None and rc.fuse_colsum and wt.get("l2_w") is not None
+        fuse_cs = jobs is not None and rc.fuse_colsum
         g_out = torch.empty_like(u) if g is None else None  # re-created gelu(u) (RunCtx.remat_gelu)
         du = K.linear_dx(df, L["l2_w"], gelu_u=u, wt=wt.get("l2_w"),
                          colsum=(jobs, G["l1_b"].buf, acc) if fuse_cs else None, aux_out=g_out)
@@ -342,10 +352,11 @@ class LayerFn(torch.autograd.Function):
         if not fuse_cs:
             K.colsum(du, G["l1_b"].buf, acc, jobs)
         # sa_layer_norm(out_lin + x): dh = du W1 + dz2, then its LayerNorm backward
-        if fused_bwd and wt.get("l1_w") is not None:
-            dz1, _ = K.linear_dx_ln_bwd(du, wt["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
+        if fused_bwd:
+            b1, mn1 = _wsel(L, wt, "l1_w")
+            dz1, _ = K.linear_dx_ln_bwd(du, b1, dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
                                         G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs,
-                                        xsite=K.ln_xsite(ctx.idx, 0, True))
+                                        xsite=K.ln_xsite(ctx.idx, 0, True), b_mn=mn1)
         else:
             dh = K.linear_dx(du, L["l1_w"], res=dz2, wt=wt.get("l1_w"))
             dz1, _ = K.ln_bwd(dh, ao, None if fused else x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
@@ -365,7 +376,7 @@ class LayerFn(torch.autograd.Function):
             rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))  # partials at the end, batched
         else:
             K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
-        prev = rc.ln2_saved.get(ctx.idx - 1) if fused_bwd and wt.get("qkv_w") is not None else None
+        prev = rc.ln2_saved.get(ctx.idx - 1) if fused_bwd else None
         if prev is not None:
             # dx = dqkv Wqkv + dz1 is block idx-1's output-LN gradient: finish that LayerNorm
             # backward in this GEMM's epilogue and hand (dz2, df) to block idx-1
@@ -375,9 +386,10 @@ class LayerFn(torch.autograd.Function):
             if len(set(acc_p)) != 1:
                 raise RuntimeError("output-LN gradient sinks out of step")
             acc_p = acc_p[0]
-            dx, df_p = K.linear_dx_ln_bwd(dqkv, wt["qkv_w"], dz1, z2p, Lp["ln2_w"], m2p, r2p, Gp["ln2_w"].buf,
+            bq, mnq = _wsel(L, wt, "qkv_w")
+            dx, df_p = K.linear_dx_ln_bwd(dqkv, bq, dz1, z2p, Lp["ln2_w"], m2p, r2p, Gp["ln2_w"].buf,
                                           Gp["ln2_b"].buf, Gp["l2_b"].buf, rc.seed, site_p, p_p, acc_p, rc.row_map,
-                                          jobs, xsite=K.ln_xsite(ctx.idx, 1, True))
+                                          jobs, xsite=K.ln_xsite(ctx.idx, 1, True), b_mn=mnq)
             rc.ln2_pending[ctx.idx - 1] = (dx, df_p)
         else:
             dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1, wt=wt.get("qkv_w"))

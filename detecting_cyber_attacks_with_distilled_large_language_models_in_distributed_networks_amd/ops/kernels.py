@@ -61,8 +61,9 @@ def _splitk_ok(M: int, N: int, K: int) -> bool:
 
 def _splitk(epi, x, wt, y, **kw):
     """One split-K GEMM + epilogue (``ext().gemm_splitk``) on the shared slab workspace (slabs
-    are consumed by the epilogue launch right behind the GEMM on the same stream)."""
-    M, N = x.shape[0], wt.shape[0]
+    are consumed by the epilogue launch right behind the GEMM on the same stream).  b_mn=True:
+    ``wt`` is the weight W [K, N] itself (y = epi(x W))."""
+    M, N = x.shape[0], (wt.shape[1] if kw.get("b_mn") else wt.shape[0])
     ws = workspace(x.device, "splitk_small", 256 * M * N // max(1, ((M + 63) // 64) * (N // 64)) + M * N)
     return ext().gemm_splitk(epi, x, wt, y, ws, **kw)
 
@@ -91,51 +92,43 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] 
               colsum: Optional[tuple] = None, aux_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx = dy w  [* gelu'(u)]  [+ res]  (bf16).
 
-    With ``wt`` (= w^T, contiguous) the product runs as the K-major "NT" kernel
-    dx = dy (w^T)^T, whose operand staging is faster than the MN-major read of w.
-    colsum = (deferred colsum jobs, out, accumulate): the GEMM epilogue also leaves the
-    column sums of dx per M tile (the producer-bias gradient) as a deferred job, instead
-    of a separate column-sum pass over dx.  aux_out (with gelu_u): the epilogue also writes
-    gelu(gelu_u) there -- the forward's activation, bitwise.  Returns dx."""
+    The product reads the weight ``w`` itself (MN-major B, "NN"), or, with ``wt`` (= w^T,
+    contiguous), a transposed copy (K-major B, "NT").  The two run the same tile configurations
+    (csrc/kernels/gemm.hip pick_cfg) and measured the same, so the model keeps no W^T copies by
+    default (models/distilbert.py transposed_dx).
+    colsum = (deferred colsum jobs, out, accumulate): the GEMM epilogue also leaves the column
+    sums of dx per M tile (the producer-bias gradient) as a deferred job, instead of a separate
+    column-sum pass over dx.  aux_out (with gelu_u): the epilogue also writes gelu(gelu_u) there
+    -- the forward's activation, bitwise.  Returns dx."""
     M, N = dy.shape[0], w.shape[1]
     dx = torch.empty(M, N, dtype=torch.bfloat16, device=dy.device)
-    if wt is not None and _splitk_ok(M, N, dy.shape[1]):
-        epi = EPI_GELU_BWD if gelu_u is not None else (EPI_ADD if res is not None else EPI_BF16)
+    B, bmn = (wt, False) if wt is not None else (w, True)
+    kind = 1 if bmn else 0
+    epi = EPI_GELU_BWD if gelu_u is not None else (EPI_ADD if res is not None else EPI_BF16)
+    ao = aux_out if gelu_u is not None else None
+    if colsum is not None and epi == EPI_BF16:
+        raise ValueError("fused column sums need a GELU' / residual epilogue")
+    if _splitk_ok(M, N, dy.shape[1]):
         if colsum is not None:
-            if epi == EPI_BF16:
-                raise ValueError("fused column sums need a GELU' / residual epilogue")
             jobs, out, acc = colsum
             cs = workspace(dy.device, f"colsum_job{len(jobs)}", ((M + 31) // 32) * N)
-            _, nblk = _splitk(epi, dy, wt, dx, aux=gelu_u, aux_out=aux_out if gelu_u is not None else None, res=res,
-                              colsum=cs)
+            _, nblk = _splitk(epi, dy, B, dx, aux=gelu_u, aux_out=ao, res=res, colsum=cs, b_mn=bmn)
             jobs.append((cs, [out], nblk, N, N, acc))
             return dx
-        _splitk(epi, dy, wt, dx, aux=gelu_u, aux_out=aux_out if gelu_u is not None else None, res=res)
+        _splitk(epi, dy, B, dx, aux=gelu_u, aux_out=ao, res=res, b_mn=bmn)
         return dx
-    if colsum is not None and wt is not None and (gelu_u is not None or res is not None):
+    if colsum is not None:
         jobs, out, acc = colsum
         ws = workspace(dy.device, f"colsum_job{len(jobs)}", ((M + 127) // 128) * N)
-        epi = EPI_GELU_BWD if gelu_u is not None else EPI_ADD
-        nblk = ext().gemm_colsum(epi, dy, wt, dx, gelu_u, res, ws, aux_out)
+        nblk = ext().gemm_colsum(epi, dy, B, dx, gelu_u, res, ws, ao, kind)
         if nblk:
             jobs.append((ws, [out], nblk, N, N, acc))
             return dx
         # this shape's tile has no fused column sums: plain GEMM, then the separate pass
-        ext().gemm(0, epi, dy, wt, dx, None, gelu_u, res, None, False, aux_out)
+        ext().gemm(kind, epi, dy, B, dx, None, gelu_u, res, None, False, ao)
         _colsum_pass(dx, out, acc, jobs)
         return dx
-    if colsum is not None:
-        raise ValueError("fused column sums need the transposed weight and a GELU' / residual epilogue")
-    if wt is not None:
-        epi = EPI_GELU_BWD if gelu_u is not None else (EPI_ADD if res is not None else EPI_BF16)
-        ext().gemm(0, epi, dy, wt, dx, None, gelu_u, res, None, False, aux_out if gelu_u is not None else None)
-        return dx
-    if gelu_u is not None:
-        ext().gemm(1, EPI_GELU_BWD, dy, w, dx, None, gelu_u, None, None, False, aux_out)
-    elif res is not None:
-        ext().gemm(1, EPI_ADD, dy, w, dx, None, None, res, None, False)
-    else:
-        ext().gemm(1, EPI_BF16, dy, w, dx, None, None, None, None, False)
+    ext().gemm(kind, epi, dy, B, dx, None, gelu_u, res, None, False, ao)
     return dx
 
 
@@ -514,12 +507,13 @@ def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, k
 
 
 def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False,
-                     row_map=None, jobs: Optional[list] = None, xsite=None):
+                     row_map=None, jobs: Optional[list] = None, xsite=None, b_mn: bool = False):
     """LayerNorm backward fused into the dX GEMM that produces its output gradient:
     dy = a wt^T + res, then (dz, dx) of y = LN(dropout(f) + r) from the saved z = dropout(f) + r
     (dz: gradient of the pre-LN sum, i.e. of the residual input r; dx: of f, = dz without dropout).
-    dgamma / dbeta / dbias (+)= the column sums (deferred to ``colsum_flush`` with ``jobs``)."""
-    M, N = a.shape[0], wt.shape[0]
+    dgamma / dbeta / dbias (+)= the column sums (deferred to ``colsum_flush`` with ``jobs``).
+    b_mn=True: ``wt`` is the weight W [K, N] itself (dy = a W + res; no W^T copy needed)."""
+    M, N = a.shape[0], (wt.shape[1] if b_mn else wt.shape[0])
     dz = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
     thr, sc = _drop(p)
     dx = torch.empty_like(dz) if thr else None
@@ -527,7 +521,7 @@ def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, see
         key = "ln_colpart" if jobs is None else f"ln_colpart_job{len(jobs)}"
         ws = workspace(a.device, key, M * 3 * N)
         _splitk(EPI_LN_BWD, a, wt, dz, res=res, gamma=gamma, mean=mean, rstd=rstd, z=z, dx=dx, colpart=ws,
-                seed=seed, site=site, thr=thr, dscale=sc, row_map=row_map if thr else None)
+                seed=seed, site=site, thr=thr, dscale=sc, row_map=row_map if thr else None, b_mn=b_mn)
         job = (ws, [dgamma, dbeta, dbias], M, 3 * N, N, accumulate)
         if jobs is not None:
             jobs.append(job)
@@ -539,7 +533,7 @@ def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, see
     stats, cnt, err = _ln_state(a.device, M, N)
     xs = _xsite(a.device, N, xsite)
     nblk = ext().gemm_ln(True, a, wt, dz, None, res, gamma, None, mean, rstd, z, dx, ws, stats, cnt, err, 0.0, seed,
-                         site, thr, sc, row_map if thr else None, LN_CFG, xs)
+                         site, thr, sc, row_map if thr else None, LN_CFG, xs, b_mn)
     job = (ws, [dgamma, dbeta, dbias], nblk, 3 * N, N, accumulate)
     if jobs is not None:
         jobs.append(job)

@@ -49,6 +49,9 @@ def test_fused_adam_training_matches_unfused(graph, nosplit):
     for fuse in (True, False):
         m = DDoSClassifier(config=cfg, device=DEV, impl="hip", seed=13)
         m.batch_dw = False  # per-layer grouped dW launches (batched: test_dw_batch_gpu.py)
+        # (Adam fused into a per-layer dW launch updates weights mid-backward: the later dX GEMMs
+        # must read W^T copies taken before the step)
+        m.transposed_dx = True
         m.train()
         opt = ArenaAdam(m, lr=1e-3, fuse_dw=fuse)
         assert opt.can_fuse() == fuse
@@ -231,7 +234,7 @@ def _wT_equal_shadow_T(m) -> bool:
 
 
 def test_wT_written_by_fused_adam_epilogue(monkeypatch):
-    """Round 4: the fused Adam epilogue of the all-layer weight-gradient launch also writes the
+    """Round 4 (A/B path, FD_TRANSPOSED_DX=1): the fused Adam epilogue of the all-layer weight-gradient launch also writes the
     updated weights' bf16 transpose (the W^T the next backward's dX GEMMs read), so the per-step
     transpose launch is gone.  W^T stays bitwise shadow^T after fused steps and graph replays, and
     every out-of-band weight change (FedAvg, checkpoint load, an unfused optimizer step) re-runs
@@ -239,6 +242,7 @@ def test_wT_written_by_fused_adam_epilogue(monkeypatch):
     from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.parallel.fedavg import (
         fedavg_)
     m = DDoSClassifier(config=DistilBertConfig(n_layers=2), device=DEV, impl="hip", seed=3)
+    m.transposed_dx = True  # (FD_TRANSPOSED_DX=1: the dX GEMMs read W^T copies; default: W itself)
     m.train()
     opt = ArenaAdam(m, lr=1e-3)
     fn = make_step_fn(m, opt)

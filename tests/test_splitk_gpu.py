@@ -96,7 +96,7 @@ def test_splitk_ln_forward_matches_fused_and_reference(p, rowmap):
     hrow = rm.long() if rm is not None else torch.arange(M, device=DEV)
     if p:
         idx = hrow[:, None] * D + torch.arange(D, device=DEV)[None]
-        keep = (DR.hash32_t(DR.site_seed(int(seed.item()), 9), idx) >= DR.threshold(p)).float()
+        keep = DR.keep_t(DR.site_seed(int(seed.item()), 9), idx, DR.threshold(p)).float()
     zr = (f * keep / (1 - p) if p else f) + res.float()
     zr_b = zr.to(torch.bfloat16).float()
     yr = torch.nn.functional.layer_norm(zr_b, (D,), gamma, beta, 1e-12)
