@@ -252,12 +252,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     for (int i = 0; i < 4; ++i) o[i] *= alpha;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const uint32_t kb = drop ? drop_keep_bits<4>(seed, rowidx + k0 + 16 * t + 4 * g, a.drop_threshold) : 0xfu;
+      const uint32_t kbits = drop ? drop_keep_bits<4>(seed, rowidx + k0 + 16 * t + 4 * g, a.drop_threshold) : 0xfu;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float pv = __expf(sc[t][r] - mref);
         l += pv;
-        sc[t][r] = drop ? ((kb >> r) & 1u ? pv * a.drop_scale : 0.f) : pv;
+        sc[t][r] = drop ? ((kbits >> r) & 1u ? pv * a.drop_scale : 0.f) : pv;
       }
     }
 #pragma unroll
@@ -567,7 +567,8 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   for (int s2 = 0; s2 < 2; ++s2) qf[s2] = load_frag_global(a.qkv + (tok0 + qr) * ld3 + h * DH + 32 * s2 + 8 * g);
   stage_rows(ks, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
   stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
-  if (!varlen && tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) : -INFINITY;
+  // (the softmax runs in log2 units: scores and key biases pre-scaled by log2(e), v_exp_f32 direct)
+  if (!varlen && tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) * LOG2E : -INFINITY;
   __syncthreads();
   ASTAMP(1);
   const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows needed
@@ -601,6 +602,7 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
     }
   }
   float mx = -INFINITY;
+  const float scale2 = a.scale * LOG2E;
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -610,7 +612,7 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int k = 64 * kt + 16 * t + 4 * g + r;
         const float bias = varlen ? (k < len ? 0.f : -INFINITY) : kb[k];
-        sc[kt][t][r] = sc[kt][t][r] * a.scale + bias;
+        sc[kt][t][r] = sc[kt][t][r] * scale2 + bias;
         mx = fmaxf(mx, sc[kt][t][r]);
       }
     }
@@ -625,13 +627,13 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       if (!((live >> (4 * kt + t)) & 1u)) continue;  // stays 0: exp(-inf) = 0, nothing to hash
-      const uint32_t kb = drop ? drop_keep_bits<4>(seed, rowidx + 64 * kt + 16 * t + 4 * g, a.drop_threshold) : 0xfu;
-      if (drop) kw[kt] |= kb << (4 * t);
+      const uint32_t kbits = drop ? drop_keep_bits<4>(seed, rowidx + 64 * kt + 16 * t + 4 * g, a.drop_threshold) : 0xfu;
+      if (drop) kw[kt] |= kbits << (4 * t);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = __expf(sc[kt][t][r] - mref);
+        const float pv = __builtin_amdgcn_exp2f(sc[kt][t][r] - mref);
         l += pv;
-        sc[kt][t][r] = drop ? ((kb >> r) & 1u ? pv * a.drop_scale : 0.f) : pv;
+        sc[kt][t][r] = (kbits >> r) & 1u ? pv : 0.f;  // (the dropout scale is applied with 1 / l)
       }
     }
   // ---- P . V over every live 32-key half
@@ -656,16 +658,204 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   l += __shfl_xor(l, 32, 64);
   ASTAMP(2);
   if (q >= qlen) return;
-  const float inv = 1.f / l;
+  const float inv = (drop ? a.drop_scale : 1.f) / l;
   bf16_t* out = a.ctx + (tok0 + q) * D + h * DH;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
     *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) =
         make_uint2(pack_bf2(o[dt][0] * inv, o[dt][1] * inv), pack_bf2(o[dt][2] * inv, o[dt][3] * inv));
-  if (g == 0) a.lse[((size_t)b * H + h) * S + q] = mref + __logf(l);
+  if (g == 0) a.lse[((size_t)b * H + h) * S + q] = mref * LN2 + __logf(l);
   ASTAMP(3);
 }
 
+// ---- S <= 128 backward phases (shared by the fused one-block kernel and the two-block split)
+// Scores and biases in log2 units: P = exp2(s * scale * log2e + bias2 - lse2).
+
+// Phase 1 for this wave's 16 query rows (lane row q, read row qr = min(q, len - 1)): dQ from the
+// K / V images in LDS, the rows' Q / dO fragments, delta dl, lse2 and the forward's keep-bit words
+// (mrow_p[kt * 4] = this lane's u16 of key tile kt; null without stored keep bits).
+DEV void bwd_dq_rows(const AttnArgs& a, const char* ks, const char* vs, const float* kb, uint64_t vk0,
+                     uint64_t vk1, const bf16x8 (&qf)[2], const bf16x8 (&dof)[2], float dl, float lse,
+                     const uint16_t* mrow_p, int b, int h, int q, int len, int nt, size_t tok0, int lane) {
+  const int g = lane >> 4, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  const bool drop = a.drop_threshold != 0, varlen = a.cu != nullptr;
+  const uint32_t seed = site_seed(a);
+  const float scale2 = a.scale * LOG2E;
+  const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
+  f32x4 dq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const uint64_t vk = kt ? vk1 : vk0;
+    if (kt >= nt || vk == 0) continue;  // fully masked key tile: dS = 0
+    bool tv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) tv[t] = ((vk >> (16 * t)) & 0xffffull) != 0;
+    const char* kst = ks + kt * 8192;
+    const char* vst = vs + kt * 8192;
+    const uint32_t mrow = (drop && mrow_p) ? mrow_p[kt * 4] : 0u;  // this lane's keys 16 t + 4 g + r
+    f32x4 sc[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!tv[t]) continue;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        sc[t] = mfma16(row_frag(kst, 16 * t, s2, lane), qf[s2], sc[t]);
+        dp[t] = mfma16(row_frag(vst, 16 * t, s2, lane), dof[s2], dp[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (!tv[t]) continue;  // sc[t] = 0 = dS of a fully masked sub-tile
+      const uint32_t kw = !drop   ? 0xfu
+                          : mrow_p ? (mrow >> (4 * t)) & 0xfu
+                                   : drop_keep_bits<4>(seed, rowidx + kt * 64 + 16 * t + 4 * g, a.drop_threshold);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kl = 16 * t + 4 * g + r;
+        const float bias = varlen ? (kt * 64 + kl < len ? 0.f : -INFINITY) : kb[kt * 64 + kl];
+        const float pv = __builtin_amdgcn_exp2f(sc[t][r] * scale2 + bias - lse);
+        float dpv = dp[t][r];
+        if (drop) dpv = (kw >> r) & 1u ? dpv * a.drop_scale : 0.f;
+        sc[t][r] = pv * (dpv - dl);  // dS
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (!(tv[2 * kk] || tv[2 * kk + 1])) continue;
+      const bf16x8 df = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(tr_frag(kst, 16 * dt, kk, lane), df, dq[dt]);
+    }
+  }
+  if (q < len) {
+    const float sc_out = a.scale;
+    bf16_t* out = a.dqkv + (tok0 + q) * ld3 + h * DH;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+      *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) = make_uint2(
+          pack_bf2(dq[dt][0] * sc_out, dq[dt][1] * sc_out), pack_bf2(dq[dt][2] * sc_out, dq[dt][3] * sc_out));
+  }
+}
+
+// Phase 2 for this wave's 16 keys key0 .. key0 + 15: dK and dV from the Q / dO images in LDS, the
+// keys' K / V fragments, lse2 / delta of every query row (LDS) and the keep bits (LDS, mk16).
+DEV void bwd_dkv_keys(const AttnArgs& a, const char* qs, const char* os, const float* lse_s, const float* dl_s,
+                      const uint16_t* mk16, bool keys_live, const bf16x8 (&kf)[2], const bf16x8 (&vf)[2],
+                      float kbias, int b, int h, int key, int len, int nt, int qlen, size_t tok0, int lane) {
+  const int g = lane >> 4, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  const bool drop = a.drop_threshold != 0;
+  const uint32_t seed = site_seed(a);
+  const float scale2 = a.scale * LOG2E;
+  const uint32_t headidx = (uint32_t)(b * H + h) * S;
+  // this lane's key in the forward's lane-major keep bits: word kt * 4 + g', bit 4 t' + r'
+  const int kword = (key >> 6) * 4 + ((key >> 2) & 3), kbit = 4 * ((key >> 4) & 3) + (key & 3);
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dk[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    if (!keys_live || qt >= nt) continue;
+    const char* qst = qs + qt * 8192;
+    const char* ost = os + qt * 8192;
+    // 16-query sub-tiles past the sequence (varlen) have lse = +inf: P = dS = 0, skipped
+    bool tv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) tv[t] = qt * 64 + 16 * t < qlen;
+    f32x4 sc[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!tv[t]) continue;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        sc[t] = mfma16(row_frag(qst, 16 * t, s2, lane), kf[s2], sc[t]);  // S[q][key]
+        dp[t] = mfma16(row_frag(ost, 16 * t, s2, lane), vf[s2], dp[t]);  // dP[q][key]
+      }
+    }
+    // one 32-query half at a time: P / dS of tiles 2kk, 2kk+1 are packed to bf16 right away
+    // (keeps the live set small -> several blocks per CU)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (!(tv[2 * kk] || tv[2 * kk + 1])) continue;
+      f32x4 pd[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = 2 * kk + u;
+        if (!tv[t]) {
+          pd[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+          continue;  // sc[t] = 0 already
+        }
+        // the 4 query rows of this lane: one 16-byte LDS read each for their lse and delta
+        const float4 lse4 = *reinterpret_cast<const float4*>(lse_s + qt * 64 + 16 * t + 4 * g);
+        const float4 dl4 = *reinterpret_cast<const float4*>(dl_s + qt * 64 + 16 * t + 4 * g);
+        const float lsev[4] = {lse4.x, lse4.y, lse4.z, lse4.w}, dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = qt * 64 + 16 * t + 4 * g + r;
+          const float pv = __builtin_amdgcn_exp2f(sc[t][r] * scale2 + kbias - lsev[r]);
+          float dpv = dp[t][r], pdv = pv;
+          if (drop) {
+            const bool keep = mk16 ? ((mk16[ql * 8 + kword] >> kbit) & 1u) != 0
+                                   : drop_keep(seed, (headidx + ql) * (uint32_t)S + key, a.drop_threshold);
+            dpv = keep ? dpv * a.drop_scale : 0.f;
+            pdv = keep ? pv : 0.f;  // (the dropout scale is applied to dV once, at the store)
+          }
+          pd[u][r] = pdv;
+          sc[t][r] = pv * (dpv - dlv[r]);  // dS
+        }
+      }
+      const bf16x8 pf = pack_acc(pd[0], pd[1]);
+      const bf16x8 sf = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma16(tr_frag(ost, 16 * dt, kk, lane), pf, dv[dt]);
+        dk[dt] = mfma16(tr_frag(qst, 16 * dt, kk, lane), sf, dk[dt]);
+      }
+    }
+  }
+  if (key >= len) return;
+  const float sc_out = a.scale, dv_sc = drop ? a.drop_scale : 1.f;
+  bf16_t* outk = a.dqkv + (tok0 + key) * ld3 + D + h * DH;
+  bf16_t* outv = a.dqkv + (tok0 + key) * ld3 + 2 * D + h * DH;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    *reinterpret_cast<uint2*>(outk + 16 * dt + 4 * g) = make_uint2(
+        pack_bf2(dk[dt][0] * sc_out, dk[dt][1] * sc_out), pack_bf2(dk[dt][2] * sc_out, dk[dt][3] * sc_out));
+    *reinterpret_cast<uint2*>(outv + 16 * dt + 4 * g) = make_uint2(
+        pack_bf2(dv[dt][0] * dv_sc, dv[dt][1] * dv_sc), pack_bf2(dv[dt][2] * dv_sc, dv[dt][3] * dv_sc));
+  }
+}
+
+// delta = rowsum(dO * O) of the lane's row from its two 32-wide fragment halves (16 lanes per row)
+DEV float row_delta(const bf16x8 (&of)[2], const bf16x8 (&dof)[2]) {
+  float dl = 0.f;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)of[s2][j]) * bf2f((uint16_t)dof[s2][j]);
+  dl += __shfl_xor(dl, 16, 64);
+  dl += __shfl_xor(dl, 32, 64);
+  return dl;
+}
+
+// Zero dQ of rows without a gradient (q_live: not among the query rows the loss reaches).
+DEV void zero_dq_rows(const AttnArgs& a, int h, int q, int len, size_t tok0, int g) {
+  if (q >= len) return;
+  bf16_t* out = a.dqkv + (tok0 + q) * (3 * a.H * DH) + h * DH;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) = make_uint2(0u, 0u);
+}
+
+// One block per (sequence, head): phase 1 (waves own 16 query rows: delta, dQ), a barrier, phase 2
+// (waves own 16 keys: dK, dV) from the same four LDS images.  FD_ATTN_BWD_SPLIT=0.
 __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[8 * 8192 + 3 * 512 + 2048];
   char* qs = smem;
@@ -706,112 +896,37 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
   stage_rows(os, a.dctx + tok0 * D + h * DH, D, tid, nt, len);
   if (tid < 128) {
-    kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) : -INFINITY;
+    kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) * LOG2E : -INFINITY;
     // query rows past the sequence: lse = +inf makes their P (and dS) exactly 0
-    lse_s[tid] = tid < qlen ? a.lse[st0 + tid] : INFINITY;
+    lse_s[tid] = tid < qlen ? a.lse[st0 + tid] * LOG2E : INFINITY;
     dl_s[tid] = 0.f;
   }
-  const bool drop = a.drop_threshold != 0;
   // the forward's keep bits (rows the forward did not write are past the sequence: P = 0 there)
-  const bool mk = drop && a.dmask != nullptr;
+  const bool mk = a.drop_threshold != 0 && a.dmask != nullptr;
   if (mk && tid < 256) mk_s[tid] = a.dmask[((size_t)b * H + h) * 256 + tid];
   __syncthreads();
   ASTAMP(1);
-  const uint32_t seed = site_seed(a);
-  const float sc_out = a.scale;
-  const bool varlen = a.cu != nullptr;  // key masks are arithmetic (k < len)
   // unmasked-key bits of the two 64-key tiles (see attn_fwd_s128_kernel): 16-key sub-tiles
   // with every key masked have P = dS = 0 exactly and are skipped in both phases
   const uint64_t vk0 = __ballot(kb[lane] != -INFINITY);
   const uint64_t vk1 = __ballot(kb[64 + lane] != -INFINITY);
 
   // ---- phase 1: dQ and delta; wave w owns queries 16w .. 16w+15
-  if (q0 >= qlen && q0 < len) {  // rows without a gradient (q_live): dQ = 0
-    const int q = q0 + (lane & 15);
-    if (q < len) {
-      bf16_t* out = a.dqkv + (tok0 + q) * ld3 + h * DH;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) = make_uint2(0u, 0u);
-    }
-  }
+  if (q0 >= qlen && q0 < len) zero_dq_rows(a, h, q0 + (lane & 15), len, tok0, g);
   if (q0 < qlen) {
     const int q = q0 + (lane & 15);
     const int qr = min(q, len - 1);
-    const char* qst = qs + (q0 >> 6) * 8192;
-    const char* ost = os + (q0 >> 6) * 8192;
     bf16x8 qf[2], dof[2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      qf[s2] = row_frag(qst, q0 & 63, s2, lane);
-      dof[s2] = row_frag(ost, q0 & 63, s2, lane);
+      qf[s2] = row_frag(qs + (q0 >> 6) * 8192, q0 & 63, s2, lane);
+      dof[s2] = row_frag(os + (q0 >> 6) * 8192, q0 & 63, s2, lane);
     }
-    const float lse = lse_s[qr];
-    float dl = 0.f;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)of[s2][j]) * bf2f((uint16_t)dof[s2][j]);
-    dl += __shfl_xor(dl, 16, 64);
-    dl += __shfl_xor(dl, 32, 64);
+    float dl = row_delta(of, dof);
     if (q >= qlen) dl = 0.f;  // (q_live: this row's O was never written -- it has no gradient)
     if (g == 0 && q < len) dl_s[q] = dl;
-    const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
-    f32x4 dq[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const uint64_t vk = kt ? vk1 : vk0;
-      if (kt >= nt || vk == 0) continue;  // fully masked key tile: dS = 0
-      bool tv[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) tv[t] = ((vk >> (16 * t)) & 0xffffull) != 0;
-      const char* kst = ks + kt * 8192;
-      const char* vst = vs + kt * 8192;
-      const uint32_t mrow = mk ? mk16[qr * 8 + kt * 4 + g] : 0u;  // this lane's keys 16 t + 4 g + r
-      f32x4 sc[4], dp[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (!tv[t]) continue;
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          sc[t] = mfma16(row_frag(kst, 16 * t, s2, lane), qf[s2], sc[t]);
-          dp[t] = mfma16(row_frag(vst, 16 * t, s2, lane), dof[s2], dp[t]);
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (!tv[t]) continue;  // sc[t] = 0 = dS of a fully masked sub-tile
-        const uint32_t kw = !drop ? 0xfu
-                            : mk  ? (mrow >> (4 * t)) & 0xfu
-                                  : drop_keep_bits<4>(seed, rowidx + kt * 64 + 16 * t + 4 * g, a.drop_threshold);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int kl = 16 * t + 4 * g + r;
-          const float bias = varlen ? (kt * 64 + kl < len ? 0.f : -INFINITY) : kb[kt * 64 + kl];
-          const float pv = __expf(sc[t][r] * a.scale + bias - lse);
-          float dpv = dp[t][r];
-          if (drop) dpv = (kw >> r) & 1u ? dpv * a.drop_scale : 0.f;
-          sc[t][r] = pv * (dpv - dl);  // dS
-        }
-      }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        if (!(tv[2 * kk] || tv[2 * kk + 1])) continue;
-        const bf16x8 df = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(tr_frag(kst, 16 * dt, kk, lane), df, dq[dt]);
-      }
-    }
-    if (q < len) {
-      bf16_t* out = a.dqkv + (tok0 + q) * ld3 + h * DH;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) = make_uint2(
-            pack_bf2(dq[dt][0] * sc_out, dq[dt][1] * sc_out), pack_bf2(dq[dt][2] * sc_out, dq[dt][3] * sc_out));
-    }
+    bwd_dq_rows(a, ks, vs, kb, vk0, vk1, qf, dof, dl, lse_s[qr], mk ? mk16 + qr * 8 + g : nullptr, b, h, q, len,
+                nt, tok0, lane);
   }
   ASTAMP(2);
   __syncthreads();  // delta of every query row is in LDS
@@ -820,98 +935,103 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   // ---- phase 2: dK and dV; wave w owns keys 16w .. 16w+15
   const int key0 = w * 16;
   if (key0 >= len) return;
-  const int key = key0 + (lane & 15);
-  const char* kst = ks + (key0 >> 6) * 8192;
-  const char* vst = vs + (key0 >> 6) * 8192;
   bf16x8 kf[2], vf[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
-    kf[s2] = row_frag(kst, key0 & 63, s2, lane);
-    vf[s2] = row_frag(vst, key0 & 63, s2, lane);
-  }
-  const float kbias = kb[key];
-  const uint32_t headidx = (uint32_t)(b * H + h) * S;
-  // this lane's key in the forward's lane-major keep bits: word kt * 4 + g', bit 4 t' + r'
-  const int kword = (key >> 6) * 4 + ((key >> 2) & 3), kbit = 4 * ((key >> 4) & 3) + (key & 3);
-  f32x4 dk[4], dv[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    dk[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    kf[s2] = row_frag(ks + (key0 >> 6) * 8192, key0 & 63, s2, lane);
+    vf[s2] = row_frag(vs + (key0 >> 6) * 8192, key0 & 63, s2, lane);
   }
   // this wave's 16 keys all masked (padded layout): P and dS columns are 0, dK = dV = 0
   const bool keys_live = (((key0 < 64 ? vk0 >> key0 : vk1 >> (key0 - 64))) & 0xffffull) != 0;
+  const int key = key0 + (lane & 15);
+  bwd_dkv_keys(a, qs, os, lse_s, dl_s, mk ? mk16 : nullptr, keys_live, kf, vf, kb[key], b, h, key, len, nt, qlen,
+               tok0, lane);
+  ASTAMP(4);
+}
+
+// Two blocks per (sequence, head) (FD_ATTN_BWD_SPLIT=1, default): blockIdx.x 0 runs phase 1 from K / V
+// images with its rows' Q / dO / O fragments straight from global memory; blockIdx.x 1 recomputes
+// delta for every row, then runs phase 2 from Q / dO images with its keys' K / V fragments from
+// global memory.  The phases no longer run one after the other behind a barrier, and each block
+// stages only two images (36 KiB of LDS instead of 69 KiB: more blocks per CU).
+__global__ __launch_bounds__(512) void attn_bwd_s128_split_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 3 * 512 + 2048];
+  char* im0 = smem;              // role 0: K   role 1: Q
+  char* im1 = smem + 2 * 8192;   // role 0: V   role 1: dO
+  float* kb = reinterpret_cast<float*>(smem + 4 * 8192);
+  float* lse_s = kb + 128;
+  float* dl_s = lse_s + 128;
+  uint64_t* mk_s = reinterpret_cast<uint64_t*>(smem + 4 * 8192 + 3 * 512);
+  const uint16_t* mk16 = reinterpret_cast<const uint16_t*>(mk_s);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int role = blockIdx.x;
+  const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
+  ASTAMP(0);
+  astamp_hwid();
+  if (b == a.B) {
+    zero_filler(a, a.dqkv, ld3, 3, h);
+    return;
+  }
+  int tok0i, len;
+  seq_span(a, b, tok0i, len);
+  const int nt = (len + 63) >> 6;
+  const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;
+  const size_t tok0 = (size_t)tok0i;
+  const size_t st0 = ((size_t)b * H + h) * S;
+  const bool mk = a.drop_threshold != 0 && a.dmask != nullptr;
+  const int r0 = w * 16;                        // role 0: query rows, role 1: keys (and delta rows)
+  const int rr = min(r0 + (lane & 15), len - 1);
+  // this wave's row fragments, in flight together with the staging loads
+  bf16x8 f0[2], f1[2], of[2], dof[2];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    if (!keys_live || qt >= nt) continue;
-    const char* qst = qs + qt * 8192;
-    const char* ost = os + qt * 8192;
-    // 16-query sub-tiles past the sequence (varlen) have lse = +inf: P = dS = 0, skipped
-    bool tv[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) tv[t] = qt * 64 + 16 * t < qlen;
-    f32x4 sc[4], dp[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (!tv[t]) continue;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        sc[t] = mfma16(row_frag(qst, 16 * t, s2, lane), kf[s2], sc[t]);  // S[q][key]
-        dp[t] = mfma16(row_frag(ost, 16 * t, s2, lane), vf[s2], dp[t]);  // dP[q][key]
-      }
-    }
-    // one 32-query half at a time: P / dS of tiles 2kk, 2kk+1 are packed to bf16 right away
-    // (keeps the live set under 128 VGPRs -> two blocks per CU)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      if (!(tv[2 * kk] || tv[2 * kk + 1])) continue;
-      f32x4 pd[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int t = 2 * kk + u;
-        if (!tv[t]) {
-          pd[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-          continue;  // sc[t] = 0 already
-        }
-        // the 4 query rows of this lane: one 16-byte LDS read each for their lse and delta
-        const float4 lse4 = *reinterpret_cast<const float4*>(lse_s + qt * 64 + 16 * t + 4 * g);
-        const float4 dl4 = *reinterpret_cast<const float4*>(dl_s + qt * 64 + 16 * t + 4 * g);
-        const float lsev[4] = {lse4.x, lse4.y, lse4.z, lse4.w}, dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ql = qt * 64 + 16 * t + 4 * g + r;
-          const float pv = __expf(sc[t][r] * a.scale + kbias - lsev[r]);
-          float dpv = dp[t][r], pdv = pv;
-          if (drop) {
-            const bool keep = mk ? ((mk16[ql * 8 + kword] >> kbit) & 1u) != 0
-                                 : drop_keep(seed, (headidx + ql) * (uint32_t)S + key, a.drop_threshold);
-            dpv = keep ? dpv * a.drop_scale : 0.f;
-            pdv = keep ? pv * a.drop_scale : 0.f;
-          }
-          pd[u][r] = pdv;
-          sc[t][r] = pv * (dpv - dlv[r]);  // dS
-        }
-      }
-      const bf16x8 pf = pack_acc(pd[0], pd[1]);
-      const bf16x8 sf = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        dv[dt] = mfma16(tr_frag(ost, 16 * dt, kk, lane), pf, dv[dt]);
-        dk[dt] = mfma16(tr_frag(qst, 16 * dt, kk, lane), sf, dk[dt]);
-      }
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const size_t c = h * DH + 32 * s2 + 8 * g;
+    of[s2] = load_frag_global(a.ctx + (tok0 + rr) * D + c);
+    dof[s2] = load_frag_global(a.dctx + (tok0 + rr) * D + c);
+    if (role == 0) {
+      f0[s2] = load_frag_global(a.qkv + (tok0 + rr) * ld3 + c);          // Q rows
+    } else {
+      f0[s2] = load_frag_global(a.qkv + (tok0 + rr) * ld3 + D + c);      // K rows (this wave's keys)
+      f1[s2] = load_frag_global(a.qkv + (tok0 + rr) * ld3 + 2 * D + c);  // V rows
     }
   }
-  if (key >= len) return;
-  bf16_t* outk = a.dqkv + (tok0 + key) * ld3 + D + h * DH;
-  bf16_t* outv = a.dqkv + (tok0 + key) * ld3 + 2 * D + h * DH;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    *reinterpret_cast<uint2*>(outk + 16 * dt + 4 * g) = make_uint2(
-        pack_bf2(dk[dt][0] * sc_out, dk[dt][1] * sc_out), pack_bf2(dk[dt][2] * sc_out, dk[dt][3] * sc_out));
-    *reinterpret_cast<uint2*>(outv + 16 * dt + 4 * g) =
-        make_uint2(pack_bf2(dv[dt][0], dv[dt][1]), pack_bf2(dv[dt][2], dv[dt][3]));
+  if (role == 0) {
+    stage_rows(im0, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
+    stage_rows(im1, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
+  } else {
+    stage_rows(im0, a.qkv + tok0 * ld3 + h * DH, ld3, tid, nt, len);
+    stage_rows(im1, a.dctx + tok0 * D + h * DH, D, tid, nt, len);
+    if (tid < 128) lse_s[tid] = tid < qlen ? a.lse[st0 + tid] * LOG2E : INFINITY;
+    if (mk && tid < 256) mk_s[tid] = a.dmask[((size_t)b * H + h) * 256 + tid];
+  }
+  if (tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) * LOG2E : -INFINITY;
+  const int q = r0 + (lane & 15);
+  float dl = 0.f;
+  if (r0 < qlen) {
+    dl = row_delta(of, dof);
+    if (q >= qlen) dl = 0.f;
+  }
+  // every row's delta once, by its wave (0 past qlen / the sequence: with lse = +inf there, P = 0)
+  if (role == 1 && g == 0) dl_s[q] = (r0 < qlen && q < len) ? dl : 0.f;
+  __syncthreads();
+  ASTAMP(1);
+  const uint64_t vk0 = __ballot(kb[lane] != -INFINITY);
+  const uint64_t vk1 = __ballot(kb[64 + lane] != -INFINITY);
+  if (role == 0) {
+    if (r0 >= qlen) {
+      if (r0 < len) zero_dq_rows(a, h, q, len, tok0, g);
+      return;
+    }
+    const float lse = q < qlen ? a.lse[st0 + q] * LOG2E : INFINITY;
+    const uint16_t* mrow_p =
+        mk ? reinterpret_cast<const uint16_t*>(a.dmask) + (((size_t)b * H + h) * 128 + rr) * 8 + g : nullptr;
+    bwd_dq_rows(a, im0, im1, kb, vk0, vk1, f0, dof, dl, lse, mrow_p, b, h, q, len, nt, tok0, lane);
+  } else {
+    if (r0 >= len) return;
+    const bool keys_live = (((r0 < 64 ? vk0 >> r0 : vk1 >> (r0 - 64))) & 0xffffull) != 0;
+    bwd_dkv_keys(a, im0, im1, lse_s, dl_s, mk ? mk16 : nullptr, keys_live, f0, f1, kb[q], b, h, q, len, nt, qlen,
+                 tok0, lane);
   }
   ASTAMP(4);
 }
@@ -957,7 +1077,11 @@ int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const floa
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
   if (use_s128(S)) {
-    hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
+    static const int split = [] { const char* e = getenv("FD_ATTN_BWD_SPLIT"); return e ? atoi(e) : 1; }();
+    if (split)
+      hipLaunchKernelGGL(attn_bwd_s128_split_kernel, dim3(2, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
+    else
+      hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
     return 0;
   }
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);

@@ -47,6 +47,9 @@ DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
 // ---------------------------------------------------------------- dropout hash
 // lowbias32-style finaliser over (idx * golden + seed).  Mirrored bit-exactly by
 // ops/dropout.py::keep_mask (torch int64 arithmetic) for the CPU reference.

@@ -159,13 +159,16 @@ DEV int fk(int k) {
 // logical chunk land on 16 distinct 16-byte bank slots.
 DEV int ksw(int r) { return (r >> 1) & 7; }
 
-template <int ROWS, bool KMAJ, int NWAVES>
+// BK: K depth of one ring slot -- 64 (two 32-deep MFMA k-steps), or 32 for MN-major operands
+// (half the bytes per slot: twice the slots in flight for the same LDS).
+template <int ROWS, bool KMAJ, int NWAVES, int BK = BKT>
 struct Operand {
-  static constexpr int BYTES = ROWS * BKT * 2;              // one LDS slot
+  static_assert(BK == BKT || (!KMAJ && BK == 32), "32-deep slots: MN-major images only");
+  static constexpr int BYTES = ROWS * BK * 2;               // one LDS slot
   static constexpr int PER_WAVE = BYTES / 1024 / NWAVES;   // 1 KiB DMA pieces per wave per tile
-  // MN-major: [BKT][SUB] sub-images stacked along mn
+  // MN-major: [BK][SUB] sub-images stacked along mn
   static constexpr int SUB = (ROWS % 128 == 0) ? 128 : 64;
-  static constexpr int SUB_BYTES = BKT * SUB * 2;
+  static constexpr int SUB_BYTES = BK * SUB * 2;
   static constexpr int SUB_CH = SUB / 8;
 
   // LDS-DMA of the K tile starting at k0.  K-major rows beyond `lim` are clamped
@@ -899,11 +902,11 @@ DEV void wait_tiles(int n) {
   wait_vm<0>();
 }
 
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, int BK = BKT>
 struct GemmCfg {
   static constexpr int NW = WM * WN;
-  using OA = Operand<BM, AK, NW>;
-  using OB = Operand<BN, BKM, NW>;
+  using OA = Operand<BM, AK, NW, BK>;
+  using OB = Operand<BN, BKM, NW, BK>;
   static constexpr int BUF = OA::BYTES + OB::BYTES;
   // DIRECT fp32 tiles are staged one wave-row band (BM / WM rows) at a time
   static constexpr int EPI_BYTES = EpiTraits<EPI, BM, BN>::DIRECT ? (BM / WM) * (BN * 4 + 16)
@@ -933,10 +936,11 @@ struct GemmGroup {
 #endif
 
 // One output tile (tm, tn) of problem p: the K loop over the LDS-DMA ring, then the epilogue.
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, int BK = BKT>
 DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
   const int tm_ = tm, tn_ = tn;
-  using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S>;
+  using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S, BK>;
+  constexpr int KS = BK / 32;  // 32-deep MFMA k-steps per ring slot
   using OA = typename G::OA;
   using OB = typename G::OB;
   constexpr int NW = G::NW;
@@ -953,7 +957,7 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
   const int wr = wid / WN, wc = wid % WN;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = blockIdx.z * p.k_split;
-  const int nk = p.k_split / BKT;
+  const int nk = p.k_split / BK;
 
   f32x4 acc[MI][NI];
 #pragma unroll
@@ -963,8 +967,8 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
 
   auto issue = [&](int t) {
     char* b = smem + (t % S) * BUF;
-    OA::stage(p.A, p.lda, m0, kbeg + t * BKT, p.M, b, wid, lane);
-    OB::stage(p.B, p.ldb, n0, kbeg + t * BKT, p.N, b + OA::BYTES, wid, lane);
+    OA::stage(p.A, p.lda, m0, kbeg + t * BK, p.M, b, wid, lane);
+    OB::stage(p.B, p.ldb, n0, kbeg + t * BK, p.N, b + OA::BYTES, wid, lane);
   };
   bf16x8 a0[MI], b0[NI], a1[MI], b1[NI];
   auto read_frags = [&](const char* cur) {
@@ -972,10 +976,12 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
     for (int i = 0; i < MI; ++i) a0[i] = OA::frag(cur, wr * TM + i * 16, 0, lane);
 #pragma unroll
     for (int j = 0; j < NI; ++j) b0[j] = OB::frag(cur + OA::BYTES, wc * TN + j * 16, 0, lane);
+    if constexpr (KS == 2) {
 #pragma unroll
-    for (int i = 0; i < MI; ++i) a1[i] = OA::frag(cur, wr * TM + i * 16, 1, lane);
+      for (int i = 0; i < MI; ++i) a1[i] = OA::frag(cur, wr * TM + i * 16, 1, lane);
 #pragma unroll
-    for (int j = 0; j < NI; ++j) b1[j] = OB::frag(cur + OA::BYTES, wc * TN + j * 16, 1, lane);
+      for (int j = 0; j < NI; ++j) b1[j] = OB::frag(cur + OA::BYTES, wc * TN + j * 16, 1, lane);
+    }
   };
   auto mfmas = [&]() {
     if constexpr (!SCHED) __builtin_amdgcn_s_setprio(1);  // (s_setprio would split the scheduling region)
@@ -983,10 +989,12 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b0[j], a0[i], acc[i][j]);
+    if constexpr (KS == 2) {
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b1[j], a1[i], acc[i][j]);
+        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b1[j], a1[i], acc[i][j]);
+    }
     if constexpr (!SCHED) __builtin_amdgcn_s_setprio(0);
   };
 
@@ -1011,7 +1019,7 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
       if (kt + S - 1 < nk && !(p.diag & 1)) issue(kt + S - 1);
       read_frags(smem + (kt % S) * BUF);
       mfmas();
-      if constexpr (SCHED) sched_ktile<MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2), MI * NI>();
+      if constexpr (SCHED) sched_ktile<(MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2)) * KS / 2, MI * NI * KS / 2>();
     }
   } else {
     // Two K tiles per barrier (S >= 6): the slots of the pair read in the previous step are
@@ -1044,11 +1052,11 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
       }
       read_frags(smem + (kt % S) * BUF);
       mfmas();
-      if constexpr (SCHED) sched_ktile<MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2), MI * NI>();
+      if constexpr (SCHED) sched_ktile<(MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2)) * KS / 2, MI * NI * KS / 2>();
       if (kt + 1 < nk) {
         read_frags(smem + ((kt + 1) % S) * BUF);
         mfmas();
-        if constexpr (SCHED) sched_ktile<MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2), MI * NI>();
+        if constexpr (SCHED) sched_ktile<(MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2)) * KS / 2, MI * NI * KS / 2>();
       }
     }
   }
@@ -1097,11 +1105,11 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
 }
 
 // bid = the tile's index within p, walked in group-M order
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, int BK = BKT>
 DEV void gemm_tile(const GemmParams& p, int bid, char* smem) {
   int tm, tn;
   tile_coords(bid, (p.M + BM - 1) / BM, p.N / BN, p.group_m, tm, tn);
-  gemm_tile_at<BM, BN, AK, BKM, EPI, WM, WN, S>(p, tm, tn, smem);
+  gemm_tile_at<BM, BN, AK, BKM, EPI, WM, WN, S, BK>(p, tm, tn, smem);
 }
 
 template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S>
@@ -1332,7 +1340,7 @@ struct DwBatch {
 };
 
 // One tile of the batch: logical tile id lid -> (problem, tile) -> K loop + epilogue.
-template <int BM, int BN, int WM, int WN, int S>
+template <int BM, int BN, int WM, int WN, int S, int BK>
 DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
   int i = 0;
   while (i + 1 < bt.n && lid >= bt.pr[i + 1].tile0) ++i;  // block-uniform
@@ -1352,14 +1360,15 @@ DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
     p.adam.lr = bt.lr; p.adam.b1 = bt.b1; p.adam.b2 = bt.b2; p.adam.eps = bt.eps; p.adam.wd = bt.wd;
     p.adam.decoupled = bt.decoupled;
   }
-  gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S>(p, lid - q.tile0, smem);
+  gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S, BK>(p, lid - q.tile0, smem);
 }
 
-template <int BM, int BN, int WM, int WN, int S>
+template <int BM, int BN, int WM, int WN, int S, int BK = BKT>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch bt) {
-  using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S>;
+  using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S, BK>;
+  static_assert(G::SMEM <= LDS_MAX, "LDS");
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
-  dwb_tile<BM, BN, WM, WN, S>(bt, xcd_remap(blockIdx.x, bt.ntiles), smem);
+  dwb_tile<BM, BN, WM, WN, S, BK>(bt, xcd_remap(blockIdx.x, bt.ntiles), smem);
 }
 
 // out[i] = (accumulate ? out[i] : 0) + sum_z slab[z][i]   (deterministic split-K reduce)
@@ -1910,6 +1919,9 @@ bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
     case 1: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 2>, 128, 128, 256);
     case 8: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 2>, 128, 64, 256);
     case 11: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 2>, 256, 256, 512);
+    // 256 x 256 with 32-deep slots: 3 / 4 slots (96 / 128 KiB) in flight instead of one 64 KiB slot
+    case 25: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 4, 32>, 256, 256, 512);
+    case 26: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 5, 32>, 256, 256, 512);
   }
   return false;
 }
