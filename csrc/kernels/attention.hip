@@ -519,11 +519,12 @@ __global__ __launch_bounds__(256) void mask_to_bias_kernel(const M* mask, float*
 // same per-element arithmetic order and dropout indices as the 64-row kernels.
 
 // Stage rows [0, 64*nt) of a [rows][64]-per-head operand into nt swizzled [64][64]
-// images (8 KiB apart); rows >= len re-read row len-1.  512 threads.
+// images (8 KiB apart); rows >= len re-read row len-1.  NT threads.
+template <int NT = 512>
 DEV void stage_rows(char* lds, const bf16_t* src, long ld, int tid, int nt, int len) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int id = i * 512 + tid;
+  for (int i = 0; i < 1024 / NT; ++i) {
+    const int id = i * NT + tid;
     const int r = id >> 3, c = id & 7;
     if (r < 64 * nt) {
       const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)min(r, len - 1) * ld + c * 8);
@@ -540,7 +541,11 @@ DEV void stage_rows(char* lds, const bf16_t* src, long ld, int tid, int nt, int 
 // waiting (PMC, profiles/r3_rejected_register_staging.txt).  Varlen key masks are arithmetic
 // (k < len), not an LDS table.  Keep bits go out lane-major: u16 [q][kt * 4 + g], bit 4 t + r =
 // key 64 kt + 16 t + 4 g + r -- each lane stores its own bits, no cross-lane OR.
-__global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
+// NW waves per block own query rows [blockIdx.x * 16 NW, + 16 NW): NW = 8 -> one block per
+// (sequence, head); NW = 4 (FD_ATTN_FWD_SPLIT=1) -> two, each staging all of K / V -- the grid's
+// live waves spread over the CUs in smaller units (a sequence of ~84 tokens has 6 live query waves).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_s128_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 512];
   char* ks = smem;
   char* vs = smem + 2 * 8192;
@@ -558,20 +563,21 @@ __global__ __launch_bounds__(512) void attn_fwd_s128_kernel(AttnArgs a) {
   seq_span(a, b, tok0i, len);
   const int nt = (len + 63) >> 6;
   const size_t tok0 = (size_t)tok0i;
-  const int q0 = w * 16;
+  const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows needed
+  if ((int)blockIdx.x * 16 * NW >= qlen) return;  // the whole block past the needed rows
+  const int q0 = (blockIdx.x * NW + w) * 16;
   const int q = q0 + (lane & 15);
   const int qr = min(q, len - 1);
   const bool varlen = a.cu != nullptr;
   bf16x8 qf[2];  // this wave's Q rows, fetched together with the K/V staging loads
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) qf[s2] = load_frag_global(a.qkv + (tok0 + qr) * ld3 + h * DH + 32 * s2 + 8 * g);
-  stage_rows(ks, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
-  stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
+  stage_rows<64 * NW>(ks, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
+  stage_rows<64 * NW>(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
   // (the softmax runs in log2 units: scores and key biases pre-scaled by log2(e), v_exp_f32 direct)
   if (!varlen && tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) * LOG2E : -INFINITY;
   __syncthreads();
   ASTAMP(1);
-  const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows needed
   if (q0 >= qlen) return;  // no barrier follows
   const uint32_t seed = site_seed(a);
   const bool drop = a.drop_threshold != 0;
@@ -1036,6 +1042,17 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_split_kernel(AttnArgs a) {
   ASTAMP(4);
 }
 
+// FD_ATTN_FWD_SPLIT / FD_ATTN_BWD_SPLIT, or fd_attn_set_split (tests: both forms in one process)
+int g_fwd_split = -1, g_bwd_split = -1;
+int fwd_split() {
+  if (g_fwd_split < 0) { const char* e = getenv("FD_ATTN_FWD_SPLIT"); g_fwd_split = e ? atoi(e) : 0; }
+  return g_fwd_split;
+}
+int bwd_split() {
+  if (g_bwd_split < 0) { const char* e = getenv("FD_ATTN_BWD_SPLIT"); g_bwd_split = e ? atoi(e) : 1; }
+  return g_bwd_split;
+}
+
 bool use_s128(int S) {
   static const int on = [] { const char* e = getenv("FD_ATTN_S128"); return e ? atoi(e) : 1; }();
   return on && S <= 128;
@@ -1044,6 +1061,13 @@ bool use_s128(int S) {
 }  // namespace
 
 extern "C" {
+
+// fwd / bwd < 0: leave as is.  Returns 0.
+int fd_attn_set_split(int fwd, int bwd) {
+  if (fwd >= 0) g_fwd_split = fwd;
+  if (bwd >= 0) g_bwd_split = bwd;
+  return 0;
+}
 
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
@@ -1056,8 +1080,10 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
-  if (use_s128(S))
-    hipLaunchKernelGGL(attn_fwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
+  if (use_s128(S) && fwd_split())
+    hipLaunchKernelGGL(attn_fwd_s128_kernel<4>, dim3(2, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
+  else if (use_s128(S))
+    hipLaunchKernelGGL(attn_fwd_s128_kernel<8>, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
   else
     hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
   return 0;
@@ -1077,8 +1103,7 @@ int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const floa
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
   if (use_s128(S)) {
-    static const int split = [] { const char* e = getenv("FD_ATTN_BWD_SPLIT"); return e ? atoi(e) : 1; }();
-    if (split)
+    if (bwd_split())
       hipLaunchKernelGGL(attn_bwd_s128_split_kernel, dim3(2, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
     else
       hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);

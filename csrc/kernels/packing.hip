@@ -111,22 +111,41 @@ __global__ __launch_bounds__(256) void scatter_rows2_kernel(const uint4* a, cons
   if (lds)
     for (int k = threadIdx.x; k < nsrc; k += 256) sidx[k] = idx[k];
   __syncthreads();
-  const long long i = blockIdx.x * 256ll + threadIdx.x;
-  if (i >= (long long)T * d16) return;
-  const long long r = i / d16, c = i - r * d16;
+  // 32-bit index math (T * d16 < 2^31, checked by the launcher): a 64-bit division is a runtime
+  // call with a scratch frame
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= T * d16) return;
+  const int r = i / d16, c = i - r * d16;
   // LAST k with idx[k] == r: an empty sequence (all-zero mask row) repeats its successor's [CLS]
   // row cu[b] == cu[b+1], and -- as in head_bwd's last-owner rule -- the later sequence (the one
   // that actually owns the row) wins
+  // (one search loop per address space: a select between the LDS and the global list made the
+  //  pointer generic and cost the kernel a scratch frame)
   int lo = 0, hi = nsrc;  // first k with idx[k] > r
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if ((lds ? sidx[mid] : idx[mid]) <= r) lo = mid + 1; else hi = mid;
+  bool hit;
+  if (lds) {
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sidx[mid] <= r) lo = mid + 1; else hi = mid;
+    }
+    hit = lo > 0 && sidx[lo - 1] == r;
+  } else {
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (idx[mid] <= r) lo = mid + 1; else hi = mid;
+    }
+    hit = lo > 0 && idx[lo - 1] == r;
   }
   const int k = lo - 1;
-  const bool hit = k >= 0 && (lds ? sidx[k] : idx[k]) == r;
-  const uint4 z = make_uint4(0, 0, 0, 0);
-  oa[i] = hit ? a[(long long)k * d16 + c] : z;
-  ob[i] = hit ? b[(long long)k * d16 + c] : z;
+  // (branches, not `hit ? a[..] : z`: hipcc turned that select into a load through a pointer to
+  //  either the row or a stack copy of z -- flat loads and a scratch frame)
+  if (hit) {
+    oa[i] = a[(long long)k * d16 + c];
+    ob[i] = b[(long long)k * d16 + c];
+  } else {
+    oa[i] = make_uint4(0, 0, 0, 0);
+    ob[i] = make_uint4(0, 0, 0, 0);
+  }
 }
 
 }  // namespace
@@ -146,6 +165,7 @@ int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const lon
                      int d_bytes, hipStream_t st) {
   if (nsrc < 0 || T <= 0 || d_bytes <= 0 || d_bytes % 16) return 1;
   const long long tot = (long long)T * (d_bytes / 16);
+  if (tot >= (1ll << 31)) return 1;
   hipLaunchKernelGGL(scatter_rows2_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const uint4*)a,
                      (const uint4*)b, (uint4*)oa, (uint4*)ob, idx, nsrc, T, d_bytes / 16);
   return 0;

@@ -7,5 +7,6 @@ timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-quality > $O/bench
 FD_ATTN_BWD_SPLIT=0 timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-quality > $O/bench_nosplit.log 2>&1 && tail -n 1 $O/bench_nosplit.log | cut -c1-220 &&
 FD_GEMM_DWB_CFG=25 timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-quality > $O/bench_dwb25.log 2>&1 && tail -n 1 $O/bench_dwb25.log | cut -c1-220 &&
 FD_GEMM_DWB_CFG=26 timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-quality > $O/bench_dwb26.log 2>&1 && tail -n 1 $O/bench_dwb26.log | cut -c1-220
+FD_ATTN_FWD_SPLIT=1 timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-quality > $O/bench_fsplit.log 2>&1 && tail -n 1 $O/bench_fsplit.log | cut -c1-220
 bash scripts/gpu.sh prof r4i
 echo done

@@ -178,3 +178,20 @@ def test_plots_reference_files_and_per_client_dpi(tmp_path):
         sizes[cid] = Image.open(out[0]).size
     assert reference_dpi(1) is None and reference_dpi(2) == 300
     assert sizes[2][0] > 2 * sizes[1][0]  # 300 dpi vs the default 100
+
+
+def test_dropout_hash_pairs_mirror_common_h():
+    """ops/dropout.py mirrors common.h drop_keep: element i keeps iff its 16-bit half (low: even i,
+    high: odd i) of hash32(seed, i >> 1) >= round(p * 2^16); the keep rate is 1 - p."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import dropout as DR
+    assert DR.threshold(0.0) == 0 and DR.threshold(0.1) == 6554 and DR.threshold(1.0) == 0xFFFF
+    seed = DR.site_seed(12345, DR.Sites.attn(2))
+    idx = torch.arange(0, 4096, dtype=torch.int64) + 7  # odd start: pairs straddle the slice
+    got = DR.keep_t(seed, idx, DR.threshold(0.1))
+    for i in (7, 8, 9, 100, 4101):
+        h = DR.hash32(seed, i >> 1)
+        half = (h >> 16) if i & 1 else (h & 0xFFFF)
+        assert bool(got[i - 7]) == (half >= 6554)
+    mask = DR.keep_mask(3, DR.Sites.ffn(0), 1 << 18, 0.1)
+    assert abs(mask.float().mean().item() - 0.9) < 0.003
+    assert torch.equal(DR.keep_mask(3, 5, 64, 0.1, offset=32), DR.keep_mask(3, 5, 96, 0.1)[32:])
