@@ -34,7 +34,6 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
 int fd_gemm_set_da(int id);
-int fd_attn_set_split(int fwd, int bwd);
 int fd_gemm_stamps(unsigned long long* host, int nblocks);
 int fd_attn_stamps(unsigned long long* host, int nblocks);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
@@ -1232,9 +1231,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("aux"), py::arg("res"), py::arg("workspace"), py::arg("accumulate"), py::arg("aux_out") = py::none());
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_set_da", [](int64_t id) { check_rc(fd_gemm_set_da((int)id), "gemm_set_da"); });
-  m.def("attn_set_split", [](int64_t fwd, int64_t bwd) {
-    check_rc(fd_attn_set_split((int)fwd, (int)bwd), "attn_set_split");
-  });
   m.def("gemm_stamps", &gemm_stamps);
   m.def("attn_stamps", &attn_stamps);
   m.def("gemm_splitk", &gemm_splitk, py::arg("epi"), py::arg("A"), py::arg("Bt"), py::arg("C"), py::arg("workspace"),

@@ -542,8 +542,8 @@ DEV void stage_rows(char* lds, const bf16_t* src, long ld, int tid, int nt, int 
 // (k < len), not an LDS table.  Keep bits go out lane-major: u16 [q][kt * 4 + g], bit 4 t + r =
 // key 64 kt + 16 t + 4 g + r -- each lane stores its own bits, no cross-lane OR.
 // NW waves per block own query rows [blockIdx.x * 16 NW, + 16 NW): NW = 8 -> one block per
-// (sequence, head); NW = 4 (FD_ATTN_FWD_SPLIT=1) -> two, each staging all of K / V -- the grid's
-// live waves spread over the CUs in smaller units (a sequence of ~84 tokens has 6 live query waves).
+// (sequence, head).  (NW = 4, two blocks per (sequence, head), measured no faster:
+// profiles/r4_rejected_ab.txt.)
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_s128_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 512];
@@ -861,7 +861,8 @@ DEV void zero_dq_rows(const AttnArgs& a, int h, int q, int len, size_t tok0, int
 }
 
 // One block per (sequence, head): phase 1 (waves own 16 query rows: delta, dQ), a barrier, phase 2
-// (waves own 16 keys: dK, dV) from the same four LDS images.  FD_ATTN_BWD_SPLIT=0.
+// (waves own 16 keys: dK, dV) from the same four LDS images.  (A dQ block beside a dK/dV block per
+// (sequence, head) lost its A/B: 23.8 vs 19.3 us per layer, profiles/r4_rejected_ab.txt.)
 __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[8 * 8192 + 3 * 512 + 2048];
   char* qs = smem;
@@ -955,104 +956,6 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   ASTAMP(4);
 }
 
-// Two blocks per (sequence, head) (FD_ATTN_BWD_SPLIT=1, default): blockIdx.x 0 runs phase 1 from K / V
-// images with its rows' Q / dO / O fragments straight from global memory; blockIdx.x 1 recomputes
-// delta for every row, then runs phase 2 from Q / dO images with its keys' K / V fragments from
-// global memory.  The phases no longer run one after the other behind a barrier, and each block
-// stages only two images (36 KiB of LDS instead of 69 KiB: more blocks per CU).
-__global__ __launch_bounds__(512) void attn_bwd_s128_split_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 3 * 512 + 2048];
-  char* im0 = smem;              // role 0: K   role 1: Q
-  char* im1 = smem + 2 * 8192;   // role 0: V   role 1: dO
-  float* kb = reinterpret_cast<float*>(smem + 4 * 8192);
-  float* lse_s = kb + 128;
-  float* dl_s = lse_s + 128;
-  uint64_t* mk_s = reinterpret_cast<uint64_t*>(smem + 4 * 8192 + 3 * 512);
-  const uint16_t* mk16 = reinterpret_cast<const uint16_t*>(mk_s);
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
-  const int role = blockIdx.x;
-  const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
-  ASTAMP(0);
-  astamp_hwid();
-  if (b == a.B) {
-    zero_filler(a, a.dqkv, ld3, 3, h);
-    return;
-  }
-  int tok0i, len;
-  seq_span(a, b, tok0i, len);
-  const int nt = (len + 63) >> 6;
-  const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;
-  const size_t tok0 = (size_t)tok0i;
-  const size_t st0 = ((size_t)b * H + h) * S;
-  const bool mk = a.drop_threshold != 0 && a.dmask != nullptr;
-  const int r0 = w * 16;                        // role 0: query rows, role 1: keys (and delta rows)
-  const int rr = min(r0 + (lane & 15), len - 1);
-  // this wave's row fragments, in flight together with the staging loads
-  bf16x8 f0[2], f1[2], of[2], dof[2];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    const size_t c = h * DH + 32 * s2 + 8 * g;
-    of[s2] = load_frag_global(a.ctx + (tok0 + rr) * D + c);
-    dof[s2] = load_frag_global(a.dctx + (tok0 + rr) * D + c);
-    if (role == 0) {
-      f0[s2] = load_frag_global(a.qkv + (tok0 + rr) * ld3 + c);          // Q rows
-    } else {
-      f0[s2] = load_frag_global(a.qkv + (tok0 + rr) * ld3 + D + c);      // K rows (this wave's keys)
-      f1[s2] = load_frag_global(a.qkv + (tok0 + rr) * ld3 + 2 * D + c);  // V rows
-    }
-  }
-  if (role == 0) {
-    stage_rows(im0, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
-    stage_rows(im1, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
-  } else {
-    stage_rows(im0, a.qkv + tok0 * ld3 + h * DH, ld3, tid, nt, len);
-    stage_rows(im1, a.dctx + tok0 * D + h * DH, D, tid, nt, len);
-    if (tid < 128) lse_s[tid] = tid < qlen ? a.lse[st0 + tid] * LOG2E : INFINITY;
-    if (mk && tid < 256) mk_s[tid] = a.dmask[((size_t)b * H + h) * 256 + tid];
-  }
-  if (tid < 128) kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) * LOG2E : -INFINITY;
-  const int q = r0 + (lane & 15);
-  float dl = 0.f;
-  if (r0 < qlen) {
-    dl = row_delta(of, dof);
-    if (q >= qlen) dl = 0.f;
-  }
-  // every row's delta once, by its wave (0 past qlen / the sequence: with lse = +inf there, P = 0)
-  if (role == 1 && g == 0) dl_s[q] = (r0 < qlen && q < len) ? dl : 0.f;
-  __syncthreads();
-  ASTAMP(1);
-  const uint64_t vk0 = __ballot(kb[lane] != -INFINITY);
-  const uint64_t vk1 = __ballot(kb[64 + lane] != -INFINITY);
-  if (role == 0) {
-    if (r0 >= qlen) {
-      if (r0 < len) zero_dq_rows(a, h, q, len, tok0, g);
-      return;
-    }
-    const float lse = q < qlen ? a.lse[st0 + q] * LOG2E : INFINITY;
-    const uint16_t* mrow_p =
-        mk ? reinterpret_cast<const uint16_t*>(a.dmask) + (((size_t)b * H + h) * 128 + rr) * 8 + g : nullptr;
-    bwd_dq_rows(a, im0, im1, kb, vk0, vk1, f0, dof, dl, lse, mrow_p, b, h, q, len, nt, tok0, lane);
-  } else {
-    if (r0 >= len) return;
-    const bool keys_live = (((r0 < 64 ? vk0 >> r0 : vk1 >> (r0 - 64))) & 0xffffull) != 0;
-    bwd_dkv_keys(a, im0, im1, lse_s, dl_s, mk ? mk16 : nullptr, keys_live, f0, f1, kb[q], b, h, q, len, nt, qlen,
-                 tok0, lane);
-  }
-  ASTAMP(4);
-}
-
-// FD_ATTN_FWD_SPLIT / FD_ATTN_BWD_SPLIT, or fd_attn_set_split (tests: both forms in one process)
-int g_fwd_split = -1, g_bwd_split = -1;
-int fwd_split() {
-  if (g_fwd_split < 0) { const char* e = getenv("FD_ATTN_FWD_SPLIT"); g_fwd_split = e ? atoi(e) : 0; }
-  return g_fwd_split;
-}
-int bwd_split() {
-  if (g_bwd_split < 0) { const char* e = getenv("FD_ATTN_BWD_SPLIT"); g_bwd_split = e ? atoi(e) : 1; }
-  return g_bwd_split;
-}
-
 bool use_s128(int S) {
   static const int on = [] { const char* e = getenv("FD_ATTN_S128"); return e ? atoi(e) : 1; }();
   return on && S <= 128;
@@ -1061,13 +964,6 @@ bool use_s128(int S) {
 }  // namespace
 
 extern "C" {
-
-// fwd / bwd < 0: leave as is.  Returns 0.
-int fd_attn_set_split(int fwd, int bwd) {
-  if (fwd >= 0) g_fwd_split = fwd;
-  if (bwd >= 0) g_bwd_split = bwd;
-  return 0;
-}
 
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
@@ -1080,9 +976,7 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
-  if (use_s128(S) && fwd_split())
-    hipLaunchKernelGGL(attn_fwd_s128_kernel<4>, dim3(2, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
-  else if (use_s128(S))
+  if (use_s128(S))
     hipLaunchKernelGGL(attn_fwd_s128_kernel<8>, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
   else
     hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
@@ -1103,10 +997,7 @@ int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const floa
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
   if (use_s128(S)) {
-    if (bwd_split())
-      hipLaunchKernelGGL(attn_bwd_s128_split_kernel, dim3(2, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
-    else
-      hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
+    hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
     return 0;
   }
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);

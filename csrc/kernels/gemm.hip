@@ -160,7 +160,8 @@ DEV int fk(int k) {
 DEV int ksw(int r) { return (r >> 1) & 7; }
 
 // BK: K depth of one ring slot -- 64 (two 32-deep MFMA k-steps), or 32 for MN-major operands
-// (half the bytes per slot: twice the slots in flight for the same LDS).
+// (half the bytes per slot: twice the slots in flight for the same LDS; the all-layer dW launch
+// with 4 / 5 such slots lost its A/B, profiles/r4_rejected_ab.txt, and is not instantiated).
 template <int ROWS, bool KMAJ, int NWAVES, int BK = BKT>
 struct Operand {
   static_assert(BK == BKT || (!KMAJ && BK == 32), "32-deep slots: MN-major images only");
@@ -1919,9 +1920,6 @@ bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
     case 1: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 2>, 128, 128, 256);
     case 8: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 2>, 128, 64, 256);
     case 11: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 2>, 256, 256, 512);
-    // 256 x 256 with 32-deep slots: 3 / 4 slots (96 / 128 KiB) in flight instead of one 64 KiB slot
-    case 25: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 4, 32>, 256, 256, 512);
-    case 26: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 5, 32>, 256, 256, 512);
   }
   return false;
 }

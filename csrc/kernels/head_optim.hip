@@ -331,6 +331,27 @@ DEV void adam_math4(const AdamArgs& a, float (&pp)[4], const float (&gg)[4], flo
   }
 }
 
+// One flagged row of a [rows][row4] float4 table starting at float4 base4 (one wave; gradient 0
+// unless now[row]).
+DEV void adam_row(const AdamArgs& a, long long base4, int row, int row4, int lane, float step_size,
+                  float inv_sqrt_bc2) {
+  const bool gvalid = a.now == nullptr || a.now[row] != 0;
+  for (int c = lane; c < row4; c += 64) {
+    const long long i = base4 + (long long)row * row4 + c;
+    const float4 p = ld_nt(reinterpret_cast<const float4*>(a.p) + i);
+    const float4 g = gvalid ? ld_nt(reinterpret_cast<const float4*>(a.g) + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 m = ld_nt(reinterpret_cast<const float4*>(a.m) + i);
+    const float4 v = ld_nt(reinterpret_cast<const float4*>(a.v) + i);
+    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
+    float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+    adam_math4(a, pp, gg, mm, vv, step_size, inv_sqrt_bc2);
+    st_nt(reinterpret_cast<float4*>(a.p) + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
+    st_nt(reinterpret_cast<float4*>(a.m) + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
+    st_nt(reinterpret_cast<float4*>(a.v) + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
+    if (a.shadow) reinterpret_cast<uint2*>(a.shadow)[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
+  }
+}
+
 template <bool NT, bool NTP = false>
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   const int t = a.step[0];
@@ -390,23 +411,7 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a, int rows, in
   const int t = a.step[0];
   const float bc1 = 1.f - powf(a.b1, (float)t);
   const float bc2 = 1.f - powf(a.b2, (float)t);
-  const float step_size = a.lr / bc1;
-  const float inv_sqrt_bc2 = 1.f / sqrtf(bc2);
-  const bool gvalid = a.now == nullptr || a.now[row] != 0;
-  for (int c = lane; c < row4; c += 64) {
-    const long long i = (long long)row * row4 + c;
-    const float4 p = ld_nt(reinterpret_cast<const float4*>(a.p) + i);
-    const float4 g = gvalid ? ld_nt(reinterpret_cast<const float4*>(a.g) + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 m = ld_nt(reinterpret_cast<const float4*>(a.m) + i);
-    const float4 v = ld_nt(reinterpret_cast<const float4*>(a.v) + i);
-    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
-    float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
-    adam_math4(a, pp, gg, mm, vv, step_size, inv_sqrt_bc2);
-    st_nt(reinterpret_cast<float4*>(a.p) + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
-    st_nt(reinterpret_cast<float4*>(a.m) + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
-    st_nt(reinterpret_cast<float4*>(a.v) + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
-    if (a.shadow) reinterpret_cast<uint2*>(a.shadow)[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
-  }
+  adam_row(a, 0, row, row4, lane, a.lr / bc1, 1.f / sqrtf(bc2));
 }
 
 __global__ void step_kernel(int* step, uint32_t* seed) {
@@ -501,15 +506,16 @@ int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long lon
   if (runs && (nruns <= 0 || run_total4 <= 0)) return 4;
   AdamArgs a{p, g, m, v, (bf16_t*)shadow, runs ? run_total4 : n / 4, step, lr, b1, b2, eps, wd, decoupled,
              skip_off / 4, (skip_off + skip_rows * row_len) / 4, row_len / 4, touched, now, runs, nruns};
+  const int grid = grid_for(n / 4);
   // FD_ADAM_NT: 0 = default cache policy, 1 = nontemporal g/m/v, 2 = also the fp32 master (default:
   // 2.336 vs 2.366-2.387 ms/step, profiles/r1_ab_adam_nt_master.txt -- only the bf16 shadow is re-read soon)
   static const int nt = [] { const char* e = getenv("FD_ADAM_NT"); return e ? atoi(e) : 2; }();
   if (nt == 2)
-    hipLaunchKernelGGL((adam_kernel<true, true>), dim3(grid_for(n / 4)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((adam_kernel<true, true>), dim3(grid), dim3(256), 0, st, a);
   else if (nt)
-    hipLaunchKernelGGL((adam_kernel<true, false>), dim3(grid_for(n / 4)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((adam_kernel<true, false>), dim3(grid), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((adam_kernel<false, false>), dim3(grid_for(n / 4)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((adam_kernel<false, false>), dim3(grid), dim3(256), 0, st, a);
   return 0;
 }
 

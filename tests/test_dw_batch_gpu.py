@@ -22,7 +22,7 @@ def _frel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("cfg", [-1, 1, 8, 11, 25, 26])
+@pytest.mark.parametrize("cfg", [-1, 1, 8, 11])
 def test_dw_batch_kernel_matches_fp32(cfg):
     g = torch.Generator(device="cuda").manual_seed(cfg + 5)
     T = 2688

@@ -213,48 +213,6 @@ def test_attention_keep_bits_match_hash(S, varlen):
     assert torch.equal(d0, d1)
 
 
-@pytest.mark.parametrize("varlen,q_live", [(False, 0), (True, 0), (True, 1)])
-def test_attention_split_forms_bitwise_equal(varlen, q_live):
-    """The S <= 128 kernels' block decompositions -- forward: one 8-wave block or two 4-wave blocks
-    per (sequence, head); backward: one block (dQ, barrier, dK/dV) or a dQ block beside a dK/dV
-    block -- run the same per-wave arithmetic: outputs, lse, keep bits and gradients bitwise equal."""
-    B, S, H, p = 6, 128, 12, 0.1
-    g = torch.Generator().manual_seed(77)
-    lens = torch.randint(40, S + 1, (B,), generator=g)
-    lens[0], lens[1] = S, 63
-    if varlen:
-        cu = torch.zeros(B + 1, dtype=torch.int32)
-        cu[1:] = torch.cumsum(lens, 0)
-        rows = (int(cu[-1]) + 127) // 128 * 128
-        cu, kb = cu.to(DEV), torch.zeros(1, device=DEV)
-    else:
-        cu, rows = None, B * S
-        kb = kn.mask_bias((torch.arange(S)[None, :] < lens[:, None]).long().to(DEV))
-    qkv = bf(rows, 3 * H * 64, seed=51)
-    dctx = bf(rows, H * 64, seed=52)
-    out = []
-    try:
-        for fwd, bwd in ((0, 0), (1, 1), (0, 1), (1, 0)):
-            kn.ext().attn_set_split(fwd, bwd)
-            dm = kn.attn_keep_bits(B, S, H, p, DEV)
-            dm.fill_(0)
-            ctx, lse = kn.attn_fwd(qkv, kb, B, S, H, seed_t(4), 22, p, cu=cu, dmask=dm, q_live=q_live)
-            d = kn.attn_bwd(qkv, kb, ctx, lse, dctx, B, S, H, seed_t(4), 22, p, cu=cu, dmask=dm, q_live=q_live)
-            torch.cuda.synchronize()
-            out.append((ctx, lse, dm, d))
-    finally:
-        kn.ext().attn_set_split(0, 1)
-    valid = (torch.arange(S)[None, :] < (lens.clamp(max=q_live) if q_live else lens)[:, None]).to(DEV)
-    valid = valid[:, None, :].expand(B, H, S)
-    live_rows = torch.cat([torch.arange(int(c0), int(c0) + (min(int(n), q_live) if q_live else int(n)))
-                           for c0, n in zip((cu.cpu() if cu is not None else torch.arange(B) * S)[:B], lens)]).to(DEV)
-    c0, l0, m0, d0 = out[0]
-    for c1, l1, m1, d1 in out[1:]:
-        assert torch.equal(c0[live_rows], c1[live_rows]) and torch.equal(l0[valid], l1[valid])
-        assert torch.equal(m0, m1)
-        assert torch.equal(d0, d1)
-
-
 @pytest.mark.parametrize("B,S,p", [(2, 128, 0.0), (3, 128, 0.1), (2, 256, 0.1), (1, 64, 0.0), (2, 512, 0.1),
                                    (1, 512, 0.0)])
 def test_attention_fwd(B, S, p):
