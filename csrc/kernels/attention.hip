@@ -539,8 +539,9 @@ DEV void stage_rows(char* lds, const bf16_t* src, long ld, int tid, int nt, int 
 // all P.V MFMAs -- the earlier tile-by-tile loop paid two dependent cross-lane reductions, the
 // rescale and a keep-bit OR-reduction per tile, and the kernel spent 60 % of its wave-cycles
 // waiting (PMC, profiles/r3_rejected_register_staging.txt).  Varlen key masks are arithmetic
-// (k < len), not an LDS table.  Keep bits go out lane-major: u16 [q][kt * 4 + g], bit 4 t + r =
-// key 64 kt + 16 t + 4 g + r -- each lane stores its own bits, no cross-lane OR.
+// (k < len), not an LDS table.  Keep bits go out lane-major: u16 [q / 4][kt * 4 + g][q % 4], bit
+// 4 t + r = key 64 kt + 16 t + 4 g + r -- each lane stores its own bits, no cross-lane OR, and the
+// backward's key-major phase reads the 4 consecutive query rows of a key word with ONE 8-byte read.
 // NW waves per block own query rows [blockIdx.x * 16 NW, + 16 NW): NW = 8 -> one block per
 // (sequence, head).  (NW = 4, two blocks per (sequence, head), measured no faster:
 // profiles/r4_rejected_ab.txt.)
@@ -656,9 +657,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_s128_kernel(AttnArgs a) {
       for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(tr_frag(vs + kt * 8192, 16 * dt, kk, lane), pf, o[dt]);
     }
   if (drop && a.dmask) {
-    uint16_t* dm = reinterpret_cast<uint16_t*>(a.dmask) + (((size_t)b * H + h) * 128 + q) * 8 + g;
+    uint16_t* dm = reinterpret_cast<uint16_t*>(a.dmask) + ((((size_t)b * H + h) * 32 + (q >> 2)) * 8 + g) * 4 + (q & 3);
     dm[0] = (uint16_t)kw[0];
-    dm[4] = (uint16_t)kw[1];
+    dm[16] = (uint16_t)kw[1];  // word 4 + g
   }
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -679,7 +680,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_s128_kernel(AttnArgs a) {
 
 // Phase 1 for this wave's 16 query rows (lane row q, read row qr = min(q, len - 1)): dQ from the
 // K / V images in LDS, the rows' Q / dO fragments, delta dl, lse2 and the forward's keep-bit words
-// (mrow_p[kt * 4] = this lane's u16 of key tile kt; null without stored keep bits).
+// (mrow_p[kt * 16] = this lane's u16 of key tile kt; null without stored keep bits).
 DEV void bwd_dq_rows(const AttnArgs& a, const char* ks, const char* vs, const float* kb, uint64_t vk0,
                      uint64_t vk1, const bf16x8 (&qf)[2], const bf16x8 (&dof)[2], float dl, float lse,
                      const uint16_t* mrow_p, int b, int h, int q, int len, int nt, size_t tok0, int lane) {
@@ -700,7 +701,7 @@ DEV void bwd_dq_rows(const AttnArgs& a, const char* ks, const char* vs, const fl
     for (int t = 0; t < 4; ++t) tv[t] = ((vk >> (16 * t)) & 0xffffull) != 0;
     const char* kst = ks + kt * 8192;
     const char* vst = vs + kt * 8192;
-    const uint32_t mrow = (drop && mrow_p) ? mrow_p[kt * 4] : 0u;  // this lane's keys 16 t + 4 g + r
+    const uint32_t mrow = (drop && mrow_p) ? mrow_p[kt * 16] : 0u;  // this lane's keys 16 t + 4 g + r
     f32x4 sc[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -803,13 +804,16 @@ DEV void bwd_dkv_keys(const AttnArgs& a, const char* qs, const char* os, const f
         const float4 lse4 = *reinterpret_cast<const float4*>(lse_s + qt * 64 + 16 * t + 4 * g);
         const float4 dl4 = *reinterpret_cast<const float4*>(dl_s + qt * 64 + 16 * t + 4 * g);
         const float lsev[4] = {lse4.x, lse4.y, lse4.z, lse4.w}, dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
+        // the key's words of the 4 query rows: one 8-byte LDS read
+        const uint64_t kq = (drop && mk16)
+            ? *reinterpret_cast<const uint64_t*>(mk16 + (((qt * 16 + 4 * t + g) * 8 + kword) << 2)) : 0ull;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ql = qt * 64 + 16 * t + 4 * g + r;
           const float pv = __builtin_amdgcn_exp2f(sc[t][r] * scale2 + kbias - lsev[r]);
           float dpv = dp[t][r], pdv = pv;
           if (drop) {
-            const bool keep = mk16 ? ((mk16[ql * 8 + kword] >> kbit) & 1u) != 0
+            const bool keep = mk16 ? ((kq >> (16 * r + kbit)) & 1ull) != 0
                                    : drop_keep(seed, (headidx + ql) * (uint32_t)S + key, a.drop_threshold);
             dpv = keep ? dpv * a.drop_scale : 0.f;
             pdv = keep ? pv : 0.f;  // (the dropout scale is applied to dV once, at the store)
@@ -873,7 +877,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   float* lse_s = kb + 128;
   float* dl_s = lse_s + 128;
   uint64_t* mk_s = reinterpret_cast<uint64_t*>(smem + 8 * 8192 + 3 * 512);  // the forward's keep bits
-  const uint16_t* mk16 = reinterpret_cast<const uint16_t*>(mk_s);  // [128 q][kt * 4 + g], bit 4 t + r
+  const uint16_t* mk16 = reinterpret_cast<const uint16_t*>(mk_s);  // [q / 4][kt * 4 + g][q % 4], bit 4 t + r
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
@@ -932,7 +936,8 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
     float dl = row_delta(of, dof);
     if (q >= qlen) dl = 0.f;  // (q_live: this row's O was never written -- it has no gradient)
     if (g == 0 && q < len) dl_s[q] = dl;
-    bwd_dq_rows(a, ks, vs, kb, vk0, vk1, qf, dof, dl, lse_s[qr], mk ? mk16 + qr * 8 + g : nullptr, b, h, q, len,
+    const uint16_t* mrow_p = mk ? mk16 + ((qr >> 2) * 8 + g) * 4 + (qr & 3) : nullptr;
+    bwd_dq_rows(a, ks, vs, kb, vk0, vk1, qf, dof, dl, lse_s[qr], mrow_p, b, h, q, len,
                 nt, tok0, lane);
   }
   ASTAMP(2);
