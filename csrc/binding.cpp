@@ -326,10 +326,7 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
   std::vector<const at::Tensor*> cs(n);
   std::vector<FdDwProb> pr(n);
   for (size_t i = 0; i < n; ++i) {
-    // A may be a column slice of a wider [K][lda] matrix (a problem split by output rows)
-    TORCH_CHECK(on_device(As[i]) && As[i].scalar_type() == at::kBFloat16 && As[i].dim() == 2 &&
-                    As[i].stride(1) == 1 && As[i].stride(0) >= As[i].size(1) && As[i].stride(0) % 8 == 0,
-                "gemm_dw_batch: A must be a bf16 GPU matrix with unit column stride (a column slice at most)");
+    need(As[i], at::kBFloat16, "A");
     need(Bs[i], at::kBFloat16, "B");
     need(Cs[i], at::kFloat, "C");
     TORCH_CHECK(As[i].dim() == 2 && Bs[i].dim() == 2 && Cs[i].dim() == 2, "gemm_dw_batch operands must be 2-D");
@@ -347,7 +344,6 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
     q.M = (int)As[i].size(1);
     q.N = (int)Bs[i].size(1);
     q.K = (int)Ki;
-    q.lda = (int)As[i].stride(0);
     q.accumulate = accumulate[i] ? 1 : 0;
   }
   std::vector<FdAdamEpi> ad(n);

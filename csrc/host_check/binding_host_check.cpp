@@ -109,9 +109,7 @@ int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const
     const long long mn = (long long)q.M * q.N;
     const long long Kq = q.K > 0 ? q.K : K;
     if (Kq % 64) hc::violations.push_back("dw_batch: K % 64");
-    const long long lda = q.lda > 0 ? q.lda : q.M;
-    if (lda < q.M) hc::violations.push_back("dw_batch: lda < M");
-    hc::span(q.A, ((Kq - 1) * lda + q.M) * 2, "dw_batch A");
+    hc::span(q.A, Kq * q.M * 2, "dw_batch A");
     hc::span(q.B, Kq * q.N * 2, "dw_batch B");
     if (q.shT) {
       if (!q.p || !q.sh || q.M % 8) hc::violations.push_back("dw_batch: W^T without its shadow's Adam");

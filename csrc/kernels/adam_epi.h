@@ -37,7 +37,6 @@ struct FdDwProb {
   int tile0;          // filled by the launcher
   int accumulate;
   int K;              // rows of A and B (0: the launch's K)
-  int lda;            // row pitch of A in elements (0: M) -- a problem may be a column slice of A
 };
 
 #define FD_LN_XSITES 128

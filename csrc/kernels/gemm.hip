@@ -1350,7 +1350,7 @@ DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
   p.A = q.A; p.B = q.B; p.C = q.C;
   const int K = q.K > 0 ? q.K : bt.K;
   p.M = q.M; p.N = q.N; p.K = K;
-  p.lda = q.lda > 0 ? q.lda : q.M; p.ldb = q.N; p.ldc = q.N;
+  p.lda = q.M; p.ldb = q.N; p.ldc = q.N;
   p.k_split = K;
   p.group_m = bt.group_m;
   p.diag = bt.diag;

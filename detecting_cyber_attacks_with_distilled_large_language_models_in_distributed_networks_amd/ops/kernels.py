@@ -169,45 +169,6 @@ def linear_dw2(dy0: torch.Tensor, x0: torch.Tensor, out0: torch.Tensor, dy1: tor
 DW_BATCH_MAX = 32  # problems per all-layer weight-gradient launch (csrc/kernels/gemm.hip DWB_MAXP)
 
 
-# The all-layer dW launch runs 256 x 256 tiles at one block per CU: with F full-K tiles on C CUs
-# the last round holds F % C tiles -- at the bs32 step 55 of 256 CUs (567 = 2 x 256 + 55), a whole
-# tile time for a fifth of the chip.  FD_DW_TAIL=1: those tiles' output rows (whole 256-row blocks,
-# taken from the end of the list) and the pruned block's short-K problems go to a second launch of
-# 128 x 128 tiles (FD_DW_TAIL_CFG), which runs them as one round of quarter-size tiles.
-DW_TAIL = _os.environ.get("FD_DW_TAIL", "0") == "1"
-DW_TAIL_CFG = int(_os.environ.get("FD_DW_TAIL_CFG", "1"))
-
-
-def _dw_tail_split(jobs: list):
-    """(main, tail) job lists for the tail launch, or None when the last round is not mostly empty."""
-    if not jobs or any(len(j) > 4 and j[4] is not None for j in jobs):
-        return None
-    if any(j[2].shape[0] % 256 or j[2].shape[1] % 256 for j in jobs):
-        return None
-    kmax = max(j[0].shape[0] for j in jobs)
-    big = [j for j in jobs if j[0].shape[0] == kmax]
-    small = [j for j in jobs if j[0].shape[0] < kmax]
-    C = _cu_count()
-    F = sum((j[2].shape[0] // 256) * (j[2].shape[1] // 256) for j in big)
-    R = F % C
-    if F < C or R == 0 or R > C // 2:
-        return None
-    main, tail, moved = list(big), [], 0
-    while moved < R and main:
-        dy, x, out, acc = main.pop()[:4]
-        per_rb, rbs = out.shape[1] // 256, out.shape[0] // 256
-        need = -(-(R - moved) // per_rb)
-        if need >= rbs:
-            tail.append((dy, x, out, acc))
-            moved += rbs * per_rb
-            continue
-        r0 = (rbs - need) * 256
-        main.append((dy[:, :r0], x, out[:r0], acc))
-        tail.append((dy[:, r0:], x, out[r0:], acc))
-        moved += need * per_rb
-    return main, tail[::-1] + small
-
-
 def linear_dw_batch(jobs: list, adam=None, cfg: int = -1):
     """Every weight gradient of a backward in one launch per 32 problems: for each job
     (dy [K, M], x [K, N], out [M, N] fp32, accumulate[, wT]) out (+)= dy^T x.  No split-K: each
@@ -216,12 +177,6 @@ def linear_dw_batch(jobs: list, adam=None, cfg: int = -1):
     optimizer step to each finished gradient tile instead of storing it; a job's optional wT
     (bf16 [N, M]) is then refreshed by the same epilogue with the updated weights transposed (the
     next step's dX GEMMs read it: no transpose launch)."""
-    if DW_TAIL and cfg in (-1, 11) and len(jobs) <= DW_BATCH_MAX:
-        split = _dw_tail_split(jobs)
-        if split is not None:
-            linear_dw_batch(split[0], adam, 11)
-            linear_dw_batch(split[1], adam, DW_TAIL_CFG)
-            return
     for i in range(0, len(jobs), DW_BATCH_MAX):
         chunk = jobs[i:i + DW_BATCH_MAX]
         outs = [j[2] for j in chunk]

@@ -139,51 +139,3 @@ def test_colsum_partials_batched_kernel():
     for x, a, b in zip(xs, outs_a, outs_b):
         assert torch.equal(a + 1.0, b)
         assert ((a - x.float().sum(0)).abs().max() / x.float().sum(0).abs().max()).item() < 1e-5
-
-
-def test_dw_tail_launch_bitwise_equals_single_launch():
-    """FD_DW_TAIL: the last, mostly empty round of 256 x 256 tiles (and the pruned block's short-K
-    problems) goes to a second launch of 128 x 128 tiles.  Every output element accumulates the
-    same K products in the same order and takes the same fused Adam step: bitwise equal."""
-    g = torch.Generator(device="cuda").manual_seed(9)
-    T, Tc = 2688, 64
-    shapes = [(2304, 768, T), (768, 768, T), (3072, 768, T), (768, 3072, T)] * 5 + \
-        [(2304, 768, T), (768, 768, Tc), (3072, 768, Tc), (768, 3072, Tc)]  # the step's 24 problems
-    jobs, base = [], []
-    for M, N, Kr in shapes:
-        dy = (torch.randn(Kr, M, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
-        x = torch.randn(Kr, N, device="cuda", generator=g).to(torch.bfloat16)
-        jobs.append((dy, x, torch.empty(M, N, device="cuda"), False))
-        base.append([torch.randn(M, N, device="cuda", generator=g), torch.rand(M, N, device="cuda", generator=g) * 1e-3,
-                     torch.rand(M, N, device="cuda", generator=g) * 1e-6])
-    split = K._dw_tail_split(jobs)
-    F = sum((M // 256) * (N // 256) for M, N, Kr in shapes if Kr == T)
-    if F % K._cu_count() in range(1, K._cu_count() // 2 + 1):
-        assert split is not None and sum(o.numel() for _, _, o, _ in split[0] + split[1]) == \
-            sum(o.numel() for _, _, o, _ in jobs)
-    arms = []
-    for tail in (False, True):
-        st = [[t.clone() for t in b] + [b[0].to(torch.bfloat16)] for b in base]
-        step = torch.full((1,), 2, dtype=torch.int32, device="cuda")
-        views = {j[2].data_ptr(): i for i, j in enumerate(jobs)}
-
-        def adam(outs, n_wT=0, st=st, step=step):
-            flat = []
-            for o in outs:  # the state slice under each (possibly row-sliced) gradient view
-                i = next(k for p0, k in views.items()
-                         if p0 <= o.data_ptr() < p0 + jobs[k][2].numel() * 4)
-                r0 = (o.data_ptr() - jobs[i][2].data_ptr()) // (4 * o.shape[1])
-                flat += [t[r0:r0 + o.shape[0]] for t in st[i]]
-            return flat + [step], [1e-3, 0.9, 0.999, 1e-8, 0.0, 0.0]
-
-        old = K.DW_TAIL
-        K.DW_TAIL = tail
-        try:
-            K.linear_dw_batch(jobs, adam=adam)
-        finally:
-            K.DW_TAIL = old
-        torch.cuda.synchronize()
-        arms.append(st)
-    for a, b in zip(*arms):
-        for x, y in zip(a, b):
-            assert torch.equal(x, y)
