@@ -33,7 +33,6 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
                long long workspace_elems, int accumulate, const FdAdamEpi* adam,
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
-int fd_gemm_set_da(int id);
 int fd_gemm_stamps(unsigned long long* host, int nblocks);
 int fd_attn_stamps(unsigned long long* host, int nblocks);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
@@ -1230,7 +1229,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, py::arg("kind"), py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"),
         py::arg("aux"), py::arg("res"), py::arg("workspace"), py::arg("accumulate"), py::arg("aux_out") = py::none());
   m.def("gemm_set_cfg", &gemm_set_cfg);
-  m.def("gemm_set_da", [](int64_t id) { check_rc(fd_gemm_set_da((int)id), "gemm_set_da"); });
   m.def("gemm_stamps", &gemm_stamps);
   m.def("attn_stamps", &attn_stamps);
   m.def("gemm_splitk", &gemm_splitk, py::arg("epi"), py::arg("A"), py::arg("Bt"), py::arg("C"), py::arg("workspace"),

@@ -100,7 +100,6 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
   return 0;
 }
 int fd_gemm_dw2_splits(int, int, int, int, int) { return 1; }
-int fd_gemm_set_da(int) { return 0; }
 int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg, hipStream_t) {
   ++hc::calls;
   if (n <= 0 || n > 32) hc::violations.push_back("dw_batch: problem count");

@@ -539,9 +539,9 @@ constexpr int LN_MAXK = 4;  // column tiles per row block <= LN_MAXK * (BN / 8)
 constexpr int LN_MAX_TILES = 256;
 
 // The per-thread operands of the LayerNorm epilogue's element math (a thread owns IT rows x 8
-// columns): residual, backward z / mean / rstd, dropout-hash rows, gamma, the exchange tag.  The
-// direct-A kernels load them during their last K tiles (gemm_ln_da_kernel), the LDS-DMA kernels
-// right after their K loop (their inline-asm ring waits would count these loads as ring tiles).
+// columns): residual, backward z / mean / rstd, dropout-hash rows, gamma, the exchange tag --
+// LDS-DMA'd under the last K tiles (ln_dma), or loaded right after the K loop (their ring's
+// inline-asm waits would count VGPR loads issued inside the loop as ring tiles).
 template <int IT>
 struct LnPre {
   uint4 res_v[IT], z_v[IT];
@@ -1148,176 +1148,6 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_ln_kernel(GemmParams p) 
 #endif
 }
 
-// ---------------------------------------------------------------- direct-A K loop (round 4)
-// The one-round NT GEMMs (M ~ 2.7 k packed tokens) were bound by getting operand bytes into the
-// CU: 24 KiB per 64-deep K tile of a 128 x 64 tile, and LDS-DMA fills only 77-88 GB/s per CU with
-// 8 waves against ~108 GB/s for plain global loads into VGPRs (profiles/r3_l2_fill.txt); the K
-// loop ran at ~64 GB/s.  Here a block of WM waves (WN = 1) owns BM x BN; wave w owns TM = BM / WM
-// rows and all BN columns, so no two waves share an A row:
-//  * A (the activations, 2/3 of the bytes) goes global -> VGPRs straight in MFMA fragment layout
-//    (lane l: row l & 15, 8 consecutive k = 16 contiguous bytes) -- no LDS write, no LDS read;
-//  * B (BN weight rows x 64 k) goes global -> VGPRs -> one ds_write_b128 per thread into a
-//    double-buffered swizzled LDS slot (the K-major image of Operand<.., true, ..>) and is read
-//    as fragments by every wave;
-//  * both through a D-deep register ring: tile t + D is requested while tile t computes, every
-//    load compiler-visible, so hipcc's counted vmcnt waits are exact (no inline-asm DMA whose
-//    waits it cannot see); one barrier per K tile.
-// nk % D == 0 and nk >= D (the host falls back to the LDS-DMA kernels otherwise).
-template <int BM, int BN, int WM, int D>
-struct DaCfg {
-  static constexpr int NW = WM;
-  static constexpr int TM = BM / WM;
-  static constexpr int MI = TM / 16, NI = BN / 16;
-  static constexpr int BSLOT = BN * BKT * 2;                // one B slot: BN rows x 128 B
-  static constexpr int BCH = BN * (BKT / 8) / (64 * NW);    // 16-byte B chunks per thread per tile
-  static constexpr int KBYTES = 2 * BSLOT;
-  static_assert(TM % 16 == 0 && BN % 16 == 0 && BCH >= 1 && BCH * 64 * NW * 8 == BN * BKT && D % 2 == 0,
-                "direct-A tile");
-};
-
-// BKM: B K-major (B(k, n) = B[n * ldb + k]: a W^T copy / the NT weight) or MN-major (B(k, n) =
-// B[k * ldb + n]: the dX GEMMs reading the weight W itself -- its LDS image is the [64 k][SUB n]
-// swizzled one of Operand<.., false, ..>, read with the transposing ds_read_b64_tr_b16).
-// before_tail(): called once every load of the K loop has been issued, before the last D tiles
-// compute -- the epilogue's own global loads go there, so their latency hides under those tiles.
-struct NoTail {
-  DEV void operator()() const {}
-};
-
-template <int BM, int BN, int WM, int D, bool BKM = true, typename Tail = NoTail>
-DEV void da_kloop(const GemmParams& p, int m0, int n0, char* smem, f32x4 (&acc)[BM / WM / 16][BN / 16],
-                  Tail before_tail = Tail()) {
-  using C = DaCfg<BM, BN, WM, D>;
-  using OB = Operand<BN, BKM, WM>;
-  constexpr int MI = C::MI, NI = C::NI, TM = C::TM, BCH = C::BCH;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nk = p.K / BKT;
-  const bf16_t* pa[MI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int r = min(m0 + wid * TM + i * 16 + (lane & 15), p.M - 1);  // (clamped rows are never stored)
-    pa[i] = p.A + (size_t)r * p.lda + 8 * (lane >> 4);
-  }
-  const bf16_t* pb[BCH];
-  int bo[BCH];
-#pragma unroll
-  for (int c = 0; c < BCH; ++c) {
-    const int id = tid + c * 64 * C::NW;
-    if constexpr (BKM) {  // 8 lanes = one weight row's 128 contiguous bytes of the K tile
-      const int n = id >> 3, ch = id & 7;
-      pb[c] = p.B + (size_t)(n0 + n) * p.ldb + ch * 8;
-      bo[c] = n * 128 + ((ch ^ ksw(n)) << 4);
-    } else {              // BN / 8 lanes = one k row's BN contiguous columns
-      constexpr int CPRB = BN / 8;
-      const int k = id / CPRB, n = (id % CPRB) * 8;
-      pb[c] = p.B + (size_t)k * p.ldb + n0 + n;
-      bo[c] = (n / OB::SUB) * OB::SUB_BYTES + k * OB::SUB * 2 + ((((n % OB::SUB) >> 3) ^ fk<OB::SUB>(k)) << 4);
-    }
-  }
-  const size_t bstep = BKM ? (size_t)BKT : (size_t)BKT * p.ldb;  // B elements per K tile
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // One register ring for both operands (slots 0 .. 2 MI - 1: A fragments [i][s], then BCH B
-  // chunks): kept as ONE ext-vector array so hipcc promotes it to VGPRs (a separate small B ring
-  // went to scratch).
-  constexpr int RS = 2 * MI + BCH;
-  bf16x8 ring[D][RS];
-  auto load = [&](int t, bf16x8 (&r)[RS]) {
-#pragma unroll
-    for (int c = 0; c < BCH; ++c) r[2 * MI + c] = *reinterpret_cast<const bf16x8*>(pb[c] + t * bstep);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) r[2 * i + s] = *reinterpret_cast<const bf16x8*>(pa[i] + t * BKT + s * 32);
-  };
-  // tile in ring slot d (LDS slot d & 1: tiles alternate parity since D is even)
-  auto compute = [&](int d, const bf16x8 (&r)[RS]) {
-    char* slot = smem + (d & 1) * C::BSLOT;
-#pragma unroll
-    for (int c = 0; c < BCH; ++c) *reinterpret_cast<bf16x8*>(slot + bo[c]) = r[2 * MI + c];
-    // this tile's B is in LDS for every wave; every wave is done reading this slot's previous
-    // tile (two tiles ago: it passed the previous tile's barrier after its fragment reads)
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 bf[NI];
-#pragma unroll
-      for (int j = 0; j < NI; ++j) bf[j] = OB::frag(slot, j * 16, s, lane);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(bf[j], r[2 * i + s], acc[i][j]);
-    }
-  };
-#pragma unroll
-  for (int d = 0; d < D; ++d) load(d, ring[d]);
-  for (int t0 = 0; t0 < nk - D; t0 += D) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      compute(d, ring[d]);
-      load(t0 + d + D, ring[d]);
-    }
-  }
-  before_tail();
-#pragma unroll
-  for (int d = 0; d < D; ++d) compute(d, ring[d]);
-  __syncthreads();  // every wave is done with the B slots: the epilogue may reuse the LDS
-}
-
-template <int BM, int BN, int EPI, int WM, int D>
-struct DaKern {
-  using TR = EpiTraits<EPI, BM, BN>;
-  static constexpr int SMEM = DaCfg<BM, BN, WM, D>::KBYTES > TR::BYTES ? DaCfg<BM, BN, WM, D>::KBYTES : TR::BYTES;
-  static constexpr bool VALID = SMEM <= LDS_MAX && !TR::DIRECT && EPI != EPI_F32 && (!TR::LN || TR::F32S);
-};
-
-// Plain NT / NN GEMM (y = x W^T, dx = dy W; + epilogue) on the direct-A K loop.
-template <int BM, int BN, int EPI, int WM, int D, bool BKM = true>
-__global__ __launch_bounds__(64 * WM, 2) void gemm_da_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(1024))) char smem[DaKern<BM, BN, EPI, WM, D>::SMEM];
-  FD_STAMP(0);
-  stamp_hwid();
-  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = p.N / BN;
-  int tm, tn;
-  tile_coords(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, p.group_m, tm, tn);
-  f32x4 acc[BM / WM / 16][BN / 16];
-  da_kloop<BM, BN, WM, D, BKM>(p, tm * BM, tn * BN, smem, acc);
-  FD_STAMP(2);
-  const int tid = threadIdx.x;
-  staged_epilogue<BM, BN, BM / WM, BN, EPI, 64 * WM>(p, acc, smem, tm * BM, tn * BN, tid >> 6, 0, tid & 63, tid);
-#if FD_GEMM_STAMPS
-  __syncthreads();
-  FD_STAMP(5);
-#endif
-}
-
-// LayerNorm-fused NT GEMM on the direct-A K loop (row-major tile order: a row block's tiles are
-// consecutive logical tiles, so after the XCD remap they run on one XCD, in order).
-template <int BM, int BN, int EPI, int WM, int D, bool BKM = true>
-__global__ __launch_bounds__(64 * WM, 2) void gemm_ln_da_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(1024))) char smem[DaKern<BM, BN, EPI, WM, D>::SMEM];
-  FD_STAMP(0);
-  stamp_hwid();
-  const int tiles_n = p.N / BN;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = lid / tiles_n, tn = lid % tiles_n;
-  f32x4 acc[BM / WM / 16][BN / 16];
-  const int tid = threadIdx.x;
-  LnPre<BM * (BN / 8) / (64 * WM)> pre;
-  // the epilogue's residual / z / mean / rstd / gamma loads are issued under the last K tiles
-  da_kloop<BM, BN, WM, D, BKM>(p, tm * BM, tn * BN, smem, acc,
-                               [&] { pre = ln_prefetch<BM, BN, EPI == EPI_LN_BWD, 64 * WM>(p, tm, tn, tid); });
-  FD_STAMP(2);
-  ln_epilogue<BM, BN, BM / WM, BN, EPI == EPI_LN_BWD, 64 * WM>(p, acc, smem, tm, tn, tid >> 6, 0, tid & 63, tid, pre);
-#if FD_GEMM_STAMPS
-  __syncthreads();
-  FD_STAMP(5);
-#endif
-}
-
 // ---------------------------------------------------------------- all-layer weight gradients
 // Every weight gradient of a backward pass in ONE launch, at the end of the backward
 // (RunCtx.dw_batch, ops/functional.py): C_i[M_i][N_i] (+)= A_i^T B_i over the same token
@@ -1556,8 +1386,8 @@ int pick_cfg(int kind, int M, int N, int K) {
     return K >= 2048 ? 0 : 8;
   }
   if (kind == 1) {  // NN dX (on the weight W itself: MN-major B through the transposing LDS reads)
-    // the NT rules above, measured equal per configuration (round 4, scripts/da_bench.py
-    // DX_LAYOUTS: the LayerNorm-fused dX reads W as fast as W^T on cfg 24)
+    // the NT rules above, measured equal per configuration (round 4, profiles/r4_ab_dx_layouts.txt:
+    // the LayerNorm-fused dX reads W as fast as W^T on cfg 24)
     if (N % 192 == 0 && N >= 3072 && M >= 3584) return 3;
     if (N % 128 == 0 && N >= 3072 && M >= 2048) return 1;
     if (N % 192 == 0 && N >= 1536 && M >= 2048) return 6;
@@ -1566,61 +1396,6 @@ int pick_cfg(int kind, int M, int N, int K) {
     return 8;
   }
   return (N % 128 == 0 && M > 1024 && M < 3072 && N < 3072) ? 1 : 8;  // TN dW
-}
-
-// Direct-A NT GEMMs (gemm_da_kernel): FD_GEMM_DA=<id> selects them for the kind-0 launches
-// (50: 128 x 64 on 8 waves, 52: 128 x 128 on 8 waves -- 16 rows x all columns per wave);
-// unset / -1 = off.  K / 64 must be a multiple of the ring depth (4).
-int g_da = -2;  // FD_GEMM_DA / fd_gemm_set_da
-int da_cfg(int M, int N, int K) {
-  if (g_da == -2) {
-    const char* e = getenv("FD_GEMM_DA");
-    g_da = e ? atoi(e) : -1;
-  }
-  if (g_da < 0 || (K / BKT) % 4 || K / BKT < 4 || M < 128) return -1;
-  if (g_da == 52 && N % 128 == 0) return 52;
-  return N % 64 == 0 ? 50 : -1;
-}
-
-template <int BM, int BN, int EPI, int WM, int D, bool BKM>
-bool launch_da_cfg(const GemmParams& p, hipStream_t st) {
-  if constexpr (!DaKern<BM, BN, EPI, WM, D>::VALID) {
-    return false;
-  } else {
-    if (p.N % BN) return false;
-    const int tiles = ((p.M + BM - 1) / BM) * (p.N / BN);
-    hipLaunchKernelGGL((gemm_da_kernel<BM, BN, EPI, WM, D, BKM>), dim3(tiles), dim3(64 * WM), 0, st, p);
-    return true;
-  }
-}
-
-template <int EPI, bool BKM>
-bool launch_da_id(const GemmParams& p, int id, hipStream_t st) {
-  switch (id) {
-    case 50: return launch_da_cfg<128, 64, EPI, 8, 4, BKM>(p, st);
-    case 52: return launch_da_cfg<128, 128, EPI, 8, 4, BKM>(p, st);
-  }
-  return false;
-}
-
-// bkm: B K-major (kind 0, NT) or MN-major (kind 1, NN: the dX GEMMs on the weight itself)
-bool launch_da(int epi, const GemmParams& p, int id, bool bkm, hipStream_t st) {
-  if (bkm) {
-    switch (epi) {
-      case EPI_BF16: return launch_da_id<EPI_BF16, true>(p, id, st);
-      case EPI_BIAS: return launch_da_id<EPI_BIAS, true>(p, id, st);
-      case EPI_BIAS_GELU: return launch_da_id<EPI_BIAS_GELU, true>(p, id, st);
-      case EPI_GELU_BWD: return launch_da_id<EPI_GELU_BWD, true>(p, id, st);
-      case EPI_ADD: return launch_da_id<EPI_ADD, true>(p, id, st);
-    }
-    return false;
-  }
-  switch (epi) {
-    case EPI_BF16: return launch_da_id<EPI_BF16, false>(p, id, st);
-    case EPI_GELU_BWD: return launch_da_id<EPI_GELU_BWD, false>(p, id, st);
-    case EPI_ADD: return launch_da_id<EPI_ADD, false>(p, id, st);
-  }
-  return false;
 }
 
 template <bool AK, bool BKM>
@@ -1699,13 +1474,6 @@ int fd_gemm_stamps(unsigned long long* host, int nblocks) {
 #endif
 }
 
-// Direct-A NT GEMMs for the kind-0 launches: 50 / 52 (see da_cfg), -1 = off (tests / A/B).
-int fd_gemm_set_da(int id) {
-  if (id != -1 && id != 50 && id != 52) return 1;
-  g_da = id;
-  return 0;
-}
-
 // Force a configuration id / split count for a GEMM kind (tuning; -1 = auto).
 int fd_gemm_set_cfg(int kind, int cfg, int splits) {
   if (kind < 0 || kind > 2 || cfg < -1 || cfg >= NCFG || (cfg >= 0 && !cfg_instantiated(cfg))) return 1;
@@ -1756,14 +1524,6 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
     if (e) gm = atoi(e);
     p.group_m = std::max(1, gm);
   }
-  // direct-A kernels (da_cfg; 128-row tiles with the staged-fp32 epilogue, so column sums too)
-  const int da = (kind == 0 || kind == 1) ? da_cfg(M, N, K) : -1;
-  if (colsum && da >= 0 && (epi == EPI_GELU_BWD || epi == EPI_ADD)) {
-    p.colsum = colsum;
-    if (colsum_blocks) *colsum_blocks = (M + 127) / 128;
-    if (launch_da(epi, p, da, kind == 0, st)) return 0;
-    p.colsum = nullptr;
-  }
   if (colsum) {
     // only the staged-fp32 epilogues sum columns: 128 x {128, 64} tiles (never 256-row ones)
     if (epi != EPI_GELU_BWD && epi != EPI_ADD) return 2;
@@ -1781,13 +1541,11 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
   // (NN launches fall back to cfg 8 below when the picked tile does not fit; that keeps 128 x 64)
   if (kind == 0) {  // also dX = dy (W^T)^T with a transposed weight copy: GELU' / residual epilogues
     if (epi == EPI_F32) return 2;
-    if (da >= 0 && !colsum && launch_da(epi, p, da, true, st)) return 0;
     if (launch_epi<true, true>(epi, p, id, 1, st)) return 0;
     return launch_epi<true, true>(epi, p, 0, 1, st) ? 0 : 2;  // 128x64 fits any N % 64 == 0
   }
   if (kind == 1) {
     if (epi != EPI_BF16 && epi != EPI_GELU_BWD && epi != EPI_ADD) return 2;
-    if (da >= 0 && !colsum && launch_da(epi, p, da, false, st)) return 0;
     if (launch_epi<true, false>(epi, p, id, 1, st)) return 0;
     return launch_epi<true, false>(epi, p, 0, 1, st) ? 0 : 2;
   }
@@ -2004,9 +1762,6 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
     static const int env = [] { const char* e = getenv("FD_GEMM_LN_CFG"); return e ? atoi(e) : -1; }();
     id = env >= 0 ? env : (M <= 64 && smallm_tiles() ? 13 : 24);
   }
-  // direct-A K loop (cfg 50: 8 waves x 16 rows, 51: 4 waves x 32 rows; 4-deep register ring) needs
-  // K / 64 to be a multiple of the ring depth; otherwise the LDS-DMA configuration
-  if (id >= 50 && ((K / BKT) % 4 || K / BKT < 4)) id = 24;
   const int bm = id == 13 ? 64 : 128, bn = 64;
   if (N / bn > LN_MAXK * (bn / 8)) return -2;
   {
@@ -2044,26 +1799,6 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
     else go(gemm_ln_kernel<BM_, BN_, EPI_LN, WM_, WN_, S_>, 64 * WM_ * WN_);           \
     break;
   switch (id) {
-    case 50:
-      if (b_mn) {  // (the dX GEMMs only: LayerNorm backward)
-        if (!bwd) return -6;
-        go(gemm_ln_da_kernel<128, 64, EPI_LN_BWD, 8, 4, false>, 512);
-      } else if (bwd) {
-        go(gemm_ln_da_kernel<128, 64, EPI_LN_BWD, 8, 4>, 512);
-      } else {
-        go(gemm_ln_da_kernel<128, 64, EPI_LN, 8, 4>, 512);
-      }
-      break;
-    case 51:
-      if (b_mn) {
-        if (!bwd) return -6;
-        go(gemm_ln_da_kernel<128, 64, EPI_LN_BWD, 4, 4, false>, 256);
-      } else if (bwd) {
-        go(gemm_ln_da_kernel<128, 64, EPI_LN_BWD, 4, 4>, 256);
-      } else {
-        go(gemm_ln_da_kernel<128, 64, EPI_LN, 4, 4>, 256);
-      }
-      break;
     FD_LN_CASE(24, 128, 64, 4, 2, 6)
     FD_LN_CASE(0, 128, 64, 2, 2, 3)
     FD_LN_CASE(18, 128, 64, 4, 2, 3)

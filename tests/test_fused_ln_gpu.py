@@ -48,11 +48,10 @@ def state_clean(M):
     return int(err.item()) == 0 and int(cnt[0].item()) > 0
 
 
-@pytest.fixture(params=[-1, 0, 18, 50, 51])
+@pytest.fixture(params=[-1, 0, 18])
 def ln_cfg(request, monkeypatch):
-    """Every instantiated LayerNorm-fused tile configuration (gemm.hip fd_gemm_ln): the default,
-    the 4- / 8-wave 3-slot LDS-DMA rings, and the direct-A K loops (50: 8 waves x 16 rows,
-    51: 4 waves x 32 rows; shapes whose K / 64 is no multiple of 4 fall back)."""
+    """Every instantiated LayerNorm-fused tile configuration (gemm.hip fd_gemm_ln): the default
+    (cfg 24, 6-slot ring with the LDS-DMA'd epilogue operands) and the 4- / 8-wave 3-slot rings."""
     monkeypatch.setattr(kn, "LN_CFG", request.param)
     return request.param
 

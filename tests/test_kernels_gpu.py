@@ -547,36 +547,3 @@ def test_gelu_bwd_rematerialises_activation(M, N, K):
     out = torch.full_like(u, float("nan"))
     du = kn.linear_dx(dy, w2, gelu_u=u, wt=wt, colsum=(jobs, bgrad, False), aux_out=out)
     assert torch.equal(out, g) and torch.equal(du, base)
-
-
-@pytest.fixture(params=[50, 52])
-def direct_a(request):
-    """The direct-A NT GEMMs (gemm.hip gemm_da_kernel: A straight into VGPR fragments, B through
-    a double-buffered LDS slot, 4-deep register ring), forced on for the kind-0 launches."""
-    kn.ext().gemm_set_da(request.param)
-    yield request.param
-    kn.ext().gemm_set_da(-1)
-
-
-@pytest.mark.parametrize("M,N,K", [(2688, 768, 768), (2688, 2304, 768), (2688, 3072, 768), (2600, 768, 3072),
-                                   (300, 768, 2304), (4096, 3072, 768)])
-def test_gemm_direct_a_epilogues(M, N, K, direct_a):
-    x, w = bf(M, K, seed=31), bf(N, K, scale=0.05, seed=32)
-    b = torch.randn(N, device=DEV) * 0.1
-    ref = x.float() @ w.float().t()
-    assert rel_err(kn.linear_fwd(x, w, None), ref) < 1e-2                     # EPI_BF16
-    assert rel_err(kn.linear_fwd(x, w, b), ref + b) < 1e-2                     # EPI_BIAS
-    g, u = kn.linear_fwd(x, w, b, gelu=True)                                   # EPI_BIAS_GELU
-    assert rel_err(u, ref + b) < 1e-2
-    assert rel_err(g, torch.nn.functional.gelu(u.float())) < 1e-2
-    # dX GEMMs on a transposed weight copy: GELU' and residual epilogues
-    wt = w.t().contiguous()                                                    # a [K, N] weight; w = its W^T
-    dy = bf(M, K, seed=33)
-    uu = bf(M, N, seed=34)
-    dref = dy.float() @ wt.float()
-    dx = kn.linear_dx(dy, wt, gelu_u=uu, wt=w)
-    gp = uu.float()
-    cdf = 0.5 * (1 + torch.erf(gp / math.sqrt(2)))
-    assert rel_err(dx, dref * (cdf + gp * torch.exp(-0.5 * gp * gp) / math.sqrt(2 * math.pi))) < 2e-2
-    res = bf(M, N, seed=35)
-    assert rel_err(kn.linear_dx(dy, wt, res=res, wt=w), dref + res.float()) < 1e-2
