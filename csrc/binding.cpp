@@ -944,7 +944,9 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
   if (packed) need(*cu, at::kInt, "cu");
   TORCH_CHECK(S <= P && (packed || T % S == 0), "emb_bwd: S / layout");
   const int64_t nseq = packed ? cu->numel() - 1 : T / S;
-  TORCH_CHECK(dword.numel() == V * D && dpos.numel() == P * D && work.numel() >= std::max<int64_t>(T * D, std::min<int64_t>(256, (T + 7) / 8) * 3 * D),
+  // work: [T][D] word-gradient pieces, then the [min(256, ceil(T / 8))][3][D] LayerNorm partials
+  TORCH_CHECK(dword.numel() == V * D && dpos.numel() == P * D &&
+                  work.numel() >= T * D + std::min<int64_t>(256, (T + 7) / 8) * 3 * D,
               "emb_bwd: grad/work sizes");
   check_rc(fd_emb_bwd(dy.data_ptr(), ids.data_ptr(), ids.scalar_type() == at::kLong,
                       reinterpret_cast<const long long*>(sorted.data_ptr()),

@@ -320,10 +320,23 @@ int fd_emb_fwd(const void*, int, const void*, const void*, const float*, const f
   if ((sorted == nullptr) != (perm == nullptr)) hc::violations.push_back("emb_fwd: sorted without perm");
   return 0;
 }
-int fd_emb_bwd(const void*, const void*, int, const long long*, const long long*, const void*, const void*,
-               const float*, const float*, const float*, float*, float*, float*, float*, float*, float*, int, int, int,
-               int, int, int, const uint32_t*, uint32_t, uint32_t, float, int, unsigned char*, unsigned char*,
-               const int*, const int*, hipStream_t) { ++hc::calls; return 0; }
+int fd_emb_bwd(const void* dy, const void*, int, const long long* sorted, const long long* perm, const void*,
+               const void*, const float*, const float*, const float*, float* dword, float* dpos, float*, float*,
+               float* dz, float* work, int T, int, int, int P, int V, int D, const uint32_t*, uint32_t, uint32_t, float,
+               int, unsigned char* now, unsigned char* ever, const int*, const int*, hipStream_t) {
+  ++hc::calls;
+  hc::span(dy, (long long)T * D * 2, "emb_bwd dy");
+  hc::span(sorted, (long long)T * 8, "emb_bwd sorted");
+  hc::span(perm, (long long)T * 8, "emb_bwd perm");
+  hc::span(dz, (long long)T * D * 4, "emb_bwd dz");
+  // word-gradient pieces [T][D], then the LayerNorm partials [min(256, ceil(T / 8))][3][D]
+  hc::span(work, ((long long)T * D + (long long)std::min(256, (T + 7) / 8) * 3 * D) * 4, "emb_bwd work");
+  hc::span(dword, (long long)V * D * 4, "emb_bwd dword");
+  hc::span(dpos, (long long)P * D * 4, "emb_bwd dpos");
+  hc::opt_span(now, V, "emb_bwd now");
+  hc::opt_span(ever, V, "emb_bwd ever");
+  return 0;
+}
 int fd_gather_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int n, int d_bytes,
                     hipStream_t) {
   ++hc::calls;
@@ -731,6 +744,18 @@ int main() {
     expect_reject("adam rows flags", [&] { adam_rows(p, g, m, v, sh, step, 2e-5, 0.9, 0.999, 1e-8, ever_small, now,
                                                      64); });
     expect_reject("adam rows row_len", [&] { adam_rows(p, g, m, v, sh, step, 2e-5, 0.9, 0.999, 1e-8, ever, now, 6); });
+  }
+  // ---- embedding backward (work = pieces + LayerNorm partials)
+  {
+    const int64_t Tn = 2688, D = 768, V = 1000, P = 512;
+    auto dy = T_({Tn, D}, bf), ids = T_({Tn}, i64), srt = T_({Tn}, i64), prm = T_({Tn}, i64);
+    auto word = T_({V, D}, bf), pos = T_({P, D}, bf), ga = T_({D}, f32), mean = T_({Tn}, f32), rstd = T_({Tn}, f32);
+    auto dword = T_({V, D}, f32), dpos = T_({P, D}, f32), dg = T_({D}, f32), db = T_({D}, f32), dz = T_({Tn, D}, f32);
+    auto work = T_({Tn * D + 256 * 3 * D}, f32), work_small = T_({Tn * D}, f32), seed = T_({1}, i32);
+    expect_ok("emb bwd", [&] { emb_bwd(dy, ids, srt, prm, word, pos, ga, mean, rstd, dword, dpos, dg, db, dz, work,
+                                       128, seed, 1, 0, 1.0, false, none, none, none, none); });
+    expect_reject("emb bwd work", [&] { emb_bwd(dy, ids, srt, prm, word, pos, ga, mean, rstd, dword, dpos, dg, db, dz,
+                                                work_small, 128, seed, 1, 0, 1.0, false, none, none, none, none); });
   }
   // ---- unpadded layout
   {

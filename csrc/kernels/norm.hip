@@ -289,6 +289,10 @@ struct EmbArgs {
   long long* sorted;
   long long* perm;
   int sort_blocks;
+  // backward only (nullable): the word-gradient row flags to clear ([V] bytes) before the tail
+  // launch sets this step's (first write of a step's gradient)
+  unsigned char* now_clear;
+  int V;
 };
 
 DEV int padded_row(const EmbArgs& a, int row) { return a.row_map ? max(a.row_map[row], 0) : row; }
@@ -413,6 +417,8 @@ __global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
   float dg[NC][4] = {}, db[NC][4] = {};
   const int nw = blockDim.x >> 6;
+  if (a.now_clear)
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.V; i += gridDim.x * blockDim.x) a.now_clear[i] = 0;
   for (int row = blockIdx.x * nw + w; row < a.T; row += gridDim.x * nw) {
     const long id = load_id(a, row);
     const int prow = padded_row(a, row);
@@ -470,20 +476,13 @@ __global__ __launch_bounds__(512) void emb_bwd_kernel(EmbArgs a) {
 // padded layout's extra terms are exact zeros, so both layouts give the same sums.
 // grid (S, D/256): a block sums one position over the batch for 64 float4 columns, its 4
 // thread groups taking every 4th sequence (8 loads in flight each), combined in a fixed order.
-// Rows s < S: position gradient (sum over sequences).  Rows S <= s < gridDim.x (first write
-// only): zero -- those positions never occur.  Also clears the `now` row flags (V bytes) the
-// word-gradient kernels set next, so neither needs a memset launch of its own.
+// Rows s < S: position gradient (sum over sequences).  Rows S <= s (first write only): zero --
+// those positions never occur.  Block (s, cy) of a (rows, gy) grid.
 constexpr int PG_GROUPS = 4, PG_COLS = 64;  // per block: 64 float4 columns x 4 sequence groups
-__global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* dpos, int B, int S, int D,
-                                                       int accumulate, const int* cu, unsigned char* now, int V) {
-  const int s = blockIdx.x;
-  if (now) {
-    const long long nthr = (long long)gridDim.x * gridDim.y * 256;
-    for (long long i = ((long long)blockIdx.x * gridDim.y + blockIdx.y) * 256 + threadIdx.x; i < V; i += nthr)
-      now[i] = 0;
-  }
+DEV void pos_grad_block(int s, int cy, int gy, const float* dz, float* dpos, int B, int S, int D, int accumulate,
+                        const int* cu) {
   if (s >= S) {
-    for (int col = blockIdx.y * 256 + threadIdx.x; col < D; col += gridDim.y * 256) dpos[(size_t)s * D + col] = 0.f;
+    for (int col = cy * 256 + threadIdx.x; col < D; col += gy * 256) dpos[(size_t)s * D + col] = 0.f;
     return;
   }
   __shared__ int s_cu[257];
@@ -491,7 +490,7 @@ __global__ __launch_bounds__(256) void pos_grad_kernel(const float* dz, float* d
   if (cu)
     for (int b = threadIdx.x; b <= B && b < 257; b += 256) s_cu[b] = cu[b];
   __syncthreads();
-  const int c4 = blockIdx.y * PG_COLS + (threadIdx.x % PG_COLS), grp = threadIdx.x / PG_COLS;
+  const int c4 = cy * PG_COLS + (threadIdx.x % PG_COLS), grp = threadIdx.x / PG_COLS;
   const bool live = c4 < D / 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int b0 = grp; b0 < B; b0 += PG_GROUPS * 8) {
@@ -536,14 +535,12 @@ DEV void word_row_store(float* dword, long long id, int col, float acc, bool add
   *dst = add ? *dst + acc : acc;
 }
 
-__global__ __launch_bounds__(256) void word_grad_pieces_kernel(const long long* sorted, const long long* perm,
-                                                              const float* dz, float* piece, float* dword, int T,
-                                                              int accumulate, unsigned char* now,
-                                                              unsigned char* ever) {
+DEV void word_pieces_block(int bx, const long long* sorted, const long long* perm, const float* dz, float* piece,
+                          float* dword, int T, int accumulate, unsigned char* now, unsigned char* ever) {
   constexpr int D = 768;
   __shared__ long long sid[WCH + 2];
   __shared__ long long sperm[WCH];
-  const int c0 = blockIdx.x * WCH, c1 = min(T, c0 + WCH), n = c1 - c0;
+  const int c0 = bx * WCH, c1 = min(T, c0 + WCH), n = c1 - c0;
   if (threadIdx.x < n) {
     sid[threadIdx.x + 1] = sorted[c0 + threadIdx.x];
     sperm[threadIdx.x] = perm[c0 + threadIdx.x];
@@ -583,11 +580,10 @@ __global__ __launch_bounds__(256) void word_grad_pieces_kernel(const long long* 
   }
 }
 
-__global__ __launch_bounds__(256) void word_grad_combine_kernel(const long long* sorted, const float* piece,
-                                                               float* dword, int T, int accumulate,
-                                                               unsigned char* now, unsigned char* ever) {
+DEV void word_combine_block(int bx, const long long* sorted, const float* piece, float* dword, int T, int accumulate,
+                           unsigned char* now, unsigned char* ever) {
   constexpr int D = 768;
-  const int c0 = blockIdx.x * WCH, c1 = min(T, c0 + WCH);
+  const int c0 = bx * WCH, c1 = min(T, c0 + WCH);
   if (c1 >= T || sorted[c1] != sorted[c1 - 1]) return;  // no run crosses this chunk's end
   // The crossing run's first position in this chunk (the run is a suffix of the chunk) and its
   // end, found by the whole block at once instead of walking the sorted ids one dependent load
@@ -628,12 +624,11 @@ __global__ __launch_bounds__(256) void word_grad_combine_kernel(const long long*
 // loads back to back (UNR in flight) before summing them in a fixed order, so the
 // reduction is bandwidth- not latency-bound; groups combine through LDS.
 template <int UNR>
-__global__ __launch_bounds__(256) void colsum_kernel(const float* part, int nblk, int stride_blk, int D,
-                                                     float* o0, float* o1, float* o2, int accumulate) {
+DEV void colsum_block(int bx, int k, const float* part, int nblk, int stride_blk, int D, float* o0, float* o1,
+                      float* o2, int accumulate) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int j = blockIdx.x * 64 + lane;
-  const int k = blockIdx.y;
+  const int j = bx * 64 + lane;
   float* out = k == 0 ? o0 : (k == 1 ? o1 : o2);
   if (!out) return;
   float s = 0.f;
@@ -656,6 +651,50 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* part, int nblk
     const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
     out[j] = accumulate ? out[j] + t : t;
   }
+}
+template <int UNR>
+__global__ __launch_bounds__(256) void colsum_kernel(const float* part, int nblk, int stride_blk, int D,
+                                                     float* o0, float* o1, float* o2, int accumulate) {
+  colsum_block<UNR>(blockIdx.x, blockIdx.y, part, nblk, stride_blk, D, o0, o1, o2, accumulate);
+}
+
+// The embedding backward's tail in two launches (after emb_bwd_kernel): A = the word-gradient
+// pieces (chunk blocks) beside the position gradient (pos blocks); B = the crossing runs'
+// combine beside the LayerNorm dgamma / dbeta column sums of emb_bwd_kernel's partials.  Each
+// launch's two block kinds touch disjoint outputs, so they need no order between them.
+struct EmbTail {
+  const long long* sorted;
+  const long long* perm;
+  const float* dz;
+  float* piece;         // [T][768] (pieces of runs crossing a chunk boundary)
+  const float* lnpart;  // [lnblk][3][D] (emb_bwd_kernel's dgamma / dbeta partials)
+  float* dword;
+  float* dpos;
+  float* dgamma;
+  float* dbeta;
+  const int* cu;
+  unsigned char* now;
+  unsigned char* ever;
+  int T, B, S, D, chunks, pos_gy, cs_gx, lnblk, acc_mode, accumulate;
+};
+__global__ __launch_bounds__(256) void emb_tail_a_kernel(EmbTail t) {
+  const int bx = blockIdx.x;
+  if (bx < t.chunks) {
+    word_pieces_block(bx, t.sorted, t.perm, t.dz, t.piece, t.dword, t.T, t.acc_mode, t.now, t.ever);
+    return;
+  }
+  const int r = bx - t.chunks;
+  pos_grad_block(r / t.pos_gy, r % t.pos_gy, t.pos_gy, t.dz, t.dpos, t.B, t.S, t.D, t.accumulate, t.cu);
+}
+__global__ __launch_bounds__(256) void emb_tail_b_kernel(EmbTail t) {
+  const int bx = blockIdx.x;
+  if (bx < t.chunks) {
+    word_combine_block(bx, t.sorted, t.piece, t.dword, t.T, t.acc_mode, t.now, t.ever);
+    return;
+  }
+  const int r = bx - t.chunks;
+  colsum_block<16>(r % t.cs_gx, r / t.cs_gx, t.lnpart, t.lnblk, 3 * t.D, t.D, t.dgamma, t.dbeta, nullptr,
+                   t.accumulate);
 }
 
 // Column sums of a bf16 [T][N] matrix into per-block partials [grid][N] (bias grads).
@@ -847,22 +886,27 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
   a.pos = (const bf16_t*)pos; a.gamma = gamma; a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = dz_buf;
   a.part = work; a.T = T; a.S = S; a.D = D; a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale;
   a.row_map = row_map;
+  // work = [T][D] word-gradient pieces, then the [grid][3][D] LayerNorm partials
+  a.part = work + (size_t)T * D;
+  a.now_clear = !accumulate ? now : nullptr;  // (set again by the tail for this step's ids)
+  a.V = V;
   const int grid = std::min(LN_GRID, (T + 7) / 8);
   hipLaunchKernelGGL(emb_bwd_kernel<3>, dim3(grid), dim3(LN_BWD_THREADS), (LN_BWD_THREADS / 64) * D * sizeof(float),
                      st, a);
-  hipLaunchKernelGGL(colsum_kernel<16>, dim3((D + 63) / 64, 2), dim3(256), 0, st, work, grid, 3 * D, D, dgamma,
-                     dbeta, (float*)nullptr, accumulate);
-  hipLaunchKernelGGL(pos_grad_kernel, dim3(!accumulate && P > S ? P : S, (D / 4 + PG_COLS - 1) / PG_COLS), dim3(256), 0,
-                     st, dz_buf,
-                     dpos, B, S, D, accumulate, cu, !accumulate ? now : nullptr, V);
   if (!accumulate && !now) hipMemsetAsync(dword, 0, (size_t)V * D * sizeof(float), st);
-  // piece sums reuse `work` (T*D floats)
-  const int chunks = (T + WCH - 1) / WCH;
-  const int acc_mode = now ? accumulate : 1;
-  hipLaunchKernelGGL(word_grad_pieces_kernel, dim3(chunks), dim3(256), 0, st, sorted, perm, dz_buf, work, dword, T,
-                     acc_mode, now, ever);
-  hipLaunchKernelGGL(word_grad_combine_kernel, dim3(chunks), dim3(256), 0, st, sorted, work, dword, T, acc_mode, now,
-                     ever);
+  EmbTail t{};
+  t.sorted = sorted; t.perm = perm; t.dz = dz_buf; t.piece = work; t.lnpart = a.part;
+  t.dword = dword; t.dpos = dpos; t.dgamma = dgamma; t.dbeta = dbeta; t.cu = cu; t.now = now; t.ever = ever;
+  t.T = T; t.B = B; t.S = S; t.D = D;
+  t.chunks = (T + WCH - 1) / WCH;
+  t.pos_gy = (D / 4 + PG_COLS - 1) / PG_COLS;
+  t.cs_gx = (D + 63) / 64;
+  t.lnblk = grid;
+  t.acc_mode = now ? accumulate : 1;
+  t.accumulate = accumulate;
+  const int pos_rows = !accumulate && P > S ? P : S;
+  hipLaunchKernelGGL(emb_tail_a_kernel, dim3(t.chunks + pos_rows * t.pos_gy), dim3(256), 0, st, t);
+  hipLaunchKernelGGL(emb_tail_b_kernel, dim3(t.chunks + 2 * t.cs_gx), dim3(256), 0, st, t);
   return 0;
 }
 

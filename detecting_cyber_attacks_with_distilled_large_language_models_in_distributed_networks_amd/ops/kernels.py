@@ -587,7 +587,7 @@ def emb_bwd(dy, ids, sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos
     T = ids.numel()
     D = gamma.numel()
     dz = workspace(ids.device, "emb_dz", T * D)
-    ws = workspace(ids.device, "emb_work", max(T * D, LN_GRID * 3 * D))
+    ws = workspace(ids.device, "emb_work", T * D + LN_GRID * 3 * D)  # word pieces, then LN partials
     thr, sc = _drop(p)
     ext().emb_bwd(dy.contiguous(), ids.contiguous(), sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos,
                   dgamma, dbeta, dz, ws, S, seed, site, thr, sc, accumulate, now, ever, row_map, cu)
