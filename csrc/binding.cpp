@@ -317,7 +317,9 @@ int64_t gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C
 void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tensor>& Bs,
                    const std::vector<at::Tensor>& Cs, const std::vector<int64_t>& accumulate,
                    const std::vector<at::Tensor>& adam, const std::vector<double>& hp, int64_t cfg,
-                   const std::vector<at::Tensor>& wts = {}) {
+                   const std::vector<at::Tensor>& wts = {}, const std::vector<at::Tensor>& biases = {}) {
+  // biases: empty, or per problem an fp32 [M] producer-bias gradient (+)= column sums of A (an
+  // empty tensor: none), accumulated like the problem's gradient
   const size_t n = As.size();
   TORCH_CHECK(n > 0 && n <= 32, "gemm_dw_batch: 1..32 problems, got ", n);
   TORCH_CHECK(Bs.size() == n && Cs.size() == n && accumulate.size() == n, "gemm_dw_batch: ragged problem lists");
@@ -344,6 +346,13 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
     q.N = (int)Bs[i].size(1);
     q.K = (int)Ki;
     q.accumulate = accumulate[i] ? 1 : 0;
+  }
+  TORCH_CHECK(biases.empty() || biases.size() == n, "gemm_dw_batch: one bias entry per problem");
+  for (size_t i = 0; i < biases.size(); ++i) {
+    if (!biases[i].defined() || biases[i].numel() == 0) continue;
+    need(biases[i], at::kFloat, "bias");
+    TORCH_CHECK(biases[i].numel() == As[i].size(1), "gemm_dw_batch: a bias has the M entries of its problem");
+    pr[i].bias = biases[i].data_ptr<float>();
   }
   std::vector<FdAdamEpi> ad(n);
   const int* step = nullptr;
@@ -1250,7 +1259,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("row_map"),
         py::arg("cfg") = -1, py::arg("xsite") = 0, py::arg("b_mn") = false);
   m.def("gemm_dw_batch", &gemm_dw_batch, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("accumulate"),
-        py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1, py::arg("wts") = std::vector<at::Tensor>{});
+        py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1, py::arg("wts") = std::vector<at::Tensor>{},
+        py::arg("biases") = std::vector<at::Tensor>{});
   m.def("gemm_colsum", &gemm_colsum, py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("aux"),
         py::arg("res"), py::arg("colsum"), py::arg("aux_out") = py::none(), py::arg("kind") = 0);
   m.def("splitk_reduce_batched", &splitk_reduce_batched);

@@ -114,6 +114,7 @@ int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const
       if (!q.p || !q.sh || q.M % 8) hc::violations.push_back("dw_batch: W^T without its shadow's Adam");
       hc::span(q.shT, mn * 2, "dw_batch W^T");
     }
+    hc::opt_span(q.bias, (long long)q.M * 4, "dw_batch bias");
     if (q.p) {
       hc::span(q.p, mn * 4, "dw_batch adam p");
       hc::span(q.m, mn * 4, "dw_batch adam m");

@@ -37,6 +37,9 @@ struct FdDwProb {
   int tile0;          // filled by the launcher
   int accumulate;
   int K;              // rows of A and B (0: the launch's K)
+  // nullable: also bias[m] (+)= sum_k A[k][m] -- the producer's bias gradient (the qkv bias: A is
+  // dqkv), summed by the tiles of the first column block while their K loops read A anyway
+  float* bias;
 };
 
 #define FD_LN_XSITES 128

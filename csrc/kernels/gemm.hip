@@ -77,6 +77,9 @@ struct GemmParams {
   // the forward keeping it: bitwise the forward's values (same bf16 u, same gelu_erf).
   bf16_t* aux_out;
   FdLnEpi ln;            // EPI_LN / EPI_LN_BWD (adam_epi.h)
+  // EPI_F32, nullable: acol[m] (+= when accumulate) = sum over the K range of A[k][m], written by
+  // the tiles with tn == 0 (FdDwProb::bias)
+  float* acol;
 };
 
 constexpr int BKT = 64;
@@ -972,6 +975,28 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
     OB::stage(p.B, p.ldb, n0, kbeg + t * BK, p.N, b + OA::BYTES, wid, lane);
   };
   bf16x8 a0[MI], b0[NI], a1[MI], b1[NI];
+  // column sums of A (EPI_F32 acol): lane l's A fragments hold 8 k values of column m = l % 16
+  // of each 16-column block; only the first column block's tiles and their wc == 0 waves sum
+  const bool acs = EPI == EPI_F32 && p.acol != nullptr && tn == 0 && wc == 0;
+  float asum[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) asum[i] = 0.f;
+  auto sum_a = [&]() {
+    if constexpr (EPI == EPI_F32) {
+      if (acs) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          float s = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            s += bf2f((uint16_t)a0[i][e]);
+            if constexpr (KS == 2) s += bf2f((uint16_t)a1[i][e]);
+          }
+          asum[i] += s;
+        }
+      }
+    }
+  };
   auto read_frags = [&](const char* cur) {
 #pragma unroll
     for (int i = 0; i < MI; ++i) a0[i] = OA::frag(cur, wr * TM + i * 16, 0, lane);
@@ -1020,6 +1045,7 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
       if (kt + S - 1 < nk && !(p.diag & 1)) issue(kt + S - 1);
       read_frags(smem + (kt % S) * BUF);
       mfmas();
+      sum_a();
       if constexpr (SCHED) sched_ktile<(MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2)) * KS / 2, MI * NI * KS / 2>();
     }
   } else {
@@ -1053,15 +1079,29 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
       }
       read_frags(smem + (kt % S) * BUF);
       mfmas();
+      sum_a();
       if constexpr (SCHED) sched_ktile<(MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2)) * KS / 2, MI * NI * KS / 2>();
       if (kt + 1 < nk) {
         read_frags(smem + ((kt + 1) % S) * BUF);
         mfmas();
+        sum_a();
         if constexpr (SCHED) sched_ktile<(MI * (AK ? 1 : 2) + NI * (BKM ? 1 : 2)) * KS / 2, MI * NI * KS / 2>();
       }
     }
   }
   FD_STAMP(2);
+  if constexpr (EPI == EPI_F32) {
+    if (acs) {  // the 4 lane groups of a column hold disjoint k: fold them, lanes 0-15 store
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        float s = asum[i];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        const int m = m0 + wr * TM + i * 16 + lane;
+        if (lane < 16 && m < p.M) p.acol[m] = p.accumulate ? p.acol[m] + s : s;
+      }
+    }
+  }
   if constexpr (EpiTraits<EPI, BM, BN>::DIRECT) {
     // fp32 tile too large for LDS: finish it one wave-row band (TM rows) at a time through the
     // staged row-chunk epilogue (coalesced 16-byte rows for the gradient / Adam streams)
@@ -1186,6 +1226,7 @@ DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
   p.diag = bt.diag;
   p.out = q.C;
   p.accumulate = q.accumulate;
+  p.acol = q.bias;
   if (q.p) {
     p.adam.p = q.p; p.adam.m = q.m; p.adam.v = q.v; p.adam.sh = q.sh; p.adam.shT = q.shT; p.adam.step = bt.step;
     p.adam.lr = bt.lr; p.adam.b1 = bt.b1; p.adam.b2 = bt.b2; p.adam.eps = bt.eps; p.adam.wd = bt.wd;

@@ -280,11 +280,14 @@ class LayerFn(torch.autograd.Function):
         dcx, dz1 = K.scatter_rows2(dcxc, dz1c, ci, B, cx.shape[0])
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask,
                           q_live=1)
-        batch += [(dz1c, cxc, G["o_w"].buf, acc, wt.get("o_w")), (dqkv, x, G["qkv_w"].buf, acc, wt.get("qkv_w"))]
-        if rc.colsum_pending is not None:
-            rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))
-        else:
-            K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
+        # (the qkv bias gradient: column sums of dqkv in the dW launch's qkv tiles, K.DW_QKV_BIAS)
+        batch += [(dz1c, cxc, G["o_w"].buf, acc, wt.get("o_w")),
+                  (dqkv, x, G["qkv_w"].buf, acc, wt.get("qkv_w"), G["qkv_b"].buf if K.DW_QKV_BIAS else None)]
+        if not K.DW_QKV_BIAS:
+            if rc.colsum_pending is not None:
+                rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))
+            else:
+                K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
         prev = rc.ln2_saved.get(ctx.idx - 1) if rc.fuse_ln_bwd else None
         if prev is not None:
             z2p, m2p, r2p, Lp, site_p, p_p = prev
@@ -365,17 +368,20 @@ class LayerFn(torch.autograd.Function):
         if not rc.group_dw and batch is None:
             K.linear_dw(dz1, cx, G["o_w"].buf, acc)
         dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask)
+        dw_bias = batch is not None and K.DW_QKV_BIAS  # qkv bias gradient in the dW launch
         if batch is not None:
-            batch += [(dz1, cx, G["o_w"].buf, acc, wt.get("o_w")), (dqkv, x, G["qkv_w"].buf, acc, wt.get("qkv_w"))]
+            batch += [(dz1, cx, G["o_w"].buf, acc, wt.get("o_w")),
+                      (dqkv, x, G["qkv_w"].buf, acc, wt.get("qkv_w"), G["qkv_b"].buf if dw_bias else None)]
         elif rc.group_dw:
             K.linear_dw2(dz1, cx, G["o_w"].buf, dqkv, x, G["qkv_w"].buf, acc,
                          adam=fa.fused_args([G["o_w"].buf, G["qkv_w"].buf]) if fa else None, jobs=rc.dw_jobs)
         else:
             K.linear_dw(dqkv, x, G["qkv_w"].buf, acc)
-        if batch is not None and jobs is not None and rc.colsum_pending is not None:
-            rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))  # partials at the end, batched
-        else:
-            K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
+        if not dw_bias:
+            if batch is not None and jobs is not None and rc.colsum_pending is not None:
+                rc.colsum_pending.append((dqkv, G["qkv_b"].buf, acc))  # partials at the end, batched
+            else:
+                K.colsum(dqkv, G["qkv_b"].buf, acc, jobs)
         prev = rc.ln2_saved.get(ctx.idx - 1) if fused_bwd else None
         if prev is not None:
             # dx = dqkv Wqkv + dz1 is block idx-1's output-LN gradient: finish that LayerNorm

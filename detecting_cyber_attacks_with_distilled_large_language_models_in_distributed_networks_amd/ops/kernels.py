@@ -171,7 +171,8 @@ DW_BATCH_MAX = 32  # problems per all-layer weight-gradient launch (csrc/kernels
 
 def linear_dw_batch(jobs: list, adam=None, cfg: int = -1):
     """Every weight gradient of a backward in one launch per 32 problems: for each job
-    (dy [K, M], x [K, N], out [M, N] fp32, accumulate[, wT]) out (+)= dy^T x.  No split-K: each
+    (dy [K, M], x [K, N], out [M, N] fp32, accumulate[, wT[, bias]]) out (+)= dy^T x, and the
+    optional fp32 [M] bias (+)= the column sums of dy (``DW_QKV_BIAS``).  No split-K: each
     output tile runs the whole token dimension (deterministic, no slabs, no reduce).
     adam: a callable (grads, n_with_wT) -> (state, hyper) (``ArenaAdam.fused_args``): apply the
     optimizer step to each finished gradient tile instead of storing it; a job's optional wT
@@ -186,8 +187,20 @@ def linear_dw_batch(jobs: list, adam=None, cfg: int = -1):
         empty = None
         if nwt:
             empty = torch.empty(0, dtype=torch.bfloat16, device=outs[0].device)
+        bias = [j[5] if len(j) > 5 else None for j in chunk]
+        if any(b is not None for b in bias):
+            none = torch.empty(0, dtype=torch.float32, device=outs[0].device)
+            bias = [b if b is not None else none for b in bias]
+        else:
+            bias = []
         ext().gemm_dw_batch([j[0] for j in chunk], [j[1] for j in chunk], outs, [int(j[3]) for j in chunk],
-                            st, hp, cfg, [w if w is not None else empty for w in wts] if nwt else [])
+                            st, hp, cfg, [w if w is not None else empty for w in wts] if nwt else [], bias)
+
+
+# The qkv bias gradient from the all-layer dW launch itself: the qkv weight gradient's tiles of the
+# first column block sum dqkv's columns while their K loops read it (gemm.hip GemmParams::acol),
+# instead of a separate column-sum pass over every block's dqkv.  FD_DW_QKV_BIAS=0: the pass.
+DW_QKV_BIAS = _os.environ.get("FD_DW_QKV_BIAS", "1") != "0"
 
 
 def dw_flush(jobs: list):

@@ -27,19 +27,26 @@ def test_dw_batch_kernel_matches_fp32(cfg):
     g = torch.Generator(device="cuda").manual_seed(cfg + 5)
     T = 2688
     shapes = [(768, 3072), (3072, 768), (768, 768), (2304, 768)] * 2
-    jobs, refs = [], []
+    jobs, refs, brefs = [], [], []
     for i, (M, N) in enumerate(shapes):
         dy = (torch.randn(T, M, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
         x = torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16)
         acc = i % 3 == 2
         out = torch.randn(M, N, device="cuda", generator=g) if acc else torch.empty(M, N, device="cuda")
         ref = dy.float().t() @ x.float() + (out.clone() if acc else 0.0)
-        jobs.append((dy, x, out, acc))
+        # the producer-bias column sums of dy for half the problems (the qkv bias path)
+        bias = None
+        if i % 2 == 1:
+            bias = torch.randn(M, device="cuda", generator=g) if acc else torch.full((M,), float("nan"), device="cuda")
+            brefs.append((bias, dy.float().sum(0) + (bias.clone() if acc else 0.0)))
+        jobs.append((dy, x, out, acc, None, bias))
         refs.append(ref)
     K.linear_dw_batch(jobs, cfg=cfg)
     torch.cuda.synchronize()
-    for (_, _, out, _), ref in zip(jobs, refs):
+    for (_, _, out, _, _, _), ref in zip(jobs, refs):
         assert _frel(out, ref) < 1e-5, _frel(out, ref)
+    for bias, bref in brefs:
+        assert _frel(bias, bref) < 1e-5, _frel(bias, bref)
 
 
 def _batch(B, S, seed=0):
