@@ -49,8 +49,7 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
                const void* res, int ldres, const FdLnEpi* ln, int cfg, int b_mn, hipStream_t st);
 int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
                              const int* splits, const int* accumulate, hipStream_t st);
-int fd_transpose_batched(const void* const* srcs, void* const* dsts, const int* rows, const int* cols, int n,
-                         hipStream_t st);
+
 const char* fd_comm_last_error();
 int fd_comm_load(const char* path);
 int fd_comm_unique_id_bytes();
@@ -86,7 +85,8 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                const void* word, const void* pos, const float* gamma, const float* mean, const float* rstd,
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
-               int accumulate, unsigned char* now, unsigned char* ever, const int* row_map, const int* cu, hipStream_t st);
+               int accumulate, unsigned char* now, unsigned char* ever, const int* row_map, const int* cu, int ncs, const float* const* cs_parts, float* const* cs_outs, const int* cs_nblk,
+               const int* cs_stride, const int* cs_D, const int* cs_nout, const int* cs_acc, hipStream_t st);
 int fd_gather_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int n, int d_bytes,
                     hipStream_t st);
 int fd_scatter_rows2(const void* a, const void* b, void* oa, void* ob, const long long* idx, int nsrc, int T,
@@ -108,6 +108,12 @@ int fd_head_fwd(const void* hidden, int B, int S, int D, const float* W, const f
 int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float dscale, const float* dlogits, float* dW, float* db, void* dhidden,
                 int accumulate, const int* cls, int T, const float* gscale, const int* own, hipStream_t st);
+int fd_head_ln_bwd(const void* hidden, int B, int T, int D, const float* W, const float* bias,
+                   const uint32_t* seed_ptr, uint32_t hsite, uint32_t hthr, float hdscale, const long long* labels,
+                   float* logits, float* loss, float* dlogits, float* row_loss, float* loss_acc, float* dW, float* db,
+                   int accumulate, const int* own, const float* tlogits, float kd_T, float kd_alpha, const void* z,
+                   const float* gamma, const float* mean, const float* rstd, void* dz, void* dx, float* part,
+                   uint32_t site, uint32_t thr, float dscale, const int* row_map, int* nblk_out, hipStream_t st);
 int fd_eval_metrics(const float* logits, const long long* labels, int B, double* acc, long long* counts,
                     float* prob1, long long* preds, hipStream_t st);
 int fd_adam(float* p, const float* g, float* m, float* v, void* shadow, long long n, const int* step, float lr,
@@ -195,7 +201,9 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
 // NT dX GEMM (GELU' or residual epilogue) that also leaves per-M-tile column sums of its bf16
 // output in `colsum` ([ceil(M / 128)][N] fp32; returns the tile count) for a deferred
 // producer-bias gradient.
-// kind 0: B = W^T [N][K] (NT); kind 1: B = W [K][N] (NN; direct-A kernels only, else 0 tiles).
+// kind 0: B = W^T [N][K] (NT, K-major B); kind 1: B = W [K][N] (NN: the MN-major B through the
+// LDS-DMA ring with transposing fragment reads).  Returns 0 tiles (no partials left) only for a
+// tile configuration without the fused column-sum epilogue.
 int64_t gemm_colsum(int64_t epi, const at::Tensor& A, const at::Tensor& B, const at::Tensor& C,
                     const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& res,
                     const at::Tensor& colsum, const c10::optional<at::Tensor>& aux_out, int64_t kind = 0) {
@@ -312,12 +320,10 @@ int64_t gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C
 // Cs[i] (+)= As[i]^T Bs[i] (fp32), As[i] [K_i][M_i], Bs[i] [K_i][N_i] bf16 (K_i % 64 == 0).
 // adam: empty, or [p, m, v, shadow] per problem + the device step counter last (fused
 // optimizer step instead of storing the gradients; hp = [lr, b1, b2, eps, wd, decoupled]).
-// wts: empty, or per problem the bf16 transposed shadow W^T [N][M] the fused Adam epilogue also
-// refreshes (an empty tensor: none for that problem).
 void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tensor>& Bs,
                    const std::vector<at::Tensor>& Cs, const std::vector<int64_t>& accumulate,
                    const std::vector<at::Tensor>& adam, const std::vector<double>& hp, int64_t cfg,
-                   const std::vector<at::Tensor>& wts = {}, const std::vector<at::Tensor>& biases = {}) {
+                   const std::vector<at::Tensor>& biases = {}) {
   // biases: empty, or per problem an fp32 [M] producer-bias gradient (+)= column sums of A (an
   // empty tensor: none), accumulated like the problem's gradient
   const size_t n = As.size();
@@ -363,15 +369,6 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
       TORCH_CHECK(!accumulate[i], "gemm_dw_batch: a fused Adam step cannot accumulate into a gradient");
       pr[i].p = ad[i].p; pr[i].m = ad[i].m; pr[i].v = ad[i].v; pr[i].sh = ad[i].sh;
     }
-    TORCH_CHECK(wts.empty() || wts.size() == n, "gemm_dw_batch: one W^T entry per problem");
-    for (size_t i = 0; i < wts.size(); ++i) {
-      if (!wts[i].defined() || wts[i].numel() == 0) continue;
-      need(wts[i], at::kBFloat16, "W^T");
-      TORCH_CHECK(wts[i].dim() == 2 && wts[i].size(0) == Cs[i].size(1) && wts[i].size(1) == Cs[i].size(0),
-                  "gemm_dw_batch: W^T must be [N][M] of its problem's [M][N] gradient");
-      TORCH_CHECK(pr[i].sh != nullptr, "gemm_dw_batch: W^T needs the problem's bf16 shadow");
-      pr[i].shT = reinterpret_cast<uint16_t*>(wts[i].data_ptr());
-    }
     step = ad[0].step;
     hyper[0] = ad[0].lr; hyper[1] = ad[0].b1; hyper[2] = ad[0].b2; hyper[3] = ad[0].eps; hyper[4] = ad[0].wd;
     hyper[5] = (float)ad[0].decoupled;
@@ -397,7 +394,7 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
                 const at::Tensor& err, double eps, const c10::optional<at::Tensor>& seed, int64_t site, int64_t thr,
                 double dscale, const c10::optional<at::Tensor>& row_map, int64_t cfg, int64_t xsite,
                 bool b_mn = false) {
-  // b_mn: Bt is the weight itself, W [K][N] (MN-major B, a dX GEMM without a W^T copy; direct-A only)
+  // b_mn: Bt is the weight itself, W [K][N] (MN-major B through the LDS-DMA ring, transposing fragment reads)
   need(A, at::kBFloat16, "A");
   need(Bt, at::kBFloat16, "Bt");
   need(C, at::kBFloat16, "C");
@@ -418,7 +415,9 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
   TORCH_CHECK(mean.numel() >= M && rstd.numel() >= M, "gemm_ln: mean / rstd need M entries");
   TORCH_CHECK(stats.numel() >= 2 * (M + 128) * (N / 64), "gemm_ln: stats too small");
   TORCH_CHECK(cnt.numel() >= 1 && err.numel() >= 1, "gemm_ln: counters too small");
-  TORCH_CHECK(xsite >= 0 && xsite < FD_LN_XSITES, "gemm_ln: exchange call site out of range");
+  // (xsite + 1 < FD_LN_XSITES: a granule tag epoch * FD_LN_XSITES + xsite + 1 is then never 0 mod
+  // FD_LN_XSITES, so it can never equal the 0 of a granule zeroed at an epoch wrap)
+  TORCH_CHECK(xsite >= 0 && xsite < FD_LN_XSITES - 1, "gemm_ln: exchange call site out of range");
   need_opt(bias, at::kFloat, "bias");
   need_opt(beta, at::kFloat, "beta");
   need_opt(z, at::kBFloat16, "z");
@@ -704,26 +703,6 @@ void comm_allgather(int64_t h, const at::Tensor& send, const at::Tensor& recv) {
 }
 
 // dsts[i] = srcs[i]^T for a batch of bf16 matrices (one launch).
-void transpose_batched(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
-  TORCH_CHECK(srcs.size() == dsts.size() && srcs.size() <= 32, "transpose_batched: 1..32 matching matrices");
-  std::vector<const void*> sp;
-  std::vector<void*> dp;
-  std::vector<int> rows, cols;
-  for (size_t i = 0; i < srcs.size(); ++i) {
-    need(srcs[i], at::kBFloat16, "transpose src");
-    need(dsts[i], at::kBFloat16, "transpose dst");
-    TORCH_CHECK(srcs[i].dim() == 2 && dsts[i].dim() == 2 && dsts[i].size(0) == srcs[i].size(1) &&
-                    dsts[i].size(1) == srcs[i].size(0),
-                "transpose_batched: dst must be src^T shaped");
-    TORCH_CHECK(srcs[i].size(0) % 64 == 0 && srcs[i].size(1) % 64 == 0, "transpose_batched: dims % 64");
-    sp.push_back(srcs[i].data_ptr());
-    dp.push_back(dsts[i].data_ptr());
-    rows.push_back((int)srcs[i].size(0));
-    cols.push_back((int)srcs[i].size(1));
-  }
-  check_rc(fd_transpose_batched(sp.data(), dp.data(), rows.data(), cols.data(), (int)sp.size(), stream()),
-           "transpose_batched");
-}
 
 // Diagnostic builds (FD_GEMM_STAMPS): per-block phase stamps of the last one-round GEMM launch
 // into `out` (CPU int64 [nblocks][8]); returns the blocks copied (-1: a normal build).
@@ -925,13 +904,57 @@ void emb_fwd(const at::Tensor& ids, const at::Tensor& word, const at::Tensor& po
            "emb_fwd");
 }
 
+// Validated host arrays of a deferred column-sum batch (ops/kernels.py colsum_flush jobs).
+struct ColsumHost {
+  std::vector<const float*> pp;
+  std::vector<float*> op;
+  std::vector<int> nb, sd, dd, no, ac;
+};
+ColsumHost colsum_prepare(const std::vector<at::Tensor>& parts,
+                          const std::vector<std::vector<c10::optional<at::Tensor>>>& outs,
+                          const std::vector<int64_t>& nblk, const std::vector<int64_t>& stride,
+                          const std::vector<int64_t>& D, const std::vector<int64_t>& accumulate) {
+  const size_t n = parts.size();
+  TORCH_CHECK(outs.size() == n && nblk.size() == n && stride.size() == n && D.size() == n && accumulate.size() == n,
+              "colsum_batched: ragged job lists");
+  ColsumHost h;
+  h.pp.resize(n);
+  h.op.assign(3 * n, nullptr);
+  h.nb.resize(n); h.sd.resize(n); h.dd.resize(n); h.no.resize(n); h.ac.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    need(parts[i], at::kFloat, "colsum part");
+    TORCH_CHECK(outs[i].size() >= 1 && outs[i].size() <= 3, "colsum_batched: 1..3 outputs per job");
+    TORCH_CHECK(stride[i] >= (int64_t)outs[i].size() * D[i] && parts[i].numel() >= nblk[i] * stride[i],
+                "colsum_batched: partial buffer too small");
+    for (size_t k = 0; k < outs[i].size(); ++k) {
+      if (outs[i][k].has_value() && outs[i][k]->defined()) {
+        need(*outs[i][k], at::kFloat, "colsum out");
+        TORCH_CHECK(outs[i][k]->numel() == D[i], "colsum_batched: output size");
+        h.op[3 * i + k] = outs[i][k]->data_ptr<float>();
+      }
+    }
+    h.pp[i] = parts[i].data_ptr<float>();
+    h.nb[i] = (int)nblk[i]; h.sd[i] = (int)stride[i]; h.dd[i] = (int)D[i];
+    h.no[i] = (int)outs[i].size(); h.ac[i] = accumulate[i] ? 1 : 0;
+  }
+  return h;
+}
+
 void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sorted, const at::Tensor& perm,
              const at::Tensor& word, const at::Tensor& pos, const at::Tensor& gamma, const at::Tensor& mean,
              const at::Tensor& rstd, const at::Tensor& dword, const at::Tensor& dpos, const at::Tensor& dgamma,
              const at::Tensor& dbeta, const at::Tensor& dz_buf, const at::Tensor& work, int64_t S,
              const at::Tensor& seed, int64_t site, int64_t thr, double dscale, bool accumulate,
              const c10::optional<at::Tensor>& now, const c10::optional<at::Tensor>& ever,
-             const c10::optional<at::Tensor>& row_map, const c10::optional<at::Tensor>& cu) {
+             const c10::optional<at::Tensor>& row_map, const c10::optional<at::Tensor>& cu,
+             const std::vector<at::Tensor>& cs_parts = {},
+             const std::vector<std::vector<c10::optional<at::Tensor>>>& cs_outs = {},
+             const std::vector<int64_t>& cs_nblk = {}, const std::vector<int64_t>& cs_stride = {},
+             const std::vector<int64_t>& cs_D = {}, const std::vector<int64_t>& cs_acc = {}) {
+  // cs_*: deferred column-sum jobs (colsum_batched's arguments, <= 32) finalised by extra blocks of
+  // the embedding tail's first launch instead of a launch of their own
+  TORCH_CHECK(cs_parts.size() <= 32, "emb_bwd: at most 32 column-sum jobs");
+  ColsumHost cs = colsum_prepare(cs_parts, cs_outs, cs_nblk, cs_stride, cs_D, cs_acc);
   need_opt(now, at::kByte, "now");
   need_opt(ever, at::kByte, "ever");
   TORCH_CHECK(now.has_value() == ever.has_value(), "emb_bwd: now/ever go together");
@@ -964,7 +987,9 @@ void emb_bwd(const at::Tensor& dy, const at::Tensor& ids, const at::Tensor& sort
                       dpos.data_ptr<float>(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
                       dz_buf.data_ptr<float>(), work.data_ptr<float>(), (int)T, (int)S, (int)nseq, (int)P, (int)V,
                       (int)D, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, accumulate ? 1 : 0,
-                      ptr<unsigned char>(now), ptr<unsigned char>(ever), map_ptr(row_map, T), ptr<int>(cu), stream()),
+                      ptr<unsigned char>(now), ptr<unsigned char>(ever), map_ptr(row_map, T), ptr<int>(cu),
+                      (int)cs_parts.size(), cs.pp.data(), cs.op.data(), cs.nb.data(), cs.sd.data(), cs.dd.data(),
+                      cs.no.data(), cs.ac.data(), stream()),
            "emb_bwd");
 }
 
@@ -1028,31 +1053,11 @@ std::vector<int64_t> colsum_bf16_batched(const std::vector<at::Tensor>& xs, cons
 void colsum_batched(const std::vector<at::Tensor>& parts, const std::vector<std::vector<c10::optional<at::Tensor>>>& outs,
                     const std::vector<int64_t>& nblk, const std::vector<int64_t>& stride, const std::vector<int64_t>& D,
                     const std::vector<int64_t>& accumulate) {
+  ColsumHost h = colsum_prepare(parts, outs, nblk, stride, D, accumulate);
   const size_t n = parts.size();
-  TORCH_CHECK(outs.size() == n && nblk.size() == n && stride.size() == n && D.size() == n && accumulate.size() == n,
-              "colsum_batched: ragged job lists");
-  std::vector<const float*> pp(n);
-  std::vector<float*> op(3 * n, nullptr);
-  std::vector<int> nb(n), sd(n), dd(n), no(n), ac(n);
-  for (size_t i = 0; i < n; ++i) {
-    need(parts[i], at::kFloat, "colsum part");
-    TORCH_CHECK(outs[i].size() >= 1 && outs[i].size() <= 3, "colsum_batched: 1..3 outputs per job");
-    TORCH_CHECK(stride[i] >= (int64_t)outs[i].size() * D[i] && parts[i].numel() >= nblk[i] * stride[i],
-                "colsum_batched: partial buffer too small");
-    for (size_t k = 0; k < outs[i].size(); ++k) {
-      if (outs[i][k].has_value() && outs[i][k]->defined()) {
-        need(*outs[i][k], at::kFloat, "colsum out");
-        TORCH_CHECK(outs[i][k]->numel() == D[i], "colsum_batched: output size");
-        op[3 * i + k] = outs[i][k]->data_ptr<float>();
-      }
-    }
-    pp[i] = parts[i].data_ptr<float>();
-    nb[i] = (int)nblk[i]; sd[i] = (int)stride[i]; dd[i] = (int)D[i];
-    no[i] = (int)outs[i].size(); ac[i] = accumulate[i] ? 1 : 0;
-  }
   if (n == 0) return;
-  check_rc(fd_colsum_batched((int)n, pp.data(), op.data(), nb.data(), sd.data(), dd.data(), no.data(), ac.data(),
-                             stream()),
+  check_rc(fd_colsum_batched((int)n, h.pp.data(), h.op.data(), h.nb.data(), h.sd.data(), h.dd.data(), h.no.data(),
+                             h.ac.data(), stream()),
            "colsum_batched");
 }
 
@@ -1120,6 +1125,70 @@ void head_bwd(const at::Tensor& hidden, int64_t B, int64_t S, const at::Tensor& 
                        db.data_ptr<float>(), dhidden.data_ptr(), accumulate ? 1 : 0, ptr<int>(cls),
                        (int)(hidden.numel() / D), ptr<float>(gscale), ptr<int>(own), stream()),
            "head_bwd");
+}
+
+
+// The pruned training step's head forward + backward + the last block's output-LayerNorm backward
+// in one launch (norm.hip head_ln_bwd_kernel; the loss's upstream gradient is 1).  hidden / z /
+// dz / dx [T][D] (head row b = hidden row b, b < B <= T); returns the partial rows written to
+// `work` ([n][3][D] dgamma / dbeta / dbias, for a deferred column-sum job).
+int64_t head_ln_bwd(const at::Tensor& hidden, int64_t B, const at::Tensor& W, const at::Tensor& bias,
+                    const at::Tensor& seed, int64_t hsite, int64_t hthr, double hdscale, const at::Tensor& labels,
+                    const at::Tensor& logits, const at::Tensor& loss, const at::Tensor& dlogits,
+                    const at::Tensor& row_loss, const c10::optional<at::Tensor>& loss_acc, const at::Tensor& dW,
+                    const at::Tensor& db, bool accumulate, const c10::optional<at::Tensor>& own,
+                    const c10::optional<at::Tensor>& tlogits, double kd_T, double kd_alpha, const at::Tensor& z,
+                    const at::Tensor& gamma, const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& dz,
+                    const c10::optional<at::Tensor>& dx, const at::Tensor& work, int64_t site, int64_t thr,
+                    double dscale, const c10::optional<at::Tensor>& row_map) {
+  need(hidden, at::kBFloat16, "hidden");
+  need(W, at::kFloat, "W");
+  need(bias, at::kFloat, "bias");
+  need(labels, at::kLong, "labels");
+  need(logits, at::kFloat, "logits");
+  need(loss, at::kFloat, "loss");
+  need(dlogits, at::kFloat, "dlogits");
+  need(row_loss, at::kFloat, "row_loss");
+  need_opt(loss_acc, at::kFloat, "loss_acc");
+  need(dW, at::kFloat, "dW");
+  need(db, at::kFloat, "db");
+  need_opt(own, at::kInt, "own");
+  need_opt(tlogits, at::kFloat, "teacher logits");
+  need(z, at::kBFloat16, "z");
+  need(gamma, at::kFloat, "gamma");
+  need(mean, at::kFloat, "mean");
+  need(rstd, at::kFloat, "rstd");
+  need(dz, at::kBFloat16, "dz");
+  need_opt(dx, at::kBFloat16, "dx");
+  need(work, at::kFloat, "work");
+  const int64_t D = W.size(1);
+  const int64_t T = hidden.numel() / std::max<int64_t>(D, 1);
+  TORCH_CHECK(D == 768 && W.size(0) == 2 && gamma.numel() == D && bias.numel() == 2 && hidden.numel() == T * D,
+              "head_ln_bwd: shapes");
+  TORCH_CHECK(B > 0 && B <= T && B <= 1024, "head_ln_bwd: 0 < B <= min(T, 1024)");
+  TORCH_CHECK(labels.numel() == B && logits.numel() == 2 * B && dlogits.numel() == 2 * B && loss.numel() == 1 &&
+                  row_loss.numel() >= B && dW.numel() == 2 * D && db.numel() == 2,
+              "head_ln_bwd: head outputs");
+  TORCH_CHECK(z.numel() == T * D && dz.numel() == T * D && mean.numel() >= T && rstd.numel() >= T,
+              "head_ln_bwd: LayerNorm operands");
+  if (own.has_value() && own->defined()) TORCH_CHECK(own->numel() == B + 1, "head_ln_bwd: own must be [B + 1]");
+  if (loss_acc.has_value() && loss_acc->defined()) TORCH_CHECK(loss_acc->numel() >= 1, "head_ln_bwd: loss_acc [1]");
+  if (tlogits.has_value() && tlogits->defined())
+    TORCH_CHECK(tlogits->numel() == 2 * B && kd_T > 0.0, "head_ln_bwd: teacher logits [B, 2], T > 0");
+  if (thr != 0) TORCH_CHECK(dx.has_value() && dx->defined() && dx->numel() == T * D, "head_ln_bwd: dx required with dropout");
+  TORCH_CHECK(work.numel() >= ((T + 15) / 16) * 3 * D, "head_ln_bwd: work too small");
+  int nblk = 0;
+  check_rc(fd_head_ln_bwd(hidden.data_ptr(), (int)B, (int)T, (int)D, W.data_ptr<float>(), bias.data_ptr<float>(),
+                          seedp(seed), (uint32_t)hsite, (uint32_t)hthr, (float)hdscale,
+                          reinterpret_cast<const long long*>(labels.data_ptr()), logits.data_ptr<float>(),
+                          loss.data_ptr<float>(), dlogits.data_ptr<float>(), row_loss.data_ptr<float>(),
+                          ptr<float>(loss_acc), dW.data_ptr<float>(), db.data_ptr<float>(), accumulate ? 1 : 0,
+                          ptr<int>(own), ptr<const float>(tlogits), (float)kd_T, (float)kd_alpha, z.data_ptr(),
+                          gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), dz.data_ptr(),
+                          ptr<void>(dx), work.data_ptr<float>(), (uint32_t)site, (uint32_t)thr, (float)dscale,
+                          map_ptr(row_map, T), &nblk, stream()),
+           "head_ln_bwd");
+  return nblk;
 }
 
 void eval_metrics(const at::Tensor& logits, const at::Tensor& labels, const at::Tensor& acc, const at::Tensor& counts,
@@ -1259,7 +1328,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("row_map"),
         py::arg("cfg") = -1, py::arg("xsite") = 0, py::arg("b_mn") = false);
   m.def("gemm_dw_batch", &gemm_dw_batch, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("accumulate"),
-        py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1, py::arg("wts") = std::vector<at::Tensor>{},
+        py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1,
         py::arg("biases") = std::vector<at::Tensor>{});
   m.def("gemm_colsum", &gemm_colsum, py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("aux"),
         py::arg("res"), py::arg("colsum"), py::arg("aux_out") = py::none(), py::arg("kind") = 0);
@@ -1272,7 +1341,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pack", &pack, py::arg("mask"), py::arg("ids"), py::arg("row_map"), py::arg("cu"), py::arg("ids_packed"),
         py::arg("step") = py::none(), py::arg("seed") = py::none(), py::arg("cls_rows") = py::none(),
         py::arg("cls_rmap") = py::none());
-  m.def("transpose_batched", &transpose_batched);
   m.def("comm_load", &comm_load);
   m.def("comm_unique_id", &comm_unique_id);
   m.def("comm_init", &comm_init);
@@ -1310,6 +1378,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("dlogits"), py::arg("dW"), py::arg("db"),
         py::arg("dhidden"), py::arg("accumulate"), py::arg("cls") = py::none(), py::arg("gscale") = py::none(),
         py::arg("own") = py::none());
+  m.def("head_ln_bwd", &head_ln_bwd);
   m.def("eval_metrics", &eval_metrics);
   m.def("adam", &adam);
   m.def("step_inc", &step_inc);

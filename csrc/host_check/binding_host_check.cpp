@@ -110,10 +110,6 @@ int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const
     if (Kq % 64) hc::violations.push_back("dw_batch: K % 64");
     hc::span(q.A, Kq * q.M * 2, "dw_batch A");
     hc::span(q.B, Kq * q.N * 2, "dw_batch B");
-    if (q.shT) {
-      if (!q.p || !q.sh || q.M % 8) hc::violations.push_back("dw_batch: W^T without its shadow's Adam");
-      hc::span(q.shT, mn * 2, "dw_batch W^T");
-    }
     hc::opt_span(q.bias, (long long)q.M * 4, "dw_batch bias");
     if (q.p) {
       hc::span(q.p, mn * 4, "dw_batch adam p");
@@ -221,15 +217,6 @@ int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* out
   }
   return 0;
 }
-int fd_transpose_batched(const void* const* srcs, void* const* dsts, const int* rows, const int* cols, int n,
-                         hipStream_t) {
-  ++hc::calls;
-  for (int i = 0; i < n; ++i) {
-    hc::span(srcs[i], (long long)rows[i] * cols[i] * 2, "transpose src");
-    hc::span(dsts[i], (long long)rows[i] * cols[i] * 2, "transpose dst");
-  }
-  return 0;
-}
 const char* fd_comm_last_error() { return ""; }
 int fd_comm_load(const char*) { return 0; }
 int fd_comm_unique_id_bytes() { return 128; }
@@ -324,8 +311,15 @@ int fd_emb_fwd(const void*, int, const void*, const void*, const float*, const f
 int fd_emb_bwd(const void* dy, const void*, int, const long long* sorted, const long long* perm, const void*,
                const void*, const float*, const float*, const float*, float* dword, float* dpos, float*, float*,
                float* dz, float* work, int T, int, int, int P, int V, int D, const uint32_t*, uint32_t, uint32_t, float,
-               int, unsigned char* now, unsigned char* ever, const int*, const int*, hipStream_t) {
+               int, unsigned char* now, unsigned char* ever, const int*, const int*, int ncs,
+               const float* const* cs_parts, float* const* cs_outs, const int* cs_nblk, const int* cs_stride,
+               const int* cs_D, const int* cs_nout, const int*, hipStream_t) {
   ++hc::calls;
+  if (ncs < 0 || ncs > 32) hc::violations.push_back("emb_bwd: column-sum job count");
+  for (int i = 0; i < ncs; ++i) {
+    hc::span(cs_parts[i], (long long)cs_nblk[i] * cs_stride[i] * 4, "emb_bwd colsum part");
+    for (int k = 0; k < cs_nout[i]; ++k) hc::opt_span(cs_outs[3 * i + k], (long long)cs_D[i] * 4, "emb_bwd colsum out");
+  }
   hc::span(dy, (long long)T * D * 2, "emb_bwd dy");
   hc::span(sorted, (long long)T * 8, "emb_bwd sorted");
   hc::span(perm, (long long)T * 8, "emb_bwd perm");
@@ -426,6 +420,41 @@ int fd_head_bwd(const void* hidden, int B, int S, int D, const float* W, const u
   hc::opt_span(gscale, 4, "head bwd gscale");
   hc::span(seed, 4, "head bwd seed");
   (void)S;
+  return 0;
+}
+int fd_head_ln_bwd(const void* hidden, int B, int T, int D, const float* W, const float* bias, const uint32_t* seed,
+                   uint32_t, uint32_t, float, const long long* labels, float* logits, float* loss, float* dlogits,
+                   float* row_loss, float* loss_acc, float* dW, float* db, int, const int* own, const float* tlogits,
+                   float, float, const void* z, const float* gamma, const float* mean, const float* rstd, void* dz,
+                   void* dx, float* part, uint32_t, uint32_t thr, float, const int* row_map, int* nblk_out,
+                   hipStream_t) {
+  ++hc::calls;
+  const long long td = (long long)T * D;
+  if (B > T) hc::violations.push_back("head_ln_bwd: B > T");
+  hc::span(hidden, td * 2, "head_ln hidden");
+  hc::span(W, 2LL * D * 4, "head_ln W");
+  hc::span(bias, 8, "head_ln bias");
+  hc::span(labels, (long long)B * 8, "head_ln labels");
+  hc::span(logits, 2LL * B * 4, "head_ln logits");
+  hc::span(loss, 4, "head_ln loss");
+  hc::span(dlogits, 2LL * B * 4, "head_ln dlogits");
+  hc::span(row_loss, (long long)B * 4, "head_ln row_loss");
+  hc::opt_span(loss_acc, 4, "head_ln loss_acc");
+  hc::span(dW, 2LL * D * 4, "head_ln dW");
+  hc::span(db, 8, "head_ln db");
+  hc::opt_span(own, (B + 1LL) * 4, "head_ln own");
+  hc::opt_span(tlogits, 2LL * B * 4, "head_ln teacher logits");
+  hc::span(z, td * 2, "head_ln z");
+  hc::span(gamma, (long long)D * 4, "head_ln gamma");
+  hc::span(mean, (long long)T * 4, "head_ln mean");
+  hc::span(rstd, (long long)T * 4, "head_ln rstd");
+  hc::span(dz, td * 2, "head_ln dz");
+  if (thr) hc::span(dx, td * 2, "head_ln dx");
+  const int nlb = (T + 15) / 16;
+  hc::span(part, (long long)nlb * 3 * D * 4, "head_ln part");
+  hc::opt_span(row_map, (long long)T * 4, "head_ln row_map");
+  hc::span(seed, 4, "head_ln seed");
+  if (nblk_out) *nblk_out = nlb;
   return 0;
 }
 int fd_eval_metrics(const float*, const long long*, int, double*, long long*, float*, long long*, hipStream_t) {
@@ -574,14 +603,6 @@ int main() {
     expect_ok("dw_batch", [&] { gemm_dw_batch(As, Bs, Cs, acc, {}, {}, -1); });
     expect_ok("dw_batch adam", [&] { gemm_dw_batch(As, Bs, Cs, acc, st, hp, -1); });
     expect_reject("dw_batch adam+accumulate", [&] { gemm_dw_batch(As, Bs, Cs, acc1, st, hp, -1); });
-    std::vector<at::Tensor> wts;
-    for (auto& sh : shapes) wts.push_back(T_({sh[1], sh[0]}, bf));
-    wts[1] = at::Tensor();  // a problem without W^T
-    expect_ok("dw_batch adam + W^T", [&] { gemm_dw_batch(As, Bs, Cs, acc, st, hp, -1, wts); });
-    auto wbad = wts;
-    wbad[0] = T_({2304, 768}, bf);  // not transposed
-    expect_reject("dw_batch W^T shape", [&] { gemm_dw_batch(As, Bs, Cs, acc, st, hp, -1, wbad); });
-    expect_reject("dw_batch W^T ragged", [&] { gemm_dw_batch(As, Bs, Cs, acc, st, hp, -1, {wts[0]}); });
     auto Bbad = Bs;
     Bbad[2] = T_({2000, 768}, bf);
     expect_reject("dw_batch K mismatch", [&] { gemm_dw_batch(As, Bbad, Cs, acc, {}, {}, -1); });
@@ -757,6 +778,15 @@ int main() {
                                        128, seed, 1, 0, 1.0, false, none, none, none, none); });
     expect_reject("emb bwd work", [&] { emb_bwd(dy, ids, srt, prm, word, pos, ga, mean, rstd, dword, dpos, dg, db, dz,
                                                 work_small, 128, seed, 1, 0, 1.0, false, none, none, none, none); });
+    // the backward's deferred column sums riding on the tail launch
+    auto part = T_({21 * 3 * D}, f32), part_small = T_({20 * 3 * D}, f32);
+    std::vector<std::vector<c10::optional<at::Tensor>>> outs = {{dg, db, c10::optional<at::Tensor>(T_({D}, f32))}};
+    expect_ok("emb bwd + colsum jobs", [&] { emb_bwd(dy, ids, srt, prm, word, pos, ga, mean, rstd, dword, dpos, dg, db,
+                                                     dz, work, 128, seed, 1, 0, 1.0, false, none, none, none, none,
+                                                     {part}, outs, {21}, {3 * D}, {D}, {0}); });
+    expect_reject("emb bwd colsum part", [&] { emb_bwd(dy, ids, srt, prm, word, pos, ga, mean, rstd, dword, dpos, dg,
+                                                       db, dz, work, 128, seed, 1, 0, 1.0, false, none, none, none,
+                                                       none, {part_small}, outs, {21}, {3 * D}, {D}, {0}); });
   }
   // ---- unpadded layout
   {

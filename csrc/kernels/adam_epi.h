@@ -15,9 +15,6 @@ struct FdAdamEpi {
   const int* step;    // device step counter (already advanced for this step)
   float lr, b1, b2, eps, wd;
   int decoupled;      // AdamW-style decay
-  uint16_t* shT;      // bf16 TRANSPOSED shadow W^T [N][M] (nullable; all-layer dW launch only): the
-                      // backward's dX GEMMs read it, so it is refreshed here instead of by a
-                      // per-step transpose launch
 };
 
 // One weight-gradient problem of the all-layer launch (gemm.hip gemm_dw_batch_kernel):
@@ -32,7 +29,6 @@ struct FdDwProb {
   float* m;
   float* v;
   uint16_t* sh;       // bf16 shadow (nullable)
-  uint16_t* shT;      // bf16 transposed shadow [N][M] (nullable; needs sh's Adam)
   int M, N;
   int tile0;          // filled by the launcher
   int accumulate;

@@ -302,52 +302,21 @@ DEV void f32_epilogue(const GemmParams& p, const char* smem, int ldc_lds, int m0
     step_size = p.adam.lr / bc1;
     inv_sqrt_bc2 = 1.f / sqrtf(bc2);
   }
-  const bool wt = adam && p.adam.shT != nullptr;
 #pragma unroll 2
   for (int id = tid; id < BM * CPR; id += NT) {
     const int r = id / CPR, cc = id - r * CPR;
     const int m = m0 + r;
     if (m >= p.M) break;
     const size_t i = (size_t)m * p.ldc + n0 + cc * 4;
-    char* slot = const_cast<char*>(smem) + r * ldc_lds + cc * 16;
-    float4 g = *reinterpret_cast<const float4*>(slot);
+    float4 g = *reinterpret_cast<const float4*>(smem + r * ldc_lds + cc * 16);
     if (p.accumulate) {
       const float4 o = *reinterpret_cast<const float4*>(p.out + i);
       g.x += o.x; g.y += o.y; g.z += o.z; g.w += o.w;
     }
     if (adam) {
-      const float4 np = adam_epi4(p.adam, i, g, step_size, inv_sqrt_bc2);
-      // the updated bf16 weights back into this thread's own staging slot (it read g from there):
-      // the transposed copy is written from LDS below
-      if (wt) *reinterpret_cast<uint2*>(slot) = make_uint2(pack_bf2(np.x, np.y), pack_bf2(np.z, np.w));
+      adam_epi4(p.adam, i, g, step_size, inv_sqrt_bc2);
     } else {
       *reinterpret_cast<float4*>(p.out + i) = g;
-    }
-  }
-  if (wt) {
-    // W^T [N][M] (row pitch p.M): 8 consecutive rows m of one column n are 16 contiguous bytes of
-    // W^T row n.  A thread takes TWO adjacent columns (one 4-byte LDS word holds both bf16) and 8
-    // rows: 8 ds_read_b32, two 16-byte stores.  Lanes of a wave walk adjacent column pairs of the
-    // same 8 rows (conflict-free: one 16-byte slot per two lanes).
-    __syncthreads();
-    const int rows = min(BM, p.M - m0);
-    constexpr int PAIRS = BN / 2;
-    for (int id = tid; id < (BM / 8) * PAIRS; id += NT) {
-      const int r8 = id / PAIRS, pr = id - r8 * PAIRS;
-      if (r8 * 8 >= rows) break;  // rows ascend with id
-      const int c = 2 * pr;       // first of the two columns (tile-local)
-      uint32_t w[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        w[j] = *reinterpret_cast<const uint32_t*>(smem + (r8 * 8 + j) * ldc_lds + (c >> 2) * 16 + (c & 3) * 2);
-      uint4 lo, hi;  // column c: low halves, column c + 1: high halves
-      lo.x = (w[0] & 0xffffu) | (w[1] << 16); lo.y = (w[2] & 0xffffu) | (w[3] << 16);
-      lo.z = (w[4] & 0xffffu) | (w[5] << 16); lo.w = (w[6] & 0xffffu) | (w[7] << 16);
-      hi.x = (w[0] >> 16) | (w[1] & 0xffff0000u); hi.y = (w[2] >> 16) | (w[3] & 0xffff0000u);
-      hi.z = (w[4] >> 16) | (w[5] & 0xffff0000u); hi.w = (w[6] >> 16) | (w[7] & 0xffff0000u);
-      uint16_t* dst = p.adam.shT + (size_t)(n0 + c) * p.M + m0 + r8 * 8;
-      *reinterpret_cast<uint4*>(dst) = lo;
-      *reinterpret_cast<uint4*>(dst + p.M) = hi;
     }
   }
 }
@@ -1228,7 +1197,7 @@ DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
   p.accumulate = q.accumulate;
   p.acol = q.bias;
   if (q.p) {
-    p.adam.p = q.p; p.adam.m = q.m; p.adam.v = q.v; p.adam.sh = q.sh; p.adam.shT = q.shT; p.adam.step = bt.step;
+    p.adam.p = q.p; p.adam.m = q.m; p.adam.v = q.v; p.adam.sh = q.sh; p.adam.step = bt.step;
     p.adam.lr = bt.lr; p.adam.b1 = bt.b1; p.adam.b2 = bt.b2; p.adam.eps = bt.eps; p.adam.wd = bt.wd;
     p.adam.decoupled = bt.decoupled;
   }
@@ -1407,7 +1376,7 @@ bool smallm_tiles() {
 
 int pick_cfg(int kind, int M, int N, int K) {
   if (kind == 0 && M <= 64 && N % 64 == 0 && smallm_tiles()) return 13;
-  if (kind == 0) {  // NT forward (and dX on transposed weights)
+  if (kind == 0) {  // NT: forward (and any y = x B^T with a K-major B)
     // FFN1 forward / FFN2 dX (N = 3072): 256x192 fills the chip at M = 4096 (padded bs32),
     // 128x128 wins at the packed M ~ 2.7 k (21.5 vs 25.7 us; profiles/r1_gemm_cfg_sweep_T2688_packed.txt)
     // FD_GEMM_WIDE_CFG=<id>: configuration of the N >= 1536 NT GEMMs (QKV / FFN1 forward, FFN2 dX)
@@ -1580,7 +1549,7 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
     if (colsum_blocks) *colsum_blocks = (M + CFGS[id].bm - 1) / CFGS[id].bm;
   }
   // (NN launches fall back to cfg 8 below when the picked tile does not fit; that keeps 128 x 64)
-  if (kind == 0) {  // also dX = dy (W^T)^T with a transposed weight copy: GELU' / residual epilogues
+  if (kind == 0) {  // K-major B: GELU' / residual epilogues as in the NN dX kind
     if (epi == EPI_F32) return 2;
     if (launch_epi<true, true>(epi, p, id, 1, st)) return 0;
     return launch_epi<true, true>(epi, p, 0, 1, st) ? 0 : 2;  // 128x64 fits any N % 64 == 0
@@ -1736,7 +1705,6 @@ int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const f
     if (!probs[i].A || !probs[i].B || (!probs[i].C && !probs[i].p) || probs[i].M <= 0 || probs[i].N <= 0) return 2;
     if (probs[i].K < 0 || probs[i].K % BKT) return 5;
     if (probs[i].p && (!probs[i].m || !probs[i].v || !step || !hyper)) return 3;
-    if (probs[i].shT && (!probs[i].p || probs[i].M % 8)) return 6;
   }
   if (hyper) {
     bt.step = step;

@@ -19,118 +19,13 @@
 
 namespace {
 
-struct HeadArgs {
-  const bf16_t* hidden;  // [B*S, D]
-  int B, S, D;
-  const float* W;        // [2, D] fp32 master
-  const float* bias;     // [2]
-  const uint32_t* seed_ptr;
-  uint32_t site, thr;
-  float dscale;
-  const long long* labels;  // nullable
-  float* logits;         // [B, 2]
-  float* loss;           // [1]
-  float* dlogits;        // [B, 2] (written when labels given)
-  float* row_loss;       // [B] scratch
-  // backward
-  const float* dlog_in;  // [B, 2]
-  const float* gscale;   // nullable: dlog_in is scaled by gscale[0] (upstream grad of a fused loss)
-  float* dW;             // [2, D]
-  float* db;             // [2]
-  bf16_t* dhidden;       // [B*S, D]; only CLS rows written
-  int accumulate;
-  // packed (unpadded) rows: sequence b's [CLS] is row cls[b] of a [T, D] hidden (nullable:
-  // padded layout, row b*S); rows are clamped to T-1
-  const int* cls;
-  int T;
-  // packed sequence starts (int32 [B+1], nullable): sequence b is EMPTY (all-zero mask row) when
-  // own[b] == own[b+1]; its [CLS] row is not its own (the next sequence's, or a filler row), so
-  // the backward gives it no hidden-state gradient -- the same in the pruned layout (distinct
-  // rows) as in the packed one (shared rows), ADVICE r2
-  const int* own;
-  // knowledge distillation (nullable): teacher logits [B, 2]; the row loss becomes
-  // kd_alpha * CE(z, y) + (1 - kd_alpha) * T^2 * KL(softmax(t / T) || softmax(z / T))
-  const float* tlogits;
-  float kd_T, kd_alpha;
-  // nullable: the mean loss is also added here (a device-side running sum, e.g. a benchmark's
-  // loss over a graph-replayed loop, with no separate add launch per step)
-  float* loss_acc;
-};
-
-DEV size_t cls_row(const HeadArgs& a, int b) {
-  return a.cls ? (size_t)min(max(a.cls[b], 0), a.T - 1) : (size_t)b * a.S;
-}
-
-// Row b of the head (one wave): logits, and with labels the row loss and dlogits.
-DEV void head_row(const HeadArgs& a, int b, int lane) {
-  const bool drop = a.thr != 0;
-  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
-  const bf16_t* x = a.hidden + cls_row(a, b) * a.D;
-  float z0 = 0.f, z1 = 0.f;
-  for (int col = 4 * lane; col < a.D; col += 256) {
-    const uint2 xv = *reinterpret_cast<const uint2*>(x + col);
-    float v[4] = {lo_bf(xv.x), hi_bf(xv.x), lo_bf(xv.y), hi_bf(xv.y)};
-    const float4 w0 = *reinterpret_cast<const float4*>(a.W + col);
-    const float4 w1 = *reinterpret_cast<const float4*>(a.W + a.D + col);
-    if (drop) {
-      const uint32_t kb = drop_keep_bits<4>(seed, (uint32_t)(b * a.D + col), a.thr);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (kb >> e) & 1u ? v[e] * a.dscale : 0.f;
-    }
-    z0 += v[0] * w0.x + v[1] * w0.y + v[2] * w0.z + v[3] * w0.w;
-    z1 += v[0] * w1.x + v[1] * w1.y + v[2] * w1.z + v[3] * w1.w;
-  }
-  z0 = wave_sum(z0) + a.bias[0];
-  z1 = wave_sum(z1) + a.bias[1];
-  if (lane == 0) {
-    a.logits[2 * b] = z0;
-    a.logits[2 * b + 1] = z1;
-    if (a.labels) {
-      const float mx = fmaxf(z0, z1);
-      const float lse = mx + __logf(__expf(z0 - mx) + __expf(z1 - mx));
-      const int y = (int)a.labels[b];
-      const float p1 = __expf(z1 - lse), p0 = __expf(z0 - lse);
-      float loss = lse - (y ? z1 : z0);
-      float d0 = p0 - (y == 0), d1 = p1 - (y == 1);
-      if (a.tlogits) {
-        // soft term at temperature T (2 classes): log-softmax of z / T and t / T
-        const float iT = 1.f / a.kd_T;
-        const float s0 = z0 * iT, s1 = z1 * iT, t0 = a.tlogits[2 * b] * iT, t1 = a.tlogits[2 * b + 1] * iT;
-        const float ms = fmaxf(s0, s1), mt = fmaxf(t0, t1);
-        const float ls = ms + __logf(__expf(s0 - ms) + __expf(s1 - ms));
-        const float lt = mt + __logf(__expf(t0 - mt) + __expf(t1 - mt));
-        const float lq0 = s0 - ls, lq1 = s1 - ls;   // student log-probs
-        const float lp0 = t0 - lt, lp1 = t1 - lt;   // teacher log-probs
-        const float pt0 = __expf(lp0), pt1 = __expf(lp1);
-        const float kl = pt0 * (lp0 - lq0) + pt1 * (lp1 - lq1);
-        const float al = a.kd_alpha, T2 = a.kd_T * a.kd_T;
-        loss = al * loss + (1.f - al) * T2 * kl;
-        // d/dz of T^2 KL(p_t || softmax(z / T)) = T (q - p_t)
-        d0 = al * d0 + (1.f - al) * a.kd_T * (__expf(lq0) - pt0);
-        d1 = al * d1 + (1.f - al) * a.kd_T * (__expf(lq1) - pt1);
-      }
-      a.row_loss[b] = loss;
-      a.dlogits[2 * b] = d0 / a.B;
-      a.dlogits[2 * b + 1] = d1 / a.B;
-    }
-  }
-}
+#include "head_common.h"
 
 // One wave per batch row (grid = ceil(B/4) blocks): logits only (no labels), or the rows of a
 // batch too large for head_fwd_mean_kernel (their loss reduced by head_loss_mean_kernel).
 __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b < a.B) head_row(a, b, threadIdx.x & 63);
-}
-
-DEV void loss_mean(const HeadArgs& a, int lane) {  // one wave; fixed order
-  float s = 0.f;
-  for (int b = lane; b < a.B; b += 64) s += a.row_loss[b];
-  s = wave_sum(s);
-  if (lane == 0) {
-    a.loss[0] = s / a.B;
-    if (a.loss_acc) a.loss_acc[0] += s / a.B;
-  }
 }
 
 __global__ __launch_bounds__(64) void head_loss_mean_kernel(HeadArgs a) { loss_mean(a, threadIdx.x); }
@@ -141,12 +36,17 @@ __global__ __launch_bounds__(64) void head_loss_mean_kernel(HeadArgs a) { loss_m
 constexpr int HEAD_MEAN_MAXB = 1024;
 __global__ __launch_bounds__(1024) void head_fwd_mean_kernel(HeadArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int b = w; b < a.B; b += 16) head_row(a, b, lane);
+  for (int b = w; b < a.B; b += 32) {  // rows b and b + 16 of this wave, loads interleaved
+    const int rows[2] = {b, b + 16 < a.B ? b + 16 : -1};
+    float z0[2], z1[2];
+    head_logits_n<2>(a, rows, lane, z0, z1);
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      if (rows[r] >= 0) head_row_out(a, rows[r], lane, z0[r], z1[r]);
+  }
   __syncthreads();  // (every row loss written; workgroup-visible)
   if (w == 0) loss_mean(a, lane);
 }
-
-DEV bool empty_seq(const HeadArgs& a, int b) { return a.own && a.own[b] == a.own[b + 1]; }
 
 // Is `row` the [CLS] row of some non-empty sequence (the rows the compute blocks write)?
 DEV bool is_cls_row(const HeadArgs& a, int row) {
@@ -207,11 +107,11 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
       const bool keep = !drop || drop_keep(seed, (uint32_t)(b * a.D + colc), a.thr);
       const float sc = drop ? (keep ? a.dscale : 0.f) : 1.f;
       const float xv = x[u] * sc;
-      g0 += d0 * xv;
-      g1 += d1 * xv;
+      head_col_acc(g0, d0, xv);
+      head_col_acc(g1, d1, xv);
       // an empty sequence shares its [CLS] row with the next one: the later sequence writes it
       const bool last_owner = b + 1 >= a.B || cls_row(a, b + 1) != row[u];
-      if (live && last_owner && !empty_seq(a, b)) a.dhidden[row[u] * a.D + col] = (bf16_t)f2bf((d0 * w0 + d1 * w1) * sc);
+      if (live && last_owner && !empty_seq(a, b)) a.dhidden[row[u] * a.D + col] = (bf16_t)head_dh(d0, d1, w0, w1, sc);
     }
   }
   red[0][grp][c] = g0;

@@ -64,6 +64,7 @@ DEV uint4 pack8(const float (&f)[8]) {
 // z = dropout(x) + r for one lane's 24 elements of `row`; keep bits recorded (bit 8c+e).
 DEV void ln_load_sum(const LnArgs& a, int row, int hl, bool drop, uint32_t seed, float (&z)[CH][8],
                      uint32_t& keep) {
+#pragma clang fp contract(off)
   uint4 xv[CH], rv[CH];
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
@@ -159,6 +160,48 @@ DEV void block_colsum(float (&acc)[NC][4], float* lds, float* out, int D) {
   __syncthreads();
 }
 
+// LayerNorm backward of one half-wave row from its output gradient dyv and pre-LN sum z (in xh,
+// replaced by xhat): dz, dx (dropout), and this lane's dgamma / dbeta / dbias partials.  Shared by
+// ln_bwd_kernel and head_ln_bwd_kernel with contraction off, so both round every product and sum
+// the same way (the fused head launch's LayerNorm backward is bitwise ln_bwd_kernel's).
+DEV void ln_bwd_row(const LnArgs& a, int row, int hl, bool drop, const float4 (&gm)[CH][2], const float (&dyv)[CH][8],
+                    float (&xh)[CH][8], uint32_t keep, float mean, float rstd, float (&dg)[CH][8],
+                    float (&db)[CH][8], float (&dbias)[CH][8]) {
+#pragma clang fp contract(off)
+  const int D = a.D;
+  float gd[CH][8];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const float4 g0 = gm[c][0], g1 = gm[c][1];
+    const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xh[c][e] = (xh[c][e] - mean) * rstd;
+      gd[c][e] = g[e] * dyv[c][e];
+      s1 += gd[c][e];
+      s2 += gd[c][e] * xh[c][e];
+    }
+  }
+  s1 = half_sum(s1) / D;
+  s2 = half_sum(s2) / D;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const size_t off = (size_t)row * D + 8 * (hl + HL * c);
+    float dz[8], dx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      dz[e] = rstd * (gd[c][e] - s1 - xh[c][e] * s2);
+      dx[e] = ((keep >> (8 * c + e)) & 1u) ? dz[e] * (drop ? a.dscale : 1.f) : 0.f;
+      dg[c][e] += dyv[c][e] * xh[c][e];
+      db[c][e] += dyv[c][e];
+      dbias[c][e] += dx[e];
+    }
+    *reinterpret_cast<uint4*>(a.dz + off) = pack8(dz);
+    if (drop && a.dx) *reinterpret_cast<uint4*>(a.dx + off) = pack8(dx);
+  }
+}
+
 // 16 rows per 512-thread block per iteration (two per wave); per-lane column
 // partials for dgamma / dbeta / producer-bias, folded across the two half-waves
 // and the 8 waves into part[blockIdx.x][3][D] (fixed order: deterministic).
@@ -188,38 +231,10 @@ __global__ __launch_bounds__(512) void ln_bwd_kernel(LnArgs a) {
     float xh[CH][8];
     uint32_t keep;
     ln_load_sum(a, row, hl, drop, seed, xh, keep);
-    float dyv[CH][8], gd[CH][8];
-    float s1 = 0.f, s2 = 0.f;
+    float dyv[CH][8];
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const float4 g0 = gm[c][0], g1 = gm[c][1];
-      const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-      unpack8(dv[c], dyv[c]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        xh[c][e] = (xh[c][e] - mean) * rstd;
-        gd[c][e] = g[e] * dyv[c][e];
-        s1 += gd[c][e];
-        s2 += gd[c][e] * xh[c][e];
-      }
-    }
-    s1 = half_sum(s1) / D;
-    s2 = half_sum(s2) / D;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const size_t off = (size_t)row * D + 8 * (hl + HL * c);
-      float dz[8], dx[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        dz[e] = rstd * (gd[c][e] - s1 - xh[c][e] * s2);
-        dx[e] = ((keep >> (8 * c + e)) & 1u) ? dz[e] * (drop ? a.dscale : 1.f) : 0.f;
-        dg[c][e] += dyv[c][e] * xh[c][e];
-        db[c][e] += dyv[c][e];
-        dbias[c][e] += dx[e];
-      }
-      *reinterpret_cast<uint4*>(a.dz + off) = pack8(dz);
-      if (drop && a.dx) *reinterpret_cast<uint4*>(a.dx + off) = pack8(dx);
-    }
+    for (int c = 0; c < CH; ++c) unpack8(dv[c], dyv[c]);
+    ln_bwd_row(a, row, hl, drop, gm, dyv, xh, keep, mean, rstd, dg, db, dbias);
   }
   // fold the two half-waves (same columns, different rows), then the 8 waves
   float* out = a.part + (size_t)blockIdx.x * 3 * D;
@@ -658,6 +673,56 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* part, int nblk
   colsum_block<UNR>(blockIdx.x, blockIdx.y, part, nblk, stride_blk, D, o0, o1, o2, accumulate);
 }
 
+// Deferred column-sum finalisation: every bias / LayerNorm-affine gradient of the
+// backward leaves its per-block partials in a slot of its own, and ONE launch at the
+// end of the backward reduces all of them (instead of one small launch per producer).
+// Same per-column fixed-order sum as colsum_kernel: bitwise identical results.
+constexpr int COLSUM_MAXJ = 32;
+struct ColsumJob {
+  const float* part;
+  float* out[3];
+  int nblk, stride_blk, D, nout, accumulate;
+};
+struct ColsumBatch {
+  ColsumJob j[COLSUM_MAXJ];
+  int start[COLSUM_MAXJ + 1];  // first block of job i (blocks = ceil(D/64) * nout)
+  int n;
+};
+
+template <int UNR>
+DEV void colsum_batched_block(const ColsumBatch& cb, int bx) {
+  __shared__ float red[4][64];
+  int ji = 0;
+  while (ji + 1 < cb.n && bx >= cb.start[ji + 1]) ++ji;
+  const ColsumJob& jb = cb.j[ji];
+  const int local = bx - cb.start[ji];
+  const int cblk = (jb.D + 63) / 64;
+  const int k = local / cblk;
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int j = (local - k * cblk) * 64 + lane;
+  float* out = jb.out[k];
+  float s = 0.f;
+  if (j < jb.D) {
+    const float* p = jb.part + k * jb.D + j;
+    for (int b0 = grp; b0 < jb.nblk; b0 += 4 * UNR) {
+      float v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int b = b0 + 4 * u;
+        v[u] = b < jb.nblk ? p[(size_t)b * jb.stride_blk] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) s += v[u];
+    }
+  }
+  red[grp][lane] = s;
+  __syncthreads();
+  if (grp == 0 && j < jb.D && out) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[j] = jb.accumulate ? out[j] + t : t;
+  }
+}
+
 // The embedding backward's tail in two launches (after emb_bwd_kernel): A = the word-gradient
 // pieces (chunk blocks) beside the position gradient (pos blocks); B = the crossing runs'
 // combine beside the LayerNorm dgamma / dbeta column sums of emb_bwd_kernel's partials.  Each
@@ -676,6 +741,10 @@ struct EmbTail {
   unsigned char* now;
   unsigned char* ever;
   int T, B, S, D, chunks, pos_gy, cs_gx, lnblk, acc_mode, accumulate;
+  int pos_blocks;
+  // the backward's deferred column sums (bias / LayerNorm-affine gradients of every block), run as
+  // extra blocks of the A launch instead of a colsum_batched launch of their own (cs.n == 0: none)
+  ColsumBatch cs;
 };
 __global__ __launch_bounds__(256) void emb_tail_a_kernel(EmbTail t) {
   const int bx = blockIdx.x;
@@ -684,6 +753,10 @@ __global__ __launch_bounds__(256) void emb_tail_a_kernel(EmbTail t) {
     return;
   }
   const int r = bx - t.chunks;
+  if (r >= t.pos_blocks) {
+    colsum_batched_block<16>(t.cs, r - t.pos_blocks);
+    return;
+  }
   pos_grad_block(r / t.pos_gy, r % t.pos_gy, t.pos_gy, t.dz, t.dpos, t.B, t.S, t.D, t.accumulate, t.cu);
 }
 __global__ __launch_bounds__(256) void emb_tail_b_kernel(EmbTail t) {
@@ -754,53 +827,200 @@ __global__ __launch_bounds__(256) void colsum_bf16_partial_batched_kernel(Colsum
   *reinterpret_cast<float4*>(cb.part[j] + (size_t)bx * N + c4) = make_float4(s0, s1, s2, s3);
 }
 
-// Deferred column-sum finalisation: every bias / LayerNorm-affine gradient of the
-// backward leaves its per-block partials in a slot of its own, and ONE launch at the
-// end of the backward reduces all of them (instead of one small launch per producer).
-// Same per-column fixed-order sum as colsum_kernel: bitwise identical results.
-constexpr int COLSUM_MAXJ = 32;
-struct ColsumJob {
-  const float* part;
-  float* out[3];
-  int nblk, stride_blk, D, nout, accumulate;
-};
-struct ColsumBatch {
-  ColsumJob j[COLSUM_MAXJ];
-  int start[COLSUM_MAXJ + 1];  // first block of job i (blocks = ceil(D/64) * nout)
-  int n;
-};
-
 template <int UNR>
 __global__ __launch_bounds__(256) void colsum_batched_kernel(ColsumBatch cb) {
-  __shared__ float red[4][64];
-  int ji = 0;
-  while (ji + 1 < cb.n && (int)blockIdx.x >= cb.start[ji + 1]) ++ji;
-  const ColsumJob& jb = cb.j[ji];
-  const int local = blockIdx.x - cb.start[ji];
-  const int cblk = (jb.D + 63) / 64;
-  const int k = local / cblk;
-  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int j = (local - k * cblk) * 64 + lane;
-  float* out = jb.out[k];
-  float s = 0.f;
-  if (j < jb.D) {
-    const float* p = jb.part + k * jb.D + j;
-    for (int b0 = grp; b0 < jb.nblk; b0 += 4 * UNR) {
-      float v[UNR];
+  colsum_batched_block<UNR>(cb, blockIdx.x);
+}
+
+
+// ------------------------------------------------------------------ pruned head + output-LN backward
+// The [CLS]-pruned training step's head (ops/functional.py HeadFn, fold_head): ONE launch for what
+// were three -- the head forward with its loss mean (head_fwd_mean_kernel), the head backward
+// (head_bwd_kernel) and the last block's output-LayerNorm backward (ln_bwd_kernel on the pruned
+// rows), with the upstream gradient of the loss known to be 1 (loss.backward(unit_grad)).
+//   blocks [0, nlb): ln_bwd_kernel's row blocks (16 rows per 512-thread block, half-wave rows);
+//     each wave first computes the logits / dlogits of its two rows (head_logits: the head
+//     forward's own code), the half-wave rebuilds its row's head gradient dy = (d0 w0 + d1 w1) *
+//     keep (head_dh, bf16 -- head_bwd_kernel's dhidden) and runs the LayerNorm backward on it.
+//   blocks [nlb, nlb + D / 64): head_bwd_kernel's column work, two 32-column groups per block,
+//     after every wave has computed the dlogits of B / 8 rows; the first of them also writes the
+//     logits / row losses / dlogits and the loss mean (head_fwd_mean_kernel's outputs).
+// Every value is computed by the same expressions as in the three kernels it replaces, over the
+// same rows per lane, so the outputs are bitwise theirs.  Head row b is hidden row b (the pruned
+// layout); rows in [B, T) are the filler rows (no head gradient).
+#include "head_common.h"
+
+struct HeadLnArgs {
+  HeadArgs h;
+  LnArgs ln;
+  int nlb;
+};
+
+constexpr int HLB_COLS = 32, HLB_GROUPS = 8, HLB_ROWS = 8;  // head_bwd_kernel's column tiling
+
+__global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const HeadArgs& h = args.h;
+  const LnArgs& a = args.ln;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int D = a.D;
+  const bool hdrop = h.thr != 0;
+  const uint32_t hseed = hdrop ? hash32(h.seed_ptr[0], h.site) : 0u;
+  if ((int)blockIdx.x >= args.nlb) {
+    // ---- head_bwd_kernel's column blocks (+ the head forward's outputs in the first one)
+    const int cb = blockIdx.x - args.nlb;
+    float* dl = lds;                        // [B][2] dlogits
+    float* red = lds + 2 * ((h.B + 3) & ~3);  // [2 groups][2][8][32]
+    for (int b = w; b < h.B; b += 16) {  // rows b and b + 8 of this wave, interleaved
+      const int rows[2] = {b, b + 8 < h.B ? b + 8 : -1};
+      float z0[2], z1[2];
+      head_logits_n<2>(h, rows, lane, z0, z1);
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        const int b = b0 + 4 * u;
-        v[u] = b < jb.nblk ? p[(size_t)b * jb.stride_blk] : 0.f;
+      for (int r = 0; r < 2; ++r) {
+        if (rows[r] < 0) continue;
+        const int br = rows[r];
+        float loss, d0, d1;
+        head_loss_grad(h, br, z0[r], z1[r], loss, d0, d1);
+        if (lane == 0) {
+          dl[2 * br] = d0;
+          dl[2 * br + 1] = d1;
+          if (cb == 0) {
+            h.logits[2 * br] = z0[r];
+            h.logits[2 * br + 1] = z1[r];
+            h.row_loss[br] = loss;
+            h.dlogits[2 * br] = d0;
+            h.dlogits[2 * br + 1] = d1;
+          }
+        }
+      }
+    }
+    __syncthreads();  // dlogits in LDS; (block 0) every row loss written, workgroup-visible
+    if (cb == 0 && w == 0) loss_mean(h, lane);
+    const int sub = threadIdx.x >> 8, t = threadIdx.x & 255;
+    const int c = t % HLB_COLS, grp = t / HLB_COLS;
+    const int col = cb * 2 * HLB_COLS + sub * HLB_COLS + c;
+    const bool live = col < D;
+    const int colc = live ? col : 0;
+    float g0 = 0.f, g1 = 0.f;
+    for (int b0 = grp; b0 < h.B; b0 += HLB_GROUPS * HLB_ROWS) {
+      float x[HLB_ROWS];
+#pragma unroll
+      for (int u = 0; u < HLB_ROWS; ++u) {
+        const int b = min(b0 + u * HLB_GROUPS, h.B - 1);
+        x[u] = bf2f(h.hidden[cls_row(h, b) * D + colc]);
       }
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) s += v[u];
+      for (int u = 0; u < HLB_ROWS; ++u) {
+        const int b = b0 + u * HLB_GROUPS;
+        if (b >= h.B) break;
+        const float d0 = dl[2 * b], d1 = dl[2 * b + 1];
+        const bool keep = !hdrop || drop_keep(hseed, (uint32_t)(b * D + colc), h.thr);
+        const float sc = hdrop ? (keep ? h.dscale : 0.f) : 1.f;
+        const float xv = x[u] * sc;
+        head_col_acc(g0, d0, xv);
+        head_col_acc(g1, d1, xv);
+      }
     }
+    float* rd = red + sub * 2 * HLB_GROUPS * HLB_COLS;
+    rd[(0 * HLB_GROUPS + grp) * HLB_COLS + c] = g0;
+    rd[(1 * HLB_GROUPS + grp) * HLB_COLS + c] = g1;
+    __syncthreads();
+    if (grp < 2 && live) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < HLB_GROUPS; ++i) s += rd[(grp * HLB_GROUPS + i) * HLB_COLS + c];
+      float* dst = h.dW + grp * D + col;
+      *dst = h.accumulate ? *dst + s : s;
+    }
+    if (cb == 0 && threadIdx.x < 2) {
+      float s = 0.f;
+      for (int b = 0; b < h.B; ++b) s += dl[2 * b + threadIdx.x];
+      h.db[threadIdx.x] = h.accumulate ? h.db[threadIdx.x] + s : s;
+    }
+    return;
   }
-  red[grp][lane] = s;
-  __syncthreads();
-  if (grp == 0 && j < jb.D && out) {
-    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    out[j] = jb.accumulate ? out[j] + t : t;
+  // ---- ln_bwd_kernel's row blocks, dy from the head
+  const int hl = lane & (HL - 1);
+  const bool drop = a.thr != 0;
+  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
+  float dg[CH][8] = {}, db[CH][8] = {}, dbias[CH][8] = {};
+  float4 gm[CH][2], w0v[CH][2], w1v[CH][2];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = 8 * (hl + HL * c);
+    gm[c][0] = *reinterpret_cast<const float4*>(a.gamma + col);
+    gm[c][1] = *reinterpret_cast<const float4*>(a.gamma + col + 4);
+    w0v[c][0] = *reinterpret_cast<const float4*>(h.W + col);
+    w0v[c][1] = *reinterpret_cast<const float4*>(h.W + col + 4);
+    w1v[c][0] = *reinterpret_cast<const float4*>(h.W + D + col);
+    w1v[c][1] = *reinterpret_cast<const float4*>(h.W + D + col + 4);
+  }
+  const int rows_per_iter = (blockDim.x >> 5);
+  for (int base = blockIdx.x * rows_per_iter; base < a.T; base += args.nlb * rows_per_iter) {
+    const int row = base + (threadIdx.x >> 5);
+    const int rr = min(row, a.T - 1);
+    // this half-wave's row operands first (their latency overlaps the logits)
+    const float mean = a.mean[rr], rstd = a.rstd[rr];
+    float xh[CH][8];
+    uint32_t keep;
+    ln_load_sum(a, rr, hl, drop, seed, xh, keep);
+    // the wave's two rows' dlogits (whole-wave reductions: wave-uniform control flow)
+    const int rA = base + 2 * w;
+    const int rows[2] = {rA < h.B ? rA : -1, rA + 1 < h.B ? rA + 1 : -1};
+    float z0[2] = {0.f, 0.f}, z1[2] = {0.f, 0.f};
+    if (rows[0] >= 0) head_logits_n<2>(h, rows, lane, z0, z1);
+    const int mine = lane < HL ? 0 : 1;
+    float d0 = 0.f, d1 = 0.f;
+    if (rows[mine] >= 0) {
+      float loss;
+      head_loss_grad(h, rows[mine], z0[mine], z1[mine], loss, d0, d1);
+    }
+    if (row >= a.T) continue;  // (whole half-waves)
+    const bool grad_row = row < h.B && !empty_seq(h, row);
+    float dyv[CH][8];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col0 = 8 * (hl + HL * c);
+      const uint32_t kb = hdrop ? drop_keep_bits<8>(hseed, (uint32_t)(row * D + col0), h.thr) : 0xffu;
+      const float wa[8] = {w0v[c][0].x, w0v[c][0].y, w0v[c][0].z, w0v[c][0].w,
+                           w0v[c][1].x, w0v[c][1].y, w0v[c][1].z, w0v[c][1].w};
+      const float wb[8] = {w1v[c][0].x, w1v[c][0].y, w1v[c][0].z, w1v[c][0].w,
+                           w1v[c][1].x, w1v[c][1].y, w1v[c][1].z, w1v[c][1].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sc = hdrop ? (((kb >> e) & 1u) ? h.dscale : 0.f) : 1.f;
+        dyv[c][e] = grad_row ? bf2f(head_dh(d0, d1, wa[e], wb[e], sc)) : 0.f;
+      }
+    }
+    ln_bwd_row(a, row, hl, drop, gm, dyv, xh, keep, mean, rstd, dg, db, dbias);
+  }
+  // fold the two half-waves (same columns, different rows), then the 8 waves (ln_bwd_kernel)
+  float* out = a.part + (size_t)blockIdx.x * 3 * D;
+  float (*accs[3])[8] = {dg, db, dbias};
+#pragma unroll
+  for (int which = 0; which < 3; ++which) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) accs[which][c][e] += __shfl_xor(accs[which][c][e], 32, 64);
+    if (lane < HL) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        float* dst = lds + w * D + 8 * (hl + HL * c);
+        *reinterpret_cast<float4*>(dst) =
+            make_float4(accs[which][c][0], accs[which][c][1], accs[which][c][2], accs[which][c][3]);
+        *reinterpret_cast<float4*>(dst + 4) =
+            make_float4(accs[which][c][4], accs[which][c][5], accs[which][c][6], accs[which][c][7]);
+      }
+    }
+    __syncthreads();
+    const int nw = blockDim.x >> 6;
+    for (int col = threadIdx.x; col < D; col += blockDim.x) {
+      float sum = 0.f;
+      for (int i = 0; i < nw; ++i) sum += lds[i * D + col];
+      out[which * D + col] = sum;
+    }
+    __syncthreads();
   }
 }
 
@@ -850,6 +1070,42 @@ int fd_ln_bwd(const void* dy, const void* x, const void* r, const float* gamma, 
   return 0;
 }
 
+
+// The pruned training step's head + output-LayerNorm backward in one launch (head_ln_bwd_kernel).
+// Head: hidden [T][D] (head row b = row b, b < B), W [2][D], bias [2], labels [B], logits / dlogits
+// [B][2], loss [1], row_loss [B], loss_acc (nullable), dW [2][D] / db [2] (first-write unless
+// accumulate), own [B + 1] (nullable), teacher logits (nullable).  LayerNorm: z = the saved pre-LN sum
+// [T][D], gamma, mean / rstd [T], dz / dx out [T][D] (dx nullable without dropout), part: the
+// [*nblk_out][3][D] dgamma / dbeta / dbias partials (deferred column sums).  D == 768.
+int fd_head_ln_bwd(const void* hidden, int B, int T, int D, const float* W, const float* bias,
+                   const uint32_t* seed_ptr, uint32_t hsite, uint32_t hthr, float hdscale, const long long* labels,
+                   float* logits, float* loss, float* dlogits, float* row_loss, float* loss_acc, float* dW, float* db,
+                   int accumulate, const int* own, const float* tlogits, float kd_T, float kd_alpha, const void* z,
+                   const float* gamma, const float* mean, const float* rstd, void* dz, void* dx, float* part,
+                   uint32_t site, uint32_t thr, float dscale, const int* row_map, int* nblk_out, hipStream_t st) {
+  if (D != 768 || B <= 0 || B > T || B > 1024 || !labels || !row_loss) return 1;
+  if (tlogits && !(kd_T > 0.f)) return 3;
+  HeadLnArgs x{};
+  HeadArgs& h = x.h;
+  h.hidden = (const bf16_t*)hidden; h.B = B; h.S = 1; h.D = D; h.W = W; h.bias = bias;
+  h.seed_ptr = seed_ptr; h.site = hsite; h.thr = hthr; h.dscale = hdscale; h.labels = labels;
+  h.logits = logits; h.loss = loss; h.dlogits = dlogits; h.row_loss = row_loss; h.loss_acc = loss_acc;
+  h.dW = dW; h.db = db; h.accumulate = accumulate; h.cls = nullptr; h.T = T; h.own = own;
+  h.tlogits = tlogits; h.kd_T = kd_T; h.kd_alpha = kd_alpha;
+  LnArgs& a = x.ln;
+  a.zin = 1;
+  a.x = (const bf16_t*)z; a.gamma = gamma; a.mean = (float*)mean; a.rstd = (float*)rstd;
+  a.dz = (bf16_t*)dz; a.dx = (bf16_t*)dx; a.part = part; a.T = T; a.D = D;
+  a.seed_ptr = seed_ptr; a.site = site; a.thr = thr; a.dscale = dscale; a.row_map = row_map;
+  const int rows = LN_BWD_THREADS / 32;
+  x.nlb = std::min(LN_GRID, (T + rows - 1) / rows);  // = ln_bwd's grid: the same partial rows
+  if (nblk_out) *nblk_out = x.nlb;
+  const size_t smem = std::max<size_t>((LN_BWD_THREADS / 64) * D * sizeof(float),
+                                       (2 * ((B + 3) & ~3) + 2 * 2 * HLB_GROUPS * HLB_COLS) * sizeof(float));
+  hipLaunchKernelGGL(head_ln_bwd_kernel, dim3(x.nlb + D / (2 * HLB_COLS)), dim3(LN_BWD_THREADS), smem, st, x);
+  return 0;
+}
+
 int fd_emb_fwd(const void* ids, int ids64, const void* word, const void* pos, const float* gamma,
                const float* beta, void* y, float* mean, float* rstd, int T, int S, int D, float eps,
                const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale, const int* row_map,
@@ -879,8 +1135,10 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
                float* dword, float* dpos, float* dgamma, float* dbeta, float* dz_buf, float* work, int T, int S,
                int B, int P, int V, int D, const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float dscale,
                int accumulate, unsigned char* now, unsigned char* ever, const int* row_map, const int* cu,
-               hipStream_t st) {
+               int ncs, const float* const* cs_parts, float* const* cs_outs, const int* cs_nblk, const int* cs_stride,
+               const int* cs_D, const int* cs_nout, const int* cs_acc, hipStream_t st) {
   if (D != 768) return 1;
+  if (ncs < 0 || ncs > COLSUM_MAXJ) return 5;
   EmbArgs a{};
   a.dy = (const bf16_t*)dy; a.ids = ids; a.ids64 = ids64; a.word = (const bf16_t*)word;
   a.pos = (const bf16_t*)pos; a.gamma = gamma; a.mean = (float*)mean; a.rstd = (float*)rstd; a.dz = dz_buf;
@@ -905,7 +1163,18 @@ int fd_emb_bwd(const void* dy, const void* ids, int ids64, const long long* sort
   t.acc_mode = now ? accumulate : 1;
   t.accumulate = accumulate;
   const int pos_rows = !accumulate && P > S ? P : S;
-  hipLaunchKernelGGL(emb_tail_a_kernel, dim3(t.chunks + pos_rows * t.pos_gy), dim3(256), 0, st, t);
+  t.pos_blocks = pos_rows * t.pos_gy;
+  int cs_blocks = 0;
+  t.cs.n = ncs;
+  for (int i = 0; i < ncs; ++i) {
+    if (cs_nout[i] < 1 || cs_nout[i] > 3 || cs_D[i] <= 0) return 6;
+    t.cs.j[i] = ColsumJob{cs_parts[i], {cs_outs[3 * i], cs_outs[3 * i + 1], cs_outs[3 * i + 2]}, cs_nblk[i],
+                          cs_stride[i], cs_D[i], cs_nout[i], cs_acc[i]};
+    t.cs.start[i] = cs_blocks;
+    cs_blocks += ((cs_D[i] + 63) / 64) * cs_nout[i];
+  }
+  t.cs.start[ncs] = cs_blocks;
+  hipLaunchKernelGGL(emb_tail_a_kernel, dim3(t.chunks + t.pos_blocks + cs_blocks), dim3(256), 0, st, t);
   hipLaunchKernelGGL(emb_tail_b_kernel, dim3(t.chunks + 2 * t.cs_gx), dim3(256), 0, st, t);
   return 0;
 }

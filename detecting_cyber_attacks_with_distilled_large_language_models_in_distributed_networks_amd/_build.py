@@ -127,7 +127,7 @@ def build_hip(verbose=False, force=False, jobs=None) -> str:
     inc, defs, libdir = _torch_flags()
     bo = os.path.join(BUILD, "binding.o")
     objs.append(bo)
-    if force or _newer(bo, [binding]):
+    if force or _newer(bo, [binding] + headers):
         jobs_list.append(([HIPCC, "-O2", "-std=c++17", "-fPIC", "-w"] + defs + ["-I" + i for i in inc]
                           + ["-c", binding, "-o", bo], bo))
     if jobs_list:

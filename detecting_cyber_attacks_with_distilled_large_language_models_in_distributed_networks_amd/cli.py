@@ -167,6 +167,15 @@ def _scaling(argv):
         base = results[0]["per_client_batches_per_sec"]
         for r in results:
             r["per_client_efficiency_vs_1gpu"] = round(r["per_client_batches_per_sec"] / base, 4)
+        # per-step time and FedAvg round time side by side (bench.py times them apart: the step
+        # window holds local steps only, the round -- one per 2,541 reference steps -- its own)
+        print(f"{'gpus':>4} {'ms/step':>9} {'batches/s/client':>17} {'eff':>6} {'fedavg round ms':>16} "
+              f"{'all-reduce GB/s':>16} {'ms/step incl. round':>20}")
+        for r in results:
+            fr, bw, inc = r.get("fedavg_round_ms"), r.get("allreduce_busbw_GBps"), r.get("ms_per_step_incl_round")
+            print(f"{r['n_gpus']:>4} {r['ms_per_step']:>9.4f} {r['per_client_batches_per_sec']:>17.2f} "
+                  f"{r['per_client_efficiency_vs_1gpu']:>6.3f} {'-' if fr is None else f'{fr:.3f}':>16} "
+                  f"{'-' if bw is None else f'{bw:.1f}':>16} {'-' if inc is None else f'{inc:.4f}':>20}")
         with open(ns.out, "w") as f:
             json.dump(results, f, indent=1)
         from .utils.plots import plot_scaling

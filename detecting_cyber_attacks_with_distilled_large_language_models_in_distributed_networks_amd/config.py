@@ -22,6 +22,9 @@ class FedConfig:
     # --- data (client1.py:23, :84-93, :356) -------------------------------------------
     csv_path: Optional[str] = None          # None -> synthetic CICIDS2017-shaped data
     synthetic_rows: int = 225_745           # full Friday-DDoS file size
+    # synthetic generator setting (data/synthetic.py PROFILES): "default" (saturates near 99.95 %),
+    # "calibrated" (local models near the reference's 99.05 %), "hard" (numerics tests, ~95 %)
+    data_profile: str = "default"
     data_fraction: float = 0.1              # client1.py:23
     base_seed: int = 42                     # client1.py:89 (client2.py:84 uses 43)
     partition: str = "iid_overlap"          # "iid_overlap" (reference) | "disjoint"

@@ -13,9 +13,9 @@ differs from the captured one (the last partial batch, drop_last=False) run
 eagerly.
 
 ``step_fn.prepare`` (optional): called eagerly before every replay and before the capture, for
-state a replay does not refresh by itself -- the model's W^T copies after an out-of-band weight
-change (FedAvg, checkpoint load): the fused Adam epilogue keeps them current, so the graphs hold
-no transpose launch (models/distilbert.py refresh_wT).
+state a replay does not refresh by itself -- the model's bf16 weight shadow after an out-of-band
+write of its fp32 masters (a checkpoint load): the captured forward holds no shadow sync of its
+own (models/distilbert.py prepare_replay).
 
 Unpadded model path: a batch also carries its real-token count; ``bucket(tokens,
 B, S)`` (the model's ``packed_rows``) maps it to the packed row count the step
@@ -115,7 +115,7 @@ class GraphedTrainStep:
         prepare = getattr(self.step_fn, "prepare", None)
         if hit is not None:
             if prepare is not None:
-                prepare()  # eager state the graph does not refresh itself (the model's W^T copies)
+                prepare()  # eager state the graph does not refresh itself (the model's weight shadow)
             g, static, loss = hit
             blk = contiguous_block(ids, mask, labels) if static["flat"] is not None else None
             if blk is not None:

@@ -74,7 +74,6 @@ class ArenaAdam:
         self.host_step = 0
         self._begun = False
         self._done = []  # (offset, length) spans already updated this step
-        self._n_wT = 0   # of those, weight matrices whose W^T copy the same epilogue refreshed
         use = (self.overlap and dev.type == "cuda" and hasattr(self.model, "layer_span")
                and getattr(self.model, "impl", "hip") == "hip")
         self._side = torch.cuda.Stream(device=dev) if use else None
@@ -136,21 +135,18 @@ class ArenaAdam:
     def can_fuse(self) -> bool:
         """Whether the model's weight-gradient GEMMs may apply this optimizer's step."""
         m = self.model
-        # the fused step updates weights inside the backward: safe when the dX GEMMs read W^T copies
-        # taken before it, or when every weight gradient runs in the all-layer launch at the end
+        # the fused step updates weights inside the backward: safe only when every weight gradient
+        # runs in the all-layer launch at the end (after the last dX GEMM that reads W)
         return (self.fuse_dw and not self.overlap and self.arena.device.type == "cuda"
-                and getattr(m, "impl", "") == "hip"
-                and (getattr(m, "transposed_dx", False) or getattr(m, "batch_dw", False))
+                and getattr(m, "impl", "") == "hip" and getattr(m, "batch_dw", False)
                 and getattr(m, "group_dw", False) and getattr(m, "layer_grads_hook", None) is None
                 and self.arena.shadow is not None)
 
-    def fused_args(self, grads, n_wT: int = 0):
+    def fused_args(self, grads):
         """(state tensors, hyper-parameters) for a weight-gradient GEMM that applies Adam to
-        ``grads`` (arena grad views) in its epilogue; those spans are skipped by ``step()``.
-        n_wT: how many of them also refresh their transposed bf16 weight copy (the model's W^T)."""
+        ``grads`` (arena grad views) in its epilogue; those spans are skipped by ``step()``."""
         from ..ops import kernels as K  # noqa: F401  (extension must be present)
         self._begin()
-        self._n_wT += int(n_wT)
         A = self.arena
         base = A.grad.data_ptr()
         st = []
@@ -184,7 +180,7 @@ class ArenaAdam:
         self.v.zero_()
         self.step_t.zero_()
         self.host_step = 0
-        self._done, self._begun, self._n_wT = [], False, 0
+        self._done, self._begun = [], False
         if getattr(self.model, "emb_ever", None) is not None:
             self.model.emb_ever.zero_()
 
@@ -259,12 +255,8 @@ class ArenaAdam:
                     self._update(off, n, sparse and off <= woff < off + n)
             if self._side is not None:
                 torch.cuda.current_stream(A.device).wait_stream(self._side)
-            # the model's W^T copies stay valid only if every transposed weight was updated by an
-            # epilogue that also rewrote its W^T (models/distilbert.py refresh_wT)
-            n_t = getattr(self.model, "n_transposed", 0)
-            self.model.mark_shadow_synced(wT_kept=bool(n_t) and self._n_wT == n_t)
+            self.model.mark_shadow_synced()
             self._done = []
-            self._n_wT = 0
             self._begun = False
             return
         self.host_step += 1

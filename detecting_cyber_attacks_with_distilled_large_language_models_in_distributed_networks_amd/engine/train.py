@@ -48,16 +48,11 @@ class fused_adam_scope:
         return False
 
 
-_ONES = {}
-
-
 def _one(device) -> torch.Tensor:
-    """Persistent scalar 1.0 seeding ``backward`` (autograd would launch a fill per step)."""
-    t = _ONES.get(str(device))
-    if t is None:
-        t = torch.ones((), dtype=torch.float32, device=device)
-        _ONES[str(device)] = t
-    return t
+    """Persistent scalar 1.0 seeding ``backward`` (autograd would launch a fill per step); the
+    forward is told so (``forward_loss(unit_backward=True)``: ops/kernels.py unit_grad)."""
+    from ..ops.kernels import unit_grad
+    return unit_grad(device)
 
 
 def make_step_fn(model, optimizer, criterion=None):
@@ -67,14 +62,14 @@ def make_step_fn(model, optimizer, criterion=None):
         optimizer.zero_grad()
         with fused_adam_scope(model, optimizer):
             if fused:
-                loss, _ = model.forward_loss(ids, mask, labels, tokens=tokens)
+                loss, _ = model.forward_loss(ids, mask, labels, tokens=tokens, unit_backward=True)
             else:
                 loss = criterion(model(ids, mask, tokens=tokens), labels)
             loss.backward(_one(loss.device) if loss.dtype == torch.float32 and loss.dim() == 0 else None)
         optimizer.step()
         return loss.detach()
 
-    step.prepare = getattr(model, "refresh_wT", None)
+    step.prepare = getattr(model, "prepare_replay", None)
     return step
 
 
@@ -88,12 +83,14 @@ def make_kd_step_fn(student, teacher, optimizer, temperature: float = 2.0, alpha
         with torch.no_grad():
             t_logits = teacher(ids, mask, tokens=tokens)
         with fused_adam_scope(student, optimizer):
-            loss, _ = student.forward_loss(ids, mask, labels, tokens=tokens, kd=(t_logits, temperature, alpha))
+            loss, _ = student.forward_loss(ids, mask, labels, tokens=tokens, kd=(t_logits, temperature, alpha),
+                                           unit_backward=True)
             loss.backward(_one(loss.device) if loss.dtype == torch.float32 and loss.dim() == 0 else None)
         optimizer.step()
         return loss.detach()
 
-    step.prepare = getattr(student, "refresh_wT", None)
+    preps = [f for f in (getattr(student, "prepare_replay", None), getattr(teacher, "prepare_replay", None)) if f]
+    step.prepare = (lambda: [f() for f in preps]) if preps else None
     return step
 
 

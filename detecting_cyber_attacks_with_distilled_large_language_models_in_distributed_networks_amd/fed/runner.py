@@ -71,7 +71,7 @@ class FederatedClient:
                     self.frame = pd.read_csv(cfg.csv_path)
                 else:
                     # Same seeded synthetic file on every client (they sample it independently).
-                    self.frame = generate_cicids2017(cfg.synthetic_rows, seed=0)
+                    self.frame = generate_cicids2017(cfg.synthetic_rows, seed=0, profile=cfg.data_profile)
             self.tokenizer = WordPieceTokenizer.from_pretrained(cfg.model_path)
             self.data = build_client_data(self.frame, self.idx, cfg.data_fraction, cfg.base_seed, cfg.max_len,
                                           self.tokenizer, cfg.partition, self.num_clients, log=log)
@@ -371,33 +371,54 @@ def run_virtual_clients(client: "FederatedClient", n_clients: int = 2) -> Dict:
     (unweighted mean; ``_average_masters`` = fedavg_'s sum + ``scale_cast``) and every client then
     evaluates the aggregate on its own test split (client1_aggregated_metrics.csv).  Returns the
     per-client local / aggregated metrics, the pooled aggregated confusion matrix and each local
-    model's relative L2 distance to the aggregate (0 would mean the "average" was an identity)."""
+    model's relative L2 distance to the aggregate (0 would mean the "average" was an identity).
+
+    With a teacher (the distillation extension, BASELINE.json config 5) every virtual client does
+    what ``run_round`` does for a real one: the shared BERT-base teacher init is fine-tuned on the
+    client's own split (``teacher_epochs``), then the client's student is distilled from it; the
+    students are averaged (the teachers stay local, as in run_round).  Each record then also holds
+    the client's ``teacher_test`` metrics."""
     cfg, model = client.cfg, client.model
     if client.di.distributed:
         raise RuntimeError("virtual clients run in a single-process job (world size 1)")
-    if client.teacher is not None:
-        raise RuntimeError("virtual clients: the distillation extension runs one client per process")
+    teacher = client.teacher
     dev = model.device
     A = model.arena
     init = A.master.detach().clone()
+    t_init = teacher.arena.master.detach().clone() if teacher is not None else None
     locals_, recs = [], []
     for v in range(n_clients):
         data = build_client_data(client.frame, v, cfg.data_fraction, cfg.base_seed, cfg.max_len, client.tokenizer,
                                  cfg.partition, n_clients)
         loader = DeviceLoader(data.train, cfg.batch_size, shuffle=True, device=dev, seed=cfg.client_seed(v))
         test = DeviceLoader(data.test, cfg.eval_batch_size, device=dev)
+        rec = {"client": v + 1, "train_rows": len(data.train), "test_rows": len(data.test)}
+        t0 = time.perf_counter()
+        if teacher is not None:
+            with torch.no_grad():
+                teacher.arena.master.copy_(t_init)
+            teacher.sync_shadow(force=True)
+            t_opt = ArenaAdam(teacher, lr=cfg.lr)
+            t_opt.reset_state()
+            teacher.train()
+            rec["teacher_train"] = train_model(teacher, loader, None, t_opt, int(cfg.extra.get("teacher_epochs",
+                                                                                                cfg.epochs)),
+                                               log=client.log, use_graph=cfg.use_graph)
+            rec["teacher_test"] = _metrics_record(evaluate_model(teacher, test, name=f"Client {v + 1} teacher test"))
+            teacher.eval()
+            del t_opt
         with torch.no_grad():
             A.master.copy_(init)
         model.sync_shadow(force=True)
         opt = ArenaAdam(model, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
                         decoupled=cfg.decoupled_weight_decay)
         opt.reset_state()  # (also clears the sparse word rows' "has Adam state" flags)
-        t0 = time.perf_counter()
-        tr = train_model(model, loader, None, opt, cfg.epochs, log=client.log, use_graph=cfg.use_graph)
+        tr = train_model(model, loader, None, opt, cfg.epochs, log=client.log, use_graph=cfg.use_graph,
+                         teacher=teacher, kd_temperature=cfg.kd_temperature, kd_alpha=cfg.kd_alpha)
         local = _metrics_record(evaluate_model(model, test, name=f"Client {v + 1} local test"))
         locals_.append(A.master.detach().clone())
-        recs.append({"client": v + 1, "train_rows": len(data.train), "test_rows": len(data.test),
-                     "train": tr, "train_wall_s": time.perf_counter() - t0, "local_test": local, "test": test})
+        rec.update({"train": tr, "train_wall_s": time.perf_counter() - t0, "local_test": local, "test": test})
+        recs.append(rec)
         del opt, loader
     t0 = time.perf_counter()
     _average_masters(model, locals_)

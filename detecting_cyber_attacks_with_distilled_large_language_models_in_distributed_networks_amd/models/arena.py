@@ -83,6 +83,10 @@ class ParamArena:
         if zero_buffer:
             self.grad.zero_()
 
+    def written(self, name: str) -> bool:
+        """Whether the grad slot already holds a value this step (``mark_written`` without marking)."""
+        return name in self._written
+
     def mark_written(self, name: str) -> bool:
         """Return True if the grad slot already holds a value this step (accumulate)."""
         if name in self._written:

@@ -249,13 +249,10 @@ class DDoSClassifier(nn.Module):
         self.sparse_word_grad = True
         # set by an overlapping optimizer (engine/optim.py): called per block during backward
         self.layer_grads_hook = None
-        # HIP path: backward dX GEMMs read W^T copies (K-major staging is ~30% faster than
-        # reading W MN-major; the per-step transpose of the encoder weights is ~85 MB r+w)
-        self.transposed_dx = os.environ.get("FD_TRANSPOSED_DX", "0") == "1"
         # (Removed after losing their A/B, logs in profiles/: the weight-gradient GEMMs on a side
-        # stream -- 3.24 vs 3.20 ms/step, r1_ab_wgrad_side_stream.txt; the W^T copies on a side
-        # stream during the forward -- 2.48 vs 2.36, r1_ab_transpose_overlap_slower.txt; the
-        # embedding backward + column-sum flush beside the dW launch -- neutral,
+        # stream -- 3.24 vs 3.20 ms/step, r1_ab_wgrad_side_stream.txt; per-step W^T copies for the
+        # backward's dX GEMMs -- 1.7343 vs 1.7031 ms/step, r4_ab_dx_layouts.txt (the dX GEMMs read
+        # W itself); the embedding backward + column-sum flush beside the dW launch -- neutral,
         # r2_ab_tail_overlap_groupm.txt.)
         # HIP path: grouped weight-gradient GEMMs (RunCtx.group_dw)
         self.group_dw = True
@@ -306,10 +303,6 @@ class DDoSClassifier(nn.Module):
         self._grad_token = None
         self._synced_version = -1
         self._hip_cache = None
-        # W^T copies of the backward's dX GEMMs: stale until taken; kept current by the fused Adam
-        # epilogue (refresh_wT)
-        self._wT_dirty = True
-        self._wT_kept_by_step = False
         self.to(device)
 
     # -------------------------------------------------------------- device management
@@ -330,7 +323,6 @@ class DDoSClassifier(nn.Module):
         self._grad_token = torch.zeros((), device=dev, requires_grad=True)
         self._hip_cache = None
         self._synced_version = -1
-        self._wT_dirty = True
         return self
 
     @property
@@ -385,40 +377,20 @@ class DDoSClassifier(nn.Module):
         if force or v != self._synced_version:
             self.arena.sync_shadow()
             self._synced_version = self._param_version()
-            self._wT_dirty = True
 
-    def mark_shadow_synced(self, wT_kept: bool = False):
-        """The shadow was rewritten outside ``sync_shadow`` (an Adam step, FedAvg's scale_cast).
-        wT_kept: the writer also rewrote the W^T copies (the fused Adam epilogue of the all-layer
-        weight-gradient launch) -- otherwise they are stale until ``refresh_wT``."""
+    def mark_shadow_synced(self):
+        """The shadow was rewritten outside ``sync_shadow`` (an Adam step, FedAvg's scale_cast)."""
         self._synced_version = self._param_version()
-        self._wT_kept_by_step = bool(wT_kept)
-        if not wT_kept:
-            self._wT_dirty = True
 
-    @property
-    def n_transposed(self) -> int:
-        """Weight matrices with a W^T copy (4 per block on the HIP path, 0 otherwise)."""
-        return 4 * self.config.n_layers if self.transposed_dx else 0
-
-    def wT_stale(self) -> bool:
-        return self.transposed_dx and (self._wT_dirty or not self._wT_kept_by_step)
-
-    def refresh_wT(self, force: bool = False) -> bool:
-        """Re-derive the backward's W^T copies from the bf16 shadow (one transpose launch) if
-        anything but the fused Adam epilogue -- which rewrites them itself -- changed the weights
-        since they were taken: a FedAvg / broadcast / checkpoint load / an unfused optimizer step.
-        Called by a training forward, and before a graph replay (``GraphedTrainStep``: the graphs
-        hold no transpose launch of their own while the fused epilogue keeps W^T current).
-        Returns whether it launched."""
-        if not (self.transposed_dx and self.impl == "hip") or not (force or self.wT_stale()):
-            return False
-        from ..ops import kernels as K
+    def prepare_replay(self):
+        """Eager state a captured training step does not refresh by itself, brought up to date
+        before every replay and capture (``GraphedTrainStep``, step_fn.prepare): the bf16 shadow the
+        kernels read, after an out-of-band write of the fp32 masters (``load_state_dict``, a torch
+        optimizer, ...).  A captured forward holds no ``sync_shadow`` of its own, so without this a
+        replay after a checkpoint load would train the pre-load weights.  (Writers that keep the
+        shadow current themselves -- the Adam kernels, FedAvg's scale_cast -- call
+        ``mark_shadow_synced``; the check is a host-side version compare.)"""
         self.sync_shadow()
-        _, layers, _ = self._hip_handles()
-        K.transpose_many([L[k] for L in layers for k in L["wT"]], [L["wT"][k] for L in layers for k in L["wT"]])
-        self._wT_dirty = False
-        return True
 
     # -------------------------------------------------------------- HIP handles
     def _hip_handles(self):
@@ -468,10 +440,6 @@ class DDoSClassifier(nn.Module):
                 L[k] = A.sview(nm) if k.endswith("_w") and not k.startswith("ln") else A.view(nm)
                 sinks[k] = GradSink(A, nm)
             L["sinks"] = sinks
-            if self.transposed_dx:
-                # W^T copies for the backward dX GEMMs (refreshed each training forward)
-                L["wT"] = {k: torch.empty(L[k].shape[1], L[k].shape[0], dtype=torch.bfloat16, device=A.device)
-                           for k in ("qkv_w", "o_w", "l1_w", "l2_w")}
             layers.append(L)
         head = {"w": A.view("classifier.weight"), "b": A.view("classifier.bias"),
                 "sinks": {"w": GradSink(A, "classifier.weight"), "b": GradSink(A, "classifier.bias")}}
@@ -484,19 +452,24 @@ class DDoSClassifier(nn.Module):
         return self._run(input_ids, attention_mask, None, tokens)[1]
 
     def forward_loss(self, input_ids, attention_mask, labels,
-                     tokens: Optional[int] = None, kd=None) -> Tuple[torch.Tensor, torch.Tensor]:
+                     tokens: Optional[int] = None, kd=None,
+                     unit_backward: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
         """(mean CE loss, logits) with the head and the loss fused (one kernel).
 
         tokens: number of real (mask = 1) tokens in the batch, if the caller knows it
         without a device sync -- enables the unpadded HIP path (same math: padding
         positions never reach a real token or the loss).
         kd = (teacher logits [B, 2], temperature, alpha): the loss is the distillation loss
-        (models/bert.py ``kd_loss``), fused into the same head kernel on the HIP path."""
-        return self._run(input_ids, attention_mask, labels, tokens, kd)
+        (models/bert.py ``kd_loss``), fused into the same head kernel on the HIP path.
+        unit_backward: the caller promises ``loss.backward(ops.kernels.unit_grad(device))`` (the
+        training step functions of engine/train.py): the [CLS]-pruned HIP step then runs the head's
+        backward and the last block's output-LayerNorm backward inside the head's forward launch
+        (ops/kernels.py head_ln_bwd; a backward seeded with anything else raises)."""
+        return self._run(input_ids, attention_mask, labels, tokens, kd, unit_backward)
 
-    def _run(self, input_ids, attention_mask, labels, tokens=None, kd=None):
+    def _run(self, input_ids, attention_mask, labels, tokens=None, kd=None, unit_backward=False):
         if self.impl == "hip":
-            return self._run_hip(input_ids, attention_mask, labels, tokens, kd)
+            return self._run_hip(input_ids, attention_mask, labels, tokens, kd, unit_backward)
         loss, logits = self._run_torch(input_ids, attention_mask, labels if kd is None else None)
         if kd is not None and labels is not None:
             from .bert import kd_loss
@@ -508,7 +481,7 @@ class DDoSClassifier(nn.Module):
         q = self.pack_quantum
         return min(B * S, (int(tokens) + q - 1) // q * q)
 
-    def _run_hip(self, ids, mask, labels, tokens=None, kd=None):
+    def _run_hip(self, ids, mask, labels, tokens=None, kd=None, unit_backward=False):
         from ..ops import kernels as K
         from ..ops.functional import EmbeddingFn, HeadFn, LayerFn, RunCtx
         self.sync_shadow()
@@ -531,7 +504,7 @@ class DDoSClassifier(nn.Module):
         rc = RunCtx(B=B, S=S, H=cfg.n_heads, kbias=kbias, seed=self.rng, training=self.training,
                     eps=cfg.layer_norm_eps, p_hidden=cfg.dropout, p_attn=cfg.attention_dropout, p_head=self.dropout.p,
                     on_layer_grads=self.layer_grads_hook if grad else None, group_dw=self.group_dw,
-                    loss_acc=getattr(self, "loss_acc", None))
+                    loss_acc=getattr(self, "loss_acc", None), unit_backward=bool(unit_backward and grad))
         if grad and self.defer_colsum and self.layer_grads_hook is None:
             rc.colsum_jobs = []  # (a per-block hook needs each block's grads final at once)
         if grad and self.defer_dw_reduce and self.layer_grads_hook is None:
@@ -562,10 +535,6 @@ class DDoSClassifier(nn.Module):
             else:
                 K.step_inc(None, self.rng)
         token = self._grad_token if torch.is_grad_enabled() else None
-        if token is not None:
-            # the W^T copies the backward's dX GEMMs read: current unless something other than the
-            # fused Adam epilogue (which rewrites them) changed the weights
-            self.refresh_wT()
         if packed:
             # Unpadded step: only the real tokens (sequence-contiguous, filler rows at the end)
             # are embedded and run through the blocks; varlen attention over cu; positions and

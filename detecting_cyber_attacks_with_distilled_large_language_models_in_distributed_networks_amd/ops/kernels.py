@@ -88,22 +88,20 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu
 
 
 def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] = None,
-              res: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None,
+              res: Optional[torch.Tensor] = None,
               colsum: Optional[tuple] = None, aux_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx = dy w  [* gelu'(u)]  [+ res]  (bf16).
 
-    The product reads the weight ``w`` itself (MN-major B, "NN"), or, with ``wt`` (= w^T,
-    contiguous), a transposed copy (K-major B, "NT").  The two run the same tile configurations
-    (csrc/kernels/gemm.hip pick_cfg) and measured the same, so the model keeps no W^T copies by
-    default (models/distilbert.py transposed_dx).
+    The product reads the weight ``w`` [N_out, N_in] itself as an MN-major B operand ("NN",
+    transposing LDS fragment reads): no W^T copy is kept (a per-step W^T refresh lost its A/B,
+    profiles/r4_ab_dx_layouts.txt).
     colsum = (deferred colsum jobs, out, accumulate): the GEMM epilogue also leaves the column
     sums of dx per M tile (the producer-bias gradient) as a deferred job, instead of a separate
     column-sum pass over dx.  aux_out (with gelu_u): the epilogue also writes gelu(gelu_u) there
     -- the forward's activation, bitwise.  Returns dx."""
     M, N = dy.shape[0], w.shape[1]
     dx = torch.empty(M, N, dtype=torch.bfloat16, device=dy.device)
-    B, bmn = (wt, False) if wt is not None else (w, True)
-    kind = 1 if bmn else 0
+    B, bmn, kind = w, True, 1
     epi = EPI_GELU_BWD if gelu_u is not None else (EPI_ADD if res is not None else EPI_BF16)
     ao = aux_out if gelu_u is not None else None
     if colsum is not None and epi == EPI_BF16:
@@ -171,30 +169,23 @@ DW_BATCH_MAX = 32  # problems per all-layer weight-gradient launch (csrc/kernels
 
 def linear_dw_batch(jobs: list, adam=None, cfg: int = -1):
     """Every weight gradient of a backward in one launch per 32 problems: for each job
-    (dy [K, M], x [K, N], out [M, N] fp32, accumulate[, wT[, bias]]) out (+)= dy^T x, and the
+    (dy [K, M], x [K, N], out [M, N] fp32, accumulate[, bias]) out (+)= dy^T x, and the
     optional fp32 [M] bias (+)= the column sums of dy (``DW_QKV_BIAS``).  No split-K: each
     output tile runs the whole token dimension (deterministic, no slabs, no reduce).
-    adam: a callable (grads, n_with_wT) -> (state, hyper) (``ArenaAdam.fused_args``): apply the
-    optimizer step to each finished gradient tile instead of storing it; a job's optional wT
-    (bf16 [N, M]) is then refreshed by the same epilogue with the updated weights transposed (the
-    next step's dX GEMMs read it: no transpose launch)."""
+    adam: a callable grads -> (state, hyper) (``ArenaAdam.fused_args``): apply the optimizer
+    step to each finished gradient tile instead of storing it."""
     for i in range(0, len(jobs), DW_BATCH_MAX):
         chunk = jobs[i:i + DW_BATCH_MAX]
         outs = [j[2] for j in chunk]
-        wts = [j[4] if len(j) > 4 else None for j in chunk] if adam is not None else []
-        nwt = sum(w is not None for w in wts)
-        st, hp = adam(outs, nwt) if adam is not None else ([], [])
-        empty = None
-        if nwt:
-            empty = torch.empty(0, dtype=torch.bfloat16, device=outs[0].device)
-        bias = [j[5] if len(j) > 5 else None for j in chunk]
+        st, hp = adam(outs) if adam is not None else ([], [])
+        bias = [j[4] if len(j) > 4 else None for j in chunk]
         if any(b is not None for b in bias):
             none = torch.empty(0, dtype=torch.float32, device=outs[0].device)
             bias = [b if b is not None else none for b in bias]
         else:
             bias = []
         ext().gemm_dw_batch([j[0] for j in chunk], [j[1] for j in chunk], outs, [int(j[3]) for j in chunk],
-                            st, hp, cfg, [w if w is not None else empty for w in wts] if nwt else [], bias)
+                            st, hp, cfg, bias)
 
 
 # The qkv bias gradient from the all-layer dW launch itself: the qkv weight gradient's tiles of the
@@ -209,12 +200,6 @@ def dw_flush(jobs: list):
         ext().splitk_reduce_batched([j[0] for j in jobs], [j[1] for j in jobs], [j[2] for j in jobs],
                                     [int(j[3]) for j in jobs])
         jobs.clear()
-
-
-def transpose_many(srcs, dsts):
-    """dsts[i] = srcs[i]^T (bf16, one launch for up to 32 matrices)."""
-    for i in range(0, len(srcs), 32):
-        ext().transpose_batched(list(srcs[i:i + 32]), list(dsts[i:i + 32]))
 
 
 def _colsum_pass(x, out, accumulate, jobs):  # (linear_dx's `colsum` argument shadows colsum())
@@ -397,8 +382,9 @@ LN_XSITES = 128  # csrc/kernels/adam_epi.h FD_LN_XSITES: exchange call sites per
 def ln_xsite(layer: int, which: int, backward: bool) -> int:
     """Exchange call site of a model's LayerNorm-fused launch: forward out_lin / lin2 of block
     ``layer`` -> 2 * layer + which; the backward ones (lin1 dX / qkv dX) 64 + 2 * layer + which.
-    Unique within one forward + backward (the epoch advances once per forward)."""
-    if not 0 <= layer < 32 or which not in (0, 1):
+    Unique within one forward + backward (the epoch advances once per forward).  At most 125:
+    site 127 would let a granule tag wrap to the 0 of a freshly zeroed granule."""
+    if not 0 <= layer < 31 or which not in (0, 1):
         raise ValueError(f"no LayerNorm exchange site for block {layer} / {which}")
     return (64 if backward else 0) + 2 * layer + which
 
@@ -593,17 +579,30 @@ def emb_fwd(ids, word, pos, gamma, beta, S, eps, seed, site, p, row_map=None, ln
     return y, mean, rstd
 
 
+COLSUM_IN_EMB = _os.environ.get("FD_COLSUM_IN_EMB", "1") != "0"
+COLSUM_JOBS_MAX = 32  # deferred column-sum jobs one launch takes (csrc/kernels/norm.hip COLSUM_MAXJ)
+
+
 def emb_bwd(dy, ids, sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos, dgamma, dbeta, S, seed, site, p,
-            accumulate=False, now=None, ever=None, row_map=None, cu=None):
+            accumulate=False, now=None, ever=None, row_map=None, cu=None, colsum_jobs=None):
     """now/ever: optional uint8 [V] row flags -> sparse word gradient (see ArenaAdam).
-    row_map / cu: packed rows (position gradient summed per sequence over cu)."""
+    row_map / cu: packed rows (position gradient summed per sequence over cu).
+    colsum_jobs: the backward's deferred column sums (``colsum_flush``'s list, <= COLSUM_JOBS_MAX):
+    finalised by extra blocks of the embedding tail's first launch (the list is cleared)."""
     T = ids.numel()
     D = gamma.numel()
     dz = workspace(ids.device, "emb_dz", T * D)
     ws = workspace(ids.device, "emb_work", T * D + LN_GRID * 3 * D)  # word pieces, then LN partials
     thr, sc = _drop(p)
+    jobs = colsum_jobs or []
+    if len(jobs) > COLSUM_JOBS_MAX:
+        raise ValueError(f"emb_bwd: {len(jobs)} column-sum jobs (<= {COLSUM_JOBS_MAX})")
     ext().emb_bwd(dy.contiguous(), ids.contiguous(), sorted_ids, perm, word, pos, gamma, mean, rstd, dword, dpos,
-                  dgamma, dbeta, dz, ws, S, seed, site, thr, sc, accumulate, now, ever, row_map, cu)
+                  dgamma, dbeta, dz, ws, S, seed, site, thr, sc, accumulate, now, ever, row_map, cu,
+                  [j[0] for j in jobs], [j[1] for j in jobs], [j[2] for j in jobs], [j[3] for j in jobs],
+                  [j[4] for j in jobs], [int(j[5]) for j in jobs])
+    if colsum_jobs:
+        colsum_jobs.clear()
 
 
 # ------------------------------------------------------------------ head / metrics / optimizer
@@ -636,6 +635,63 @@ def head_bwd(hidden, B, S, W, seed, site, p, dlogits, dW, db, accumulate=False, 
     ext().head_bwd(hidden, B, S, W, seed, site, thr, sc, dlogits.contiguous(), dW, db, dhidden, accumulate, cls,
                    gscale, own)
     return dhidden
+
+
+# The pruned training step's head forward + backward + output-LayerNorm backward as one launch
+# (head_ln_bwd; FD_FUSE_HEAD=0: head_fwd, head_bwd and ln_bwd as three launches)
+FUSE_HEAD = _os.environ.get("FD_FUSE_HEAD", "1") != "0"
+_UNIT_GRAD = {}
+
+
+def unit_grad(device) -> torch.Tensor:
+    """The persistent fp32 scalar 1.0 a training step seeds ``loss.backward`` with (autograd would
+    launch a fill per step).  A forward told ``unit_backward`` (the pruned step's fused head) has
+    already applied the loss gradient for exactly this seed: its backward checks it got this tensor."""
+    key = _dev_key(device)
+    t = _UNIT_GRAD.get(key)
+    if t is None:
+        t = torch.ones((), dtype=torch.float32, device=device)
+        _UNIT_GRAD[key] = t
+    return t
+
+
+def zero_scalar(device, dtype) -> torch.Tensor:
+    """A persistent 0-d zero of ``dtype`` (expanded into a no-op gradient without a fill launch)."""
+    key = (_dev_key(device), dtype)
+    t = _UNIT_GRAD.get(key)
+    if t is None:
+        t = torch.zeros((), dtype=dtype, device=device)
+        _UNIT_GRAD[key] = t
+    return t
+
+
+def head_ln_bwd(hidden, B, W, b, seed, head_site, p_head, labels, dW, db, acc_head, own, z, gamma, mean, rstd, site,
+                p, row_map, dgamma, dbeta, dbias, acc_ln, jobs, kd=None, loss_acc=None):
+    """The [CLS]-pruned training step's head in ONE launch (csrc/kernels/norm.hip
+    head_ln_bwd_kernel), for a loss whose upstream gradient is 1: head forward (logits, loss mean,
+    dlogits), head backward (dW / db (+)= ..., acc_head) and the last block's output-LayerNorm
+    backward from the head gradient (z = its saved pre-LN sum [T, D], head row b = row b < B); the
+    LN's dgamma / dbeta / dbias partials join the deferred column sums ``jobs``.  Bitwise the
+    results of ``head_fwd`` + ``head_bwd`` + ``ln_bwd``.  Returns (logits, loss, dlogits, dz, dx)."""
+    dev = hidden.device
+    T, D = hidden.shape
+    logits = torch.empty(B, 2, dtype=torch.float32, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    dlogits = torch.empty(B, 2, dtype=torch.float32, device=dev)
+    row_loss = workspace(dev, "head_row_loss", B)
+    hthr, hsc = _drop(p_head)
+    thr, sc = _drop(p)
+    t, kT, alpha = kd if kd is not None else (None, 1.0, 1.0)
+    if t is not None:
+        t = t.detach().float().contiguous()
+    dz = torch.empty_like(z)
+    dx = torch.empty_like(z) if thr else None
+    ws = workspace(dev, f"ln_part_job{len(jobs)}", LN_BWD_PARTS * 3 * D)
+    nblk = ext().head_ln_bwd(hidden, B, W, b, seed, head_site, hthr, hsc, labels, logits, loss, dlogits, row_loss,
+                             loss_acc, dW, db, acc_head, own, t, float(kT), float(alpha), z, gamma, mean, rstd, dz,
+                             dx, ws, site, thr, sc, row_map if thr else None)
+    jobs.append((ws, [dgamma, dbeta, dbias], nblk, 3 * D, D, acc_ln))
+    return logits, loss, dlogits, dz, (dx if dx is not None else dz)
 
 
 def eval_metrics(logits, labels, acc, counts, prob1=None, preds=None):

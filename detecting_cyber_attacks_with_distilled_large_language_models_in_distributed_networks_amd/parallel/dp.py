@@ -270,7 +270,7 @@ def make_dp_step_fn(model, optimizer, sync: GradSync, teacher=None, temperature:
         optimizer.step()
         return scaled.detach()
 
-    step.prepare = getattr(model, "refresh_wT", None)
+    step.prepare = getattr(model, "prepare_replay", None)
     return step
 
 

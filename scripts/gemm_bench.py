@@ -23,11 +23,8 @@ for (N, Kd, name) in [(2304, 768, "qkv"), (768, 768, "o"), (3072, 768, "ffn1"), 
     t_ours = timeit(lambda: K.linear_fwd(x, w, b, gelu=(name == "ffn1")))
     t_ref = timeit(lambda: torch.nn.functional.linear(x, w))
     dy = rnd(T, N)
-    wt = w.t().contiguous()  # the model's dX runs NT on a transposed weight copy
-    t_nn = timeit(lambda: K.linear_dx(dy, w, wt=wt))
+    t_nn = timeit(lambda: K.linear_dx(dy, w))  # NN: W read MN-major (transposing LDS reads), no W^T copy
     t_nn_ref = timeit(lambda: dy @ w)
-    t_nn_w = timeit(lambda: K.linear_dx(dy, w))  # NN: W read MN-major (transposing LDS reads), no W^T copy
-    print(f"{name:5s} dX NT-on-W^T {t_nn:7.1f}us vs NN-on-W {t_nn_w:7.1f}us", flush=True)
     out = torch.empty(N, Kd, device="cuda")
     t_tn = timeit(lambda: K.linear_dw(dy, x, out))
     t_tn_ref = timeit(lambda: dy.t() @ x)

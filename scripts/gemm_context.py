@@ -43,7 +43,7 @@ nop = lambda: None  # noqa: E731
 ffn1 = lambda: K.linear_fwd(x, w1, b1, gelu=True)  # noqa: E731
 fl = lambda: flush.fill_(1)  # noqa: E731
 ffn2 = lambda: K.linear_fwd(gg, w2, b2)  # noqa: E731
-l1dx = lambda: K.linear_dx(gg, w2t, res=dz, wt=w2)  # noqa: E731  (dh = du W1 + dz: K=3072, N=768)
+l1dx = lambda: K.linear_dx(gg, w2t, res=dz)  # noqa: E731  (dh = du W1 + dz: K=3072, N=768)
 for name, fn in (("ffn2 fwd", ffn2), ("l1 dX+res", l1dx)):
     a = timed(nop, fn)
     b = timed(ffn1, fn)

@@ -66,7 +66,7 @@ def main():
 
     def xs():
         site[0] += 1
-        if site[0] >= kn.LN_XSITES:
+        if site[0] >= kn.LN_XSITES - 1:  # (site LN_XSITES - 1 is never a valid call site)
             kn.ln_epoch_advance(dev)
             site[0] = 0
         return site[0]
@@ -81,12 +81,14 @@ def main():
             report(f"ln fwd K={K}", nb_ln, True)
         for K in (3072, 2304):
             a, wt = bf(M, K, scale=0.5), bf(D, K, scale=0.03)
+            w_mn = wt.t().contiguous()  # W [K][N]: the model's dX GEMMs read the weight MN-major
             dz, dx = torch.empty_like(y), torch.empty_like(y)
-            for _ in range(20):
-                ext().gemm_ln(True, a, wt, dz, None, res, gamma, None, mean, rstd, z, dx, cp, stats, cnt, err, 0.0,
-                              seed, 9, thr, sc, None, -1, xs())
-            torch.cuda.synchronize()
-            report(f"ln bwd K={K}", nb_ln, True)
+            for b_mn, B, tag in ((True, w_mn, "NN"), (False, wt, "NT")):
+                for _ in range(20):
+                    ext().gemm_ln(True, a, B, dz, None, res, gamma, None, mean, rstd, z, dx, cp, stats, cnt, err, 0.0,
+                                  seed, 9, thr, sc, None, -1, xs(), b_mn)
+                torch.cuda.synchronize()
+                report(f"ln bwd {tag} K={K}", nb_ln, True)
         for (N, K, epi, nm) in ((768, 768, 0, "o dX"), (2304, 768, 1, "qkv fwd"), (3072, 768, 2, "ffn1 fwd")):
             x, w, b = bf(M, K), bf(N, K, scale=0.03), torch.zeros(N, device=dev)
             out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)

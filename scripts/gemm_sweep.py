@@ -64,14 +64,14 @@ for name, N, Kd in [("qkv", 2304, 768), ("o", 768, 768), ("ffn1", 3072, 768), ("
         u = rnd(T, Kd)
         uu = u.float().requires_grad_(True)
         ref = torch.autograd.grad(torch.nn.functional.gelu(uu), uu, dy.float() @ w.float())[0]
-        cases.append((f"{name}.dX NT+gelu'", 0, T * N * Kd,
-                      lambda dy=dy, w=w, u=u, wt=wt: K.linear_dx(dy, w, gelu_u=u, wt=wt), ref))
+        cases.append((f"{name}.dX NN+gelu'", 1, T * N * Kd,
+                      lambda dy=dy, w=w, u=u: K.linear_dx(dy, w, gelu_u=u), ref))
     elif name in ("ffn1", "qkv"):
-        cases.append((f"{name}.dX NT+add", 0, T * N * Kd,
-                      lambda dy=dy, w=w, r=res, wt=wt: K.linear_dx(dy, w, res=r, wt=wt),
+        cases.append((f"{name}.dX NN+add", 1, T * N * Kd,
+                      lambda dy=dy, w=w, r=res: K.linear_dx(dy, w, res=r),
                       dy.float() @ w.float() + res.float()))
     else:
-        cases.append((f"{name}.dX NT", 0, T * N * Kd, lambda dy=dy, w=w, wt=wt: K.linear_dx(dy, w, wt=wt),
+        cases.append((f"{name}.dX NN", 1, T * N * Kd, lambda dy=dy, w=w: K.linear_dx(dy, w),
                       dy.float() @ w.float()))
     W[name] = W[name] + (dy,)
 for a, b_ in (("ffn2", "ffn1"), ("o", "qkv")):

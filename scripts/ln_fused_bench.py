@@ -68,7 +68,7 @@ def main():
         a, wt = bf(M, K, scale=0.5), bf(D, K, scale=0.03)
         dg, db, dbi = (torch.empty(D, device=dev) for _ in range(3))
         dz, dx = torch.empty_like(y), torch.empty_like(y)
-        t_ref = timed(lambda: kn.ln_bwd(kn.linear_dx(a, wt.t(), res=res, wt=wt), z, None, gamma, mean, rstd, dg, db,
+        t_ref = timed(lambda: kn.ln_bwd(kn.linear_dx(a, wt.t().contiguous(), res=res), z, None, gamma, mean, rstd, dg, db,
                                         dbi, seed, 9, 0.1, zin=True, jobs=[]))
         line = f"bwd K={K:5d}  gemm+ln {t_ref:7.1f} us"
         for c in cfgs:

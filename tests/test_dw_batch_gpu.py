@@ -39,11 +39,11 @@ def test_dw_batch_kernel_matches_fp32(cfg):
         if i % 2 == 1:
             bias = torch.randn(M, device="cuda", generator=g) if acc else torch.full((M,), float("nan"), device="cuda")
             brefs.append((bias, dy.float().sum(0) + (bias.clone() if acc else 0.0)))
-        jobs.append((dy, x, out, acc, None, bias))
+        jobs.append((dy, x, out, acc, bias))
         refs.append(ref)
     K.linear_dw_batch(jobs, cfg=cfg)
     torch.cuda.synchronize()
-    for (_, _, out, _, _, _), ref in zip(jobs, refs):
+    for (_, _, out, _, _), ref in zip(jobs, refs):
         assert _frel(out, ref) < 1e-5, _frel(out, ref)
     for bias, bref in brefs:
         assert _frel(bias, bref) < 1e-5, _frel(bias, bref)
@@ -109,10 +109,12 @@ def test_fused_adam_in_batched_dw_matches_unfused(graph):
         assert all(st.graph is not None and st.failed is None for st in steps)
 
 
-def test_batched_qkv_bias_partials_bitwise():
+def test_batched_qkv_bias_partials_bitwise(monkeypatch):
     """The per-block qkv-bias column-sum partials computed in one launch at the end of the
     backward (model.batch_colsum, ops/kernels.py colsum_partials_batched) give bitwise the
-    gradients of one partial launch per block -- including an accumulating second backward."""
+    gradients of one partial launch per block -- including an accumulating second backward.
+    (Only reachable with the dW launch's own qkv-bias sums off: K.DW_QKV_BIAS=False.)"""
+    monkeypatch.setattr(K, "DW_QKV_BIAS", False)
     cfg = DistilBertConfig(n_layers=3)
     grads = []
     for batched in (True, False):
@@ -129,6 +131,36 @@ def test_batched_qkv_bias_partials_bitwise():
         torch.cuda.synchronize()
         grads.append(m.arena.grad.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+def test_dw_launch_qkv_bias_matches_column_sum_pass(monkeypatch):
+    """The qkv bias gradient summed by the all-layer dW launch's qkv tiles (K.DW_QKV_BIAS, the
+    default) against the separate column-sum pass over dqkv: the same fp32 column sums (up to
+    summation order), every other gradient bitwise, for a fresh and an accumulating backward."""
+    cfg = DistilBertConfig(n_layers=3)
+    grads = []
+    for fused in (True, False):
+        monkeypatch.setattr(K, "DW_QKV_BIAS", fused)
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=31)
+        m.train()
+        ids, mask, labels, tokens = _batch(32, 128, seed=710)
+        per = []
+        for acc_step in range(2):
+            if acc_step == 0:
+                m.zero_grad()
+            m.rng.fill_(acc_step)
+            loss, _ = m.forward_loss(ids, mask, labels, tokens=tokens)
+            loss.backward()
+            torch.cuda.synchronize()
+            per.append({k: m.arena.gview(k).clone() for k in m.arena.offsets})
+        grads.append(per)
+    for a, b in zip(*grads):  # after the first and after the accumulating second backward
+        for k in a:
+            if ".attention." in k and k.endswith("_lin.bias") and "out_lin" not in k:
+                err = ((a[k] - b[k]).norm() / b[k].norm().clamp_min(1e-30)).item()
+                assert err < 1e-5, (k, err)
+            else:
+                assert torch.equal(a[k], b[k]), k
 
 
 def test_colsum_partials_batched_kernel():

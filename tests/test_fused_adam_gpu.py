@@ -48,10 +48,6 @@ def test_fused_adam_training_matches_unfused(graph, nosplit):
     models, opts, steps = [], [], []
     for fuse in (True, False):
         m = DDoSClassifier(config=cfg, device=DEV, impl="hip", seed=13)
-        m.batch_dw = False  # per-layer grouped dW launches (batched: test_dw_batch_gpu.py)
-        # (Adam fused into a per-layer dW launch updates weights mid-backward: the later dX GEMMs
-        # must read W^T copies taken before the step)
-        m.transposed_dx = True
         m.train()
         opt = ArenaAdam(m, lr=1e-3, fuse_dw=fuse)
         assert opt.can_fuse() == fuse
@@ -87,8 +83,8 @@ def test_fused_adam_touches_only_encoder_matrices():
     seen = []
     orig = opt.fused_args
 
-    def spy(grads, n_wT=0):
-        out = orig(grads, n_wT)
+    def spy(grads):
+        out = orig(grads)
         seen.extend(opt._done[-len(grads):])
         return out
     opt.fused_args = spy
@@ -227,50 +223,31 @@ def test_adam_rows_matches_flagged_dense_adam():
     assert torch.equal(a[0][untouched], base[0][untouched])
 
 
-def _wT_equal_shadow_T(m) -> bool:
-    _, layers, _ = m._hip_handles()
-    torch.cuda.synchronize()
-    return all(torch.equal(L["wT"][k], L[k].t().contiguous()) for L in layers for k in L["wT"])
-
-
-def test_wT_written_by_fused_adam_epilogue(monkeypatch):
-    """Round 4 (A/B path, FD_TRANSPOSED_DX=1): the fused Adam epilogue of the all-layer weight-gradient launch also writes the
-    updated weights' bf16 transpose (the W^T the next backward's dX GEMMs read), so the per-step
-    transpose launch is gone.  W^T stays bitwise shadow^T after fused steps and graph replays, and
-    every out-of-band weight change (FedAvg, checkpoint load, an unfused optimizer step) re-runs
-    the transpose exactly once."""
-    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.parallel.fedavg import (
-        fedavg_)
-    m = DDoSClassifier(config=DistilBertConfig(n_layers=2), device=DEV, impl="hip", seed=3)
-    m.transposed_dx = True  # (FD_TRANSPOSED_DX=1: the dX GEMMs read W^T copies; default: W itself)
-    m.train()
-    opt = ArenaAdam(m, lr=1e-3)
-    fn = make_step_fn(m, opt)
-    calls = []
-    real = K.transpose_many
-    monkeypatch.setattr(K, "transpose_many", lambda s, d: (calls.append(len(s)), real(s, d)))
+def test_graph_replay_after_load_state_dict_uses_loaded_weights():
+    """A captured training step holds no shadow sync of its own: ``GraphedTrainStep`` brings the
+    bf16 shadow up to date before each replay (``DDoSClassifier.prepare_replay``).  A graphed model
+    and an eager twin take the same steps, both load the same modified checkpoint, and the next
+    step (a replay on one, eager on the other) must give the same loss and the same weights --
+    a replay that read the pre-load shadow would not."""
+    arms = []
+    for graph in (True, False):
+        m = DDoSClassifier(config=DistilBertConfig(n_layers=2), device=DEV, impl="hip", seed=3)
+        m.train()
+        opt = ArenaAdam(m, lr=1e-3)
+        arms.append((m, GraphedTrainStep(make_step_fn(m, opt), warmup=1, enabled=graph, bucket=m.packed_rows)))
     ids, mask, labels, tokens = _batch(32, 128, seed=1)
-    fn(ids, mask, labels, tokens)                       # first step: W^T taken once
-    assert len(calls) == 1 and _wT_equal_shadow_T(m)
-    for _ in range(2):
-        fn(ids, mask, labels, tokens)                   # fused steps keep it current
-    assert len(calls) == 1 and _wT_equal_shadow_T(m)
-    step = GraphedTrainStep(fn, warmup=1, bucket=m.packed_rows)
-    for _ in range(4):
-        step(ids, mask, labels, tokens)                 # eager, capture, replays: no transpose
-    assert len(calls) == 1 and _wT_equal_shadow_T(m)
-    fedavg_(m)                                          # out-of-band write -> one re-transpose
-    assert m.wT_stale()
-    step(ids, mask, labels, tokens)                     # (before the replay, GraphedTrainStep.prepare)
-    assert len(calls) == 2 and _wT_equal_shadow_T(m)
-    sd = {k: v.clone() for k, v in m.state_dict().items()}
-    sd["distilbert.transformer.layer.1.ffn.lin2.weight"] += 0.01
-    m.load_state_dict(sd)                               # checkpoint load -> one re-transpose
-    fn(ids, mask, labels, tokens)
-    assert len(calls) == 3 and _wT_equal_shadow_T(m)
-    opt2 = ArenaAdam(m, lr=1e-3, fuse_dw=False)         # unfused optimizer: W^T re-derived each step
-    fn2 = make_step_fn(m, opt2)
-    fn2(ids, mask, labels, tokens)                     # (W^T still current from the fused step)
-    fn2(ids, mask, labels, tokens)                     # the unfused step left it stale
-    assert len(calls) == 4
-    assert m.refresh_wT() and len(calls) == 5 and _wT_equal_shadow_T(m)
+    for _ in range(3):  # graphed arm: eager, capture, replay
+        losses = [float(st(ids, mask, labels, tokens)) for _, st in arms]
+        assert losses[0] == losses[1]
+    assert arms[0][1].graph is not None
+    sd = {k: v.clone() for k, v in arms[0][0].state_dict().items()}
+    sd["distilbert.transformer.layer.1.ffn.lin2.weight"].mul_(-3.0)
+    sd["distilbert.transformer.layer.0.attention.q_lin.weight"].add_(0.05)
+    for m, _ in arms:
+        m.load_state_dict(sd)
+    losses = [float(st(ids, mask, labels, tokens)) for _, st in arms]
+    torch.cuda.synchronize()
+    assert losses[0] == losses[1]
+    a, b = arms[0][0].arena, arms[1][0].arena
+    assert torch.equal(a.master, b.master) and torch.equal(a.shadow, b.shadow)
+    assert torch.equal(a.shadow, a.master.to(torch.bfloat16))

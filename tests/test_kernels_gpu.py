@@ -86,11 +86,11 @@ def test_gemm_forced_configs(cfg):
             assert rel_err(u, ref + b) < 1e-2
             assert rel_err(g, torch.nn.functional.gelu((ref + b).float())) < 2e-2
             res = bf(M, N, seed=33)
-            wt = w.t().contiguous()  # linear_dx on a transposed copy = the NT kernel
-            assert rel_err(kn.linear_dx(x, wt, res=res, wt=w), ref + res.float()) < 1e-2
+            wt = w.t().contiguous()  # dx = x W^T: the NN dX kernel on W^T [K, N]
+            assert rel_err(kn.linear_dx(x, wt, res=res), ref + res.float()) < 1e-2
             uu = bf(M, N, seed=34).float().requires_grad_(True)
             gref = torch.autograd.grad(torch.nn.functional.gelu(uu), uu, ref)[0]
-            assert rel_err(kn.linear_dx(x, wt, gelu_u=uu.detach().to(torch.bfloat16), wt=w), gref) < 1e-2
+            assert rel_err(kn.linear_dx(x, wt, gelu_u=uu.detach().to(torch.bfloat16)), gref) < 1e-2
     finally:
         ext().gemm_set_cfg(0, -1, -1)
 
@@ -443,30 +443,6 @@ def test_sparse_word_grad_and_adam_skip():
     assert torch.equal(pd_, ps_) and torch.equal(md, ms) and torch.equal(vd, vs)
 
 
-def test_transpose_batched():
-    srcs = [bf(2304, 768, seed=40), bf(768, 768, seed=41), bf(3072, 768, seed=42), bf(768, 3072, seed=43),
-            bf(64, 128, seed=44)]
-    dsts = [torch.empty(s.shape[1], s.shape[0], dtype=torch.bfloat16, device=DEV) for s in srcs]
-    kn.transpose_many(srcs, dsts)
-    for s, d in zip(srcs, dsts):
-        assert torch.equal(d, s.t())
-
-
-@pytest.mark.parametrize("M,N,K", [(4096, 768, 3072), (4000, 3072, 768), (512, 768, 2304)])
-def test_linear_dx_transposed_weight(M, N, K):
-    # dx = dy W through the NT kernel on W^T, with every dX epilogue, == the NN kernel
-    dy, w = bf(M, K, seed=45), bf(K, N, scale=0.05, seed=46)
-    wt = w.t().contiguous()
-    u, res = bf(M, N, seed=47), bf(M, N, seed=48)
-    ref = dy.float() @ w.float()
-    assert rel_err(kn.linear_dx(dy, w, wt=wt), ref) < 1e-2
-    assert rel_err(kn.linear_dx(dy, w, res=res, wt=wt), ref + res.float()) < 1e-2
-    uu = u.float().requires_grad_(True)
-    g = torch.autograd.grad(torch.nn.functional.gelu(uu), uu, ref)[0]
-    assert rel_err(kn.linear_dx(dy, w, gelu_u=u, wt=wt), g) < 1e-2
-    assert torch.equal(kn.linear_dx(dy, w, res=res, wt=wt), kn.linear_dx(dy, w, res=res, wt=wt))
-
-
 @pytest.mark.parametrize("T", [4096, 1000, 37])
 def test_rank_sort_matches_stable_sort(T):
     g = torch.Generator().manual_seed(T)
@@ -479,15 +455,15 @@ def test_rank_sort_matches_stable_sort(T):
 
 @pytest.mark.parametrize("M,N,K,epi", [(2688, 3072, 768, 3), (2700, 768, 3072, 4), (300, 3072, 768, 3)])
 def test_gemm_epilogue_column_sums(M, N, K, epi):
-    """NT dX GEMM with GELU' / residual epilogue + per-tile column sums of its bf16 output."""
-    dy, wt = bf(M, K, seed=31), bf(N, K, seed=32)
+    """NN dX GEMM (dx = dy W, W read MN-major) with GELU' / residual epilogue + per-tile column
+    sums of its bf16 output."""
+    dy, w = bf(M, K, seed=31), bf(K, N, seed=32)
     aux = bf(M, N, seed=33)
-    ref_dx = kn.linear_dx(dy, wt.t().contiguous(), gelu_u=aux if epi == 3 else None,
-                          res=aux if epi == 4 else None, wt=wt)
+    ref_dx = kn.linear_dx(dy, w, gelu_u=aux if epi == 3 else None, res=aux if epi == 4 else None)
     dx = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     tiles = (M + 127) // 128
     part = torch.full((tiles * N,), float("nan"), device=DEV)
-    nblk = kn.ext().gemm_colsum(epi, dy, wt, dx, aux if epi == 3 else None, aux if epi == 4 else None, part)
+    nblk = kn.ext().gemm_colsum(epi, dy, w, dx, aux if epi == 3 else None, aux if epi == 4 else None, part, None, 1)
     torch.cuda.synchronize()
     assert nblk == tiles
     assert torch.equal(dx, ref_dx)
@@ -530,20 +506,16 @@ def test_head_bwd_packed_rows_and_zeroing():
 @pytest.mark.parametrize("M,N,K", [(2688, 3072, 768), (4000, 3072, 768), (256, 3072, 768)])
 def test_gelu_bwd_rematerialises_activation(M, N, K):
     # The GELU' dX epilogue's aux_out re-creates the forward activation gelu(u) bitwise
-    # (forward: EPI_BIAS_GELU on x W1^T + b), on every dX path: NT, NT + fused column sums, NN.
+    # (forward: EPI_BIAS_GELU on x W1^T + b), on both dX paths: NN, NN + fused column sums.
     x, w1, b1 = bf(M, K, seed=60), bf(N, K, scale=0.05, seed=61), bf(N, seed=62).float()
     g, u = kn.linear_fwd(x, w1, b1, gelu=True)
     dy, w2 = bf(M, 768, seed=63), bf(768, N, scale=0.05, seed=64)
-    wt = w2.t().contiguous()
-    base = kn.linear_dx(dy, w2, gelu_u=u, wt=wt)
-    for kw in ({"wt": wt}, {}):
-        out = torch.full_like(u, float("nan"))
-        du = kn.linear_dx(dy, w2, gelu_u=u, aux_out=out, **kw)
-        assert torch.equal(out, g)
-        if kw:
-            assert torch.equal(du, base)
+    base = kn.linear_dx(dy, w2, gelu_u=u)
+    out = torch.full_like(u, float("nan"))
+    du = kn.linear_dx(dy, w2, gelu_u=u, aux_out=out)
+    assert torch.equal(out, g) and torch.equal(du, base)
     jobs = []
     bgrad = torch.zeros(N, device=DEV)
     out = torch.full_like(u, float("nan"))
-    du = kn.linear_dx(dy, w2, gelu_u=u, wt=wt, colsum=(jobs, bgrad, False), aux_out=out)
+    du = kn.linear_dx(dy, w2, gelu_u=u, colsum=(jobs, bgrad, False), aux_out=out)
     assert torch.equal(out, g) and torch.equal(du, base)

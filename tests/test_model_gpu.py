@@ -365,21 +365,3 @@ def test_eval_graphs_survive_interleaved_training():
         assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("packed", [False, True])
-def test_dx_on_weight_equals_dx_on_transposed_copy(packed):
-    """The backward's dX GEMMs read the weight W itself (MN-major B, the default) or a W^T copy
-    (FD_TRANSPOSED_DX=1): same tile configurations, same fp32 sums -> identical gradients, for the
-    full model (LayerNorm-fused dX, GELU' + bias column sums, pruned last block, split-K)."""
-    ids, mask, labels = _batch(B=16, S=128, seed=7)
-    tok = int(mask.sum()) if packed else None
-    grads = []
-    for wt in (True, False):
-        model = DDoSClassifier(config=DistilBertConfig(n_layers=3), device="cuda", impl="hip", seed=4)
-        model.transposed_dx = wt
-        model.train()
-        model.zero_grad()
-        loss, _ = model.forward_loss(ids, mask, labels, tokens=tok)
-        loss.backward()
-        torch.cuda.synchronize()
-        grads.append(model.arena.grad.clone())
-    assert torch.equal(grads[0], grads[1])

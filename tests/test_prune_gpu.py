@@ -151,3 +151,61 @@ def test_attention_q_live_matches_full_and_ignores_garbage():
         torch.cuda.synchronize()
         assert torch.isfinite(d_q.float()).all()
         assert _frel(d_q, d_full) < 1e-2
+
+
+@pytest.mark.parametrize("packed,B,empty,kd", [(True, 32, None, False), (True, 20, 3, False), (False, 16, None, False),
+                                               (True, 32, None, True)])
+def test_fused_head_ln_backward_bitwise(packed, B, empty, kd, monkeypatch):
+    """The pruned training step's head forward + backward + the last block's output-LayerNorm
+    backward as ONE launch (ops/kernels.py head_ln_bwd, forward_loss(unit_backward=True)) against
+    the three launches it replaces (FD_FUSE_HEAD=0): loss, logits and every gradient bitwise equal,
+    including an accumulating second backward, an empty sequence and the distillation loss."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+    cfg = DistilBertConfig(n_layers=3)
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setattr(K, "FUSE_HEAD", fused)
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=41)
+        m.train()
+        ids, mask, labels, tokens = _batch(B, 128, seed=810, empty=empty)
+        t = None
+        if kd:
+            g = torch.Generator(device="cuda").manual_seed(3)
+            t = (torch.randn(B, 2, device="cuda", generator=g), 2.0, 0.9)
+        m.zero_grad()
+        res = []
+        for it in range(2):  # the second backward accumulates
+            m.rng.fill_(5 + it)
+            calls = []
+            real = K.head_ln_bwd
+            monkeypatch.setattr(K, "head_ln_bwd", lambda *a, **k: (calls.append(1), real(*a, **k))[1])
+            loss, logits = m.forward_loss(ids, mask, labels, tokens=tokens if packed else None, kd=t,
+                                          unit_backward=True)
+            loss.backward(K.unit_grad("cuda"))
+            monkeypatch.setattr(K, "head_ln_bwd", real)
+            assert len(calls) == (1 if fused else 0)
+            torch.cuda.synchronize()
+            res.append((loss.detach().clone(), logits.detach().clone()))
+        outs.append((res, m.arena.grad.clone(), {k: m.dense_grad(k).clone() for k in m.state_dict()}))
+    (r0, g0, d0), (r1, g1, d1) = outs
+    for (l0, z0), (l1, z1) in zip(r0, r1):
+        assert torch.equal(z0, z1) and l0.item() == l1.item()
+    for k in d1:
+        assert torch.equal(d0[k], d1[k]), k
+
+
+def test_fused_head_rejects_a_foreign_backward_seed():
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+    if not K.FUSE_HEAD:
+        pytest.skip("FD_FUSE_HEAD=0")
+    m = DDoSClassifier(config=DistilBertConfig(n_layers=2), device="cuda", impl="hip", seed=42)
+    m.train()
+    ids, mask, labels, tokens = _batch(16, 128, seed=811)
+    loss, _ = m.forward_loss(ids, mask, labels, tokens=tokens, unit_backward=True)
+    with pytest.raises(RuntimeError, match="unit_grad"):
+        loss.backward(torch.ones((), device="cuda"))
+    # without the promise the usual three launches run and any seed works
+    loss, _ = m.forward_loss(ids, mask, labels, tokens=tokens)
+    (loss * 2.0).backward()
+    torch.cuda.synchronize()
+    assert torch.isfinite(m.arena.grad).all()

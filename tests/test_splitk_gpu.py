@@ -64,8 +64,7 @@ def test_splitk_dispatch_covers_linear_wrappers():
     uu = bf(M, N, seed=7)
     jobs, out = [], torch.zeros(N, device=DEV)
     g_out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    du = K.linear_dx(bf(M, D, seed=8), wt2, gelu_u=uu, wt=wt2.t().contiguous(), colsum=(jobs, out, False),
-                     aux_out=g_out)
+    du = K.linear_dx(bf(M, D, seed=8), wt2, gelu_u=uu, colsum=(jobs, out, False), aux_out=g_out)
     K.colsum_flush(jobs)
     torch.cuda.synchronize()
     a8 = bf(M, D, seed=8).float()
@@ -77,7 +76,7 @@ def test_splitk_dispatch_covers_linear_wrappers():
     assert rel(out, du.float().sum(0)) < 1e-5  # sums of the stored bf16 values
     # residual epilogue
     res = bf(M, D, seed=9)
-    dx = K.linear_dx(dy, wt2.t(), res=res, wt=wt2)
+    dx = K.linear_dx(dy, wt2.t().contiguous(), res=res)
     assert rel(dx, dy.float() @ wt2.float().t() + res.float()) < 5e-3
 
 
