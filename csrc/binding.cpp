@@ -40,7 +40,7 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
                 const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st);
 int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K);
 int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg,
-                     hipStream_t st);
+                     const FdAdamRest* rest, hipStream_t st);
 int fd_gemm_ln_set_diag(int diag);
 int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, float* workspace,
                    long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
@@ -323,9 +323,13 @@ int64_t gemm_dw2(const at::Tensor& A0, const at::Tensor& B0, const at::Tensor& C
 void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tensor>& Bs,
                    const std::vector<at::Tensor>& Cs, const std::vector<int64_t>& accumulate,
                    const std::vector<at::Tensor>& adam, const std::vector<double>& hp, int64_t cfg,
-                   const std::vector<at::Tensor>& biases = {}) {
+                   const std::vector<at::Tensor>& biases = {}, const std::vector<at::Tensor>& rest = {},
+                   const std::vector<int64_t>& rest_i = {}) {
   // biases: empty, or per problem an fp32 [M] producer-bias gradient (+)= column sums of A (an
   // empty tensor: none), accumulated like the problem's gradient
+  // rest (with adam): the rest of the optimizer step in the same launch (FdAdamRest) -- [master,
+  // grad, m, v, shadow] arenas, the run table (int64 [nruns][3]) and optionally the word table's
+  // [ever, now] flags; rest_i = [n4 of the run table, word offset, word rows, word row length]
   const size_t n = As.size();
   TORCH_CHECK(n > 0 && n <= 32, "gemm_dw_batch: 1..32 problems, got ", n);
   TORCH_CHECK(Bs.size() == n && Cs.size() == n && accumulate.size() == n, "gemm_dw_batch: ragged problem lists");
@@ -373,7 +377,41 @@ void gemm_dw_batch(const std::vector<at::Tensor>& As, const std::vector<at::Tens
     hyper[0] = ad[0].lr; hyper[1] = ad[0].b1; hyper[2] = ad[0].b2; hyper[3] = ad[0].eps; hyper[4] = ad[0].wd;
     hyper[5] = (float)ad[0].decoupled;
   }
-  check_rc(fd_gemm_dw_batch((int)n, pr.data(), (int)K, step, adam.empty() ? nullptr : hyper, (int)cfg, stream()),
+  FdAdamRest rs{};
+  if (!rest.empty()) {
+    TORCH_CHECK(!adam.empty(), "gemm_dw_batch: the rest of the optimizer step needs the fused Adam");
+    TORCH_CHECK((rest.size() == 6 || rest.size() == 8) && rest_i.size() == 4, "gemm_dw_batch: rest = 6 or 8 tensors, 4 ints");
+    for (int k = 0; k < 4; ++k) need(rest[k], at::kFloat, "rest arena");
+    need(rest[4], at::kBFloat16, "rest shadow");
+    need(rest[5], at::kLong, "rest runs");
+    const int64_t numel = rest[0].numel();
+    for (int k = 1; k < 5; ++k) TORCH_CHECK(rest[k].numel() == numel, "gemm_dw_batch: rest arenas differ in size");
+    TORCH_CHECK(rest[5].dim() == 2 && rest[5].size(1) == 3, "gemm_dw_batch: run table [n][3]");
+    const int64_t n4 = rest_i[0], woff = rest_i[1], wrows = rest_i[2], wlen = rest_i[3];
+    TORCH_CHECK(n4 >= 0 && n4 * 4 <= numel, "gemm_dw_batch: run table total out of range");
+    rs.p = rest[0].data_ptr<float>(); rs.g = rest[1].data_ptr<float>(); rs.m = rest[2].data_ptr<float>();
+    rs.v = rest[3].data_ptr<float>(); rs.sh = reinterpret_cast<uint16_t*>(rest[4].data_ptr());
+    rs.runs = rest[5].size(0) ? reinterpret_cast<const long long*>(rest[5].data_ptr()) : nullptr;
+    rs.nruns = (int)rest[5].size(0);
+    rs.n4 = n4;
+    if (rest.size() == 8) {
+      need(rest[6], at::kByte, "rest ever");
+      need(rest[7], at::kByte, "rest now");
+      TORCH_CHECK(wlen > 0 && wlen % 4 == 0 && woff % 4 == 0 && woff >= 0 && woff + wrows * wlen <= numel &&
+                      rest[6].numel() == wrows && rest[7].numel() == wrows,
+                  "gemm_dw_batch: word table out of range");
+      rs.ever = rest[6].data_ptr<unsigned char>(); rs.now = rest[7].data_ptr<unsigned char>();
+      rs.woff = woff; rs.wrows = (int)wrows; rs.wrow4 = (int)(wlen / 4);
+    }
+    for (size_t i = 0; i < biases.size(); ++i)
+      if (pr[i].bias) {
+        const float* gb = rs.g;
+        TORCH_CHECK(pr[i].bias >= gb && pr[i].bias + As[i].size(1) <= gb + numel,
+                    "gemm_dw_batch: an in-launch bias Adam needs the bias gradient inside the grad arena");
+      }
+  }
+  check_rc(fd_gemm_dw_batch((int)n, pr.data(), (int)K, step, adam.empty() ? nullptr : hyper, (int)cfg,
+                            rest.empty() ? nullptr : &rs, stream()),
            "gemm_dw_batch");
 }
 
@@ -1329,7 +1367,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("cfg") = -1, py::arg("xsite") = 0, py::arg("b_mn") = false);
   m.def("gemm_dw_batch", &gemm_dw_batch, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("accumulate"),
         py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1,
-        py::arg("biases") = std::vector<at::Tensor>{});
+        py::arg("biases") = std::vector<at::Tensor>{}, py::arg("rest") = std::vector<at::Tensor>{},
+        py::arg("rest_i") = std::vector<int64_t>{});
   m.def("gemm_colsum", &gemm_colsum, py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("aux"),
         py::arg("res"), py::arg("colsum"), py::arg("aux_out") = py::none(), py::arg("kind") = 0);
   m.def("splitk_reduce_batched", &splitk_reduce_batched);

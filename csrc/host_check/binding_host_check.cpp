@@ -100,8 +100,18 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
   return 0;
 }
 int fd_gemm_dw2_splits(int, int, int, int, int) { return 1; }
-int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg, hipStream_t) {
+int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg,
+                     const FdAdamRest* rest, hipStream_t) {
   ++hc::calls;
+  if (rest) {
+    if (!hyper || !step) hc::violations.push_back("dw_batch rest without the fused Adam");
+    if (rest->runs) hc::span(rest->runs, (long long)rest->nruns * 3 * 8, "dw_batch rest runs");
+    if (rest->ever) {
+      hc::span(rest->ever, rest->wrows, "dw_batch rest ever");
+      hc::span(rest->now, rest->wrows, "dw_batch rest now");
+      hc::span(rest->p + rest->woff, (long long)rest->wrows * rest->wrow4 * 16, "dw_batch rest word rows");
+    }
+  }
   if (n <= 0 || n > 32) hc::violations.push_back("dw_batch: problem count");
   for (int i = 0; i < n; ++i) {
     const FdDwProb& q = probs[i];

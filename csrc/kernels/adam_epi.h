@@ -38,6 +38,30 @@ struct FdDwProb {
   float* bias;
 };
 
+// The rest of the optimizer step, run by extra blocks of the all-layer dW launch beside its last
+// tiles (gemm.hip dwb_rest) instead of two launches of its own after it: every parameter the fused
+// epilogues do not update.  p / g / m / v / sh are the whole arenas; runs: the run table over them
+// ([start4, count4, prefix4] rows, head_optim.hip AdamArgs) of everything but the word table, n4
+// its float4 total; the word table ([wrows][wrow4 float4] at element woff) by its row flags
+// (ever: has Adam state, now: has a gradient this step; weight decay 0).  The qkv bias, whose
+// gradient the launch itself sums, is updated by the tiles that sum it (GemmParams::acol_*).
+struct FdAdamRest {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  uint16_t* sh;
+  const long long* runs;
+  long long n4;
+  int nruns;
+  int wrows, wrow4;
+  long long woff;
+  const unsigned char* ever;
+  const unsigned char* now;
+  int flat_blocks, row_blocks;  // filled by the launcher
+  int first;                    // the rest blocks lead the grid (else they follow the tiles)
+};
+
 #define FD_LN_XSITES 128
 
 // LayerNorm fused into an N = hidden GEMM (gemm.hip gemm_ln_kernel).  The column tiles of one

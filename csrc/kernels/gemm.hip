@@ -36,6 +36,8 @@
 
 namespace {
 
+#include "adam_common.h"
+
 enum Epi : int {
   EPI_BF16 = 0,       // C(bf16) = acc
   EPI_BIAS = 1,       // C(bf16) = acc + bias[n]
@@ -80,6 +82,12 @@ struct GemmParams {
   // EPI_F32, nullable: acol[m] (+= when accumulate) = sum over the K range of A[k][m], written by
   // the tiles with tn == 0 (FdDwProb::bias)
   float* acol;
+  // with the fused Adam (adam.p) and these set: the finished acol[m] is not stored -- Adam (adam_elem,
+  // hyper-parameters of `adam`) updates the bias's master / moments / bf16 shadow at that element
+  float* acol_p;
+  float* acol_m;
+  float* acol_v;
+  uint16_t* acol_sh;
 };
 
 constexpr int BKT = 64;
@@ -252,24 +260,15 @@ DEV void st_nt4(float* p, float4 v) {
   __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
 }
 
-// Adam on 4 consecutive elements of a finished gradient tile: the same arithmetic, in the
-// same order, as adam_kernel (head_optim.hip), so a fused step matches the unfused one.
+// Adam on 4 consecutive elements of a finished gradient tile: adam_elem (adam_common.h), as in
+// adam_kernel (head_optim.hip), so a fused step matches the unfused one bitwise.
 DEV float4 adam_epi4(const FdAdamEpi& a, size_t i, float4 g4, float step_size, float inv_sqrt_bc2) {
   const float4 p4 = ld_nt4(a.p + i), m4 = ld_nt4(a.m + i), v4 = ld_nt4(a.v + i);
   float pp[4] = {p4.x, p4.y, p4.z, p4.w}, gg[4] = {g4.x, g4.y, g4.z, g4.w};
   float mm[4] = {m4.x, m4.y, m4.z, m4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float gr = gg[e];
-    if (a.wd != 0.f) {
-      if (a.decoupled) pp[e] *= 1.f - a.lr * a.wd;
-      else gr += a.wd * pp[e];
-    }
-    mm[e] = a.b1 * mm[e] + (1.f - a.b1) * gr;
-    vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gr * gr;
-    const float denom = sqrtf(vv[e]) * inv_sqrt_bc2 + a.eps;
-    pp[e] -= step_size * mm[e] / denom;
-  }
+  for (int e = 0; e < 4; ++e)
+    adam_elem(a.lr, a.b1, a.b2, a.eps, a.wd, a.decoupled, pp[e], gg[e], mm[e], vv[e], step_size, inv_sqrt_bc2);
   st_nt4(a.p + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
   st_nt4(a.m + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
   st_nt4(a.v + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
@@ -1067,7 +1066,21 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
         s += __shfl_xor(s, 16, 64);
         s += __shfl_xor(s, 32, 64);
         const int m = m0 + wr * TM + i * 16 + lane;
-        if (lane < 16 && m < p.M) p.acol[m] = p.accumulate ? p.acol[m] + s : s;
+        if (lane < 16 && m < p.M) {
+          if (p.acol_p) {  // the bias's Adam step (fused epilogues never accumulate)
+            float ss, inv;
+            adam_bias_corr(p.adam.step, p.adam.lr, p.adam.b1, p.adam.b2, ss, inv);
+            float pb = p.acol_p[m], mb = p.acol_m[m], vb = p.acol_v[m];
+            adam_elem(p.adam.lr, p.adam.b1, p.adam.b2, p.adam.eps, p.adam.wd, p.adam.decoupled, pb, s, mb, vb, ss,
+                      inv);
+            p.acol_p[m] = pb;
+            p.acol_m[m] = mb;
+            p.acol_v[m] = vb;
+            if (p.acol_sh) p.acol_sh[m] = (uint16_t)f2bf(pb);
+          } else {
+            p.acol[m] = p.accumulate ? p.acol[m] + s : s;
+          }
+        }
       }
     }
   }
@@ -1177,6 +1190,7 @@ struct DwBatch {
   const int* step;
   float lr, b1, b2, eps, wd;
   int decoupled;
+  FdAdamRest rest;  // rest.p != nullptr: blocks [ntiles, ntiles + rest blocks) finish the optimizer step
 };
 
 // One tile of the batch: logical tile id lid -> (problem, tile) -> K loop + epilogue.
@@ -1200,8 +1214,43 @@ DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
     p.adam.p = q.p; p.adam.m = q.m; p.adam.v = q.v; p.adam.sh = q.sh; p.adam.step = bt.step;
     p.adam.lr = bt.lr; p.adam.b1 = bt.b1; p.adam.b2 = bt.b2; p.adam.eps = bt.eps; p.adam.wd = bt.wd;
     p.adam.decoupled = bt.decoupled;
+    if (q.bias && bt.rest.p) {  // the qkv bias's state lies at its gradient's arena offset
+      const ptrdiff_t off = q.bias - bt.rest.g;
+      p.acol_p = bt.rest.p + off; p.acol_m = bt.rest.m + off; p.acol_v = bt.rest.v + off;
+      p.acol_sh = bt.rest.sh ? bt.rest.sh + off : nullptr;
+    }
   }
   gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S, BK>(p, lid - q.tile0, smem);
+}
+
+// Blocks past the tiles: the rest of the optimizer step (FdAdamRest), dispatched after every tile,
+// i.e. on the CUs the launch's last, partial round of tiles leaves idle.  The first flat_blocks
+// walk the run table (adam_kernel<true, true>'s element body), the others take 64-row flag chunks
+// of the word table per wave (adam_rows_kernel's row body) -- the same arithmetic, bitwise.
+template <int NT>
+DEV void dwb_rest(const DwBatch& bt, int rb) {
+  const FdAdamRest& r = bt.rest;
+  float ss, inv;
+  adam_bias_corr(bt.step, bt.lr, bt.b1, bt.b2, ss, inv);
+  AdamArgs a{};
+  a.step = bt.step; a.lr = bt.lr; a.b1 = bt.b1; a.b2 = bt.b2; a.eps = bt.eps;
+  if (rb < r.flat_blocks) {
+    a.p = r.p; a.g = r.g; a.m = r.m; a.v = r.v; a.shadow = reinterpret_cast<bf16_t*>(r.sh);
+    a.wd = bt.wd; a.decoupled = bt.decoupled;
+    a.runs = r.runs; a.nruns = r.nruns; a.n4 = r.n4;
+    for (long long vi = (long long)rb * NT + threadIdx.x; vi < r.n4; vi += (long long)r.flat_blocks * NT)
+      adam_flat4<true, true>(a, vi, ss, inv);
+    return;
+  }
+  if (!r.ever) return;
+  a.p = r.p + r.woff; a.g = r.g + r.woff; a.m = r.m + r.woff; a.v = r.v + r.woff;
+  a.shadow = r.sh ? reinterpret_cast<bf16_t*>(r.sh) + r.woff : nullptr;
+  a.wd = 0.f; a.decoupled = 0;
+  a.touched = r.ever; a.now = r.now;
+  const int lane = threadIdx.x & 63;
+  const int nwaves = r.row_blocks * (NT / 64);
+  for (int r0 = ((rb - r.flat_blocks) * (NT / 64) + (int)(threadIdx.x >> 6)) * 16; r0 < r.wrows; r0 += nwaves * 16)
+    adam_rows16(a, r0, r.wrows, r.wrow4, lane, ss, inv);
 }
 
 template <int BM, int BN, int WM, int WN, int S, int BK = BKT>
@@ -1209,7 +1258,22 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch 
   using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S, BK>;
   static_assert(G::SMEM <= LDS_MAX, "LDS");
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
-  dwb_tile<BM, BN, WM, WN, S, BK>(bt, xcd_remap(blockIdx.x, bt.ntiles), smem);
+  // the rest blocks lead the grid (their HBM stream beside the first round's K loops, while the
+  // memory is otherwise idle) or follow the tiles (on the CUs the last, partial round leaves idle);
+  // a leading group is a multiple of 8 blocks, so every tile keeps its XCD under xcd_remap
+  const int nrest = bt.rest.flat_blocks + bt.rest.row_blocks;
+  int bid = blockIdx.x;
+  if (bt.rest.first) {
+    if (bid < nrest) {  // block-uniform
+      dwb_rest<64 * WM * WN>(bt, bid);
+      return;
+    }
+    bid -= nrest;
+  } else if (bid >= bt.ntiles) {
+    dwb_rest<64 * WM * WN>(bt, bid - bt.ntiles);
+    return;
+  }
+  dwb_tile<BM, BN, WM, WN, S, BK>(bt, xcd_remap(bid, bt.ntiles), smem);
 }
 
 // out[i] = (accumulate ? out[i] : 0) + sum_z slab[z][i]   (deterministic split-K reduce)
@@ -1681,7 +1745,7 @@ bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
       t += (bt.pr[i].M / bm) * (bt.pr[i].N / bn);
     }
     bt.ntiles = t;
-    if (!dry) hipLaunchKernelGGL(kern, dim3(t), dim3(threads), 0, st, bt);
+    if (!dry) hipLaunchKernelGGL(kern, dim3(t + bt.rest.flat_blocks + bt.rest.row_blocks), dim3(threads), 0, st, bt);
     return true;
   };
   switch (id) {
@@ -1693,9 +1757,26 @@ bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
 }
 
 int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const float* hyper, int cfg,
-                     hipStream_t st) {
+                     const FdAdamRest* rest, hipStream_t st) {
   if (n <= 0 || n > DWB_MAXP || K <= 0 || K % BKT) return 1;
   DwBatch bt{};
+  if (rest && rest->p) {
+    if (!hyper || !step || !rest->g || !rest->m || !rest->v || (rest->nruns > 0) != (rest->runs != nullptr) ||
+        rest->n4 < 0 || (rest->ever && (rest->wrows <= 0 || rest->wrow4 <= 0 || rest->woff % 4)))
+      return 7;
+    bt.rest = *rest;
+    // ~4 float4 per thread of the run table; one 64-row flag chunk per wave of the word table
+    bt.rest.flat_blocks = rest->n4 > 0 ? (int)std::min<long long>(128, (rest->n4 + 2047) / 2048) : 0;
+    bt.rest.row_blocks = rest->ever ? std::min(128, (rest->wrows + 127) / 128) : 0;
+    // (FD_DW_REST_FIRST=0: after the tiles; leading measured 1.6395 / 1.6434 vs 1.6452 / 1.6436 ms/step,
+    // profiles/r5_ab_adam_in_dw.txt)
+    static const int first = [] { const char* e = getenv("FD_DW_REST_FIRST"); return e ? atoi(e) : 1; }();
+    bt.rest.first = first;
+    if (first) {  // (a multiple of 8 blocks in all)
+      const int pad = (8 - (bt.rest.flat_blocks + bt.rest.row_blocks) % 8) % 8;
+      bt.rest.row_blocks += pad;
+    }
+  }
   bt.n = n;
   bt.K = K;
   static const int diag = [] { const char* e = getenv("FD_GEMM_DIAG"); return e ? atoi(e) : 0; }();

@@ -170,133 +170,14 @@ __global__ __launch_bounds__(256) void eval_metrics_kernel(const float* logits, 
   }
 }
 
-struct AdamArgs {
-  float* p;
-  const float* g;
-  float* m;
-  float* v;
-  bf16_t* shadow;
-  long long n4;
-  const int* step;
-  float lr, b1, b2, eps, wd;
-  int decoupled;
-  long long skip_off4, skip_end4;  // float4 range whose rows may be skipped
-  int row4;                         // float4s per row in that range
-  const unsigned char* touched;     // sticky row flags: nonzero Adam state (nullable)
-  const unsigned char* now;         // rows with a valid gradient this step (nullable = all)
-  // Disjoint float4 runs of the arena to update ([start4, count4, first virtual index] each,
-  // ascending), nullable = all of [0, n4).  Used when the weight-gradient GEMMs already
-  // applied Adam to the encoder matrices in their epilogues: one launch covers the rest.
-  const long long* runs;
-  int nruns;
-};
-
-// virtual index -> arena float4 index through the run table (binary search on the prefix)
-DEV long long run_index(const long long* runs, int nruns, long long i) {
-  int lo = 0, hi = nruns - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (runs[3 * mid + 2] <= i) lo = mid;
-    else hi = mid - 1;
-  }
-  return runs[3 * lo] + (i - runs[3 * lo + 2]);
-}
-
-// NT: the moments (and the gradient) are touched once per step -> stream them with
-// nontemporal loads/stores so they do not evict the weights / bf16 shadow the next
-// forward re-reads from L2 / MALL.
-DEV float4 ld_nt(const float4* p) {
-  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-  return make_float4(v[0], v[1], v[2], v[3]);
-}
-DEV void st_nt(float4* p, float4 v) {
-  __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
-}
-
-// The Adam update of 4 elements -- ONE copy of the arithmetic for every Adam kernel, so the
-// dense launch and the row-flag launch round identically (bitwise equal results).
-DEV void adam_math4(const AdamArgs& a, float (&pp)[4], const float (&gg)[4], float (&mm)[4], float (&vv)[4],
-                    float step_size, float inv_sqrt_bc2) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float gr = gg[e];
-    if (a.wd != 0.f) {
-      if (a.decoupled) pp[e] *= 1.f - a.lr * a.wd;
-      else gr += a.wd * pp[e];
-    }
-    mm[e] = a.b1 * mm[e] + (1.f - a.b1) * gr;
-    vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gr * gr;
-    const float denom = sqrtf(vv[e]) * inv_sqrt_bc2 + a.eps;
-    pp[e] -= step_size * mm[e] / denom;
-  }
-}
-
-// One flagged row of a [rows][row4] float4 table starting at float4 base4 (one wave; gradient 0
-// unless now[row]).
-DEV void adam_row(const AdamArgs& a, long long base4, int row, int row4, int lane, float step_size,
-                  float inv_sqrt_bc2) {
-  const bool gvalid = a.now == nullptr || a.now[row] != 0;
-  for (int c = lane; c < row4; c += 64) {
-    const long long i = base4 + (long long)row * row4 + c;
-    const float4 p = ld_nt(reinterpret_cast<const float4*>(a.p) + i);
-    const float4 g = gvalid ? ld_nt(reinterpret_cast<const float4*>(a.g) + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 m = ld_nt(reinterpret_cast<const float4*>(a.m) + i);
-    const float4 v = ld_nt(reinterpret_cast<const float4*>(a.v) + i);
-    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
-    float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
-    adam_math4(a, pp, gg, mm, vv, step_size, inv_sqrt_bc2);
-    st_nt(reinterpret_cast<float4*>(a.p) + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
-    st_nt(reinterpret_cast<float4*>(a.m) + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
-    st_nt(reinterpret_cast<float4*>(a.v) + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
-    if (a.shadow) reinterpret_cast<uint2*>(a.shadow)[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
-  }
-}
+#include "adam_common.h"
 
 template <bool NT, bool NTP = false>
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
-  const int t = a.step[0];
-  const float bc1 = 1.f - powf(a.b1, (float)t);
-  const float bc2 = 1.f - powf(a.b2, (float)t);
-  const float step_size = a.lr / bc1;
-  const float inv_sqrt_bc2 = 1.f / sqrtf(bc2);
-  for (long long vi = blockIdx.x * 256ll + threadIdx.x; vi < a.n4; vi += (long long)gridDim.x * 256) {
-    const long long i = a.runs ? run_index(a.runs, a.nruns, vi) : vi;
-    // Rows never touched since the moments were reset have m = v = g = 0: their
-    // Adam update is exactly zero, so skip all their traffic (wd == 0 only).
-    bool gvalid = true;
-    if (a.touched && i >= a.skip_off4 && i < a.skip_end4) {
-      const long long row = (i - a.skip_off4) / a.row4;
-      if (!a.touched[row]) continue;
-      gvalid = a.now == nullptr || a.now[row] != 0;
-    }
-    float4 p = NTP ? ld_nt(reinterpret_cast<const float4*>(a.p) + i) : reinterpret_cast<float4*>(a.p)[i];
-    float4 g, m, v;
-    if constexpr (NT) {
-      g = gvalid ? ld_nt(reinterpret_cast<const float4*>(a.g) + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      m = ld_nt(reinterpret_cast<const float4*>(a.m) + i);
-      v = ld_nt(reinterpret_cast<const float4*>(a.v) + i);
-    } else {
-      g = gvalid ? reinterpret_cast<const float4*>(a.g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-      m = reinterpret_cast<float4*>(a.m)[i];
-      v = reinterpret_cast<float4*>(a.v)[i];
-    }
-    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
-    float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
-    adam_math4(a, pp, gg, mm, vv, step_size, inv_sqrt_bc2);
-    if constexpr (NTP)
-      st_nt(reinterpret_cast<float4*>(a.p) + i, make_float4(pp[0], pp[1], pp[2], pp[3]));
-    else
-      reinterpret_cast<float4*>(a.p)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-    if constexpr (NT) {
-      st_nt(reinterpret_cast<float4*>(a.m) + i, make_float4(mm[0], mm[1], mm[2], mm[3]));
-      st_nt(reinterpret_cast<float4*>(a.v) + i, make_float4(vv[0], vv[1], vv[2], vv[3]));
-    } else {
-      reinterpret_cast<float4*>(a.m)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
-      reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-    }
-    if (a.shadow)
-      reinterpret_cast<uint2*>(a.shadow)[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
-  }
+  float step_size, inv_sqrt_bc2;
+  adam_bias_corr(a.step, a.lr, a.b1, a.b2, step_size, inv_sqrt_bc2);
+  for (long long vi = blockIdx.x * 256ll + threadIdx.x; vi < a.n4; vi += (long long)gridDim.x * 256)
+    adam_flat4<NT, NTP>(a, vi, step_size, inv_sqrt_bc2);
 }
 
 // Adam over the rows of a table that have state (ever[row] != 0; weight decay 0): one wave per
@@ -308,10 +189,10 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
 __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a, int rows, int row4) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows || !a.touched[row]) return;  // wave-uniform
-  const int t = a.step[0];
-  const float bc1 = 1.f - powf(a.b1, (float)t);
-  const float bc2 = 1.f - powf(a.b2, (float)t);
-  adam_row(a, 0, row, row4, lane, a.lr / bc1, 1.f / sqrtf(bc2));
+  float step_size, inv_sqrt_bc2;
+  adam_bias_corr(a.step, a.lr, a.b1, a.b2, step_size, inv_sqrt_bc2);
+  if (row4 == 192) adam_row768(a, row, lane, step_size, inv_sqrt_bc2);
+  else adam_row(a, 0, row, row4, lane, step_size, inv_sqrt_bc2);
 }
 
 __global__ void step_kernel(int* step, uint32_t* seed) {

@@ -181,11 +181,94 @@ class ArenaAdam:
         self.step_t.zero_()
         self.host_step = 0
         self._done, self._begun = [], False
+        self._rest_in_launch = False
         if getattr(self.model, "emb_ever", None) is not None:
             self.model.emb_ever.zero_()
 
     def zero_grad(self, set_to_none: bool = False):
         self.model.zero_grad()
+
+    def mark_done(self, grads):
+        """Arena gradient views that a launch other than ``step()`` updates this step (the qkv
+        biases, updated by the all-layer weight-gradient tiles that sum their gradient)."""
+        self._begin()
+        A = self.arena
+        base = A.grad.data_ptr()
+        for g in grads:
+            off = (g.data_ptr() - base) // A.grad.element_size()
+            if not (0 <= off and off + g.numel() <= A.numel) or not g.is_contiguous():
+                raise ValueError("mark_done: not a contiguous arena gradient view")
+            self._done.append((off, g.numel()))
+
+    def _sparse_words(self) -> bool:
+        # Only the HIP path leaves a sparse word gradient (and sets the emb_now / emb_ever row
+        # flags, in its embedding backward): the torch path's autograd writes the dense table
+        # and sets no flag, so the row-flag Adam would skip every word row there.  (Round 3's
+        # "HIP learns faster than fp32" loss-curve bias was exactly that: the fp32 reference
+        # arm on the GPU never updated its word embeddings -- results/numerics_r4/.)
+        hip_sparse = getattr(self.model, "impl", None) == "hip" and getattr(self.model, "sparse_word_grad", False)
+        sparse = (hip_sparse and self.weight_decay == 0.0
+                  and getattr(self.model, "emb_ever", None) is not None)
+        if hip_sparse and not sparse and getattr(self.model, "emb_now", None) is not None:
+            raise RuntimeError("sparse word-embedding grads need weight_decay == 0 "
+                               "(set model.sparse_word_grad = False for AdamW)")
+        return sparse
+
+    def _rest_runs(self, sparse: bool):
+        """(runs, rest): every element span not updated yet this step, and -- with the sparse word
+        table -- the same minus that table (which the row-flag Adam takes)."""
+        A = self.arena
+        done = sorted(self._done)
+        pos, runs = 0, []
+        for off, n in done:
+            if off > pos:
+                runs.append((pos, off - pos))
+            pos = max(pos, off + n)
+        if pos < A.numel:
+            runs.append((pos, A.numel - pos))
+        if not sparse:
+            return runs, None
+        woff, rows, rl = self.model.word_embedding_span()
+        wend = woff + rows * rl
+        rest = []
+        for off, n in runs:
+            a, b = off, off + n
+            if b <= woff or a >= wend:
+                rest.append((a, n))
+                continue
+            if not (a <= woff and wend <= b):
+                raise RuntimeError("the word-embedding table must lie inside one Adam run")
+            if woff > a:
+                rest.append((a, woff - a))
+            if b > wend:
+                rest.append((wend, b - wend))
+        return runs, rest
+
+    def rest_args(self):
+        """The rest of this step's update for the all-layer weight-gradient launch to run beside its
+        last tiles (csrc/kernels/gemm.hip dwb_rest; FD_ADAM_IN_DW=0: ``step()`` launches it):
+        (tensors, ints) for ``gemm_dw_batch(rest=, rest_i=)``, or None when it cannot (no cached
+        run table during a capture, a dense word table, ...).  Call after every other span of the
+        step is marked done; ``step()`` then only finishes the bookkeeping."""
+        from ..ops import kernels as K
+        A = self.arena
+        if not (K.ADAM_IN_DW and A.master.is_cuda and self._side is None and A.shadow is not None):
+            return None
+        self._begin()
+        sparse = self._sparse_words()
+        if not sparse:
+            return None
+        _, rest = self._rest_runs(True)
+        if not rest:
+            return None
+        table = self._runs_table(rest)
+        if table is None:
+            return None
+        woff, rows, rl = self.model.word_embedding_span()
+        tab, total4, _ = table
+        self._rest_in_launch = True
+        return ([A.master, A.grad, self.m, self.v, A.shadow, tab, self.model.emb_ever, self.model.emb_now],
+                [total4, woff, rows, rl])
 
     @torch.no_grad()
     def step(self):
@@ -195,26 +278,18 @@ class ArenaAdam:
         b1, b2 = self.betas
         if A.master.is_cuda:
             self._begin()
-            # Only the HIP path leaves a sparse word gradient (and sets the emb_now / emb_ever row
-            # flags, in its embedding backward): the torch path's autograd writes the dense table
-            # and sets no flag, so the row-flag Adam would skip every word row there.  (Round 3's
-            # "HIP learns faster than fp32" loss-curve bias was exactly that: the fp32 reference
-            # arm on the GPU never updated its word embeddings -- results/numerics_r4/.)
-            hip_sparse = getattr(self.model, "impl", None) == "hip" and getattr(self.model, "sparse_word_grad", False)
-            sparse = (hip_sparse and self.weight_decay == 0.0
-                      and getattr(self.model, "emb_ever", None) is not None)
-            if hip_sparse and not sparse and getattr(self.model, "emb_now", None) is not None:
-                raise RuntimeError("sparse word-embedding grads need weight_decay == 0 "
-                                   "(set model.sparse_word_grad = False for AdamW)")
+            if getattr(self, "_rest_in_launch", False):
+                # the all-layer weight-gradient launch already ran the rest (rest_args)
+                self._rest_in_launch = False
+                if self._side is not None:
+                    torch.cuda.current_stream(A.device).wait_stream(self._side)
+                self.model.mark_shadow_synced()
+                self._done = []
+                self._begun = False
+                return
+            sparse = self._sparse_words()
             # everything not already updated by the per-block hook, in contiguous runs
-            done = sorted(self._done)
-            pos, runs = 0, []
-            for off, n in done:
-                if off > pos:
-                    runs.append((pos, off - pos))
-                pos = max(pos, off + n)
-            if pos < A.numel:
-                runs.append((pos, A.numel - pos))
+            runs, rest = self._rest_runs(sparse)
             woff = self.model.word_embedding_span()[0] if sparse else -1
             table = self._runs_table(runs) if len(runs) > 1 else None
             if table is not None and sparse:
@@ -223,18 +298,6 @@ class ArenaAdam:
                 from ..ops import kernels as K
                 _, rows, rl = self.model.word_embedding_span()
                 wend = woff + rows * rl
-                rest = []
-                for off, n in runs:
-                    a, b = off, off + n
-                    if b <= woff or a >= wend:
-                        rest.append((a, n))
-                        continue
-                    if not (a <= woff and wend <= b):
-                        raise RuntimeError("the word-embedding table must lie inside one Adam run")
-                    if woff > a:
-                        rest.append((a, woff - a))
-                    if b > wend:
-                        rest.append((wend, b - wend))
                 sl = slice(woff, wend)
                 K.adam_rows(A.master[sl], A.grad[sl], self.m[sl], self.v[sl], A.shadow[sl], self.step_t, self.lr, b1,
                             b2, self.eps, self.model.emb_ever, self.model.emb_now, rl)

@@ -150,7 +150,8 @@ class EmbeddingFn(torch.autograd.Function):
         if rc.dw_batch:
             fa = rc.fused_adam
             acc_any = any(j[3] for j in rc.dw_batch)
-            K.linear_dw_batch(rc.dw_batch, adam=fa.fused_args if fa is not None and not acc_any else None)
+            fused = fa is not None and not acc_any
+            K.linear_dw_batch(rc.dw_batch, adam=fa.fused_args if fused else None, opt=fa if fused else None)
             rc.dw_batch.clear()
 
     @staticmethod

@@ -167,25 +167,44 @@ def linear_dw2(dy0: torch.Tensor, x0: torch.Tensor, out0: torch.Tensor, dy1: tor
 DW_BATCH_MAX = 32  # problems per all-layer weight-gradient launch (csrc/kernels/gemm.hip DWB_MAXP)
 
 
-def linear_dw_batch(jobs: list, adam=None, cfg: int = -1):
+# The rest of the optimizer step (biases, LayerNorms, embeddings, head, the flagged word rows) run
+# by extra blocks of the all-layer dW launch, on the CUs its last round of tiles leaves idle,
+# instead of two launches after it; the qkv bias by the tiles that sum its gradient
+# (engine/optim.py ArenaAdam.rest_args; FD_ADAM_IN_DW=0: step() launches it).
+ADAM_IN_DW = _os.environ.get("FD_ADAM_IN_DW", "1") != "0"
+
+
+def linear_dw_batch(jobs: list, adam=None, cfg: int = -1, opt=None):
     """Every weight gradient of a backward in one launch per 32 problems: for each job
     (dy [K, M], x [K, N], out [M, N] fp32, accumulate[, bias]) out (+)= dy^T x, and the
     optional fp32 [M] bias (+)= the column sums of dy (``DW_QKV_BIAS``).  No split-K: each
     output tile runs the whole token dimension (deterministic, no slabs, no reduce).
     adam: a callable grads -> (state, hyper) (``ArenaAdam.fused_args``): apply the optimizer
-    step to each finished gradient tile instead of storing it."""
-    for i in range(0, len(jobs), DW_BATCH_MAX):
+    step to each finished gradient tile instead of storing it.  opt (with adam): the optimizer
+    (``ArenaAdam``) -- the last launch also runs the rest of its step (``ADAM_IN_DW``)."""
+    starts = list(range(0, len(jobs), DW_BATCH_MAX))
+    for i in starts:
         chunk = jobs[i:i + DW_BATCH_MAX]
         outs = [j[2] for j in chunk]
         st, hp = adam(outs) if adam is not None else ([], [])
         bias = [j[4] if len(j) > 4 else None for j in chunk]
+        rest = None
+        if adam is not None and opt is not None and ADAM_IN_DW and i == starts[-1]:
+            # the qkv biases summed by this launch are updated by its tiles when it also finishes
+            # the step: mark them, then hand the rest of the step to the launch
+            sums = [b for b in bias if b is not None]
+            done0 = len(opt._done)
+            opt.mark_done(sums)
+            rest = opt.rest_args()
+            if rest is None:
+                del opt._done[done0:]  # (step() updates them after all)
         if any(b is not None for b in bias):
             none = torch.empty(0, dtype=torch.float32, device=outs[0].device)
             bias = [b if b is not None else none for b in bias]
         else:
             bias = []
         ext().gemm_dw_batch([j[0] for j in chunk], [j[1] for j in chunk], outs, [int(j[3]) for j in chunk],
-                            st, hp, cfg, bias)
+                            st, hp, cfg, bias, *(rest if rest is not None else ([], [])))
 
 
 # The qkv bias gradient from the all-layer dW launch itself: the qkv weight gradient's tiles of the

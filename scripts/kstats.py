@@ -4,8 +4,9 @@ path = sys.argv[1]
 rows = list(csv.DictReader(open(path)))
 arg = sys.argv[2] if len(sys.argv) > 2 else "1"
 if arg == "auto":
-    # the single-launch Adam kernel runs once per training step
-    steps = float(next(r['Calls'] for r in rows if 'adam_kernel' in r['Name']))
+    # the all-layer weight-gradient launch runs once per training step (so did the Adam launch,
+    # which now runs inside it)
+    steps = float(next(r['Calls'] for r in rows if 'gemm_dw_batch_kernel' in r['Name'] or 'adam_kernel' in r['Name']))
 else:
     steps = float(arg)
 tot = sum(float(r['TotalDurationNs']) for r in rows)

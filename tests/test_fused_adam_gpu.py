@@ -251,3 +251,30 @@ def test_graph_replay_after_load_state_dict_uses_loaded_weights():
     a, b = arms[0][0].arena, arms[1][0].arena
     assert torch.equal(a.master, b.master) and torch.equal(a.shadow, b.shadow)
     assert torch.equal(a.shadow, a.master.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_rest_of_step_in_dw_launch_bitwise(graph, monkeypatch):
+    """The rest of the optimizer step (biases, LayerNorms, embeddings, head, flagged word rows)
+    run by extra blocks of the all-layer dW launch and the qkv bias by its summing tiles
+    (ops/kernels.py ADAM_IN_DW) == the separate adam_rows + run-table launches after it: masters,
+    moments and the bf16 shadow bitwise equal after graph-replayed steps."""
+    states = []
+    for in_dw in (True, False):
+        monkeypatch.setattr(K, "ADAM_IN_DW", in_dw)
+        m = DDoSClassifier(config=DistilBertConfig(n_layers=2), device=DEV, impl="hip", seed=17)
+        m.train()
+        opt = ArenaAdam(m, lr=1e-3)
+        calls = []
+        real = K.adam
+        monkeypatch.setattr(K, "adam", lambda *a, **k: (calls.append(1), real(*a, **k))[1])
+        step = GraphedTrainStep(make_step_fn(m, opt), warmup=1, enabled=graph, bucket=m.packed_rows)
+        for it in range(4):
+            ids, mask, labels, tokens = _batch(32, 128, seed=40 + it)
+            step(ids, mask, labels, tokens)
+        torch.cuda.synchronize()
+        monkeypatch.setattr(K, "adam", real)
+        assert (len(calls) == 0) == in_dw  # (eager launches only: replays bypass Python)
+        states.append((m.arena.master.clone(), opt.m.clone(), opt.v.clone(), m.arena.shadow.clone()))
+    for x, y in zip(*states):
+        assert torch.equal(x, y)
