@@ -64,7 +64,8 @@ int fd_comm_broadcast(void* comm, void* buf, long long count, int dtype, int roo
 int fd_comm_allgather(void* comm, const void* send, void* recv, long long count, int dtype, hipStream_t st);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                int rows, uint64_t* dmask, int q_live, hipStream_t st);
+                int rows, uint64_t* dmask, int q_live, void* cxc, void* xc, const void* xres, int Bp,
+                hipStream_t st);
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx,
                 float* delta, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float drop_scale, const int* cu, int rows, const uint64_t* dmask, int q_live,
@@ -791,9 +792,22 @@ void check_dmask(const c10::optional<at::Tensor>& dmask, int64_t B, int64_t S, i
 
 void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
               int64_t B, int64_t S, int64_t H, const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
-              const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask, int64_t q_live = 0) {
+              const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask, int64_t q_live = 0,
+              const c10::optional<at::Tensor>& cxc = c10::nullopt, const c10::optional<at::Tensor>& xc = c10::nullopt,
+              const c10::optional<at::Tensor>& xres = c10::nullopt) {
   need(qkv, at::kBFloat16, "qkv");
   TORCH_CHECK(q_live >= 0, "attention: q_live >= 0");
+  const bool compact = cxc.has_value() && cxc->defined();
+  int64_t Bp = 0;
+  if (compact) {  // [CLS] rows of ctx and of the residual stream, compacted to [Bp, D]
+    TORCH_CHECK(q_live == 1 && xc.has_value() && xres.has_value(), "attention: compact rows need q_live 1, xc, xres");
+    need(*cxc, at::kBFloat16, "cxc");
+    need(*xc, at::kBFloat16, "xc");
+    need(*xres, at::kBFloat16, "xres");
+    Bp = cxc->numel() / (H * 64);
+    TORCH_CHECK(Bp >= B && cxc->numel() == Bp * H * 64 && xc->numel() == cxc->numel(), "attention: cxc/xc size");
+    TORCH_CHECK(xres->numel() == ctx.numel(), "attention: xres size");
+  }
   need(kbias, at::kFloat, "kbias");
   need(ctx, at::kBFloat16, "ctx");
   need(lse, at::kFloat, "lse");
@@ -806,7 +820,8 @@ void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
   check_cu(cu, B, rows, ctx.numel() / (H * 64));
   check_rc(fd_attn_fwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(), (int)B,
                        (int)S, (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu),
-                       (int)rows, ptr<uint64_t>(dmask), (int)q_live, stream()),
+                       (int)rows, ptr<uint64_t>(dmask), (int)q_live, compact ? cxc->data_ptr() : nullptr,
+                       compact ? xc->data_ptr() : nullptr, compact ? xres->data_ptr() : nullptr, (int)Bp, stream()),
            "attn_fwd");
 }
 
@@ -1392,7 +1407,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_allgather", &comm_allgather);
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("B"),
         py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"),
-        py::arg("dmask"), py::arg("q_live") = 0);
+        py::arg("dmask"), py::arg("q_live") = 0, py::arg("cxc") = py::none(), py::arg("xc") = py::none(),
+        py::arg("xres") = py::none());
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("dctx"),
         py::arg("delta"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"),
         py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("q_live") = 0);

@@ -240,9 +240,13 @@ int fd_comm_allreduce(void*, const void*, void*, long long, int, int, hipStream_
 int fd_comm_broadcast(void*, void*, long long, int, int, hipStream_t) { return 0; }
 int fd_comm_allgather(void*, const void*, void*, long long, int, hipStream_t) { return 0; }
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H, const uint32_t* seed,
-                uint32_t, uint32_t, float, const int* cu, int rows, uint64_t* dmask, int, hipStream_t) {
+                uint32_t, uint32_t, float, const int* cu, int rows, uint64_t* dmask, int, void* cxc, void* xc,
+                const void* xres, int Bp, hipStream_t) {
   ++hc::calls;
   const long long D = (long long)H * 64;
+  hc::opt_span(cxc, (long long)Bp * D * 2, "attn cxc");
+  hc::opt_span(xc, (long long)Bp * D * 2, "attn xc");
+  hc::opt_span(xres, rows * D * 2, "attn xres");
   hc::opt_span(dmask, (long long)B * H * 256 * 8, "attn dmask");
   hc::span(qkv, rows * 3 * D * 2, "attn qkv");
   hc::span(ctx, rows * D * 2, "attn ctx");

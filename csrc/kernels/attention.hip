@@ -122,7 +122,33 @@ struct AttnArgs {
   // rows unwritten; the backward treats them as rows with no gradient (lse = +inf -> P = 0,
   // delta = 0, dQ = 0 written) -- the caller's dctx is 0 on them.
   int q_live;
+  // q_live forward of the pruned last block (nullable): also the compact [CLS] rows its out-proj
+  // reads -- cxc[b] = ctx of sequence b's [CLS] row and xc[b] = that row of xres (the block's
+  // input, the out-proj residual), for b < B; rows B .. Bp-1 (filler) copy row 0.  An empty packed
+  // sequence shares its [CLS] row with the next one: that sequence's blocks write its rows too.
+  bf16_t* cxc;
+  bf16_t* xc;
+  const bf16_t* xres;
+  int Bp;
 };
+
+// ctx / xres head-h slices of [CLS] row `tok` into compact row b (4 lanes x 4 uint2 = 64 columns)
+DEV void cls_compact_row(const AttnArgs& a, int b, size_t tok, int h, int g, const uint2 (&ov)[4]) {
+  const int D = a.H * DH;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int c = h * DH + 16 * dt + 4 * g;
+    *reinterpret_cast<uint2*>(a.cxc + (size_t)b * D + c) = ov[dt];
+    *reinterpret_cast<uint2*>(a.xc + (size_t)b * D + c) = *reinterpret_cast<const uint2*>(a.xres + tok * D + c);
+  }
+}
+DEV void cls_compact(const AttnArgs& a, int b, size_t tok, int h, int g, const uint2 (&ov)[4]) {
+  cls_compact_row(a, b, tok, h, g, ov);
+  if (a.cu)  // empty sequences before b share this [CLS] row
+    for (int b2 = b - 1; b2 >= 0 && a.cu[b2] == (int)tok; --b2) cls_compact_row(a, b2, tok, h, g, ov);
+  if (tok == 0)  // the filler rows copy row 0
+    for (int i = a.B; i < a.Bp; ++i) cls_compact_row(a, i, tok, h, g, ov);
+}
 
 // Varlen: the extra grid slice z == B zeroes head h's columns of the filler rows
 // (cu[B] .. rows-1) of `out` (`nsec` 64-wide sections, row stride ld): they are read by
@@ -558,6 +584,22 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_s128_kernel(AttnArgs a) {
   astamp_hwid();
   if (b == a.B) {
     zero_filler(a, a.ctx, D, 1, h);
+    if (a.cxc && tid < 4) {  // trailing empty sequences' [CLS] row is the (zeroed) filler row cu[B]
+      const int tok = a.cu[a.B];
+      const uint2 zero[4] = {make_uint2(0u, 0u), make_uint2(0u, 0u), make_uint2(0u, 0u), make_uint2(0u, 0u)};
+      for (int b2 = a.B - 1; b2 >= 0 && a.cu[b2] == tok; --b2) {
+        if (tok < a.rows) {
+          cls_compact_row(a, b2, (size_t)tok, h, tid, zero);
+        } else {  // (no filler row: zeros)
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const size_t c = (size_t)b2 * D + h * DH + 16 * dt + 4 * tid;
+            *reinterpret_cast<uint2*>(a.cxc + c) = zero[dt];
+            *reinterpret_cast<uint2*>(a.xc + c) = zero[dt];
+          }
+        }
+      }
+    }
     return;
   }
   int tok0i, len;
@@ -667,11 +709,14 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_s128_kernel(AttnArgs a) {
   if (q >= qlen) return;
   const float inv = (drop ? a.drop_scale : 1.f) / l;
   bf16_t* out = a.ctx + (tok0 + q) * D + h * DH;
+  uint2 ov[4];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-    *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) =
-        make_uint2(pack_bf2(o[dt][0] * inv, o[dt][1] * inv), pack_bf2(o[dt][2] * inv, o[dt][3] * inv));
+  for (int dt = 0; dt < 4; ++dt) {
+    ov[dt] = make_uint2(pack_bf2(o[dt][0] * inv, o[dt][1] * inv), pack_bf2(o[dt][2] * inv, o[dt][3] * inv));
+    *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) = ov[dt];
+  }
   if (g == 0) a.lse[((size_t)b * H + h) * S + q] = mref * LN2 + __logf(l);
+  if (a.cxc && q == 0) cls_compact(a, b, tok0, h, g, ov);
   ASTAMP(3);
 }
 
@@ -972,9 +1017,13 @@ extern "C" {
 
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                int rows, uint64_t* dmask, int q_live, hipStream_t st) {
+                int rows, uint64_t* dmask, int q_live, void* cxc, void* xc, const void* xres, int Bp,
+                hipStream_t st) {
   if (S % 64 != 0) return 1;
+  // compact [CLS] rows: the S <= 128 q_live = 1 kernel only
+  if (cxc && (!xc || !xres || q_live != 1 || !use_s128(S) || Bp < B)) return 2;
   AttnArgs a{};
+  a.cxc = (bf16_t*)cxc; a.xc = (bf16_t*)xc; a.xres = (const bf16_t*)xres; a.Bp = Bp;
   a.q_live = q_live;
   a.cu = cu;
   a.dmask = use_s128(S) ? dmask : nullptr;

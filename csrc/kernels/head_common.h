@@ -79,9 +79,63 @@ DEV void head_logit_chunk(const HeadArgs& a, const int (&b)[NR], const bf16_t* c
 // head_fwd_mean_kernel + head_bwd_kernel, whatever the surrounding code lets the compiler fuse.
 // D = 768 (DistilBERT / BERT-base): the three chunks' loads are all issued before the first sum
 // (one memory round trip instead of three); other widths walk the chunks (same sums, same order).
+// The loads of NR rows' logits at D = 768 (three 4-column chunks per lane), issued together so a
+// caller can put them in flight beside its own loads before the first use (head_logits_finish).
+template <int NR>
+struct HeadLoads {
+  uint2 xv[3][NR];
+  float4 w0[3], w1[3];
+};
+template <int NR>
+DEV void head_logits_load(const HeadArgs& a, const int (&b)[NR], int lane, HeadLoads<NR>& L) {
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int col = 4 * lane + 256 * j;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      L.xv[j][r] = *reinterpret_cast<const uint2*>(a.hidden + cls_row(a, b[r] < 0 ? 0 : b[r]) * a.D + col);
+    L.w0[j] = *reinterpret_cast<const float4*>(a.W + col);
+    L.w1[j] = *reinterpret_cast<const float4*>(a.W + a.D + col);
+  }
+}
+template <int NR>
+DEV void head_logits_finish(const HeadArgs& a, const int (&b)[NR], int lane, const HeadLoads<NR>& L,
+                            float (&z0)[NR], float (&z1)[NR]) {
+  const bool drop = a.thr != 0;
+  const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
+  const bf16_t* x[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    x[r] = nullptr;
+    z0[r] = 0.f;
+    z1[r] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    head_logit_chunk<NR>(a, b, x, 4 * lane + 256 * j, drop, seed, L.xv[j], L.w0[j], L.w1[j], z0, z1);
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    z0[r] = wave_sum(z0[r]) + a.bias[0];
+    z1[r] = wave_sum(z1[r]) + a.bias[1];
+  }
+}
+
+// Logits of NR rows b[r] (one wave, the rows' loads and chains interleaved; b[r] < 0: skipped).
+// Every lane returns the same bits (the xor butterfly of wave_sum adds the same pairs in every
+// lane).  Floating-point contraction is off in the head helpers: every kernel that inlines them
+// then rounds each product and sum the same way -- the fused pruned head (norm.hip) is bitwise
+// head_fwd_mean_kernel + head_bwd_kernel, whatever the surrounding code lets the compiler fuse.
+// D = 768 (DistilBERT / BERT-base): the three chunks' loads are all issued before the first sum
+// (one memory round trip instead of three); other widths walk the chunks (same sums, same order).
 template <int NR>
 DEV void head_logits_n(const HeadArgs& a, const int (&b)[NR], int lane, float (&z0)[NR], float (&z1)[NR]) {
 #pragma clang fp contract(off)
+  if (a.D == 768) {
+    HeadLoads<NR> L;
+    head_logits_load<NR>(a, b, lane, L);
+    head_logits_finish<NR>(a, b, lane, L, z0, z1);
+    return;
+  }
   const bool drop = a.thr != 0;
   const uint32_t seed = drop ? hash32(a.seed_ptr[0], a.site) : 0u;
   const bf16_t* x[NR];
@@ -91,29 +145,13 @@ DEV void head_logits_n(const HeadArgs& a, const int (&b)[NR], int lane, float (&
     z0[r] = 0.f;
     z1[r] = 0.f;
   }
-  if (a.D == 768) {
-    constexpr int J = 3;
-    uint2 xv[J][NR];
-    float4 w0[J], w1[J];
+  for (int col = 4 * lane; col < a.D; col += 256) {
+    uint2 xv[NR];
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int col = 4 * lane + 256 * j;
-#pragma unroll
-      for (int r = 0; r < NR; ++r) xv[j][r] = *reinterpret_cast<const uint2*>(x[r] + col);
-      w0[j] = *reinterpret_cast<const float4*>(a.W + col);
-      w1[j] = *reinterpret_cast<const float4*>(a.W + a.D + col);
-    }
-#pragma unroll
-    for (int j = 0; j < J; ++j) head_logit_chunk<NR>(a, b, x, 4 * lane + 256 * j, drop, seed, xv[j], w0[j], w1[j], z0, z1);
-  } else {
-    for (int col = 4 * lane; col < a.D; col += 256) {
-      uint2 xv[NR];
-#pragma unroll
-      for (int r = 0; r < NR; ++r) xv[r] = *reinterpret_cast<const uint2*>(x[r] + col);
-      const float4 w0 = *reinterpret_cast<const float4*>(a.W + col);
-      const float4 w1 = *reinterpret_cast<const float4*>(a.W + a.D + col);
-      head_logit_chunk<NR>(a, b, x, col, drop, seed, xv, w0, w1, z0, z1);
-    }
+    for (int r = 0; r < NR; ++r) xv[r] = *reinterpret_cast<const uint2*>(x[r] + col);
+    const float4 w0 = *reinterpret_cast<const float4*>(a.W + col);
+    const float4 w1 = *reinterpret_cast<const float4*>(a.W + a.D + col);
+    head_logit_chunk<NR>(a, b, x, col, drop, seed, xv, w0, w1, z0, z1);
   }
 #pragma unroll
   for (int r = 0; r < NR; ++r) {

@@ -871,12 +871,22 @@ __global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
     const int cb = blockIdx.x - args.nlb;
     float* dl = lds;                        // [B][2] dlogits
     float* red = lds + 2 * ((h.B + 3) & ~3);  // [2 groups][2][8][32]
-    for (int b = w; b < h.B; b += 16) {  // rows b and b + 8 of this wave, interleaved
-      const int rows[2] = {b, b + 8 < h.B ? b + 8 : -1};
-      float z0[2], z1[2];
-      head_logits_n<2>(h, rows, lane, z0, z1);
+    const int sub = threadIdx.x >> 8, t = threadIdx.x & 255;
+    const int c = t % HLB_COLS, grp = t / HLB_COLS;
+    const int col = cb * 2 * HLB_COLS + sub * HLB_COLS + c;
+    const bool live = col < D;
+    const int colc = live ? col : 0;
+    // this thread's column of the first HLB_ROWS [CLS] rows it sums (all of them for B <= 64),
+    // loaded beside the logits' loads
+    float xpre[HLB_ROWS];
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
+    for (int u = 0; u < HLB_ROWS; ++u) xpre[u] = bf2f(h.hidden[cls_row(h, min(grp + u * HLB_GROUPS, h.B - 1)) * D + colc]);
+    for (int b = w; b < h.B; b += 32) {  // rows b, b + 8, b + 16, b + 24 of this wave, interleaved
+      const int rows[4] = {b, b + 8 < h.B ? b + 8 : -1, b + 16 < h.B ? b + 16 : -1, b + 24 < h.B ? b + 24 : -1};
+      float z0[4], z1[4];
+      head_logits_n<4>(h, rows, lane, z0, z1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
         if (rows[r] < 0) continue;
         const int br = rows[r];
         float loss, d0, d1;
@@ -896,18 +906,13 @@ __global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
     }
     __syncthreads();  // dlogits in LDS; (block 0) every row loss written, workgroup-visible
     if (cb == 0 && w == 0) loss_mean(h, lane);
-    const int sub = threadIdx.x >> 8, t = threadIdx.x & 255;
-    const int c = t % HLB_COLS, grp = t / HLB_COLS;
-    const int col = cb * 2 * HLB_COLS + sub * HLB_COLS + c;
-    const bool live = col < D;
-    const int colc = live ? col : 0;
     float g0 = 0.f, g1 = 0.f;
     for (int b0 = grp; b0 < h.B; b0 += HLB_GROUPS * HLB_ROWS) {
       float x[HLB_ROWS];
 #pragma unroll
       for (int u = 0; u < HLB_ROWS; ++u) {
         const int b = min(b0 + u * HLB_GROUPS, h.B - 1);
-        x[u] = bf2f(h.hidden[cls_row(h, b) * D + colc]);
+        x[u] = b0 == grp ? xpre[u] : bf2f(h.hidden[cls_row(h, b) * D + colc]);
       }
 #pragma unroll
       for (int u = 0; u < HLB_ROWS; ++u) {
@@ -959,16 +964,19 @@ __global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
   for (int base = blockIdx.x * rows_per_iter; base < a.T; base += args.nlb * rows_per_iter) {
     const int row = base + (threadIdx.x >> 5);
     const int rr = min(row, a.T - 1);
-    // this half-wave's row operands first (their latency overlaps the logits)
+    // every load of the iteration in flight at once: this half-wave's row operands and the wave's
+    // two head rows (whole-wave reductions: wave-uniform control flow)
+    const int rA = base + 2 * w;
+    const int rows[2] = {rA < h.B ? rA : -1, rA + 1 < h.B ? rA + 1 : -1};
+    HeadLoads<2> hlo;
+    head_logits_load<2>(h, rows, lane, hlo);
     const float mean = a.mean[rr], rstd = a.rstd[rr];
+    const bool empty = rr < h.B && empty_seq(h, rr);
     float xh[CH][8];
     uint32_t keep;
     ln_load_sum(a, rr, hl, drop, seed, xh, keep);
-    // the wave's two rows' dlogits (whole-wave reductions: wave-uniform control flow)
-    const int rA = base + 2 * w;
-    const int rows[2] = {rA < h.B ? rA : -1, rA + 1 < h.B ? rA + 1 : -1};
     float z0[2] = {0.f, 0.f}, z1[2] = {0.f, 0.f};
-    if (rows[0] >= 0) head_logits_n<2>(h, rows, lane, z0, z1);
+    if (rows[0] >= 0) head_logits_finish<2>(h, rows, lane, hlo, z0, z1);
     const int mine = lane < HL ? 0 : 1;
     float d0 = 0.f, d1 = 0.f;
     if (rows[mine] >= 0) {
@@ -976,7 +984,7 @@ __global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
       head_loss_grad(h, rows[mine], z0[mine], z1[mine], loss, d0, d1);
     }
     if (row >= a.T) continue;  // (whole half-waves)
-    const bool grad_row = row < h.B && !empty_seq(h, row);
+    const bool grad_row = row < h.B && !empty;
     float dyv[CH][8];
 #pragma unroll
     for (int c = 0; c < CH; ++c) {

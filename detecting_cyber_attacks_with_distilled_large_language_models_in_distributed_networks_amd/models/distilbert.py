@@ -564,7 +564,7 @@ class DDoSClassifier(nn.Module):
         """Last-block [CLS] pruning (RunCtx.prune_idx; ops/functional.py LayerFn._forward_pruned):
         exact -- the dropped rows reach neither the loss nor any gradient.  Needs the fused
         LayerNorm path and, for a training step, the all-layer dW launch (the pruned block's
-        out-proj / FFN weight gradients join it with K = Bp rows) and the W^T copies.  Returns the
+        out-proj / FFN weight gradients join it with K = Bp rows).  Returns the
         per-shape index buffers (the packing launch fills the packed [CLS] rows), or None."""
         from ..ops import kernels as K
         B, S, D = rc.B, rc.S, self.config.dim

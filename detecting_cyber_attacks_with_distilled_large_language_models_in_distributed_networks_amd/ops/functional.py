@@ -239,9 +239,13 @@ class LayerFn(torch.autograd.Function):
         qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
         dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
         # only each sequence's first query row ([CLS]) is needed: the other rows' context is never read
-        cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask, q_live=1)
         ci, rm = rc.cls_rows, rc.cls_rmap
-        cxc, xc = K.gather_rows2(cx, x, ci)
+        if K.attn_cls_compact_ok(rc.S):  # the attention launch also writes the compact [CLS] rows
+            cx, lse, cxc, xc = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask,
+                                          q_live=1, cls=(x, ci.numel()))
+        else:
+            cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask, q_live=1)
+            cxc, xc = K.gather_rows2(cx, x, ci)
         h, ao, m1, r1 = K.linear_ln_fwd(cxc, L["o_w"], L["o_b"], xc, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0,
                                         keep_z=grad, xsite=K.ln_xsite(idx, 0, False))
         g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)

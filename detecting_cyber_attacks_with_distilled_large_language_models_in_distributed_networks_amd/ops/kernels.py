@@ -318,17 +318,38 @@ def attn_keep_bits(B, S, H, p, device) -> Optional[torch.Tensor]:
     return torch.empty(B * H * 256, dtype=torch.int64, device=device)
 
 
-def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+# The S <= 128 attention kernel writes the pruned block's compact [CLS] rows itself (gather_rows2
+# folded into the attention launch); FD_ATTN_CLS_COMPACT=0 restores the separate gather.
+ATTN_CLS_COMPACT = _os.environ.get("FD_ATTN_CLS_COMPACT", "1") != "0"
+
+
+def attn_cls_compact_ok(S: int) -> bool:
+    return ATTN_CLS_COMPACT and S <= 128 and _os.environ.get("FD_ATTN_S128", "1") != "0"
+
+
+def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, cls=None):
     """cu (int32 [B+1]): varlen mode -- qkv/ctx hold packed sequences (rows cu[b]..cu[b+1]-1);
     the kernel zeroes ctx's filler rows past cu[B] itself.  dmask (``attn_keep_bits``): also
-    record the dropout keep bits for ``attn_bwd``."""
+    record the dropout keep bits for ``attn_bwd``.
+
+    cls = (x, Bp) (q_live 1, ``attn_cls_compact_ok(S)``): also return ctx[cls_rows] and
+    x[cls_rows] as [Bp, D] -- sequence b's [CLS] row in compact row b, rows B..Bp-1 copies of
+    row 0 (the pruned block's ``cls_rows`` layout) -- written by the attention blocks that own the
+    rows.  Returns (ctx, lse) or (ctx, lse, cxc, xc)."""
     rows = qkv.shape[0] if cu is not None else B * S
     ctx = torch.empty(rows, H * 64, dtype=torch.bfloat16, device=qkv.device)
     lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
     thr, sc = _drop(p)
-    # q_live > 0 (S <= 128): only the first q_live query rows of each sequence are computed
-    ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None, q_live)
-    return ctx, lse
+    if cls is None:
+        # q_live > 0 (S <= 128): only the first q_live query rows of each sequence are computed
+        ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None, q_live)
+        return ctx, lse
+    x, Bp = cls
+    cxc = torch.empty(Bp, H * 64, dtype=torch.bfloat16, device=qkv.device)
+    xc = torch.empty_like(cxc)
+    ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None, q_live,
+                   cxc, xc, x)
+    return ctx, lse, cxc, xc
 
 
 def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0) -> torch.Tensor:

@@ -153,6 +153,65 @@ def test_attention_q_live_matches_full_and_ignores_garbage():
         assert _frel(d_q, d_full) < 1e-2
 
 
+@pytest.mark.parametrize("lens", [[70, 84, 60, 77, 81, 65, 83, 72], [0, 84, 0, 0, 81, 65, 83, 72],
+                                  [70, 84, 60, 77, 81, 65, 0, 0], None])
+def test_attention_writes_compact_cls_rows(lens):
+    """The pruned block's attention launch also writes ctx[cls_rows] / x[cls_rows] as [Bp, D]
+    (ops/kernels.py attn_fwd cls=; it replaced the separate gather_rows2 launch): bitwise the
+    gather, with empty sequences (leading, inner, trailing: their [CLS] row is the next sequence's
+    first row or the zeroed filler row cu[B]), the filler rows B..Bp-1 (row 0) and the padded
+    layout (lens None)."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import (
+        kernels as K)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    B, S, H = 8, 128, 12
+    if lens is None:
+        cu, rows = None, B * S
+        cls = torch.arange(B, device="cuda") * S
+    else:
+        cu = torch.zeros(B + 1, dtype=torch.int32)
+        cu[1:] = torch.cumsum(torch.tensor(lens), 0)
+        rows = (int(cu[-1]) + 127) // 128 * 128
+        cu = cu.cuda()
+        cls = cu[:-1].long()
+    Bp = 64
+    ci = torch.zeros(Bp, dtype=torch.int64, device="cuda")
+    ci[:B] = cls
+    qkv = (torch.randn(rows, 3 * H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    x = torch.randn(rows, H * 64, device="cuda", generator=g).to(torch.bfloat16)
+    kb = torch.zeros(1, device="cuda") if cu is not None else torch.zeros(B * S, device="cuda")
+    seed = torch.tensor([3], dtype=torch.int32, device="cuda")
+    for p in (0.0, 0.1):
+        dm = K.attn_keep_bits(B, S, H, p, "cuda")
+        ctx, lse, cxc, xc = K.attn_fwd(qkv, kb, B, S, H, seed, 5, p, cu=cu, dmask=dm, q_live=1, cls=(x, Bp))
+        ref_c, ref_x = K.gather_rows2(ctx, x, ci)
+        torch.cuda.synchronize()
+        assert torch.equal(cxc, ref_c) and torch.equal(xc, ref_x)
+        assert torch.isfinite(cxc.float()).all()
+
+
+@pytest.mark.parametrize("packed,empty", [(True, None), (True, 3), (False, None)])
+def test_compact_cls_attention_step_bitwise(packed, empty, monkeypatch):
+    """A pruned training forward + backward with the compact-row attention launch equals the one
+    with the separate gather launch bit for bit (loss, logits, every gradient)."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+    outs = []
+    for on in (True, False):
+        monkeypatch.setattr(K, "ATTN_CLS_COMPACT", on)
+        m = DDoSClassifier(config=DistilBertConfig(n_layers=2), device="cuda", impl="hip", seed=37)
+        m.prune_last = True
+        m.train()
+        ids, mask, labels, tokens = _batch(20, 128, seed=820, empty=empty)
+        m.zero_grad()
+        m.rng.fill_(5)
+        loss, logits = m.forward_loss(ids, mask, labels, tokens=tokens if packed else None)
+        loss.backward()
+        torch.cuda.synchronize()
+        outs.append((loss.detach().clone(), logits.detach().clone(), m.arena.grad.clone()))
+    (l0, z0, g0), (l1, z1, g1) = outs
+    assert torch.equal(z0, z1) and l0.item() == l1.item() and torch.equal(g0, g1)
+
+
 @pytest.mark.parametrize("packed,B,empty,kd", [(True, 32, None, False), (True, 20, 3, False), (False, 16, None, False),
                                                (True, 32, None, True)])
 def test_fused_head_ln_backward_bitwise(packed, B, empty, kd, monkeypatch):
