@@ -69,7 +69,7 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx,
                 float* delta, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float drop_scale, const int* cu, int rows, const uint64_t* dmask, int q_live,
-                hipStream_t st);
+                const void* dresc, void* dres, hipStream_t st);
 int fd_mask_to_bias(const void* mask, int mask_bytes, float* bias, long n, hipStream_t st);
 int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, float* mean,
               float* rstd, int T, int D, float eps, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
@@ -828,9 +828,13 @@ void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
 void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
               const at::Tensor& dctx, const at::Tensor& delta, const at::Tensor& dqkv, int64_t B, int64_t S, int64_t H,
               const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& cu,
-              const c10::optional<at::Tensor>& dmask, int64_t q_live = 0) {
+              const c10::optional<at::Tensor>& dmask, int64_t q_live = 0,
+              const c10::optional<at::Tensor>& dresc = c10::nullopt, const c10::optional<at::Tensor>& dres = c10::nullopt) {
   TORCH_CHECK(q_live >= 0, "attention: q_live >= 0");
   check_dmask(dmask, B, S, H);
+  // compact [CLS] gradients: dctx and dresc are [Bp, D], dres is the full-layout [rows, D] output
+  const bool compact = dresc.has_value() && dresc->defined();
+  TORCH_CHECK(compact == (dres.has_value() && dres->defined()), "attention bwd: dresc and dres go together");
   need(qkv, at::kBFloat16, "qkv");
   need(kbias, at::kFloat, "kbias");
   need(ctx, at::kBFloat16, "ctx");
@@ -842,14 +846,24 @@ void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
   const bool varlen = cu.has_value() && cu->defined();
   const int64_t rows = varlen ? qkv.numel() / (3 * H * 64) : B * S;
   TORCH_CHECK(qkv.numel() == rows * 3 * H * 64 && dqkv.numel() == qkv.numel(), "attention bwd: qkv size");
-  TORCH_CHECK(ctx.numel() == rows * H * 64 && dctx.numel() == ctx.numel(), "attention bwd: ctx size");
+  if (compact) {
+    TORCH_CHECK(q_live == 1, "attention bwd: compact [CLS] gradients need q_live 1");
+    need(*dresc, at::kBFloat16, "dresc");
+    need(*dres, at::kBFloat16, "dres");
+    TORCH_CHECK(dctx.numel() % (H * 64) == 0 && dctx.numel() / (H * 64) >= B && dresc->numel() == dctx.numel(),
+                "attention bwd: compact dctx / dresc size");
+    TORCH_CHECK(ctx.numel() == rows * H * 64 && dres->numel() == ctx.numel(), "attention bwd: ctx / dres size");
+  } else {
+    TORCH_CHECK(ctx.numel() == rows * H * 64 && dctx.numel() == ctx.numel(), "attention bwd: ctx size");
+  }
   TORCH_CHECK(lse.numel() == B * H * S && delta.numel() == B * H * S && (varlen || kbias.numel() == B * S),
               "attention bwd: stats");
   check_cu(cu, B, rows, ctx.numel() / (H * 64));
   check_rc(fd_attn_bwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(),
                        dctx.data_ptr(), delta.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)S, (int)H,
                        seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), (int)rows,
-                       ptr<uint64_t>(dmask), (int)q_live, stream()),
+                       ptr<uint64_t>(dmask), (int)q_live, compact ? dresc->data_ptr() : nullptr,
+                       compact ? dres->data_ptr() : nullptr, stream()),
            "attn_bwd");
 }
 
@@ -1411,7 +1425,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("xres") = py::none());
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("dctx"),
         py::arg("delta"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"),
-        py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("q_live") = 0);
+        py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("q_live") = 0,
+        py::arg("dresc") = py::none(), py::arg("dres") = py::none());
   m.def("mask_to_bias", &mask_to_bias);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);

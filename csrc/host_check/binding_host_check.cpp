@@ -258,14 +258,17 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
 }
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx, float* delta,
                 void* dqkv, int B, int S, int H, const uint32_t* seed, uint32_t, uint32_t, float, const int* cu,
-                int rows, const uint64_t* dmask, int, hipStream_t) {
+                int rows, const uint64_t* dmask, int, const void* dresc, void* dres, hipStream_t) {
   ++hc::calls;
   const long long D = (long long)H * 64;
   hc::opt_span(dmask, (long long)B * H * 256 * 8, "attn bwd dmask");
   hc::span(qkv, rows * 3 * D * 2, "attn bwd qkv");
   hc::span(dqkv, rows * 3 * D * 2, "attn bwd dqkv");
   hc::span(ctx, rows * D * 2, "attn bwd ctx");
-  hc::span(dctx, rows * D * 2, "attn bwd dctx");
+  // (compact [CLS] gradients: dctx / dresc hold >= B rows, dres the full layout)
+  hc::span(dctx, (dres ? B : rows) * D * 2, "attn bwd dctx");
+  hc::opt_span(dresc, (long long)B * D * 2, "attn bwd dresc");
+  hc::opt_span(dres, rows * D * 2, "attn bwd dres");
   hc::span(lse, (long long)B * H * S * 4, "attn bwd lse");
   hc::span(delta, (long long)B * H * S * 4, "attn bwd delta");
   hc::span(seed, 4, "attn bwd seed");

@@ -130,24 +130,41 @@ struct AttnArgs {
   bf16_t* xc;
   const bf16_t* xres;
   int Bp;
+  // its q_live backward with compact [CLS] gradients (nullable): dctx is [Bp, D] (row b = sequence
+  // b's [CLS] row; the other rows' dO is 0) and the launch also scatters dresc (the out-proj
+  // residual gradient, [Bp, D]) into the full layout dres (row cu[b] = dresc[b], other rows 0;
+  // a row shared with empty sequences takes the LAST owner's gradient -- ops/kernels.py
+  // scatter_rows2's rule, which this replaces)
+  const bf16_t* dresc;
+  bf16_t* dres;
 };
 
-// ctx / xres head-h slices of [CLS] row `tok` into compact row b (4 lanes x 4 uint2 = 64 columns)
-DEV void cls_compact_row(const AttnArgs& a, int b, size_t tok, int h, int g, const uint2 (&ov)[4]) {
+// ctx / xres head-h slices of [CLS] row `tok` into compact row b (4 lanes x 4 uint2 = 64 columns;
+// xv = the xres slice, loaded once by the caller: the filler fan-out below must not pay a
+// dependent load per row)
+DEV void cls_compact_row(const AttnArgs& a, int b, int h, int g, const uint2 (&ov)[4], const uint2 (&xv)[4]) {
   const int D = a.H * DH;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
     const int c = h * DH + 16 * dt + 4 * g;
     *reinterpret_cast<uint2*>(a.cxc + (size_t)b * D + c) = ov[dt];
-    *reinterpret_cast<uint2*>(a.xc + (size_t)b * D + c) = *reinterpret_cast<const uint2*>(a.xres + tok * D + c);
+    *reinterpret_cast<uint2*>(a.xc + (size_t)b * D + c) = xv[dt];
   }
 }
+DEV void cls_xres(const AttnArgs& a, size_t tok, int h, int g, uint2 (&xv)[4]) {
+  const int D = a.H * DH;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+    xv[dt] = *reinterpret_cast<const uint2*>(a.xres + tok * D + h * DH + 16 * dt + 4 * g);
+}
 DEV void cls_compact(const AttnArgs& a, int b, size_t tok, int h, int g, const uint2 (&ov)[4]) {
-  cls_compact_row(a, b, tok, h, g, ov);
+  uint2 xv[4];
+  cls_xres(a, tok, h, g, xv);
+  cls_compact_row(a, b, h, g, ov, xv);
   if (a.cu)  // empty sequences before b share this [CLS] row
-    for (int b2 = b - 1; b2 >= 0 && a.cu[b2] == (int)tok; --b2) cls_compact_row(a, b2, tok, h, g, ov);
+    for (int b2 = b - 1; b2 >= 0 && a.cu[b2] == (int)tok; --b2) cls_compact_row(a, b2, h, g, ov, xv);
   if (tok == 0)  // the filler rows copy row 0
-    for (int i = a.B; i < a.Bp; ++i) cls_compact_row(a, i, tok, h, g, ov);
+    for (int i = a.B; i < a.Bp; ++i) cls_compact_row(a, i, h, g, ov, xv);
 }
 
 // Varlen: the extra grid slice z == B zeroes head h's columns of the filler rows
@@ -589,7 +606,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_s128_kernel(AttnArgs a) {
       const uint2 zero[4] = {make_uint2(0u, 0u), make_uint2(0u, 0u), make_uint2(0u, 0u), make_uint2(0u, 0u)};
       for (int b2 = a.B - 1; b2 >= 0 && a.cu[b2] == tok; --b2) {
         if (tok < a.rows) {
-          cls_compact_row(a, b2, (size_t)tok, h, tid, zero);
+          uint2 xv[4];
+          cls_xres(a, (size_t)tok, h, tid, xv);
+          cls_compact_row(a, b2, h, tid, zero, xv);
         } else {  // (no filler row: zeros)
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) {
@@ -901,6 +920,33 @@ DEV float row_delta(const bf16x8 (&of)[2], const bf16x8 (&dof)[2]) {
   return dl;
 }
 
+// dO tiles of a compact-[CLS] backward (AttnArgs::dresc): row 0 = the sequence's compact row,
+// every other row 0 (what stage_rows reads from the scattered layout, clamp included)
+template <int NT = 512>
+DEV void stage_cls_rows(char* lds, const bf16_t* src, int tid, int nt, int len) {
+#pragma unroll
+  for (int i = 0; i < 1024 / NT; ++i) {
+    const int id = i * NT + tid;
+    const int r = id >> 3, c = id & 7;
+    if (r < 64 * nt) {
+      const uint4 v = min(r, len - 1) == 0 ? *reinterpret_cast<const uint4*>(src + c * 8) : make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(lds + (r >> 6) * 8192 + tile_off(r & 63, c)) = v;
+    }
+  }
+}
+
+// Head h's columns of the sequence's rows of dres: row 0 = dresc[b], the others 0.
+template <int NT = 512>
+DEV void scatter_cls_rows(const AttnArgs& a, int b, size_t tok0, int len, int h, int tid) {
+  const int D = a.H * DH;
+  for (int id = tid; id < len * 8; id += NT) {
+    const int r = id >> 3, c = id & 7;
+    const uint4 v = r == 0 ? *reinterpret_cast<const uint4*>(a.dresc + (size_t)b * D + h * DH + c * 8)
+                           : make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(a.dres + (tok0 + r) * D + h * DH + c * 8) = v;
+  }
+}
+
 // Zero dQ of rows without a gradient (q_live: not among the query rows the loss reaches).
 DEV void zero_dq_rows(const AttnArgs& a, int h, int q, int len, size_t tok0, int g) {
   if (q >= len) return;
@@ -930,6 +976,16 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   astamp_hwid();
   if (b == a.B) {
     zero_filler(a, a.dqkv, ld3, 3, h);
+    if (a.dres) {
+      zero_filler(a, a.dres, D, 1, h);
+      const int tok = a.cu[a.B];  // trailing empty sequences: the last one's gradient on row cu[B]
+      if (a.B > 0 && a.cu[a.B - 1] == tok && tok < a.rows) {
+        __syncthreads();
+        if (tid < 8)
+          *reinterpret_cast<uint4*>(a.dres + (size_t)tok * D + h * DH + tid * 8) =
+              *reinterpret_cast<const uint4*>(a.dresc + (size_t)(a.B - 1) * D + h * DH + tid * 8);
+      }
+    }
     return;
   }
   int tok0i, len;
@@ -937,6 +993,7 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   const int nt = (len + 63) >> 6;
   const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows with a gradient
   const size_t tok0 = (size_t)tok0i;
+  if (a.dres) scatter_cls_rows(a, b, tok0, len, h, tid);
   const size_t st0 = ((size_t)b * H + h) * S;
   // phase 1's O rows (for delta) are fetched together with the staging loads: no second
   // dependent global round trip after the barrier
@@ -950,7 +1007,10 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   stage_rows(qs, a.qkv + tok0 * ld3 + h * DH, ld3, tid, nt, len);
   stage_rows(ks, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
   stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
-  stage_rows(os, a.dctx + tok0 * D + h * DH, D, tid, nt, len);
+  if (a.dres)
+    stage_cls_rows(os, a.dctx + (size_t)b * D + h * DH, tid, nt, len);
+  else
+    stage_rows(os, a.dctx + tok0 * D + h * DH, D, tid, nt, len);
   if (tid < 128) {
     kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) * LOG2E : -INFINITY;
     // query rows past the sequence: lse = +inf makes their P (and dS) exactly 0
@@ -1040,9 +1100,12 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse,
                 const void* dctx, float* delta, void* dqkv, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                int rows, const uint64_t* dmask, int q_live, hipStream_t st) {
+                int rows, const uint64_t* dmask, int q_live, const void* dresc, void* dres, hipStream_t st) {
   if (S % 64 != 0) return 1;
+  // compact [CLS] gradients: the S <= 128 q_live = 1 kernel only
+  if ((dresc != nullptr) != (dres != nullptr) || (dres && (q_live != 1 || !use_s128(S)))) return 2;
   AttnArgs a{};
+  a.dresc = (const bf16_t*)dresc; a.dres = (bf16_t*)dres;
   a.q_live = q_live;
   a.cu = cu;
   a.dmask = use_s128(S) ? const_cast<uint64_t*>(dmask) : nullptr;

@@ -293,10 +293,16 @@ class LayerFn(torch.autograd.Function):
                                      G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, xsite=K.ln_xsite(ctx.idx, 0, True),
                                      b_mn=True)
         dcxc = K.linear_dx(dz1c, L["o_w"])
-        # the [CLS] rows' gradients back into the full layout (every other row exactly 0)
-        dcx, dz1 = K.scatter_rows2(dcxc, dz1c, ci, B, cx.shape[0])
-        dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask,
-                          q_live=1)
+        if K.attn_cls_compact_ok(rc.S):
+            # the attention backward reads the compact [CLS] gradient and scatters dz1c into the
+            # full layout itself (every other row exactly 0)
+            dqkv, dz1 = K.attn_bwd(qkv, rc.kbias, cx, lse, dcxc, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu,
+                                   ctx.dmask, q_live=1, dresc=dz1c)
+        else:
+            # the [CLS] rows' gradients back into the full layout (every other row exactly 0)
+            dcx, dz1 = K.scatter_rows2(dcxc, dz1c, ci, B, cx.shape[0])
+            dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu,
+                              ctx.dmask, q_live=1)
         # (the qkv bias gradient: column sums of dqkv in the dW launch's qkv tiles, K.DW_QKV_BIAS)
         batch += [(dz1c, cxc, G["o_w"].buf, acc),
                   (dqkv, x, G["qkv_w"].buf, acc, G["qkv_b"].buf if K.DW_QKV_BIAS else None)]

@@ -352,14 +352,24 @@ def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: in
     return ctx, lse, cxc, xc
 
 
-def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0) -> torch.Tensor:
-    """dmask: the keep bits recorded by the matching ``attn_fwd`` (same seed / site / p)."""
+def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, dresc=None):
+    """dmask: the keep bits recorded by the matching ``attn_fwd`` (same seed / site / p).
+
+    dresc ([Bp, D], q_live 1, ``attn_cls_compact_ok(S)``): ``dctx`` is the compact [CLS]
+    gradient [Bp, D] (row b = sequence b's [CLS] row, every other row's dO 0) and the launch also
+    scatters ``dresc`` into the full layout -- returns (dqkv, dres) with dres = what
+    ``scatter_rows2(dctx, dresc, cls_rows, B, rows)[1]`` gives; otherwise dqkv."""
     dqkv = torch.empty_like(qkv)  # varlen: filler rows zeroed by the dQ kernel
     delta = workspace(qkv.device, "attn_delta", B * H * S)
     thr, sc = _drop(p)
+    if dresc is None:
+        ext().attn_bwd(qkv, kbias, ctx, lse, dctx.contiguous(), delta, dqkv, B, S, H, seed, site, thr, sc, cu,
+                       dmask if thr else None, q_live)
+        return dqkv
+    dres = torch.empty_like(ctx)
     ext().attn_bwd(qkv, kbias, ctx, lse, dctx.contiguous(), delta, dqkv, B, S, H, seed, site, thr, sc, cu,
-                   dmask if thr else None, q_live)
-    return dqkv
+                   dmask if thr else None, q_live, dresc.contiguous(), dres)
+    return dqkv, dres
 
 
 # ------------------------------------------------------------------ layernorm / embedding

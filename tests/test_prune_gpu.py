@@ -160,7 +160,8 @@ def test_attention_writes_compact_cls_rows(lens):
     (ops/kernels.py attn_fwd cls=; it replaced the separate gather_rows2 launch): bitwise the
     gather, with empty sequences (leading, inner, trailing: their [CLS] row is the next sequence's
     first row or the zeroed filler row cu[B]), the filler rows B..Bp-1 (row 0) and the padded
-    layout (lens None)."""
+    layout (lens None).  Its backward (attn_bwd dresc=) reads the compact [CLS] gradient and
+    scatters the residual gradient: bitwise scatter_rows2 + the plain backward."""
     from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import (
         kernels as K)
     g = torch.Generator(device="cuda").manual_seed(6)
@@ -188,6 +189,16 @@ def test_attention_writes_compact_cls_rows(lens):
         torch.cuda.synchronize()
         assert torch.equal(cxc, ref_c) and torch.equal(xc, ref_x)
         assert torch.isfinite(cxc.float()).all()
+        # backward: compact dO + the residual-gradient scatter in the attention launch == the
+        # scatter_rows2 launch followed by the plain q_live backward
+        dcxc = (torch.randn(Bp, H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+        dresc = torch.randn(Bp, H * 64, device="cuda", generator=g).to(torch.bfloat16)
+        dq, dres = K.attn_bwd(qkv, kb, ctx, lse, dcxc, B, S, H, seed, 5, p, cu=cu, dmask=dm, q_live=1, dresc=dresc)
+        dcx, ref_res = K.scatter_rows2(dcxc, dresc, ci, B, rows)
+        ref_q = K.attn_bwd(qkv, kb, ctx, lse, dcx, B, S, H, seed, 5, p, cu=cu, dmask=dm, q_live=1)
+        torch.cuda.synchronize()
+        assert torch.equal(dres, ref_res)
+        assert torch.equal(dq, ref_q)
 
 
 @pytest.mark.parametrize("packed,empty", [(True, None), (True, 3), (False, None)])
