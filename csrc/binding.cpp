@@ -432,7 +432,7 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
                 const c10::optional<at::Tensor>& colpart, const at::Tensor& stats, const at::Tensor& cnt,
                 const at::Tensor& err, double eps, const c10::optional<at::Tensor>& seed, int64_t site, int64_t thr,
                 double dscale, const c10::optional<at::Tensor>& row_map, int64_t cfg, int64_t xsite,
-                bool b_mn = false) {
+                bool b_mn = false, const c10::optional<at::Tensor>& xbuf = c10::nullopt) {
   // b_mn: Bt is the weight itself, W [K][N] (MN-major B through the LDS-DMA ring, transposing fragment reads)
   need(A, at::kBFloat16, "A");
   need(Bt, at::kBFloat16, "Bt");
@@ -496,6 +496,18 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
     TORCH_CHECK(seed.has_value() && seed->defined(), "gemm_ln: dropout needs the seed tensor");
     ln.seed_ptr = seedp(*seed);
     ln.row_map = ptr<int>(row_map);
+  }
+  // two-K-half tiles: the partial exchange (xbuf: >= tiles_m * N / 64 * 32 KiB) and its flag
+  // granules, the last LN2_FLAGS entries of stats (zeroed with it at an epoch wrap)
+  constexpr int64_t LN2_FLAGS = 512;
+  if (xbuf.has_value() && xbuf->defined()) {
+    need(*xbuf, at::kFloat, "xbuf");
+    const int64_t pairs = ((M + 127) / 128) * (N / 128);
+    if (xbuf->numel() >= pairs * 2 * 8192 && pairs * 2 <= LN2_FLAGS &&
+        stats.numel() >= 2 * (M + 128) * (N / 64) + LN2_FLAGS) {
+      ln.xbuf = xbuf->data_ptr<float>();
+      ln.xflag = reinterpret_cast<uint64_t*>(stats.data_ptr()) + (stats.numel() - LN2_FLAGS);
+    }
   }
   const int rc = fd_gemm_ln(bwd ? 1 : 0, A.data_ptr(), Bt.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
                             ptr<float>(bias), res.data_ptr(), (int)N, &ln, (int)cfg, b_mn ? 1 : 0, stream());
@@ -1393,7 +1405,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("rstd"), py::arg("z"),
         py::arg("dx"), py::arg("colpart"), py::arg("stats"), py::arg("cnt"), py::arg("err"), py::arg("eps"),
         py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("row_map"),
-        py::arg("cfg") = -1, py::arg("xsite") = 0, py::arg("b_mn") = false);
+        py::arg("cfg") = -1, py::arg("xsite") = 0, py::arg("b_mn") = false, py::arg("xbuf") = py::none());
   m.def("gemm_dw_batch", &gemm_dw_batch, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("accumulate"),
         py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1,
         py::arg("biases") = std::vector<at::Tensor>{}, py::arg("rest") = std::vector<at::Tensor>{},

@@ -203,6 +203,11 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   hc::span(ln->stats, tm * (N / 64) * 2 * bm * 8, "gemm_ln stats");
   hc::span(ln->cnt, 4, "gemm_ln cnt");
   hc::span(ln->err, 4, "gemm_ln err");
+  if (ln->xbuf) {  // two-K-half tiles: pairs x 2 x 32 KiB of partials, pairs x 2 flag granules
+    const long long pairs = tm * (N / 128);
+    hc::span(ln->xbuf, pairs * 2 * 32768, "gemm_ln xbuf");
+    hc::span(ln->xflag, pairs * 2 * 8, "gemm_ln xflag");
+  }
   if (bwd) {
     hc::span(ln->z, mn * 2, "gemm_ln z");
     hc::span(ln->colpart, tm * 3 * N * 4, "gemm_ln colpart");

@@ -94,4 +94,9 @@ struct FdLnEpi {
   float dscale;
   const int* row_map;     // packed row -> padded row (dropout hash only; nullable)
   float eps;
+  // two-K-half tiles (gemm.hip gemm_ln2_kernel): the two blocks of a 128 x 128 product tile trade
+  // the fp32 column halves they do not finish -- xbuf [pairs][2][32 KiB] and xflag [pairs][2]
+  // {tag, 1} granules (the stats buffer's tail: zeroed with it at an epoch wrap).  Nullable.
+  float* xbuf;
+  uint64_t* xflag;
 };

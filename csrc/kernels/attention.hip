@@ -992,6 +992,9 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   seq_span(a, b, tok0i, len);
   const int nt = (len + 63) >> 6;
   const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows with a gradient
+  // an empty sequence (varlen) owns no rows: nothing to write, and its clamped row len - 1 = -1
+  // must not be read (a leading empty sequence would read before the tensors)
+  if (len == 0) return;
   const size_t tok0 = (size_t)tok0i;
   if (a.dres) scatter_cls_rows(a, b, tok0, len, h, tid);
   const size_t st0 = ((size_t)b * H + h) * S;

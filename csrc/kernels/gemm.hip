@@ -47,6 +47,8 @@ enum Epi : int {
   EPI_F32 = 5,        // C(fp32 slab z) = acc
   EPI_LN = 6,         // C(bf16) = LN(dropout(acc + bias) + res)    (p.ln; gemm_ln_kernel only)
   EPI_LN_BWD = 7,     // C(bf16) = LN backward of dy = acc + res    (p.ln; gemm_ln_kernel only)
+  EPI_LN2 = 8,        // EPI_LN / EPI_LN_BWD of a 128 x 64 tile from the two K halves of a 128 x 128
+  EPI_LN2_BWD = 9,    //   product tile (gemm_ln2_kernel only; p.ln2_half = which half this block runs)
 };
 
 struct GemmParams {
@@ -88,6 +90,7 @@ struct GemmParams {
   float* acol_m;
   float* acol_v;
   uint16_t* acol_sh;
+  int ln2_half;          // EPI_LN2*: this block's K half and the 64-column half of the tile it finishes
 };
 
 constexpr int BKT = 64;
@@ -243,7 +246,8 @@ struct Operand {
 template <int EPI, int BM, int BN>
 struct EpiTraits {
   static constexpr bool ELEM = (EPI == EPI_ADD || EPI == EPI_GELU_BWD);
-  static constexpr bool LN = (EPI == EPI_LN || EPI == EPI_LN_BWD);
+  static constexpr bool LN2 = (EPI == EPI_LN2 || EPI == EPI_LN2_BWD);
+  static constexpr bool LN = (EPI == EPI_LN || EPI == EPI_LN_BWD || LN2);
   // fp32 weight-gradient tiles too large to stage in LDS (256 x 192, 256 x 256) are finished
   // straight from the accumulators (direct_f32_epilogue): 16-byte stores per lane
   static constexpr bool DIRECT = EPI == EPI_F32 && BM * (BN * 4 + 16) > LDS_MAX;
@@ -613,10 +617,34 @@ DEV LnPre<BM * (BN / 8) / NT> ln_from_lds(const GemmParams& p, int tm, int tn, i
   return pre;
 }
 
-template <int BM, int BN, int TM, int TN, bool BWD, int NT>
-DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int tm, int tn,
-                     int wr, int wc, int lane, int tid, const LnPre<BM * (BN / 8) / NT>& pre) {
+// The LayerNorm epilogue in two steps: ln_park (each wave's accumulators, + bias in the forward,
+// into the fp32 LDS tile [BM][BN]) and ln_finish (the element math, the row-statistics exchange,
+// the normalisation and the stores).  ln_epilogue = both; the two-K-half kernel parks only the
+// waves that hold its final columns (gemm_ln2_kernel).
+template <int BM, int BN, int TM, int TN, bool BWD>
+DEV void ln_park(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int n0, int wr, int wc,
+                 int lane) {
   constexpr int MI = TM / 16, NI = TN / 16;
+  constexpr int LDC = BN * 4 + 16;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int r = wr * TM + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int c = wc * TN + j * 16 + 4 * (lane >> 4);
+      float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      if constexpr (!BWD) {
+        const float4 b = *reinterpret_cast<const float4*>(p.bias + n0 + c);
+        v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+      }
+      *reinterpret_cast<float4*>(smem + r * LDC + c * 4) = v;
+    }
+  }
+}
+
+template <int BM, int BN, bool BWD, int NT>
+DEV void ln_finish(const GemmParams& p, char* smem, int tm, int tn, int lane, int tid,
+                   const LnPre<BM * (BN / 8) / NT>& pre) {
   constexpr int LDC = BN * 4 + 16;
   constexpr int CPR = BN / 8;            // lanes per row (8 columns each)
   constexpr int IT = BM * CPR / NT;      // rows per thread
@@ -633,20 +661,6 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
 #pragma unroll
   for (int it = 0; it < IT; ++it) z_v[it] = pre.z_v[it];
   const float* g = pre.g;
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int r = wr * TM + i * 16 + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int c = wc * TN + j * 16 + 4 * (lane >> 4);
-      float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      if constexpr (!BWD) {
-        const float4 b = *reinterpret_cast<const float4*>(p.bias + n0 + c);
-        v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
-      }
-      *reinterpret_cast<float4*>(smem + r * LDC + c * 4) = v;
-    }
-  }
   __syncthreads();
   const bool drop = L.thr != 0;
   const uint32_t seed = drop ? hash32(L.seed_ptr[0], L.site) : 0u;
@@ -825,6 +839,94 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
     __syncthreads();
     flush(1, 2);
   }
+}
+
+template <int BM, int BN, int TM, int TN, bool BWD, int NT>
+DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int tm, int tn,
+                     int wr, int wc, int lane, int tid, const LnPre<BM * (BN / 8) / NT>& pre) {
+  ln_park<BM, BN, TM, TN, BWD>(p, acc, smem, tn * BN, wr, wc, lane);
+  ln_finish<BM, BN, BWD, NT>(p, smem, tm, tn, lane, tid, pre);
+}
+
+// ---------------------------------------------------------------- two-K-half LayerNorm tiles
+// gemm_ln2_kernel: the blocks s = 0, 1 of a pair each run HALF of the K loop of one 128 x 128
+// product tile (twice the MFMA work per staged byte of a 128 x 64 tile, half the K steps), then
+// trade the fp32 partial of the 64-column half they do not finish: block s finishes columns
+// [64 s, 64 s + 64) -- LayerNorm tile tn = 2 tnp + s of the plain 128 x 64 layout, so the
+// row-statistics exchange and everything after it is ln_finish's.  Wave (wr, wc) holds rows
+// 32 wr.. and columns 64 wc.. of the product (TM = 32, TN = 64); the waves with wc != s send,
+// the partner's waves with the same (wr, wc) receive -- the same fragment layout, so the sum is
+// element by element, no shuffles.  Final = own + partner's partial in both blocks: the same
+// IEEE sum either way (addition commutes), independent of timing.
+// Hand-off (cdna_hip_programming.md Guideline 16, write-through form; one block per CU): the
+// payload goes out with 16-byte sc1 (write-through) stores, every storing wave drains them
+// (vmcnt(0)), a workgroup barrier, then ONE lane stores the {tag, 1} flag granule with an
+// agent-scope atomic store; each receiving wave polls the partner's flag with agent-scope atomic
+// loads and reads the payload with sc1 loads only after its own poll has matched.  The tag is the
+// LayerNorm exchange's (epoch * FD_LN_XSITES + xsite + 1): stale flags never match.
+constexpr uint32_t LN2_SC1 = 16;  // buffer-op cache policy: sc1 (write-through / L1 bypass)
+
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
+DEV __amdgpu_buffer_rsrc_t ln2_rsrc(const FdLnEpi& L) {
+  // the whole exchange buffer, from kernel arguments only (wave-uniform: no waterfall loops);
+  // every per-block / per-wave part of an address goes in the 32-bit voffset
+  return __builtin_amdgcn_make_buffer_rsrc(L.xbuf, 0, 0x7fffffff, 0x00020000);
+}
+template <int MI, int NI>
+constexpr int ln2_wave_bytes() { return MI * NI * 64 * 16; }
+
+template <int MI, int NI>
+DEV void ln2_send(const GemmParams& p, const f32x4 (&acc)[MI][NI], int pair, int s, int wr, int wc, int lane,
+                  uint32_t tag) {
+  const FdLnEpi& L = p.ln;
+  if (wc != s) {  // these columns are the partner's
+    const __amdgpu_buffer_rsrc_t rs = ln2_rsrc(L);
+    const int base = ((pair * 2 + s) * 4 + wr) * ln2_wave_bytes<MI, NI>() + lane * 16;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, acc[i][j]), rs,
+                                               base + (i * NI + j) * 64 * 16, 0, LN2_SC1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its own stores
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(L.xflag + pair * 2 + s, ((uint64_t)tag << 32) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int MI, int NI>
+DEV void ln2_recv(const GemmParams& p, f32x4 (&acc)[MI][NI], int pair, int s, int wc, int wr, int lane,
+                  uint32_t tag) {
+  const FdLnEpi& L = p.ln;
+  if (wc != s) return;
+  uint64_t* fl = L.xflag + pair * 2 + (1 - s);
+  const uint32_t want = (p.diag & 64) ? tag + 1u : tag;
+  const uint64_t t0 = wall_clock64();
+  for (;;) {
+    const uint64_t f = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(f >> 32) == want) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > 25000000ull) {  // 0.25 s: never in a healthy launch
+      if (lane == 0) __hip_atomic_fetch_or(L.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
+  const __amdgpu_buffer_rsrc_t rs = ln2_rsrc(L);
+  const int base = ((pair * 2 + (1 - s)) * 4 + wr) * ln2_wave_bytes<MI, NI>() + lane * 16;
+  f32x4 other[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      other[i][j] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (i * NI + j) * 64 * 16, 0, LN2_SC1));
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = acc[i][j] + other[i][j];
 }
 
 // Scheduling hints for one K tile: the first 32-deep fragment set's ds_reads,
@@ -1107,6 +1209,18 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
       __syncthreads();
       f32_epilogue<TM, BN, 64 * NW>(p, smem, LDC, m0 + band * TM, n0, tid);
     }
+  } else if constexpr (EpiTraits<EPI, BM, BN>::LN2) {
+    static_assert(BM == 128 && BN == 128 && TM == 32 && TN == 64, "two-K-half LayerNorm tile");
+    constexpr bool BWD2 = EPI == EPI_LN2_BWD;
+    const int s = p.ln2_half, tn_ln = 2 * tn + s, pair = tm * (p.N / BN) + tn;
+    const uint32_t tag =
+        (uint32_t)__hip_atomic_load(p.ln.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * FD_LN_XSITES + p.ln.xsite + 1u;
+    ln2_send<MI, NI>(p, acc, pair, s, wr, wc, lane, tag);  // (its barrier: no wave still reads a ring slot)
+    // this block's LayerNorm operands in flight while the partner's partial arrives
+    const auto pre = ln_prefetch<128, 64, BWD2, 64 * NW>(p, tm, tn_ln, tid);
+    ln2_recv<MI, NI>(p, acc, pair, s, wc, wr, lane, tag);
+    if (wc == s) ln_park<128, 64, TM, TN, BWD2>(p, acc, smem, tn_ln * 64, wr, 0, lane);
+    ln_finish<128, 64, BWD2, 64 * NW>(p, smem, tm, tn_ln, lane, tid, pre);
   } else if constexpr (EpiTraits<EPI, BM, BN>::LN) {
     if (LNPF && lnpf) {
       wait_vm<0>();     // this wave's epilogue DMAs have landed ...
@@ -1164,6 +1278,31 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_ln_kernel(GemmParams p) 
   const int tiles_n = p.N / BN;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   gemm_tile_at<BM, BN, true, BKM, EPI, WM, WN, S>(p, lid / tiles_n, lid % tiles_n, smem);
+#if FD_GEMM_STAMPS
+  __syncthreads();
+  FD_STAMP(5);
+#endif
+}
+
+// Two-K-half LayerNorm-fused GEMM (EPI_LN2 / EPI_LN2_BWD): block pair (lid / 2) owns the 128 x 128
+// product tile pair, block lid % 2 its K half (A / B offset by that half; one K loop of K / 2).
+// The pair's blocks are consecutive logical ids (one XCD after the remap); the row block's 12
+// LayerNorm tiles stay consecutive.  One resident round (one 128 KiB block per CU).
+template <int EPI, bool BKM>
+__global__ __launch_bounds__(512, 1) void gemm_ln2_kernel(GemmParams p) {
+  using G = GemmCfg<128, 128, true, BKM, EPI, 4, 2, 4>;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  FD_STAMP(0);
+  stamp_hwid();
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int pair = lid >> 1, s = lid & 1, tiles_n2 = p.N / 128;
+  GemmParams q = p;
+  const int kh = p.K / 2;
+  q.A = p.A + (size_t)s * kh;
+  q.B = BKM ? p.B + (size_t)s * kh : p.B + (size_t)s * kh * p.ldb;
+  q.k_split = kh;
+  q.ln2_half = s;
+  gemm_tile_at<128, 128, true, BKM, EPI, 4, 2, 4>(q, pair / tiles_n2, pair % tiles_n2, smem);
 #if FD_GEMM_STAMPS
   __syncthreads();
   FD_STAMP(5);
@@ -1460,6 +1599,7 @@ int pick_cfg(int kind, int M, int N, int K) {
     return K >= 2048 ? 0 : 8;
   }
   if (kind == 1) {  // NN dX (on the weight W itself: MN-major B through the transposing LDS reads)
+    if (M <= 64 && N % 64 == 0 && smallm_tiles()) return 13;  // (as for NT: no half-empty 128-row tiles)
     // the NT rules above, measured equal per configuration (round 4, profiles/r4_ab_dx_layouts.txt:
     // the LayerNorm-fused dX reads W as fast as W^T on cfg 24)
     if (N % 192 == 0 && N >= 3072 && M >= 3584) return 3;
@@ -1852,6 +1992,11 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
     static const int env = [] { const char* e = getenv("FD_GEMM_LN_CFG"); return e ? atoi(e) : -1; }();
     id = env >= 0 ? env : (M <= 64 && smallm_tiles() ? 13 : 24);
   }
+  // two-K-half tiles (gemm_ln2_kernel): FD_GEMM_LN2_MINK (default 2048) <= K, needs the exchange
+  // buffers; the grid stays one resident round (2 blocks per 128 x 128 tile = one per 128 x 64)
+  static const int ln2_mink = [] { const char* e = getenv("FD_GEMM_LN2_MINK"); return e ? atoi(e) : 2048; }();
+  const bool ln2 = cfg < 0 && id == 24 && ln2_mink > 0 && K >= ln2_mink && K % 128 == 0 && N % 128 == 0 &&
+                   ln->xbuf && ln->xflag;
   const int bm = id == 13 ? 64 : 128, bn = 64;
   if (N / bn > LN_MAXK * (bn / 8)) return -2;
   {
@@ -1882,6 +2027,12 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   const int tiles_m = (M + bm - 1) / bm;
   const dim3 grid(tiles_m * (N / bn));
   auto go = [&](auto kern, int threads) { hipLaunchKernelGGL(kern, grid, dim3(threads), 0, st, p); };
+  if (ln2) {  // (same grid: 2 blocks per 128 x 128 product tile = one per 128 x 64 LayerNorm tile)
+    if (b_mn) go(gemm_ln2_kernel<EPI_LN2_BWD, false>, 512);
+    else if (bwd) go(gemm_ln2_kernel<EPI_LN2_BWD, true>, 512);
+    else go(gemm_ln2_kernel<EPI_LN2, true>, 512);
+    return tiles_m;
+  }
 #define FD_LN_CASE(ID, BM_, BN_, WM_, WN_, S_)                                          \
   case ID:                                                                             \
     if (b_mn) go(gemm_ln_kernel<BM_, BN_, EPI_LN_BWD, WM_, WN_, S_, false>, 64 * WM_ * WN_); \

@@ -53,10 +53,12 @@ EPI_LN, EPI_LN_BWD = 6, 7
 # the whole K loop on the dozen CUs its 64 x 64 tiles cover.  FD_SPLITK_SMALLM=0: off.
 import os as _os
 SPLITK_MAX_M = 64 if _os.environ.get("FD_SPLITK_SMALLM", "1") != "0" else 0
+# FD_SPLITK_MINK: split only problems with K >= this (the shorter ones run single-pass)
+SPLITK_MIN_K = int(_os.environ.get("FD_SPLITK_MINK", "0"))
 
 
 def _splitk_ok(M: int, N: int, K: int) -> bool:
-    return 0 < M <= SPLITK_MAX_M and N % 64 == 0 and K % 64 == 0
+    return 0 < M <= SPLITK_MAX_M and N % 64 == 0 and K % 64 == 0 and K >= SPLITK_MIN_K
 
 
 def _splitk(epi, x, wt, y, **kw):
@@ -421,12 +423,22 @@ def _ln_state(device, M: int, N: int):
         # the epoch survives a regrow: a granule tag must never repeat on the same state
         epoch = st[1] if st is not None else torch.zeros(2, dtype=torch.int32, device=device)
         err = st[2] if st is not None else torch.zeros(1, dtype=torch.int32, device=device)
-        st = (torch.zeros(2 * (rows + 128) * (N // 64), dtype=torch.int64, device=device), epoch, err, rows)
+        # (+ LN2_FLAGS granules at the tail: the two-K-half tiles' exchange flags, csrc/binding.cpp)
+        st = (torch.zeros(2 * (rows + 128) * (N // 64) + LN2_FLAGS, dtype=torch.int64, device=device), epoch, err,
+              rows)
         _WS[key] = st
     return st[:3]
 
 
 LN_XSITES = 128  # csrc/kernels/adam_epi.h FD_LN_XSITES: exchange call sites per epoch
+LN2_FLAGS = 512  # csrc/binding.cpp gemm_ln: flag granules of the two-K-half tiles
+# Two-K-half LayerNorm-fused GEMMs (csrc/kernels/gemm.hip gemm_ln2_kernel, K >= FD_GEMM_LN2_MINK):
+# the fp32 partial-tile exchange buffer (FD_LN2=0: never passed, the one-pass kernels run)
+LN2 = _os.environ.get("FD_LN2", "1") != "0"
+
+
+def _ln2_xbuf(device):
+    return workspace(device, "ln2_xbuf", 128 * 2 * 8192) if LN2 else None
 
 
 def ln_xsite(layer: int, which: int, backward: bool) -> int:
@@ -551,7 +563,7 @@ def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, k
     stats, cnt, err = _ln_state(x.device, M, N)
     xs = _xsite(x.device, N, xsite)
     ext().gemm_ln(False, x, w, y, b, res, gamma, beta, mean, rstd, z, None, None, stats, cnt, err, eps, seed, site,
-                  thr, sc, row_map if thr else None, LN_CFG, xs)
+                  thr, sc, row_map if thr else None, LN_CFG, xs, False, _ln2_xbuf(x.device))
     return y, z, mean, rstd
 
 
@@ -582,7 +594,7 @@ def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, see
     stats, cnt, err = _ln_state(a.device, M, N)
     xs = _xsite(a.device, N, xsite)
     nblk = ext().gemm_ln(True, a, wt, dz, None, res, gamma, None, mean, rstd, z, dx, ws, stats, cnt, err, 0.0, seed,
-                         site, thr, sc, row_map if thr else None, LN_CFG, xs, b_mn)
+                         site, thr, sc, row_map if thr else None, LN_CFG, xs, b_mn, _ln2_xbuf(a.device))
     job = (ws, [dgamma, dbeta, dbias], nblk, 3 * N, N, accumulate)
     if jobs is not None:
         jobs.append(job)

@@ -147,6 +147,39 @@ def test_linear_dx_ln_bwd(M, K, p, defer, ln_cfg):
     assert state_clean(M)
 
 
+@pytest.mark.parametrize("bwd,b_mn", [(False, False), (True, False), (True, True)])
+def test_two_k_half_tiles_match_one_pass(bwd, b_mn, monkeypatch):
+    """K >= FD_GEMM_LN2_MINK: two blocks per 128 x 128 product tile run half the K loop each and
+    trade fp32 column-half partials through write-through stores and a tagged flag
+    (gemm.hip gemm_ln2_kernel).  Equal to the one-pass kernel up to fp32 summation order,
+    bitwise repeatable (the pair's sum commutes), no exchange timeout."""
+    M, K, p = 2600, 3072, 0.1
+    gamma, beta = affine(31)
+    b = (torch.randn(D, generator=torch.Generator().manual_seed(32)) * 0.1).to(DEV)
+    res = bf(M, D, seed=33)
+    if not bwd:
+        x, w = bf(M, K, seed=34), bf(D, K, scale=0.03, seed=35)
+        run = lambda: kn.linear_ln_fwd(x, w, b, res, gamma, beta, 1e-12, seed_t(9), 33, p)[:2]
+    else:
+        x2, w2 = bf(M, D, seed=36), bf(D, D, scale=0.03, seed=37)
+        _, z, mean, rstd = kn.linear_ln_fwd(x2, w2, b, res, gamma, beta, 1e-12, seed_t(9), 33, p)
+        a = bf(M, K, scale=0.5, seed=38)
+        wt = bf(K, D, scale=0.03, seed=39) if b_mn else bf(D, K, scale=0.03, seed=39)
+        sinks = [torch.zeros(D, device=DEV) for _ in range(3)]
+        run = lambda: kn.linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, *sinks, seed_t(9), 33, p,
+                                          b_mn=b_mn) + (sinks[0].clone(),)
+    monkeypatch.setattr(kn, "LN2", True)
+    r1 = [t.clone() for t in run()]
+    r2 = [t.clone() for t in run()]
+    monkeypatch.setattr(kn, "LN2", False)
+    r0 = [t.clone() for t in run()]
+    torch.cuda.synchronize()
+    for t1, t2, t0 in zip(r1, r2, r0):
+        assert torch.equal(t1, t2)
+        assert rel_err(t1, t0) < 2e-2
+    assert state_clean(M)
+
+
 def test_many_launches_and_graph_replay_rearm_counters():
     """Standalone launches start a fresh exchange epoch each (graph replays re-run the advance);
     results are bitwise reproducible across launches (fixed-order merge)."""

@@ -44,7 +44,9 @@ def _frel(a, b):
 def test_pruned_last_block_matches_full(packed, B, empty, splitk, monkeypatch):
     from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
     if not splitk:
+        # (bitwise: the same one-pass kernels in both arms -- no split-K, no two-K-half LN tiles)
         monkeypatch.setattr(K, "SPLITK_MAX_M", 0)
+        monkeypatch.setattr(K, "LN2", False)
     cfg = DistilBertConfig(n_layers=3)
     outs = []
     for prune in (True, False):
@@ -79,6 +81,7 @@ def test_pruned_last_block_matches_full(packed, B, empty, splitk, monkeypatch):
 def test_pruned_eval_logits_match(monkeypatch):
     from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
     monkeypatch.setattr(K, "SPLITK_MAX_M", 0)  # (bitwise: the same one-pass kernels in both arms)
+    monkeypatch.setattr(K, "LN2", False)
     cfg = DistilBertConfig(n_layers=2)
     res = []
     for prune in (True, False):
@@ -96,6 +99,7 @@ def test_pruned_graph_training_tracks_full(splitk, monkeypatch):
     from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
     if not splitk:
         monkeypatch.setattr(K, "SPLITK_MAX_M", 0)
+        monkeypatch.setattr(K, "LN2", False)
     cfg = DistilBertConfig(n_layers=2)
     models, steps = [], []
     for prune in (True, False):
