@@ -1290,7 +1290,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_ln_kernel(GemmParams p) 
 // LayerNorm tiles stay consecutive.  One resident round (one 128 KiB block per CU).
 template <int EPI, bool BKM>
 __global__ __launch_bounds__(512, 1) void gemm_ln2_kernel(GemmParams p) {
-  using G = GemmCfg<128, 128, true, BKM, EPI, 4, 2, 4>;
+  constexpr int S = 4;
+  using G = GemmCfg<128, 128, true, BKM, EPI, 4, 2, S>;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   FD_STAMP(0);
   stamp_hwid();
@@ -1302,7 +1303,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ln2_kernel(GemmParams p) {
   q.B = BKM ? p.B + (size_t)s * kh : p.B + (size_t)s * kh * p.ldb;
   q.k_split = kh;
   q.ln2_half = s;
-  gemm_tile_at<128, 128, true, BKM, EPI, 4, 2, 4>(q, pair / tiles_n2, pair % tiles_n2, smem);
+  gemm_tile_at<128, 128, true, BKM, EPI, 4, 2, S>(q, pair / tiles_n2, pair % tiles_n2, smem);
 #if FD_GEMM_STAMPS
   __syncthreads();
   FD_STAMP(5);
@@ -2028,6 +2029,8 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   const dim3 grid(tiles_m * (N / bn));
   auto go = [&](auto kern, int threads) { hipLaunchKernelGGL(kern, grid, dim3(threads), 0, st, p); };
   if (ln2) {  // (same grid: 2 blocks per 128 x 128 product tile = one per 128 x 64 LayerNorm tile)
+    // (4 ring slots of 32 KiB; the whole 160 KiB as 5 slots measured slower: 1.630 vs 1.623 ms,
+    //  profiles/r5_rejected_ab.txt)
     if (b_mn) go(gemm_ln2_kernel<EPI_LN2_BWD, false>, 512);
     else if (bwd) go(gemm_ln2_kernel<EPI_LN2_BWD, true>, 512);
     else go(gemm_ln2_kernel<EPI_LN2, true>, 512);
