@@ -502,9 +502,10 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
   constexpr int64_t LN2_FLAGS = 512;
   if (xbuf.has_value() && xbuf->defined()) {
     need(*xbuf, at::kFloat, "xbuf");
-    const int64_t pairs = ((M + 127) / 128) * (N / 128);
-    if (xbuf->numel() >= pairs * 2 * 8192 && pairs * 2 <= LN2_FLAGS &&
-        stats.numel() >= 2 * (M + 128) * (N / 64) + LN2_FLAGS) {
+    // (the launcher picks 128- or 256-row tiles: room for either)
+    const int64_t pairs = ((M + 127) / 128) * (N / 128), pairs256 = ((M + 255) / 256) * (N / 128);
+    if (xbuf->numel() >= std::max(pairs * 2 * 8192, pairs256 * 2 * 16384) && pairs * 2 <= LN2_FLAGS &&
+        stats.numel() >= 2 * (M + 256) * (N / 64) + LN2_FLAGS) {
       ln.xbuf = xbuf->data_ptr<float>();
       ln.xflag = reinterpret_cast<uint64_t*>(stats.data_ptr()) + (stats.numel() - LN2_FLAGS);
     }

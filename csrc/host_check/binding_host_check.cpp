@@ -203,10 +203,12 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   hc::span(ln->stats, tm * (N / 64) * 2 * bm * 8, "gemm_ln stats");
   hc::span(ln->cnt, 4, "gemm_ln cnt");
   hc::span(ln->err, 4, "gemm_ln err");
-  if (ln->xbuf) {  // two-K-half tiles: pairs x 2 x 32 KiB of partials, pairs x 2 flag granules
-    const long long pairs = tm * (N / 128);
-    hc::span(ln->xbuf, pairs * 2 * 32768, "gemm_ln xbuf");
+  if (ln->xbuf) {  // two-K-half tiles: pairs x 2 x 32 (128-row) / 64 KiB (256-row) of partials,
+                   // pairs x 2 flag granules; the 256-row tiles' statistics rows
+    const long long pairs = tm * (N / 128), tm256 = (M + 255) / 256;
+    hc::span(ln->xbuf, std::max(pairs * 2 * 32768, tm256 * (N / 128) * 2 * 65536), "gemm_ln xbuf");
     hc::span(ln->xflag, pairs * 2 * 8, "gemm_ln xflag");
+    hc::span(ln->stats, tm256 * (N / 64) * 2 * 256 * 8, "gemm_ln stats (256-row tiles)");
   }
   if (bwd) {
     hc::span(ln->z, mn * 2, "gemm_ln z");

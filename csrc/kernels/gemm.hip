@@ -1210,17 +1210,17 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
       f32_epilogue<TM, BN, 64 * NW>(p, smem, LDC, m0 + band * TM, n0, tid);
     }
   } else if constexpr (EpiTraits<EPI, BM, BN>::LN2) {
-    static_assert(BM == 128 && BN == 128 && TM == 32 && TN == 64, "two-K-half LayerNorm tile");
+    static_assert((BM == 128 || BM == 256) && BN == 128 && WM == 4 && TN == 64, "two-K-half LayerNorm tile");
     constexpr bool BWD2 = EPI == EPI_LN2_BWD;
     const int s = p.ln2_half, tn_ln = 2 * tn + s, pair = tm * (p.N / BN) + tn;
     const uint32_t tag =
         (uint32_t)__hip_atomic_load(p.ln.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * FD_LN_XSITES + p.ln.xsite + 1u;
     ln2_send<MI, NI>(p, acc, pair, s, wr, wc, lane, tag);  // (its barrier: no wave still reads a ring slot)
     // this block's LayerNorm operands in flight while the partner's partial arrives
-    const auto pre = ln_prefetch<128, 64, BWD2, 64 * NW>(p, tm, tn_ln, tid);
+    const auto pre = ln_prefetch<BM, 64, BWD2, 64 * NW>(p, tm, tn_ln, tid);
     ln2_recv<MI, NI>(p, acc, pair, s, wc, wr, lane, tag);
-    if (wc == s) ln_park<128, 64, TM, TN, BWD2>(p, acc, smem, tn_ln * 64, wr, 0, lane);
-    ln_finish<128, 64, BWD2, 64 * NW>(p, smem, tm, tn_ln, lane, tid, pre);
+    if (wc == s) ln_park<BM, 64, TM, TN, BWD2>(p, acc, smem, tn_ln * 64, wr, 0, lane);
+    ln_finish<BM, 64, BWD2, 64 * NW>(p, smem, tm, tn_ln, lane, tid, pre);
   } else if constexpr (EpiTraits<EPI, BM, BN>::LN) {
     if (LNPF && lnpf) {
       wait_vm<0>();     // this wave's epilogue DMAs have landed ...
@@ -1288,10 +1288,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_ln_kernel(GemmParams p) 
 // product tile pair, block lid % 2 its K half (A / B offset by that half; one K loop of K / 2).
 // The pair's blocks are consecutive logical ids (one XCD after the remap); the row block's 12
 // LayerNorm tiles stay consecutive.  One resident round (one 128 KiB block per CU).
-template <int EPI, bool BKM>
+// BM = 256 (256 x 128 product tiles, 256 x 64 LayerNorm tiles; 3 ring slots of 48 KiB): the
+// larger batches (e.g. seq256 bs64, ~5.1 k packed rows) whose 128-row grid would exceed one round.
+template <int EPI, bool BKM, int BM = 128>
 __global__ __launch_bounds__(512, 1) void gemm_ln2_kernel(GemmParams p) {
-  constexpr int S = 4;
-  using G = GemmCfg<128, 128, true, BKM, EPI, 4, 2, S>;
+  constexpr int S = BM == 128 ? 4 : 3;
+  using G = GemmCfg<BM, 128, true, BKM, EPI, 4, 2, S>;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   FD_STAMP(0);
   stamp_hwid();
@@ -1303,7 +1305,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ln2_kernel(GemmParams p) {
   q.B = BKM ? p.B + (size_t)s * kh : p.B + (size_t)s * kh * p.ldb;
   q.k_split = kh;
   q.ln2_half = s;
-  gemm_tile_at<128, 128, true, BKM, EPI, 4, 2, S>(q, pair / tiles_n2, pair % tiles_n2, smem);
+  gemm_tile_at<BM, 128, true, BKM, EPI, 4, 2, S>(q, pair / tiles_n2, pair % tiles_n2, smem);
 #if FD_GEMM_STAMPS
   __syncthreads();
   FD_STAMP(5);
@@ -1996,9 +1998,10 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   // two-K-half tiles (gemm_ln2_kernel): FD_GEMM_LN2_MINK (default 2048) <= K, needs the exchange
   // buffers; the grid stays one resident round (2 blocks per 128 x 128 tile = one per 128 x 64)
   static const int ln2_mink = [] { const char* e = getenv("FD_GEMM_LN2_MINK"); return e ? atoi(e) : 2048; }();
-  const bool ln2 = cfg < 0 && id == 24 && ln2_mink > 0 && K >= ln2_mink && K % 128 == 0 && N % 128 == 0 &&
-                   ln->xbuf && ln->xflag;
-  const int bm = id == 13 ? 64 : 128, bn = 64;
+  const bool ln2_ok = cfg < 0 && id == 24 && K % 128 == 0 && N % 128 == 0 && ln->xbuf && ln->xflag;
+  bool ln2 = ln2_ok && ln2_mink > 0 && K >= ln2_mink;
+  int bm = id == 13 ? 64 : 128;
+  const int bn = 64;
   if (N / bn > LN_MAXK * (bn / 8)) return -2;
   {
     // one resident round: no more tiles than CUs (cfg 24: one 147 KiB block per CU)
@@ -2010,7 +2013,13 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
       return n;
     }();
     const int max_tiles = std::min(LN_MAX_TILES, cus > 0 ? cus : LN_MAX_TILES);
-    if (((M + bm - 1) / bm) * (N / bn) > max_tiles) return -4;  // caller: the unfused kernels
+    if (((M + bm - 1) / bm) * (N / bn) > max_tiles) {
+      // too many 128-row tiles for one round: 256-row two-K-half tiles (any K), else the caller
+      // takes the unfused kernels
+      if (!ln2_ok || ((M + 255) / 256) * (N / bn) > max_tiles) return -4;
+      bm = 256;
+      ln2 = true;
+    }
   }
   GemmParams p{};
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)Bt; p.C = C;
@@ -2031,9 +2040,15 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   if (ln2) {  // (same grid: 2 blocks per 128 x 128 product tile = one per 128 x 64 LayerNorm tile)
     // (4 ring slots of 32 KiB; the whole 160 KiB as 5 slots measured slower: 1.630 vs 1.623 ms,
     //  profiles/r5_rejected_ab.txt)
-    if (b_mn) go(gemm_ln2_kernel<EPI_LN2_BWD, false>, 512);
-    else if (bwd) go(gemm_ln2_kernel<EPI_LN2_BWD, true>, 512);
-    else go(gemm_ln2_kernel<EPI_LN2, true>, 512);
+    if (bm == 256) {
+      if (b_mn) go(gemm_ln2_kernel<EPI_LN2_BWD, false, 256>, 512);
+      else if (bwd) go(gemm_ln2_kernel<EPI_LN2_BWD, true, 256>, 512);
+      else go(gemm_ln2_kernel<EPI_LN2, true, 256>, 512);
+    } else {
+      if (b_mn) go(gemm_ln2_kernel<EPI_LN2_BWD, false>, 512);
+      else if (bwd) go(gemm_ln2_kernel<EPI_LN2_BWD, true>, 512);
+      else go(gemm_ln2_kernel<EPI_LN2, true>, 512);
+    }
     return tiles_m;
   }
 #define FD_LN_CASE(ID, BM_, BN_, WM_, WN_, S_)                                          \

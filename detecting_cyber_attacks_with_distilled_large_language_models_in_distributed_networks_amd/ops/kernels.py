@@ -424,7 +424,7 @@ def _ln_state(device, M: int, N: int):
         epoch = st[1] if st is not None else torch.zeros(2, dtype=torch.int32, device=device)
         err = st[2] if st is not None else torch.zeros(1, dtype=torch.int32, device=device)
         # (+ LN2_FLAGS granules at the tail: the two-K-half tiles' exchange flags, csrc/binding.cpp)
-        st = (torch.zeros(2 * (rows + 128) * (N // 64) + LN2_FLAGS, dtype=torch.int64, device=device), epoch, err,
+        st = (torch.zeros(2 * (rows + 256) * (N // 64) + LN2_FLAGS, dtype=torch.int64, device=device), epoch, err,
               rows)
         _WS[key] = st
     return st[:3]
@@ -438,7 +438,8 @@ LN2 = _os.environ.get("FD_LN2", "1") != "0"
 
 
 def _ln2_xbuf(device):
-    return workspace(device, "ln2_xbuf", 128 * 2 * 8192) if LN2 else None
+    # (<= 128 tile pairs of 2 x 128 x 64 fp32 partials, or of 2 x 256 x 64 for the 256-row tiles)
+    return workspace(device, "ln2_xbuf", 128 * 2 * 16384) if LN2 else None
 
 
 def ln_xsite(layer: int, which: int, backward: bool) -> int:
@@ -524,6 +525,8 @@ def ln_fusable(M: int, N: int, concurrent_collectives: bool = False) -> bool:
     if _SHARED_DEVICE or concurrent_collectives:
         return False
     tiles = ((M + 127) // 128) * (N // 64)
+    if LN2 and N % 128 == 0:  # (gemm.hip fd_gemm_ln: 256-row two-K-half tiles past 128-row round)
+        tiles = min(tiles, ((M + 255) // 256) * (N // 64))
     return N % 64 == 0 and N <= 2048 and tiles <= min(LN_MAX_TILES, _cu_count())
 
 

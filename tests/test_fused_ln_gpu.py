@@ -78,16 +78,52 @@ def test_linear_ln_fwd(M, K, p, ln_cfg):
     assert state_clean(M)
 
 
-def test_fused_grid_limited_to_one_resident_round():
+def test_fused_grid_limited_to_one_resident_round(monkeypatch):
     """Row blocks wait on each other's statistics, so the fused grid must fit one round of the
-    CUs (21 row blocks x 12 column tiles at N = 768); a larger M is refused by the launcher and
-    the model takes the separate LayerNorm kernels (ln_fusable)."""
-    assert kn.ln_fusable(2688, D) and not kn.ln_fusable(2689, D) and not kn.ln_fusable(4096, D)
-    M, K = 4096, 768
+    CUs: 21 row blocks x 12 column tiles of 128 x 64 at N = 768, or -- with the two-K-half
+    kernels -- 21 row blocks of 256-row tiles.  A larger M is refused by the launcher and the model
+    takes the separate LayerNorm kernels (ln_fusable)."""
+    M, K = 6000, 768
     x, w, res = bf(M, K, seed=1), bf(D, K, scale=0.03, seed=2), bf(M, D, seed=3)
     gamma, beta = affine(5)
+    monkeypatch.setattr(kn, "LN2", False)
+    assert kn.ln_fusable(2688, D) and not kn.ln_fusable(2689, D) and not kn.ln_fusable(4096, D)
+    with pytest.raises(RuntimeError):
+        kn.linear_ln_fwd(x[:4096], w, torch.zeros(D, device=DEV), res[:4096], gamma, beta, 1e-12, seed_t(9), 33, 0.0)
+    monkeypatch.setattr(kn, "LN2", True)
+    assert kn.ln_fusable(4096, D) and kn.ln_fusable(5376, D) and not kn.ln_fusable(5377, D)
     with pytest.raises(RuntimeError):
         kn.linear_ln_fwd(x, w, torch.zeros(D, device=DEV), res, gamma, beta, 1e-12, seed_t(9), 33, 0.0)
+
+
+@pytest.mark.parametrize("M,K,p", [(5000, 3072, 0.1), (5000, 768, 0.0), (4000, 2304, 0.1)])
+def test_256_row_two_k_half_tiles(M, K, p):
+    """Past one round of 128-row tiles (the seq256 bs64 distillation batch: ~5.1 k packed rows) the
+    fused kernels run 256-row two-K-half tiles: forward and backward (both B layouts) against fp32
+    references and the unfused kernels."""
+    x, w, res = bf(M, K, seed=41), bf(D, K, scale=0.03, seed=42), bf(M, D, seed=43)
+    b = (torch.randn(D, generator=torch.Generator().manual_seed(44)) * 0.1).to(DEV)
+    gamma, beta = affine(45)
+    y, z, mean, rstd = kn.linear_ln_fwd(x, w, b, res, gamma, beta, 1e-12, seed_t(9), 33, p)
+    zr = R.dropout_ref(x.float() @ w.float().t() + b, p, 9, 33) + res.float()
+    assert rel_err(z, zr) < 1e-2
+    assert rel_err(y, F.layer_norm(zr, (D,), gamma, beta, 1e-12)) < 1e-2
+    y2, _, _ = kn.ln_fwd(kn.linear_fwd(x, w, b), res, gamma, beta, 1e-12, seed_t(9), 33, p)
+    assert rel_err(y, y2) < 2e-2
+    a = bf(M, K, scale=0.5, seed=46)
+    for b_mn in (False, True):
+        wt = bf(K, D, scale=0.03, seed=47) if b_mn else bf(D, K, scale=0.03, seed=47)
+        dgamma, dbeta, dbias = (torch.zeros(D, device=DEV) for _ in range(3))
+        dz, dx = kn.linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, seed_t(9), 33, p,
+                                     b_mn=b_mn)
+        dy = a.float() @ (wt.float() if b_mn else wt.float().t()) + res.float()
+        zf = z.float().requires_grad_(True)
+        gf, bf_ = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+        gz, gg, gb = torch.autograd.grad(F.layer_norm(zf, (D,), gf, bf_, 1e-12), [zf, gf, bf_], dy)
+        assert rel_err(dz, gz) < 2e-2
+        assert rel_err(dx, R.dropout_ref(gz, p, 9, 33)) < 2e-2
+        assert rel_err(dgamma, gg) < 1e-2 and rel_err(dbeta, gb) < 1e-2
+    assert state_clean(M)
 
 
 def test_linear_ln_fwd_packed_row_map():
