@@ -71,24 +71,30 @@ def main():
             site[0] = 0
         return site[0]
     nb_ln = ((M + 127) // 128) * (D // 64)
+    xbuf = kn.workspace(torch.device(dev), "ln2_xbuf", 128 * 2 * 16384)
     for rep in range(2):
-        for K in (768, 3072):
-            x, w, b = bf(M, K), bf(D, K, scale=0.03), torch.zeros(D, device=dev)
-            for _ in range(20):
-                ext().gemm_ln(False, x, w, y, b, res, gamma, beta, mean, rstd, z, None, None, stats, cnt, err, 1e-12,
-                              seed, 9, thr, sc, None, -1, xs())
-            torch.cuda.synchronize()
-            report(f"ln fwd K={K}", nb_ln, True)
-        for K in (3072, 2304):
-            a, wt = bf(M, K, scale=0.5), bf(D, K, scale=0.03)
-            w_mn = wt.t().contiguous()  # W [K][N]: the model's dX GEMMs read the weight MN-major
-            dz, dx = torch.empty_like(y), torch.empty_like(y)
-            for b_mn, B, tag in ((True, w_mn, "NN"), (False, wt, "NT")):
+        # two-K-half tiles (ln2: K >= 2048 with the exchange buffer) and the one-pass kernel;
+        # ln2 stamps: 2 = this block's half of the K loop done, 3 = partials traded + statistics published
+        for ln2 in (True, False):
+            xb = xbuf if ln2 else None
+            tg = "ln2" if ln2 else "ln"
+            for K in (768, 3072):
+                x, w, b = bf(M, K), bf(D, K, scale=0.03), torch.zeros(D, device=dev)
                 for _ in range(20):
-                    ext().gemm_ln(True, a, B, dz, None, res, gamma, None, mean, rstd, z, dx, cp, stats, cnt, err, 0.0,
-                                  seed, 9, thr, sc, None, -1, xs(), b_mn)
+                    ext().gemm_ln(False, x, w, y, b, res, gamma, beta, mean, rstd, z, None, None, stats, cnt, err,
+                                  1e-12, seed, 9, thr, sc, None, -1, xs(), False, xb)
                 torch.cuda.synchronize()
-                report(f"ln bwd {tag} K={K}", nb_ln, True)
+                report(f"{tg} fwd K={K}", nb_ln, True)
+            for K in (3072, 2304):
+                a, wt = bf(M, K, scale=0.5), bf(D, K, scale=0.03)
+                w_mn = wt.t().contiguous()  # W [K][N]: the model's dX GEMMs read the weight MN-major
+                dz, dx = torch.empty_like(y), torch.empty_like(y)
+                for b_mn, B, tag in ((True, w_mn, "NN"), (False, wt, "NT")):
+                    for _ in range(20):
+                        ext().gemm_ln(True, a, B, dz, None, res, gamma, None, mean, rstd, z, dx, cp, stats, cnt, err,
+                                      0.0, seed, 9, thr, sc, None, -1, xs(), b_mn, xb)
+                    torch.cuda.synchronize()
+                    report(f"{tg} bwd {tag} K={K}", nb_ln, True)
         for (N, K, epi, nm) in ((768, 768, 0, "o dX"), (2304, 768, 1, "qkv fwd"), (3072, 768, 2, "ffn1 fwd")):
             x, w, b = bf(M, K), bf(N, K, scale=0.03), torch.zeros(N, device=dev)
             out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
