@@ -1216,7 +1216,9 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
     const uint32_t tag =
         (uint32_t)__hip_atomic_load(p.ln.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * FD_LN_XSITES + p.ln.xsite + 1u;
     ln2_send<MI, NI>(p, acc, pair, s, wr, wc, lane, tag);  // (its barrier: no wave still reads a ring slot)
-    // this block's LayerNorm operands in flight while the partner's partial arrives
+    // this block's LayerNorm operands in flight while the partner's partial arrives (issued before
+    // the send instead, their latency joins the senders' drain and delays the flag: 1.619 vs
+    // 1.606 ms/step, profiles/r5_rejected_ab.txt)
     const auto pre = ln_prefetch<BM, 64, BWD2, 64 * NW>(p, tm, tn_ln, tid);
     ln2_recv<MI, NI>(p, acc, pair, s, wc, wr, lane, tag);
     if (wc == s) ln_park<BM, 64, TM, TN, BWD2>(p, acc, smem, tn_ln * 64, wr, 0, lane);
