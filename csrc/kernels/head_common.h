@@ -168,12 +168,27 @@ DEV void head_logits(const HeadArgs& a, int b, int lane, float& z0, float& z1) {
   z1 = y1[0];
 }
 
-// Row loss and dlogits (before the 1/B of the mean) of row b from its logits (needs labels).
-DEV void head_loss_grad(const HeadArgs& a, int b, float z0, float z1, float& loss, float& d0, float& d1) {
+// Row b's label and (distillation) teacher logits, loadable ahead of the logits' reductions.
+struct HeadRowIn {
+  int y;
+  float t0, t1;
+};
+DEV HeadRowIn head_row_in(const HeadArgs& a, int b) {
+  HeadRowIn r;
+  r.y = (int)a.labels[b];
+  r.t0 = a.tlogits ? a.tlogits[2 * b] : 0.f;
+  r.t1 = a.tlogits ? a.tlogits[2 * b + 1] : 0.f;
+  return r;
+}
+
+// Row loss and dlogits (before the 1/B of the mean) of a row from its logits and label / teacher
+// logits (head_row_in).
+DEV void head_loss_grad_in(const HeadArgs& a, const HeadRowIn& in, float z0, float z1, float& loss, float& d0,
+                           float& d1) {
 #pragma clang fp contract(off)
   const float mx = fmaxf(z0, z1);
   const float lse = mx + __logf(__expf(z0 - mx) + __expf(z1 - mx));
-  const int y = (int)a.labels[b];
+  const int y = in.y;
   const float p1 = __expf(z1 - lse), p0 = __expf(z0 - lse);
   loss = lse - (y ? z1 : z0);
   d0 = p0 - (y == 0);
@@ -181,7 +196,7 @@ DEV void head_loss_grad(const HeadArgs& a, int b, float z0, float z1, float& los
   if (a.tlogits) {
     // soft term at temperature T (2 classes): log-softmax of z / T and t / T
     const float iT = 1.f / a.kd_T;
-    const float s0 = z0 * iT, s1 = z1 * iT, t0 = a.tlogits[2 * b] * iT, t1 = a.tlogits[2 * b + 1] * iT;
+    const float s0 = z0 * iT, s1 = z1 * iT, t0 = in.t0 * iT, t1 = in.t1 * iT;
     const float ms = fmaxf(s0, s1), mt = fmaxf(t0, t1);
     const float ls = ms + __logf(__expf(s0 - ms) + __expf(s1 - ms));
     const float lt = mt + __logf(__expf(t0 - mt) + __expf(t1 - mt));
@@ -197,6 +212,9 @@ DEV void head_loss_grad(const HeadArgs& a, int b, float z0, float z1, float& los
   }
   d0 = d0 / a.B;
   d1 = d1 / a.B;
+}
+DEV void head_loss_grad(const HeadArgs& a, int b, float z0, float z1, float& loss, float& d0, float& d1) {
+  head_loss_grad_in(a, head_row_in(a, b), z0, z1, loss, d0, d1);
 }
 
 // Row b's outputs from its logits (lane 0 writes): logits, and with labels the row loss and dlogits.
@@ -221,9 +239,11 @@ DEV void head_row(const HeadArgs& a, int b, int lane) {
   head_row_out(a, b, lane, z0, z1);
 }
 
-DEV void loss_mean(const HeadArgs& a, int lane) {  // one wave; fixed order
+// rl: the row losses (a.row_loss, or the caller's LDS copy of them -- same values, same order)
+DEV void loss_mean(const HeadArgs& a, int lane, const float* rl = nullptr) {  // one wave; fixed order
+  if (!rl) rl = a.row_loss;
   float s = 0.f;
-  for (int b = lane; b < a.B; b += 64) s += a.row_loss[b];
+  for (int b = lane; b < a.B; b += 64) s += rl[b];
   s = wave_sum(s);
   if (lane == 0) {
     a.loss[0] = s / a.B;

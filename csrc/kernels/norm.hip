@@ -871,6 +871,7 @@ __global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
     const int cb = blockIdx.x - args.nlb;
     float* dl = lds;                        // [B][2] dlogits
     float* red = lds + 2 * ((h.B + 3) & ~3);  // [2 groups][2][8][32]
+    float* rl = red + 2 * 2 * HLB_GROUPS * HLB_COLS;  // [B] row losses (block 0's loss mean)
     const int sub = threadIdx.x >> 8, t = threadIdx.x & 255;
     const int c = t % HLB_COLS, grp = t / HLB_COLS;
     const int col = cb * 2 * HLB_COLS + sub * HLB_COLS + c;
@@ -883,6 +884,10 @@ __global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
     for (int u = 0; u < HLB_ROWS; ++u) xpre[u] = bf2f(h.hidden[cls_row(h, min(grp + u * HLB_GROUPS, h.B - 1)) * D + colc]);
     for (int b = w; b < h.B; b += 32) {  // rows b, b + 8, b + 16, b + 24 of this wave, interleaved
       const int rows[4] = {b, b + 8 < h.B ? b + 8 : -1, b + 16 < h.B ? b + 16 : -1, b + 24 < h.B ? b + 24 : -1};
+      // labels / teacher logits loaded beside the logits' operands (not behind the stores below)
+      HeadRowIn in[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) in[r] = head_row_in(h, rows[r] < 0 ? 0 : rows[r]);
       float z0[4], z1[4];
       head_logits_n<4>(h, rows, lane, z0, z1);
 #pragma unroll
@@ -890,11 +895,12 @@ __global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
         if (rows[r] < 0) continue;
         const int br = rows[r];
         float loss, d0, d1;
-        head_loss_grad(h, br, z0[r], z1[r], loss, d0, d1);
+        head_loss_grad_in(h, in[r], z0[r], z1[r], loss, d0, d1);
         if (lane == 0) {
           dl[2 * br] = d0;
           dl[2 * br + 1] = d1;
           if (cb == 0) {
+            rl[br] = loss;
             h.logits[2 * br] = z0[r];
             h.logits[2 * br + 1] = z1[r];
             h.row_loss[br] = loss;
@@ -904,8 +910,8 @@ __global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
         }
       }
     }
-    __syncthreads();  // dlogits in LDS; (block 0) every row loss written, workgroup-visible
-    if (cb == 0 && w == 0) loss_mean(h, lane);
+    __syncthreads();  // dlogits (and block 0's row losses) in LDS
+    if (cb == 0 && w == 0) loss_mean(h, lane, rl);
     float g0 = 0.f, g1 = 0.f;
     for (int b0 = grp; b0 < h.B; b0 += HLB_GROUPS * HLB_ROWS) {
       float x[HLB_ROWS];
@@ -970,6 +976,8 @@ __global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
     const int rows[2] = {rA < h.B ? rA : -1, rA + 1 < h.B ? rA + 1 : -1};
     HeadLoads<2> hlo;
     head_logits_load<2>(h, rows, lane, hlo);
+    const int mine = lane < HL ? 0 : 1;
+    const HeadRowIn in = head_row_in(h, rows[mine] < 0 ? 0 : rows[mine]);
     const float mean = a.mean[rr], rstd = a.rstd[rr];
     const bool empty = rr < h.B && empty_seq(h, rr);
     float xh[CH][8];
@@ -977,11 +985,10 @@ __global__ __launch_bounds__(512) void head_ln_bwd_kernel(HeadLnArgs args) {
     ln_load_sum(a, rr, hl, drop, seed, xh, keep);
     float z0[2] = {0.f, 0.f}, z1[2] = {0.f, 0.f};
     if (rows[0] >= 0) head_logits_finish<2>(h, rows, lane, hlo, z0, z1);
-    const int mine = lane < HL ? 0 : 1;
     float d0 = 0.f, d1 = 0.f;
     if (rows[mine] >= 0) {
       float loss;
-      head_loss_grad(h, rows[mine], z0[mine], z1[mine], loss, d0, d1);
+      head_loss_grad_in(h, in, z0[mine], z1[mine], loss, d0, d1);
     }
     if (row >= a.T) continue;  // (whole half-waves)
     const bool grad_row = row < h.B && !empty;
@@ -1109,7 +1116,7 @@ int fd_head_ln_bwd(const void* hidden, int B, int T, int D, const float* W, cons
   x.nlb = std::min(LN_GRID, (T + rows - 1) / rows);  // = ln_bwd's grid: the same partial rows
   if (nblk_out) *nblk_out = x.nlb;
   const size_t smem = std::max<size_t>((LN_BWD_THREADS / 64) * D * sizeof(float),
-                                       (2 * ((B + 3) & ~3) + 2 * 2 * HLB_GROUPS * HLB_COLS) * sizeof(float));
+                                       (2 * ((B + 3) & ~3) + 2 * 2 * HLB_GROUPS * HLB_COLS + B) * sizeof(float));
   hipLaunchKernelGGL(head_ln_bwd_kernel, dim3(x.nlb + D / (2 * HLB_COLS)), dim3(LN_BWD_THREADS), smem, st, x);
   return 0;
 }
