@@ -44,7 +44,8 @@ int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const
 int fd_gemm_ln_set_diag(int diag);
 int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, float* workspace,
                    long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
-                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, int b_mn, hipStream_t st);
+                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, const FdSkHead* hd,
+                   int b_mn, hipStream_t st);
 int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, int K, const float* bias,
                const void* res, int ldres, const FdLnEpi* ln, int cfg, int b_mn, hipStream_t st);
 int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* outs, const long long* numel,
@@ -530,7 +531,11 @@ std::vector<int64_t> gemm_splitk(int64_t epi, const at::Tensor& A, const at::Ten
                                  const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& dx,
                                  const c10::optional<at::Tensor>& colpart, double eps,
                                  const c10::optional<at::Tensor>& seed, int64_t site, int64_t thr, double dscale,
-                                 const c10::optional<at::Tensor>& row_map, bool b_mn = false) {
+                                 const c10::optional<at::Tensor>& row_map, bool b_mn = false,
+                                 const std::vector<at::Tensor>& head = {}, const std::vector<double>& head_f = {},
+                                 const c10::optional<at::Tensor>& head_dx = c10::nullopt,
+                                 const c10::optional<at::Tensor>& head_tlogits = c10::nullopt,
+                                 const c10::optional<at::Tensor>& head_own = c10::nullopt) {
   // b_mn: Bt is the weight W [K][N] itself (C = epi(A W); a dX GEMM without a W^T copy)
   need(A, at::kBFloat16, "A");
   need(Bt, at::kBFloat16, "Bt");
@@ -592,11 +597,59 @@ std::vector<int64_t> gemm_splitk(int64_t epi, const at::Tensor& A, const at::Ten
       if (has(row_map)) TORCH_CHECK(row_map->numel() >= M, "gemm_splitk: row_map needs M entries");
     }
   }
+  // the pruned step's head fused into the output-LayerNorm epilogue (splitk.hip sk_head_row):
+  // head = [W [2][N], bias [2], labels [B] int64, logits [B][2], dlogits [B][2], dz [M][N] bf16,
+  // colpart [M][3][N], hpart [M][2][N], dbpart [M][2], lpart [M], head seed int32],
+  // head_f = [site, thr, dscale, kd_T, kd_alpha, B]
+  FdSkHead hd{};
+  if (!head.empty()) {
+    TORCH_CHECK(epi == 6 && N == 768 && head.size() == 11 && head_f.size() == 6, "gemm_splitk head: arguments");
+    const int64_t Bh = (int64_t)head_f[5];
+    TORCH_CHECK(Bh > 0 && Bh <= M, "gemm_splitk head: B");
+    need(head[0], at::kFloat, "head W");
+    need(head[1], at::kFloat, "head bias");
+    need(head[2], at::kLong, "head labels");
+    for (int k : {3, 4, 6, 7, 8, 9}) need(head[k], at::kFloat, "head fp32 output");
+    need(head[5], at::kBFloat16, "head dz");
+    TORCH_CHECK(head[0].numel() == 2 * N && head[1].numel() == 2 && head[2].numel() == Bh &&
+                    head[3].numel() == 2 * Bh && head[4].numel() == 2 * Bh && head[5].numel() == M * N &&
+                    head[6].numel() >= M * 3 * N && head[7].numel() >= M * 2 * N && head[8].numel() >= M * 2 &&
+                    head[9].numel() >= M,
+                "gemm_splitk head: sizes");
+    need_opt(head_dx, at::kBFloat16, "head dx");
+    need_opt(head_tlogits, at::kFloat, "head teacher logits");
+    need_opt(head_own, at::kInt, "head own");
+    if (thr) TORCH_CHECK(head_dx.has_value() && head_dx->defined() && head_dx->numel() == M * N, "gemm_splitk head: dx");
+    if (head_tlogits.has_value() && head_tlogits->defined())
+      TORCH_CHECK(head_tlogits->numel() == 2 * Bh && head_f[3] > 0.0, "gemm_splitk head: teacher logits [B, 2], T > 0");
+    if (head_own.has_value() && head_own->defined()) TORCH_CHECK(head_own->numel() == Bh + 1, "gemm_splitk head: own");
+    hd.W = head[0].data_ptr<float>();
+    hd.bias = head[1].data_ptr<float>();
+    hd.labels = reinterpret_cast<const long long*>(head[2].data_ptr());
+    hd.logits = head[3].data_ptr<float>();
+    hd.dlogits = head[4].data_ptr<float>();
+    hd.dz = reinterpret_cast<uint16_t*>(head[5].data_ptr());
+    hd.colpart = head[6].data_ptr<float>();
+    hd.hpart = head[7].data_ptr<float>();
+    hd.dbpart = head[8].data_ptr<float>();
+    hd.lpart = head[9].data_ptr<float>();
+    hd.seed_ptr = seedp(head[10]);
+    hd.site = (uint32_t)head_f[0];
+    hd.thr = (uint32_t)head_f[1];
+    hd.dscale = (float)head_f[2];
+    hd.kd_T = (float)head_f[3];
+    hd.kd_alpha = (float)head_f[4];
+    hd.B = (int)Bh;
+    hd.dx = ptr<uint16_t>(head_dx);
+    hd.tlogits = ptr<const float>(head_tlogits);
+    hd.own = ptr<int>(head_own);
+  }
   int blocks = 0;
   const int rc = fd_gemm_splitk((int)epi, A.data_ptr(), Bt.data_ptr(), (int)M, (int)N, (int)K,
                                 workspace.data_ptr<float>(), workspace.numel(), (int)splits, ptr<float>(bias),
                                 C.data_ptr(), ptr<void>(aux), ptr<void>(aux_out), ptr<void>(res), ptr<float>(colsum),
-                                &blocks, epi >= 6 ? &ln : nullptr, b_mn ? 1 : 0, stream());
+                                &blocks, epi >= 6 ? &ln : nullptr, head.empty() ? nullptr : &hd, b_mn ? 1 : 0,
+                                stream());
   TORCH_CHECK(rc > 0, "gemm_splitk: launcher rejected arguments (rc=", rc, ")");
   return {rc, blocks};
 }
@@ -1398,7 +1451,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rstd") = py::none(), py::arg("z") = py::none(), py::arg("dx") = py::none(),
         py::arg("colpart") = py::none(), py::arg("eps") = 1e-12, py::arg("seed") = py::none(),
         py::arg("site") = 0, py::arg("thr") = 0, py::arg("dscale") = 1.0, py::arg("row_map") = py::none(),
-        py::arg("b_mn") = false);
+        py::arg("b_mn") = false, py::arg("head") = std::vector<at::Tensor>{}, py::arg("head_f") = std::vector<double>{},
+        py::arg("head_dx") = py::none(), py::arg("head_tlogits") = py::none(), py::arg("head_own") = py::none());
   m.def("gemm_dw2", &gemm_dw2);
   m.def("gemm_dw", &gemm_dw);
   m.def("adam_rows", &adam_rows);

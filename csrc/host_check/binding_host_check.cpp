@@ -151,10 +151,24 @@ int fd_adam_rows(float* p, const float* g, float* m, float* v, void* shadow, int
 }
 int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, float* workspace,
                    long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
-                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, int b_mn, hipStream_t) {
+                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, const FdSkHead* hd,
+                   int b_mn, hipStream_t) {
   ++hc::calls;
   (void)b_mn;  // (W [K][N] or W^T [N][K]: the same N * K elements)
   const long long mn = (long long)M * N;
+  if (hd && hd->W) {  // the fused head (FdSkHead): B rows of head outputs, M rows of partials
+    hc::span(hd->W, (long long)2 * N * 4, "splitk head W");
+    hc::span(hd->labels, (long long)hd->B * 8, "splitk head labels");
+    hc::span(hd->logits, (long long)hd->B * 8, "splitk head logits");
+    hc::span(hd->dlogits, (long long)hd->B * 8, "splitk head dlogits");
+    hc::span(hd->dz, mn * 2, "splitk head dz");
+    hc::opt_span(hd->dx, mn * 2, "splitk head dx");
+    hc::span(hd->colpart, mn * 3 * 4, "splitk head colpart");
+    hc::span(hd->hpart, mn * 2 * 4, "splitk head hpart");
+    hc::span(hd->dbpart, (long long)M * 8, "splitk head dbpart");
+    hc::span(hd->lpart, (long long)M * 4, "splitk head lpart");
+    hc::opt_span(hd->own, (long long)(hd->B + 1) * 4, "splitk head own");
+  }
   if (splits <= 0) splits = 1;
   hc::span(A, (long long)M * K * 2, "splitk A");
   hc::span(Bt, (long long)N * K * 2, "splitk Bt");

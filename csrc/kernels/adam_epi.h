@@ -100,3 +100,30 @@ struct FdLnEpi {
   float* xbuf;
   uint64_t* xflag;
 };
+
+// The pruned training step's head fused into the split-K LayerNorm epilogue of the last block's
+// output LayerNorm (splitk.hip sk_ln_kernel, FD_HEAD_IN_SK): row m's block, after writing y[m],
+// computes the head logits / loss / dlogits of [CLS] row m (< B), the head gradient of y[m] and the
+// LayerNorm backward of the row (the unit-seeded loss's gradient), and leaves per-row partials of
+// the head dW / db, the loss mean and the LayerNorm affine gradients for the deferred column sums.
+struct FdSkHead {
+  const float* W;          // [2][N] head weight (fp32 master)
+  const float* bias;       // [2]
+  const long long* labels; // [B]
+  const float* tlogits;    // [B][2] teacher logits (nullable: plain cross-entropy)
+  float kd_T, kd_alpha;
+  const uint32_t* seed_ptr;  // head dropout (hashed like head_common.h)
+  uint32_t site, thr;
+  float dscale;
+  int B;
+  const int* own;          // [B + 1] packed sequence starts (nullable): empty sequences get no dh
+  float* logits;           // [B][2]
+  float* dlogits;          // [B][2]
+  uint16_t* dz;            // [M][N] bf16 LayerNorm input gradient
+  uint16_t* dx;            // [M][N] bf16 dropout-masked (nullable without dropout)
+  float* colpart;          // [M][3][N] dgamma / dbeta / dbias rows
+  float* hpart;            // [M][2][N] head dW rows
+  float* dbpart;           // [M][2] head db rows
+  float* lpart;            // [M] row loss / B
+};
+

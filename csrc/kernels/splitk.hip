@@ -15,6 +15,8 @@
 
 namespace {
 
+#include "head_common.h"
+
 enum : int { SK_BF16 = 0, SK_BIAS = 1, SK_BIAS_GELU = 2, SK_GELU_BWD = 3, SK_ADD = 4, SK_LN = 6, SK_LN_BWD = 7 };
 
 struct SkArgs {
@@ -29,6 +31,7 @@ struct SkArgs {
   float* colsum;        // GELU_BWD / ADD: [ceil(M / 32)][N] column partials of C (nullable)
   FdLnEpi ln;           // LN: gamma, beta, mean, rstd (out), z (out, nullable), dropout, row_map, eps
                         // LN_BWD: gamma, mean, rstd, z (in), dx (out), colpart [M][3][N] (out)
+  FdSkHead hd;          // LN (hd.W != nullptr): the pruned step's head + the LayerNorm backward
 };
 
 // Sum of the split-K slabs at element offset i (8 consecutive fp32), slab order.  The loads of
@@ -142,6 +145,121 @@ DEV float block_sum4(float v, float* lds) {
   return (lds[0] + lds[1]) + (lds[2] + lds[3]);
 }
 
+// The pruned step's head on output row m (a.hd, FdSkHead), inside the output-LayerNorm epilogue
+// block of that row: the logits by one wave in head_logits_finish's lane / chunk order over the
+// row's bf16 values staged in LDS, then the loss / dlogits (head_loss_grad_in), the head gradient
+// of the row (head_dh, zero for rows >= B and empty sequences) and the LayerNorm backward of it
+// (sk_ln_kernel<true>'s arithmetic).  Per-row partials of the head dW / db, the loss mean and the
+// LayerNorm affine gradients go to the deferred column sums.  N == 768.
+DEV void sk_head_row(const SkArgs& a, int m, int t, bool act, int n, const float (&yb)[8], const float (&z)[8],
+                     float mean, float rstd, const float (&g)[8], uint32_t lseed, size_t hrow) {
+  __shared__ __attribute__((aligned(16))) uint16_t ys[768];
+  __shared__ float hs[4];
+  __shared__ float red[4];
+  const FdSkHead& H = a.hd;
+  const FdLnEpi& L = a.ln;
+  const int N = a.N, lane = t & 63;
+  HeadArgs h{};
+  h.D = N; h.B = H.B; h.W = H.W; h.bias = H.bias; h.seed_ptr = H.seed_ptr; h.site = H.site; h.thr = H.thr;
+  h.dscale = H.dscale; h.labels = H.labels; h.tlogits = H.tlogits; h.kd_T = H.kd_T; h.kd_alpha = H.kd_alpha;
+  const bool hr = m < H.B;
+  if (act) *reinterpret_cast<uint4*>(ys + n) = pack8bf(yb);
+  __syncthreads();
+  if (hr && t < 64) {
+    const int b[1] = {m};
+    const bf16_t* x[1] = {nullptr};
+    const bool hdrop = H.thr != 0;
+    const uint32_t hseed = hdrop ? hash32(H.seed_ptr[0], H.site) : 0u;
+    const HeadRowIn in = head_row_in(h, m);
+    float z0[1] = {0.f}, z1[1] = {0.f};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int col = 4 * lane + 256 * j;
+      const uint2 xv[1] = {*reinterpret_cast<const uint2*>(ys + col)};
+      const float4 w0 = *reinterpret_cast<const float4*>(H.W + col);
+      const float4 w1 = *reinterpret_cast<const float4*>(H.W + N + col);
+      head_logit_chunk<1>(h, b, x, col, hdrop, hseed, xv, w0, w1, z0, z1);
+    }
+    const float l0 = wave_sum(z0[0]) + H.bias[0], l1 = wave_sum(z1[0]) + H.bias[1];
+    float loss, d0, d1;
+    head_loss_grad_in(h, in, l0, l1, loss, d0, d1);
+    if (lane == 0) {
+      H.logits[2 * m] = l0;
+      H.logits[2 * m + 1] = l1;
+      H.dlogits[2 * m] = d0;
+      H.dlogits[2 * m + 1] = d1;
+      hs[0] = d0; hs[1] = d1; hs[2] = loss;
+    }
+  }
+  __syncthreads();
+  const float d0 = hr ? hs[0] : 0.f, d1 = hr ? hs[1] : 0.f;
+  if (t == 0) {
+    H.lpart[m] = hr ? hs[2] / H.B : 0.f;
+    H.dbpart[2 * m] = d0;
+    H.dbpart[2 * m + 1] = d1;
+  }
+  const bool grad_row = hr && !(H.own && H.own[m] == H.own[m + 1]);
+  const bool hdrop = H.thr != 0;
+  const uint32_t hseed = hdrop ? hash32(H.seed_ptr[0], H.site) : 0u;
+  float dy[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, xh[8], gd[8];
+  float s1 = 0.f, s2 = 0.f;
+  if (act) {
+    float w0[8], w1[8];
+    const float4 a0 = *reinterpret_cast<const float4*>(H.W + n), a1 = *reinterpret_cast<const float4*>(H.W + n + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(H.W + N + n), b1 = *reinterpret_cast<const float4*>(H.W + N + n + 4);
+    w0[0] = a0.x; w0[1] = a0.y; w0[2] = a0.z; w0[3] = a0.w; w0[4] = a1.x; w0[5] = a1.y; w0[6] = a1.z; w0[7] = a1.w;
+    w1[0] = b0.x; w1[1] = b0.y; w1[2] = b0.z; w1[3] = b0.w; w1[4] = b1.x; w1[5] = b1.y; w1[6] = b1.z; w1[7] = b1.w;
+    const uint32_t kb = hdrop ? drop_keep_bits<8>(hseed, (uint32_t)(m * N + n), H.thr) : 0xffu;
+    float hp0[8], hp1[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sc = hdrop ? (((kb >> e) & 1u) ? H.dscale : 0.f) : 1.f;
+      dy[e] = grad_row ? bf2f(head_dh(d0, d1, w0[e], w1[e], sc)) : 0.f;
+      // head dW rows: d * dropout(x) (head_bwd's product; its column sums then run deferred)
+      const float xd = yb[e] * sc;
+      hp0[e] = hr ? d0 * xd : 0.f;
+      hp1[e] = hr ? d1 * xd : 0.f;
+    }
+    float* hp = H.hpart + (size_t)m * 2 * N + n;
+    *reinterpret_cast<float4*>(hp) = make_float4(hp0[0], hp0[1], hp0[2], hp0[3]);
+    *reinterpret_cast<float4*>(hp + 4) = make_float4(hp0[4], hp0[5], hp0[6], hp0[7]);
+    *reinterpret_cast<float4*>(hp + N) = make_float4(hp1[0], hp1[1], hp1[2], hp1[3]);
+    *reinterpret_cast<float4*>(hp + N + 4) = make_float4(hp1[4], hp1[5], hp1[6], hp1[7]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xh[e] = (z[e] - mean) * rstd;
+      gd[e] = g[e] * dy[e];
+      s1 += gd[e];
+      s2 += gd[e] * xh[e];
+    }
+  }
+  s1 = block_sum4(s1, red) / N;
+  s2 = block_sum4(s2, red) / N;
+  if (act) {
+    const size_t i = (size_t)m * N + n;
+    const bool drop = L.thr != 0;
+    const uint32_t kb = drop ? drop_keep_bits<8>(lseed, (uint32_t)(hrow * N + n), L.thr) : 0xffu;
+    float dz[8], dx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      dz[e] = rstd * (gd[e] - s1 - xh[e] * s2);
+      dx[e] = drop ? ((kb >> e) & 1u ? dz[e] * L.dscale : 0.f) : dz[e];
+    }
+    *reinterpret_cast<uint4*>(H.dz + i) = pack8bf(dz);
+    if (drop && H.dx) *reinterpret_cast<uint4*>(H.dx + i) = pack8bf(dx);
+    float* cp = H.colpart + (size_t)m * 3 * N + n;
+    float gx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gx[e] = dy[e] * xh[e];
+    *reinterpret_cast<float4*>(cp) = make_float4(gx[0], gx[1], gx[2], gx[3]);
+    *reinterpret_cast<float4*>(cp + 4) = make_float4(gx[4], gx[5], gx[6], gx[7]);
+    *reinterpret_cast<float4*>(cp + N) = make_float4(dy[0], dy[1], dy[2], dy[3]);
+    *reinterpret_cast<float4*>(cp + N + 4) = make_float4(dy[4], dy[5], dy[6], dy[7]);
+    *reinterpret_cast<float4*>(cp + 2 * N) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+    *reinterpret_cast<float4*>(cp + 2 * N + 4) = make_float4(dx[4], dx[5], dx[6], dx[7]);
+  }
+}
+
 // LayerNorm epilogues: one 256-thread block per row, thread t owns columns 8t .. 8t+7 (t < N / 8,
 // N <= 2048).  Forward: the math of gemm.hip's ln_epilogue (z rounded to bf16 before the
 // statistics; mean, then the centred sum of squares).  Backward: s1 = mean(gamma dy),
@@ -167,7 +285,7 @@ __global__ __launch_bounds__(256) void sk_ln_kernel(SkArgs a) {
     g[0] = g0.x; g[1] = g0.y; g[2] = g0.z; g[3] = g0.w; g[4] = g1.x; g[5] = g1.y; g[6] = g1.z; g[7] = g1.w;
   }
   if constexpr (!BWD) {
-    float z[8];
+    float z[8], yb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (act) {
       const float4 b0 = *reinterpret_cast<const float4*>(a.bias + n), b1 = *reinterpret_cast<const float4*>(a.bias + n + 4);
       const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
@@ -202,8 +320,10 @@ __global__ __launch_bounds__(256) void sk_ln_kernel(SkArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) y[e] = (z[e] - mean) * rstd * g[e] + bt[e];
       *reinterpret_cast<uint4*>(a.C + i) = pack8bf(y);
+      if (a.hd.W) unpack8bf(pack8bf(y), yb);  // (the head reads the stored bf16 values)
     }
     if (t == 0) { L.mean[m] = mean; L.rstd[m] = rstd; }
+    if (a.hd.W) sk_head_row(a, m, t, act, n, yb, z, mean, rstd, g, seed, hrow);
   } else {
     const float mean = L.mean[m], rstd = L.rstd[m];
     float dy[8], xh[8], gd[8];
@@ -257,13 +377,20 @@ extern "C" {
 // gemm.hip's gemm_ln_kernel (LN_BWD: colpart has M partial rows of [3][N]).  0 or an error code.
 int fd_splitk_epilogue(int epi, const float* slabs, long long sstride, int splits, int M, int N, const float* bias,
                        void* C, void* aux, void* aux_out, const void* res, float* colsum, int* colsum_blocks,
-                       const FdLnEpi* ln, hipStream_t st) {
+                       const FdLnEpi* ln, const FdSkHead* hd, hipStream_t st) {
   if (M <= 0 || N <= 0 || splits <= 0 || sstride < (long long)M * N || !slabs || !C) return 1;
   SkArgs a{};
   a.slabs = slabs; a.sstride = sstride; a.splits = splits; a.M = M; a.N = N;
   a.bias = bias; a.C = (bf16_t*)C; a.aux = (bf16_t*)aux; a.aux_out = (bf16_t*)aux_out;
   a.res = (const bf16_t*)res; a.colsum = colsum;
   if (ln) a.ln = *ln;
+  if (hd && hd->W) {  // the fused head: LayerNorm forward only, N = 768, every output buffer given
+    if (epi != SK_LN || N != 768 || hd->B <= 0 || hd->B > M || !hd->labels || !hd->logits || !hd->dlogits ||
+        !hd->dz || !hd->colpart || !hd->hpart || !hd->dbpart || !hd->lpart || !hd->bias || !hd->seed_ptr ||
+        (ln && ln->thr && !hd->dx))
+      return 8;
+    a.hd = *hd;
+  }
   if (colsum_blocks) *colsum_blocks = 0;
   if (epi == SK_LN || epi == SK_LN_BWD) {
     if (!ln || !res || N % 8 || N > 2048 || !ln->gamma || !ln->mean || !ln->rstd) return 2;
@@ -310,11 +437,13 @@ int fd_gemm_f32_splits(const void* A, const void* Bt, float* slabs, long long sl
 // b_mn: Bt is the weight W [K][N] itself (C = epi(A W)), read MN-major.
 int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, float* workspace,
                    long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
-                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, int b_mn, hipStream_t st) {
+                   const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, const FdSkHead* hd,
+                   int b_mn, hipStream_t st) {
+  if (hd && hd->W && (epi != SK_LN || N != 768)) return -18;  // (checked before anything launches)
   const int s = fd_gemm_f32_splits(A, Bt, workspace, workspace_elems, M, N, K, K, b_mn ? N : K, splits, b_mn, st);
   if (s <= 0) return s == 0 ? -9 : s;
   const int rc = fd_splitk_epilogue(epi, workspace, (long long)M * N, s, M, N, bias, C, aux, aux_out, res, colsum,
-                                    colsum_blocks, ln, st);
+                                    colsum_blocks, ln, hd, st);
   return rc ? -10 - rc : s;
 }
 }  // extern "C"

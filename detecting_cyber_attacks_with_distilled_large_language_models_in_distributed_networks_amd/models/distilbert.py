@@ -552,6 +552,10 @@ class DDoSClassifier(nn.Module):
                                             cls_rmap=plan[5] if plan is not None else None)
         x = EmbeddingFn.apply(token, ids, emb["word"], emb["pos"], emb["ln_w"], emb["ln_b"], emb["sinks"], rc)
         self._setup_prune(rc, plan, len(layers), packed)
+        if (labels is not None and grad and self.training and rc.unit_backward and rc.prune_idx >= 0
+                and rc.colsum_jobs is not None and rc.head_rows is not None):
+            # (the pruned block may run the head inside its output-LayerNorm launch: ops/functional.py)
+            rc.head_req = (head, labels.to(torch.int64), kd)
         for i, L in enumerate(layers):
             x = LayerFn.apply(x, L, rc, i)
         if labels is not None:

@@ -101,6 +101,11 @@ class RunCtx:
     unit_backward: bool = False
     pruned_ln2: Optional[tuple] = None
     head_fold: Optional[tuple] = None
+    # the same fold one launch earlier (ops/kernels.py HEAD_IN_SK): head_req = (head handles,
+    # labels, kd) set by the model before the blocks; the pruned block's output-LayerNorm split-K
+    # epilogue then runs the head too and leaves head_done = (logits, loss, dz2, df) for HeadFn
+    head_req: Optional[tuple] = None
+    head_done: Optional[tuple] = None
 
 
 class GradSink:
@@ -249,8 +254,24 @@ class LayerFn(torch.autograd.Function):
         h, ao, m1, r1 = K.linear_ln_fwd(cxc, L["o_w"], L["o_b"], xc, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0,
                                         keep_z=grad, xsite=K.ln_xsite(idx, 0, False))
         g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
-        y, f, m2, r2 = K.linear_ln_fwd(g, L["l2_w"], L["l2_b"], h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed,
-                                       ffn_site, p_h, rm, keep_z=grad, xsite=K.ln_xsite(idx, 1, False))
+        hq = rc.head_req if grad else None
+        if hq is not None and K.head_in_sk_ok(g.shape[0], L["l2_w"].shape[0], g.shape[1]):
+            # the head + this LayerNorm's backward in the LayerNorm's own split-K epilogue launch
+            head, labels, kd = hq
+            G = L["sinks"]
+            hs = head["sinks"]
+            acc_ln = G["l2_w"].written()  # (peek: the pruned block's backward marks it)
+            acc_h = hs["w"].accumulate()
+            hs["b"].accumulate()
+            y, f, m2, r2, hout = K.linear_ln_fwd_head(
+                g, L["l2_w"], L["l2_b"], h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed, ffn_site, p_h, rm,
+                head["w"], head["b"], 2, rc.p_head, labels, rc.B, rc.cu, kd, hs["w"].buf, hs["b"].buf, acc_h,
+                G["ln2_w"].buf, G["ln2_b"].buf, G["l2_b"].buf, acc_ln, rc.colsum_jobs, rc.loss_acc)
+            rc.head_done = hout
+            rc.head_req = None
+        else:
+            y, f, m2, r2 = K.linear_ln_fwd(g, L["l2_w"], L["l2_b"], h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed,
+                                           ffn_site, p_h, rm, keep_z=grad, xsite=K.ln_xsite(idx, 1, False))
         if grad:
             ctx.save_for_backward(x)
             ctx.acts = (qkv, cx, lse, cxc, ao, h, m1, r1, u, None if rc.remat_gelu else g, f, m2, r2)
@@ -430,6 +451,20 @@ class HeadFn(torch.autograd.Function):
         ctx.rc, ctx.sinks, ctx.p, ctx.W = rc, sinks, p, W
         ctx.fused_loss = labels is not None
         ctx.folded = False
+        hd = rc.head_done
+        if hd is not None and labels is not None and ctx.needs_input_grad[0]:
+            # the pruned block's output-LayerNorm launch already ran the head (forward and backward)
+            logits, loss, dz2, df = hd
+            rc.head_done = None
+            rc.head_fold = (dz2, df)
+            rc.pruned_ln2 = None
+            ctx.folded = True
+            ctx.unit = K.unit_grad(hidden.device)
+            ctx.zero = K.zero_scalar(hidden.device, hidden.dtype)
+            ctx.shape = hidden.shape
+            ctx.set_materialize_grads(False)
+            ctx.mark_non_differentiable(logits)
+            return loss, logits
         ln2 = rc.pruned_ln2
         if (K.FUSE_HEAD and labels is not None and rc.training and rc.unit_backward and ctx.needs_input_grad[0]
                 and ln2 is not None and rc.head_rows is not None and rc.colsum_jobs is not None

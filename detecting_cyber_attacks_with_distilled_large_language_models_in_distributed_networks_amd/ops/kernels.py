@@ -570,6 +570,57 @@ def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, k
     return y, z, mean, rstd
 
 
+# The pruned training step's head inside the output-LayerNorm split-K epilogue of the last block
+# (csrc/kernels/splitk.hip sk_head_row): one launch fewer than head_ln_bwd; FD_HEAD_IN_SK=0: off.
+HEAD_IN_SK = _os.environ.get("FD_HEAD_IN_SK", "0") != "0"
+
+
+def head_in_sk_ok(M: int, N: int, K: int) -> bool:
+    return HEAD_IN_SK and FUSE_HEAD and N == 768 and _splitk_ok(M, N, K)
+
+
+def linear_ln_fwd_head(x, w, b, res, gamma, beta, eps, seed, site, p, row_map, hW, hb, head_site, p_head, labels,
+                       B, own, kd, dW, db, acc_head, dgamma, dbeta, dbias, acc_ln, jobs, loss_acc=None):
+    """``linear_ln_fwd`` on the pruned [CLS] rows (split-K) with the head fused into its epilogue:
+    per row the head logits / loss / dlogits, the head gradient of the row (the loss's upstream
+    gradient is 1) and the LayerNorm backward of it.  The head dW / db, the loss mean (and the
+    running ``loss_acc``) and the LayerNorm affine gradients are column sums of per-row partials,
+    appended to the deferred ``jobs``.  Returns (y, z, mean, rstd, (logits, loss, dz, dx))."""
+    M, N = x.shape[0], w.shape[0]
+    dev = x.device
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    z = torch.empty_like(y)
+    mean = torch.empty(M, dtype=torch.float32, device=dev)
+    rstd = torch.empty(M, dtype=torch.float32, device=dev)
+    thr, sc = _drop(p)
+    hthr, hsc = _drop(p_head)
+    logits = torch.empty(B, 2, dtype=torch.float32, device=dev)
+    dlogits = torch.empty(B, 2, dtype=torch.float32, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    dz = torch.empty_like(y)
+    dx = torch.empty_like(y) if thr else None
+    n = len(jobs)
+    colpart = workspace(dev, f"ln_colpart_job{n}", M * 3 * N)
+    hpart = workspace(dev, f"head_part_job{n}", M * 2 * N)
+    dbpart = workspace(dev, f"head_db_job{n}", M * 2)
+    lpart = workspace(dev, f"head_loss_job{n}", M)
+    t, kT, alpha = kd if kd is not None else (None, 1.0, 1.0)
+    if t is not None:
+        t = t.detach().float().contiguous()
+    _splitk(EPI_LN, x, w, y, bias=b, res=res, gamma=gamma, beta=beta, mean=mean, rstd=rstd, z=z, eps=eps,
+            seed=seed, site=site, thr=thr, dscale=sc, row_map=row_map if thr else None,
+            head=[hW, hb, labels, logits, dlogits, dz, colpart, hpart, dbpart, lpart, seed],
+            head_f=[float(head_site), float(hthr), float(hsc), float(kT), float(alpha), float(B)],
+            head_dx=dx, head_tlogits=t, head_own=own)
+    jobs.append((colpart, [dgamma, dbeta, dbias], M, 3 * N, N, acc_ln))
+    jobs.append((hpart, [dW[0], dW[1]], M, 2 * N, N, acc_head))
+    jobs.append((dbpart, [db[0:1], db[1:2]], M, 2, 1, acc_head))
+    jobs.append((lpart, [loss.view(1)], M, 1, 1, False))
+    if loss_acc is not None:
+        jobs.append((lpart, [loss_acc], M, 1, 1, True))
+    return y, z, mean, rstd, (logits, loss, dz, dx if dx is not None else dz)
+
+
 def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False,
                      row_map=None, jobs: Optional[list] = None, xsite=None, b_mn: bool = False):
     """LayerNorm backward fused into the dX GEMM that produces its output gradient:

@@ -235,6 +235,7 @@ def test_fused_head_ln_backward_bitwise(packed, B, empty, kd, monkeypatch):
     the three launches it replaces (FD_FUSE_HEAD=0): loss, logits and every gradient bitwise equal,
     including an accumulating second backward, an empty sequence and the distillation loss."""
     from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+    monkeypatch.setattr(K, "HEAD_IN_SK", False)  # (this test is about the head_ln_bwd launch)
     cfg = DistilBertConfig(n_layers=3)
     outs = []
     for fused in (True, False):
@@ -266,6 +267,51 @@ def test_fused_head_ln_backward_bitwise(packed, B, empty, kd, monkeypatch):
         assert torch.equal(z0, z1) and l0.item() == l1.item()
     for k in d1:
         assert torch.equal(d0[k], d1[k]), k
+
+
+@pytest.mark.parametrize("packed,B,empty,kd", [(True, 32, None, False), (True, 20, 3, False), (False, 16, None, False),
+                                               (True, 32, None, True)])
+def test_head_in_output_ln_epilogue(packed, B, empty, kd, monkeypatch):
+    """The pruned training step's head inside the output-LayerNorm split-K epilogue launch
+    (ops/kernels.py HEAD_IN_SK, splitk.hip sk_head_row) against the separate fused-head launch
+    (head_ln_bwd): logits bitwise (same per-row arithmetic on the same y), the loss and every
+    gradient to fp32 summation order (per-row partials summed by the deferred column sums),
+    including an accumulating second backward, an empty sequence and the distillation loss."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+    cfg = DistilBertConfig(n_layers=3)
+    outs = []
+    for in_sk in (True, False):
+        monkeypatch.setattr(K, "HEAD_IN_SK", in_sk)
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=43)
+        m.train()
+        ids, mask, labels, tokens = _batch(B, 128, seed=812, empty=empty)
+        t = None
+        if kd:
+            g = torch.Generator(device="cuda").manual_seed(4)
+            t = (torch.randn(B, 2, device="cuda", generator=g), 2.0, 0.9)
+        m.zero_grad()
+        res = []
+        for it in range(2):  # the second backward accumulates
+            m.rng.fill_(7 + it)
+            calls = []
+            real = K.head_ln_bwd
+            monkeypatch.setattr(K, "head_ln_bwd", lambda *a, **k: (calls.append(1), real(*a, **k))[1])
+            loss, logits = m.forward_loss(ids, mask, labels, tokens=tokens if packed else None, kd=t,
+                                          unit_backward=True)
+            loss.backward(K.unit_grad("cuda"))
+            monkeypatch.setattr(K, "head_ln_bwd", real)
+            assert len(calls) == (0 if in_sk else 1)
+            torch.cuda.synchronize()
+            res.append((loss.detach().clone(), logits.detach().clone()))
+        outs.append((res, m.arena.grad.clone(), {k: m.dense_grad(k).clone() for k in m.state_dict()}))
+    (r0, g0, d0), (r1, g1, d1) = outs
+    for (l0, z0), (l1, z1) in zip(r0, r1):
+        assert torch.equal(z0, z1)
+        assert abs(l0.item() - l1.item()) <= 1e-6 * max(1.0, abs(l1.item()))
+    assert _frel(g0, g1) < 1e-5
+    for k in d1:
+        if d1[k].norm() > 0:
+            assert (d0[k] - d1[k]).norm().item() <= 1e-4 * d1[k].norm().item() + 1e-7, k
 
 
 def test_fused_head_rejects_a_foreign_backward_seed():
