@@ -572,7 +572,7 @@ def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, k
 
 # The pruned training step's head inside the output-LayerNorm split-K epilogue of the last block
 # (csrc/kernels/splitk.hip sk_head_row): one launch fewer than head_ln_bwd; FD_HEAD_IN_SK=0: off.
-HEAD_IN_SK = _os.environ.get("FD_HEAD_IN_SK", "0") != "0"
+HEAD_IN_SK = _os.environ.get("FD_HEAD_IN_SK", "1") != "0"
 
 
 def head_in_sk_ok(M: int, N: int, K: int) -> bool:
