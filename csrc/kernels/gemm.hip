@@ -337,6 +337,22 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
   using TR = EpiTraits<EPI, BM, BN>;
   constexpr int MI = TM / 16, NI = TN / 16;
   constexpr int LDC = BN * TR::ES + 16;
+  // staged element epilogues: this thread's aux / residual chunks (16 B each) are all loaded up
+  // front, in flight while the tile is parked -- in the chunk loop below each load would wait
+  // for the previous chunk's store (they may alias), one chunk per thread in flight
+  constexpr int CPR8 = BN / 8, NCH = BM * CPR8 / NT;
+  constexpr bool PRE = TR::ELEM && TR::F32S && (BM * CPR8) % NT == 0 && NCH <= 8;
+  // (1.581 vs 1.590 ms/step, profiles/r5_ab_elem_epilogue_prefetch.txt)
+  uint4 pre[PRE ? NCH : 1];
+  if constexpr (PRE) {
+    const bf16_t* src = EPI == EPI_GELU_BWD ? p.aux : p.res;
+    const int lds = EPI == EPI_GELU_BWD ? p.ldaux : p.ldres;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int id = tid + k * NT, r = id / CPR8, cc = id - r * CPR8;
+      pre[k] = *reinterpret_cast<const uint4*>(src + (size_t)min(m0 + r, p.M - 1) * lds + n0 + cc * 8);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int r = wr * TM + i * 16 + (lane & 15);
@@ -399,17 +415,14 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
     constexpr int CPR = BN / 8;
     constexpr bool CS_OK = NT % CPR == 0;  // a thread keeps one column chunk for the whole tile
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums of this thread's rows (p.colsum)
-#pragma unroll 2
-    for (int id = tid; id < BM * CPR; id += NT) {
-      const int r = id / CPR, cc = id - r * CPR;
+    // one chunk: 8 fp32 of row r from LDS, finished with the 16-byte aux / residual chunk u
+    auto chunk = [&](int r, int cc, const uint4& u) {
       const int m = m0 + r;
-      if (m >= p.M) break;
       const float4 va = *reinterpret_cast<const float4*>(smem + r * LDC + cc * 32);
       const float4 vb = *reinterpret_cast<const float4*>(smem + r * LDC + cc * 32 + 16);
       float v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
       const int n = n0 + cc * 8;
       if constexpr (EPI == EPI_GELU_BWD) {
-        const uint4 u = *reinterpret_cast<const uint4*>(p.aux + (size_t)m * p.ldaux + n);
         const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -421,8 +434,7 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
           gelu_remat(p, m, n + 4, make_uint2(u.z, u.w));
         }
       } else {  // EPI_ADD
-        const uint4 r2 = *reinterpret_cast<const uint4*>(p.res + (size_t)m * p.ldres + n);
-        const uint32_t rw[4] = {r2.x, r2.y, r2.z, r2.w};
+        const uint32_t rw[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           v[2 * e] += lo_bf(rw[e]);
@@ -437,6 +449,23 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
         const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) { cs[2 * e] += lo_bf(ow[e]); cs[2 * e + 1] += hi_bf(ow[e]); }
+      }
+    };
+    if constexpr (PRE) {
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int id = tid + k * NT, r = id / CPR, cc = id - r * CPR;
+        if (m0 + r < p.M) chunk(r, cc, pre[k]);
+      }
+    } else {
+#pragma unroll 2
+      for (int id = tid; id < BM * CPR; id += NT) {
+        const int r = id / CPR, cc = id - r * CPR;
+        const int m = m0 + r;
+        if (m >= p.M) break;
+        const uint4 u = EPI == EPI_GELU_BWD ? *reinterpret_cast<const uint4*>(p.aux + (size_t)m * p.ldaux + n0 + cc * 8)
+                                            : *reinterpret_cast<const uint4*>(p.res + (size_t)m * p.ldres + n0 + cc * 8);
+        chunk(r, cc, u);
       }
     }
     if (CS_OK && p.colsum) {
