@@ -89,8 +89,8 @@ best = {}
 for name, kind, macs, fn, ref in cases:
     opts = [(c, -1) for c in range(NCFG)] if kind != 2 else [(c, s) for c in range(NCFG) for s in (1, 2, 4, 8)]
     for cfg, sp in opts:
-        ext().gemm_set_cfg(kind, cfg, sp)
         try:
+            ext().gemm_set_cfg(kind, cfg, sp)  # (ids not instantiated are rejected)
             out = fn()
             torch.cuda.synchronize()
         except RuntimeError as e:
