@@ -996,7 +996,6 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   // must not be read (a leading empty sequence would read before the tensors)
   if (len == 0) return;
   const size_t tok0 = (size_t)tok0i;
-  if (a.dres) scatter_cls_rows(a, b, tok0, len, h, tid);
   const size_t st0 = ((size_t)b * H + h) * S;
   // phase 1's O rows (for delta) are fetched together with the staging loads: no second
   // dependent global round trip after the barrier
@@ -1023,6 +1022,8 @@ __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
   // the forward's keep bits (rows the forward did not write are past the sequence: P = 0 there)
   const bool mk = a.drop_threshold != 0 && a.dmask != nullptr;
   if (mk && tid < 256) mk_s[tid] = a.dmask[((size_t)b * H + h) * 256 + tid];
+  // (after the staging loads are issued: wave 0's [CLS] row store waits for its load)
+  if (a.dres) scatter_cls_rows(a, b, tok0, len, h, tid);
   __syncthreads();
   ASTAMP(1);
   // unmasked-key bits of the two 64-key tiles (see attn_fwd_s128_kernel): 16-key sub-tiles
