@@ -322,7 +322,17 @@ DEV long load_id(const EmbArgs& a, int t) {
 // broadcast).  4 threads per token each scan a quarter of the keys.
 template <typename I>
 DEV void rank_sort_block(const I* ids, int T, long long* sorted, long long* perm, int* keys, int blk) {
-  for (int i = threadIdx.x; i < T; i += 256) keys[i] = (int)ids[i];
+  // every load of a pass issued before its LDS stores (a plain copy loop waits for each id in
+  // turn: ~11 dependent round trips for a bs32 batch); rows past T re-read id T - 1, not stored
+  constexpr int U = 16;
+  for (int i0 = threadIdx.x; i0 < T; i0 += 256 * U) {
+    I v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ids[min(i0 + u * 256, T - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * 256 < T) keys[i0 + u * 256] = (int)v[u];
+  }
   __syncthreads();
   // 16 tokens per block, 16 threads per token (grid = T/16 blocks: ~256 for a bs32 batch,
   // one per CU, instead of T/64 blocks that left 3/4 of the chip idle)
