@@ -2011,9 +2011,12 @@ int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const f
     static const int env = [] { const char* e = getenv("FD_GEMM_DWB_CFG"); return e ? atoi(e) : -1; }();
     id = env >= 0 ? env : 11;
   }
-  // Group height: A-panels of gm x BM rows x K (bf16) should take ~half of a 4 MiB L2.
-  const long long panel = 128ll * K * 2;
-  bt.group_m = (int)std::max(1ll, std::min(16ll, (2ll << 20) / panel));
+  // Group height: every tile row of a problem (column-major tile order, so consecutive tiles -- one
+  // XCD after the remap -- share the B panel of a column).  In the step 1.585 vs 1.605 ms/step
+  // against the earlier ~half-an-L2 heuristic (3 rows at K = 2688); 12, 16, 24 and 64 alike
+  // (profiles/r5_ab_dwb_group_m.txt; isolated, with operands not just written by the backward, no
+  // difference).
+  bt.group_m = 64;
   static const int gm_env = [] { const char* e = getenv("FD_DWB_GROUP_M"); return e ? atoi(e) : 0; }();
   if (gm_env > 0) bt.group_m = gm_env;  // tuning override
   if (!dwb_launch_cfg(id, bt, st, true)) {
