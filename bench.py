@@ -103,6 +103,9 @@ def _args(argv=None):
                     help="one-GPU job: the quality protocol trains this many federated clients in turn on the "
                          "GPU (seeds 42, 43, ...) and averages them -- the reference's 2-client FedAvg round "
                          "(1: a single client, whose FedAvg is an identity)")
+    ap.add_argument("--rounds", type=int, default=1,
+                    help="FedAvg rounds of the quality protocol (BASELINE.json config 4: 3); each round every "
+                         "client restarts from the previous aggregate with a fresh Adam (client1.py:375-380)")
     return ap.parse_args(argv)
 
 
@@ -257,15 +260,19 @@ def main():
                 yield b
 
     it = batches()
-    if on_gpu and args.spinup_seconds > 0:
-        a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
-        t_end = time.perf_counter() + args.spinup_seconds
-        while time.perf_counter() < t_end:
-            for _ in range(20):
-                a = (a @ a).clamp_(-1.0, 1.0)
-            torch.cuda.synchronize()
-        del a
+
+    def spinup():
+        if on_gpu and args.spinup_seconds > 0:
+            a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+            t_end = time.perf_counter() + args.spinup_seconds
+            while time.perf_counter() < t_end:
+                for _ in range(20):
+                    a = (a @ a).clamp_(-1.0, 1.0)
+                torch.cuda.synchronize()
+            del a
+
     if args.mode == "infer":
+        spinup()
         return _bench_infer(args, model, it, di, comm, B, S)
     # The timed batches are drawn up front; any packed-row bucket among them without a
     # captured graph yet gets one extra (untimed) training step on that batch, so no HIP
@@ -283,13 +290,6 @@ def main():
             if key not in step.graphs and key not in primed and not step.failed:
                 primed.add(key)
                 step(b["input_ids"], b["attention_mask"], b["labels"], b.get("n_tokens"))
-    # the warmup steps accumulate their loss exactly like the timed loop, so the first timed
-    # step does not pay the one-time load of torch's add kernel
-    warm_acc = torch.zeros((), device=dev)
-    for b in warm[n_early:]:
-        out = step(b["input_ids"], b["attention_mask"], b["labels"], b.get("n_tokens"))
-        if not dev_acc:
-            warm_acc += out
     if di.distributed:
         fedavg.fedavg_(model, weight=1.0 / k, comm=ncomm)
     sync = torch.cuda.synchronize if on_gpu else (lambda: None)
@@ -298,6 +298,20 @@ def main():
     gc.collect()
     gc.disable()
     loss_acc = torch.zeros((), device=dev)
+    # All host-side preparation (graph captures, batch draws, GC) is done: bring the GPU to its
+    # working clock with the spin-up loop, then run the remaining warmup steps back to back and go
+    # straight into the timed loop.  (With the spin-up before the captures the idle gap let the
+    # clock fall again: the first timed steps of a 20-step window ran at 1.91 / 1.70 ms against a
+    # 1.57 ms steady state -- profiles/r6_step_events_window.txt.)
+    sync()
+    spinup()
+    # the warmup steps accumulate their loss exactly like the timed loop, so the first timed
+    # step does not pay the one-time load of torch's add kernel
+    warm_acc = torch.zeros((), device=dev)
+    for b in warm[n_early:]:
+        out = step(b["input_ids"], b["attention_mask"], b["labels"], b.get("n_tokens"))
+        if not dev_acc:
+            warm_acc += out
     if dev_acc:
         model.loss_acc.zero_()
     sync()
@@ -348,7 +362,7 @@ def main():
 
     # ---- quality: 3 local epochs + 1 FedAvg round through the federated client (untimed)
     quality = {} if args.no_quality else _quality(client, di, comm, q_rows, q_epochs, on_gpu,
-                                                  n_virtual=args.virtual_clients)
+                                                  n_virtual=args.virtual_clients, n_rounds=args.rounds)
     n = di.world_size
     clients = topo.num_clients
     per_client = args.steps / dt
@@ -456,7 +470,7 @@ def _fedavg_timing(model, di, fedavg, comm, ncomm, k, sync):
             "allreduce_busbw_GBps": round(2.0 * (n - 1) / n * nbytes / r / 1e9, 2)}
 
 
-def _quality_virtual(client, rows, epochs, on_gpu, n_virtual):
+def _quality_virtual(client, rows, epochs, on_gpu, n_virtual, n_rounds=1):
     """1-GPU job: the reference's 2-client round with both clients trained one after the other on
     this GPU (fed/runner.py run_virtual_clients): seeds 42 / 43, the same init, 3 local epochs each,
     the FedAvg sum + scale_cast, each client's test split evaluated on its local model and on the
@@ -464,7 +478,8 @@ def _quality_virtual(client, rows, epochs, on_gpu, n_virtual):
     from importlib import import_module
     runner = import_module(f"{PKG}.fed.runner")
     t0 = time.perf_counter()
-    res = runner.run_virtual_clients(client, n_virtual)
+    res = runner.run_virtual_clients(client, n_virtual, rounds=n_rounds,
+                                     progress=lambda m: print(f"[quality] {m}", file=sys.stderr, flush=True))
     if on_gpu:
         torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -474,6 +489,7 @@ def _quality_virtual(client, rows, epochs, on_gpu, n_virtual):
     f1 = 2 * prec * rec_ / (prec + rec_) if prec + rec_ else 0.0
     total = tp + fp + fn + tn
     cl = res["clients"]
+    cl1 = res["rounds"][0]["clients"]  # (the teachers are fine-tuned in each client's first round)
     return {"aggregated_f1": round(f1, 5),
             "aggregated_accuracy_pct": round(100.0 * (tp + tn) / max(total, 1), 3),
             "aggregated_confusion": [[int(tn), int(fp)], [int(fn), int(tp)]],
@@ -494,27 +510,72 @@ def _quality_virtual(client, rows, epochs, on_gpu, n_virtual):
                             "epoch_losses": [round(x, 5) for x in c["train"]["epoch_losses"]],
                             "train_steps": c["train"]["steps"]} for c in cl],
             "eval_rows": int(total), "eval_rows_per_client": int(total) // max(len(cl), 1),
-            "train_rows_per_client": cl[0]["train_rows"], "fedavg_rounds": 1, "local_epochs": epochs,
+            "train_rows_per_client": cl[0]["train_rows"], "fedavg_rounds": n_rounds, "local_epochs": epochs,
+            **({"per_round": [_round_summary(h) for h in res["rounds"]]} if n_rounds > 1 else {}),
             "quality_file_rows": rows, "quality_fedavg_ms": round(res["fedavg_ms"], 3),
             "quality_train_batches_per_sec": round(float(np.mean([c["train"]["batches_per_sec"] for c in cl])), 2),
             "quality_wall_s": round(wall, 2), "quality_lr": client.cfg.lr,
             **({"kd_alpha": client.cfg.kd_alpha, "kd_temperature": client.cfg.kd_temperature,
-                "teacher_test_accuracy_pct": round(float(np.mean([c["teacher_test"]["accuracy"] for c in cl])), 3),
-                "teacher_test_f1": round(float(np.mean([c["teacher_test"]["f1"] for c in cl])), 5),
+                "teacher_test_accuracy_pct": round(float(np.mean([c["teacher_test"]["accuracy"] for c in cl1])), 3),
+                "teacher_test_f1": round(float(np.mean([c["teacher_test"]["f1"] for c in cl1])), 5),
                 "per_client_teacher": [{"client": c["client"], "accuracy_pct": round(c["teacher_test"]["accuracy"], 3),
                                         "f1": round(c["teacher_test"]["f1"], 5),
-                                        "confusion": c["teacher_test"]["confusion_matrix"]} for c in cl]}
+                                        "confusion": c["teacher_test"]["confusion_matrix"]} for c in cl1]}
                if client.teacher is not None else {})}
 
 
-def _quality(client, di, comm, rows, epochs, on_gpu, n_virtual=1):
+def _acc_f1(cm):
+    (tn, fp), (fn, tp) = cm
+    prec = tp / (tp + fp) if tp + fp else 0.0
+    rec_ = tp / (tp + fn) if tp + fn else 0.0
+    f1 = 2 * prec * rec_ / (prec + rec_) if prec + rec_ else 0.0
+    return 100.0 * (tp + tn) / max(tp + tn + fp + fn, 1), f1
+
+
+def _round_summary(h):
+    """One FedAvg round of the virtual-client protocol: pooled and per-client local / aggregated
+    accuracy, F1 and confusion (the reference's clientN_{local,aggregated}_metrics.csv, per round)."""
+    acc, f1 = _acc_f1(h["aggregated_confusion"])
+    lacc, lf1 = _acc_f1(h["local_confusion"])
+    cl = h["clients"]
+    return {"round": h["round"], "aggregated_accuracy_pct": round(acc, 3), "aggregated_f1": round(f1, 5),
+            "aggregated_confusion": h["aggregated_confusion"], "local_accuracy_pct": round(lacc, 3),
+            "local_f1": round(lf1, 5), "local_confusion": h["local_confusion"],
+            "min_client_aggregated_accuracy_pct": round(min(c["aggregated_test"]["accuracy"] for c in cl), 3),
+            "min_client_aggregated_f1": round(min(c["aggregated_test"]["f1"] for c in cl), 5),
+            "fedavg_ms": round(h["fedavg_ms"], 3),
+            "clients": [{"client": c["client"], "local_accuracy_pct": round(c["local_test"]["accuracy"], 3),
+                         "local_f1": round(c["local_test"]["f1"], 5),
+                         "local_confusion": c["local_test"]["confusion_matrix"],
+                         "aggregated_accuracy_pct": round(c["aggregated_test"]["accuracy"], 3),
+                         "aggregated_f1": round(c["aggregated_test"]["f1"], 5),
+                         "aggregated_confusion": c["aggregated_test"]["confusion_matrix"],
+                         "epoch_losses": [round(x, 5) for x in c["train"]["epoch_losses"]],
+                         "rel_l2_local_to_aggregate": float(f"{c['rel_l2_local_to_aggregate']:.4e}"),
+                         **({"teacher_accuracy_pct": round(c["teacher_test"]["accuracy"], 3),
+                             "teacher_f1": round(c["teacher_test"]["f1"], 5)} if "teacher_test" in c else {})}
+                        for c in cl]}
+
+
+def _quality(client, di, comm, rows, epochs, on_gpu, n_virtual=1, n_rounds=1):
     """Run round 1 of the federated client (fed/runner.py run_round: local train -> local eval
     -> FedAvg -> aggregated eval) and pool the aggregated test confusion matrices of all clients.
     n_virtual > 1 (a one-process job): that many clients trained in turn on this device instead."""
-    if n_virtual > 1 and not di.distributed:
-        return _quality_virtual(client, rows, epochs, on_gpu, n_virtual)
+    if (n_virtual > 1 or n_rounds > 1) and not di.distributed:
+        return _quality_virtual(client, rows, epochs, on_gpu, n_virtual, n_rounds)
     t0 = time.perf_counter()
-    rec = client.run_round(0)
+    client.cfg.rounds = n_rounds
+    per_round = []
+    for r in range(n_rounds):
+        rec = client.run_round(r)
+        if n_rounds > 1:
+            cm = rec["aggregated_test"]["confusion_matrix"]
+            w = 1.0 if client.topo.dp_rank == 0 else 0.0  # data-parallel replicas share one client's split
+            v = [w * float(x) for row in cm for x in row] if len(cm) == 2 else [0.0] * 4
+            pooled = [sum(x[i] for x in comm.all_gather_floats(v)) for i in range(4)]
+            acc, f1 = _acc_f1([[pooled[0], pooled[1]], [pooled[2], pooled[3]]])
+            per_round.append({"round": r + 1, "aggregated_accuracy_pct": round(acc, 3),
+                              "aggregated_f1": round(f1, 5)})
     if on_gpu:
         torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -538,7 +599,8 @@ def _quality(client, di, comm, rows, epochs, on_gpu, n_virtual=1):
             "mean_client_local_f1": round(float(np.mean([v[7] for v in allv])), 5),
             "eval_rows": int(total), "eval_rows_per_client": int(total) // max(len(allv), 1),
             "train_rows_per_client": len(client.data.train), "quality_clients": len(allv),
-            "fedavg_rounds": 1, "local_epochs": epochs, "quality_file_rows": rows,
+            "fedavg_rounds": n_rounds, "local_epochs": epochs, "quality_file_rows": rows,
+            **({"per_round": per_round} if per_round else {}),
             "quality_epoch_losses": [round(x, 5) for x in tr["epoch_losses"]],
             "quality_train_steps": tr["steps"], "quality_train_batches_per_sec": round(tr["batches_per_sec"], 2),
             "quality_fedavg_ms": round(rec["fedavg_ms"], 3), "quality_wall_s": round(wall, 2),

@@ -188,6 +188,7 @@ class FederatedClient:
         log.phase(f"Starting round {r + 1}/{cfg.rounds}")
         opt = ArenaAdam(model, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
                         decoupled=cfg.decoupled_weight_decay)
+        opt.reset_state()  # a fresh Adam every round (client1.py:380), "has state" row flags included
         opt_path = os.path.join(cfg.out_dir, f"client{self.client_id}_optim.pth")
         if cfg.save_optimizer and r == self.start_round:
             ck.load_optimizer(opt, opt_path)
@@ -360,79 +361,127 @@ def _average_masters(model, states: List[torch.Tensor]) -> None:
         model.sync_shadow(force=True)
 
 
-def run_virtual_clients(client: "FederatedClient", n_clients: int = 2) -> Dict:
-    """One FedAvg round of ``n_clients`` federated clients on THIS process's device, trained one
-    after another (a 1-GPU job: ``bench.py`` quality half, ``cli launch --virtual-clients``).
+def _pooled(recs, key: str):
+    return [[sum(r[key]["confusion_matrix"][i][j] for r in recs if len(r[key]["confusion_matrix"]) == 2)
+             for j in range(2)] for i in range(2)]
+
+
+def run_virtual_clients(client: "FederatedClient", n_clients: int = 2, rounds: int = 1,
+                        progress=None) -> Dict:
+    """``rounds`` FedAvg rounds of ``n_clients`` federated clients on THIS process's device, the
+    clients trained one after another (a 1-GPU job: ``bench.py`` quality half with
+    ``--virtual-clients N --rounds R``, ``cli launch --virtual-clients``).
 
     Reference protocol (client1.py / client2.py + server.py:67-79): client k samples its own 10 %
     of the file with seed 42 + k (client1.py:89, client2.py:84), every client starts from the same
-    weights (here: the model's broadcast init), trains ``cfg.epochs`` local epochs with
-    a fresh Adam, is evaluated on its test split, the server averages the fp32 state dicts
-    (unweighted mean; ``_average_masters`` = fedavg_'s sum + ``scale_cast``) and every client then
-    evaluates the aggregate on its own test split (client1_aggregated_metrics.csv).  Returns the
-    per-client local / aggregated metrics, the pooled aggregated confusion matrix and each local
-    model's relative L2 distance to the aggregate (0 would mean the "average" was an identity).
+    weights (round 1: the model's broadcast init; round r > 1: round r-1's aggregate --
+    the reference's next round is a re-run of the scripts that loads the aggregate,
+    client1.py:375-377), trains ``cfg.epochs`` local epochs with a FRESH Adam (client1.py:380
+    re-creates it every run), is evaluated on its test split, the server averages the fp32 state
+    dicts (unweighted mean; ``_average_masters`` = fedavg_'s sum + ``scale_cast``) and every client
+    then evaluates the aggregate on its own test split (client1_aggregated_metrics.csv).
+
+    Each virtual client keeps, across rounds, exactly the state a real client process keeps in
+    ``FederatedClient.run`` (one process per client): its shuffling loader (the epoch permutations
+    continue) and its dropout counters (``model.rng`` / ``torch_counter``), so for the same config
+    the R-round virtual run equals the N-rank collective ``run_federated`` run bit for bit
+    (tests/test_virtual_rounds.py, N = 2, R = 2 on gloo).
+
+    Returns ``rounds`` (one record per round: per-client local / aggregated metrics, the pooled
+    aggregated confusion, the FedAvg time) plus the LAST round's ``clients`` /
+    ``aggregated_confusion`` / ``fedavg_ms`` at the top level (the 1-round API of earlier rounds).
 
     With a teacher (the distillation extension, BASELINE.json config 5) every virtual client does
-    what ``run_round`` does for a real one: the shared BERT-base teacher init is fine-tuned on the
-    client's own split (``teacher_epochs``), then the client's student is distilled from it; the
-    students are averaged (the teachers stay local, as in run_round).  Each record then also holds
-    the client's ``teacher_test`` metrics."""
+    what ``run_round`` does for a real one: in its first round the shared BERT-base teacher init is
+    fine-tuned on the client's own split (``teacher_epochs``) and kept for the later rounds (the
+    teachers stay local, as in run_round), then the client's student is distilled from it; the
+    students are averaged.  Each first-round record then also holds the client's ``teacher_test``."""
     cfg, model = client.cfg, client.model
     if client.di.distributed:
         raise RuntimeError("virtual clients run in a single-process job (world size 1)")
     teacher = client.teacher
     dev = model.device
     A = model.arena
-    init = A.master.detach().clone()
+    glob = A.master.detach().clone()  # what every client starts the round from
     t_init = teacher.arena.master.detach().clone() if teacher is not None else None
-    locals_, recs = [], []
+    say = progress or (lambda msg: None)
+    # per-client state that survives the rounds (a real client's process keeps it)
+    cs = []
     for v in range(n_clients):
         data = build_client_data(client.frame, v, cfg.data_fraction, cfg.base_seed, cfg.max_len, client.tokenizer,
                                  cfg.partition, n_clients)
-        loader = DeviceLoader(data.train, cfg.batch_size, shuffle=True, device=dev, seed=cfg.client_seed(v))
-        test = DeviceLoader(data.test, cfg.eval_batch_size, device=dev)
-        rec = {"client": v + 1, "train_rows": len(data.train), "test_rows": len(data.test)}
-        t0 = time.perf_counter()
-        if teacher is not None:
+        cs.append({"data": data,
+                   "loader": DeviceLoader(data.train, cfg.batch_size, shuffle=True, device=dev,
+                                          seed=cfg.client_seed(v)),
+                   "test": DeviceLoader(data.test, cfg.eval_batch_size, device=dev),
+                   "rng": model.rng.detach().clone(), "torch_counter": model.torch_counter, "teacher": None})
+    hist = []
+    for r in range(rounds):
+        locals_, recs = [], []
+        for v, c in enumerate(cs):
+            data, loader, test = c["data"], c["loader"], c["test"]
+            rec = {"client": v + 1, "round": r + 1, "train_rows": len(data.train), "test_rows": len(data.test)}
+            t0 = time.perf_counter()
+            if teacher is not None:
+                if c["teacher"] is None:
+                    with torch.no_grad():
+                        teacher.arena.master.copy_(t_init)
+                    teacher.sync_shadow(force=True)
+                    t_opt = ArenaAdam(teacher, lr=cfg.lr)
+                    t_opt.reset_state()
+                    teacher.train()
+                    rec["teacher_train"] = train_model(
+                        teacher, loader, None, t_opt, int(cfg.extra.get("teacher_epochs", cfg.epochs)),
+                        log=client.log, use_graph=cfg.use_graph)
+                    rec["teacher_test"] = _metrics_record(evaluate_model(teacher, test,
+                                                                         name=f"Client {v + 1} teacher test"))
+                    c["teacher"] = teacher.arena.master.detach().clone()
+                    del t_opt
+                else:
+                    with torch.no_grad():
+                        teacher.arena.master.copy_(c["teacher"])
+                    teacher.sync_shadow(force=True)
+                teacher.eval()
             with torch.no_grad():
-                teacher.arena.master.copy_(t_init)
-            teacher.sync_shadow(force=True)
-            t_opt = ArenaAdam(teacher, lr=cfg.lr)
-            t_opt.reset_state()
-            teacher.train()
-            rec["teacher_train"] = train_model(teacher, loader, None, t_opt, int(cfg.extra.get("teacher_epochs",
-                                                                                                cfg.epochs)),
-                                               log=client.log, use_graph=cfg.use_graph)
-            rec["teacher_test"] = _metrics_record(evaluate_model(teacher, test, name=f"Client {v + 1} teacher test"))
-            teacher.eval()
-            del t_opt
-        with torch.no_grad():
-            A.master.copy_(init)
-        model.sync_shadow(force=True)
-        opt = ArenaAdam(model, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
-                        decoupled=cfg.decoupled_weight_decay)
-        opt.reset_state()  # (also clears the sparse word rows' "has Adam state" flags)
-        tr = train_model(model, loader, None, opt, cfg.epochs, log=client.log, use_graph=cfg.use_graph,
-                         teacher=teacher, kd_temperature=cfg.kd_temperature, kd_alpha=cfg.kd_alpha)
-        local = _metrics_record(evaluate_model(model, test, name=f"Client {v + 1} local test"))
-        locals_.append(A.master.detach().clone())
-        rec.update({"train": tr, "train_wall_s": time.perf_counter() - t0, "local_test": local, "test": test})
-        recs.append(rec)
-        del opt, loader
-    t0 = time.perf_counter()
-    _average_masters(model, locals_)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    fed_ms = 1e3 * (time.perf_counter() - t0)
-    agg = A.master.detach()
-    for r, loc in zip(recs, locals_):
-        r["aggregated_test"] = _metrics_record(evaluate_model(model, r.pop("test"), name=f"Client {r['client']} "
-                                                                                          "aggregated test"))
-        r["rel_l2_local_to_aggregate"] = float((loc - agg).norm() / loc.norm().clamp_min(1e-30))
-    pooled = [[sum(r["aggregated_test"]["confusion_matrix"][i][j] for r in recs
-                   if len(r["aggregated_test"]["confusion_matrix"]) == 2) for j in range(2)] for i in range(2)]
-    return {"clients": recs, "fedavg_ms": fed_ms, "aggregated_confusion": pooled}
+                A.master.copy_(glob)
+                model.rng.copy_(c["rng"])
+            model.torch_counter = c["torch_counter"]
+            model.sync_shadow(force=True)
+            opt = ArenaAdam(model, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
+                            decoupled=cfg.decoupled_weight_decay)
+            opt.reset_state()  # (also clears the sparse word rows' "has Adam state" flags)
+            tr = train_model(model, loader, None, opt, cfg.epochs, log=client.log, use_graph=cfg.use_graph,
+                             teacher=teacher, kd_temperature=cfg.kd_temperature, kd_alpha=cfg.kd_alpha)
+            with torch.no_grad():
+                c["rng"].copy_(model.rng)
+            c["torch_counter"] = model.torch_counter
+            local = _metrics_record(evaluate_model(model, test, name=f"Client {v + 1} local test"))
+            locals_.append(A.master.detach().clone())
+            rec.update({"train": tr, "train_wall_s": time.perf_counter() - t0, "local_test": local})
+            recs.append(rec)
+            del opt
+            say(f"round {r + 1}/{rounds} client {v + 1}/{n_clients}: local acc {local['accuracy']:.3f} % "
+                f"f1 {local['f1']:.5f} ({tr['steps']} steps, {time.perf_counter() - t0:.1f} s)")
+        t0 = time.perf_counter()
+        _average_masters(model, locals_)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        fed_ms = 1e3 * (time.perf_counter() - t0)
+        agg = A.master.detach()
+        for rec, c, loc in zip(recs, cs, locals_):
+            rec["aggregated_test"] = _metrics_record(evaluate_model(model, c["test"], name=f"Client {rec['client']} "
+                                                                                           "aggregated test"))
+            rec["rel_l2_local_to_aggregate"] = float((loc - agg).norm() / loc.norm().clamp_min(1e-30))
+        glob = agg.clone()
+        del locals_
+        pooled = _pooled(recs, "aggregated_test")
+        hist.append({"round": r + 1, "clients": recs, "fedavg_ms": fed_ms, "aggregated_confusion": pooled,
+                     "local_confusion": _pooled(recs, "local_test")})
+        (tn, fp), (fn, tp) = pooled
+        say(f"round {r + 1}/{rounds} aggregate: pooled acc {100.0 * (tp + tn) / max(tp + tn + fp + fn, 1):.3f} %")
+    last = hist[-1]
+    return {"clients": last["clients"], "fedavg_ms": last["fedavg_ms"],
+            "aggregated_confusion": last["aggregated_confusion"], "rounds": hist}
 
 
 def run_federated(cfg: FedConfig, frame=None, model_config: Optional[DistilBertConfig] = None) -> Dict:

@@ -1,4 +1,5 @@
-"""Multi-process federated paths on CPU with the gloo backend (world_size 2 and 4).
+"""Multi-process federated paths on CPU with the gloo backend (world_size 2, 4 and 8 -- the target
+node's 8 clients).
 
 Mirrors BASELINE.json config 1 (2-client FedAvg plumbing, no GPU): the FedAvg
 result must equal the mean of the per-rank weights -- bit-exact for N = 2.
@@ -32,6 +33,7 @@ def _fedavg_worker(rank, world, port, outdir, mode):
     fedavg = import_module(f"{PKG}.parallel.fedavg")
     models = import_module(f"{PKG}.models")
     comm.init_distributed(device="cpu")
+    torch.set_num_threads(1)  # (8 ranks share this container's CPUs)
     m = models.DDoSClassifier(config=models.DistilBertConfig(n_layers=1), seed=100 + rank)
     before = m.arena.master.clone()
     torch.save(before, os.path.join(outdir, f"before{rank}.pt"))
@@ -41,6 +43,8 @@ def _fedavg_worker(rank, world, port, outdir, mode):
         fedavg.fedavg_(m, weight=float(rank + 1))
     elif mode == "drop":
         fedavg.fedavg_(m, participate=(rank != 1))
+    elif mode == "drop5":
+        fedavg.fedavg_(m, participate=(rank != 5))
     elif mode == "broadcast":
         fedavg.broadcast_model(m)
     torch.save(m.arena.master.clone(), os.path.join(outdir, f"after{rank}.pt"))
@@ -69,6 +73,28 @@ def test_fedavg_four_clients(tmp_path):
         assert torch.allclose(a, mean, atol=1e-7)
 
 
+def test_fedavg_eight_clients(tmp_path):
+    """The 8-client FedAvg of BASELINE.json config 4 (one client per GPU of the node): every rank
+    holds the numpy mean of the eight fp32 arenas."""
+    import numpy as np
+    before, after = _run(8, "plain", tmp_path)
+    mean = torch.from_numpy(np.mean(np.stack([b.double().numpy() for b in before]), axis=0))
+    for a in after:
+        assert torch.equal(a, after[0])
+        assert (a.double() - mean).abs().max().item() <= 1e-7
+
+
+def test_fedavg_eight_clients_one_dropped(tmp_path):
+    """Client 6 (rank 5) dropped at N = 8: the other seven are averaged and rank 5 still
+    receives that aggregate (partial participation)."""
+    before, after = _run(8, "drop5", tmp_path)
+    live = [b for r, b in enumerate(before) if r != 5]
+    mean = torch.stack(live).double().mean(0)
+    for a in after:
+        assert torch.equal(a, after[0])
+        assert (a.double() - mean).abs().max().item() <= 1e-7
+
+
 def test_fedavg_weighted(tmp_path):
     before, after = _run(2, "weighted", tmp_path)
     ref = (before[0] * 1 + before[1] * 2) / 3
@@ -87,6 +113,7 @@ def test_broadcast_initial_model(tmp_path):
 
 def _fed_worker(rank, world, port, outdir):
     _env(rank, world, port)
+    torch.set_num_threads(max(1, 8 // world))
     from importlib import import_module
     runner = import_module(f"{PKG}.fed.runner")
     config = import_module(f"{PKG}.config")
@@ -120,3 +147,21 @@ def test_two_client_federated_run(tmp_path):
     rep = json.load(open(tmp_path / "federated_report.json"))
     assert len(rep["clients"]) == 2
     assert (tmp_path / "client1_plots" / "metrics_comparison.png").exists()
+
+
+def test_eight_client_federated_run(tmp_path):
+    """BASELINE.json config 4's protocol in miniature: 8 clients x 2 rounds over gloo (1-layer
+    model): every client finishes both rounds, holds the global aggregate, and rank 0's report
+    lists all eight."""
+    port = _free_port()
+    mp.spawn(_fed_worker, args=(8, port, str(tmp_path)), nprocs=8, join=True)
+    g = torch.load(tmp_path / "ddos_distilbert_model.pth", weights_only=True)
+    for cid in range(1, 9):
+        st = json.load(open(tmp_path / f"client{cid}_fed_state.json"))
+        assert st["completed_rounds"] == 2 and [h["round"] for h in st["history"]] == [1, 2]
+        assert (tmp_path / f"client{cid}_aggregated_metrics_round2.csv").exists()
+        c = torch.load(tmp_path / f"client{cid}_model.pth", weights_only=True)
+        assert all(torch.equal(c[k], g[k]) for k in g), cid
+    rep = json.load(open(tmp_path / "federated_report.json"))
+    assert rep["world_size"] == 8 and len(rep["clients"]) == 8
+    assert [c["client"] for c in rep["clients"]] == list(range(1, 9))

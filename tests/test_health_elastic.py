@@ -25,16 +25,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, dead=1):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     from importlib import import_module
     comm = import_module(f"{PKG}.parallel.comm")
     health = import_module(f"{PKG}.parallel.health")
     comm.init_distributed(device="cpu")
+    import torch
+    torch.set_num_threads(1)
     mon = health.start(interval=0.2, stale_s=2.0, timeout_s=60.0)
     mon.barrier("warm")  # everyone alive: passes
-    if rank == 1:
+    if rank == dead:
         mon.stop()
         time.sleep(30)  # hangs without beating (a wedged process looks the same as a dead one)
         os._exit(0)
@@ -44,7 +46,7 @@ def _worker(rank, world, port, outdir):
         res = "no failure detected"
     except health.PeerFailure as e:
         res = f"dead={e.dead} after {time.monotonic() - t0:.1f}s"
-    with open(os.path.join(outdir, "result.txt"), "w") as f:
+    with open(os.path.join(outdir, f"result{rank}.txt" if world > 2 else "result.txt"), "w") as f:
         f.write(res)
     os._exit(0)
 
@@ -62,6 +64,27 @@ def test_dead_peer_detected_fast(tmp_path):
     res = (tmp_path / "result.txt").read_text()
     assert res.startswith("dead=[1]"), res
     assert float(res.split("after ")[1][:-1]) < 15
+
+
+def test_dead_peer_detected_fast_eight_ranks(tmp_path):
+    """N = 8 (the target node): rank 5 wedges; EVERY survivor names it within seconds."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_worker, args=(r, 8, port, str(tmp_path), 5)) for r in range(8)]
+    for p in ps:
+        p.start()
+    for r, p in enumerate(ps):
+        if r != 5:
+            p.join(120)
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    for r in range(8):
+        if r == 5:
+            continue
+        res = (tmp_path / f"result{r}.txt").read_text()
+        assert res.startswith("dead=[5]"), (r, res)
+        assert float(res.split("after ")[1][:-1]) < 20
 
 
 def test_elastic_restart_resumes_round(tmp_path):
@@ -109,6 +132,29 @@ def test_elastic_restart_after_fedavg_first_round(tmp_path):
     for cid in (1, 2):
         c = torch.load(tmp_path / f"client{cid}_model.pth", weights_only=True)
         assert all(torch.equal(g[k], c[k]) for k in g)
+
+
+def test_elastic_restart_eight_clients(tmp_path):
+    """N = 8: client 6 is killed in round 2; the restarted 8-process group resumes from the
+    round-1 aggregate and all eight clients finish both rounds on the same final aggregate."""
+    import torch
+    env = dict(os.environ, FEDDDOS_KILL_CLIENT="5", FEDDDOS_KILL_ROUND="1", PYTHONPATH=ROOT,
+               CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", PKG, "launch", "--nproc", "8", "--port", str(_free_port()), "--max-restarts", "1",
+           "--out-dir", str(tmp_path), "--synthetic-rows", "600", "--max-len", "64", "--epochs", "1",
+           "--batch-size", "8", "--eval-batch-size", "32", "--rounds", "2", "--plots", "false", "--layers", "1",
+           "--heartbeat-s", "0.2", "--heartbeat-stale-s", "5"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    log = out.stdout + out.stderr
+    assert out.returncode == 0, log[-3000:]
+    assert (tmp_path / ".killed_client5_round1_r0").exists()
+    assert "elastic restart #1" in log
+    g = torch.load(tmp_path / "ddos_distilbert_model.pth", weights_only=True)
+    for cid in range(1, 9):
+        st = json.load(open(tmp_path / f"client{cid}_fed_state.json"))
+        assert st["completed_rounds"] == 2, cid
+        c = torch.load(tmp_path / f"client{cid}_model.pth", weights_only=True)
+        assert all(torch.equal(g[k], c[k]) for k in g), cid
 
 
 def _tiny_client(tmp_path):
