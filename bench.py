@@ -465,7 +465,10 @@ def _fedavg_timing(model, di, fedavg, comm, ncomm, k, sync):
     f = comm.all_reduce_max(min(fed))
     f0 = comm.all_reduce_max(fed[0])  # the first round after the timed steps (what a real round sees)
     r = comm.all_reduce_max(min(raw))
-    return {"fedavg_round_ms": round(1e3 * f0, 3), "fedavg_ms": round(1e3 * f, 3), "allreduce_ms": round(1e3 * r, 3),
+    fm = comm.all_reduce_max(float(np.median(fed)))
+    return {"fedavg_round_ms": round(1e3 * f0, 3), "fedavg_ms": round(1e3 * f, 3),
+            "fedavg_round_ms_median": round(1e3 * fm, 3), "fedavg_rounds_timed": len(fed),
+            "allreduce_ms": round(1e3 * r, 3),
             "allreduce_bytes": nbytes,
             "allreduce_busbw_GBps": round(2.0 * (n - 1) / n * nbytes / r / 1e9, 2)}
 

@@ -197,6 +197,18 @@ DEV void sk_head_row(const SkArgs& a, int m, int t, bool act, int n, const float
     H.lpart[m] = hr ? hs[2] / H.B : 0.f;
     H.dbpart[2 * m] = d0;
     H.dbpart[2 * m + 1] = d1;
+    // The batch loss inside this launch (valid as soon as the forward returns, not only after the
+    // deferred column sums of the backward): the last row block to finish sums the M row losses in
+    // row order (deterministic) and re-arms the ticket for the next launch / graph replay.
+    __threadfence();
+    const unsigned done = __hip_atomic_fetch_add(H.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == gridDim.x - 1) {
+      __threadfence();
+      float s = 0.f;
+      for (int r = 0; r < (int)gridDim.x; ++r) s += H.lpart[r];
+      *H.loss = s;
+      __hip_atomic_store(H.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   const bool grad_row = hr && !(H.own && H.own[m] == H.own[m + 1]);
   const bool hdrop = H.thr != 0;
@@ -386,7 +398,8 @@ int fd_splitk_epilogue(int epi, const float* slabs, long long sstride, int split
   if (ln) a.ln = *ln;
   if (hd && hd->W) {  // the fused head: LayerNorm forward only, N = 768, every output buffer given
     if (epi != SK_LN || N != 768 || hd->B <= 0 || hd->B > M || !hd->labels || !hd->logits || !hd->dlogits ||
-        !hd->dz || !hd->colpart || !hd->hpart || !hd->dbpart || !hd->lpart || !hd->bias || !hd->seed_ptr ||
+        !hd->dz || !hd->colpart || !hd->hpart || !hd->dbpart || !hd->lpart || !hd->loss || !hd->ticket ||
+        !hd->bias || !hd->seed_ptr ||
         (ln && ln->thr && !hd->dx))
       return 8;
     a.hd = *hd;

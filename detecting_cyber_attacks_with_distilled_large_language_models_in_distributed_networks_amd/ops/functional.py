@@ -208,7 +208,7 @@ class LayerFn(torch.autograd.Function):
         qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
         dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
         cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask)
-        fuse_ln = rc.fuse_ln and K.ln_fusable(x.shape[0], x.shape[1])
+        fuse_ln = rc.fuse_ln and K.ln_fusable(x.shape[0], x.shape[1], K=(x.shape[1], L["l2_w"].shape[1]))
         if fuse_ln:
             # bias + (dropout) + residual + LayerNorm in the N = 768 GEMMs' epilogues; the
             # backward reads the saved bf16 pre-LN sums z1 / z2 instead of ao / f

@@ -514,18 +514,29 @@ def set_shared_device(shared: bool) -> None:
     _SHARED_DEVICE = bool(shared)
 
 
-def ln_fusable(M: int, N: int, concurrent_collectives: bool = False) -> bool:
+_LN2_FLAGS = 512  # csrc/binding.cpp gemm_ln: the two-K-half exchange's flag granules
+
+
+def ln_fusable(M: int, N: int, concurrent_collectives: bool = False, K=None) -> bool:
     """Whether a LayerNorm-fused GEMM of M rows x N (= hidden) columns runs as one resident
     round (its row blocks exchange statistics, so no tile may wait on an undispatched peer):
     at most one 128 x 64 tile per CU, no other process on the device, and no collective of this
     process in flight beside it (``concurrent_collectives``: a data-parallel client's gradient
     all-reduces overlapping the backward -- RCCL's kernels hold CUs and LDS while they wait on a
     slower replica, so a fused tile's row-block peers might not get a CU until the 0.25 s
-    rendezvous timeout).  Otherwise the plain GEMMs + separate LayerNorm kernels."""
+    rendezvous timeout).  Otherwise the plain GEMMs + separate LayerNorm kernels.
+    K (an int or the inner sizes of every GEMM the caller will fuse): the 256-row two-K-half route
+    is counted only where the launcher takes it (gemm.hip fd_gemm_ln ``ln2_ok``: K % 128 == 0, no
+    FD_GEMM_LN_CFG / LN_CFG override, and the exchange flags of binding.cpp's capacity) -- a shape
+    judged fusable here never makes ``gemm_ln`` raise instead of falling back."""
     if _SHARED_DEVICE or concurrent_collectives:
         return False
     tiles = ((M + 127) // 128) * (N // 64)
-    if LN2 and N % 128 == 0:  # (gemm.hip fd_gemm_ln: 256-row two-K-half tiles past 128-row round)
+    ks = () if K is None else ((K,) if isinstance(K, int) else tuple(K))
+    ln2_ok = (LN2 and N % 128 == 0 and all(k % 128 == 0 for k in ks) and LN_CFG < 0
+              and int(_os.environ.get("FD_GEMM_LN_CFG", "-1")) < 0
+              and ((M + 127) // 128) * (N // 128) * 2 <= _LN2_FLAGS)
+    if ln2_ok:  # (gemm.hip fd_gemm_ln: 256-row two-K-half tiles past the 128-row round)
         tiles = min(tiles, ((M + 255) // 256) * (N // 64))
     return N % 64 == 0 and N <= 2048 and tiles <= min(LN_MAX_TILES, _cu_count())
 
@@ -579,13 +590,28 @@ def head_in_sk_ok(M: int, N: int, K: int) -> bool:
     return HEAD_IN_SK and FUSE_HEAD and N == 768 and _splitk_ok(M, N, K)
 
 
+_HEAD_TICKETS = {}
+
+
+def _head_ticket(dev) -> torch.Tensor:
+    """The fused head's completion counter (int32 [1], zero between launches: the launch's last row
+    block re-arms it), one per device."""
+    t = _HEAD_TICKETS.get(dev)
+    if t is None:
+        t = _HEAD_TICKETS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return t
+
+
 def linear_ln_fwd_head(x, w, b, res, gamma, beta, eps, seed, site, p, row_map, hW, hb, head_site, p_head, labels,
                        B, own, kd, dW, db, acc_head, dgamma, dbeta, dbias, acc_ln, jobs, loss_acc=None):
     """``linear_ln_fwd`` on the pruned [CLS] rows (split-K) with the head fused into its epilogue:
     per row the head logits / loss / dlogits, the head gradient of the row (the loss's upstream
     gradient is 1) and the LayerNorm backward of it.  The head dW / db, the loss mean (and the
     running ``loss_acc``) and the LayerNorm affine gradients are column sums of per-row partials,
-    appended to the deferred ``jobs``.  Returns (y, z, mean, rstd, (logits, loss, dz, dx))."""
+    appended to the deferred ``jobs``; the loss mean itself is finished inside the launch (its last
+    row block sums the row losses in row order), so ``loss`` is valid as soon as the forward returns
+    (it used to be filled only by the backward's deferred sums).
+    Returns (y, z, mean, rstd, (logits, loss, dz, dx))."""
     M, N = x.shape[0], w.shape[0]
     dev = x.device
     y = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
@@ -609,13 +635,13 @@ def linear_ln_fwd_head(x, w, b, res, gamma, beta, eps, seed, site, p, row_map, h
         t = t.detach().float().contiguous()
     _splitk(EPI_LN, x, w, y, bias=b, res=res, gamma=gamma, beta=beta, mean=mean, rstd=rstd, z=z, eps=eps,
             seed=seed, site=site, thr=thr, dscale=sc, row_map=row_map if thr else None,
-            head=[hW, hb, labels, logits, dlogits, dz, colpart, hpart, dbpart, lpart, seed],
+            head=[hW, hb, labels, logits, dlogits, dz, colpart, hpart, dbpart, lpart, seed, loss.view(1),
+                  _head_ticket(dev)],
             head_f=[float(head_site), float(hthr), float(hsc), float(kT), float(alpha), float(B)],
             head_dx=dx, head_tlogits=t, head_own=own)
     jobs.append((colpart, [dgamma, dbeta, dbias], M, 3 * N, N, acc_ln))
     jobs.append((hpart, [dW[0], dW[1]], M, 2 * N, N, acc_head))
     jobs.append((dbpart, [db[0:1], db[1:2]], M, 2, 1, acc_head))
-    jobs.append((lpart, [loss.view(1)], M, 1, 1, False))
     if loss_acc is not None:
         jobs.append((lpart, [loss_acc], M, 1, 1, True))
     return y, z, mean, rstd, (logits, loss, dz, dx if dx is not None else dz)

@@ -298,10 +298,13 @@ def test_head_in_output_ln_epilogue(packed, B, empty, kd, monkeypatch):
             monkeypatch.setattr(K, "head_ln_bwd", lambda *a, **k: (calls.append(1), real(*a, **k))[1])
             loss, logits = m.forward_loss(ids, mask, labels, tokens=tokens if packed else None, kd=t,
                                           unit_backward=True)
+            torch.cuda.synchronize()
+            before = loss.detach().clone()  # (valid before the backward, too)
             loss.backward(K.unit_grad("cuda"))
             monkeypatch.setattr(K, "head_ln_bwd", real)
             assert len(calls) == (0 if in_sk else 1)
             torch.cuda.synchronize()
+            assert torch.equal(before, loss.detach())
             res.append((loss.detach().clone(), logits.detach().clone()))
         outs.append((res, m.arena.grad.clone(), {k: m.dense_grad(k).clone() for k in m.state_dict()}))
     (r0, g0, d0), (r1, g1, d1) = outs
@@ -332,3 +335,27 @@ def test_fused_head_rejects_a_foreign_backward_seed():
     (loss * 2.0).backward()
     torch.cuda.synchronize()
     assert torch.isfinite(m.arena.grad).all()
+
+
+def test_head_in_epilogue_loss_valid_before_backward():
+    """with the head inside the output-LayerNorm epilogue the loss is finished inside that
+    forward launch (its last row block sums the row losses), so a NaN guard or a log line reading
+    it between forward and backward sees the real mean cross-entropy of the returned logits -- over
+    several launches in a row (the completion ticket re-arms itself)."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import kernels as K
+    if not (K.HEAD_IN_SK and K.FUSE_HEAD):
+        pytest.skip("head not in the output-LayerNorm epilogue")
+    m = DDoSClassifier(config=DistilBertConfig(n_layers=2), device="cuda", impl="hip", seed=44)
+    m.train()
+    for it in range(3):
+        ids, mask, labels, tokens = _batch(32, 128, seed=900 + it)
+        m.rng.fill_(11 + it)
+        loss, logits = m.forward_loss(ids, mask, labels, tokens=tokens, unit_backward=True)
+        torch.cuda.synchronize()
+        ref = torch.nn.functional.cross_entropy(logits.double(), labels.cuda().long()).item()
+        got = loss.item()
+        assert abs(got - ref) <= 1e-5 * max(1.0, abs(ref)), (it, got, ref)
+        loss.backward(K.unit_grad("cuda"))
+        torch.cuda.synchronize()
+        assert loss.item() == got
+    assert int(K._head_ticket(torch.device("cuda", torch.cuda.current_device())).item()) == 0
