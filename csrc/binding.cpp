@@ -42,6 +42,8 @@ int fd_gemm_dw2_splits(int M0, int N0, int M1, int N1, int K);
 int fd_gemm_dw_batch(int n, const FdDwProb* probs, int K, const int* step, const float* hyper, int cfg,
                      const FdAdamRest* rest, hipStream_t st);
 int fd_gemm_ln_set_diag(int diag);
+int fd_gemm_dwb_set_mix(int mode);
+long long fd_gemm_dwb_mixed_launches();
 int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, float* workspace,
                    long long workspace_elems, int splits, const float* bias, void* C, void* aux, void* aux_out,
                    const void* res, float* colsum, int* colsum_blocks, const FdLnEpi* ln, const FdSkHead* hd,
@@ -1508,6 +1510,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("thr"), py::arg("dscale"), py::arg("row_map") = py::none(), py::arg("ln_epoch") = py::none(),
         py::arg("sorted") = py::none(), py::arg("perm") = py::none(), py::arg("ln_stats") = py::none());
   m.def("gemm_ln_set_diag", [](int64_t d) { fd_gemm_ln_set_diag((int)d); });
+  m.def("gemm_dwb_set_mix", [](int64_t mode) { return (int64_t)fd_gemm_dwb_set_mix((int)mode); },
+        "all-layer dW launch schedule: 0 plain, 1 mixed tiles when shorter (default), 2 forced; returns the old mode");
+  m.def("gemm_dwb_mixed_launches", []() { return (int64_t)fd_gemm_dwb_mixed_launches(); });
   m.def("emb_bwd", &emb_bwd);
   m.def("colsum_bf16", &colsum_bf16);
   m.def("colsum_bf16_batched", &colsum_bf16_batched);

@@ -36,6 +36,7 @@ struct FdDwProb {
   // nullable: also bias[m] (+)= sum_k A[k][m] -- the producer's bias gradient (the qkv bias: A is
   // dqkv), summed by the tiles of the first column block while their K loops read A anyway
   float* bias;
+  int half;           // filled by the launcher: 1 = tiled 256 x 128 (the mixed schedule's tail class)
 };
 
 // The rest of the optimizer step, run by extra blocks of the all-layer dW launch beside its last

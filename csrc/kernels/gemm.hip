@@ -1364,10 +1364,22 @@ struct DwBatch {
   float lr, b1, b2, eps, wd;
   int decoupled;
   FdAdamRest rest;  // rest.p != nullptr: blocks [ntiles, ntiles + rest blocks) finish the optimizer step
+  // Mixed schedule (fd_gemm_dw_batch plan_dwb_mix; mixed != 0): problems are ordered in three classes
+  // -- [long 256 x 256 | long 256 x 128 (half) | short-K 256 x 256] -- and each class is dealt to the
+  // 8 XCDs in contiguous ranges of cls_pad[c] blocks per XCD (padding blocks return at once), so every
+  // XCD runs its full-size long tiles first, then its share of the half tiles and short tiles in the
+  // rounds the long tiles leave partly idle.
+  int mixed;
+  int cls_tiles[3], cls_off[3], cls_pad[3];
 };
 
+// The mixed schedule's half tiles: 256 x 128 on the same 8 waves (4 x 2, 64 x 64 per wave).  Every
+// output element runs the same K-step / MFMA chain as in a 256 x 256 tile and the same f32_epilogue
+// (Adam) arithmetic, so a problem's gradient and optimizer step are bitwise those of the full tiles.
+constexpr int DWB_HBM = 256, DWB_HBN = 128, DWB_HWM = 4, DWB_HWN = 2;
+
 // One tile of the batch: logical tile id lid -> (problem, tile) -> K loop + epilogue.
-template <int BM, int BN, int WM, int WN, int S, int BK>
+template <int BM, int BN, int WM, int WN, int S, int BK, bool MIX = false>
 DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
   int i = 0;
   while (i + 1 < bt.n && lid >= bt.pr[i + 1].tile0) ++i;  // block-uniform
@@ -1393,7 +1405,27 @@ DEV void dwb_tile(const DwBatch& bt, int lid, char* smem) {
       p.acol_sh = bt.rest.sh ? bt.rest.sh + off : nullptr;
     }
   }
+  if constexpr (MIX) {
+    if (q.half) {  // block-uniform
+      gemm_tile<DWB_HBM, DWB_HBN, false, false, EPI_F32, DWB_HWM, DWB_HWN, S, BK>(p, lid - q.tile0, smem);
+      return;
+    }
+  }
   gemm_tile<BM, BN, false, false, EPI_F32, WM, WN, S, BK>(p, lid - q.tile0, smem);
+}
+
+// Mixed schedule: tile block b (past the rest blocks, whose count is a multiple of 8, so b % 8 is
+// the block's XCD) -> logical tile id, or -1 for a padding block.
+DEV int dwb_mixed_lid(const DwBatch& bt, int b) {
+  const int x = b % 8;
+  int j = b / 8, c = 0;
+  while (c < 2 && j >= bt.cls_pad[c]) {
+    j -= bt.cls_pad[c];
+    ++c;
+  }
+  if (j >= bt.cls_pad[c]) return -1;
+  const int t = x * bt.cls_pad[c] + j;
+  return t < bt.cls_tiles[c] ? bt.cls_off[c] + t : -1;
 }
 
 // Blocks past the tiles: the rest of the optimizer step (FdAdamRest), dispatched after every tile,
@@ -1466,11 +1498,19 @@ DEV void dwb_rest(const DwBatch& bt, int rb, char* smem) {
     adam_rows16(a, r0, r.wrows, r.wrow4, lane, ss, inv);
 }
 
-template <int BM, int BN, int WM, int WN, int S, int BK = BKT>
-__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch bt) {
+template <int BM, int BN, int WM, int WN, int S, int BK, bool MIX>
+constexpr int dwb_smem() {
   using G = GemmCfg<BM, BN, false, false, EPI_F32, WM, WN, S, BK>;
-  static_assert(G::SMEM <= LDS_MAX, "LDS");
-  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  using H = GemmCfg<DWB_HBM, DWB_HBN, false, false, EPI_F32, DWB_HWM, DWB_HWN, S, BK>;
+  return MIX && H::SMEM > G::SMEM ? H::SMEM : G::SMEM;
+}
+
+template <int BM, int BN, int WM, int WN, int S, int BK = BKT, bool MIX = false>
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch bt) {
+  constexpr int SMEM = dwb_smem<BM, BN, WM, WN, S, BK, MIX>();
+  static_assert(SMEM <= LDS_MAX, "LDS");
+  static_assert(!MIX || (BM == DWB_HBM && WM * WN == DWB_HWM * DWB_HWN), "mixed tiles share the block shape");
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   // the rest blocks lead the grid (their HBM stream beside the first round's K loops, while the
   // memory is otherwise idle) or follow the tiles (on the CUs the last, partial round leaves idle);
   // a leading group is a multiple of 8 blocks, so every tile keeps its XCD under xcd_remap
@@ -1482,9 +1522,19 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_dw_batch_kernel(DwBatch 
       return;
     }
     bid -= nrest;
-  } else if (bid >= bt.ntiles) {
-    dwb_rest<64 * WM * WN>(bt, bid - bt.ntiles, smem);
-    return;
+  } else {
+    const int nblk = MIX && bt.mixed ? 8 * (bt.cls_pad[0] + bt.cls_pad[1] + bt.cls_pad[2]) : bt.ntiles;
+    if (bid >= nblk) {
+      dwb_rest<64 * WM * WN>(bt, bid - nblk, smem);
+      return;
+    }
+  }
+  if constexpr (MIX) {
+    if (bt.mixed) {
+      const int lid = dwb_mixed_lid(bt, bid);
+      if (lid >= 0) dwb_tile<BM, BN, WM, WN, S, BK, true>(bt, lid, smem);
+      return;
+    }
   }
   dwb_tile<BM, BN, WM, WN, S, BK>(bt, xcd_remap(bid, bt.ntiles), smem);
 }
@@ -1952,22 +2002,112 @@ int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const
 bool dwb_launch_cfg(int id, DwBatch& bt, hipStream_t st, bool dry) {
   auto go = [&](auto kern, int bm, int bn, int threads) {
     for (int i = 0; i < bt.n; ++i)
-      if (bt.pr[i].M % bm || bt.pr[i].N % bn) return false;
+      if (bt.pr[i].M % bm || bt.pr[i].N % (bt.pr[i].half ? DWB_HBN : bn)) return false;
     int t = 0;
     for (int i = 0; i < bt.n; ++i) {
       bt.pr[i].tile0 = t;
-      t += (bt.pr[i].M / bm) * (bt.pr[i].N / bn);
+      t += (bt.pr[i].M / bm) * (bt.pr[i].N / (bt.pr[i].half ? DWB_HBN : bn));
     }
     bt.ntiles = t;
-    if (!dry) hipLaunchKernelGGL(kern, dim3(t + bt.rest.flat_blocks + bt.rest.row_blocks), dim3(threads), 0, st, bt);
+    const int nblk = bt.mixed ? 8 * (bt.cls_pad[0] + bt.cls_pad[1] + bt.cls_pad[2]) : t;
+    if (!dry) hipLaunchKernelGGL(kern, dim3(nblk + bt.rest.flat_blocks + bt.rest.row_blocks), dim3(threads), 0, st, bt);
     return true;
   };
+  if (bt.mixed && id != 11) return false;
   switch (id) {
     case 1: return go(gemm_dw_batch_kernel<128, 128, 2, 2, 2>, 128, 128, 256);
     case 8: return go(gemm_dw_batch_kernel<128, 64, 2, 2, 2>, 128, 64, 256);
-    case 11: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 2>, 256, 256, 512);
+    case 11: return go(gemm_dw_batch_kernel<256, 256, 2, 4, 2, BKT, true>, 256, 256, 512);
   }
   return false;
+}
+
+// FD_DWB_MIX / fd_gemm_dwb_set_mix: 0 off, 1 (default) when it shortens the schedule, 2 forced
+// (tests: any launch with at least two long problems gets a half-tile class)
+int g_dwb_mix = -1;
+long long g_dwb_mixed_launches = 0;  // (tests: proof the mixed schedule ran)
+
+int dwb_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess)
+      n = 0;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
+// The all-layer launch's tile rounds (256 x 256 tiles, one block per CU).  The bs32 step has 567
+// long tiles (K = the packed tokens) and 81 short ones (the pruned block's K = 64 [CLS] rows): with
+// the XCD remap's equal-count ranges XCD 0 got every short tile and XCDs 1..7 81 long tiles each --
+// three rounds of long tiles, the third at 17 / 32 occupancy.  Plan instead: long tiles in whole
+// rounds, the excess long work E as 256 x 128 half tiles of whole problems (the smallest subset of
+// long problems holding >= E tiles), and every class dealt evenly over the XCDs, so the half and
+// short tiles share ONE partial round.  Returns whether it applies (else the launch is unchanged).
+bool plan_dwb_mix(DwBatch& bt, int mode) {
+  if (mode <= 0 || bt.n < 2) return false;
+  const int cus = dwb_cus();
+  int kmax = 0;
+  for (int i = 0; i < bt.n; ++i) kmax = std::max(kmax, bt.pr[i].K > 0 ? bt.pr[i].K : bt.K);
+  int cls[DWB_MAXP], tiles[DWB_MAXP], L = 0, Sh = 0, nlong = 0;
+  for (int i = 0; i < bt.n; ++i) {
+    const DwProb& q = bt.pr[i];
+    if (q.M % 256 || q.N % 256) return false;
+    const int k = q.K > 0 ? q.K : bt.K;
+    tiles[i] = (q.M / 256) * (q.N / 256);
+    cls[i] = 8 * k <= kmax ? 2 : 0;
+    if (cls[i] == 0) { L += tiles[i]; ++nlong; } else Sh += tiles[i];
+  }
+  if (nlong < 2) return false;
+  const int rounds = L / cus, E = L - rounds * cus;
+  int target = E;
+  if (mode == 1 && (rounds == 0 || E == 0)) return false;
+  if (mode == 2 && target == 0) target = 1;
+  // smallest subset sum >= target over the long problems (reachable sums; <= 32 problems)
+  std::vector<int> from(L + 1, -2);  // from[s]: last problem added to reach sum s (-1: empty set)
+  from[0] = -1;
+  std::vector<int> used_at(L + 1, 0);
+  for (int i = 0; i < bt.n; ++i) {
+    if (cls[i]) continue;
+    for (int s = L; s >= tiles[i]; --s)
+      if (from[s] == -2 && from[s - tiles[i]] != -2 && s - tiles[i] >= 0) {
+        // (0/1 knapsack, descending s: problem i is used at most once per reachable sum)
+        from[s] = i;
+        used_at[s] = s - tiles[i];
+      }
+  }
+  int best = -1;
+  for (int s = target; s <= L; ++s)
+    if (from[s] != -2 && s < L) { best = s; break; }
+  if (best < 0) return false;
+  // the half + short tiles must fit the partial round's free blocks per XCD
+  const int per = cus / 8;
+  const int big_x = (L - best + 7) / 8, tail_x = (2 * best + 7) / 8 + (Sh + 7) / 8;
+  const int free_x = (rounds * per > big_x ? rounds * per - big_x : 0) + per;
+  if (mode == 1 && (big_x > rounds * per || tail_x > free_x)) return false;
+  for (int s = best; s > 0; s = used_at[s]) cls[from[s]] = 1;
+  // stable reorder by class: long full tiles, long half tiles, short
+  DwProb pr[DWB_MAXP];
+  int k = 0;
+  for (int c = 0; c < 3; ++c) {
+    int t = 0;
+    for (int i = 0; i < bt.n; ++i)
+      if (cls[i] == c) {
+        pr[k] = bt.pr[i];
+        pr[k].half = c == 1;
+        ++k;
+        t += c == 1 ? 2 * tiles[i] : tiles[i];
+      }
+    bt.cls_tiles[c] = t;
+    bt.cls_pad[c] = (t + 7) / 8;
+  }
+  for (int i = 0; i < bt.n; ++i) bt.pr[i] = pr[i];
+  bt.cls_off[0] = 0;
+  bt.cls_off[1] = bt.cls_tiles[0];
+  bt.cls_off[2] = bt.cls_tiles[0] + bt.cls_tiles[1];
+  bt.mixed = 1;
+  return true;
 }
 
 int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const float* hyper, int cfg,
@@ -2019,6 +2159,16 @@ int fd_gemm_dw_batch(int n, const DwProb* probs, int K, const int* step, const f
   bt.group_m = 64;
   static const int gm_env = [] { const char* e = getenv("FD_DWB_GROUP_M"); return e ? atoi(e) : 0; }();
   if (gm_env > 0) bt.group_m = gm_env;  // tuning override
+  if (g_dwb_mix < 0) {
+    const char* e = getenv("FD_DWB_MIX");
+    g_dwb_mix = e ? atoi(e) : 1;
+  }
+  if (id == 11 && plan_dwb_mix(bt, g_dwb_mix) && !dwb_launch_cfg(id, bt, st, true)) {
+    // (a shape the half tiles do not cover: the plain schedule)
+    bt.mixed = 0;
+    for (int i = 0; i < n; ++i) bt.pr[i] = probs[i];
+  }
+  if (bt.mixed) ++g_dwb_mixed_launches;
   if (!dwb_launch_cfg(id, bt, st, true)) {
     id = 8;  // 128 x 64 fits every supported shape (M % 128, N % 64)
     if (!dwb_launch_cfg(id, bt, st, true)) return 4;
@@ -2053,6 +2203,14 @@ int fd_splitk_reduce_batched(int n, const float* const* slabs, float* const* out
 // cfg < 0: FD_GEMM_LN_CFG or 24 (128 x 64, 8 waves, two K tiles per barrier -- the N = 768
 // configuration of the plain GEMM).  Returns the number of row blocks (the colpart rows),
 // or a negative code on an unsupported shape (nothing launched).
+long long fd_gemm_dwb_mixed_launches() { return g_dwb_mixed_launches; }
+
+int fd_gemm_dwb_set_mix(int mode) {
+  const int old = g_dwb_mix;
+  g_dwb_mix = mode;
+  return old;
+}
+
 int fd_gemm_ln_set_diag(int diag) {
   g_ln_diag = diag;
   return 0;

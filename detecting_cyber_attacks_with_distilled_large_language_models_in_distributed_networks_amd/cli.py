@@ -5,6 +5,8 @@
            --client-index k`` it is the reference's ``python clientK.py``
   server   the reference's ``python server.py``: TCP gather -> FedAvg -> broadcast
   launch   spawn N local ranks (torch.distributed.run, 127.0.0.1) running ``client``
+  virtual  N federated clients x R FedAvg rounds in ONE process on one device, trained in turn
+           (BASELINE.json config 4's protocol on a single GPU): per-round CSVs + virtual_report.json
   predict  classify every row of a CICIDS2017-format CSV with a trained checkpoint (serving path:
            unpadded HIP forward replayed from HIP graphs); writes probabilities + labels
   bench    the headline benchmark (bench.py)
@@ -92,6 +94,62 @@ def _launch(argv):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     sys.exit(subprocess.call(cmd, env=env))
+
+
+def _virtual(argv):
+    """``--clients N`` virtual clients x ``--rounds R`` (fed/runner.py run_virtual_clients): client k
+    samples its own 10 % with seed 42 + k, every round starts from the previous aggregate with a
+    fresh Adam, the aggregate is the unweighted mean (server.py:67-79) and every client evaluates it
+    on its own test split.  Writes clientK_{local,aggregated}_metrics[_roundR].csv (run_round's
+    names), the final aggregate ddos_distilbert_model.pth (+ its round tag) and virtual_report.json."""
+    ap = argparse.ArgumentParser(prog="virtual")
+    FedConfig.add_cli(ap)
+    ap.add_argument("--clients", type=int, default=2)
+    ap.add_argument("--layers", type=int, default=None, help="override DistilBERT depth (tests)")
+    ns = ap.parse_args(argv)
+    cfg = FedConfig.from_args(ns)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):  # one process, whatever launched it
+        os.environ.pop(k, None)
+    from .fed.runner import FederatedClient, run_virtual_clients
+    from .models import DistilBertConfig
+    from .utils import checkpoint as ck
+    from .utils.metrics import save_metrics
+    mc = DistilBertConfig() if ns.layers is None else DistilBertConfig(n_layers=ns.layers)
+    cfg.num_clients = ns.clients
+    client = FederatedClient(cfg, model_config=mc)
+    client.setup()
+    log = client.log
+    res = run_virtual_clients(client, ns.clients, rounds=cfg.rounds, progress=log.info)
+    os.makedirs(cfg.out_dir, exist_ok=True)
+
+    def tup(m):
+        return (m["accuracy"], m["loss"], m["precision"], m["recall"], m["f1"])
+
+    report = {"clients": ns.clients, "rounds": []}
+    for h in res["rounds"]:
+        r = h["round"]
+        sfx = "" if r == 1 else f"_round{r}"
+        for c in h["clients"]:
+            k = c["client"]
+            save_metrics(tup(c["local_test"]), os.path.join(cfg.out_dir, f"client{k}_local_metrics{sfx}.csv"))
+            save_metrics(tup(c["aggregated_test"]), os.path.join(cfg.out_dir, f"client{k}_aggregated_metrics{sfx}.csv"))
+        (tn, fp), (fn, tp) = h["aggregated_confusion"]
+        report["rounds"].append({
+            "round": r, "fedavg_ms": h["fedavg_ms"], "aggregated_confusion": h["aggregated_confusion"],
+            "aggregated_accuracy": 100.0 * (tp + tn) / max(tp + tn + fp + fn, 1),
+            "clients": [{"client": c["client"], "local_test": c["local_test"], "aggregated_test": c["aggregated_test"],
+                         "epoch_losses": c["train"]["epoch_losses"], "train_steps": c["train"]["steps"],
+                         "rel_l2_local_to_aggregate": c["rel_l2_local_to_aggregate"],
+                         **({"teacher_test": c["teacher_test"]} if "teacher_test" in c else {})}
+                        for c in h["clients"]]})
+    if cfg.save_checkpoints:
+        ck.save_global(client.model, cfg.out_dir, cfg.rounds)
+    path = os.path.join(cfg.out_dir, "virtual_report.json")
+    with open(path, "w") as f:
+        json.dump(report, f, indent=1)
+    log.info(f"virtual federated report written to {path}")
+    print(json.dumps({"report": path, "rounds": [
+        {"round": r["round"], "aggregated_accuracy": round(r["aggregated_accuracy"], 4)} for r in report["rounds"]]}))
 
 
 def _predict(argv):
@@ -201,7 +259,8 @@ def _tokenize(argv):
     print(tok(text, max_length=128)["input_ids"])
 
 
-COMMANDS = {"client": _client, "server": _server, "launch": _launch, "predict": _predict, "bench": _bench,
+COMMANDS = {"client": _client, "server": _server, "launch": _launch, "virtual": _virtual, "predict": _predict,
+            "bench": _bench,
             "scaling": _scaling,
             "gen-data": _gen_data, "tokenize": _tokenize}
 

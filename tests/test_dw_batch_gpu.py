@@ -178,3 +178,68 @@ def test_colsum_partials_batched_kernel():
     for x, a, b in zip(xs, outs_a, outs_b):
         assert torch.equal(a + 1.0, b)
         assert ((a - x.float().sum(0)).abs().max() / x.float().sum(0).abs().max()).item() < 1e-5
+
+
+def _dw_problems(layers, seed, pruned=True, T=2688):
+    """The packed bs32 step's all-layer dW problems in backward order: the pruned block's lin2 / lin1
+    / out_lin (K = 64 [CLS] rows) and qkv (K = T), then ``layers`` full blocks (K = T)."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    blk = [(768, 3072), (3072, 768), (768, 768), (2304, 768)]
+    spec = ([(64, M, N) for M, N in blk[:3]] + [(T, *blk[3])] if pruned else []) + [(T, M, N) for _ in range(layers)
+                                                                                   for M, N in blk]
+    probs = []
+    for Kt, M, N in spec:
+        dy = (torch.randn(Kt, M, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+        x = torch.randn(Kt, N, device="cuda", generator=g).to(torch.bfloat16)
+        st = [torch.randn(M * N, device="cuda", generator=g), torch.randn(M * N, device="cuda", generator=g) * 1e-3,
+              torch.rand(M * N, device="cuda", generator=g) * 1e-6, torch.empty(M * N, device="cuda", dtype=torch.bfloat16)]
+        probs.append((dy, x, M, N, st))
+    return probs
+
+
+def _run_dw(probs, mode, fused):
+    old = K.ext().gemm_dwb_set_mix(mode)
+    try:
+        n0 = K.ext().gemm_dwb_mixed_launches()
+        jobs, states = [], []
+        for dy, x, M, N, st in probs:
+            bias = torch.zeros(M, device="cuda") if M == 2304 else None  # the qkv bias column sums
+            jobs.append((dy, x, torch.zeros(M, N, device="cuda"), False, bias))
+            states.append([t.clone() for t in st])
+        step = torch.full((1,), 3, dtype=torch.int32, device="cuda")
+
+        def adam(outs):
+            flat = [t for s in states[:len(outs)] for t in s]
+            return flat + [step], [2e-5, 0.9, 0.999, 1e-8, 0.0, 0.0]
+
+        K.linear_dw_batch(jobs, adam=adam if fused else None)
+        torch.cuda.synchronize()
+        mixed = K.ext().gemm_dwb_mixed_launches() - n0
+    finally:
+        K.ext().gemm_dwb_set_mix(old)
+    return jobs, states, mixed
+
+
+@pytest.mark.parametrize("layers,mode", [(5, 1), (2, 2)])
+@pytest.mark.parametrize("fused", [False, True])
+def test_mixed_tile_dw_schedule_bitwise(layers, mode, fused):
+    """The all-layer dW launch's mixed schedule (gemm.hip plan_dwb_mix: long tiles in whole rounds,
+    the excess as 256 x 128 half tiles, every class dealt evenly over the XCDs) against the plain
+    256 x 256 schedule: every gradient, qkv-bias column sum and fused Adam state bitwise.  (5, 1): the
+    bs32 step's own problem set, mixed by the default rule on a 256-CU MI355X; (2, 2): forced."""
+    probs = _dw_problems(layers, seed=17 + layers)
+    ja, sa, ma = _run_dw(probs, 0, fused)
+    jb, sb, mb = _run_dw(probs, mode, fused)
+    assert ma == 0
+    if mode == 2 or torch.cuda.get_device_properties(0).multi_processor_count == 256:
+        assert mb == 1, "the mixed schedule did not run"
+    for (dya, xa, oa, _, ba), (_, _, ob, _, bb), s0, s1 in zip(ja, jb, sa, sb):
+        if not fused:
+            assert torch.equal(oa, ob)
+            ref = dya.float().t() @ xa.float()
+            assert _frel(oa, ref) < 1e-5
+        else:
+            for t0, t1 in zip(s0, s1):
+                assert torch.equal(t0, t1)
+        if ba is not None:
+            assert torch.equal(ba, bb)

@@ -131,3 +131,29 @@ def test_virtual_rounds_bookkeeping(tmp_path):
     # every client ran 1 epoch per round: the last client's counter advanced by its own steps only
     steps = two["rounds"][0]["clients"][-1]["train"]["steps"]
     assert client.model.torch_counter == 2 * steps
+
+
+def test_virtual_cli_writes_per_round_artifacts(tmp_path):
+    """``python -m <pkg> virtual --clients 3 --rounds 2``: the one-process N x R protocol from the
+    command line -- per-client, per-round CSVs in the reference schema, the tagged final aggregate
+    and the JSON report."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", PKG, "virtual", "--clients", "3", "--rounds", "2", "--out-dir", str(tmp_path),
+           "--synthetic-rows", "600", "--max-len", "64", "--epochs", "1", "--batch-size", "8",
+           "--eval-batch-size", "32", "--plots", "false", "--layers", "1", "--verbose", "false"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
+    for k in (1, 2, 3):
+        for name in ("local_metrics.csv", "aggregated_metrics.csv", "local_metrics_round2.csv",
+                     "aggregated_metrics_round2.csv"):
+            assert (tmp_path / f"client{k}_{name}").exists(), (k, name)
+    rep = json.load(open(tmp_path / "virtual_report.json"))
+    assert rep["clients"] == 3 and [r["round"] for r in rep["rounds"]] == [1, 2]
+    assert all(len(r["clients"]) == 3 for r in rep["rounds"])
+    assert json.load(open(tmp_path / "ddos_distilbert_model.json"))["round"] == 2
+    assert (tmp_path / "ddos_distilbert_model.pth").exists()
