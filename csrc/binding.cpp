@@ -435,7 +435,10 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
                 const c10::optional<at::Tensor>& colpart, const at::Tensor& stats, const at::Tensor& cnt,
                 const at::Tensor& err, double eps, const c10::optional<at::Tensor>& seed, int64_t site, int64_t thr,
                 double dscale, const c10::optional<at::Tensor>& row_map, int64_t cfg, int64_t xsite,
-                bool b_mn = false, const c10::optional<at::Tensor>& xbuf = c10::nullopt) {
+                bool b_mn = false, const c10::optional<at::Tensor>& xbuf = c10::nullopt,
+                const c10::optional<at::Tensor>& prefetch = c10::nullopt) {
+  // prefetch: the NEXT launch's weight operand (any dtype, contiguous), touched by the LayerNorm
+  // epilogue while it waits for the row statistics (FdLnEpi::pf)
   // b_mn: Bt is the weight itself, W [K][N] (MN-major B through the LDS-DMA ring, transposing fragment reads)
   need(A, at::kBFloat16, "A");
   need(Bt, at::kBFloat16, "Bt");
@@ -495,6 +498,11 @@ int64_t gemm_ln(bool bwd, const at::Tensor& A, const at::Tensor& Bt, const at::T
   ln.site = (uint32_t)site;
   ln.dscale = (float)dscale;
   ln.xsite = (uint32_t)xsite;
+  if (prefetch.has_value() && prefetch->defined() && prefetch->numel() > 0) {
+    TORCH_CHECK(prefetch->is_cuda() == A.is_cuda() && prefetch->is_contiguous(), "gemm_ln: prefetch must be a contiguous device tensor");
+    ln.pf = reinterpret_cast<const char*>(prefetch->data_ptr());
+    ln.pf_bytes = (long long)(prefetch->numel() * prefetch->element_size());
+  }
   if (thr) {
     TORCH_CHECK(seed.has_value() && seed->defined(), "gemm_ln: dropout needs the seed tensor");
     ln.seed_ptr = seedp(*seed);
@@ -1468,7 +1476,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("rstd"), py::arg("z"),
         py::arg("dx"), py::arg("colpart"), py::arg("stats"), py::arg("cnt"), py::arg("err"), py::arg("eps"),
         py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("row_map"),
-        py::arg("cfg") = -1, py::arg("xsite") = 0, py::arg("b_mn") = false, py::arg("xbuf") = py::none());
+        py::arg("cfg") = -1, py::arg("xsite") = 0, py::arg("b_mn") = false, py::arg("xbuf") = py::none(),
+        py::arg("prefetch") = py::none());
   m.def("gemm_dw_batch", &gemm_dw_batch, py::arg("As"), py::arg("Bs"), py::arg("Cs"), py::arg("accumulate"),
         py::arg("adam"), py::arg("hp"), py::arg("cfg") = -1,
         py::arg("biases") = std::vector<at::Tensor>{}, py::arg("rest") = std::vector<at::Tensor>{},

@@ -219,6 +219,7 @@ int fd_gemm_ln(int bwd, const void* A, const void* Bt, void* C, int M, int N, in
   hc::span(ln->stats, tm * (N / 64) * 2 * bm * 8, "gemm_ln stats");
   hc::span(ln->cnt, 4, "gemm_ln cnt");
   hc::span(ln->err, 4, "gemm_ln err");
+  if (ln->pf) hc::span(ln->pf, ln->pf_bytes, "gemm_ln prefetch");  // (loads one dword per 64 B inside it)
   if (ln->xbuf) {  // two-K-half tiles: pairs x 2 x 32 (128-row) / 64 KiB (256-row) of partials,
                    // pairs x 2 flag granules; the 256-row tiles' statistics rows
     const long long pairs = tm * (N / 128), tm256 = (M + 255) / 256;

@@ -100,6 +100,11 @@ struct FdLnEpi {
   // {tag, 1} granules (the stats buffer's tail: zeroed with it at an epoch wrap).  Nullable.
   float* xbuf;
   uint64_t* xflag;
+  // Next-launch operand prefetch (nullable): while waiting for the row statistics each block
+  // touches its 1/grid slice of pf (one load per 64 bytes), so the next GEMM finds its weight in
+  // MALL / L2 instead of HBM.  The loaded values are dead.
+  const char* pf;
+  long long pf_bytes;
 };
 
 // The pruned training step's head fused into the split-K LayerNorm epilogue of the last block's

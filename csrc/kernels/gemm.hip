@@ -671,6 +671,38 @@ DEV void ln_park(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char
   }
 }
 
+// Next-launch weight prefetch (FdLnEpi::pf, cold operands: profiles/r4_cold_operands.txt -- a QKV
+// forward whose weight comes from HBM is ~4 us slower).  Issued just before the row-statistics
+// poll: every block loads one dword per 64 bytes of its 1/grid slice of pf (at most PF_N per
+// thread), which fills MALL and this XCD's L2 for the next launch.  vmcnt retires loads in order,
+// so the first poll also waits for these -- the poll waits ~1.7 us for the slowest tile of the row
+// block anyway.  The values are dead: an empty asm at the end of the epilogue consumes them.
+constexpr int PF_N = 2;
+struct PfRegs {
+  uint32_t v[PF_N];
+};
+template <int NT>
+DEV PfRegs pf_issue(const FdLnEpi& L, int tid) {
+  PfRegs r;
+#pragma unroll
+  for (int k = 0; k < PF_N; ++k) r.v[k] = 0u;
+  if (L.pf == nullptr) return r;  // (kernel argument: uniform)
+  const long long lines = L.pf_bytes >> 6, nb = gridDim.x * gridDim.y;
+  const long long per = (lines + nb - 1) / nb;
+  const long long c0 = (long long)(blockIdx.y * gridDim.x + blockIdx.x) * per;
+  const long long c1 = c0 + per < lines ? c0 + per : lines;
+#pragma unroll
+  for (int k = 0; k < PF_N; ++k) {
+    const long long c = c0 + k * NT + tid;
+    if (c < c1) r.v[k] = *reinterpret_cast<const uint32_t*>(L.pf + (c << 6));  // (cached: that is the point)
+  }
+  return r;
+}
+DEV void pf_consume(const PfRegs& r) {
+#pragma unroll
+  for (int k = 0; k < PF_N; ++k) asm volatile("" ::"v"(r.v[k]));
+}
+
 template <int BM, int BN, bool BWD, int NT>
 DEV void ln_finish(const GemmParams& p, char* smem, int tm, int tn, int lane, int tid,
                    const LnPre<BM * (BN / 8) / NT>& pre) {
@@ -783,6 +815,7 @@ DEV void ln_finish(const GemmParams& p, char* smem, int tm, int tn, int lane, in
   // granules until every tag is this launch's (wave-uniform exit)
   float2 st[IT][LN_MAXK];
   FD_STAMP(3);
+  const PfRegs pfr = pf_issue<NT>(L, tid);
   {
     // diag 64 (tests only): wait for a tag no launch writes -> the timeout path
     const uint32_t want = (p.diag & 64) ? tag + 1u : tag;
@@ -868,6 +901,7 @@ DEV void ln_finish(const GemmParams& p, char* smem, int tm, int tn, int lane, in
     __syncthreads();
     flush(1, 2);
   }
+  pf_consume(pfr);
 }
 
 template <int BM, int BN, int TM, int TN, bool BWD, int NT>
@@ -2063,7 +2097,7 @@ bool plan_dwb_mix(DwBatch& bt, int mode) {
   const int rounds = L / cus, E = L - rounds * cus;
   int target = E;
   if (mode == 1 && (rounds == 0 || E == 0)) return false;
-  if (mode == 2 && target == 0) target = 1;
+  if (mode == 2) target = 1;  // forced (tests): the smallest long problem goes to half tiles
   // smallest subset sum >= target over the long problems (reachable sums; <= 32 problems)
   std::vector<int> from(L + 1, -2);  // from[s]: last problem added to reach sum s (-1: empty set)
   from[0] = -1;

@@ -514,6 +514,7 @@ class DDoSClassifier(nn.Module):
             if rc.colsum_jobs is not None and self.batch_colsum:
                 rc.colsum_pending = []
         rc.fuse_colsum = self.fuse_colsum
+        rc.qkv_ws = [L["qkv_w"] for L in layers]
         rc.remat_gelu = self.remat_gelu
         rc.fuse_ln = self.fuse_ln and cfg.dim % 64 == 0 and cfg.dim <= 2048
         # a data-parallel client's gradient exchange overlaps the backward (parallel/dp.py GradSync

@@ -105,6 +105,9 @@ class RunCtx:
     # labels, kd) set by the model before the blocks; the pruned block's output-LayerNorm split-K
     # epilogue then runs the head too and leaves head_done = (logits, loss, dz2, df) for HeadFn
     head_req: Optional[tuple] = None
+    # every block's fused QKV weight, in block order (the forward's output-LN GEMM of block i prefetches
+    # block i+1's: ops/kernels.py LN_PREFETCH)
+    qkv_ws: Optional[list] = None
     head_done: Optional[tuple] = None
 
 
@@ -212,11 +215,15 @@ class LayerFn(torch.autograd.Function):
         if fuse_ln:
             # bias + (dropout) + residual + LayerNorm in the N = 768 GEMMs' epilogues; the
             # backward reads the saved bf16 pre-LN sums z1 / z2 instead of ao / f
+            # (each LayerNorm-fused GEMM touches the next launch's weight while it waits for its row
+            # statistics: FFN1's, and the next block's QKV weight)
+            nxt = rc.qkv_ws[idx + 1] if rc.qkv_ws is not None and idx + 1 < len(rc.qkv_ws) else None
             h, ao, m1, r1 = K.linear_ln_fwd(cx, L["o_w"], L["o_b"], x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0,
-                                            0.0, keep_z=grad, xsite=K.ln_xsite(idx, 0, False))
+                                            0.0, keep_z=grad, xsite=K.ln_xsite(idx, 0, False), prefetch=L["l1_w"])
             g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
             y, f, m2, r2 = K.linear_ln_fwd(g, L["l2_w"], L["l2_b"], h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed,
-                                           ffn_site, p_h, rc.row_map, keep_z=grad, xsite=K.ln_xsite(idx, 1, False))
+                                           ffn_site, p_h, rc.row_map, keep_z=grad, xsite=K.ln_xsite(idx, 1, False),
+                                           prefetch=nxt)
             if grad:
                 rc.ln2_saved[idx] = (f, m2, r2, L, ffn_site, p_h)
         else:
@@ -312,7 +319,7 @@ class LayerFn(torch.autograd.Function):
         batch += [(df, g, G["l2_w"].buf, acc), (du, h, G["l1_w"].buf, acc)]
         dz1c, _ = K.linear_dx_ln_bwd(du, L["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
                                      G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, xsite=K.ln_xsite(ctx.idx, 0, True),
-                                     b_mn=True)
+                                     b_mn=True, prefetch=L["o_w"])
         dcxc = K.linear_dx(dz1c, L["o_w"])
         if K.attn_cls_compact_ok(rc.S):
             # the attention backward reads the compact [CLS] gradient and scatters dz1c into the
@@ -341,7 +348,8 @@ class LayerFn(torch.autograd.Function):
                 raise RuntimeError("output-LN gradient sinks out of step")
             dx, df_p = K.linear_dx_ln_bwd(dqkv, L["qkv_w"], dz1, z2p, Lp["ln2_w"], m2p, r2p, Gp["ln2_w"].buf,
                                           Gp["ln2_b"].buf, Gp["l2_b"].buf, rc.seed, site_p, p_p, acc_p[0], rc.row_map,
-                                          jobs, xsite=K.ln_xsite(ctx.idx, 1, True), b_mn=True)
+                                          jobs, xsite=K.ln_xsite(ctx.idx, 1, True), b_mn=True,
+                                          prefetch=Lp["l2_w"])
             rc.ln2_pending[ctx.idx - 1] = (dx, df_p)
         else:
             dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1)
@@ -395,7 +403,7 @@ class LayerFn(torch.autograd.Function):
         if fused_bwd:
             dz1, _ = K.linear_dx_ln_bwd(du, L["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
                                         G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs,
-                                        xsite=K.ln_xsite(ctx.idx, 0, True), b_mn=True)
+                                        xsite=K.ln_xsite(ctx.idx, 0, True), b_mn=True, prefetch=L["o_w"])
         else:
             dh = K.linear_dx(du, L["l1_w"], res=dz2)
             dz1, _ = K.ln_bwd(dh, ao, None if fused else x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
@@ -429,7 +437,8 @@ class LayerFn(torch.autograd.Function):
             acc_p = acc_p[0]
             dx, df_p = K.linear_dx_ln_bwd(dqkv, L["qkv_w"], dz1, z2p, Lp["ln2_w"], m2p, r2p, Gp["ln2_w"].buf,
                                           Gp["ln2_b"].buf, Gp["l2_b"].buf, rc.seed, site_p, p_p, acc_p, rc.row_map,
-                                          jobs, xsite=K.ln_xsite(ctx.idx, 1, True), b_mn=True)
+                                          jobs, xsite=K.ln_xsite(ctx.idx, 1, True), b_mn=True,
+                                          prefetch=Lp["l2_w"])
             rc.ln2_pending[ctx.idx - 1] = (dx, df_p)
         else:
             dx = K.linear_dx(dqkv, L["qkv_w"], res=dz1)

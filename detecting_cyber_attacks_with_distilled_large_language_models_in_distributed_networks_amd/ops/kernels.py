@@ -559,7 +559,18 @@ def _dev_key(device) -> str:
     return str(d)
 
 
-def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, keep_z: bool = True, xsite=None):
+# The LayerNorm-fused GEMMs touch the NEXT launch's weight while they wait for their row statistics
+# (csrc/kernels/gemm.hip pf_issue; cold weights cost the QKV forward ~4 us, profiles/r4_cold_operands.txt).
+# FD_LN_PREFETCH=0: off (A/B).
+LN_PREFETCH = _os.environ.get("FD_LN_PREFETCH", "1") != "0"
+
+
+def _pf(t):
+    return t if (LN_PREFETCH and t is not None and t.is_cuda and t.is_contiguous()) else None
+
+
+def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, keep_z: bool = True, xsite=None,
+                  prefetch=None):
     """y = LN(dropout(x w^T + b) + res) in ONE launch (the N = hidden GEMM's epilogue does the
     bias, dropout, residual and LayerNorm).  Returns (y, z, mean, rstd): z = the bf16 pre-LN sum
     (what the backward reads; None with keep_z=False), mean / rstd fp32 per row.  xsite: the
@@ -577,7 +588,7 @@ def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, k
     stats, cnt, err = _ln_state(x.device, M, N)
     xs = _xsite(x.device, N, xsite)
     ext().gemm_ln(False, x, w, y, b, res, gamma, beta, mean, rstd, z, None, None, stats, cnt, err, eps, seed, site,
-                  thr, sc, row_map if thr else None, LN_CFG, xs, False, _ln2_xbuf(x.device))
+                  thr, sc, row_map if thr else None, LN_CFG, xs, False, _ln2_xbuf(x.device), _pf(prefetch))
     return y, z, mean, rstd
 
 
@@ -648,7 +659,7 @@ def linear_ln_fwd_head(x, w, b, res, gamma, beta, eps, seed, site, p, row_map, h
 
 
 def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, seed, site, p, accumulate=False,
-                     row_map=None, jobs: Optional[list] = None, xsite=None, b_mn: bool = False):
+                     row_map=None, jobs: Optional[list] = None, xsite=None, b_mn: bool = False, prefetch=None):
     """LayerNorm backward fused into the dX GEMM that produces its output gradient:
     dy = a wt^T + res, then (dz, dx) of y = LN(dropout(f) + r) from the saved z = dropout(f) + r
     (dz: gradient of the pre-LN sum, i.e. of the residual input r; dx: of f, = dz without dropout).
@@ -674,7 +685,8 @@ def linear_dx_ln_bwd(a, wt, res, z, gamma, mean, rstd, dgamma, dbeta, dbias, see
     stats, cnt, err = _ln_state(a.device, M, N)
     xs = _xsite(a.device, N, xsite)
     nblk = ext().gemm_ln(True, a, wt, dz, None, res, gamma, None, mean, rstd, z, dx, ws, stats, cnt, err, 0.0, seed,
-                         site, thr, sc, row_map if thr else None, LN_CFG, xs, b_mn, _ln2_xbuf(a.device))
+                         site, thr, sc, row_map if thr else None, LN_CFG, xs, b_mn, _ln2_xbuf(a.device),
+                         _pf(prefetch))
     job = (ws, [dgamma, dbeta, dbias], nblk, 3 * N, N, accumulate)
     if jobs is not None:
         jobs.append(job)
