@@ -33,6 +33,7 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
                long long workspace_elems, int accumulate, const FdAdamEpi* adam,
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st);
 int fd_gemm_set_cfg(int kind, int cfg, int splits);
+int fd_gemm_pf(const void* pf, long long bytes);
 int fd_gemm_stamps(unsigned long long* host, int nblocks);
 int fd_attn_stamps(unsigned long long* host, int nblocks);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
@@ -161,11 +162,23 @@ const uint32_t* seedp(const at::Tensor& s) {
   return reinterpret_cast<const uint32_t*>(s.data_ptr());
 }
 
+// Arm the next-launch weight prefetch of the fd_gemm_ex call that follows (same host thread).
+void set_prefetch(const c10::optional<at::Tensor>& prefetch, const at::Tensor& like) {
+  if (prefetch.has_value() && prefetch->defined() && prefetch->numel() > 0) {
+    TORCH_CHECK(prefetch->device() == like.device() && prefetch->is_contiguous(),
+                "prefetch must be a contiguous tensor on the GEMM's device");
+    fd_gemm_pf(prefetch->data_ptr(), (long long)(prefetch->numel() * prefetch->element_size()));
+  } else {
+    fd_gemm_pf(nullptr, 0);
+  }
+}
+
 // kind 0: C[M,N] = A[M,K] B[N,K]^T ; kind 1: C[M,N] = A[M,K] B[K,N] ; kind 2: C[M,N] fp32 = A[K,M]^T B[K,N]
 void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, const at::Tensor& C,
           const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
           const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& workspace, bool accumulate,
-          const c10::optional<at::Tensor>& aux_out) {
+          const c10::optional<at::Tensor>& aux_out, const c10::optional<at::Tensor>& prefetch = c10::nullopt) {
+  // prefetch: the NEXT launch's weight, touched by this GEMM's epilogue (fd_gemm_pf)
   need(A, at::kBFloat16, "A");
   need(B, at::kBFloat16, "B");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
@@ -195,6 +208,7 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
     TORCH_CHECK(epi == 3 && kind != 2 && aux_out->size(0) == M && aux_out->size(1) == N,
                 "aux_out [M,N] only with the GELU' epilogue");
   const long long ws = (workspace.has_value() && workspace->defined()) ? workspace->numel() : 0;
+  set_prefetch(prefetch, A);
   check_rc(fd_gemm_ex((int)kind, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
                       (int)A.size(1), (int)B.size(1), (int)N, ptr<float>(bias), ptr<void>(aux), (int)N,
                       ptr<void>(res), (int)N, ptr<float>(workspace), ws, accumulate ? 1 : 0, nullptr, nullptr,
@@ -210,7 +224,8 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
 // tile configuration without the fused column-sum epilogue.
 int64_t gemm_colsum(int64_t epi, const at::Tensor& A, const at::Tensor& B, const at::Tensor& C,
                     const c10::optional<at::Tensor>& aux, const c10::optional<at::Tensor>& res,
-                    const at::Tensor& colsum, const c10::optional<at::Tensor>& aux_out, int64_t kind = 0) {
+                    const at::Tensor& colsum, const c10::optional<at::Tensor>& aux_out, int64_t kind = 0,
+                    const c10::optional<at::Tensor>& prefetch = c10::nullopt) {
   need(A, at::kBFloat16, "A");
   need(B, at::kBFloat16, "B");
   need(C, at::kBFloat16, "C");
@@ -231,6 +246,7 @@ int64_t gemm_colsum(int64_t epi, const at::Tensor& A, const at::Tensor& B, const
   if (aux_out.has_value() && aux_out->defined())
     TORCH_CHECK(epi == 3 && aux_out->size(0) == M && aux_out->size(1) == N, "aux_out [M,N] only with GELU'");
   int blocks = 0;
+  set_prefetch(prefetch, A);
   check_rc(fd_gemm_ex((int)kind, (int)epi, A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K,
                       (int)K, (int)B.size(1), (int)N, nullptr, ptr<void>(aux), (int)N, ptr<void>(res), (int)N,
                       nullptr, 0, 0, nullptr, colsum.data_ptr<float>(), &blocks, ptr<void>(aux_out), stream()),
@@ -610,14 +626,16 @@ std::vector<int64_t> gemm_splitk(int64_t epi, const at::Tensor& A, const at::Ten
   // the pruned step's head fused into the output-LayerNorm epilogue (splitk.hip sk_head_row):
   // head = [W [2][N], bias [2], labels [B] int64, logits [B][2], dlogits [B][2], dz [M][N] bf16,
   // colpart [M][3][N], hpart [M][2][N], dbpart [M][2], lpart [M], head seed int32, loss [1] fp32,
-  // ticket [1] int32 (zero; the launch leaves it zero)],
+  // ticket [1] int32 and loss granules [>= M] int64 (both zeroed once; splitk.hip sk_head_row)],
   // head_f = [site, thr, dscale, kd_T, kd_alpha, B]
   FdSkHead hd{};
   if (!head.empty()) {
-    TORCH_CHECK(epi == 6 && N == 768 && head.size() == 13 && head_f.size() == 6, "gemm_splitk head: arguments");
+    TORCH_CHECK(epi == 6 && N == 768 && head.size() == 14 && head_f.size() == 6, "gemm_splitk head: arguments");
     need(head[11], at::kFloat, "head loss");
     need(head[12], at::kInt, "head ticket");
-    TORCH_CHECK(head[11].numel() == 1 && head[12].numel() == 1, "gemm_splitk head: loss / ticket [1]");
+    need(head[13], at::kLong, "head loss granules");
+    TORCH_CHECK(head[11].numel() == 1 && head[12].numel() == 1 && head[13].numel() >= M,
+                "gemm_splitk head: loss / ticket [1], loss granules [M]");
     const int64_t Bh = (int64_t)head_f[5];
     TORCH_CHECK(Bh > 0 && Bh <= M, "gemm_splitk head: B");
     need(head[0], at::kFloat, "head W");
@@ -650,6 +668,7 @@ std::vector<int64_t> gemm_splitk(int64_t epi, const at::Tensor& A, const at::Ten
     hd.seed_ptr = seedp(head[10]);
     hd.loss = head[11].data_ptr<float>();
     hd.ticket = reinterpret_cast<unsigned*>(head[12].data_ptr<int>());
+    hd.lgran = reinterpret_cast<uint64_t*>(head[13].data_ptr());
     hd.site = (uint32_t)head_f[0];
     hd.thr = (uint32_t)head_f[1];
     hd.dscale = (float)head_f[2];
@@ -1456,7 +1475,8 @@ void axpby(const at::Tensor& dst, const at::Tensor& x, const c10::optional<at::T
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for the federated DistilBERT engine";
   m.def("gemm", &gemm, py::arg("kind"), py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"),
-        py::arg("aux"), py::arg("res"), py::arg("workspace"), py::arg("accumulate"), py::arg("aux_out") = py::none());
+        py::arg("aux"), py::arg("res"), py::arg("workspace"), py::arg("accumulate"), py::arg("aux_out") = py::none(),
+        py::arg("prefetch") = py::none());
   m.def("gemm_set_cfg", &gemm_set_cfg);
   m.def("gemm_stamps", &gemm_stamps);
   m.def("attn_stamps", &attn_stamps);
@@ -1483,7 +1503,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("biases") = std::vector<at::Tensor>{}, py::arg("rest") = std::vector<at::Tensor>{},
         py::arg("rest_i") = std::vector<int64_t>{});
   m.def("gemm_colsum", &gemm_colsum, py::arg("epi"), py::arg("A"), py::arg("B"), py::arg("C"), py::arg("aux"),
-        py::arg("res"), py::arg("colsum"), py::arg("aux_out") = py::none(), py::arg("kind") = 0);
+        py::arg("res"), py::arg("colsum"), py::arg("aux_out") = py::none(), py::arg("kind") = 0,
+        py::arg("prefetch") = py::none());
   m.def("splitk_reduce_batched", &splitk_reduce_batched);
   m.def("gemm_dw2_splits", [](int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K) {
     return (int64_t)fd_gemm_dw2_splits((int)M0, (int)N0, (int)M1, (int)N1, (int)K);

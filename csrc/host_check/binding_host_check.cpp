@@ -40,11 +40,21 @@ void opt_span(const void* p, long long bytes, const char* what) { if (p) span(p,
 
 // ------------------------------------------------------------------ stub launchers
 extern "C" {
+const void* g_hc_pf = nullptr;
+long long g_hc_pf_bytes = 0;
+int fd_gemm_pf(const void* pf, long long bytes) {
+  g_hc_pf = pf;
+  g_hc_pf_bytes = pf ? bytes : 0;
+  return 0;
+}
 int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
                long long workspace_elems, int accumulate, const FdAdamEpi* adam,
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t) {
   ++hc::calls;
+  if (g_hc_pf) hc::span(g_hc_pf, g_hc_pf_bytes, "gemm prefetch");  // (the launch's one-shot prefetch)
+  g_hc_pf = nullptr;
+  g_hc_pf_bytes = 0;
   if (kind == 0) {  // A [M][lda] (K used), B [N][ldb], C [M][ldc] bf16
     hc::span(A, ((long long)(M - 1) * lda + K) * 2, "gemm A");
     hc::span(B, ((long long)(N - 1) * ldb + K) * 2, "gemm B");
@@ -169,6 +179,7 @@ int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, 
     hc::span(hd->lpart, (long long)M * 4, "splitk head lpart");
     hc::span(hd->loss, 4, "splitk head loss");
     hc::span(hd->ticket, 4, "splitk head ticket");
+    hc::span(hd->lgran, (long long)M * 8, "splitk head loss granules");
     hc::opt_span(hd->own, (long long)(hd->B + 1) * 4, "splitk head own");
   }
   if (splits <= 0) splits = 1;

@@ -331,6 +331,41 @@ DEV void gelu_remat(const GemmParams& p, int m, int n, const uint2& u) {
                  pack_bf2(gelu_erf(lo_bf(u.y)), gelu_erf(hi_bf(u.y))));
 }
 
+// Next-launch weight prefetch (FdLnEpi::pf, cold operands: profiles/r4_cold_operands.txt -- a QKV
+// forward whose weight comes from HBM is ~4 us slower).  Issued just before the row-statistics
+// poll: every block loads one dword per 64 bytes of its 1/grid slice of pf (at most PF_N per
+// thread), which fills MALL and this XCD's L2 for the next launch.  vmcnt retires loads in order,
+// so the first poll also waits for these -- the poll waits ~1.7 us for the slowest tile of the row
+// block anyway.  The values are dead: an empty asm at the end of the epilogue consumes them.
+constexpr int PF_N = 2;
+struct PfRegs {
+  uint32_t v[PF_N];
+};
+template <int NT>
+DEV PfRegs pf_issue(const FdLnEpi& L, int tid) {
+  PfRegs r;
+#pragma unroll
+  for (int k = 0; k < PF_N; ++k) r.v[k] = 0u;
+  if (L.pf == nullptr) return r;  // (kernel argument: uniform)
+  const long long lines = L.pf_bytes >> 6, nb = gridDim.x * gridDim.y;
+  const long long per = (lines + nb - 1) / nb;
+  const long long c0 = (long long)(blockIdx.y * gridDim.x + blockIdx.x) * per;
+  const long long c1 = c0 + per < lines ? c0 + per : lines;
+#pragma unroll
+  for (int k = 0; k < PF_N; ++k) {
+    const long long c = c0 + k * NT + tid;
+    if (c < c1) r.v[k] = *reinterpret_cast<const uint32_t*>(L.pf + (c << 6));  // (cached: that is the point)
+  }
+  return r;
+}
+DEV void pf_consume(const PfRegs& r) {
+#pragma unroll
+  for (int k = 0; k < PF_N; ++k) asm volatile("" ::"v"(r.v[k]));
+}
+
+template <int BM, int BN, int TM, int TN, int EPI, int NT, int NPRE>
+DEV void staged_epilogue_out(const GemmParams& p, char* smem, int m0, int n0, int tid, const uint4 (&pre)[NPRE]);
+
 template <int BM, int BN, int TM, int TN, int EPI, int NT>
 DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int m0, int n0,
                          int wr, int wc, int lane, int tid) {
@@ -385,6 +420,22 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
   }
   __syncthreads();
   if (p.diag & 4) return;
+  if constexpr (EPI == EPI_F32) {  // (weight gradients: no next-launch prefetch)
+    staged_epilogue_out<BM, BN, TM, TN, EPI, NT>(p, smem, m0, n0, tid, pre);
+  } else {
+    // the next launch's weight (p.ln.pf, fd_gemm_pf): issued after every load this epilogue waits for
+    const PfRegs pfr = pf_issue<NT>(p.ln, tid);
+    staged_epilogue_out<BM, BN, TM, TN, EPI, NT>(p, smem, m0, n0, tid, pre);
+    pf_consume(pfr);
+  }
+}
+
+template <int BM, int BN, int TM, int TN, int EPI, int NT, int NPRE>
+DEV void staged_epilogue_out(const GemmParams& p, char* smem, int m0, int n0, int tid, const uint4 (&pre)[NPRE]) {
+  using TR = EpiTraits<EPI, BM, BN>;
+  constexpr int LDC = BN * TR::ES + 16;
+  constexpr int CPR8 = BN / 8, NCH = BM * CPR8 / NT;
+  constexpr bool PRE = TR::ELEM && TR::F32S && (BM * CPR8) % NT == 0 && NCH <= 8;
   if constexpr (!TR::F32S) {
     constexpr int CPR = BN / 8;  // 16-byte chunks (8 bf16) per row
     bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
@@ -671,37 +722,6 @@ DEV void ln_park(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char
   }
 }
 
-// Next-launch weight prefetch (FdLnEpi::pf, cold operands: profiles/r4_cold_operands.txt -- a QKV
-// forward whose weight comes from HBM is ~4 us slower).  Issued just before the row-statistics
-// poll: every block loads one dword per 64 bytes of its 1/grid slice of pf (at most PF_N per
-// thread), which fills MALL and this XCD's L2 for the next launch.  vmcnt retires loads in order,
-// so the first poll also waits for these -- the poll waits ~1.7 us for the slowest tile of the row
-// block anyway.  The values are dead: an empty asm at the end of the epilogue consumes them.
-constexpr int PF_N = 2;
-struct PfRegs {
-  uint32_t v[PF_N];
-};
-template <int NT>
-DEV PfRegs pf_issue(const FdLnEpi& L, int tid) {
-  PfRegs r;
-#pragma unroll
-  for (int k = 0; k < PF_N; ++k) r.v[k] = 0u;
-  if (L.pf == nullptr) return r;  // (kernel argument: uniform)
-  const long long lines = L.pf_bytes >> 6, nb = gridDim.x * gridDim.y;
-  const long long per = (lines + nb - 1) / nb;
-  const long long c0 = (long long)(blockIdx.y * gridDim.x + blockIdx.x) * per;
-  const long long c1 = c0 + per < lines ? c0 + per : lines;
-#pragma unroll
-  for (int k = 0; k < PF_N; ++k) {
-    const long long c = c0 + k * NT + tid;
-    if (c < c1) r.v[k] = *reinterpret_cast<const uint32_t*>(L.pf + (c << 6));  // (cached: that is the point)
-  }
-  return r;
-}
-DEV void pf_consume(const PfRegs& r) {
-#pragma unroll
-  for (int k = 0; k < PF_N; ++k) asm volatile("" ::"v"(r.v[k]));
-}
 
 template <int BM, int BN, bool BWD, int NT>
 DEV void ln_finish(const GemmParams& p, char* smem, int tm, int tn, int lane, int tid,
@@ -1869,6 +1889,16 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
                     workspace_elems, accumulate, adam, colsum, colsum_blocks, nullptr, st);
 }
 
+// The next fd_gemm_ex launch on this host thread touches `pf` in its epilogue (GemmParams::ln.pf:
+// staged_epilogue's pf_issue) -- the following launch's weight, so it comes from MALL / L2.
+thread_local const char* g_gemm_pf = nullptr;
+thread_local long long g_gemm_pf_bytes = 0;
+int fd_gemm_pf(const void* pf, long long bytes) {
+  g_gemm_pf = reinterpret_cast<const char*>(pf);
+  g_gemm_pf_bytes = pf ? bytes : 0;
+  return 0;
+}
+
 // fd_gemm + aux_out: the GELU' epilogue also re-creates gelu(aux) (nullable; EPI_GELU_BWD only).
 int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
@@ -1877,6 +1907,10 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
   if (K % BKT != 0 || N % 64 != 0 || M <= 0 || kind < 0 || kind > 2 || epi >= EPI_LN) return 1;
   if (aux_out && (epi != EPI_GELU_BWD || kind == 2)) return 7;
   GemmParams p{};
+  p.ln.pf = g_gemm_pf;  // (one launch only)
+  p.ln.pf_bytes = g_gemm_pf_bytes;
+  g_gemm_pf = nullptr;
+  g_gemm_pf_bytes = 0;
   p.aux_out = (bf16_t*)aux_out;
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.C = C;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;

@@ -194,20 +194,35 @@ DEV void sk_head_row(const SkArgs& a, int m, int t, bool act, int n, const float
   __syncthreads();
   const float d0 = hr ? hs[0] : 0.f, d1 = hr ? hs[1] : 0.f;
   if (t == 0) {
-    H.lpart[m] = hr ? hs[2] / H.B : 0.f;
+    const float lv = hr ? hs[2] / H.B : 0.f;
+    H.lpart[m] = lv;
     H.dbpart[2 * m] = d0;
     H.dbpart[2 * m + 1] = d1;
     // The batch loss inside this launch (valid as soon as the forward returns, not only after the
-    // deferred column sums of the backward): the last row block to finish sums the M row losses in
-    // row order (deterministic) and re-arms the ticket for the next launch / graph replay.
-    __threadfence();
-    const unsigned done = __hip_atomic_fetch_add(H.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == gridDim.x - 1) {
-      __threadfence();
+    // deferred column sums of the backward).  No fences (an agent-scope release / acquire writes
+    // back / invalidates the whole L2): every row block takes a ticket (relaxed, agent scope) and
+    // publishes its row loss as ONE tagged granule {generation + 1, value} (gemm.hip st_gran's form;
+    // generation = ticket / rows, so stale granules never match); the block holding the launch's
+    // last ticket polls the granules until every tag is this generation's and sums them in row order
+    // (deterministic).  The ticket is never reset: graph replays just advance the generation.
+    const unsigned rows = gridDim.x;
+    const unsigned done = __hip_atomic_fetch_add(H.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t tag = done / rows + 1u;
+    __hip_atomic_store(H.lgran + m, ((uint64_t)tag << 32) | __float_as_uint(lv), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (done % rows == rows - 1) {
       float s = 0.f;
-      for (int r = 0; r < (int)gridDim.x; ++r) s += H.lpart[r];
+      for (unsigned r = 0; r < rows; ++r) {
+        uint64_t g;
+        const uint64_t t0 = wall_clock64();
+        for (;;) {  // (every other block has taken its ticket: its granule store is in flight)
+          g = __hip_atomic_load(H.lgran + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((uint32_t)(g >> 32) == tag || wall_clock64() - t0 > 25000000ull) break;  // (0.25 s: never)
+          __builtin_amdgcn_s_sleep(1);
+        }
+        s += __uint_as_float((uint32_t)g);
+      }
       *H.loss = s;
-      __hip_atomic_store(H.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   const bool grad_row = hr && !(H.own && H.own[m] == H.own[m + 1]);
@@ -398,7 +413,7 @@ int fd_splitk_epilogue(int epi, const float* slabs, long long sstride, int split
   if (ln) a.ln = *ln;
   if (hd && hd->W) {  // the fused head: LayerNorm forward only, N = 768, every output buffer given
     if (epi != SK_LN || N != 768 || hd->B <= 0 || hd->B > M || !hd->labels || !hd->logits || !hd->dlogits ||
-        !hd->dz || !hd->colpart || !hd->hpart || !hd->dbpart || !hd->lpart || !hd->loss || !hd->ticket ||
+        !hd->dz || !hd->colpart || !hd->hpart || !hd->dbpart || !hd->lpart || !hd->loss || !hd->ticket || !hd->lgran ||
         !hd->bias || !hd->seed_ptr ||
         (ln && ln->thr && !hd->dx))
       return 8;

@@ -208,7 +208,7 @@ class LayerFn(torch.autograd.Function):
         p_h = rc.p_hidden if rc.training else 0.0
         attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
         grad = ctx.needs_input_grad[0]
-        qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
+        qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"], prefetch=L["o_w"])  # (out_lin follows attention)
         dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
         cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask)
         fuse_ln = rc.fuse_ln and K.ln_fusable(x.shape[0], x.shape[1], K=(x.shape[1], L["l2_w"].shape[1]))
@@ -220,7 +220,7 @@ class LayerFn(torch.autograd.Function):
             nxt = rc.qkv_ws[idx + 1] if rc.qkv_ws is not None and idx + 1 < len(rc.qkv_ws) else None
             h, ao, m1, r1 = K.linear_ln_fwd(cx, L["o_w"], L["o_b"], x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0,
                                             0.0, keep_z=grad, xsite=K.ln_xsite(idx, 0, False), prefetch=L["l1_w"])
-            g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
+            g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True, prefetch=L["l2_w"])
             y, f, m2, r2 = K.linear_ln_fwd(g, L["l2_w"], L["l2_b"], h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed,
                                            ffn_site, p_h, rc.row_map, keep_z=grad, xsite=K.ln_xsite(idx, 1, False),
                                            prefetch=nxt)
@@ -386,7 +386,8 @@ class LayerFn(torch.autograd.Function):
         fuse_cs = jobs is not None and rc.fuse_colsum
         g_out = torch.empty_like(u) if g is None else None  # re-created gelu(u) (RunCtx.remat_gelu)
         du = K.linear_dx(df, L["l2_w"], gelu_u=u,
-                         colsum=(jobs, G["l1_b"].buf, acc) if fuse_cs else None, aux_out=g_out)
+                         colsum=(jobs, G["l1_b"].buf, acc) if fuse_cs else None, aux_out=g_out,
+                         prefetch=L["l1_w"])
         if g is None:
             g = g_out
         if batch is not None:

@@ -70,8 +70,19 @@ def _splitk(epi, x, wt, y, **kw):
     return ext().gemm_splitk(epi, x, wt, y, ws, **kw)
 
 
-def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu: bool = False):
-    """y = x w^T + b (bf16), optionally also returning u (pre-GELU) with y = gelu(u)."""
+# The LayerNorm-fused GEMMs touch the NEXT launch's weight while they wait for their row statistics
+# (csrc/kernels/gemm.hip pf_issue; cold weights cost the QKV forward ~4 us, profiles/r4_cold_operands.txt).
+# FD_LN_PREFETCH=0: off (A/B).
+LN_PREFETCH = _os.environ.get("FD_LN_PREFETCH", "1") != "0"
+
+
+def _pf(t):
+    return t if (LN_PREFETCH and t is not None and t.is_cuda and t.is_contiguous()) else None
+
+
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu: bool = False, prefetch=None):
+    """y = x w^T + b (bf16), optionally also returning u (pre-GELU) with y = gelu(u).  prefetch: the
+    next launch's weight, touched by the epilogue (``LN_PREFETCH``)."""
     M, N = x.shape[0], w.shape[0]
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
     if _splitk_ok(M, N, x.shape[1]):
@@ -83,15 +94,15 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu
         return y
     if gelu:
         u = torch.empty_like(y)
-        ext().gemm(0, EPI_BIAS_GELU, x, w, y, b, u, None, None, False)
+        ext().gemm(0, EPI_BIAS_GELU, x, w, y, b, u, None, None, False, None, _pf(prefetch))
         return y, u
-    ext().gemm(0, EPI_BIAS if b is not None else EPI_BF16, x, w, y, b, None, None, None, False)
+    ext().gemm(0, EPI_BIAS if b is not None else EPI_BF16, x, w, y, b, None, None, None, False, None, _pf(prefetch))
     return y
 
 
 def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] = None,
               res: Optional[torch.Tensor] = None,
-              colsum: Optional[tuple] = None, aux_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+              colsum: Optional[tuple] = None, aux_out: Optional[torch.Tensor] = None, prefetch=None) -> torch.Tensor:
     """dx = dy w  [* gelu'(u)]  [+ res]  (bf16).
 
     The product reads the weight ``w`` [N_out, N_in] itself as an MN-major B operand ("NN",
@@ -120,15 +131,15 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, gelu_u: Optional[torch.Tensor] 
     if colsum is not None:
         jobs, out, acc = colsum
         ws = workspace(dy.device, f"colsum_job{len(jobs)}", ((M + 127) // 128) * N)
-        nblk = ext().gemm_colsum(epi, dy, B, dx, gelu_u, res, ws, ao, kind)
+        nblk = ext().gemm_colsum(epi, dy, B, dx, gelu_u, res, ws, ao, kind, _pf(prefetch))
         if nblk:
             jobs.append((ws, [out], nblk, N, N, acc))
             return dx
         # this shape's tile has no fused column sums: plain GEMM, then the separate pass
-        ext().gemm(kind, epi, dy, B, dx, None, gelu_u, res, None, False, ao)
+        ext().gemm(kind, epi, dy, B, dx, None, gelu_u, res, None, False, ao, _pf(prefetch))
         _colsum_pass(dx, out, acc, jobs)
         return dx
-    ext().gemm(kind, epi, dy, B, dx, None, gelu_u, res, None, False, ao)
+    ext().gemm(kind, epi, dy, B, dx, None, gelu_u, res, None, False, ao, _pf(prefetch))
     return dx
 
 
@@ -176,6 +187,11 @@ DW_BATCH_MAX = 32  # problems per all-layer weight-gradient launch (csrc/kernels
 ADAM_IN_DW = _os.environ.get("FD_ADAM_IN_DW", "1") != "0"
 
 
+# Problem order of the all-layer dW launch (A/B): 0 = backward order as recorded (the pruned last
+# block's problems first), 1 = reversed (forward block order).
+DWB_ORDER = int(_os.environ.get("FD_DWB_ORDER", "0"))
+
+
 def linear_dw_batch(jobs: list, adam=None, cfg: int = -1, opt=None):
     """Every weight gradient of a backward in one launch per 32 problems: for each job
     (dy [K, M], x [K, N], out [M, N] fp32, accumulate[, bias]) out (+)= dy^T x, and the
@@ -184,6 +200,8 @@ def linear_dw_batch(jobs: list, adam=None, cfg: int = -1, opt=None):
     adam: a callable grads -> (state, hyper) (``ArenaAdam.fused_args``): apply the optimizer
     step to each finished gradient tile instead of storing it.  opt (with adam): the optimizer
     (``ArenaAdam``) -- the last launch also runs the rest of its step (``ADAM_IN_DW``)."""
+    if DWB_ORDER == 1 and len(jobs) <= DW_BATCH_MAX:
+        jobs = jobs[::-1]  # (forward block order: the pruned block's problems last)
     starts = list(range(0, len(jobs), DW_BATCH_MAX))
     for i in starts:
         chunk = jobs[i:i + DW_BATCH_MAX]
@@ -559,16 +577,6 @@ def _dev_key(device) -> str:
     return str(d)
 
 
-# The LayerNorm-fused GEMMs touch the NEXT launch's weight while they wait for their row statistics
-# (csrc/kernels/gemm.hip pf_issue; cold weights cost the QKV forward ~4 us, profiles/r4_cold_operands.txt).
-# FD_LN_PREFETCH=0: off (A/B).
-LN_PREFETCH = _os.environ.get("FD_LN_PREFETCH", "1") != "0"
-
-
-def _pf(t):
-    return t if (LN_PREFETCH and t is not None and t.is_cuda and t.is_contiguous()) else None
-
-
 def linear_ln_fwd(x, w, b, res, gamma, beta, eps, seed, site, p, row_map=None, keep_z: bool = True, xsite=None,
                   prefetch=None):
     """y = LN(dropout(x w^T + b) + res) in ONE launch (the N = hidden GEMM's epilogue does the
@@ -605,11 +613,23 @@ _HEAD_TICKETS = {}
 
 
 def _head_ticket(dev) -> torch.Tensor:
-    """The fused head's completion counter (int32 [1], zero between launches: the launch's last row
-    block re-arms it), one per device."""
+    """The fused head's ticket counter (int32 [1], zeroed once and only ever advanced: the launch
+    generation is ticket / rows), one per device."""
     t = _HEAD_TICKETS.get(dev)
     if t is None:
         t = _HEAD_TICKETS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return t
+
+
+_HEAD_LGRAN = {}
+
+
+def _head_lgran(dev, M: int) -> torch.Tensor:
+    """The fused head's tagged row-loss granules (int64 [>= M], zeroed once; tags are generation + 1,
+    so a fresh larger buffer is as good as the old one)."""
+    t = _HEAD_LGRAN.get(dev)
+    if t is None or t.numel() < M:
+        t = _HEAD_LGRAN[dev] = torch.zeros(max(M, 256), dtype=torch.int64, device=dev)
     return t
 
 
@@ -647,7 +667,7 @@ def linear_ln_fwd_head(x, w, b, res, gamma, beta, eps, seed, site, p, row_map, h
     _splitk(EPI_LN, x, w, y, bias=b, res=res, gamma=gamma, beta=beta, mean=mean, rstd=rstd, z=z, eps=eps,
             seed=seed, site=site, thr=thr, dscale=sc, row_map=row_map if thr else None,
             head=[hW, hb, labels, logits, dlogits, dz, colpart, hpart, dbpart, lpart, seed, loss.view(1),
-                  _head_ticket(dev)],
+                  _head_ticket(dev), _head_lgran(dev, M)],
             head_f=[float(head_site), float(hthr), float(hsc), float(kT), float(alpha), float(B)],
             head_dx=dx, head_tlogits=t, head_own=own)
     jobs.append((colpart, [dgamma, dbeta, dbias], M, 3 * N, N, acc_ln))

@@ -64,6 +64,8 @@ flat = [p for layer in full for p in layer]
 sets = [
     ("step order (pruned first), 24 problems", pruned + flat),
     ("pruned block last", flat + pruned),
+    ("reversed (forward block order)", (pruned + flat)[::-1]),
+    ("reversed blocks, backward order inside", [p for layer in full[::-1] for p in layer] + pruned),
     ("5 long blocks only", flat),
     ("pruned block only (81 short + 27 long)", pruned),
     ("pruned short only (81 tiles, K=64)", pruned[:3]),

@@ -48,6 +48,12 @@ def _worker(rank, world, port, outdir, dead=1):
         res = f"dead={e.dead} after {time.monotonic() - t0:.1f}s"
     with open(os.path.join(outdir, f"result{rank}.txt" if world > 2 else "result.txt"), "w") as f:
         f.write(res)
+    if rank == 0 and world > 2:
+        # rank 0 hosts the TCPStore: stay up until every survivor has recorded its verdict
+        t_end = time.monotonic() + 60
+        while time.monotonic() < t_end and not all(
+                os.path.exists(os.path.join(outdir, f"result{r}.txt")) for r in range(world) if r != dead):
+            time.sleep(0.1)
     os._exit(0)
 
 

@@ -347,6 +347,8 @@ def test_head_in_epilogue_loss_valid_before_backward():
         pytest.skip("head not in the output-LayerNorm epilogue")
     m = DDoSClassifier(config=DistilBertConfig(n_layers=2), device="cuda", impl="hip", seed=44)
     m.train()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    t0 = int(K._head_ticket(dev).item())
     for it in range(3):
         ids, mask, labels, tokens = _batch(32, 128, seed=900 + it)
         m.rng.fill_(11 + it)
@@ -358,4 +360,5 @@ def test_head_in_epilogue_loss_valid_before_backward():
         loss.backward(K.unit_grad("cuda"))
         torch.cuda.synchronize()
         assert loss.item() == got
-    assert int(K._head_ticket(torch.device("cuda", torch.cuda.current_device())).item()) == 0
+    # one ticket per row block (64 [CLS] rows) per launch, never reset (generation = ticket / rows)
+    assert int(K._head_ticket(dev).item()) - t0 == 3 * 64
