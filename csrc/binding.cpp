@@ -626,16 +626,14 @@ std::vector<int64_t> gemm_splitk(int64_t epi, const at::Tensor& A, const at::Ten
   // the pruned step's head fused into the output-LayerNorm epilogue (splitk.hip sk_head_row):
   // head = [W [2][N], bias [2], labels [B] int64, logits [B][2], dlogits [B][2], dz [M][N] bf16,
   // colpart [M][3][N], hpart [M][2][N], dbpart [M][2], lpart [M], head seed int32, loss [1] fp32,
-  // ticket [1] int32 and loss granules [>= M] int64 (both zeroed once; splitk.hip sk_head_row)],
+  // ticket [1] int32 (zeroed once; splitk.hip sk_head_row)],
   // head_f = [site, thr, dscale, kd_T, kd_alpha, B]
   FdSkHead hd{};
   if (!head.empty()) {
-    TORCH_CHECK(epi == 6 && N == 768 && head.size() == 14 && head_f.size() == 6, "gemm_splitk head: arguments");
+    TORCH_CHECK(epi == 6 && N == 768 && head.size() == 13 && head_f.size() == 6, "gemm_splitk head: arguments");
     need(head[11], at::kFloat, "head loss");
     need(head[12], at::kInt, "head ticket");
-    need(head[13], at::kLong, "head loss granules");
-    TORCH_CHECK(head[11].numel() == 1 && head[12].numel() == 1 && head[13].numel() >= M,
-                "gemm_splitk head: loss / ticket [1], loss granules [M]");
+    TORCH_CHECK(head[11].numel() == 1 && head[12].numel() == 1, "gemm_splitk head: loss / ticket [1]");
     const int64_t Bh = (int64_t)head_f[5];
     TORCH_CHECK(Bh > 0 && Bh <= M, "gemm_splitk head: B");
     need(head[0], at::kFloat, "head W");
@@ -668,7 +666,6 @@ std::vector<int64_t> gemm_splitk(int64_t epi, const at::Tensor& A, const at::Ten
     hd.seed_ptr = seedp(head[10]);
     hd.loss = head[11].data_ptr<float>();
     hd.ticket = reinterpret_cast<unsigned*>(head[12].data_ptr<int>());
-    hd.lgran = reinterpret_cast<uint64_t*>(head[13].data_ptr());
     hd.site = (uint32_t)head_f[0];
     hd.thr = (uint32_t)head_f[1];
     hd.dscale = (float)head_f[2];

@@ -179,7 +179,6 @@ int fd_gemm_splitk(int epi, const void* A, const void* Bt, int M, int N, int K, 
     hc::span(hd->lpart, (long long)M * 4, "splitk head lpart");
     hc::span(hd->loss, 4, "splitk head loss");
     hc::span(hd->ticket, 4, "splitk head ticket");
-    hc::span(hd->lgran, (long long)M * 8, "splitk head loss granules");
     hc::opt_span(hd->own, (long long)(hd->B + 1) * 4, "splitk head own");
   }
   if (splits <= 0) splits = 1;

@@ -131,8 +131,7 @@ struct FdSkHead {
   float* hpart;            // [M][2][N] head dW rows
   float* dbpart;           // [M][2] head db rows
   float* lpart;            // [M] row loss / B
-  float* loss;             // [1] the batch loss: sum of the row losses, written by the launch's last row block
-  unsigned* ticket;        // [1] row blocks done, ever (launch generation = ticket / rows; never reset)
-  uint64_t* lgran;         // [M] {generation + 1, row loss / B} granules (zeroed once)
+  float* loss;             // [1] the batch loss: sum of lpart, written by the launch's last row block
+  unsigned* ticket;        // [1] row blocks done, ever (zeroed once, never reset)
 };
 

@@ -156,6 +156,7 @@ DEV void sk_head_row(const SkArgs& a, int m, int t, bool act, int n, const float
   __shared__ __attribute__((aligned(16))) uint16_t ys[768];
   __shared__ float hs[4];
   __shared__ float red[4];
+  __shared__ unsigned ticket_s;
   const FdSkHead& H = a.hd;
   const FdLnEpi& L = a.ln;
   const int N = a.N, lane = t & 63;
@@ -195,35 +196,19 @@ DEV void sk_head_row(const SkArgs& a, int m, int t, bool act, int n, const float
   const float d0 = hr ? hs[0] : 0.f, d1 = hr ? hs[1] : 0.f;
   if (t == 0) {
     const float lv = hr ? hs[2] / H.B : 0.f;
-    H.lpart[m] = lv;
     H.dbpart[2 * m] = d0;
     H.dbpart[2 * m + 1] = d1;
     // The batch loss inside this launch (valid as soon as the forward returns, not only after the
-    // deferred column sums of the backward).  No fences (an agent-scope release / acquire writes
-    // back / invalidates the whole L2): every row block takes a ticket (relaxed, agent scope) and
-    // publishes its row loss as ONE tagged granule {generation + 1, value} (gemm.hip st_gran's form;
-    // generation = ticket / rows, so stale granules never match); the block holding the launch's
-    // last ticket polls the granules until every tag is this generation's and sums them in row order
-    // (deterministic).  The ticket is never reset: graph replays just advance the generation.
-    const unsigned rows = gridDim.x;
+    // deferred column sums of the backward), without fences (an agent-scope release / acquire writes
+    // back / invalidates the whole L2): the row loss goes out as a write-through (agent-scope) store
+    // that this thread drains (vmcnt(0)) BEFORE it takes a ticket (relaxed, agent scope) -- ln2_send's
+    // hand-off form -- so the block holding the launch's last ticket finds every row loss in place and
+    // sums them (at the end of this function, after its own row's work).  The ticket is never reset:
+    // graph replays just count on (the last block of a launch holds ticket % rows == rows - 1).
+    __hip_atomic_store(H.lpart + m, lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned done = __hip_atomic_fetch_add(H.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t tag = done / rows + 1u;
-    __hip_atomic_store(H.lgran + m, ((uint64_t)tag << 32) | __float_as_uint(lv), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    if (done % rows == rows - 1) {
-      float s = 0.f;
-      for (unsigned r = 0; r < rows; ++r) {
-        uint64_t g;
-        const uint64_t t0 = wall_clock64();
-        for (;;) {  // (every other block has taken its ticket: its granule store is in flight)
-          g = __hip_atomic_load(H.lgran + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((uint32_t)(g >> 32) == tag || wall_clock64() - t0 > 25000000ull) break;  // (0.25 s: never)
-          __builtin_amdgcn_s_sleep(1);
-        }
-        s += __uint_as_float((uint32_t)g);
-      }
-      *H.loss = s;
-    }
+    ticket_s = done;
   }
   const bool grad_row = hr && !(H.own && H.own[m] == H.own[m + 1]);
   const bool hdrop = H.thr != 0;
@@ -284,6 +269,15 @@ DEV void sk_head_row(const SkArgs& a, int m, int t, bool act, int n, const float
     *reinterpret_cast<float4*>(cp + N + 4) = make_float4(dy[4], dy[5], dy[6], dy[7]);
     *reinterpret_cast<float4*>(cp + 2 * N) = make_float4(dx[0], dx[1], dx[2], dx[3]);
     *reinterpret_cast<float4*>(cp + 2 * N + 4) = make_float4(dx[4], dx[5], dx[6], dx[7]);
+  }
+  // the launch's last row block: the batch loss (one wave: lane l sums rows l, l + 64, ... in that
+  // order, then a fixed butterfly -- deterministic)
+  const unsigned rows = gridDim.x, done = ticket_s;  // (written before this function's later barriers)
+  if (done % rows == rows - 1 && t < 64) {
+    float s = 0.f;
+    for (unsigned r = lane; r < rows; r += 64) s += __hip_atomic_load(H.lpart + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s = wave_sum(s);
+    if (lane == 0) *H.loss = s;
   }
 }
 
@@ -413,7 +407,7 @@ int fd_splitk_epilogue(int epi, const float* slabs, long long sstride, int split
   if (ln) a.ln = *ln;
   if (hd && hd->W) {  // the fused head: LayerNorm forward only, N = 768, every output buffer given
     if (epi != SK_LN || N != 768 || hd->B <= 0 || hd->B > M || !hd->labels || !hd->logits || !hd->dlogits ||
-        !hd->dz || !hd->colpart || !hd->hpart || !hd->dbpart || !hd->lpart || !hd->loss || !hd->ticket || !hd->lgran ||
+        !hd->dz || !hd->colpart || !hd->hpart || !hd->dbpart || !hd->lpart || !hd->loss || !hd->ticket ||
         !hd->bias || !hd->seed_ptr ||
         (ln && ln->thr && !hd->dx))
       return 8;

@@ -613,23 +613,11 @@ _HEAD_TICKETS = {}
 
 
 def _head_ticket(dev) -> torch.Tensor:
-    """The fused head's ticket counter (int32 [1], zeroed once and only ever advanced: the launch
-    generation is ticket / rows), one per device."""
+    """The fused head's ticket counter (int32 [1], zeroed once and only ever advanced: a launch's
+    last row block holds ticket % rows == rows - 1), one per device."""
     t = _HEAD_TICKETS.get(dev)
     if t is None:
         t = _HEAD_TICKETS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
-    return t
-
-
-_HEAD_LGRAN = {}
-
-
-def _head_lgran(dev, M: int) -> torch.Tensor:
-    """The fused head's tagged row-loss granules (int64 [>= M], zeroed once; tags are generation + 1,
-    so a fresh larger buffer is as good as the old one)."""
-    t = _HEAD_LGRAN.get(dev)
-    if t is None or t.numel() < M:
-        t = _HEAD_LGRAN[dev] = torch.zeros(max(M, 256), dtype=torch.int64, device=dev)
     return t
 
 
@@ -667,7 +655,7 @@ def linear_ln_fwd_head(x, w, b, res, gamma, beta, eps, seed, site, p, row_map, h
     _splitk(EPI_LN, x, w, y, bias=b, res=res, gamma=gamma, beta=beta, mean=mean, rstd=rstd, z=z, eps=eps,
             seed=seed, site=site, thr=thr, dscale=sc, row_map=row_map if thr else None,
             head=[hW, hb, labels, logits, dlogits, dz, colpart, hpart, dbpart, lpart, seed, loss.view(1),
-                  _head_ticket(dev), _head_lgran(dev, M)],
+                  _head_ticket(dev)],
             head_f=[float(head_site), float(hthr), float(hsc), float(kT), float(alpha), float(B)],
             head_dx=dx, head_tlogits=t, head_own=own)
     jobs.append((colpart, [dgamma, dbeta, dbias], M, 3 * N, N, acc_ln))

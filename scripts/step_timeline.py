@@ -7,7 +7,7 @@ from collections import defaultdict
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 last = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"] or "gemm_dw_batch_kernel" in r["Kernel_Name"]]
 spans = []
 for a, b in zip(ends[:-1], ends[1:]):
     ks = rows[a + 1:b + 1]
