@@ -103,6 +103,10 @@ def _args(argv=None):
                     help="one-GPU job: the quality protocol trains this many federated clients in turn on the "
                          "GPU (seeds 42, 43, ...) and averages them -- the reference's 2-client FedAvg round "
                          "(1: a single client, whose FedAvg is an identity)")
+    ap.add_argument("--warm-start-epochs", type=int, default=0,
+                    help="virtual-client quality protocol: first train the shared init this many epochs on a "
+                         "separate public synthetic file (fed/runner.py warm_start) -- the analog of the "
+                         "reference's pretrained DistilBERT start (client1.py:56)")
     ap.add_argument("--rounds", type=int, default=1,
                     help="FedAvg rounds of the quality protocol (BASELINE.json config 4: 3); each round every "
                          "client restarts from the previous aggregate with a fresh Adam (client1.py:375-380)")
@@ -362,7 +366,8 @@ def main():
 
     # ---- quality: 3 local epochs + 1 FedAvg round through the federated client (untimed)
     quality = {} if args.no_quality else _quality(client, di, comm, q_rows, q_epochs, on_gpu,
-                                                  n_virtual=args.virtual_clients, n_rounds=args.rounds)
+                                                  n_virtual=args.virtual_clients, n_rounds=args.rounds,
+                                                  warm_epochs=args.warm_start_epochs)
     n = di.world_size
     clients = topo.num_clients
     per_client = args.steps / dt
@@ -473,7 +478,7 @@ def _fedavg_timing(model, di, fedavg, comm, ncomm, k, sync):
             "allreduce_busbw_GBps": round(2.0 * (n - 1) / n * nbytes / r / 1e9, 2)}
 
 
-def _quality_virtual(client, rows, epochs, on_gpu, n_virtual, n_rounds=1):
+def _quality_virtual(client, rows, epochs, on_gpu, n_virtual, n_rounds=1, warm_epochs=0):
     """1-GPU job: the reference's 2-client round with both clients trained one after the other on
     this GPU (fed/runner.py run_virtual_clients): seeds 42 / 43, the same init, 3 local epochs each,
     the FedAvg sum + scale_cast, each client's test split evaluated on its local model and on the
@@ -481,6 +486,11 @@ def _quality_virtual(client, rows, epochs, on_gpu, n_virtual, n_rounds=1):
     from importlib import import_module
     runner = import_module(f"{PKG}.fed.runner")
     t0 = time.perf_counter()
+    warm = None
+    if warm_epochs > 0:
+        warm = runner.warm_start(client, warm_epochs, rows=rows)
+        print(f"[quality] warm start: {warm_epochs} epoch(s) on a public synthetic file, public test "
+              f"{warm['public_test']['accuracy']:.3f} %", file=sys.stderr, flush=True)
     res = runner.run_virtual_clients(client, n_virtual, rounds=n_rounds,
                                      progress=lambda m: print(f"[quality] {m}", file=sys.stderr, flush=True))
     if on_gpu:
@@ -514,7 +524,11 @@ def _quality_virtual(client, rows, epochs, on_gpu, n_virtual, n_rounds=1):
                             "train_steps": c["train"]["steps"]} for c in cl],
             "eval_rows": int(total), "eval_rows_per_client": int(total) // max(len(cl), 1),
             "train_rows_per_client": cl[0]["train_rows"], "fedavg_rounds": n_rounds, "local_epochs": epochs,
-            **({"per_round": [_round_summary(h) for h in res["rounds"]]} if n_rounds > 1 else {}),
+            **({"per_round": [_round_summary(h) for h in res["rounds"]]} if n_rounds > 1 or warm else {}),
+            **({"warm_start": {"epochs": warm_epochs, "public_rows": warm["rows"], "public_seed": warm["seed"],
+                               "public_train_rows": warm["train_rows"],
+                               "public_test_accuracy_pct": round(warm["public_test"]["accuracy"], 3),
+                               "public_test_f1": round(warm["public_test"]["f1"], 5)}} if warm else {}),
             "quality_file_rows": rows, "quality_fedavg_ms": round(res["fedavg_ms"], 3),
             "quality_train_batches_per_sec": round(float(np.mean([c["train"]["batches_per_sec"] for c in cl])), 2),
             "quality_wall_s": round(wall, 2), "quality_lr": client.cfg.lr,
@@ -560,12 +574,12 @@ def _round_summary(h):
                         for c in cl]}
 
 
-def _quality(client, di, comm, rows, epochs, on_gpu, n_virtual=1, n_rounds=1):
+def _quality(client, di, comm, rows, epochs, on_gpu, n_virtual=1, n_rounds=1, warm_epochs=0):
     """Run round 1 of the federated client (fed/runner.py run_round: local train -> local eval
     -> FedAvg -> aggregated eval) and pool the aggregated test confusion matrices of all clients.
     n_virtual > 1 (a one-process job): that many clients trained in turn on this device instead."""
-    if (n_virtual > 1 or n_rounds > 1) and not di.distributed:
-        return _quality_virtual(client, rows, epochs, on_gpu, n_virtual, n_rounds)
+    if (n_virtual > 1 or n_rounds > 1 or warm_epochs > 0) and not di.distributed:
+        return _quality_virtual(client, rows, epochs, on_gpu, n_virtual, n_rounds, warm_epochs)
     t0 = time.perf_counter()
     client.cfg.rounds = n_rounds
     per_round = []

@@ -106,11 +106,14 @@ def _virtual(argv):
     FedConfig.add_cli(ap)
     ap.add_argument("--clients", type=int, default=2)
     ap.add_argument("--layers", type=int, default=None, help="override DistilBERT depth (tests)")
+    ap.add_argument("--warm-start-epochs", type=int, default=0,
+                    help="train the shared init on a separate public synthetic file first (fed/runner.py "
+                         "warm_start: the analog of the reference's pretrained start)")
     ns = ap.parse_args(argv)
     cfg = FedConfig.from_args(ns)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):  # one process, whatever launched it
         os.environ.pop(k, None)
-    from .fed.runner import FederatedClient, run_virtual_clients
+    from .fed.runner import FederatedClient, run_virtual_clients, warm_start
     from .models import DistilBertConfig
     from .utils import checkpoint as ck
     from .utils.metrics import save_metrics
@@ -119,13 +122,19 @@ def _virtual(argv):
     client = FederatedClient(cfg, model_config=mc)
     client.setup()
     log = client.log
+    warm = None
+    if ns.warm_start_epochs > 0:
+        warm = warm_start(client, ns.warm_start_epochs, rows=cfg.synthetic_rows)
+        log.info(f"warm start: {ns.warm_start_epochs} epoch(s) on a public synthetic file, public test "
+                 f"accuracy {warm['public_test']['accuracy']:.3f} %")
     res = run_virtual_clients(client, ns.clients, rounds=cfg.rounds, progress=log.info)
     os.makedirs(cfg.out_dir, exist_ok=True)
 
     def tup(m):
         return (m["accuracy"], m["loss"], m["precision"], m["recall"], m["f1"])
 
-    report = {"clients": ns.clients, "rounds": []}
+    report = {"clients": ns.clients, "rounds": [],
+              **({"warm_start": {"epochs": ns.warm_start_epochs, "public_test": warm["public_test"]}} if warm else {})}
     for h in res["rounds"]:
         r = h["round"]
         sfx = "" if r == 1 else f"_round{r}"

@@ -361,6 +361,33 @@ def _average_masters(model, states: List[torch.Tensor]) -> None:
         model.sync_shadow(force=True)
 
 
+def warm_start(client: "FederatedClient", epochs: int = 1, rows: int = 225_745, seed: int = 1,
+               profile: str = "default", fraction: float = 0.1) -> Dict:
+    """A shared "pretrained" starting point for every client (the reference fine-tunes a PRETRAINED
+    DistilBERT, client1.py:56, so its clients start near one point; no weights can be downloaded
+    here): ``client.model`` is trained ``epochs`` epochs on a public synthetic sample -- a separate
+    file (generator seed ``seed``, profile ``profile``) that no client samples from -- with a fresh
+    Adam.  The model's dropout counters are then reset, so the federated clients start exactly as
+    they would from a loaded checkpoint.  Returns the training record and the public test metrics."""
+    cfg, model = client.cfg, client.model
+    frame = generate_cicids2017(rows, seed=seed, profile=profile)
+    data = build_client_data(frame, 0, fraction, cfg.base_seed + 1000, cfg.max_len, client.tokenizer)
+    dev = model.device
+    loader = DeviceLoader(data.train, cfg.batch_size, shuffle=True, device=dev, seed=cfg.base_seed + 1000)
+    opt = ArenaAdam(model, lr=cfg.lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
+                    decoupled=cfg.decoupled_weight_decay)
+    opt.reset_state()
+    tr = train_model(model, loader, None, opt, epochs, log=client.log, use_graph=cfg.use_graph)
+    test = _metrics_record(evaluate_model(model, DeviceLoader(data.test, cfg.eval_batch_size, device=dev),
+                                          name="Public warm-start test"))
+    opt.reset_state()  # (also clears the "has Adam state" word-row flags)
+    with torch.no_grad():
+        model.rng.zero_()
+    model.torch_counter = 0
+    return {"train": tr, "public_test": test, "rows": rows, "seed": seed, "profile": profile,
+            "train_rows": len(data.train)}
+
+
 def _pooled(recs, key: str):
     return [[sum(r[key]["confusion_matrix"][i][j] for r in recs if len(r[key]["confusion_matrix"]) == 2)
              for j in range(2)] for i in range(2)]

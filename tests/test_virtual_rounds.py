@@ -145,7 +145,8 @@ def test_virtual_cli_writes_per_round_artifacts(tmp_path):
         env.pop(k, None)
     cmd = [sys.executable, "-m", PKG, "virtual", "--clients", "3", "--rounds", "2", "--out-dir", str(tmp_path),
            "--synthetic-rows", "600", "--max-len", "64", "--epochs", "1", "--batch-size", "8",
-           "--eval-batch-size", "32", "--plots", "false", "--layers", "1", "--verbose", "false"]
+           "--eval-batch-size", "32", "--plots", "false", "--layers", "1", "--verbose", "false",
+           "--warm-start-epochs", "1"]
     out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
     for k in (1, 2, 3):
@@ -154,6 +155,7 @@ def test_virtual_cli_writes_per_round_artifacts(tmp_path):
             assert (tmp_path / f"client{k}_{name}").exists(), (k, name)
     rep = json.load(open(tmp_path / "virtual_report.json"))
     assert rep["clients"] == 3 and [r["round"] for r in rep["rounds"]] == [1, 2]
+    assert rep["warm_start"]["epochs"] == 1 and "accuracy" in rep["warm_start"]["public_test"]
     assert all(len(r["clients"]) == 3 for r in rep["rounds"])
     assert json.load(open(tmp_path / "ddos_distilbert_model.json"))["round"] == 2
     assert (tmp_path / "ddos_distilbert_model.pth").exists()
