@@ -1904,13 +1904,16 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
                int ldc, const float* bias, void* aux, int ldaux, const void* res, int ldres, float* workspace,
                long long workspace_elems, int accumulate, const FdAdamEpi* adam,
                float* colsum, int* colsum_blocks, void* aux_out, hipStream_t st) {
+  // the armed prefetch belongs to THIS call whatever happens below (never to a later launch)
+  const char* pf = g_gemm_pf;
+  const long long pf_bytes = g_gemm_pf_bytes;
+  g_gemm_pf = nullptr;
+  g_gemm_pf_bytes = 0;
   if (K % BKT != 0 || N % 64 != 0 || M <= 0 || kind < 0 || kind > 2 || epi >= EPI_LN) return 1;
   if (aux_out && (epi != EPI_GELU_BWD || kind == 2)) return 7;
   GemmParams p{};
-  p.ln.pf = g_gemm_pf;  // (one launch only)
-  p.ln.pf_bytes = g_gemm_pf_bytes;
-  g_gemm_pf = nullptr;
-  g_gemm_pf_bytes = 0;
+  p.ln.pf = pf;
+  p.ln.pf_bytes = pf_bytes;
   p.aux_out = (bf16_t*)aux_out;
   p.A = (const bf16_t*)A; p.B = (const bf16_t*)B; p.C = C;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
@@ -2155,10 +2158,15 @@ bool plan_dwb_mix(DwBatch& bt, int mode) {
   const int free_x = (rounds * per > big_x ? rounds * per - big_x : 0) + per;
   if (mode == 1 && (big_x > rounds * per || tail_x > free_x)) return false;
   for (int s = best; s > 0; s = used_at[s]) cls[from[s]] = 1;
-  // stable reorder by class: long full tiles, long half tiles, short
+  // stable reorder by class, in dispatch order: long full tiles, long half tiles, short -- or, with
+  // FD_DWB_SHORT_FIRST=1 (A/B), the short tiles (a one-step K loop + a full Adam epilogue: HBM-bound)
+  // first, beside the first round's operand-bound K loops
+  static const int short_first = [] { const char* e = getenv("FD_DWB_SHORT_FIRST"); return e ? atoi(e) : 0; }();
+  const int order[3] = {short_first ? 2 : 0, short_first ? 0 : 1, short_first ? 1 : 2};
   DwProb pr[DWB_MAXP];
-  int k = 0;
-  for (int c = 0; c < 3; ++c) {
+  int k = 0, off = 0;
+  for (int q = 0; q < 3; ++q) {
+    const int c = order[q];
     int t = 0;
     for (int i = 0; i < bt.n; ++i)
       if (cls[i] == c) {
@@ -2167,13 +2175,12 @@ bool plan_dwb_mix(DwBatch& bt, int mode) {
         ++k;
         t += c == 1 ? 2 * tiles[i] : tiles[i];
       }
-    bt.cls_tiles[c] = t;
-    bt.cls_pad[c] = (t + 7) / 8;
+    bt.cls_tiles[q] = t;
+    bt.cls_pad[q] = (t + 7) / 8;
+    bt.cls_off[q] = off;
+    off += t;
   }
   for (int i = 0; i < bt.n; ++i) bt.pr[i] = pr[i];
-  bt.cls_off[0] = 0;
-  bt.cls_off[1] = bt.cls_tiles[0];
-  bt.cls_off[2] = bt.cls_tiles[0] + bt.cls_tiles[1];
   bt.mixed = 1;
   return true;
 }

@@ -159,3 +159,29 @@ def test_virtual_cli_writes_per_round_artifacts(tmp_path):
     assert all(len(r["clients"]) == 3 for r in rep["rounds"])
     assert json.load(open(tmp_path / "ddos_distilbert_model.json"))["round"] == 2
     assert (tmp_path / "ddos_distilbert_model.pth").exists()
+
+
+def test_warm_start_is_a_shared_pretrained_point(tmp_path):
+    """fed/runner.py warm_start: trains the shared init on a separate public synthetic file (no client
+    samples it), then resets the dropout counters -- every virtual client starts from those weights
+    exactly as from a loaded checkpoint."""
+    from importlib import import_module
+    runner = import_module(f"{PKG}.fed.runner")
+    config = import_module(f"{PKG}.config")
+    models = import_module(f"{PKG}.models")
+    data = import_module(f"{PKG}.data")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    cfg = _cfg(config, str(tmp_path), 1)
+    cfg.save_checkpoints = False
+    frame = data.generate_cicids2017(cfg.synthetic_rows, seed=0)
+    client = runner.FederatedClient(cfg, frame=frame, model_config=models.DistilBertConfig(n_layers=1)).setup()
+    before = client.model.arena.master.clone()
+    rec = runner.warm_start(client, epochs=1, rows=600)
+    after = client.model.arena.master.clone()
+    assert not torch.equal(before, after)
+    assert rec["train"]["steps"] > 0 and 0.0 <= rec["public_test"]["accuracy"] <= 100.0
+    assert client.model.torch_counter == 0 and int(client.model.rng.item()) == 0
+    res = runner.run_virtual_clients(client, 2, rounds=1)
+    # both clients started from the warm weights: their local models moved away from them
+    assert res["rounds"][0]["clients"][0]["rel_l2_local_to_aggregate"] > 0
