@@ -113,6 +113,7 @@ def test_shard_loader_splits_and_skips():
 
 def _fed_worker(rank, world, port, outdir):
     _env(rank, world, port)
+    torch.set_num_threads(max(1, 8 // world))
     from importlib import import_module
     runner = import_module(f"{PKG}.fed.runner")
     config = import_module(f"{PKG}.config")
@@ -268,3 +269,18 @@ def test_fused_ln_backward_off_beside_collectives():
     assert not m.collectives_in_backward
     dp.GradSync(m, None, 2, overlap=False)  # no per-block hook: nothing runs beside the backward
     assert not m.collectives_in_backward
+
+
+def test_four_dp_clients_on_eight_ranks(tmp_path):
+    """The target node's 8 ranks as 4 clients x 2 data-parallel replicas (--gpus-per-client 2): every
+    replica of every client ends on the same FedAvg aggregate, and rank 0's report has 4 clients."""
+    port = _free_port()
+    mp.spawn(_fed_worker, args=(8, port, str(tmp_path)), nprocs=8, join=True)
+    ms = [torch.load(tmp_path / f"master{r}.pt", weights_only=True) for r in range(8)]
+    for m in ms[1:]:
+        assert torch.equal(ms[0], m)
+    rep = json.load(open(tmp_path / "federated_report.json"))
+    assert len(rep["clients"]) == 4 and rep["gpus_per_client"] == 2 and rep["world_size"] == 8
+    for cid in range(1, 5):
+        assert (tmp_path / f"client{cid}_aggregated_metrics.csv").exists()
+    assert not (tmp_path / "client5_model.pth").exists()
