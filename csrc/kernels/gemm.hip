@@ -2161,7 +2161,7 @@ bool plan_dwb_mix(DwBatch& bt, int mode) {
   // stable reorder by class, in dispatch order: long full tiles, long half tiles, short -- or, with
   // FD_DWB_SHORT_FIRST=1 (A/B), the short tiles (a one-step K loop + a full Adam epilogue: HBM-bound)
   // first, beside the first round's operand-bound K loops
-  static const int short_first = [] { const char* e = getenv("FD_DWB_SHORT_FIRST"); return e ? atoi(e) : 0; }();
+  static const int short_first = [] { const char* e = getenv("FD_DWB_SHORT_FIRST"); return e ? atoi(e) : 1; }();
   const int order[3] = {short_first ? 2 : 0, short_first ? 0 : 1, short_first ? 1 : 2};
   DwProb pr[DWB_MAXP];
   int k = 0, off = 0;
