@@ -66,6 +66,11 @@ int fd_comm_abort(void* comm);
 int fd_comm_allreduce(void* comm, const void* send, void* recv, long long count, int dtype, int op, hipStream_t st);
 int fd_comm_broadcast(void* comm, void* buf, long long count, int dtype, int root, hipStream_t st);
 int fd_comm_allgather(void* comm, const void* send, void* recv, long long count, int dtype, hipStream_t st);
+int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv, int M, int K, const float* kbias,
+                     void* ctx, float* lse, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
+                     float drop_scale, const int* cu, int rows, uint64_t* dmask, int q_live, void* cxc, void* xc,
+                     const void* xres, int Bp, uint64_t* flags, int nflags, const int* cnt, int xsite, int* err,
+                     hipStream_t st);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
                 int rows, uint64_t* dmask, int q_live, void* cxc, void* xc, const void* xres, int Bp,
@@ -923,6 +928,70 @@ void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
            "attn_fwd");
 }
 
+// QKV projection + S <= 128 attention forward in ONE launch (gemm.hip gemm_attn_fwd_kernel):
+// qkv = x w^T + bias, then attn_fwd's outputs.  The tiles hand off to the attention items through
+// QA_FLAGS tagged granules just before the LN2_FLAGS tail of the LayerNorm exchange state `stats`
+// (same epoch `cnt`, timeout flag `err`; xsite unique per launch within an epoch).
+constexpr int64_t QA_FLAGS = 1024, QA_LN2_FLAGS = 512;
+void gemm_attn_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, const at::Tensor& qkv,
+                   const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse, int64_t B, int64_t S,
+                   int64_t H, const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
+                   const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask, int64_t q_live,
+                   const at::Tensor& stats, const at::Tensor& cnt, const at::Tensor& err, int64_t xsite,
+                   const c10::optional<at::Tensor>& cxc = c10::nullopt, const c10::optional<at::Tensor>& xc = c10::nullopt,
+                   const c10::optional<at::Tensor>& xres = c10::nullopt,
+                   const c10::optional<at::Tensor>& prefetch = c10::nullopt) {
+  need(x, at::kBFloat16, "x");
+  need(w, at::kBFloat16, "w");
+  need(bias, at::kFloat, "bias");
+  need(qkv, at::kBFloat16, "qkv");
+  need(kbias, at::kFloat, "kbias");
+  need(ctx, at::kBFloat16, "ctx");
+  need(lse, at::kFloat, "lse");
+  need(stats, at::kLong, "stats");
+  need(cnt, at::kInt, "cnt");
+  need(err, at::kInt, "err");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && qkv.dim() == 2, "gemm_attn_fwd: x, w, qkv must be 2-D");
+  const int64_t M = x.size(0), K = x.size(1), D = H * 64, N = 3 * D;
+  TORCH_CHECK(H > 0 && w.size(0) == N && w.size(1) == K && bias.numel() == N && qkv.size(0) == M && qkv.size(1) == N,
+              "gemm_attn_fwd: w [3 H 64, K], bias [3 H 64], qkv [M, 3 H 64] required");
+  TORCH_CHECK(M > 0 && K % 64 == 0, "gemm_attn_fwd: K must be a multiple of 64");
+  TORCH_CHECK(S % 64 == 0 && S <= 128 && B > 0, "gemm_attn_fwd: S must be 64 or 128");
+  TORCH_CHECK(M * N * 2 < (int64_t(1) << 31), "gemm_attn_fwd: qkv must stay below 2 GiB (32-bit buffer offsets)");
+  TORCH_CHECK(q_live >= 0, "gemm_attn_fwd: q_live >= 0");
+  TORCH_CHECK(xsite >= 0 && xsite < FD_LN_XSITES - 1, "gemm_attn_fwd: exchange call site out of range");
+  TORCH_CHECK(cnt.numel() >= 1 && err.numel() >= 1, "gemm_attn_fwd: counters too small");
+  const int64_t ntiles = ((M + 127) / 128) * (N / 192);
+  TORCH_CHECK(ntiles <= QA_FLAGS && stats.numel() >= QA_FLAGS + QA_LN2_FLAGS,
+              "gemm_attn_fwd: more tiles than flag granules, or stats too small");
+  const bool compact = cxc.has_value() && cxc->defined();
+  int64_t Bp = 0;
+  if (compact) {
+    TORCH_CHECK(q_live == 1 && xc.has_value() && xres.has_value(), "gemm_attn_fwd: compact rows need q_live 1, xc, xres");
+    need(*cxc, at::kBFloat16, "cxc");
+    need(*xc, at::kBFloat16, "xc");
+    need(*xres, at::kBFloat16, "xres");
+    Bp = cxc->numel() / D;
+    TORCH_CHECK(Bp >= B && cxc->numel() == Bp * D && xc->numel() == cxc->numel(), "gemm_attn_fwd: cxc/xc size");
+    TORCH_CHECK(xres->numel() == ctx.numel(), "gemm_attn_fwd: xres size");
+  }
+  check_dmask(dmask, B, S, H);
+  const bool varlen = cu.has_value() && cu->defined();
+  const int64_t rows = varlen ? M : B * S;
+  TORCH_CHECK(M == rows && ctx.numel() == rows * D, "gemm_attn_fwd: qkv/ctx rows");
+  TORCH_CHECK((varlen || kbias.numel() == B * S) && lse.numel() == B * H * S, "gemm_attn_fwd: kbias/lse size");
+  check_cu(cu, B, rows, rows);
+  uint64_t* flags = reinterpret_cast<uint64_t*>(stats.data_ptr()) + (stats.numel() - QA_LN2_FLAGS - QA_FLAGS);
+  set_prefetch(prefetch, x);
+  check_rc(fd_gemm_attn_fwd(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), qkv.data_ptr(), (int)M, (int)K,
+                            kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(), (int)B, (int)S, (int)H,
+                            seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), (int)rows,
+                            ptr<uint64_t>(dmask), (int)q_live, compact ? cxc->data_ptr() : nullptr,
+                            compact ? xc->data_ptr() : nullptr, compact ? xres->data_ptr() : nullptr, (int)Bp, flags,
+                            (int)QA_FLAGS, cnt.data_ptr<int>(), (int)xsite, err.data_ptr<int>(), stream()),
+           "gemm_attn_fwd");
+}
+
 void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
               const at::Tensor& dctx, const at::Tensor& delta, const at::Tensor& dqkv, int64_t B, int64_t S, int64_t H,
               const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& cu,
@@ -1521,6 +1590,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_allreduce", &comm_allreduce);
   m.def("comm_broadcast", &comm_broadcast);
   m.def("comm_allgather", &comm_allgather);
+  m.def("gemm_attn_fwd", &gemm_attn_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("qkv"),
+        py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"),
+        py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("q_live"),
+        py::arg("stats"), py::arg("cnt"), py::arg("err"), py::arg("xsite"), py::arg("cxc") = py::none(),
+        py::arg("xc") = py::none(), py::arg("xres") = py::none(), py::arg("prefetch") = py::none());
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("B"),
         py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"),
         py::arg("dmask"), py::arg("q_live") = 0, py::arg("cxc") = py::none(), py::arg("xc") = py::none(),

@@ -290,6 +290,35 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
   else hc::span(kbias, (long long)B * S * 4, "attn kbias");
   return 0;
 }
+int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv, int M, int K, const float* kbias,
+                     void* ctx, float* lse, int B, int S, int H, const uint32_t* seed, uint32_t, uint32_t, float,
+                     const int* cu, int rows, uint64_t* dmask, int, void* cxc, void* xc, const void* xres, int Bp,
+                     uint64_t* flags, int nflags, const int* cnt, int, int* err, hipStream_t) {
+  ++hc::calls;
+  if (g_hc_pf) hc::span(g_hc_pf, g_hc_pf_bytes, "gemm_attn prefetch");
+  g_hc_pf = nullptr;
+  g_hc_pf_bytes = 0;
+  const long long D = (long long)H * 64, N = 3 * D;
+  hc::span(x, (long long)M * K * 2, "gemm_attn x");
+  hc::span(w, N * K * 2, "gemm_attn w");
+  hc::span(bias, N * 4, "gemm_attn bias");
+  hc::span(qkv, (long long)M * N * 2, "gemm_attn qkv");
+  const long long tiles = ((M + 127) / 128) * (N / 192);
+  if (tiles > nflags) hc::violations.push_back("gemm_attn: more tiles than flags");
+  hc::span(flags, tiles * 8, "gemm_attn flags");
+  hc::span(cnt, 4, "gemm_attn cnt");
+  hc::span(err, 4, "gemm_attn err");
+  hc::opt_span(cxc, (long long)Bp * D * 2, "gemm_attn cxc");
+  hc::opt_span(xc, (long long)Bp * D * 2, "gemm_attn xc");
+  hc::opt_span(xres, rows * D * 2, "gemm_attn xres");
+  hc::opt_span(dmask, (long long)B * H * 256 * 8, "gemm_attn dmask");
+  hc::span(ctx, rows * D * 2, "gemm_attn ctx");
+  hc::span(lse, (long long)B * H * S * 4, "gemm_attn lse");
+  hc::span(seed, 4, "gemm_attn seed");
+  if (cu) hc::span(cu, (long long)(B + 1) * 4, "gemm_attn cu");
+  else hc::span(kbias, (long long)B * S * 4, "gemm_attn kbias");
+  return 0;
+}
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx, float* delta,
                 void* dqkv, int B, int S, int H, const uint32_t* seed, uint32_t, uint32_t, float, const int* cu,
                 int rows, const uint64_t* dmask, int, const void* dresc, void* dres, hipStream_t) {

@@ -37,6 +37,7 @@
 namespace {
 
 #include "adam_common.h"
+#include "attn_s128.h"
 
 enum Epi : int {
   EPI_BF16 = 0,       // C(bf16) = acc
@@ -237,6 +238,9 @@ struct Operand {
   }
 };
 
+constexpr uint32_t LN2_SC1 = 16;  // buffer-op cache policy: sc1 (write-through / L1 bypass)
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
 // ---------------------------------------------------------------- epilogue
 // Each wave parks its accumulators in LDS (bias applied; bf16, or fp32 when the
 // finishing math needs per-element operands and the fp32 tile fits), then the
@@ -363,10 +367,12 @@ DEV void pf_consume(const PfRegs& r) {
   for (int k = 0; k < PF_N; ++k) asm volatile("" ::"v"(r.v[k]));
 }
 
-template <int BM, int BN, int TM, int TN, int EPI, int NT, int NPRE>
+template <int BM, int BN, int TM, int TN, int EPI, int NT, int NPRE, bool WT = false>
 DEV void staged_epilogue_out(const GemmParams& p, char* smem, int m0, int n0, int tid, const uint4 (&pre)[NPRE]);
 
-template <int BM, int BN, int TM, int TN, int EPI, int NT>
+// WT: the bf16 tile goes out with write-through (sc1) stores that every thread drains before
+// returning (the fused QKV + attention launch: blocks of the same launch on other XCDs read it)
+template <int BM, int BN, int TM, int TN, int EPI, int NT, bool WT = false>
 DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], char* smem, int m0, int n0,
                          int wr, int wc, int lane, int tid) {
   using TR = EpiTraits<EPI, BM, BN>;
@@ -425,14 +431,15 @@ DEV void staged_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 1
   } else {
     // the next launch's weight (p.ln.pf, fd_gemm_pf): issued after every load this epilogue waits for
     const PfRegs pfr = pf_issue<NT>(p.ln, tid);
-    staged_epilogue_out<BM, BN, TM, TN, EPI, NT>(p, smem, m0, n0, tid, pre);
+    staged_epilogue_out<BM, BN, TM, TN, EPI, NT, PRE ? NCH : 1, WT>(p, smem, m0, n0, tid, pre);
     pf_consume(pfr);
   }
 }
 
-template <int BM, int BN, int TM, int TN, int EPI, int NT, int NPRE>
+template <int BM, int BN, int TM, int TN, int EPI, int NT, int NPRE, bool WT>
 DEV void staged_epilogue_out(const GemmParams& p, char* smem, int m0, int n0, int tid, const uint4 (&pre)[NPRE]) {
   using TR = EpiTraits<EPI, BM, BN>;
+  static_assert(!WT || EPI == EPI_BIAS || EPI == EPI_BF16, "write-through stores: plain bf16 epilogues only");
   constexpr int LDC = BN * TR::ES + 16;
   constexpr int CPR8 = BN / 8, NCH = BM * CPR8 / NT;
   constexpr bool PRE = TR::ELEM && TR::F32S && (BM * CPR8) % NT == 0 && NCH <= 8;
@@ -455,10 +462,16 @@ DEV void staged_epilogue_out(const GemmParams& p, char* smem, int m0, int n0, in
         y.z = pack_bf2(gelu_erf(lo_bf(u.z)), gelu_erf(hi_bf(u.z)));
         y.w = pack_bf2(gelu_erf(lo_bf(u.w)), gelu_erf(hi_bf(u.w)));
         *reinterpret_cast<uint4*>(C + (size_t)m * p.ldc + n) = y;
+      } else if constexpr (WT) {
+        // (the resource from kernel arguments only: uniform; < 2 GiB checked by the launcher)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, u),
+                                               __builtin_amdgcn_make_buffer_rsrc(p.C, 0, 0x7fffffff, 0x00020000),
+                                               (int)(((size_t)m * p.ldc + n) * 2), 0, LN2_SC1);
       } else {
         *reinterpret_cast<uint4*>(C + (size_t)m * p.ldc + n) = u;
       }
     }
+    if constexpr (WT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing thread drains
   } else if constexpr (EPI == EPI_F32) {
     f32_epilogue<BM, BN, NT>(p, smem, LDC, m0, n0, tid);
   } else {
@@ -947,9 +960,6 @@ DEV void ln_epilogue(const GemmParams& p, const f32x4 (&acc)[TM / 16][TN / 16], 
 // agent-scope atomic store; each receiving wave polls the partner's flag with agent-scope atomic
 // loads and reads the payload with sc1 loads only after its own poll has matched.  The tag is the
 // LayerNorm exchange's (epoch * FD_LN_XSITES + xsite + 1): stale flags never match.
-constexpr uint32_t LN2_SC1 = 16;  // buffer-op cache policy: sc1 (write-through / L1 bypass)
-
-typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 
 DEV __amdgpu_buffer_rsrc_t ln2_rsrc(const FdLnEpi& L) {
   // the whole exchange buffer, from kernel arguments only (wave-uniform: no waterfall loops);
@@ -1093,7 +1103,7 @@ struct GemmGroup {
 #endif
 
 // One output tile (tm, tn) of problem p: the K loop over the LDS-DMA ring, then the epilogue.
-template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, int BK = BKT>
+template <int BM, int BN, bool AK, bool BKM, int EPI, int WM, int WN, int S, int BK = BKT, bool WT = false>
 DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
   const int tm_ = tm, tn_ = tn;
   using G = GemmCfg<BM, BN, AK, BKM, EPI, WM, WN, S, BK>;
@@ -1322,7 +1332,7 @@ DEV void gemm_tile_at(const GemmParams& p, int tm, int tn, char* smem) {
     // every DMA has been waited for (the last iteration waits vmcnt(0)); after this
     // barrier no wave still reads a ring slot, so the epilogue may reuse the LDS.
     __syncthreads();
-    staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW>(p, acc, smem, m0, n0, wr, wc, lane, tid);
+    staged_epilogue<BM, BN, TM, TN, EPI, 64 * NW, WT>(p, acc, smem, m0, n0, wr, wc, lane, tid);
   }
 }
 
@@ -1349,6 +1359,70 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmParams p0, Ge
   __syncthreads();
   FD_STAMP(5);
 #endif
+}
+
+// ---------------------------------------------------------------- QKV projection + attention forward
+// One launch instead of two per block: blocks [0, ntiles) are the QKV GEMM's
+// 128 x 192 tiles (cfg 6, bias epilogue), blocks after them the S <= 128 attention forward's
+// (sequence, head) items (attn_fwd_s128_body, attn_s128.h).  A tile's bf16 output goes out with
+// write-through (sc1) stores that every thread drains; then ONE lane stores the tile's {tag, 1}
+// granule (agent-scope relaxed atomic, no fence: gfx950's release fence would write back the whole
+// L2).  An attention item polls the granules of the tiles holding its rows' Q, K and V columns
+// (<= 2 row blocks x 3 column tiles), then stages them with sc1 loads -- the LayerNorm exchange's
+// hand-off (ln2_send / ln2_recv).  The tag is the exchange's: epoch * FD_LN_XSITES + xsite + 1, so
+// granules of earlier launches never match.  Progress: a GEMM tile never waits, and every tile has
+// a lower block index than every attention item, so the items wait only on tiles that were
+// dispatched before them.  The poll is bounded (0.25 s; err |= 4, fatal on the host).
+struct QkvAttnSync {
+  uint64_t* flags;  // [ntiles] tile granules (the LayerNorm state's tail: zeroed at a tag wrap)
+  const int* cnt;   // exchange epoch (advanced once per model forward)
+  int* err;
+  int xsite;
+  int ntiles, tiles_n;
+};
+constexpr int QA_BM = 128, QA_BN = 192, QA_NW = 8;
+using QaCfg = GemmCfg<QA_BM, QA_BN, true, true, EPI_BIAS, 2, 4, 2>;
+static_assert(QaCfg::VALID && QaCfg::NW == QA_NW && QaCfg::SMEM >= ATT_FWD_SMEM, "fused QKV + attention tile");
+
+__global__ __launch_bounds__(64 * QA_NW, 2) void gemm_attn_fwd_kernel(GemmParams p, AttnArgs a, QkvAttnSync q) {
+  __shared__ __attribute__((aligned(1024))) char smem[QaCfg::SMEM];
+  const uint32_t tag =
+      (uint32_t)__hip_atomic_load(q.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * FD_LN_XSITES + q.xsite + 1u;
+  if ((int)blockIdx.x < q.ntiles) {
+    FD_STAMP(0);
+    stamp_hwid();
+    int tm, tn;
+    tile_coords(xcd_remap(blockIdx.x, q.ntiles), (p.M + QA_BM - 1) / QA_BM, q.tiles_n, p.group_m, tm, tn);
+    gemm_tile_at<QA_BM, QA_BN, true, true, EPI_BIAS, 2, 4, 2, BKT, true>(p, tm, tn, smem);
+    __syncthreads();  // every thread's write-through stores have completed
+    if (threadIdx.x == 0)
+      __hip_atomic_store(q.flags + tm * q.tiles_n + tn, ((uint64_t)tag << 32) | 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int item = (int)blockIdx.x - q.ntiles, b = item / a.H, h = item - b * a.H;
+  if (b < a.B) {  // (the filler item b == B reads no projection)
+    int tok0, len;
+    seq_span(a, b, tok0, len);
+    if (len > 0 && threadIdx.x < 64) {
+      const int lane = threadIdx.x, D = a.H * DH;
+      const int tm0 = tok0 / QA_BM, nf = ((tok0 + len - 1) / QA_BM - tm0 + 1) * 3;
+      uint64_t* fp = nullptr;
+      if (lane < nf) fp = q.flags + (tm0 + lane / 3) * q.tiles_n + ((lane % 3) * D + h * DH) / QA_BN;
+      const uint64_t t0 = wall_clock64();
+      for (;;) {
+        const bool ok = fp == nullptr || (uint32_t)(ld_gran(fp) >> 32) == tag;
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > 25000000ull) {  // 0.25 s: never in a healthy launch
+          if (lane == 0) __hip_atomic_fetch_or(q.err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();  // (no load of the body is issued before the poll matched)
+  }
+  attn_fwd_s128_body<QA_NW, true>(a, b, h, 0, smem);
 }
 
 // LayerNorm-fused NT GEMM (EPI_LN / EPI_LN_BWD): the tiles of a row block are consecutive
@@ -1973,6 +2047,48 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
   }
   if (ldc != N) return 4;
   return dw_launch(&p, 1, id, splits, K, workspace, workspace_elems, accumulate, adam, 0, nullptr, st);
+}
+
+// QKV projection (x [M][K] W^T [N = 3 H 64][K] + bias -> qkv bf16) fused with the S <= 128 attention
+// forward (fd_attn_fwd's arguments) in ONE launch (gemm_attn_fwd_kernel).  flags: >= tiles granules
+// (int64, zeroed once), cnt the LayerNorm exchange epoch, err its timeout flag, xsite < FD_LN_XSITES - 1
+// unique per launch within an epoch.  Nothing is launched on a non-zero return.
+int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv, int M, int K, const float* kbias,
+                     void* ctx, float* lse, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
+                     float drop_scale, const int* cu, int rows, uint64_t* dmask, int q_live, void* cxc, void* xc,
+                     const void* xres, int Bp, uint64_t* flags, int nflags, const int* cnt, int xsite, int* err,
+                     hipStream_t st) {
+  const char* pf = g_gemm_pf;  // (an armed prefetch belongs to this call whatever happens below)
+  const long long pf_bytes = g_gemm_pf_bytes;
+  g_gemm_pf = nullptr;
+  g_gemm_pf_bytes = 0;
+  const int D = H * DH, N = 3 * D;
+  if (M <= 0 || K % BKT || N % QA_BN || S % 64 || S > 128 || B <= 0 || !bias || !flags || !cnt || !err) return 1;
+  if (xsite < 0 || xsite >= FD_LN_XSITES - 1) return 2;
+  if ((cu ? rows : B * S) != M || (long long)M * N * 2 >= (1ll << 31)) return 3;
+  if (cxc && (!xc || !xres || q_live != 1 || Bp < B)) return 4;
+  const int tiles_n = N / QA_BN, ntiles = ((M + QA_BM - 1) / QA_BM) * tiles_n;
+  if (ntiles > nflags) return 5;
+  GemmParams p{};
+  p.ln.pf = pf;
+  p.ln.pf_bytes = pf_bytes;
+  p.A = (const bf16_t*)x; p.B = (const bf16_t*)w; p.C = qkv;
+  p.M = M; p.N = N; p.K = K; p.lda = K; p.ldb = K; p.ldc = N;
+  p.bias = bias;
+  p.k_split = K;
+  p.group_m = (int)std::max(1ll, std::min(16ll, (2ll << 20) / ((long long)QA_BM * K * 2)));  // (as fd_gemm_ex)
+  AttnArgs a{};
+  a.cxc = (bf16_t*)cxc; a.xc = (bf16_t*)xc; a.xres = (const bf16_t*)xres; a.Bp = Bp;
+  a.q_live = q_live;
+  a.cu = cu;
+  a.dmask = dmask;
+  a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
+  a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
+  a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
+  QkvAttnSync q{flags, cnt, err, xsite, ntiles, tiles_n};
+  const int items = H * (B + (cu ? 1 : 0));
+  hipLaunchKernelGGL(gemm_attn_fwd_kernel, dim3(ntiles + items), dim3(64 * QA_NW), 0, st, p, a, q);
+  return 0;
 }
 
 // Split-K NT product into fp32 slabs: slabs[z][M][N] = A[M][k in split z] Bt[N][k in split z]^T

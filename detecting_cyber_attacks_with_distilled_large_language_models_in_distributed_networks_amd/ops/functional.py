@@ -208,9 +208,14 @@ class LayerFn(torch.autograd.Function):
         p_h = rc.p_hidden if rc.training else 0.0
         attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
         grad = ctx.needs_input_grad[0]
-        qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"], prefetch=L["o_w"])  # (out_lin follows attention)
         dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
-        cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask)
+        if rc.fuse_ln and K.qkv_attn_ok(x.shape[0], x.shape[1], rc.S):
+            # QKV projection + attention in one launch (the exchange epoch advances per forward)
+            qkv, cx, lse = K.qkv_attn_fwd(x, L["qkv_w"], L["qkv_b"], rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site,
+                                          p_a, rc.cu, dmask, xsite=K.ln_xsite(idx, 0, False), prefetch=L["o_w"])
+        else:
+            qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"], prefetch=L["o_w"])  # (out_lin follows attention)
+            cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask)
         fuse_ln = rc.fuse_ln and K.ln_fusable(x.shape[0], x.shape[1], K=(x.shape[1], L["l2_w"].shape[1]))
         if fuse_ln:
             # bias + (dropout) + residual + LayerNorm in the N = 768 GEMMs' epilogues; the
@@ -248,14 +253,20 @@ class LayerFn(torch.autograd.Function):
         p_h = rc.p_hidden if rc.training else 0.0
         attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
         grad = ctx.needs_input_grad[0]
-        qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
         dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
         # only each sequence's first query row ([CLS]) is needed: the other rows' context is never read
         ci, rm = rc.cls_rows, rc.cls_rmap
-        if K.attn_cls_compact_ok(rc.S):  # the attention launch also writes the compact [CLS] rows
+        if rc.fuse_ln and K.attn_cls_compact_ok(rc.S) and K.qkv_attn_ok(x.shape[0], x.shape[1], rc.S):
+            # QKV projection + [CLS]-row attention (+ the compact rows) in one launch
+            qkv, cx, lse, cxc, xc = K.qkv_attn_fwd(x, L["qkv_w"], L["qkv_b"], rc.kbias, rc.B, rc.S, rc.H, rc.seed,
+                                                   attn_site, p_a, rc.cu, dmask, q_live=1, cls=(x, ci.numel()),
+                                                   xsite=K.ln_xsite(idx, 0, False))
+        elif K.attn_cls_compact_ok(rc.S):  # the attention launch also writes the compact [CLS] rows
+            qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
             cx, lse, cxc, xc = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask,
                                           q_live=1, cls=(x, ci.numel()))
         else:
+            qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
             cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask, q_live=1)
             cxc, xc = K.gather_rows2(cx, x, ci)
         h, ao, m1, r1 = K.linear_ln_fwd(cxc, L["o_w"], L["o_b"], xc, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0,

@@ -372,6 +372,47 @@ def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: in
     return ctx, lse, cxc, xc
 
 
+# QKV projection + S <= 128 attention forward in ONE launch (csrc/kernels/gemm.hip gemm_attn_fwd_kernel):
+# the attention items start on the tiles they need instead of after a launch boundary.  Needs the
+# LayerNorm exchange epoch to advance once per model forward (RunCtx.fuse_ln: emb_fwd does it).
+# Off by default: bitwise equal, but step-neutral (26.0 vs 15.7 + 10.4 us per layer; the one-round
+# GEMM's tiles all finish together, so the attention items cannot start early --
+# profiles/r6_ab_fused_qkv_attention.txt).  FD_FUSE_QKV_ATTN=1: on.
+FUSE_QKV_ATTN = _os.environ.get("FD_FUSE_QKV_ATTN", "0") != "0"
+
+
+def qkv_attn_ok(M: int, D: int, S: int) -> bool:
+    """Shapes the fused QKV + attention launch takes (csrc/binding.cpp gemm_attn_fwd)."""
+    return (FUSE_QKV_ATTN and not _SHARED_DEVICE and _os.environ.get("FD_ATTN_S128", "1") != "0"
+            and S in (64, 128) and D % 64 == 0 and M > 0 and M * 3 * D * 2 < 2 ** 31
+            and ((M + 127) // 128) * (3 * D // 192) <= QA_FLAGS)
+
+
+def qkv_attn_fwd(x, w, b, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, cls=None,
+                 xsite: int = 0, prefetch=None):
+    """``linear_fwd(x, w, b)`` then ``attn_fwd(qkv, ...)`` as one launch (``qkv_attn_ok``).  xsite:
+    this launch's call site within the current exchange epoch (``ln_xsite``; the fused launches
+    keep their own granules, so a block's LayerNorm site number can be reused).  Returns
+    (qkv, ctx, lse) or, with cls = (x_res, Bp), (qkv, ctx, lse, cxc, xc)."""
+    M, D = x.shape[0], H * 64
+    qkv = torch.empty(M, 3 * D, dtype=torch.bfloat16, device=x.device)
+    rows = M if cu is not None else B * S
+    ctx = torch.empty(rows, D, dtype=torch.bfloat16, device=x.device)
+    lse = torch.empty(B, H, S, dtype=torch.float32, device=x.device)
+    thr, sc = _drop(p)
+    stats, cnt, err = _ln_state(x.device, M, D)
+    kw = {}
+    if cls is not None:
+        xr, Bp = cls
+        kw = dict(cxc=torch.empty(Bp, D, dtype=torch.bfloat16, device=x.device), xres=xr)
+        kw["xc"] = torch.empty_like(kw["cxc"])
+    ext().gemm_attn_fwd(x, w, b, qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None,
+                        q_live, stats, cnt, err, int(xsite), prefetch=_pf(prefetch), **kw)
+    if cls is None:
+        return qkv, ctx, lse
+    return qkv, ctx, lse, kw["cxc"], kw["xc"]
+
+
 def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, dresc=None):
     """dmask: the keep bits recorded by the matching ``attn_fwd`` (same seed / site / p).
 
@@ -441,15 +482,17 @@ def _ln_state(device, M: int, N: int):
         # the epoch survives a regrow: a granule tag must never repeat on the same state
         epoch = st[1] if st is not None else torch.zeros(2, dtype=torch.int32, device=device)
         err = st[2] if st is not None else torch.zeros(1, dtype=torch.int32, device=device)
-        # (+ LN2_FLAGS granules at the tail: the two-K-half tiles' exchange flags, csrc/binding.cpp)
-        st = (torch.zeros(2 * (rows + 256) * (N // 64) + LN2_FLAGS, dtype=torch.int64, device=device), epoch, err,
-              rows)
+        # (+ QA_FLAGS granules of the fused QKV + attention launch, then LN2_FLAGS at the tail: the
+        # two-K-half tiles' exchange flags, csrc/binding.cpp)
+        st = (torch.zeros(2 * (rows + 256) * (N // 64) + QA_FLAGS + LN2_FLAGS, dtype=torch.int64, device=device),
+              epoch, err, rows)
         _WS[key] = st
     return st[:3]
 
 
 LN_XSITES = 128  # csrc/kernels/adam_epi.h FD_LN_XSITES: exchange call sites per epoch
 LN2_FLAGS = 512  # csrc/binding.cpp gemm_ln: flag granules of the two-K-half tiles
+QA_FLAGS = 1024  # csrc/binding.cpp gemm_attn_fwd: tile granules of the fused QKV + attention launch
 # Two-K-half LayerNorm-fused GEMMs (csrc/kernels/gemm.hip gemm_ln2_kernel, K >= FD_GEMM_LN2_MINK):
 # the fp32 partial-tile exchange buffer (FD_LN2=0: never passed, the one-pass kernels run)
 LN2 = _os.environ.get("FD_LN2", "1") != "0"
