@@ -70,7 +70,7 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
                      void* ctx, float* lse, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
                      float drop_scale, const int* cu, int rows, uint64_t* dmask, int q_live, void* cxc, void* xc,
                      const void* xres, int Bp, uint64_t* flags, int nflags, const int* cnt, int xsite, int* err,
-                     hipStream_t st);
+                     int mode, hipStream_t st);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
                 int rows, uint64_t* dmask, int q_live, void* cxc, void* xc, const void* xres, int Bp,
@@ -940,8 +940,11 @@ void gemm_attn_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
                    const at::Tensor& stats, const at::Tensor& cnt, const at::Tensor& err, int64_t xsite,
                    const c10::optional<at::Tensor>& cxc = c10::nullopt, const c10::optional<at::Tensor>& xc = c10::nullopt,
                    const c10::optional<at::Tensor>& xres = c10::nullopt,
-                   const c10::optional<at::Tensor>& prefetch = c10::nullopt) {
+                   const c10::optional<at::Tensor>& prefetch = c10::nullopt, int64_t mode = 1) {
+  // mode 1: the projection's tiles hand off to the attention items (flags); mode 2: one block per
+  // (sequence, head) projects its own Q / K / V tile into the attention's LDS images
   need(x, at::kBFloat16, "x");
+  TORCH_CHECK(mode == 1 || mode == 2, "gemm_attn_fwd: mode 1 or 2");
   need(w, at::kBFloat16, "w");
   need(bias, at::kFloat, "bias");
   need(qkv, at::kBFloat16, "qkv");
@@ -988,7 +991,7 @@ void gemm_attn_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
                             seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), (int)rows,
                             ptr<uint64_t>(dmask), (int)q_live, compact ? cxc->data_ptr() : nullptr,
                             compact ? xc->data_ptr() : nullptr, compact ? xres->data_ptr() : nullptr, (int)Bp, flags,
-                            (int)QA_FLAGS, cnt.data_ptr<int>(), (int)xsite, err.data_ptr<int>(), stream()),
+                            (int)QA_FLAGS, cnt.data_ptr<int>(), (int)xsite, err.data_ptr<int>(), (int)mode, stream()),
            "gemm_attn_fwd");
 }
 
@@ -1594,7 +1597,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"),
         py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("q_live"),
         py::arg("stats"), py::arg("cnt"), py::arg("err"), py::arg("xsite"), py::arg("cxc") = py::none(),
-        py::arg("xc") = py::none(), py::arg("xres") = py::none(), py::arg("prefetch") = py::none());
+        py::arg("xc") = py::none(), py::arg("xres") = py::none(), py::arg("prefetch") = py::none(),
+        py::arg("mode") = 1);
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("B"),
         py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"),
         py::arg("dmask"), py::arg("q_live") = 0, py::arg("cxc") = py::none(), py::arg("xc") = py::none(),

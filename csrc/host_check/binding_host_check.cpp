@@ -293,7 +293,7 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
 int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv, int M, int K, const float* kbias,
                      void* ctx, float* lse, int B, int S, int H, const uint32_t* seed, uint32_t, uint32_t, float,
                      const int* cu, int rows, uint64_t* dmask, int, void* cxc, void* xc, const void* xres, int Bp,
-                     uint64_t* flags, int nflags, const int* cnt, int, int* err, hipStream_t) {
+                     uint64_t* flags, int nflags, const int* cnt, int, int* err, int, hipStream_t) {
   ++hc::calls;
   if (g_hc_pf) hc::span(g_hc_pf, g_hc_pf_bytes, "gemm_attn prefetch");
   g_hc_pf = nullptr;
@@ -755,6 +755,28 @@ int main() {
     expect_reject("attn dmask size", [&] { attn_fwd(qkv, kb, ctx, lse, B, S, H, seed, 16, 429496730, 1.1, none, dm_bad); });
     expect_reject("attn dmask S=512", [&] { attn_fwd(q5, k5, c5, l5, 2, S5, H, seed, 16, 0, 1.0, none, dm); });
     expect_reject("attn bwd dqkv size", [&] { attn_bwd(qkv, kb, ctx, lse, dctx, delta, ctx, B, S, H, seed, 16, 0, 1.0, none, none); });
+    // fused QKV projection + attention (both modes): flags in the LayerNorm state's tail
+    auto x = T_({rows, H * 64}, bf), w = T_({3 * H * 64, H * 64}, bf), bq = T_({3 * H * 64}, f32);
+    auto stats = T_({4096}, i64), cnt = T_({2}, i32), err = T_({1}, i32);
+    for (int64_t mode : {1, 2}) {
+      expect_ok("qkv attn fwd", [&] { gemm_attn_fwd(x, w, bq, qkv, kb, ctx, lse, B, S, H, seed, 16, 429496730, 1.1,
+                                                   none, dm, 0, stats, cnt, err, 2, none, none, none, none, mode); });
+      auto xv = T_({300, H * 64}, bf);
+      expect_ok("qkv attn fwd varlen", [&] { gemm_attn_fwd(xv, w, bq, qv, kb, cv, lse, B, S, H, seed, 16, 0, 1.0, cu,
+                                                          none, 0, stats, cnt, err, 2, none, none, none, none, mode); });
+    }
+    expect_reject("qkv attn S=256", [&] { gemm_attn_fwd(x, w, bq, qkv, kb, ctx, lse, 2, 256, H, seed, 16, 0, 1.0, none,
+                                                        none, 0, stats, cnt, err, 2, none, none, none, none, 1); });
+    expect_reject("qkv attn w shape", [&] { gemm_attn_fwd(x, T_({2 * H * 64, H * 64}, bf), bq, qkv, kb, ctx, lse, B, S, H,
+                                                          seed, 16, 0, 1.0, none, none, 0, stats, cnt, err, 2, none,
+                                                          none, none, none, 1); });
+    expect_reject("qkv attn stats", [&] { gemm_attn_fwd(x, w, bq, qkv, kb, ctx, lse, B, S, H, seed, 16, 0, 1.0, none,
+                                                        none, 0, T_({1000}, i64), cnt, err, 2, none, none, none, none,
+                                                        1); });
+    expect_reject("qkv attn xsite", [&] { gemm_attn_fwd(x, w, bq, qkv, kb, ctx, lse, B, S, H, seed, 16, 0, 1.0, none,
+                                                        none, 0, stats, cnt, err, 127, none, none, none, none, 1); });
+    expect_reject("qkv attn mode", [&] { gemm_attn_fwd(x, w, bq, qkv, kb, ctx, lse, B, S, H, seed, 16, 0, 1.0, none,
+                                                       none, 0, stats, cnt, err, 2, none, none, none, none, 3); });
   }
   // ---- LayerNorm fwd / bwd
   {

@@ -373,7 +373,7 @@ __global__ __launch_bounds__(256) void mask_to_bias_kernel(const M* mask, float*
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_s128_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[ATT_FWD_SMEM];
-  attn_fwd_s128_body<NW, false>(a, blockIdx.z, blockIdx.y, blockIdx.x, smem);
+  attn_fwd_s128_body<NW, 0>(a, blockIdx.z, blockIdx.y, blockIdx.x, smem);
 }
 
 // ---- S <= 128 backward phases (shared by the fused one-block kernel and the two-block split)

@@ -252,9 +252,13 @@ DEV void stage_rows_sc1(char* lds, __amdgpu_buffer_rsrc_t rs, long off0, long ld
 // (sequence, head).  (NW = 4, two blocks per (sequence, head), measured no faster:
 // profiles/r4_rejected_ab.txt.)
 // The body takes its (sequence b, head h, query block bx) and LDS from the caller: the standalone
-// kernel below, or the fused QKV + attention launch (COH: Q / K / V read with sc1 loads).
+// kernel below, or the fused QKV + attention launches (gemm.hip).  MODE: 0 Q / K / V from global
+// memory, 1 the same through write-through-coherent sc1 loads, 2 already in LDS as the swizzled
+// images K = smem, V = smem + 16 KiB, Q = smem + ATT_FWD_SMEM (written by the caller's projection
+// tile; rows past the sequence hold finite values of other rows -- masked keys, unstored queries).
 constexpr int ATT_FWD_SMEM = 4 * 8192 + 512;
-template <int NW, bool COH>
+constexpr int ATT_FWD_SMEM_Q = ATT_FWD_SMEM + 2 * 8192;
+template <int NW, int MODE>
 DEV void attn_fwd_s128_body(const AttnArgs& a, int b, int h, int bx, char* smem) {
   char* ks = smem;
   char* vs = smem + 2 * 8192;
@@ -297,7 +301,11 @@ DEV void attn_fwd_s128_body(const AttnArgs& a, int b, int h, int bx, char* smem)
   const int qr = min(q, len - 1);
   const bool varlen = a.cu != nullptr;
   bf16x8 qf[2];  // this wave's Q rows, fetched together with the K/V staging loads
-  if constexpr (COH) {
+  if constexpr (MODE == 2) {
+    const char* qs = smem + ATT_FWD_SMEM;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) qf[s2] = row_frag(qs + (q0 >> 6) * 8192, q0 & 63, s2, lane);
+  } else if constexpr (MODE == 1) {
     // (the resource from the kernel argument alone: uniform; every per-block part in the offset)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.qkv), 0, 0x7fffffff,
                                                                         0x00020000);

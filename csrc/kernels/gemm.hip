@@ -1422,7 +1422,135 @@ __global__ __launch_bounds__(64 * QA_NW, 2) void gemm_attn_fwd_kernel(GemmParams
     }
     __syncthreads();  // (no load of the body is issued before the poll matched)
   }
-  attn_fwd_s128_body<QA_NW, true>(a, b, h, 0, smem);
+  attn_fwd_s128_body<QA_NW, 1>(a, b, h, 0, smem);
+}
+
+// ---------------------------------------------------------------- per-(sequence, head) QKV + attention
+// Mode 2 of the fused QKV + attention forward: one block per (sequence, head) computes that head's
+// Q, K and V columns of the sequence's rows itself -- a 128 x 192 projection tile whose A rows start
+// at the sequence's first packed row and whose B rows are W's rows h 64.., D + h 64.., 2 D + h 64..
+// -- and parks it (bias added, bf16: the values the separate GEMM stores) straight into the
+// attention's swizzled LDS images, so the attention needs no global round trip and no hand-off.
+// The K loop is gemm_tile_at's (same MFMA chain per element, so qkv is bitwise the GEMM's); a wave
+// skips the MFMAs of its 16-row sub-tiles past the sequence (their rows are never stored).  The
+// sequence's qkv rows still go out (the backward reads them); filler rows past cu[B] are zeroed.
+// Cost: a 128-row tile per sequence of <= 128 rows (packed CICIDS2017 rows average ~84).
+struct SeqQkvArgs {
+  const bf16_t* x;   // [M][K]
+  const bf16_t* w;   // [3 D][K]
+  const float* bias; // [3 D]
+  int M, K;
+};
+using SaA = Operand<128, true, 8>;
+using SaB = Operand<192, true, 8>;
+constexpr int SA_S = 2, SA_BUF = SaA::BYTES + SaB::BYTES;
+static_assert(SA_S * SA_BUF >= ATT_FWD_SMEM_Q, "the attention images fit the projection ring");
+
+// head h's Q, K, V weight rows as one 192-row K-major B tile (Operand::stage with a row map)
+DEV void sa_stage_b(const bf16_t* w, int ld, int D, int h, int k0, char* lds, int wid, int lane) {
+  const char* sbase = reinterpret_cast<const char*>(w + k0);
+#pragma unroll
+  for (int i = 0; i < SaB::PER_WAVE; ++i) {
+    const int piece = wid * SaB::PER_WAVE + i;
+    const int pos = piece * 64 + lane;
+    const int r = pos >> 3, c = (pos & 7) ^ ksw(r);
+    const int gr = h * DH + (r >> 6) * D + (r & 63);
+    glds16(sbase + (uint32_t)(gr * ld + c * 8) * 2u, lds + piece * 1024);
+  }
+}
+
+DEV void sa_project(const SeqQkvArgs& g, const AttnArgs& a, int tok0, int len, int h, char* smem) {
+  constexpr int WN = 4, TM = 64, TN = 48, MI = TM / 16, NI = TN / 16;
+  constexpr int L = SaA::PER_WAVE + SaB::PER_WAVE;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / WN, wc = wid % WN;
+  const int D = a.H * DH, nk = g.K / BKT;
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int t) {
+    char* b = smem + (t % SA_S) * SA_BUF;
+    SaA::stage(g.x, g.K, tok0, t * BKT, g.M, b, wid, lane);
+    sa_stage_b(g.w, g.K, D, h, t * BKT, b + SaA::BYTES, wid, lane);
+  };
+  // live 16-row sub-tiles of this wave's 64 rows (wave-uniform)
+  const int rem = len - wr * TM, live = rem <= 0 ? 0 : min(MI, (rem + 15) >> 4);
+  issue(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_tiles<L, 0>(0);  // tile kt has landed (the ring holds one tile in flight)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 1 < nk) issue(kt + 1);  // into the slot everyone finished reading
+    const char* cur = smem + (kt % SA_S) * SA_BUF;
+    if (live > 0) {  // (the MFMAs of dead sub-tiles are skipped)
+      bf16x8 a0[MI], b0[NI], a1[MI], b1[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a0[i] = SaA::frag(cur, wr * TM + i * 16, 0, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b0[j] = SaB::frag(cur + SaA::BYTES, wc * TN + j * 16, 0, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a1[i] = SaA::frag(cur, wr * TM + i * 16, 1, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b1[j] = SaB::frag(cur + SaA::BYTES, wc * TN + j * 16, 1, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        if (i < live)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b0[j], a0[i], acc[i][j]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        if (i < live)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b1[j], a1[i], acc[i][j]);
+    }
+  }
+  __syncthreads();  // no wave still reads a ring slot (the last wait drained every DMA)
+  // accumulators + bias -> bf16 -> the attention's Q / K / V images (attn_fwd_s128_body MODE 2)
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int c = wc * TN + j * 16 + 4 * (lane >> 4), sec = c >> 6, cc = c & 63;
+    const float4 bv = *reinterpret_cast<const float4*>(g.bias + sec * D + h * DH + cc);
+    char* img = sec == 0 ? smem + ATT_FWD_SMEM : smem + (sec - 1) * 2 * 8192;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int r = wr * TM + i * 16 + (lane & 15);
+      const uint2 v = make_uint2(pack_bf2(acc[i][j][0] + bv.x, acc[i][j][1] + bv.y),
+                                 pack_bf2(acc[i][j][2] + bv.z, acc[i][j][3] + bv.w));
+      *reinterpret_cast<uint2*>(img + (r >> 6) * 8192 + tile_off(r & 63, cc >> 3) + (cc & 7) * 2) = v;
+    }
+  }
+  __syncthreads();
+  // the sequence's projection rows out (the backward reads qkv)
+  bf16_t* qkv = const_cast<bf16_t*>(a.qkv);
+  const int ld3 = 3 * D;
+#pragma unroll 2
+  for (int id = tid; id < 128 * 24; id += 512) {
+    const int r = id / 24, ch = id - r * 24, sec = ch >> 3, c8 = ch & 7;
+    if (r < len) {
+      const char* img = sec == 0 ? smem + ATT_FWD_SMEM : smem + (sec - 1) * 2 * 8192;
+      *reinterpret_cast<uint4*>(qkv + (size_t)(tok0 + r) * ld3 + sec * D + h * DH + c8 * 8) =
+          *reinterpret_cast<const uint4*>(img + (r >> 6) * 8192 + tile_off(r & 63, c8));
+    }
+  }
+}
+
+__global__ __launch_bounds__(512, 2) void seq_attn_fwd_kernel(SeqQkvArgs g, AttnArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[SA_S * SA_BUF];
+  const int nb = a.B + (a.cu ? 1 : 0);
+  // head-major logical order: after the XCD remap one XCD walks ~1.5 heads (their weight slices
+  // stay in its L2) over every sequence
+  const int item = xcd_remap(blockIdx.x, nb * a.H), h = item / nb, b = item - h * nb;
+  if (b < a.B) {
+    int tok0, len;
+    seq_span(a, b, tok0, len);
+    if (len > 0) sa_project(g, a, tok0, len, h, smem);
+  } else {  // filler rows of qkv: finite zeros (the separate GEMM's rows there are never read)
+    zero_filler_at(a, const_cast<bf16_t*>(a.qkv), 3 * a.H * DH, 3, h, 0, 1);
+  }
+  attn_fwd_s128_body<8, 2>(a, b, h, 0, smem);
 }
 
 // LayerNorm-fused NT GEMM (EPI_LN / EPI_LN_BWD): the tiles of a row block are consecutive
@@ -2057,12 +2185,13 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
                      void* ctx, float* lse, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
                      float drop_scale, const int* cu, int rows, uint64_t* dmask, int q_live, void* cxc, void* xc,
                      const void* xres, int Bp, uint64_t* flags, int nflags, const int* cnt, int xsite, int* err,
-                     hipStream_t st) {
+                     int mode, hipStream_t st) {
   const char* pf = g_gemm_pf;  // (an armed prefetch belongs to this call whatever happens below)
   const long long pf_bytes = g_gemm_pf_bytes;
   g_gemm_pf = nullptr;
   g_gemm_pf_bytes = 0;
   const int D = H * DH, N = 3 * D;
+  if (mode != 1 && mode != 2) return 6;
   if (M <= 0 || K % BKT || N % QA_BN || S % 64 || S > 128 || B <= 0 || !bias || !flags || !cnt || !err) return 1;
   if (xsite < 0 || xsite >= FD_LN_XSITES - 1) return 2;
   if ((cu ? rows : B * S) != M || (long long)M * N * 2 >= (1ll << 31)) return 3;
@@ -2085,8 +2214,13 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
-  QkvAttnSync q{flags, cnt, err, xsite, ntiles, tiles_n};
   const int items = H * (B + (cu ? 1 : 0));
+  if (mode == 2) {  // per-(sequence, head) projection + attention (no hand-off, no flags)
+    SeqQkvArgs g{(const bf16_t*)x, (const bf16_t*)w, bias, M, K};
+    hipLaunchKernelGGL(seq_attn_fwd_kernel, dim3(items), dim3(512), 0, st, g, a);
+    return 0;
+  }
+  QkvAttnSync q{flags, cnt, err, xsite, ntiles, tiles_n};
   hipLaunchKernelGGL(gemm_attn_fwd_kernel, dim3(ntiles + items), dim3(64 * QA_NW), 0, st, p, a, q);
   return 0;
 }

@@ -377,8 +377,9 @@ def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: in
 # LayerNorm exchange epoch to advance once per model forward (RunCtx.fuse_ln: emb_fwd does it).
 # Off by default: bitwise equal, but step-neutral (26.0 vs 15.7 + 10.4 us per layer; the one-round
 # GEMM's tiles all finish together, so the attention items cannot start early --
-# profiles/r6_ab_fused_qkv_attention.txt).  FD_FUSE_QKV_ATTN=1: on.
-FUSE_QKV_ATTN = _os.environ.get("FD_FUSE_QKV_ATTN", "0") != "0"
+# profiles/r6_ab_fused_qkv_attention.txt).  FD_FUSE_QKV_ATTN: 0 off, 1 that tile hand-off, 2 one
+# block per (sequence, head) that projects its own Q / K / V into the attention's LDS images.
+FUSE_QKV_ATTN = int(_os.environ.get("FD_FUSE_QKV_ATTN", "0"))
 
 
 def qkv_attn_ok(M: int, D: int, S: int) -> bool:
@@ -389,10 +390,12 @@ def qkv_attn_ok(M: int, D: int, S: int) -> bool:
 
 
 def qkv_attn_fwd(x, w, b, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, cls=None,
-                 xsite: int = 0, prefetch=None):
+                 xsite: int = 0, prefetch=None, mode=None):
     """``linear_fwd(x, w, b)`` then ``attn_fwd(qkv, ...)`` as one launch (``qkv_attn_ok``).  xsite:
     this launch's call site within the current exchange epoch (``ln_xsite``; the fused launches
-    keep their own granules, so a block's LayerNorm site number can be reused).  Returns
+    keep their own granules, so a block's LayerNorm site number can be reused); mode: 1 / 2 (see
+    ``FUSE_QKV_ATTN``; None = that setting, or 1 when it is off).  Mode 2 leaves qkv's filler rows
+    past cu[B] zero (nothing reads them).  Returns
     (qkv, ctx, lse) or, with cls = (x_res, Bp), (qkv, ctx, lse, cxc, xc)."""
     M, D = x.shape[0], H * 64
     qkv = torch.empty(M, 3 * D, dtype=torch.bfloat16, device=x.device)
@@ -407,7 +410,8 @@ def qkv_attn_fwd(x, w, b, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_
         kw = dict(cxc=torch.empty(Bp, D, dtype=torch.bfloat16, device=x.device), xres=xr)
         kw["xc"] = torch.empty_like(kw["cxc"])
     ext().gemm_attn_fwd(x, w, b, qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None,
-                        q_live, stats, cnt, err, int(xsite), prefetch=_pf(prefetch), **kw)
+                        q_live, stats, cnt, err, int(xsite), prefetch=_pf(prefetch),
+                        mode=int(mode if mode is not None else (FUSE_QKV_ATTN or 1)), **kw)
     if cls is None:
         return qkv, ctx, lse
     return qkv, ctx, lse, kw["cxc"], kw["xc"]

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Kernel stats of the timed step with the fused QKV + attention launch on / off
+# Kernel stats of the timed step per FD_FUSE_QKV_ATTN mode (usage: scripts/r6_qa2.sh <modes...>)
 set -o pipefail
-FD_FUSE_QKV_ATTN=1 bash scripts/gpu.sh prof r6qa_prof1 > /dev/null || exit 1
-FD_FUSE_QKV_ATTN=0 bash scripts/gpu.sh prof r6qa_prof0 > /dev/null || exit 1
+for m in ${@:-1 0}; do
+  FD_FUSE_QKV_ATTN=$m bash scripts/gpu.sh prof r6qa_prof$m > /dev/null || exit 1
+done
