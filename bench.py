@@ -357,6 +357,7 @@ def main():
     comm_stats = _fedavg_timing(model, di, fedavg, comm, ncomm, k, sync)
     graphs = len(getattr(step, "graphs", {}))
     graph_ok = step.graph is not None
+    graph_chain = step.graph_count
     graph_err = step.failed
     fused = bool(opt.can_fuse()) and gsync is None
     del step, fn, opt, model, warm, timed, it, loader, gsync, teacher
@@ -411,6 +412,7 @@ def main():
             "spinup_s": args.spinup_seconds,
             "setup_s": round(t_setup, 2),
             "hip_graph": graph_ok,
+            "hip_graph_chain": graph_chain,
             "hip_graphs": graphs,
             "unpadded": bool(rows_frac < 1.0),
             "fused_adam": fused,

@@ -31,6 +31,8 @@ from typing import Callable, Dict, Optional
 
 import torch
 
+from ..ops.graph_split import GRAPH_SPLIT, _Capture, split_point  # noqa: F401
+
 
 class no_gc:
     """Python's cyclic GC paused over a graph capture: a collection that runs mid-capture can free
@@ -91,13 +93,20 @@ class GraphedTrainStep:
         self.bucket = bucket
         self.max_graphs = max_graphs
         self.calls = 0
-        self.graphs: Dict[tuple, tuple] = {}  # key -> (graph, static inputs, static loss)
+        self.graphs: Dict[tuple, tuple] = {}  # key -> (graph chain, static inputs, static loss)
         self.failed: Optional[str] = None
+        self.split = GRAPH_SPLIT
+        self._stream: Optional[torch.cuda.Stream] = None
 
     @property
     def graph(self) -> Optional[torch.cuda.CUDAGraph]:
         """The first captured graph (None until a capture succeeded)."""
-        return next(iter(self.graphs.values()))[0] if self.graphs else None
+        return next(iter(self.graphs.values()))[0][0] if self.graphs else None
+
+    @property
+    def graph_count(self) -> int:
+        """Graphs in the first captured chain (1 without split points)."""
+        return len(next(iter(self.graphs.values()))[0]) if self.graphs else 0
 
     def _key(self, ids, tokens):
         if tokens is None or self.bucket is None:
@@ -116,7 +125,7 @@ class GraphedTrainStep:
         if hit is not None:
             if prepare is not None:
                 prepare()  # eager state the graph does not refresh itself (the model's weight shadow)
-            g, static, loss = hit
+            chain, static, loss = hit
             blk = contiguous_block(ids, mask, labels) if static["flat"] is not None else None
             if blk is not None:
                 static["flat"].copy_(blk)
@@ -124,7 +133,8 @@ class GraphedTrainStep:
                 static["ids"].copy_(ids)
                 static["mask"].copy_(mask)
                 static["labels"].copy_(labels)
-            g.replay()
+            for g in chain:
+                g.replay()
             return loss
         if self.calls <= self.warmup or len(self.graphs) >= self.max_graphs:
             s = torch.cuda.Stream()
@@ -137,17 +147,41 @@ class GraphedTrainStep:
         # every device-side quantity is recomputed from the mask on each replay)
         (s_ids, s_mask, s_lab), flat = static_block(ids, mask, labels)
         static = {"ids": s_ids, "mask": s_mask, "labels": s_lab, "flat": flat}
-        g = torch.cuda.CUDAGraph()
         if prepare is not None:
             prepare()
+        chain = [torch.cuda.CUDAGraph()]
         try:
             torch.cuda.synchronize()
-            with no_gc(), torch.cuda.graph(g):
-                loss = self.step_fn(static["ids"], static["mask"], static["labels"], key[1])
+            with no_gc():
+                if not self.split:
+                    with torch.cuda.graph(chain[0]):
+                        loss = self.step_fn(static["ids"], static["mask"], static["labels"], key[1])
+                else:
+                    loss = self._capture_split(chain, static, key[1])
         except Exception as e:  # pragma: no cover - capture support varies by op
             self.failed = f"{type(e).__name__}: {e}"
             torch.cuda.synchronize()
             return self.step_fn(ids, mask, labels, tokens)
-        self.graphs[key] = (g, static, loss)
-        g.replay()
+        self.graphs[key] = (chain, static, loss)
+        for g in chain:
+            g.replay()
+        return loss
+
+    def _capture_split(self, chain, static, tokens):
+        """torch.cuda.graph's protocol (side capture stream, one memory pool), with the capture
+        cut into a chain at the model's split points (``split_point``)."""
+        if self._stream is None:
+            self._stream = torch.cuda.Stream()
+        cs, pool = self._stream, torch.cuda.graph_pool_handle()
+        torch.cuda.empty_cache()
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):
+            _Capture.active = _Capture(chain, pool, self.split)
+            chain[0].capture_begin(pool=pool)
+            try:
+                loss = self.step_fn(static["ids"], static["mask"], static["labels"], tokens)
+            finally:
+                _Capture.active = None
+                chain[-1].capture_end()
+        torch.cuda.current_stream().wait_stream(cs)
         return loss

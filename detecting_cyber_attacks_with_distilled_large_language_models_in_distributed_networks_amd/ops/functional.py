@@ -19,6 +19,7 @@ from typing import Callable, Optional
 
 import torch
 
+from . import graph_split as _graph
 from . import kernels as K
 
 
@@ -243,6 +244,7 @@ class LayerFn(torch.autograd.Function):
             ctx.acts = (qkv, cx, lse, ao, h, m1, r1, u, None if rc.remat_gelu else g, f, m2, r2)
             ctx.dmask = dmask
         ctx.L, ctx.rc, ctx.sites, ctx.p, ctx.fused_ln = L, rc, (attn_site, ffn_site), (p_a, p_h), fuse_ln
+        _graph.split_point(idx)  # (a graph-chain boundary of a split training-step capture)
         return y
 
     @staticmethod
