@@ -275,9 +275,11 @@ class DDoSClassifier(nn.Module):
         self.defer_dw_reduce = True
         # HIP path: FFN lin1's bias gradient summed in the GELU' dX GEMM epilogue
         self.fuse_colsum = True
-        # HIP path: the backward re-creates the FFN activation gelu(u) in the GELU' dX epilogue
-        # instead of the forward keeping it (FD_REMAT_GELU=0: keep it)
-        self.remat_gelu = os.environ.get("FD_REMAT_GELU", "1") != "0"
+        # HIP path: the forward keeps the FFN activation g = gelu(u) for the backward (FD_REMAT_GELU=1:
+        # the GELU' dX epilogue re-creates it instead -- round 1's win, -1.3 %, is now a loss: the
+        # all-layer dW launch keeps every g live to the end anyway, and the epilogue's 16.5 MB write
+        # per layer costs 11 us per step, profiles/r6_ab_remat_gelu.txt)
+        self.remat_gelu = os.environ.get("FD_REMAT_GELU", "0") != "0"
         # HIP path: LayerNorm fused into the N = 768 GEMMs (RunCtx.fuse_ln; FD_FUSE_LN=0: the
         # separate LN kernels).  Hidden sizes the fused epilogue does not cover fall back.
         # Its row blocks wait on each other's statistics, so every tile of a launch must be resident
