@@ -86,7 +86,7 @@ def static_block(*ts: torch.Tensor):
 
 class GraphedTrainStep:
     def __init__(self, step_fn: Callable[..., torch.Tensor], warmup: int = 2, enabled: bool = True,
-                 bucket: Optional[Callable[[int, int, int], int]] = None, max_graphs: int = 8):
+                 bucket: Optional[Callable[[int, int, int], int]] = None, max_graphs: int = 16):
         self.step_fn = step_fn
         self.warmup = warmup
         self.enabled = enabled and torch.cuda.is_available()

@@ -268,7 +268,10 @@ class DDoSClassifier(nn.Module):
         # tokens only (~37 % of a seq128 CICIDS2017 batch is padding).  Rows are rounded up
         # to `pack_quantum` so a handful of shapes (HIP graphs) cover every batch.
         self.unpad = True
-        self.pack_quantum = 128
+        # (a multiple of 64: the weight-gradient K steps; 64 rather than 128: -4 us per step in 4
+        # interleaved 200-step pairs, profiles/r6_ab_pack_quantum.txt -- fewer padding rows, and the
+        # CICIDS2017 batches still fall in 2-3 buckets)
+        self.pack_quantum = int(os.environ.get("FD_PACK_QUANTUM", "64"))
         # HIP path: finalise all bias / LN-affine column sums of a backward in one launch
         self.defer_colsum = True
         # HIP path: reduce all split-K weight-gradient slabs of a backward in one launch
