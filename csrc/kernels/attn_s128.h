@@ -1,7 +1,8 @@
 // S <= 128 attention pieces shared by attention.hip and the fused QKV + attention forward launch
 // (gemm.hip gemm_attn_fwd_kernel): fragment layouts, AttnArgs, the varlen / [CLS] helpers, the
 // staging loops and the forward body.  Included INSIDE the includer's anonymous namespace (as
-// adam_common.h), after common.h.
+// adam_common.h), after common.h.  Reference math: HF DistilBERT MultiHeadSelfAttention, reached
+// from client1.py:61 (DistilBertForSequenceClassification.from_pretrained) -- see attention.hip.
 #pragma once
 
 constexpr int DH = 64;
