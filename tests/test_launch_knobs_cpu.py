@@ -1,0 +1,43 @@
+"""Host-side rules of this round's launch options (CPU): the fused QKV + attention shape gate
+(ops/kernels.py qkv_attn_ok, mirroring csrc/binding.cpp gemm_attn_fwd), the graph-chain split hook
+(ops/graph_split.py: a no-op outside a split capture), and the packed-row bucketing quantum."""
+import pytest
+
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.models import (
+    DDoSClassifier, DistilBertConfig)
+from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.ops import (
+    graph_split, kernels as K)
+
+
+def test_qkv_attn_gate(monkeypatch):
+    monkeypatch.setattr(K, "FUSE_QKV_ATTN", 0)
+    assert not K.qkv_attn_ok(2688, 768, 128)  # off by default
+    for mode in (1, 2):
+        monkeypatch.setattr(K, "FUSE_QKV_ATTN", mode)
+        assert K.qkv_attn_ok(2688, 768, 128) and K.qkv_attn_ok(512, 768, 64)
+        assert not K.qkv_attn_ok(2688, 768, 256)  # S <= 128 kernels only
+        assert not K.qkv_attn_ok(2688, 760, 128)  # head dim 64
+        # the hand-off granules: <= QA_FLAGS tiles of 128 x 192
+        rows_max = K.QA_FLAGS // (3 * 768 // 192) * 128
+        assert K.qkv_attn_ok(rows_max, 768, 128) and not K.qkv_attn_ok(rows_max + 1, 768, 128)
+    monkeypatch.setattr(K, "_SHARED_DEVICE", True)  # ranks sharing a GPU: never (no epoch advance)
+    assert not K.qkv_attn_ok(2688, 768, 128)
+
+
+def test_split_point_is_a_noop_outside_a_capture():
+    assert graph_split._Capture.active is None
+    for b in range(6):
+        graph_split.split_point(b)  # nothing to end / begin
+    assert graph_split._Capture.active is None
+
+
+@pytest.mark.parametrize("q", [64, 128])
+def test_packed_rows_quantum(q):
+    m = DDoSClassifier(config=DistilBertConfig(n_layers=1))
+    assert m.pack_quantum == 64  # default (profiles/r6_ab_pack_quantum.txt)
+    m.pack_quantum = q
+    for tokens in (1, 63, 64, 65, 2561, 2688, 4096):
+        r = m.packed_rows(tokens, 32, 128)
+        assert r % q == 0 or r == 32 * 128
+        assert tokens <= r < tokens + q or r == 32 * 128
+        assert r <= 32 * 128
