@@ -33,6 +33,7 @@
 #include "adam_epi.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace {
 
@@ -2412,7 +2413,18 @@ bool plan_dwb_mix(DwBatch& bt, int mode) {
   // FD_DWB_SHORT_FIRST=1 (A/B), the short tiles (a one-step K loop + a full Adam epilogue: HBM-bound)
   // first, beside the first round's operand-bound K loops
   static const int short_first = [] { const char* e = getenv("FD_DWB_SHORT_FIRST"); return e ? atoi(e) : 1; }();
-  const int order[3] = {short_first ? 2 : 0, short_first ? 0 : 1, short_first ? 1 : 2};
+  int order[3] = {short_first ? 2 : 0, short_first ? 0 : 1, short_first ? 1 : 2};
+  // FD_DWB_CLASS_ORDER=<3 digits> (A/B): any dispatch order of the classes 0 long, 1 half, 2 short
+  static const char* class_order = getenv("FD_DWB_CLASS_ORDER");
+  if (class_order && strlen(class_order) == 3) {
+    int o[3], seen = 0;
+    for (int q = 0; q < 3; ++q) {
+      o[q] = class_order[q] - '0';
+      if (o[q] >= 0 && o[q] < 3) seen |= 1 << o[q];
+    }
+    if (seen == 7)
+      for (int q = 0; q < 3; ++q) order[q] = o[q];
+  }
   DwProb pr[DWB_MAXP];
   int k = 0, off = 0;
   for (int q = 0; q < 3; ++q) {
