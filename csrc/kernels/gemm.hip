@@ -1447,6 +1447,22 @@ using SaB = Operand<192, true, 8>;
 constexpr int SA_S = 2, SA_BUF = SaA::BYTES + SaB::BYTES;
 static_assert(SA_S * SA_BUF >= ATT_FWD_SMEM_Q, "the attention images fit the projection ring");
 
+// The sequence's A rows only: the 1 KiB DMA pieces (8 rows each) of rows past the live 16-row
+// sub-tiles are skipped (their accumulators stay 0; the ring waits vmcnt(0), so no count to keep)
+DEV void sa_stage_a(const bf16_t* x, int ld, int row0, int k0, int lim, int rows_live, char* lds, int wid,
+                    int lane) {
+  const char* sbase = reinterpret_cast<const char*>(x + k0);
+#pragma unroll
+  for (int i = 0; i < SaA::PER_WAVE; ++i) {
+    const int piece = wid * SaA::PER_WAVE + i;
+    if (piece * 8 >= rows_live) continue;  // (wave-uniform)
+    const int pos = piece * 64 + lane;
+    const int r = pos >> 3, c = (pos & 7) ^ ksw(r);
+    const int gr = min(row0 + r, lim - 1);
+    glds16(sbase + (uint32_t)(gr * ld + c * 8) * 2u, lds + piece * 1024);
+  }
+}
+
 // head h's Q, K, V weight rows as one 192-row K-major B tile (Operand::stage with a row map)
 DEV void sa_stage_b(const bf16_t* w, int ld, int D, int h, int k0, char* lds, int wid, int lane) {
   const char* sbase = reinterpret_cast<const char*>(w + k0);
@@ -1472,13 +1488,14 @@ DEV void sa_project(const SeqQkvArgs& g, const AttnArgs& a, int tok0, int len, i
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // live 16-row sub-tiles of this wave's 64 rows (wave-uniform), and the tile's live rows
+  const int rem = len - wr * TM, live = rem <= 0 ? 0 : min(MI, (rem + 15) >> 4);
+  const int rows_live = min(128, (len + 15) & ~15);
   auto issue = [&](int t) {
     char* b = smem + (t % SA_S) * SA_BUF;
-    SaA::stage(g.x, g.K, tok0, t * BKT, g.M, b, wid, lane);
+    sa_stage_a(g.x, g.K, tok0, t * BKT, g.M, rows_live, b, wid, lane);
     sa_stage_b(g.w, g.K, D, h, t * BKT, b + SaA::BYTES, wid, lane);
   };
-  // live 16-row sub-tiles of this wave's 64 rows (wave-uniform)
-  const int rem = len - wr * TM, live = rem <= 0 ? 0 : min(MI, (rem + 15) >> 4);
   issue(0);
   for (int kt = 0; kt < nk; ++kt) {
     wait_tiles<L, 0>(0);  // tile kt has landed (the ring holds one tile in flight)

@@ -372,14 +372,16 @@ def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: in
     return ctx, lse, cxc, xc
 
 
-# QKV projection + S <= 128 attention forward in ONE launch (csrc/kernels/gemm.hip gemm_attn_fwd_kernel):
-# the attention items start on the tiles they need instead of after a launch boundary.  Needs the
-# LayerNorm exchange epoch to advance once per model forward (RunCtx.fuse_ln: emb_fwd does it).
-# Off by default: bitwise equal, but step-neutral (26.0 vs 15.7 + 10.4 us per layer; the one-round
-# GEMM's tiles all finish together, so the attention items cannot start early --
-# profiles/r6_ab_fused_qkv_attention.txt).  FD_FUSE_QKV_ATTN: 0 off, 1 that tile hand-off, 2 one
-# block per (sequence, head) that projects its own Q / K / V into the attention's LDS images.
-FUSE_QKV_ATTN = int(_os.environ.get("FD_FUSE_QKV_ATTN", "0"))
+# QKV projection + S <= 128 attention forward in ONE launch (csrc/kernels/gemm.hip).  FD_FUSE_QKV_ATTN:
+#   0: the two launches;
+#   1: gemm_attn_fwd_kernel -- the QKV tiles hand off to the attention items (write-through stores +
+#      tagged granules; needs the LayerNorm exchange epoch to advance per forward, RunCtx.fuse_ln):
+#      step-neutral, the one-round GEMM's tiles all finish together;
+#   2 (default): seq_attn_fwd_kernel -- one block per (sequence, head) projects its own Q / K / V
+#      rows (live rows only) straight into the attention's LDS images: 25.3 vs 25.8 us per layer,
+#      -2.4 us per step over 6 interleaved 200-step pairs (profiles/r6_ab_fused_qkv_attention.txt).
+# Both bitwise the two launches (tests/test_qkv_attn_gpu.py).
+FUSE_QKV_ATTN = int(_os.environ.get("FD_FUSE_QKV_ATTN", "2"))
 
 
 def qkv_attn_ok(M: int, D: int, S: int) -> bool:

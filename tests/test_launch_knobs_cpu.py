@@ -11,7 +11,7 @@ from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed
 
 def test_qkv_attn_gate(monkeypatch):
     monkeypatch.setattr(K, "FUSE_QKV_ATTN", 0)
-    assert not K.qkv_attn_ok(2688, 768, 128)  # off by default
+    assert not K.qkv_attn_ok(2688, 768, 128)  # off
     for mode in (1, 2):
         monkeypatch.setattr(K, "FUSE_QKV_ATTN", mode)
         assert K.qkv_attn_ok(2688, 768, 128) and K.qkv_attn_ok(512, 768, 64)
