@@ -71,6 +71,10 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
                      float drop_scale, const int* cu, int rows, uint64_t* dmask, int q_live, void* cxc, void* xc,
                      const void* xres, int Bp, uint64_t* flags, int nflags, const int* cnt, int xsite, int* err,
                      int mode, hipStream_t st);
+int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dy,
+                     const void* w, int M, int K, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr,
+                     uint32_t site, uint32_t thr, float drop_scale, const int* cu, int rows, const uint64_t* dmask,
+                     hipStream_t st);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
                 int rows, uint64_t* dmask, int q_live, void* cxc, void* xc, const void* xres, int Bp,
@@ -995,6 +999,39 @@ void gemm_attn_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
            "gemm_attn_fwd");
 }
 
+// The S <= 128 attention backward that computes its own dO: dctx = dy w (the out-projection's dX:
+// dy [rows, K], w [K, H 64] the weight itself) per (sequence, head), inside the launch
+// (gemm.hip attn_bwd_proj_kernel).  Full-query backward only.
+void attn_bwd_proj(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
+                   const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dqkv, int64_t B, int64_t S, int64_t H,
+                   const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
+                   const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask) {
+  check_dmask(dmask, B, S, H);
+  need(qkv, at::kBFloat16, "qkv");
+  need(kbias, at::kFloat, "kbias");
+  need(ctx, at::kBFloat16, "ctx");
+  need(lse, at::kFloat, "lse");
+  need(dy, at::kBFloat16, "dy");
+  need(w, at::kBFloat16, "w");
+  need(dqkv, at::kBFloat16, "dqkv");
+  TORCH_CHECK(S % 64 == 0 && S <= 128 && B > 0 && H > 0, "attn_bwd_proj: S must be 64 or 128");
+  const int64_t D = H * 64;
+  const bool varlen = cu.has_value() && cu->defined();
+  const int64_t rows = varlen ? qkv.numel() / (3 * D) : B * S;
+  TORCH_CHECK(qkv.numel() == rows * 3 * D && dqkv.numel() == qkv.numel() && ctx.numel() == rows * D,
+              "attn_bwd_proj: qkv / dqkv / ctx size");
+  TORCH_CHECK(dy.dim() == 2 && dy.size(0) == rows && w.dim() == 2 && w.size(0) == dy.size(1) && w.size(1) == D,
+              "attn_bwd_proj: dy [rows, K] and w [K, H 64] required");
+  TORCH_CHECK(dy.size(1) % 64 == 0, "attn_bwd_proj: K must be a multiple of 64");
+  TORCH_CHECK(lse.numel() == B * H * S && (varlen || kbias.numel() == B * S), "attn_bwd_proj: stats");
+  check_cu(cu, B, rows, rows);
+  check_rc(fd_attn_bwd_proj(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(),
+                            dy.data_ptr(), w.data_ptr(), (int)rows, (int)dy.size(1), dqkv.data_ptr(), (int)B, (int)S,
+                            (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), (int)rows,
+                            ptr<uint64_t>(dmask), stream()),
+           "attn_bwd_proj");
+}
+
 void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
               const at::Tensor& dctx, const at::Tensor& delta, const at::Tensor& dqkv, int64_t B, int64_t S, int64_t H,
               const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& cu,
@@ -1607,6 +1644,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("delta"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"),
         py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("q_live") = 0,
         py::arg("dresc") = py::none(), py::arg("dres") = py::none());
+  m.def("attn_bwd_proj", &attn_bwd_proj, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"),
+        py::arg("dy"), py::arg("w"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"),
+        py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"));
   m.def("mask_to_bias", &mask_to_bias);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);

@@ -319,6 +319,23 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
   else hc::span(kbias, (long long)B * S * 4, "gemm_attn kbias");
   return 0;
 }
+int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dy,
+                     const void* w, int M, int K, void* dqkv, int B, int S, int H, const uint32_t* seed, uint32_t,
+                     uint32_t, float, const int* cu, int rows, const uint64_t* dmask, hipStream_t) {
+  ++hc::calls;
+  const long long D = (long long)H * 64;
+  hc::opt_span(dmask, (long long)B * H * 256 * 8, "attn bwd proj dmask");
+  hc::span(qkv, rows * 3 * D * 2, "attn bwd proj qkv");
+  hc::span(dqkv, rows * 3 * D * 2, "attn bwd proj dqkv");
+  hc::span(ctx, rows * D * 2, "attn bwd proj ctx");
+  hc::span(dy, (long long)M * K * 2, "attn bwd proj dy");
+  hc::span(w, (long long)K * D * 2, "attn bwd proj w");
+  hc::span(lse, (long long)B * H * S * 4, "attn bwd proj lse");
+  hc::span(seed, 4, "attn bwd proj seed");
+  if (cu) hc::span(cu, (long long)(B + 1) * 4, "attn bwd proj cu");
+  else hc::span(kbias, (long long)B * S * 4, "attn bwd proj kbias");
+  return 0;
+}
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx, float* delta,
                 void* dqkv, int B, int S, int H, const uint32_t* seed, uint32_t, uint32_t, float, const int* cu,
                 int rows, const uint64_t* dmask, int, const void* dresc, void* dres, hipStream_t) {
@@ -775,6 +792,14 @@ int main() {
                                                         1); });
     expect_reject("qkv attn xsite", [&] { gemm_attn_fwd(x, w, bq, qkv, kb, ctx, lse, B, S, H, seed, 16, 0, 1.0, none,
                                                         none, 0, stats, cnt, err, 127, none, none, none, none, 1); });
+    expect_ok("attn bwd proj", [&] { attn_bwd_proj(qkv, kb, ctx, lse, x, T_({H * 64, H * 64}, bf), dqkv, B, S, H, seed, 16,
+                                                  429496730, 1.1, none, dm); });
+    expect_ok("attn bwd proj varlen", [&] { attn_bwd_proj(qv, kb, cv, lse, T_({300, H * 64}, bf), T_({H * 64, H * 64}, bf),
+                                                         T_({300, 3 * H * 64}, bf), B, S, H, seed, 16, 0, 1.0, cu, none); });
+    expect_reject("attn bwd proj S=256", [&] { attn_bwd_proj(qkv, kb, ctx, lse, x, T_({H * 64, H * 64}, bf), dqkv, 2, 256,
+                                                            H, seed, 16, 0, 1.0, none, none); });
+    expect_reject("attn bwd proj w shape", [&] { attn_bwd_proj(qkv, kb, ctx, lse, x, T_({H * 64, 64}, bf), dqkv, B, S, H,
+                                                              seed, 16, 0, 1.0, none, none); });
     expect_reject("qkv attn mode", [&] { gemm_attn_fwd(x, w, bq, qkv, kb, ctx, lse, B, S, H, seed, 16, 0, 1.0, none,
                                                        none, 0, stats, cnt, err, 2, none, none, none, none, 3); });
   }

@@ -376,335 +376,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_s128_kernel(AttnArgs a) {
   attn_fwd_s128_body<NW, 0>(a, blockIdx.z, blockIdx.y, blockIdx.x, smem);
 }
 
-// ---- S <= 128 backward phases (shared by the fused one-block kernel and the two-block split)
-// Scores and biases in log2 units: P = exp2(s * scale * log2e + bias2 - lse2).
-
-// Phase 1 for this wave's 16 query rows (lane row q, read row qr = min(q, len - 1)): dQ from the
-// K / V images in LDS, the rows' Q / dO fragments, delta dl, lse2 and the forward's keep-bit words
-// (mrow_p[kt * 16] = this lane's u16 of key tile kt; null without stored keep bits).
-DEV void bwd_dq_rows(const AttnArgs& a, const char* ks, const char* vs, const float* kb, uint64_t vk0,
-                     uint64_t vk1, const bf16x8 (&qf)[2], const bf16x8 (&dof)[2], float dl, float lse,
-                     const uint16_t* mrow_p, int b, int h, int q, int len, int nt, size_t tok0, int lane) {
-  const int g = lane >> 4, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
-  const bool drop = a.drop_threshold != 0, varlen = a.cu != nullptr;
-  const uint32_t seed = site_seed(a);
-  const float scale2 = a.scale * LOG2E;
-  const uint32_t rowidx = ((uint32_t)(b * H + h) * S + q) * (uint32_t)S;
-  f32x4 dq[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
-    const uint64_t vk = kt ? vk1 : vk0;
-    if (kt >= nt || vk == 0) continue;  // fully masked key tile: dS = 0
-    bool tv[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) tv[t] = ((vk >> (16 * t)) & 0xffffull) != 0;
-    const char* kst = ks + kt * 8192;
-    const char* vst = vs + kt * 8192;
-    const uint32_t mrow = (drop && mrow_p) ? mrow_p[kt * 16] : 0u;  // this lane's keys 16 t + 4 g + r
-    f32x4 sc[4], dp[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (!tv[t]) continue;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        sc[t] = mfma16(row_frag(kst, 16 * t, s2, lane), qf[s2], sc[t]);
-        dp[t] = mfma16(row_frag(vst, 16 * t, s2, lane), dof[s2], dp[t]);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (!tv[t]) continue;  // sc[t] = 0 = dS of a fully masked sub-tile
-      const uint32_t kw = !drop   ? 0xfu
-                          : mrow_p ? (mrow >> (4 * t)) & 0xfu
-                                   : drop_keep_bits<4>(seed, rowidx + kt * 64 + 16 * t + 4 * g, a.drop_threshold);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kl = 16 * t + 4 * g + r;
-        const float bias = varlen ? (kt * 64 + kl < len ? 0.f : -INFINITY) : kb[kt * 64 + kl];
-        const float pv = __builtin_amdgcn_exp2f(sc[t][r] * scale2 + bias - lse);
-        float dpv = dp[t][r];
-        if (drop) dpv = (kw >> r) & 1u ? dpv * a.drop_scale : 0.f;
-        sc[t][r] = pv * (dpv - dl);  // dS
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      if (!(tv[2 * kk] || tv[2 * kk + 1])) continue;
-      const bf16x8 df = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(tr_frag(kst, 16 * dt, kk, lane), df, dq[dt]);
-    }
-  }
-  if (q < len) {
-    const float sc_out = a.scale;
-    bf16_t* out = a.dqkv + (tok0 + q) * ld3 + h * DH;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-      *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) = make_uint2(
-          pack_bf2(dq[dt][0] * sc_out, dq[dt][1] * sc_out), pack_bf2(dq[dt][2] * sc_out, dq[dt][3] * sc_out));
-  }
-}
-
-// Phase 2 for this wave's 16 keys key0 .. key0 + 15: dK and dV from the Q / dO images in LDS, the
-// keys' K / V fragments, lse2 / delta of every query row (LDS) and the keep bits (LDS, mk16).
-DEV void bwd_dkv_keys(const AttnArgs& a, const char* qs, const char* os, const float* lse_s, const float* dl_s,
-                      const uint16_t* mk16, bool keys_live, const bf16x8 (&kf)[2], const bf16x8 (&vf)[2],
-                      float kbias, int b, int h, int key, int len, int nt, int qlen, size_t tok0, int lane) {
-  const int g = lane >> 4, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
-  const bool drop = a.drop_threshold != 0;
-  const uint32_t seed = site_seed(a);
-  const float scale2 = a.scale * LOG2E;
-  const uint32_t headidx = (uint32_t)(b * H + h) * S;
-  // this lane's key in the forward's lane-major keep bits: word kt * 4 + g', bit 4 t' + r'
-  const int kword = (key >> 6) * 4 + ((key >> 2) & 3), kbit = 4 * ((key >> 4) & 3) + (key & 3);
-  f32x4 dk[4], dv[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    dk[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    if (!keys_live || qt >= nt) continue;
-    const char* qst = qs + qt * 8192;
-    const char* ost = os + qt * 8192;
-    // 16-query sub-tiles past the sequence (varlen) have lse = +inf: P = dS = 0, skipped
-    bool tv[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) tv[t] = qt * 64 + 16 * t < qlen;
-    f32x4 sc[4], dp[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (!tv[t]) continue;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        sc[t] = mfma16(row_frag(qst, 16 * t, s2, lane), kf[s2], sc[t]);  // S[q][key]
-        dp[t] = mfma16(row_frag(ost, 16 * t, s2, lane), vf[s2], dp[t]);  // dP[q][key]
-      }
-    }
-    // one 32-query half at a time: P / dS of tiles 2kk, 2kk+1 are packed to bf16 right away
-    // (keeps the live set small -> several blocks per CU)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      if (!(tv[2 * kk] || tv[2 * kk + 1])) continue;
-      f32x4 pd[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int t = 2 * kk + u;
-        if (!tv[t]) {
-          pd[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-          continue;  // sc[t] = 0 already
-        }
-        // the 4 query rows of this lane: one 16-byte LDS read each for their lse and delta
-        const float4 lse4 = *reinterpret_cast<const float4*>(lse_s + qt * 64 + 16 * t + 4 * g);
-        const float4 dl4 = *reinterpret_cast<const float4*>(dl_s + qt * 64 + 16 * t + 4 * g);
-        const float lsev[4] = {lse4.x, lse4.y, lse4.z, lse4.w}, dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
-        // the key's words of the 4 query rows: one 8-byte LDS read
-        const uint64_t kq = (drop && mk16)
-            ? *reinterpret_cast<const uint64_t*>(mk16 + (((qt * 16 + 4 * t + g) * 8 + kword) << 2)) : 0ull;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ql = qt * 64 + 16 * t + 4 * g + r;
-          const float pv = __builtin_amdgcn_exp2f(sc[t][r] * scale2 + kbias - lsev[r]);
-          float dpv = dp[t][r], pdv = pv;
-          if (drop) {
-            const bool keep = mk16 ? ((kq >> (16 * r + kbit)) & 1ull) != 0
-                                   : drop_keep(seed, (headidx + ql) * (uint32_t)S + key, a.drop_threshold);
-            dpv = keep ? dpv * a.drop_scale : 0.f;
-            pdv = keep ? pv : 0.f;  // (the dropout scale is applied to dV once, at the store)
-          }
-          pd[u][r] = pdv;
-          sc[t][r] = pv * (dpv - dlv[r]);  // dS
-        }
-      }
-      const bf16x8 pf = pack_acc(pd[0], pd[1]);
-      const bf16x8 sf = pack_acc(sc[2 * kk], sc[2 * kk + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        dv[dt] = mfma16(tr_frag(ost, 16 * dt, kk, lane), pf, dv[dt]);
-        dk[dt] = mfma16(tr_frag(qst, 16 * dt, kk, lane), sf, dk[dt]);
-      }
-    }
-  }
-  if (key >= len) return;
-  const float sc_out = a.scale, dv_sc = drop ? a.drop_scale : 1.f;
-  bf16_t* outk = a.dqkv + (tok0 + key) * ld3 + D + h * DH;
-  bf16_t* outv = a.dqkv + (tok0 + key) * ld3 + 2 * D + h * DH;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    *reinterpret_cast<uint2*>(outk + 16 * dt + 4 * g) = make_uint2(
-        pack_bf2(dk[dt][0] * sc_out, dk[dt][1] * sc_out), pack_bf2(dk[dt][2] * sc_out, dk[dt][3] * sc_out));
-    *reinterpret_cast<uint2*>(outv + 16 * dt + 4 * g) = make_uint2(
-        pack_bf2(dv[dt][0] * dv_sc, dv[dt][1] * dv_sc), pack_bf2(dv[dt][2] * dv_sc, dv[dt][3] * dv_sc));
-  }
-}
-
-// delta = rowsum(dO * O) of the lane's row from its two 32-wide fragment halves (16 lanes per row)
-DEV float row_delta(const bf16x8 (&of)[2], const bf16x8 (&dof)[2]) {
-  float dl = 0.f;
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)of[s2][j]) * bf2f((uint16_t)dof[s2][j]);
-  dl += __shfl_xor(dl, 16, 64);
-  dl += __shfl_xor(dl, 32, 64);
-  return dl;
-}
-
-// dO tiles of a compact-[CLS] backward (AttnArgs::dresc): row 0 = the sequence's compact row,
-// every other row 0 (what stage_rows reads from the scattered layout, clamp included)
-template <int NT = 512>
-DEV void stage_cls_rows(char* lds, const bf16_t* src, int tid, int nt, int len) {
-#pragma unroll
-  for (int i = 0; i < 1024 / NT; ++i) {
-    const int id = i * NT + tid;
-    const int r = id >> 3, c = id & 7;
-    if (r < 64 * nt) {
-      const uint4 v = min(r, len - 1) == 0 ? *reinterpret_cast<const uint4*>(src + c * 8) : make_uint4(0u, 0u, 0u, 0u);
-      *reinterpret_cast<uint4*>(lds + (r >> 6) * 8192 + tile_off(r & 63, c)) = v;
-    }
-  }
-}
-
-// Head h's columns of the sequence's rows of dres: row 0 = dresc[b], the others 0.
-template <int NT = 512>
-DEV void scatter_cls_rows(const AttnArgs& a, int b, size_t tok0, int len, int h, int tid) {
-  const int D = a.H * DH;
-  for (int id = tid; id < len * 8; id += NT) {
-    const int r = id >> 3, c = id & 7;
-    const uint4 v = r == 0 ? *reinterpret_cast<const uint4*>(a.dresc + (size_t)b * D + h * DH + c * 8)
-                           : make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint4*>(a.dres + (tok0 + r) * D + h * DH + c * 8) = v;
-  }
-}
-
-// Zero dQ of rows without a gradient (q_live: not among the query rows the loss reaches).
-DEV void zero_dq_rows(const AttnArgs& a, int h, int q, int len, size_t tok0, int g) {
-  if (q >= len) return;
-  bf16_t* out = a.dqkv + (tok0 + q) * (3 * a.H * DH) + h * DH;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) *reinterpret_cast<uint2*>(out + 16 * dt + 4 * g) = make_uint2(0u, 0u);
-}
-
-// One block per (sequence, head): phase 1 (waves own 16 query rows: delta, dQ), a barrier, phase 2
-// (waves own 16 keys: dK, dV) from the same four LDS images.  (A dQ block beside a dK/dV block per
-// (sequence, head) lost its A/B: 23.8 vs 19.3 us per layer, profiles/r4_rejected_ab.txt.)
 __global__ __launch_bounds__(512) void attn_bwd_s128_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[8 * 8192 + 3 * 512 + 2048];
-  char* qs = smem;
-  char* ks = smem + 2 * 8192;
-  char* vs = smem + 4 * 8192;
-  char* os = smem + 6 * 8192;  // dO
-  float* kb = reinterpret_cast<float*>(smem + 8 * 8192);
-  float* lse_s = kb + 128;
-  float* dl_s = lse_s + 128;
-  uint64_t* mk_s = reinterpret_cast<uint64_t*>(smem + 8 * 8192 + 3 * 512);  // the forward's keep bits
-  const uint16_t* mk16 = reinterpret_cast<const uint16_t*>(mk_s);  // [q / 4][kt * 4 + g][q % 4], bit 4 t + r
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
-  const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
-  ASTAMP(0);
-  astamp_hwid();
-  if (b == a.B) {
-    zero_filler(a, a.dqkv, ld3, 3, h);
-    if (a.dres) {
-      zero_filler(a, a.dres, D, 1, h);
-      const int tok = a.cu[a.B];  // trailing empty sequences: the last one's gradient on row cu[B]
-      if (a.B > 0 && a.cu[a.B - 1] == tok && tok < a.rows) {
-        __syncthreads();
-        if (tid < 8)
-          *reinterpret_cast<uint4*>(a.dres + (size_t)tok * D + h * DH + tid * 8) =
-              *reinterpret_cast<const uint4*>(a.dresc + (size_t)(a.B - 1) * D + h * DH + tid * 8);
-      }
-    }
-    return;
-  }
-  int tok0i, len;
-  seq_span(a, b, tok0i, len);
-  const int nt = (len + 63) >> 6;
-  const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows with a gradient
-  // an empty sequence (varlen) owns no rows: nothing to write, and its clamped row len - 1 = -1
-  // must not be read (a leading empty sequence would read before the tensors)
-  if (len == 0) return;
-  const size_t tok0 = (size_t)tok0i;
-  const size_t st0 = ((size_t)b * H + h) * S;
-  // phase 1's O rows (for delta) are fetched together with the staging loads: no second
-  // dependent global round trip after the barrier
-  const int q0 = w * 16;
-  bf16x8 of[2];
-  {
-    const int qr = min(q0 + (lane & 15), len - 1);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) of[s2] = load_frag_global(a.ctx + (tok0 + qr) * D + h * DH + 32 * s2 + 8 * g);
-  }
-  stage_rows(qs, a.qkv + tok0 * ld3 + h * DH, ld3, tid, nt, len);
-  stage_rows(ks, a.qkv + tok0 * ld3 + D + h * DH, ld3, tid, nt, len);
-  stage_rows(vs, a.qkv + tok0 * ld3 + 2 * D + h * DH, ld3, tid, nt, len);
-  if (a.dres)
-    stage_cls_rows(os, a.dctx + (size_t)b * D + h * DH, tid, nt, len);
-  else
-    stage_rows(os, a.dctx + tok0 * D + h * DH, D, tid, nt, len);
-  if (tid < 128) {
-    kb[tid] = tid < 64 * nt ? key_bias(a, tok0i, len, tid) * LOG2E : -INFINITY;
-    // query rows past the sequence: lse = +inf makes their P (and dS) exactly 0
-    lse_s[tid] = tid < qlen ? a.lse[st0 + tid] * LOG2E : INFINITY;
-    dl_s[tid] = 0.f;
-  }
-  // the forward's keep bits (rows the forward did not write are past the sequence: P = 0 there)
-  const bool mk = a.drop_threshold != 0 && a.dmask != nullptr;
-  if (mk && tid < 256) mk_s[tid] = a.dmask[((size_t)b * H + h) * 256 + tid];
-  // (after the staging loads are issued: wave 0's [CLS] row store waits for its load)
-  if (a.dres) scatter_cls_rows(a, b, tok0, len, h, tid);
-  __syncthreads();
-  ASTAMP(1);
-  // unmasked-key bits of the two 64-key tiles (see attn_fwd_s128_kernel): 16-key sub-tiles
-  // with every key masked have P = dS = 0 exactly and are skipped in both phases
-  const uint64_t vk0 = __ballot(kb[lane] != -INFINITY);
-  const uint64_t vk1 = __ballot(kb[64 + lane] != -INFINITY);
-
-  // ---- phase 1: dQ and delta; wave w owns queries 16w .. 16w+15
-  if (q0 >= qlen && q0 < len) zero_dq_rows(a, h, q0 + (lane & 15), len, tok0, g);
-  if (q0 < qlen) {
-    const int q = q0 + (lane & 15);
-    const int qr = min(q, len - 1);
-    bf16x8 qf[2], dof[2];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      qf[s2] = row_frag(qs + (q0 >> 6) * 8192, q0 & 63, s2, lane);
-      dof[s2] = row_frag(os + (q0 >> 6) * 8192, q0 & 63, s2, lane);
-    }
-    float dl = row_delta(of, dof);
-    if (q >= qlen) dl = 0.f;  // (q_live: this row's O was never written -- it has no gradient)
-    if (g == 0 && q < len) dl_s[q] = dl;
-    const uint16_t* mrow_p = mk ? mk16 + ((qr >> 2) * 8 + g) * 4 + (qr & 3) : nullptr;
-    bwd_dq_rows(a, ks, vs, kb, vk0, vk1, qf, dof, dl, lse_s[qr], mrow_p, b, h, q, len,
-                nt, tok0, lane);
-  }
-  ASTAMP(2);
-  __syncthreads();  // delta of every query row is in LDS
-  ASTAMP(3);
-
-  // ---- phase 2: dK and dV; wave w owns keys 16w .. 16w+15
-  const int key0 = w * 16;
-  if (key0 >= len) return;
-  bf16x8 kf[2], vf[2];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    kf[s2] = row_frag(ks + (key0 >> 6) * 8192, key0 & 63, s2, lane);
-    vf[s2] = row_frag(vs + (key0 >> 6) * 8192, key0 & 63, s2, lane);
-  }
-  // this wave's 16 keys all masked (padded layout): P and dS columns are 0, dK = dV = 0
-  const bool keys_live = (((key0 < 64 ? vk0 >> key0 : vk1 >> (key0 - 64))) & 0xffffull) != 0;
-  const int key = key0 + (lane & 15);
-  bwd_dkv_keys(a, qs, os, lse_s, dl_s, mk ? mk16 : nullptr, keys_live, kf, vf, kb[key], b, h, key, len, nt, qlen,
-               tok0, lane);
-  ASTAMP(4);
+  __shared__ __attribute__((aligned(16))) char smem[ATT_BWD_SMEM];
+  attn_bwd_s128_body<0>(a, blockIdx.z, blockIdx.y, smem, NoProj{});
 }
 
 bool use_s128(int S) {

@@ -1571,6 +1571,102 @@ __global__ __launch_bounds__(512, 2) void seq_attn_fwd_kernel(SeqQkvArgs g, Attn
   attn_fwd_s128_body<8, 2>(a, b, h, 0, smem);
 }
 
+// ---------------------------------------------------------------- out-projection dX + attention backward
+// The attention backward of a (sequence, head) computes its own dO -- that head's 64 columns of the
+// out-projection's input gradient dctx = dy W (dy = the out-projection's output gradient [T][D],
+// W = its weight [D][D] as the MN-major B operand, exactly linear_dx's NN GEMM) -- for the sequence's
+// rows, straight into the backward's swizzled dO image: no dctx round trip through HBM and no launch
+// of its own.  The Q / K / V loads of the backward are in flight across the K loop, whose 2-slot ring
+// borrows the Q / K / V image region.  Same per-element MFMA chain as the cfg-24 NN GEMM (128 x 64,
+// 4 x 2 waves), so dO -- and with it every gradient -- is bitwise the two-launch path's.  Rows past
+// the sequence's live 16-row sub-tiles are neither loaded nor multiplied (dO 0 there: rows whose
+// probabilities are exactly 0).
+struct OProjArgs {
+  const bf16_t* dy;  // [M][K]
+  const bf16_t* w;   // [K][D]: W itself (MN-major B)
+  int M, K;
+};
+using OpA = Operand<128, true, 8>;
+using OpB = Operand<64, false, 8>;
+constexpr int OP_BUF = OpA::BYTES + OpB::BYTES;
+static_assert(2 * OP_BUF <= 6 * 8192, "the projection ring fits the Q / K / V image region");
+
+DEV void op_project(const OProjArgs& pj, const AttnArgs& a, int tok0, int len, int h, char* smem) {
+  constexpr int WN = 2, TM = 32, TN = 32, MI = TM / 16, NI = TN / 16;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / WN, wc = wid % WN;
+  const int D = a.H * DH, nk = pj.K / BKT;
+  const int rem = len - wr * TM, live = rem <= 0 ? 0 : min(MI, (rem + 15) >> 4);
+  const int rows_live = min(128, (len + 15) & ~15);
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int t) {
+    char* sl = smem + (t & 1) * OP_BUF;
+    const char* abase = reinterpret_cast<const char*>(pj.dy + t * BKT);
+#pragma unroll
+    for (int i = 0; i < OpA::PER_WAVE; ++i) {  // the sequence's live A rows only (8 rows per piece)
+      const int piece = wid * OpA::PER_WAVE + i;
+      if (piece * 8 >= rows_live) continue;
+      const int pos = piece * 64 + lane;
+      const int r = pos >> 3, c = (pos & 7) ^ ksw(r);
+      glds16(abase + (uint32_t)(min(tok0 + r, pj.M - 1) * pj.K + c * 8) * 2u, sl + piece * 1024);
+    }
+    OpB::stage(pj.w, D, h * DH, t * BKT, D, sl + OpA::BYTES, wid, lane);
+  };
+  issue(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt landed (one tile in flight)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 1 < nk) issue(kt + 1);
+    const char* cur = smem + (kt & 1) * OP_BUF;
+    if (live > 0) {
+      bf16x8 a0[MI], b0[NI], a1[MI], b1[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a0[i] = OpA::frag(cur, wr * TM + i * 16, 0, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b0[j] = OpB::frag(cur + OpA::BYTES, wc * TN + j * 16, 0, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a1[i] = OpA::frag(cur, wr * TM + i * 16, 1, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b1[j] = OpB::frag(cur + OpA::BYTES, wc * TN + j * 16, 1, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        if (i < live)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b0[j], a0[i], acc[i][j]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        if (i < live)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b1[j], a1[i], acc[i][j]);
+    }
+  }
+  __syncthreads();  // every wave is done with the ring (the Q / K / V images go there next)
+  char* os = smem + 6 * 8192;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int r = wr * TM + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int c = wc * TN + j * 16 + 4 * (lane >> 4);
+      *reinterpret_cast<uint2*>(os + (r >> 6) * 8192 + tile_off(r & 63, c >> 3) + (c & 7) * 2) =
+          make_uint2(pack_bf2(acc[i][j][0], acc[i][j][1]), pack_bf2(acc[i][j][2], acc[i][j][3]));
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void attn_bwd_proj_kernel(AttnArgs a, OProjArgs pj) {
+  __shared__ __attribute__((aligned(1024))) char smem[ATT_BWD_SMEM];
+  const int b = blockIdx.z, h = blockIdx.y;
+  auto proj = [&](int tok0, int len) { op_project(pj, a, tok0, len, h, smem); };
+  attn_bwd_s128_body<2>(a, b, h, smem, proj);
+}
+
 // LayerNorm-fused NT GEMM (EPI_LN / EPI_LN_BWD): the tiles of a row block are consecutive
 // logical tiles (row-major tile order), so after the XCD remap they run on one XCD, in order.
 // BKM = false: B is the weight W [K][N] itself (MN-major; the backward dX GEMMs without W^T).
@@ -2240,6 +2336,27 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
   }
   QkvAttnSync q{flags, cnt, err, xsite, ntiles, tiles_n};
   hipLaunchKernelGGL(gemm_attn_fwd_kernel, dim3(ntiles + items), dim3(64 * QA_NW), 0, st, p, a, q);
+  return 0;
+}
+
+// The S <= 128 attention backward with the out-projection's dX computed per (sequence, head) inside
+// it (attn_bwd_proj_kernel): fd_attn_bwd's arguments with dctx replaced by dy [M][K] and the
+// out-projection weight W [K][D].  Full-query backward only (q_live 0, no compact [CLS] rows).
+int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dy,
+                     const void* w, int M, int K, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr,
+                     uint32_t site, uint32_t thr, float drop_scale, const int* cu, int rows, const uint64_t* dmask,
+                     hipStream_t st) {
+  if (S % 64 || S > 128 || K % BKT || M <= 0 || B <= 0 || !dy || !w) return 1;
+  if ((cu ? rows : B * S) != M) return 2;
+  AttnArgs a{};
+  a.cu = cu;
+  a.dmask = const_cast<uint64_t*>(dmask);
+  a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = (float*)lse;
+  a.dqkv = (bf16_t*)dqkv;
+  a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
+  a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
+  OProjArgs pj{(const bf16_t*)dy, (const bf16_t*)w, M, K};
+  hipLaunchKernelGGL(attn_bwd_proj_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a, pj);
   return 0;
 }
 

@@ -422,10 +422,15 @@ class LayerFn(torch.autograd.Function):
             dh = K.linear_dx(du, L["l1_w"], res=dz2)
             dz1, _ = K.ln_bwd(dh, ao, None if fused else x, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
                               G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, zin=fused)
-        dcx = K.linear_dx(dz1, L["o_w"])
         if not rc.group_dw and batch is None:
             K.linear_dw(dz1, cx, G["o_w"].buf, acc)
-        dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, ctx.dmask)
+        if K.attn_bwd_proj_ok(rc.S):  # the out-projection's dX computed inside the attention backward
+            dqkv = K.attn_bwd_proj(qkv, rc.kbias, cx, lse, dz1, L["o_w"], rc.B, rc.S, rc.H, rc.seed, attn_site, p_a,
+                                   rc.cu, ctx.dmask)
+        else:
+            dcx = K.linear_dx(dz1, L["o_w"])
+            dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu,
+                              ctx.dmask)
         dw_bias = batch is not None and K.DW_QKV_BIAS  # qkv bias gradient in the dW launch
         if batch is not None:
             batch += [(dz1, cx, G["o_w"].buf, acc),

@@ -419,6 +419,29 @@ def qkv_attn_fwd(x, w, b, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_
     return qkv, ctx, lse, kw["cxc"], kw["xc"]
 
 
+# The S <= 128 attention backward that computes its own dO -- the out-projection's dX for the
+# (sequence, head)'s rows and columns -- inside the launch (csrc/kernels/gemm.hip
+# attn_bwd_proj_kernel): one launch and one dctx round trip less per block -- 26.7 vs 19.4 + 9.1 us per
+# layer, -12 us per step over 10 interleaved 200-step pairs (profiles/r6_ab_attn_bwd_proj.txt).
+# FD_FUSE_ATTN_BWD=0: the out-projection dX GEMM + the attention backward.
+FUSE_ATTN_BWD = int(_os.environ.get("FD_FUSE_ATTN_BWD", "1"))
+
+
+def attn_bwd_proj_ok(S: int) -> bool:
+    return bool(FUSE_ATTN_BWD) and S in (64, 128) and _os.environ.get("FD_ATTN_S128", "1") != "0"
+
+
+def attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, B, S, H, seed, site, p, cu=None, dmask=None):
+    """``attn_bwd(qkv, kbias, ctx, lse, linear_dx(dy, w), ...)`` as one launch (full-query backward,
+    S <= 128): dy [rows, K] is the out-projection's output gradient, w [K, H 64] its weight.  Bitwise
+    the two-launch path.  Returns dqkv."""
+    dqkv = torch.empty_like(qkv)
+    thr, sc = _drop(p)
+    ext().attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, dqkv, B, S, H, seed, site, thr, sc, cu,
+                        dmask if thr else None)
+    return dqkv
+
+
 def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, dresc=None):
     """dmask: the keep bits recorded by the matching ``attn_fwd`` (same seed / site / p).
 

@@ -160,3 +160,55 @@ def test_model_step_fused_qkv_attention_bitwise(packed, prune, mode, monkeypatch
     (l0, z0, g0), (l1, z1, g1) = outs
     assert torch.equal(z0, z1) and l0.item() == l1.item() and torch.equal(g0, g1)
     K.check_ln_error(ids.device)
+
+
+@pytest.mark.parametrize("packed", [True, False])
+@pytest.mark.parametrize("B,S", [(32, 128), (8, 64), (5, 128)])
+def test_attention_backward_with_projection_bitwise(packed, B, S, mode):
+    """attn_bwd_proj (the out-projection's dX computed per (sequence, head) inside the attention
+    backward, csrc/kernels/gemm.hip attn_bwd_proj_kernel) == linear_dx + attn_bwd, bit for bit,
+    with and without dropout keep bits."""
+    if mode != 1:
+        pytest.skip("(independent of the forward fusion mode)")
+    x, w, b, kb, cu, lens = _problem(B, S, packed, seed=31 + B + S)
+    g = torch.Generator(device="cuda").manual_seed(B + S)
+    seed = torch.tensor([6], dtype=torch.int32, device="cuda")
+    wo = (torch.randn(D, D, device="cuda", generator=g) * 0.03).to(torch.bfloat16)
+    dy = (torch.randn(x.shape[0], D, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+    for p in (0.0, 0.1):
+        dm = K.attn_keep_bits(B, S, H, p, "cuda")
+        if dm is not None:
+            dm.zero_()
+        qkv = K.linear_fwd(x, w, b)
+        ctx, lse = K.attn_fwd(qkv, kb, B, S, H, seed, 12, p, cu, dm)
+        ref = K.attn_bwd(qkv, kb, ctx, lse, K.linear_dx(dy, wo), B, S, H, seed, 12, p, cu, dm)
+        got = K.attn_bwd_proj(qkv, kb, ctx, lse, dy, wo, B, S, H, seed, 12, p, cu, dm)
+        torch.cuda.synchronize()
+        if packed:
+            assert torch.equal(got, ref)
+        else:
+            valid = (torch.arange(S)[None] < lens[:, None]).reshape(-1).cuda()
+            assert torch.equal(got[valid], ref[valid])
+
+
+@pytest.mark.parametrize("packed,prune", [(True, True), (False, False)])
+def test_model_step_fused_attention_backward_bitwise(packed, prune, mode, monkeypatch):
+    """A training step with the out-projection dX inside the attention backward equals the
+    two-launch step bit for bit (loss, logits, every gradient)."""
+    if mode != 2:
+        pytest.skip("(run once, with the default forward)")
+    outs = []
+    for on in (1, 0):
+        monkeypatch.setattr(K, "FUSE_ATTN_BWD", on)
+        m = DDoSClassifier(config=DistilBertConfig(n_layers=3), device="cuda", impl="hip", seed=33)
+        m.prune_last = prune
+        m.train()
+        ids, mask, labels, tokens = _batch(32, 128, seed=78)
+        m.zero_grad()
+        m.rng.fill_(4)
+        loss, logits = m.forward_loss(ids, mask, labels, tokens=tokens if packed else None)
+        loss.backward()
+        torch.cuda.synchronize()
+        outs.append((loss.detach().clone(), logits.detach().clone(), m.arena.grad.clone()))
+    (l0, z0, g0), (l1, z1, g1) = outs
+    assert torch.equal(z0, z1) and l0.item() == l1.item() and torch.equal(g0, g1)
