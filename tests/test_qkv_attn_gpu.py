@@ -162,15 +162,15 @@ def test_model_step_fused_qkv_attention_bitwise(packed, prune, mode, monkeypatch
     K.check_ln_error(ids.device)
 
 
-@pytest.mark.parametrize("packed", [True, False])
+@pytest.mark.parametrize("packed,empty", [(True, None), (True, 2), (False, None)])
 @pytest.mark.parametrize("B,S", [(32, 128), (8, 64), (5, 128)])
-def test_attention_backward_with_projection_bitwise(packed, B, S, mode):
+def test_attention_backward_with_projection_bitwise(packed, empty, B, S, mode):
     """attn_bwd_proj (the out-projection's dX computed per (sequence, head) inside the attention
     backward, csrc/kernels/gemm.hip attn_bwd_proj_kernel) == linear_dx + attn_bwd, bit for bit,
     with and without dropout keep bits."""
     if mode != 1:
         pytest.skip("(independent of the forward fusion mode)")
-    x, w, b, kb, cu, lens = _problem(B, S, packed, seed=31 + B + S)
+    x, w, b, kb, cu, lens = _problem(B, S, packed, seed=31 + B + S, empty=empty)
     g = torch.Generator(device="cuda").manual_seed(B + S)
     seed = torch.tensor([6], dtype=torch.int32, device="cuda")
     wo = (torch.randn(D, D, device="cuda", generator=g) * 0.03).to(torch.bfloat16)
