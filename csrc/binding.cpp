@@ -72,9 +72,9 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
                      const void* xres, int Bp, uint64_t* flags, int nflags, const int* cnt, int xsite, int* err,
                      int mode, hipStream_t st);
 int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dy,
-                     const void* w, int M, int K, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr,
-                     uint32_t site, uint32_t thr, float drop_scale, const int* cu, int rows, const uint64_t* dmask,
-                     hipStream_t st);
+                     const void* w, int M, int K, int splits, void* dqkv, int B, int S, int H,
+                     const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu, int rows,
+                     const uint64_t* dmask, const void* dresc, void* dres, hipStream_t st);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
                 int rows, uint64_t* dmask, int q_live, void* cxc, void* xc, const void* xres, int Bp,
@@ -1005,8 +1005,14 @@ void gemm_attn_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
 void attn_bwd_proj(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
                    const at::Tensor& dy, const at::Tensor& w, const at::Tensor& dqkv, int64_t B, int64_t S, int64_t H,
                    const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
-                   const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask) {
+                   const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask, int64_t splits = 1,
+                   const c10::optional<at::Tensor>& dresc = c10::nullopt,
+                   const c10::optional<at::Tensor>& dres = c10::nullopt) {
+  // splits: the K splits of the out-projection GEMM this stands in for (its summation order);
+  // dresc / dres: the pruned block's compact [CLS] form (dy = the [CLS] rows [Bp, K]), as attn_bwd
   check_dmask(dmask, B, S, H);
+  const bool compact = dresc.has_value() && dresc->defined();
+  TORCH_CHECK(compact == (dres.has_value() && dres->defined()), "attn_bwd_proj: dresc and dres go together");
   need(qkv, at::kBFloat16, "qkv");
   need(kbias, at::kFloat, "kbias");
   need(ctx, at::kBFloat16, "ctx");
@@ -1020,15 +1026,23 @@ void attn_bwd_proj(const at::Tensor& qkv, const at::Tensor& kbias, const at::Ten
   const int64_t rows = varlen ? qkv.numel() / (3 * D) : B * S;
   TORCH_CHECK(qkv.numel() == rows * 3 * D && dqkv.numel() == qkv.numel() && ctx.numel() == rows * D,
               "attn_bwd_proj: qkv / dqkv / ctx size");
-  TORCH_CHECK(dy.dim() == 2 && dy.size(0) == rows && w.dim() == 2 && w.size(0) == dy.size(1) && w.size(1) == D,
-              "attn_bwd_proj: dy [rows, K] and w [K, H 64] required");
-  TORCH_CHECK(dy.size(1) % 64 == 0, "attn_bwd_proj: K must be a multiple of 64");
+  TORCH_CHECK(dy.dim() == 2 && (compact ? dy.size(0) >= B : dy.size(0) == rows) && w.dim() == 2 &&
+                  w.size(0) == dy.size(1) && w.size(1) == D,
+              "attn_bwd_proj: dy [rows (compact: >= B), K] and w [K, H 64] required");
+  TORCH_CHECK(dy.size(1) % 64 == 0 && splits >= 1 && (dy.size(1) / 64) % splits == 0,
+              "attn_bwd_proj: K must be a multiple of 64 and of 64 splits");
+  if (compact) {
+    need(*dresc, at::kBFloat16, "dresc");
+    need(*dres, at::kBFloat16, "dres");
+    TORCH_CHECK(dresc->numel() == dy.size(0) * D && dres->numel() == rows * D, "attn_bwd_proj: dresc / dres size");
+  }
   TORCH_CHECK(lse.numel() == B * H * S && (varlen || kbias.numel() == B * S), "attn_bwd_proj: stats");
   check_cu(cu, B, rows, rows);
   check_rc(fd_attn_bwd_proj(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(),
-                            dy.data_ptr(), w.data_ptr(), (int)rows, (int)dy.size(1), dqkv.data_ptr(), (int)B, (int)S,
-                            (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), (int)rows,
-                            ptr<uint64_t>(dmask), stream()),
+                            dy.data_ptr(), w.data_ptr(), (int)dy.size(0), (int)dy.size(1), (int)splits, dqkv.data_ptr(),
+                            (int)B, (int)S, (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale,
+                            ptr<int>(cu), (int)rows, ptr<uint64_t>(dmask), compact ? dresc->data_ptr() : nullptr,
+                            compact ? dres->data_ptr() : nullptr, stream()),
            "attn_bwd_proj");
 }
 
@@ -1646,7 +1660,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dresc") = py::none(), py::arg("dres") = py::none());
   m.def("attn_bwd_proj", &attn_bwd_proj, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"),
         py::arg("dy"), py::arg("w"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"),
-        py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"));
+        py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("splits") = 1,
+        py::arg("dresc") = py::none(), py::arg("dres") = py::none());
   m.def("mask_to_bias", &mask_to_bias);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);

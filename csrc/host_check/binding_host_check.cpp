@@ -320,8 +320,9 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
   return 0;
 }
 int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dy,
-                     const void* w, int M, int K, void* dqkv, int B, int S, int H, const uint32_t* seed, uint32_t,
-                     uint32_t, float, const int* cu, int rows, const uint64_t* dmask, hipStream_t) {
+                     const void* w, int M, int K, int, void* dqkv, int B, int S, int H, const uint32_t* seed,
+                     uint32_t, uint32_t, float, const int* cu, int rows, const uint64_t* dmask, const void* dresc,
+                     void* dres, hipStream_t) {
   ++hc::calls;
   const long long D = (long long)H * 64;
   hc::opt_span(dmask, (long long)B * H * 256 * 8, "attn bwd proj dmask");
@@ -330,6 +331,8 @@ int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const
   hc::span(ctx, rows * D * 2, "attn bwd proj ctx");
   hc::span(dy, (long long)M * K * 2, "attn bwd proj dy");
   hc::span(w, (long long)K * D * 2, "attn bwd proj w");
+  hc::opt_span(dresc, (long long)M * D * 2, "attn bwd proj dresc");
+  hc::opt_span(dres, rows * D * 2, "attn bwd proj dres");
   hc::span(lse, (long long)B * H * S * 4, "attn bwd proj lse");
   hc::span(seed, 4, "attn bwd proj seed");
   if (cu) hc::span(cu, (long long)(B + 1) * 4, "attn bwd proj cu");

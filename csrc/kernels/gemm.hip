@@ -1576,22 +1576,28 @@ __global__ __launch_bounds__(512, 2) void seq_attn_fwd_kernel(SeqQkvArgs g, Attn
 // out-projection's input gradient dctx = dy W (dy = the out-projection's output gradient [T][D],
 // W = its weight [D][D] as the MN-major B operand, exactly linear_dx's NN GEMM) -- for the sequence's
 // rows, straight into the backward's swizzled dO image: no dctx round trip through HBM and no launch
-// of its own.  The Q / K / V loads of the backward are in flight across the K loop, whose 2-slot ring
-// borrows the Q / K / V image region.  Same per-element MFMA chain as the cfg-24 NN GEMM (128 x 64,
+// of its own.  The Q / K / V loads of the backward are in flight across the K loop, whose 3-slot ring
+// (two tiles in flight, counted waits) borrows the image region.  Same per-element MFMA chain as the cfg-24 NN GEMM (128 x 64,
 // 4 x 2 waves), so dO -- and with it every gradient -- is bitwise the two-launch path's.  Rows past
 // the sequence's live 16-row sub-tiles are neither loaded nor multiplied (dO 0 there: rows whose
 // probabilities are exactly 0).
 struct OProjArgs {
-  const bf16_t* dy;  // [M][K]
+  const bf16_t* dy;  // [M][K] (the compact [CLS] form: [Bp][K], row b = sequence b's)
   const bf16_t* w;   // [K][D]: W itself (MN-major B)
   int M, K;
+  int ksplit;        // K tiles per split: the split-K GEMM's partial chains, summed in split order
+                     // (its slab reduce), when dy is the pruned block's M <= 64 compact rows
 };
 using OpA = Operand<128, true, 8>;
 using OpB = Operand<64, false, 8>;
-constexpr int OP_BUF = OpA::BYTES + OpB::BYTES;
-static_assert(2 * OP_BUF <= 6 * 8192, "the projection ring fits the Q / K / V image region");
+constexpr int OP_BUF = OpA::BYTES + OpB::BYTES, OP_S = 3;
+// the 3-slot ring spans the Q / K / V / dO images and the row tables after them: all written after it
+constexpr int OP_SMEM = OP_S * OP_BUF > ATT_BWD_SMEM ? OP_S * OP_BUF : ATT_BWD_SMEM;
+static_assert(OP_SMEM <= 80 * 1024, "two blocks per CU");
 
-DEV void op_project(const OProjArgs& pj, const AttnArgs& a, int tok0, int len, int h, char* smem) {
+// rows [tok0, tok0 + len) of dy -> dO image rows [0, len); image rows >= keep are written as zeros
+// (the compact form: one row, the others' dO 0 like stage_cls_rows)
+DEV void op_project(const OProjArgs& pj, const AttnArgs& a, int tok0, int len, int h, char* smem, int keep = 128) {
   constexpr int WN = 2, TM = 32, TN = 32, MI = TM / 16, NI = TN / 16;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1599,13 +1605,18 @@ DEV void op_project(const OProjArgs& pj, const AttnArgs& a, int tok0, int len, i
   const int D = a.H * DH, nk = pj.K / BKT;
   const int rem = len - wr * TM, live = rem <= 0 ? 0 : min(MI, (rem + 15) >> 4);
   const int rows_live = min(128, (len + 15) & ~15);
-  f32x4 acc[MI][NI];
+  f32x4 acc[MI][NI], tot[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NI; ++j) acc[i][j] = tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool split = pj.ksplit < nk;  // (uniform)
+  // this wave's DMA ops per K tile (its A pieces of live rows + one B piece): the counted ring wait
+  const int ops = (wid * OpA::PER_WAVE * 8 < rows_live ? 1 : 0) + ((wid * OpA::PER_WAVE + 1) * 8 < rows_live ? 1 : 0) +
+                  OpB::PER_WAVE;
+  static_assert(OpA::PER_WAVE == 2, "ops count");
   auto issue = [&](int t) {
-    char* sl = smem + (t & 1) * OP_BUF;
+    char* sl = smem + (t % OP_S) * OP_BUF;
     const char* abase = reinterpret_cast<const char*>(pj.dy + t * BKT);
 #pragma unroll
     for (int i = 0; i < OpA::PER_WAVE; ++i) {  // the sequence's live A rows only (8 rows per piece)
@@ -1618,12 +1629,15 @@ DEV void op_project(const OProjArgs& pj, const AttnArgs& a, int tok0, int len, i
     OpB::stage(pj.w, D, h * DH, t * BKT, D, sl + OpA::BYTES, wid, lane);
   };
   issue(0);
+  if (nk > 1) issue(1);
   for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt landed (one tile in flight)
-    __builtin_amdgcn_s_barrier();
+    // tile kt landed; tile kt + 1 (if any) stays in flight
+    if (kt + 1 < nk) wait_ops(ops);
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // ... in every wave; everyone also finished reading tile kt - 1's slot
     asm volatile("" ::: "memory");
-    if (kt + 1 < nk) issue(kt + 1);
-    const char* cur = smem + (kt & 1) * OP_BUF;
+    if (kt + 2 < nk) issue(kt + 2);
+    const char* cur = smem + (kt % OP_S) * OP_BUF;
     if (live > 0) {
       bf16x8 a0[MI], b0[NI], a1[MI], b1[NI];
 #pragma unroll
@@ -1645,6 +1659,21 @@ DEV void op_project(const OProjArgs& pj, const AttnArgs& a, int tok0, int len, i
 #pragma unroll
           for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(b1[j], a1[i], acc[i][j]);
     }
+    if (split && kt % pj.ksplit == pj.ksplit - 1) {  // a split's partial: added in split order, then restart
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          tot[i][j] = tot[i][j] + acc[i][j];
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+  }
+  if (split) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = tot[i][j];
   }
   __syncthreads();  // every wave is done with the ring (the Q / K / V images go there next)
   char* os = smem + 6 * 8192;
@@ -1655,15 +1684,20 @@ DEV void op_project(const OProjArgs& pj, const AttnArgs& a, int tok0, int len, i
     for (int j = 0; j < NI; ++j) {
       const int c = wc * TN + j * 16 + 4 * (lane >> 4);
       *reinterpret_cast<uint2*>(os + (r >> 6) * 8192 + tile_off(r & 63, c >> 3) + (c & 7) * 2) =
-          make_uint2(pack_bf2(acc[i][j][0], acc[i][j][1]), pack_bf2(acc[i][j][2], acc[i][j][3]));
+          r < keep ? make_uint2(pack_bf2(acc[i][j][0], acc[i][j][1]), pack_bf2(acc[i][j][2], acc[i][j][3]))
+                   : make_uint2(0u, 0u);
     }
   }
 }
 
 __global__ __launch_bounds__(512) void attn_bwd_proj_kernel(AttnArgs a, OProjArgs pj) {
-  __shared__ __attribute__((aligned(1024))) char smem[ATT_BWD_SMEM];
+  __shared__ __attribute__((aligned(1024))) char smem[OP_SMEM];
   const int b = blockIdx.z, h = blockIdx.y;
-  auto proj = [&](int tok0, int len) { op_project(pj, a, tok0, len, h, smem); };
+  // compact [CLS] form (a.dres): dO row 0 = dy row b, every other row 0
+  auto proj = [&](int tok0, int len) {
+    if (a.dres) op_project(pj, a, b, 1, h, smem, 1);
+    else op_project(pj, a, tok0, len, h, smem);
+  };
   attn_bwd_s128_body<2>(a, b, h, smem, proj);
 }
 
@@ -2341,21 +2375,26 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
 
 // The S <= 128 attention backward with the out-projection's dX computed per (sequence, head) inside
 // it (attn_bwd_proj_kernel): fd_attn_bwd's arguments with dctx replaced by dy [M][K] and the
-// out-projection weight W [K][D].  Full-query backward only (q_live 0, no compact [CLS] rows).
+// out-projection weight W [K][D].  splits: the K splits of the GEMM it stands in for (1: one chain;
+// the pruned block's M <= 64 split-K slabs otherwise, summed in split order -- bitwise either way).
+// dresc / dres (the pruned block's compact [CLS] form, q_live 1): dy holds the [CLS] rows.
 int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dy,
-                     const void* w, int M, int K, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr,
-                     uint32_t site, uint32_t thr, float drop_scale, const int* cu, int rows, const uint64_t* dmask,
-                     hipStream_t st) {
-  if (S % 64 || S > 128 || K % BKT || M <= 0 || B <= 0 || !dy || !w) return 1;
-  if ((cu ? rows : B * S) != M) return 2;
+                     const void* w, int M, int K, int splits, void* dqkv, int B, int S, int H,
+                     const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu, int rows,
+                     const uint64_t* dmask, const void* dresc, void* dres, hipStream_t st) {
+  if (S % 64 || S > 128 || K % BKT || M <= 0 || B <= 0 || !dy || !w || splits <= 0 || (K / BKT) % splits) return 1;
+  // compact [CLS] form: dy = the [CLS] rows' out-projection gradient [M >= B][K]; q_live 1
+  if ((dresc != nullptr) != (dres != nullptr) || (dres ? M < B : (cu ? rows : B * S) != M)) return 2;
   AttnArgs a{};
+  a.dresc = (const bf16_t*)dresc; a.dres = (bf16_t*)dres;
+  a.q_live = dres ? 1 : 0;
   a.cu = cu;
   a.dmask = const_cast<uint64_t*>(dmask);
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = (float*)lse;
   a.dqkv = (bf16_t*)dqkv;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
-  OProjArgs pj{(const bf16_t*)dy, (const bf16_t*)w, M, K};
+  OProjArgs pj{(const bf16_t*)dy, (const bf16_t*)w, M, K, K / BKT / splits};
   hipLaunchKernelGGL(attn_bwd_proj_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a, pj);
   return 0;
 }

@@ -333,13 +333,19 @@ class LayerFn(torch.autograd.Function):
         dz1c, _ = K.linear_dx_ln_bwd(du, L["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
                                      G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, xsite=K.ln_xsite(ctx.idx, 0, True),
                                      b_mn=True, prefetch=L["o_w"])
-        dcxc = K.linear_dx(dz1c, L["o_w"])
-        if K.attn_cls_compact_ok(rc.S):
+        if K.attn_cls_compact_ok(rc.S) and K.attn_bwd_proj_ok(rc.S, cls=True):
+            # the out-projection's dX of the [CLS] rows inside the attention backward, which also
+            # scatters dz1c into the full layout
+            dqkv, dz1 = K.attn_bwd_proj(qkv, rc.kbias, cx, lse, dz1c, L["o_w"], rc.B, rc.S, rc.H, rc.seed, attn_site,
+                                        p_a, rc.cu, ctx.dmask, dresc=dz1c)
+        elif K.attn_cls_compact_ok(rc.S):
+            dcxc = K.linear_dx(dz1c, L["o_w"])
             # the attention backward reads the compact [CLS] gradient and scatters dz1c into the
             # full layout itself (every other row exactly 0)
             dqkv, dz1 = K.attn_bwd(qkv, rc.kbias, cx, lse, dcxc, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu,
                                    ctx.dmask, q_live=1, dresc=dz1c)
         else:
+            dcxc = K.linear_dx(dz1c, L["o_w"])
             # the [CLS] rows' gradients back into the full layout (every other row exactly 0)
             dcx, dz1 = K.scatter_rows2(dcxc, dz1c, ci, B, cx.shape[0])
             dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu,

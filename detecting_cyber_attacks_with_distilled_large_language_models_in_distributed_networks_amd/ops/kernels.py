@@ -427,19 +427,46 @@ def qkv_attn_fwd(x, w, b, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_
 FUSE_ATTN_BWD = int(_os.environ.get("FD_FUSE_ATTN_BWD", "1"))
 
 
-def attn_bwd_proj_ok(S: int) -> bool:
-    return bool(FUSE_ATTN_BWD) and S in (64, 128) and _os.environ.get("FD_ATTN_S128", "1") != "0"
+# the pruned block's compact [CLS] form of it (FD_FUSE_ATTN_BWD_CLS=0: the split-K out-projection dX +
+# the attention backward there)
+FUSE_ATTN_BWD_CLS = int(_os.environ.get("FD_FUSE_ATTN_BWD_CLS", "1"))
 
 
-def attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, B, S, H, seed, site, p, cu=None, dmask=None):
-    """``attn_bwd(qkv, kbias, ctx, lse, linear_dx(dy, w), ...)`` as one launch (full-query backward,
-    S <= 128): dy [rows, K] is the out-projection's output gradient, w [K, H 64] its weight.  Bitwise
-    the two-launch path.  Returns dqkv."""
+def attn_bwd_proj_ok(S: int, cls: bool = False) -> bool:
+    return (bool(FUSE_ATTN_BWD) and (not cls or bool(FUSE_ATTN_BWD_CLS)) and S in (64, 128)
+            and _os.environ.get("FD_ATTN_S128", "1") != "0")
+
+
+def _dx_splits(M: int, N: int, K: int) -> int:
+    """The K splits ``linear_dx`` runs an M x N x K product with: the split-K slabs of the small-M
+    GEMMs (csrc/kernels/gemm.hip fd_gemm_f32_splits' pick), else 1 (one chain)."""
+    if not _splitk_ok(M, N, K):
+        return 1
+    tiles = ((M + (63 if M <= 64 else 127)) // (64 if M <= 64 else 128)) * (N // 64)
+    nkt, s = K // 64, 1
+    for c in range(1, nkt + 1):
+        if nkt % c == 0 and tiles * c <= 256 and nkt // c >= 2:
+            s = c
+    return s
+
+
+def attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, B, S, H, seed, site, p, cu=None, dmask=None, dresc=None):
+    """``attn_bwd(qkv, kbias, ctx, lse, linear_dx(dy, w), ...)`` as one launch (S <= 128): dy [rows, K]
+    is the out-projection's output gradient, w [K, H 64] its weight.  dresc (the pruned block's
+    compact form, q_live 1): dy is the [CLS] rows' gradient [Bp, K] and, as in ``attn_bwd``, the launch
+    also scatters dresc into the full layout.  Bitwise the two-launch path (including the split-K
+    summation order of the small-M product).  Returns dqkv, or (dqkv, dres)."""
     dqkv = torch.empty_like(qkv)
     thr, sc = _drop(p)
+    splits = _dx_splits(dy.shape[0], w.shape[1], dy.shape[1])
+    if dresc is None:
+        ext().attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, dqkv, B, S, H, seed, site, thr, sc, cu,
+                            dmask if thr else None, splits)
+        return dqkv
+    dres = torch.empty_like(ctx)
     ext().attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, dqkv, B, S, H, seed, site, thr, sc, cu,
-                        dmask if thr else None)
-    return dqkv
+                        dmask if thr else None, splits, dresc.contiguous(), dres)
+    return dqkv, dres
 
 
 def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, dresc=None):

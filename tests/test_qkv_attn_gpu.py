@@ -212,3 +212,31 @@ def test_model_step_fused_attention_backward_bitwise(packed, prune, mode, monkey
         outs.append((loss.detach().clone(), logits.detach().clone(), m.arena.grad.clone()))
     (l0, z0, g0), (l1, z1, g1) = outs
     assert torch.equal(z0, z1) and l0.item() == l1.item() and torch.equal(g0, g1)
+
+
+@pytest.mark.parametrize("packed,empty", [(True, None), (True, 5), (False, None)])
+def test_compact_attention_backward_with_projection_bitwise(packed, empty, mode):
+    """The pruned block's form: the [CLS] rows' out-projection dX (an M = 64 split-K product in the
+    two-launch path: 6 partial chains summed in split order) inside the q_live = 1 attention
+    backward, which also scatters the residual gradient -- bitwise linear_dx + attn_bwd(dresc=)."""
+    if mode != 1:
+        pytest.skip("(independent of the forward fusion mode)")
+    B, S, Bp = 20, 128, 64
+    x, w, b, kb, cu, lens = _problem(B, S, packed, seed=23, empty=empty)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    seed = torch.tensor([8], dtype=torch.int32, device="cuda")
+    wo = (torch.randn(D, D, device="cuda", generator=g) * 0.03).to(torch.bfloat16)
+    dyc = (torch.randn(Bp, D, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+    assert K._dx_splits(Bp, D, D) > 1  # (the split-K order is what is being reproduced)
+    for p in (0.0, 0.1):
+        dm = K.attn_keep_bits(B, S, H, p, "cuda")
+        if dm is not None:
+            dm.zero_()
+        qkv = K.linear_fwd(x, w, b)
+        ctx, lse, cxc, xc = K.attn_fwd(qkv, kb, B, S, H, seed, 14, p, cu, dm, q_live=1, cls=(x, Bp))
+        ref_q, ref_r = K.attn_bwd(qkv, kb, ctx, lse, K.linear_dx(dyc, wo), B, S, H, seed, 14, p, cu, dm, q_live=1,
+                                  dresc=dyc)
+        got_q, got_r = K.attn_bwd_proj(qkv, kb, ctx, lse, dyc, wo, B, S, H, seed, 14, p, cu, dm, dresc=dyc)
+        torch.cuda.synchronize()
+        assert torch.equal(got_r, ref_r)
+        assert torch.equal(got_q, ref_q)
