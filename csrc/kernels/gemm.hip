@@ -1441,6 +1441,7 @@ struct SeqQkvArgs {
   const bf16_t* w;   // [3 D][K]
   const float* bias; // [3 D]
   int M, K;
+  int seq_major;     // logical item order: 0 head-major (an XCD walks ~1.5 heads), 1 sequence-major
 };
 using SaA = Operand<128, true, 8>;
 using SaB = Operand<192, true, 8>;
@@ -1560,7 +1561,8 @@ __global__ __launch_bounds__(512, 2) void seq_attn_fwd_kernel(SeqQkvArgs g, Attn
   const int nb = a.B + (a.cu ? 1 : 0);
   // head-major logical order: after the XCD remap one XCD walks ~1.5 heads (their weight slices
   // stay in its L2) over every sequence
-  const int item = xcd_remap(blockIdx.x, nb * a.H), h = item / nb, b = item - h * nb;
+  const int item = xcd_remap(blockIdx.x, nb * a.H);
+  const int h = g.seq_major ? item % a.H : item / nb, b = g.seq_major ? item / a.H : item - h * nb;
   if (b < a.B) {
     int tok0, len;
     seq_span(a, b, tok0, len);
@@ -1587,6 +1589,7 @@ struct OProjArgs {
   int M, K;
   int ksplit;        // K tiles per split: the split-K GEMM's partial chains, summed in split order
                      // (its slab reduce), when dy is the pruned block's M <= 64 compact rows
+  int order;         // block -> (sequence, head): 1 XCD-remapped sequence-major, 0 launch order
 };
 using OpA = Operand<128, true, 8>;
 using OpB = Operand<64, false, 8>;
@@ -1692,7 +1695,17 @@ DEV void op_project(const OProjArgs& pj, const AttnArgs& a, int tok0, int len, i
 
 __global__ __launch_bounds__(512) void attn_bwd_proj_kernel(AttnArgs a, OProjArgs pj) {
   __shared__ __attribute__((aligned(1024))) char smem[OP_SMEM];
-  const int b = blockIdx.z, h = blockIdx.y;
+  // 1-D grid, XCD remap: sequence-major (one XCD's blocks share their sequences' dy rows in its L2),
+  // or the hardware (head, sequence) order of the 3-D grid (pj.order 0)
+  int b, h;
+  if (pj.order) {
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    h = item % a.H;
+    b = item / a.H;
+  } else {
+    h = blockIdx.x % a.H;
+    b = blockIdx.x / a.H;
+  }
   // compact [CLS] form (a.dres): dO row 0 = dy row b, every other row 0
   auto proj = [&](int tok0, int len) {
     if (a.dres) op_project(pj, a, b, 1, h, smem, 1);
@@ -2364,7 +2377,10 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
   const int items = H * (B + (cu ? 1 : 0));
   if (mode == 2) {  // per-(sequence, head) projection + attention (no hand-off, no flags)
-    SeqQkvArgs g{(const bf16_t*)x, (const bf16_t*)w, bias, M, K};
+    // (sequence-major: an XCD's blocks share their sequences' x rows in its L2 -- -5 us per step over
+    //  4 pairs against head-major, profiles/r6_ab_fused_qkv_attention.txt)
+    static const int seq_major = [] { const char* e = getenv("FD_SEQATTN_SEQ_MAJOR"); return e ? atoi(e) : 1; }();
+    SeqQkvArgs g{(const bf16_t*)x, (const bf16_t*)w, bias, M, K, seq_major};
     hipLaunchKernelGGL(seq_attn_fwd_kernel, dim3(items), dim3(512), 0, st, g, a);
     return 0;
   }
@@ -2394,8 +2410,9 @@ int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const
   a.dqkv = (bf16_t*)dqkv;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
-  OProjArgs pj{(const bf16_t*)dy, (const bf16_t*)w, M, K, K / BKT / splits};
-  hipLaunchKernelGGL(attn_bwd_proj_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a, pj);
+  static const int order = [] { const char* e = getenv("FD_ATTNBWD_SEQ_MAJOR"); return e ? atoi(e) : 1; }();
+  OProjArgs pj{(const bf16_t*)dy, (const bf16_t*)w, M, K, K / BKT / splits, order};
+  hipLaunchKernelGGL(attn_bwd_proj_kernel, dim3(H * (B + (cu ? 1 : 0))), dim3(512), 0, st, a, pj);
   return 0;
 }
 
