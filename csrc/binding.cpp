@@ -36,6 +36,7 @@ int fd_gemm_set_cfg(int kind, int cfg, int splits);
 int fd_gemm_pf(const void* pf, long long bytes);
 int fd_gemm_stamps(unsigned long long* host, int nblocks);
 int fd_attn_stamps(unsigned long long* host, int nblocks);
+int fd_attn_set_split(int on);
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
                 int M1, int N1, int K, float* workspace, long long workspace_elems, int accumulate,
                 const FdAdamEpi* adams, int defer, int* splits_out, hipStream_t st);
@@ -1663,6 +1664,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("splits") = 1,
         py::arg("dresc") = py::none(), py::arg("dres") = py::none());
   m.def("mask_to_bias", &mask_to_bias);
+  m.def("attn_set_split", [](int64_t on) { return (int64_t)fd_attn_set_split((int)on); });
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
   m.def("emb_fwd", &emb_fwd, py::arg("ids"), py::arg("word"), py::arg("pos"), py::arg("gamma"), py::arg("beta"),

@@ -94,6 +94,7 @@ int fd_gemm(int kind, int epi, const void* A, const void* B, void* C, int M, int
 int fd_gemm_set_cfg(int, int, int) { return 0; }
 int fd_gemm_stamps(unsigned long long*, int) { return -1; }
 int fd_attn_stamps(unsigned long long*, int) { return -1; }
+int fd_attn_set_split(int) { return 0; }
 int fd_gemm_dw2(const void* A0, const void* B0, float* C0, int M0, int N0, const void* A1, const void* B1, float* C1,
                 int M1, int N1, int K, float* workspace, long long workspace_elems, int,
                 const FdAdamEpi* adams, int, int* splits_out, hipStream_t) {

@@ -46,13 +46,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
-  if (b == a.B) {  // varlen filler slice
-    zero_filler(a, a.ctx, D, 1, h);
+  if (b == a.B) {  // varlen filler slice (split: zeroed by the S <= 128 kernel)
+    if (!a.split) zero_filler(a, a.ctx, D, 1, h);
     return;
   }
   int tok0i, len;
   seq_span(a, b, tok0i, len);
   if (blockIdx.x * 64 >= len) return;  // varlen: query tile past the sequence (whole block)
+  if (a.split && len <= 128) return;   // split: the S <= 128 kernel's sequence
   const int q = blockIdx.x * 64 + w * 16 + (lane & 15);
   const int qr = min(q, len - 1);       // row actually read
   const size_t tok0 = (size_t)tok0i;
@@ -162,13 +163,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
-  if (b == a.B) {  // varlen filler slice: dq | dk | dv columns of head h
-    zero_filler(a, a.dqkv, ld3, 3, h);
+  if (b == a.B) {  // varlen filler slice: dq | dk | dv columns of head h (split: the S <= 128 kernel's)
+    if (!a.split) zero_filler(a, a.dqkv, ld3, 3, h);
     return;
   }
   int tok0i, len;
   seq_span(a, b, tok0i, len);
-  if (blockIdx.x * 64 >= len) return;
+  if (blockIdx.x * 64 >= len || (a.split && len <= 128)) return;
   const int q = blockIdx.x * 64 + w * 16 + (lane & 15);
   const int qr = min(q, len - 1);
   const size_t tok0 = (size_t)tok0i;
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
   const int b = blockIdx.z, h = blockIdx.y, S = a.S, H = a.H, D = H * DH, ld3 = 3 * D;
   int tok0i, len;
   seq_span(a, b, tok0i, len);
-  if (blockIdx.x * 64 >= len) return;  // varlen: key tile past the sequence (writes nothing)
+  if (blockIdx.x * 64 >= len || (a.split && len <= 128)) return;  // varlen: key tile past the sequence
   const int key = blockIdx.x * 64 + w * 16 + (lane & 15);
   const int kr = min(key, len - 1);
   const size_t tok0 = (size_t)tok0i;
@@ -386,6 +387,15 @@ bool use_s128(int S) {
   return on && S <= 128;
 }
 
+// Varlen batches padded to S > 128 whose real sequences are mostly short (the distillation config:
+// seq256, CICIDS2017 sentences of ~80 tokens): launch BOTH kernel families over the batch; each
+// (sequence, head) is taken by the S <= 128 whole-row kernel when len <= 128 and by the 64-row
+// kernels otherwise (AttnArgs.split; the other family's blocks return at once).  The dropout index
+// ((b H + h) S + q) S + k and the lse / delta layouts follow S in both, so the masks are those of
+// the padded computation either way.  FD_ATTN_SPLIT=0: the 64-row kernels alone.
+int g_attn_split = [] { const char* e = getenv("FD_ATTN_SPLIT"); return e ? atoi(e) : 1; }();
+bool use_split(int S, const int* cu) { return g_attn_split && cu != nullptr && S > 128 && use_s128(128); }
+
 }  // namespace
 
 extern "C" {
@@ -405,10 +415,15 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
-  if (use_s128(S))
+  if (use_s128(S)) {
     hipLaunchKernelGGL(attn_fwd_s128_kernel<8>, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
+    return 0;
+  }
+  if (use_split(S, cu)) {
+    a.split = 1;  // (no keep-bit buffer: the S <= 128 backward re-hashes, as the 64-row one does)
+    hipLaunchKernelGGL(attn_fwd_s128_kernel<8>, dim3(1, H, B + 1), dim3(512), 0, st, a);
+  }
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
   return 0;
 }
 
@@ -432,9 +447,20 @@ int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const floa
     hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
     return 0;
   }
+  if (use_split(S, cu)) {
+    a.split = 1;
+    hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + 1), dim3(512), 0, st, a);
+  }
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);
   return 0;
+}
+
+// FD_ATTN_SPLIT at run time (tests: both dispatches in one process); returns the previous setting.
+int fd_attn_set_split(int on) {
+  const int prev = g_attn_split;
+  g_attn_split = on;
+  return prev;
 }
 
 // Copy the diagnostic stamps (FD_ATTN_STAMPS builds) of blocks [0, nblocks) to host memory

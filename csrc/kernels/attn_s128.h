@@ -109,6 +109,9 @@ struct AttnArgs {
   // scatter_rows2's rule, which this replaces)
   const bf16_t* dresc;
   bf16_t* dres;
+  // varlen at S > 128 (attention.hip fd_attn_fwd / fd_attn_bwd, FD_ATTN_SPLIT): the launch pair splits
+  // the sequences by length -- the S <= 128 kernels take len <= 128, the 64-row kernels the rest
+  int split;
 };
 
 // ctx / xres head-h slices of [CLS] row `tok` into compact row b (4 lanes x 4 uint2 = 64 columns;
@@ -293,6 +296,7 @@ DEV void attn_fwd_s128_body(const AttnArgs& a, int b, int h, int bx, char* smem)
   }
   int tok0i, len;
   seq_span(a, b, tok0i, len);
+  if (a.split && len > 128) return;  // (block-uniform) the 64-row kernel's sequence
   const int nt = (len + 63) >> 6;
   const size_t tok0 = (size_t)tok0i;
   const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows needed
@@ -706,7 +710,7 @@ DEV void attn_bwd_s128_body(const AttnArgs& a, int b, int h, char* smem, const P
   const int qlen = a.q_live > 0 ? min(len, a.q_live) : len;  // query rows with a gradient
   // an empty sequence (varlen) owns no rows: nothing to write, and its clamped row len - 1 = -1
   // must not be read (a leading empty sequence would read before the tensors)
-  if (len == 0) return;
+  if (len == 0 || (a.split && len > 128)) return;  // (split: the 64-row kernels' sequence)
   const size_t tok0 = (size_t)tok0i;
   const size_t st0 = ((size_t)b * H + h) * S;
   // phase 1's O rows (for delta) are fetched together with the staging loads: no second

@@ -50,19 +50,82 @@ def test_varlen_attention_matches_padded(S):
     cu[1:] = torch.cumsum(lens, 0).to(torch.int32).cuda()
     qkv = torch.cat([qkv_pad.index_select(0, idx), torch.zeros(64, 3 * H * 64, dtype=torch.bfloat16,
                                                                  device="cuda")])  # + filler rows
+    # (S > 128: the varlen launch pair's length split off -- the same 64-row kernels as the padded
+    # layout, so bitwise; the split itself: test_varlen_split_dispatch below)
+    prev = K.ext().attn_set_split(0)
+    try:
+        for p in (0.0, 0.1):
+            ctx_p, lse_p = K.attn_fwd(qkv_pad, kb, B, S, H, seed, 40, p)
+            ctx_v, lse_v = K.attn_fwd(qkv, kb, B, S, H, seed, 40, p, cu=cu)
+            n = int(cu[-1])
+            assert torch.equal(ctx_v[:n], ctx_p.index_select(0, idx))
+            assert not ctx_v[n:].any()  # filler rows untouched (zero)
+            dctx_pad = (torch.randn(B * S, H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+            dctx_pad = dctx_pad * mask.reshape(-1, 1)  # padding rows carry no gradient
+            dctx = torch.cat([dctx_pad.index_select(0, idx), torch.zeros(64, H * 64, dtype=torch.bfloat16,
+                                                                          device="cuda")])
+            d_p = K.attn_bwd(qkv_pad, kb, ctx_p, lse_p, dctx_pad, B, S, H, seed, 40, p)
+            d_v = K.attn_bwd(qkv, kb, ctx_v, lse_v, dctx, B, S, H, seed, 40, p, cu=cu)
+            assert rel(d_v[:n], d_p.index_select(0, idx)) < 1e-6
+            assert not d_v[n:].any()
+    finally:
+        K.ext().attn_set_split(prev)
+
+
+def _attn_ref(qkv, lens, H, scale=0.125):
+    """fp32 attention of each packed sequence (no dropout): ctx rows [n, H 64]."""
+    D = H * 64
+    out, t0 = [], 0
+    for L in lens.tolist():
+        x = qkv[t0:t0 + L].float().view(L, 3, H, 64)
+        q, k, v = x[:, 0].transpose(0, 1), x[:, 1].transpose(0, 1), x[:, 2].transpose(0, 1)
+        pr = torch.softmax(q @ k.transpose(1, 2) * scale, -1)
+        out.append((pr @ v).transpose(0, 1).reshape(L, D))
+        t0 += L
+    return torch.cat(out)
+
+
+@pytest.mark.parametrize("S", [256, 512])
+def test_varlen_split_dispatch(S):
+    """Varlen at S > 128 (FD_ATTN_SPLIT, default on): sequences of <= 128 tokens go to the S <= 128
+    whole-row kernels, longer ones to the 64-row kernels, in one launch pair.  Against the 64-row
+    kernels alone: the long sequences are bitwise theirs; the short ones agree to bf16 rounding
+    with the SAME dropout masks (a different mask would differ by O(1)); both match fp32 at p = 0;
+    the filler rows stay zero."""
+    B, H = 8, 12
+    g = torch.Generator(device="cuda").manual_seed(3)
+    lens = torch.tensor(_LENS[S])
+    n = int(lens.sum())
+    cu = torch.zeros(B + 1, dtype=torch.int32, device="cuda")
+    cu[1:] = torch.cumsum(lens, 0).to(torch.int32).cuda()
+    qkv = torch.cat([(torch.randn(n, 3 * H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16),
+                     torch.zeros(64, 3 * H * 64, dtype=torch.bfloat16, device="cuda")])
+    dctx = torch.cat([(torch.randn(n, H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16),
+                      torch.zeros(64, H * 64, dtype=torch.bfloat16, device="cuda")])
+    kb = K.mask_bias(torch.ones(B, S, dtype=torch.int64, device="cuda"))  # (varlen: not read)
+    seed = torch.tensor([11], dtype=torch.int32, device="cuda")
+    short = torch.cat([torch.full((L,), L <= 128, dtype=torch.bool) for L in lens.tolist()]).cuda()
+    assert short.any() and (~short).any()
+    res = {}
+    prev = K.ext().attn_set_split(1)
+    try:
+        for split in (0, 1):
+            K.ext().attn_set_split(split)
+            for p in (0.0, 0.1):
+                ctx, lse = K.attn_fwd(qkv, kb, B, S, H, seed, 41, p, cu=cu)
+                d = K.attn_bwd(qkv, kb, ctx, lse, dctx, B, S, H, seed, 41, p, cu=cu)
+                torch.cuda.synchronize()
+                assert not ctx[n:].any() and not d[n:].any()
+                res[split, p] = (ctx[:n].clone(), d[:n].clone())
+    finally:
+        K.ext().attn_set_split(prev)
+    ref = _attn_ref(qkv[:n], lens, H)
     for p in (0.0, 0.1):
-        ctx_p, lse_p = K.attn_fwd(qkv_pad, kb, B, S, H, seed, 40, p)
-        ctx_v, lse_v = K.attn_fwd(qkv, kb, B, S, H, seed, 40, p, cu=cu)
-        n = int(cu[-1])
-        assert torch.equal(ctx_v[:n], ctx_p.index_select(0, idx))
-        assert not ctx_v[n:].any()  # filler rows untouched (zero)
-        dctx_pad = (torch.randn(B * S, H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
-        dctx_pad = dctx_pad * mask.reshape(-1, 1)  # padding rows carry no gradient
-        dctx = torch.cat([dctx_pad.index_select(0, idx), torch.zeros(64, H * 64, dtype=torch.bfloat16, device="cuda")])
-        d_p = K.attn_bwd(qkv_pad, kb, ctx_p, lse_p, dctx_pad, B, S, H, seed, 40, p)
-        d_v = K.attn_bwd(qkv, kb, ctx_v, lse_v, dctx, B, S, H, seed, 40, p, cu=cu)
-        assert rel(d_v[:n], d_p.index_select(0, idx)) < 1e-6
-        assert not d_v[n:].any()
+        (c0, d0), (c1, d1) = res[0, p], res[1, p]
+        assert torch.equal(c1[~short], c0[~short]) and torch.equal(d1[~short], d0[~short])
+        assert rel(c1[short], c0[short]) < 1e-2, rel(c1[short], c0[short])
+        assert rel(d1[short], d0[short]) < 2e-2, rel(d1[short], d0[short])
+    assert rel(res[1, 0.0][0], ref) < 1e-2 and rel(res[0, 0.0][0], ref) < 1e-2
 
 
 @pytest.mark.parametrize("train", [False, True])
