@@ -79,11 +79,11 @@ int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
                 int rows, uint64_t* dmask, int q_live, void* cxc, void* xc, const void* xres, int Bp,
-                hipStream_t st);
+                int split, hipStream_t st);
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx,
                 float* delta, void* dqkv, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site,
                 uint32_t thr, float drop_scale, const int* cu, int rows, const uint64_t* dmask, int q_live,
-                const void* dresc, void* dres, hipStream_t st);
+                const void* dresc, void* dres, int split, hipStream_t st);
 int fd_mask_to_bias(const void* mask, int mask_bytes, float* bias, long n, hipStream_t st);
 int fd_ln_fwd(const void* x, const void* r, const float* gamma, const float* beta, void* y, float* mean,
               float* rstd, int T, int D, float eps, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
@@ -902,9 +902,10 @@ void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
               int64_t B, int64_t S, int64_t H, const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
               const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask, int64_t q_live = 0,
               const c10::optional<at::Tensor>& cxc = c10::nullopt, const c10::optional<at::Tensor>& xc = c10::nullopt,
-              const c10::optional<at::Tensor>& xres = c10::nullopt) {
+              const c10::optional<at::Tensor>& xres = c10::nullopt, int64_t split = -1) {
   need(qkv, at::kBFloat16, "qkv");
   TORCH_CHECK(q_live >= 0, "attention: q_live >= 0");
+  TORCH_CHECK(split >= -1 && split <= 2, "attention: split in -1..2");
   const bool compact = cxc.has_value() && cxc->defined();
   int64_t Bp = 0;
   if (compact) {  // [CLS] rows of ctx and of the residual stream, compacted to [Bp, D]
@@ -929,7 +930,8 @@ void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
   check_rc(fd_attn_fwd(qkv.data_ptr(), kbias.data_ptr<float>(), ctx.data_ptr(), lse.data_ptr<float>(), (int)B,
                        (int)S, (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu),
                        (int)rows, ptr<uint64_t>(dmask), (int)q_live, compact ? cxc->data_ptr() : nullptr,
-                       compact ? xc->data_ptr() : nullptr, compact ? xres->data_ptr() : nullptr, (int)Bp, stream()),
+                       compact ? xc->data_ptr() : nullptr, compact ? xres->data_ptr() : nullptr, (int)Bp, (int)split,
+                       stream()),
            "attn_fwd");
 }
 
@@ -1051,8 +1053,10 @@ void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
               const at::Tensor& dctx, const at::Tensor& delta, const at::Tensor& dqkv, int64_t B, int64_t S, int64_t H,
               const at::Tensor& seed, int64_t site, int64_t thr, double dscale, const c10::optional<at::Tensor>& cu,
               const c10::optional<at::Tensor>& dmask, int64_t q_live = 0,
-              const c10::optional<at::Tensor>& dresc = c10::nullopt, const c10::optional<at::Tensor>& dres = c10::nullopt) {
+              const c10::optional<at::Tensor>& dresc = c10::nullopt, const c10::optional<at::Tensor>& dres = c10::nullopt,
+              int64_t split = -1) {
   TORCH_CHECK(q_live >= 0, "attention: q_live >= 0");
+  TORCH_CHECK(split >= -1 && split <= 2, "attention: split in -1..2");
   check_dmask(dmask, B, S, H);
   // compact [CLS] gradients: dctx and dresc are [Bp, D], dres is the full-layout [rows, D] output
   const bool compact = dresc.has_value() && dresc->defined();
@@ -1085,7 +1089,7 @@ void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
                        dctx.data_ptr(), delta.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)S, (int)H,
                        seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), (int)rows,
                        ptr<uint64_t>(dmask), (int)q_live, compact ? dresc->data_ptr() : nullptr,
-                       compact ? dres->data_ptr() : nullptr, stream()),
+                       compact ? dres->data_ptr() : nullptr, (int)split, stream()),
            "attn_bwd");
 }
 
@@ -1654,11 +1658,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("B"),
         py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"),
         py::arg("dmask"), py::arg("q_live") = 0, py::arg("cxc") = py::none(), py::arg("xc") = py::none(),
-        py::arg("xres") = py::none());
+        py::arg("xres") = py::none(), py::arg("split") = -1);
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("dctx"),
         py::arg("delta"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"),
         py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("q_live") = 0,
-        py::arg("dresc") = py::none(), py::arg("dres") = py::none());
+        py::arg("dresc") = py::none(), py::arg("dres") = py::none(), py::arg("split") = -1);
   m.def("attn_bwd_proj", &attn_bwd_proj, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"),
         py::arg("dy"), py::arg("w"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"),
         py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("splits") = 1,

@@ -276,7 +276,7 @@ int fd_comm_broadcast(void*, void*, long long, int, int, hipStream_t) { return 0
 int fd_comm_allgather(void*, const void*, void*, long long, int, hipStream_t) { return 0; }
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H, const uint32_t* seed,
                 uint32_t, uint32_t, float, const int* cu, int rows, uint64_t* dmask, int, void* cxc, void* xc,
-                const void* xres, int Bp, hipStream_t) {
+                const void* xres, int Bp, int, hipStream_t) {
   ++hc::calls;
   const long long D = (long long)H * 64;
   hc::opt_span(cxc, (long long)Bp * D * 2, "attn cxc");
@@ -342,7 +342,7 @@ int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const
 }
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dctx, float* delta,
                 void* dqkv, int B, int S, int H, const uint32_t* seed, uint32_t, uint32_t, float, const int* cu,
-                int rows, const uint64_t* dmask, int, const void* dresc, void* dres, hipStream_t) {
+                int rows, const uint64_t* dmask, int, const void* dresc, void* dres, int, hipStream_t) {
   ++hc::calls;
   const long long D = (long long)H * 64;
   hc::opt_span(dmask, (long long)B * H * 256 * 8, "attn bwd dmask");

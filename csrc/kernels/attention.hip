@@ -393,8 +393,13 @@ bool use_s128(int S) {
 // kernels otherwise (AttnArgs.split; the other family's blocks return at once).  The dropout index
 // ((b H + h) S + q) S + k and the lse / delta layouts follow S in both, so the masks are those of
 // the padded computation either way.  FD_ATTN_SPLIT=0: the 64-row kernels alone.
+// split (per call): -1 this setting, 0 off, 1 on, 2 the caller knows every sequence has <= 128 tokens
+// (data/dataset.py PackedTokens.max_len): the S <= 128 kernels alone, no 64-row launches at all.
 int g_attn_split = [] { const char* e = getenv("FD_ATTN_SPLIT"); return e ? atoi(e) : 1; }();
-bool use_split(int S, const int* cu) { return g_attn_split && cu != nullptr && S > 128 && use_s128(128); }
+int split_mode(int S, const int* cu, int split) {
+  if (cu == nullptr || S <= 128 || !use_s128(128)) return 0;
+  return split < 0 ? (g_attn_split ? 1 : 0) : split;
+}
 
 }  // namespace
 
@@ -403,7 +408,7 @@ extern "C" {
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
                 int rows, uint64_t* dmask, int q_live, void* cxc, void* xc, const void* xres, int Bp,
-                hipStream_t st) {
+                int split, hipStream_t st) {
   if (S % 64 != 0) return 1;
   // compact [CLS] rows: the S <= 128 q_live = 1 kernel only
   if (cxc && (!xc || !xres || q_live != 1 || !use_s128(S) || Bp < B)) return 2;
@@ -419,9 +424,11 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
     hipLaunchKernelGGL(attn_fwd_s128_kernel<8>, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
     return 0;
   }
-  if (use_split(S, cu)) {
+  const int sm = split_mode(S, cu, split);
+  if (sm) {
     a.split = 1;  // (no keep-bit buffer: the S <= 128 backward re-hashes, as the 64-row one does)
     hipLaunchKernelGGL(attn_fwd_s128_kernel<8>, dim3(1, H, B + 1), dim3(512), 0, st, a);
+    if (sm == 2) return 0;
   }
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
   return 0;
@@ -430,7 +437,8 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
 int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const float* lse,
                 const void* dctx, float* delta, void* dqkv, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
-                int rows, const uint64_t* dmask, int q_live, const void* dresc, void* dres, hipStream_t st) {
+                int rows, const uint64_t* dmask, int q_live, const void* dresc, void* dres, int split,
+                hipStream_t st) {
   if (S % 64 != 0) return 1;
   // compact [CLS] gradients: the S <= 128 q_live = 1 kernel only
   if ((dresc != nullptr) != (dres != nullptr) || (dres && (q_live != 1 || !use_s128(S)))) return 2;
@@ -447,9 +455,11 @@ int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const floa
     hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
     return 0;
   }
-  if (use_split(S, cu)) {
+  const int sm = split_mode(S, cu, split);
+  if (sm) {
     a.split = 1;
     hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + 1), dim3(512), 0, st, a);
+    if (sm == 2) return 0;
   }
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 64, H, B + (cu ? 1 : 0)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / 64, H, B), dim3(256), 0, st, a);

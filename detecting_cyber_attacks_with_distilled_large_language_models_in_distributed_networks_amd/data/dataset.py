@@ -12,6 +12,7 @@ and no sync per step.  ``drop_last=False`` like the reference.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -40,6 +41,29 @@ class CICIDS2017Dataset(torch.utils.data.Dataset):
     def __getitem__(self, idx) -> Dict[str, torch.Tensor]:
         return {"input_ids": self.input_ids[idx], "attention_mask": self.attention_mask[idx],
                 "labels": self.labels[idx]}
+
+
+class PackedTokens(int):
+    """A batch's real-token count (an ``int`` everywhere it is used as one) that also carries the
+    batch's longest sequence, ``max_len`` -- both known on the host without a device sync.  The
+    model's packed path at S > 128 runs the S <= 128 attention kernels alone when max_len <= 128
+    (ops/kernels.py attn_fwd ``short``); graph keys separate such batches (``short_batch``)."""
+
+    def __new__(cls, total: int, max_len: int):
+        obj = super().__new__(cls, int(total))
+        obj.max_len = int(max_len)
+        return obj
+
+    def __reduce__(self):
+        return (PackedTokens, (int(self), self.max_len))
+
+
+_SHORT = os.environ.get("FD_ATTN_SHORT", "1") != "0"  # 0: never (the length split alone decides)
+
+
+def short_batch(tokens, S: int) -> bool:
+    """Every sequence of the batch has <= 128 real tokens while the padded length S is longer."""
+    return _SHORT and S > 128 and 0 < getattr(tokens, "max_len", 0) <= 128
 
 
 class DeviceLoader:
@@ -96,17 +120,18 @@ class DeviceLoader:
                 lo, hi = i * B, (i + 1) * B
                 lens = self.lengths[perm_cpu[lo:hi]] if perm_cpu is not None else self.lengths[lo:hi]
                 yield {"input_ids": row[:B * S].view(B, S), "attention_mask": row[B * S:2 * B * S].view(B, S),
-                       "labels": row[2 * B * S:], "n_tokens": int(lens.sum())}
+                       "labels": row[2 * B * S:], "n_tokens": PackedTokens(lens.sum(), lens.max())}
                 continue
             lo, hi = i * self.batch_size, min(self.n, (i + 1) * self.batch_size)
             if perm is None:
+                lens = self.lengths[lo:hi]
                 yield {"input_ids": self.ids[lo:hi], "attention_mask": self.mask[lo:hi], "labels": self.labels[lo:hi],
-                       "n_tokens": int(self.lengths[lo:hi].sum())}
+                       "n_tokens": PackedTokens(lens.sum(), lens.max())}
             else:
                 idx = perm[lo:hi]
                 yield {"input_ids": self.ids.index_select(0, idx), "attention_mask": self.mask.index_select(0, idx),
                        "labels": self.labels.index_select(0, idx),
-                       "n_tokens": int(self.lengths[perm_cpu[lo:hi]].sum())}
+                       "n_tokens": PackedTokens(self.lengths[perm_cpu[lo:hi]].sum(), self.lengths[perm_cpu[lo:hi]].max())}
 
 
 @dataclass

@@ -31,6 +31,7 @@ from typing import Callable, Dict, Optional
 
 import torch
 
+from ..data.dataset import PackedTokens, short_batch
 from ..ops.graph_split import GRAPH_SPLIT, _Capture, split_point  # noqa: F401
 
 
@@ -84,6 +85,14 @@ def static_block(*ts: torch.Tensor):
     return out, flat
 
 
+def key_tokens(key):
+    """The ``tokens`` a graph of this key is captured with: the bucket's packed-row count (the
+    rows the replays run on), carrying max_len <= 128 when the key is a short batch's."""
+    if key[1] is None:
+        return None
+    return PackedTokens(key[1], 128) if key[2] else int(key[1])
+
+
 class GraphedTrainStep:
     def __init__(self, step_fn: Callable[..., torch.Tensor], warmup: int = 2, enabled: bool = True,
                  bucket: Optional[Callable[[int, int, int], int]] = None, max_graphs: int = 16):
@@ -108,11 +117,12 @@ class GraphedTrainStep:
         """Graphs in the first captured chain (1 without split points)."""
         return len(next(iter(self.graphs.values()))[0]) if self.graphs else 0
 
-    def _key(self, ids, tokens):
+    def _key(self, ids, tokens):  # (shape, packed-row bucket or None, short_batch)
         if tokens is None or self.bucket is None:
-            return tuple(ids.shape), None
+            return tuple(ids.shape), None, False
         B, S = ids.shape[0], ids.shape[1]
-        return tuple(ids.shape), int(self.bucket(tokens, B, S))
+        # (batches whose sequences all fit the S <= 128 attention kernels launch fewer kernels)
+        return tuple(ids.shape), int(self.bucket(tokens, B, S)), short_batch(tokens, S)
 
     def __call__(self, ids: torch.Tensor, mask: torch.Tensor, labels: torch.Tensor,
                  tokens: Optional[int] = None) -> torch.Tensor:
@@ -155,9 +165,9 @@ class GraphedTrainStep:
             with no_gc():
                 if not self.split:
                     with torch.cuda.graph(chain[0]):
-                        loss = self.step_fn(static["ids"], static["mask"], static["labels"], key[1])
+                        loss = self.step_fn(static["ids"], static["mask"], static["labels"], key_tokens(key))
                 else:
-                    loss = self._capture_split(chain, static, key[1])
+                    loss = self._capture_split(chain, static, key_tokens(key))
         except Exception as e:  # pragma: no cover - capture support varies by op
             self.failed = f"{type(e).__name__}: {e}"
             torch.cuda.synchronize()

@@ -15,7 +15,8 @@ from typing import Dict, Optional, Tuple
 import numpy as np
 import torch
 
-from .graph import contiguous_block, no_gc, static_block
+from ..data.dataset import short_batch
+from .graph import contiguous_block, key_tokens, no_gc, static_block
 
 
 class GraphedForward:
@@ -30,8 +31,9 @@ class GraphedForward:
 
     def _key(self, ids, tokens):
         if tokens is None or not hasattr(self.model, "packed_rows"):
-            return tuple(ids.shape), None
-        return tuple(ids.shape), int(self.model.packed_rows(tokens, ids.shape[0], ids.shape[1]))
+            return tuple(ids.shape), None, False
+        return (tuple(ids.shape), int(self.model.packed_rows(tokens, ids.shape[0], ids.shape[1])),
+                short_batch(tokens, ids.shape[1]))
 
     @torch.no_grad()
     def __call__(self, ids: torch.Tensor, mask: torch.Tensor, tokens: Optional[int] = None) -> torch.Tensor:
@@ -64,13 +66,13 @@ class GraphedForward:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            m(static["ids"], static["mask"], tokens=key[1])
+            m(static["ids"], static["mask"], tokens=key_tokens(key))
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         try:
             torch.cuda.synchronize()
             with no_gc(), torch.cuda.graph(g):
-                out = m(static["ids"], static["mask"], tokens=key[1])
+                out = m(static["ids"], static["mask"], tokens=key_tokens(key))
         except Exception as e:  # pragma: no cover - capture support varies by op
             self.failed = f"{type(e).__name__}: {e}"
             torch.cuda.synchronize()

@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import reference as R
+from ..data.dataset import short_batch
 from .arena import ParamArena
 
 
@@ -519,6 +520,7 @@ class DDoSClassifier(nn.Module):
             if rc.colsum_jobs is not None and self.batch_colsum:
                 rc.colsum_pending = []
         rc.fuse_colsum = self.fuse_colsum
+        rc.attn_short = packed and short_batch(tokens, S)
         rc.qkv_ws = [L["qkv_w"] for L in layers]
         rc.remat_gelu = self.remat_gelu
         rc.fuse_ln = self.fuse_ln and cfg.dim % 64 == 0 and cfg.dim <= 2048

@@ -47,6 +47,9 @@ class RunCtx:
     # [rows] packed -> padded row (-1 for the bucket's filler rows; dropout-hash index).
     cu: Optional[torch.Tensor] = None
     row_map: Optional[torch.Tensor] = None
+    # packed layout at S > 128 whose every sequence has <= 128 tokens (the caller's
+    # data.PackedTokens.max_len): varlen attention runs the S <= 128 kernels alone
+    attn_short: bool = False
     # deferred column sums (bias / LN-affine grads): producers leave partials, the end of
     # the backward finalises all of them in one launch (None = finalise immediately)
     colsum_jobs: Optional[list] = None
@@ -216,7 +219,8 @@ class LayerFn(torch.autograd.Function):
                                           p_a, rc.cu, dmask, xsite=K.ln_xsite(idx, 0, False), prefetch=L["o_w"])
         else:
             qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"], prefetch=L["o_w"])  # (out_lin follows attention)
-            cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask)
+            cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask,
+                                 short=rc.attn_short)
         fuse_ln = rc.fuse_ln and K.ln_fusable(x.shape[0], x.shape[1], K=(x.shape[1], L["l2_w"].shape[1]))
         if fuse_ln:
             # bias + (dropout) + residual + LayerNorm in the N = 768 GEMMs' epilogues; the
@@ -269,7 +273,8 @@ class LayerFn(torch.autograd.Function):
                                           q_live=1, cls=(x, ci.numel()))
         else:
             qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
-            cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask, q_live=1)
+            cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask, q_live=1,
+                                 short=rc.attn_short)
             cxc, xc = K.gather_rows2(cx, x, ci)
         h, ao, m1, r1 = K.linear_ln_fwd(cxc, L["o_w"], L["o_b"], xc, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0,
                                         keep_z=grad, xsite=K.ln_xsite(idx, 0, False))
@@ -349,7 +354,7 @@ class LayerFn(torch.autograd.Function):
             # the [CLS] rows' gradients back into the full layout (every other row exactly 0)
             dcx, dz1 = K.scatter_rows2(dcxc, dz1c, ci, B, cx.shape[0])
             dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu,
-                              ctx.dmask, q_live=1)
+                              ctx.dmask, q_live=1, short=rc.attn_short)
         # (the qkv bias gradient: column sums of dqkv in the dW launch's qkv tiles, K.DW_QKV_BIAS)
         batch += [(dz1c, cxc, G["o_w"].buf, acc),
                   (dqkv, x, G["qkv_w"].buf, acc, G["qkv_b"].buf if K.DW_QKV_BIAS else None)]
@@ -436,7 +441,7 @@ class LayerFn(torch.autograd.Function):
         else:
             dcx = K.linear_dx(dz1, L["o_w"])
             dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu,
-                              ctx.dmask)
+                              ctx.dmask, short=rc.attn_short)
         dw_bias = batch is not None and K.DW_QKV_BIAS  # qkv bias gradient in the dW launch
         if batch is not None:
             batch += [(dz1, cx, G["o_w"].buf, acc),

@@ -347,7 +347,7 @@ def attn_cls_compact_ok(S: int) -> bool:
     return ATTN_CLS_COMPACT and S <= 128 and _os.environ.get("FD_ATTN_S128", "1") != "0"
 
 
-def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, cls=None):
+def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, cls=None, short=False):
     """cu (int32 [B+1]): varlen mode -- qkv/ctx hold packed sequences (rows cu[b]..cu[b+1]-1);
     the kernel zeroes ctx's filler rows past cu[B] itself.  dmask (``attn_keep_bits``): also
     record the dropout keep bits for ``attn_bwd``.
@@ -355,14 +355,19 @@ def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: in
     cls = (x, Bp) (q_live 1, ``attn_cls_compact_ok(S)``): also return ctx[cls_rows] and
     x[cls_rows] as [Bp, D] -- sequence b's [CLS] row in compact row b, rows B..Bp-1 copies of
     row 0 (the pruned block's ``cls_rows`` layout) -- written by the attention blocks that own the
-    rows.  Returns (ctx, lse) or (ctx, lse, cxc, xc)."""
+    rows.  Returns (ctx, lse) or (ctx, lse, cxc, xc).
+
+    Varlen at S > 128 (csrc/kernels/attention.hip split_mode): sequences of <= 128 tokens run on the
+    S <= 128 whole-row kernel, longer ones on the 64-row kernel (FD_ATTN_SPLIT=0: the latter alone);
+    short=True (every sequence has <= 128 tokens, known on the host) skips the 64-row launch."""
     rows = qkv.shape[0] if cu is not None else B * S
     ctx = torch.empty(rows, H * 64, dtype=torch.bfloat16, device=qkv.device)
     lse = torch.empty(B, H, S, dtype=torch.float32, device=qkv.device)
     thr, sc = _drop(p)
     if cls is None:
         # q_live > 0 (S <= 128): only the first q_live query rows of each sequence are computed
-        ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None, q_live)
+        ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None, q_live,
+                       split=2 if short and cu is not None else -1)
         return ctx, lse
     x, Bp = cls
     cxc = torch.empty(Bp, H * 64, dtype=torch.bfloat16, device=qkv.device)
@@ -469,7 +474,8 @@ def attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, B, S, H, seed, site, p, cu=None, 
     return dqkv, dres
 
 
-def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, dresc=None):
+def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, dresc=None,
+             short=False):
     """dmask: the keep bits recorded by the matching ``attn_fwd`` (same seed / site / p).
 
     dresc ([Bp, D], q_live 1, ``attn_cls_compact_ok(S)``): ``dctx`` is the compact [CLS]
@@ -481,7 +487,7 @@ def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=
     thr, sc = _drop(p)
     if dresc is None:
         ext().attn_bwd(qkv, kbias, ctx, lse, dctx.contiguous(), delta, dqkv, B, S, H, seed, site, thr, sc, cu,
-                       dmask if thr else None, q_live)
+                       dmask if thr else None, q_live, split=2 if short and cu is not None else -1)
         return dqkv
     dres = torch.empty_like(ctx)
     ext().attn_bwd(qkv, kbias, ctx, lse, dctx.contiguous(), delta, dqkv, B, S, H, seed, site, thr, sc, cu,

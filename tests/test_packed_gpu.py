@@ -230,3 +230,44 @@ def test_long_sequence_model_hip_vs_torch(S):
             a, b = hip.dense_grad(name), ref.arena.gview(name)
             err = ((a - b).norm() / b.norm()).item()
             assert err < 3e-2, (tok, name, err)
+
+
+def test_short_batch_attention_bitwise():
+    """Every sequence <= 128 tokens at S = 256 (the caller's PackedTokens.max_len): the S <= 128
+    kernels alone (split=2) give exactly what the length split gives (split=1) -- the skipped
+    64-row launches had no sequence to take -- and the model step with a PackedTokens batch equals
+    the one with a plain token count bit for bit, graph replay included."""
+    from detecting_cyber_attacks_with_distilled_large_language_models_in_distributed_networks_amd.data import PackedTokens
+    B, H, S = 8, 12, 256
+    lens = torch.tensor([128, 77, 64, 1, 100, 65, 17, 16])
+    n = int(lens.sum())
+    g = torch.Generator(device="cuda").manual_seed(5)
+    cu = torch.zeros(B + 1, dtype=torch.int32, device="cuda")
+    cu[1:] = torch.cumsum(lens, 0).to(torch.int32).cuda()
+    qkv = torch.cat([(torch.randn(n, 3 * H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16),
+                     torch.zeros(64, 3 * H * 64, dtype=torch.bfloat16, device="cuda")])
+    dctx = torch.cat([(torch.randn(n, H * 64, device="cuda", generator=g) * 0.5).to(torch.bfloat16),
+                      torch.zeros(64, H * 64, dtype=torch.bfloat16, device="cuda")])
+    kb = K.mask_bias(torch.ones(B, S, dtype=torch.int64, device="cuda"))
+    seed = torch.tensor([13], dtype=torch.int32, device="cuda")
+    out = []
+    for short in (False, True):
+        ctx, lse = K.attn_fwd(qkv, kb, B, S, H, seed, 42, 0.1, cu=cu, short=short)
+        d = K.attn_bwd(qkv, kb, ctx, lse, dctx, B, S, H, seed, 42, 0.1, cu=cu, short=short)
+        out.append((ctx, d))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+    cfg = DistilBertConfig(n_layers=2)
+    ids, mask, labels, tokens = _batch(16, S, 70, 90, seed=9)
+    lmax = int(mask.sum(1).max())
+    assert lmax <= 128
+    res = []
+    for tok, graph in ((tokens, False), (PackedTokens(tokens, lmax), False), (PackedTokens(tokens, lmax), True)):
+        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=8)
+        m.train()
+        st = GraphedTrainStep(make_step_fn(m, ArenaAdam(m, lr=1e-3)), warmup=1, enabled=graph, bucket=m.packed_rows)
+        losses = [float(st(ids, mask, labels, tok)) for _ in range(3)]
+        torch.cuda.synchronize()
+        res.append((losses, m.arena.master.clone()))
+    assert res[0][0] == res[1][0] == res[2][0]
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[1][1], res[2][1])
