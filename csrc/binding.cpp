@@ -211,7 +211,9 @@ void gemm(int64_t kind, int64_t epi, const at::Tensor& A, const at::Tensor& B, c
   need_opt(res, at::kBFloat16, "res");
   need_opt(workspace, at::kFloat, "workspace");
   if (epi == 1 || epi == 2) TORCH_CHECK(bias.has_value() && bias->numel() == N, "bias of size N required");
-  if (epi == 2 || epi == 3) TORCH_CHECK(aux.has_value() && aux->size(0) == M && aux->size(1) == N, "aux [M,N] required");
+  // (epi 2: aux = u out, optional -- a forward without autograd keeps only gelu(u))
+  if (epi == 3 || (epi == 2 && aux.has_value() && aux->defined()))
+    TORCH_CHECK(aux.has_value() && aux->size(0) == M && aux->size(1) == N, "aux [M,N] required");
   if (epi == 4) TORCH_CHECK(res.has_value() && res->size(0) == M && res->size(1) == N, "res [M,N] required");
   need_opt(aux_out, at::kBFloat16, "aux_out");
   if (aux_out.has_value() && aux_out->defined())

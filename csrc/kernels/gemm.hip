@@ -455,8 +455,9 @@ DEV void staged_epilogue_out(const GemmParams& p, char* smem, int m0, int n0, in
       const uint4 u = *reinterpret_cast<const uint4*>(smem + r * LDC + cc * 16);
       const int n = n0 + cc * 8;
       if constexpr (EPI == EPI_BIAS_GELU) {
-        // GELU on the bf16-rounded pre-activation, exactly what the backward re-reads.
-        *reinterpret_cast<uint4*>(p.aux + (size_t)m * p.ldaux + n) = u;
+        // GELU on the bf16-rounded pre-activation, exactly what the backward re-reads (no aux: a
+        // forward without autograd -- the teacher, evaluation -- keeps only the activation)
+        if (p.aux) *reinterpret_cast<uint4*>(p.aux + (size_t)m * p.ldaux + n) = u;
         uint4 y;
         y.x = pack_bf2(gelu_erf(lo_bf(u.x)), gelu_erf(hi_bf(u.x)));
         y.y = pack_bf2(gelu_erf(lo_bf(u.y)), gelu_erf(hi_bf(u.y)));

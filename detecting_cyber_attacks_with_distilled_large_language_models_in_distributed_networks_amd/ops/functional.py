@@ -230,7 +230,7 @@ class LayerFn(torch.autograd.Function):
             nxt = rc.qkv_ws[idx + 1] if rc.qkv_ws is not None and idx + 1 < len(rc.qkv_ws) else None
             h, ao, m1, r1 = K.linear_ln_fwd(cx, L["o_w"], L["o_b"], x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0,
                                             0.0, keep_z=grad, xsite=K.ln_xsite(idx, 0, False), prefetch=L["l1_w"])
-            g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True, prefetch=L["l2_w"])
+            g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True, prefetch=L["l2_w"], keep_u=grad)
             y, f, m2, r2 = K.linear_ln_fwd(g, L["l2_w"], L["l2_b"], h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed,
                                            ffn_site, p_h, rc.row_map, keep_z=grad, xsite=K.ln_xsite(idx, 1, False),
                                            prefetch=nxt)
@@ -239,7 +239,7 @@ class LayerFn(torch.autograd.Function):
         else:
             ao = K.linear_fwd(cx, L["o_w"], L["o_b"])
             h, m1, r1 = K.ln_fwd(ao, x, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0)
-            g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
+            g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True, keep_u=grad)
             f = K.linear_fwd(g, L["l2_w"], L["l2_b"])
             y, m2, r2 = K.ln_fwd(f, h, L["ln2_w"], L["ln2_b"], rc.eps, rc.seed, ffn_site, p_h, rc.row_map)
         if grad:
@@ -278,7 +278,7 @@ class LayerFn(torch.autograd.Function):
             cxc, xc = K.gather_rows2(cx, x, ci)
         h, ao, m1, r1 = K.linear_ln_fwd(cxc, L["o_w"], L["o_b"], xc, L["ln1_w"], L["ln1_b"], rc.eps, rc.seed, 0, 0.0,
                                         keep_z=grad, xsite=K.ln_xsite(idx, 0, False))
-        g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True)
+        g, u = K.linear_fwd(h, L["l1_w"], L["l1_b"], gelu=True, keep_u=grad)
         hq = rc.head_req if grad else None
         if hq is not None and K.head_in_sk_ok(g.shape[0], L["l2_w"].shape[0], g.shape[1]):
             # the head + this LayerNorm's backward in the LayerNorm's own split-K epilogue launch

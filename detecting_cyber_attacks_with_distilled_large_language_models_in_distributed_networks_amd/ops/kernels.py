@@ -80,9 +80,15 @@ def _pf(t):
     return t if (LN_PREFETCH and t is not None and t.is_cuda and t.is_contiguous()) else None
 
 
-def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu: bool = False, prefetch=None):
+# FD_NOGRAD_SKIP_U=0: forwards without autograd write the FFN pre-activation u anyway (A/B knob)
+NOGRAD_SKIP_U = _os.environ.get("FD_NOGRAD_SKIP_U", "1") != "0"
+
+
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu: bool = False, prefetch=None,
+               keep_u: bool = True):
     """y = x w^T + b (bf16), optionally also returning u (pre-GELU) with y = gelu(u).  prefetch: the
-    next launch's weight, touched by the epilogue (``LN_PREFETCH``)."""
+    next launch's weight, touched by the epilogue (``LN_PREFETCH``).  keep_u=False (a forward without
+    autograd): u is not written (returned as None) -- 2 bytes per FFN element less."""
     M, N = x.shape[0], w.shape[0]
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
     if _splitk_ok(M, N, x.shape[1]):
@@ -93,7 +99,7 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu
         _splitk(EPI_BIAS if b is not None else EPI_BF16, x, w, y, bias=b)
         return y
     if gelu:
-        u = torch.empty_like(y)
+        u = torch.empty_like(y) if keep_u or not NOGRAD_SKIP_U else None
         ext().gemm(0, EPI_BIAS_GELU, x, w, y, b, u, None, None, False, None, _pf(prefetch))
         return y, u
     ext().gemm(0, EPI_BIAS if b is not None else EPI_BF16, x, w, y, b, None, None, None, False, None, _pf(prefetch))

@@ -47,6 +47,9 @@ def test_gemm_nt_gelu():
     uref = x.float() @ w.float().t() + b
     assert rel_err(u, uref) < 1e-2
     assert rel_err(g, torch.nn.functional.gelu(u.float())) < 1e-2
+    # a forward without autograd: the activation alone, bitwise the same (u is never written)
+    g2, u2 = kn.linear_fwd(x, w, b, gelu=True, keep_u=False)
+    assert u2 is None and torch.equal(g2, g)
 
 
 @pytest.mark.parametrize("M", [4096, 4000])
@@ -58,6 +61,9 @@ def test_gemm_nt_gelu_wide_tile(M):
     uref = x.float() @ w.float().t() + b
     assert rel_err(u, uref) < 1e-2
     assert rel_err(g, torch.nn.functional.gelu(u.float())) < 1e-2
+    # a forward without autograd: the activation alone, bitwise the same (u is never written)
+    g2, u2 = kn.linear_fwd(x, w, b, gelu=True, keep_u=False)
+    assert u2 is None and torch.equal(g2, g)
 
 
 def test_gemm_identity_asymmetric():
