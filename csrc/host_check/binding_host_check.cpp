@@ -67,7 +67,8 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
   }
   hc::span(C, ((long long)(M - 1) * ldc + N) * (kind == 2 ? 4 : 2), "gemm C");
   if (epi == 1 || epi == 2) hc::span(bias, (long long)N * 4, "gemm bias");
-  if (epi == 2 || epi == 3) hc::span(aux, ((long long)(M - 1) * ldaux + N) * 2, "gemm aux");
+  // (epi 2: u is optional -- the kernel writes it only when given)
+  if (epi == 3 || (epi == 2 && aux)) hc::span(aux, ((long long)(M - 1) * ldaux + N) * 2, "gemm aux");
   if (epi == 4) hc::span(res, ((long long)(M - 1) * ldres + N) * 2, "gemm res");
   if (aux_out) hc::span(aux_out, ((long long)(M - 1) * ldaux + N) * 2, "gemm aux_out");
   if (colsum && colsum_blocks) {
@@ -294,7 +295,7 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
 int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv, int M, int K, const float* kbias,
                      void* ctx, float* lse, int B, int S, int H, const uint32_t* seed, uint32_t, uint32_t, float,
                      const int* cu, int rows, uint64_t* dmask, int, void* cxc, void* xc, const void* xres, int Bp,
-                     uint64_t* flags, int nflags, const int* cnt, int, int* err, int, hipStream_t) {
+                     uint64_t* flags, int nflags, const int* cnt, int, int* err, int, int, hipStream_t) {
   ++hc::calls;
   if (g_hc_pf) hc::span(g_hc_pf, g_hc_pf_bytes, "gemm_attn prefetch");
   g_hc_pf = nullptr;
@@ -323,7 +324,7 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
 int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dy,
                      const void* w, int M, int K, int, void* dqkv, int B, int S, int H, const uint32_t* seed,
                      uint32_t, uint32_t, float, const int* cu, int rows, const uint64_t* dmask, const void* dresc,
-                     void* dres, hipStream_t) {
+                     void* dres, int, hipStream_t) {
   ++hc::calls;
   const long long D = (long long)H * 64;
   hc::opt_span(dmask, (long long)B * H * 256 * 8, "attn bwd proj dmask");
@@ -672,7 +673,10 @@ int main() {
     expect_reject("gemm bias size", [&] { gemm(0, 1, x, w, y, b1, none, none, none, false, none); });
     auto xf = T_({2688, 768}, f32);
     expect_reject("gemm dtype", [&] { gemm(0, 1, xf, w, y, b, none, none, none, false, none); });
-    expect_reject("gemm aux missing", [&] { gemm(0, 2, x, w1, g, b1, none, none, none, false, none); });
+    // (bias+GELU without u: a forward without autograd keeps only the activation)
+    expect_ok("gemm NT bias+gelu, no u", [&] { gemm(0, 2, x, w1, g, b1, none, none, none, false, none); });
+    expect_reject("gemm aux missing", [&] { gemm(0, 3, dy, w2t, du, none, none, none, none, false, none); });
+    expect_reject("gemm aux shape", [&] { gemm(0, 2, x, w1, g, b1, y, none, none, false, none); });
     expect_reject("gemm aux_out epi", [&] { gemm(0, 1, x, w, y, b, none, none, none, false, gout); });
     auto xt = x.t();
     expect_reject("gemm non-contiguous", [&] { gemm(0, 1, xt, w, y, b, none, none, none, false, none); });
