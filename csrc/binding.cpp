@@ -71,11 +71,11 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
                      void* ctx, float* lse, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
                      float drop_scale, const int* cu, int rows, uint64_t* dmask, int q_live, void* cxc, void* xc,
                      const void* xres, int Bp, uint64_t* flags, int nflags, const int* cnt, int xsite, int* err,
-                     int mode, hipStream_t st);
+                     int mode, int split, hipStream_t st);
 int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dy,
                      const void* w, int M, int K, int splits, void* dqkv, int B, int S, int H,
                      const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu, int rows,
-                     const uint64_t* dmask, const void* dresc, void* dres, hipStream_t st);
+                     const uint64_t* dmask, const void* dresc, void* dres, int split, hipStream_t st);
 int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int B, int S, int H,
                 const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu,
                 int rows, uint64_t* dmask, int q_live, void* cxc, void* xc, const void* xres, int Bp,
@@ -894,10 +894,12 @@ const int* map_ptr(const c10::optional<at::Tensor>& m, int64_t T) {
 
 // Dropout keep bits handed from the S <= 128 attention forward to its backward: int64
 // [B * H * 128 * 2] (used only by the S <= 128 kernels with dropout; nullable).
-void check_dmask(const c10::optional<at::Tensor>& dmask, int64_t B, int64_t S, int64_t H) {
+// split 2: a varlen batch at S > 128 whose sequences all have <= 128 tokens (the S <= 128 kernels alone)
+void check_dmask(const c10::optional<at::Tensor>& dmask, int64_t B, int64_t S, int64_t H, int64_t split = -1) {
   if (!dmask.has_value() || !dmask->defined()) return;
   need(*dmask, at::kLong, "dmask");
-  TORCH_CHECK(S <= 128 && dmask->numel() == B * H * 256, "attention: dmask needs S <= 128 and B*H*256 words");
+  TORCH_CHECK((S <= 128 || split == 2) && dmask->numel() == B * H * 256,
+              "attention: dmask needs S <= 128 (or split 2) and B*H*256 words");
 }
 
 void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& ctx, const at::Tensor& lse,
@@ -922,7 +924,7 @@ void attn_fwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
   need(kbias, at::kFloat, "kbias");
   need(ctx, at::kBFloat16, "ctx");
   need(lse, at::kFloat, "lse");
-  check_dmask(dmask, B, S, H);
+  check_dmask(dmask, B, S, H, split);
   TORCH_CHECK(S % 64 == 0 && S <= 512, "attention: S must be a multiple of 64 and <= 512");
   const bool varlen = cu.has_value() && cu->defined();
   const int64_t rows = varlen ? qkv.numel() / (3 * H * 64) : B * S;
@@ -949,7 +951,7 @@ void gemm_attn_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
                    const at::Tensor& stats, const at::Tensor& cnt, const at::Tensor& err, int64_t xsite,
                    const c10::optional<at::Tensor>& cxc = c10::nullopt, const c10::optional<at::Tensor>& xc = c10::nullopt,
                    const c10::optional<at::Tensor>& xres = c10::nullopt,
-                   const c10::optional<at::Tensor>& prefetch = c10::nullopt, int64_t mode = 1) {
+                   const c10::optional<at::Tensor>& prefetch = c10::nullopt, int64_t mode = 1, int64_t split = -1) {
   // mode 1: the projection's tiles hand off to the attention items (flags); mode 2: one block per
   // (sequence, head) projects its own Q / K / V tile into the attention's LDS images
   need(x, at::kBFloat16, "x");
@@ -968,7 +970,9 @@ void gemm_attn_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
   TORCH_CHECK(H > 0 && w.size(0) == N && w.size(1) == K && bias.numel() == N && qkv.size(0) == M && qkv.size(1) == N,
               "gemm_attn_fwd: w [3 H 64, K], bias [3 H 64], qkv [M, 3 H 64] required");
   TORCH_CHECK(M > 0 && K % 64 == 0, "gemm_attn_fwd: K must be a multiple of 64");
-  TORCH_CHECK(S % 64 == 0 && S <= 128 && B > 0, "gemm_attn_fwd: S must be 64 or 128");
+  const bool short_ok = split == 2 && mode == 2 && cu.has_value() && cu->defined();  // (sequences <= 128 tokens)
+  TORCH_CHECK(S % 64 == 0 && (S <= 128 || (short_ok && S <= 512)) && B > 0,
+              "gemm_attn_fwd: S must be 64 or 128 (or <= 512 with split 2, mode 2, varlen)");
   TORCH_CHECK(M * N * 2 < (int64_t(1) << 31), "gemm_attn_fwd: qkv must stay below 2 GiB (32-bit buffer offsets)");
   TORCH_CHECK(q_live >= 0, "gemm_attn_fwd: q_live >= 0");
   TORCH_CHECK(xsite >= 0 && xsite < FD_LN_XSITES - 1, "gemm_attn_fwd: exchange call site out of range");
@@ -987,7 +991,7 @@ void gemm_attn_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
     TORCH_CHECK(Bp >= B && cxc->numel() == Bp * D && xc->numel() == cxc->numel(), "gemm_attn_fwd: cxc/xc size");
     TORCH_CHECK(xres->numel() == ctx.numel(), "gemm_attn_fwd: xres size");
   }
-  check_dmask(dmask, B, S, H);
+  check_dmask(dmask, B, S, H, split);
   const bool varlen = cu.has_value() && cu->defined();
   const int64_t rows = varlen ? M : B * S;
   TORCH_CHECK(M == rows && ctx.numel() == rows * D, "gemm_attn_fwd: qkv/ctx rows");
@@ -1000,7 +1004,8 @@ void gemm_attn_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
                             seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale, ptr<int>(cu), (int)rows,
                             ptr<uint64_t>(dmask), (int)q_live, compact ? cxc->data_ptr() : nullptr,
                             compact ? xc->data_ptr() : nullptr, compact ? xres->data_ptr() : nullptr, (int)Bp, flags,
-                            (int)QA_FLAGS, cnt.data_ptr<int>(), (int)xsite, err.data_ptr<int>(), (int)mode, stream()),
+                            (int)QA_FLAGS, cnt.data_ptr<int>(), (int)xsite, err.data_ptr<int>(), (int)mode, (int)split,
+                            stream()),
            "gemm_attn_fwd");
 }
 
@@ -1012,10 +1017,10 @@ void attn_bwd_proj(const at::Tensor& qkv, const at::Tensor& kbias, const at::Ten
                    const at::Tensor& seed, int64_t site, int64_t thr, double dscale,
                    const c10::optional<at::Tensor>& cu, const c10::optional<at::Tensor>& dmask, int64_t splits = 1,
                    const c10::optional<at::Tensor>& dresc = c10::nullopt,
-                   const c10::optional<at::Tensor>& dres = c10::nullopt) {
+                   const c10::optional<at::Tensor>& dres = c10::nullopt, int64_t split = -1) {
   // splits: the K splits of the out-projection GEMM this stands in for (its summation order);
   // dresc / dres: the pruned block's compact [CLS] form (dy = the [CLS] rows [Bp, K]), as attn_bwd
-  check_dmask(dmask, B, S, H);
+  check_dmask(dmask, B, S, H, split);
   const bool compact = dresc.has_value() && dresc->defined();
   TORCH_CHECK(compact == (dres.has_value() && dres->defined()), "attn_bwd_proj: dresc and dres go together");
   need(qkv, at::kBFloat16, "qkv");
@@ -1025,7 +1030,9 @@ void attn_bwd_proj(const at::Tensor& qkv, const at::Tensor& kbias, const at::Ten
   need(dy, at::kBFloat16, "dy");
   need(w, at::kBFloat16, "w");
   need(dqkv, at::kBFloat16, "dqkv");
-  TORCH_CHECK(S % 64 == 0 && S <= 128 && B > 0 && H > 0, "attn_bwd_proj: S must be 64 or 128");
+  const bool short_ok = split == 2 && cu.has_value() && cu->defined();
+  TORCH_CHECK(S % 64 == 0 && (S <= 128 || (short_ok && S <= 512)) && B > 0 && H > 0,
+              "attn_bwd_proj: S must be 64 or 128 (or <= 512 with split 2, varlen)");
   const int64_t D = H * 64;
   const bool varlen = cu.has_value() && cu->defined();
   const int64_t rows = varlen ? qkv.numel() / (3 * D) : B * S;
@@ -1047,7 +1054,7 @@ void attn_bwd_proj(const at::Tensor& qkv, const at::Tensor& kbias, const at::Ten
                             dy.data_ptr(), w.data_ptr(), (int)dy.size(0), (int)dy.size(1), (int)splits, dqkv.data_ptr(),
                             (int)B, (int)S, (int)H, seedp(seed), (uint32_t)site, (uint32_t)thr, (float)dscale,
                             ptr<int>(cu), (int)rows, ptr<uint64_t>(dmask), compact ? dresc->data_ptr() : nullptr,
-                            compact ? dres->data_ptr() : nullptr, stream()),
+                            compact ? dres->data_ptr() : nullptr, (int)split, stream()),
            "attn_bwd_proj");
 }
 
@@ -1059,7 +1066,7 @@ void attn_bwd(const at::Tensor& qkv, const at::Tensor& kbias, const at::Tensor& 
               int64_t split = -1) {
   TORCH_CHECK(q_live >= 0, "attention: q_live >= 0");
   TORCH_CHECK(split >= -1 && split <= 2, "attention: split in -1..2");
-  check_dmask(dmask, B, S, H);
+  check_dmask(dmask, B, S, H, split);
   // compact [CLS] gradients: dctx and dresc are [Bp, D], dres is the full-layout [rows, D] output
   const bool compact = dresc.has_value() && dresc->defined();
   TORCH_CHECK(compact == (dres.has_value() && dres->defined()), "attention bwd: dresc and dres go together");
@@ -1656,7 +1663,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("q_live"),
         py::arg("stats"), py::arg("cnt"), py::arg("err"), py::arg("xsite"), py::arg("cxc") = py::none(),
         py::arg("xc") = py::none(), py::arg("xres") = py::none(), py::arg("prefetch") = py::none(),
-        py::arg("mode") = 1);
+        py::arg("mode") = 1, py::arg("split") = -1);
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"), py::arg("B"),
         py::arg("S"), py::arg("H"), py::arg("seed"), py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"),
         py::arg("dmask"), py::arg("q_live") = 0, py::arg("cxc") = py::none(), py::arg("xc") = py::none(),
@@ -1668,7 +1675,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd_proj", &attn_bwd_proj, py::arg("qkv"), py::arg("kbias"), py::arg("ctx"), py::arg("lse"),
         py::arg("dy"), py::arg("w"), py::arg("dqkv"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("seed"),
         py::arg("site"), py::arg("thr"), py::arg("dscale"), py::arg("cu"), py::arg("dmask"), py::arg("splits") = 1,
-        py::arg("dresc") = py::none(), py::arg("dres") = py::none());
+        py::arg("dresc") = py::none(), py::arg("dres") = py::none(), py::arg("split") = -1);
   m.def("mask_to_bias", &mask_to_bias);
   m.def("attn_set_split", [](int64_t on) { return (int64_t)fd_attn_set_split((int)on); });
   m.def("ln_fwd", &ln_fwd);

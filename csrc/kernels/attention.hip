@@ -410,13 +410,15 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
                 int rows, uint64_t* dmask, int q_live, void* cxc, void* xc, const void* xres, int Bp,
                 int split, hipStream_t st) {
   if (S % 64 != 0) return 1;
+  const int sm = split_mode(S, cu, split);
+  const bool s128 = use_s128(S) || sm == 2;  // the S <= 128 kernel alone
   // compact [CLS] rows: the S <= 128 q_live = 1 kernel only
-  if (cxc && (!xc || !xres || q_live != 1 || !use_s128(S) || Bp < B)) return 2;
+  if (cxc && (!xc || !xres || q_live != 1 || !s128 || Bp < B)) return 2;
   AttnArgs a{};
   a.cxc = (bf16_t*)cxc; a.xc = (bf16_t*)xc; a.xres = (const bf16_t*)xres; a.Bp = Bp;
   a.q_live = q_live;
   a.cu = cu;
-  a.dmask = use_s128(S) ? dmask : nullptr;
+  a.dmask = s128 ? dmask : nullptr;
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
@@ -424,9 +426,8 @@ int fd_attn_fwd(const void* qkv, const float* kbias, void* ctx, float* lse, int 
     hipLaunchKernelGGL(attn_fwd_s128_kernel<8>, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
     return 0;
   }
-  const int sm = split_mode(S, cu, split);
   if (sm) {
-    a.split = 1;  // (no keep-bit buffer: the S <= 128 backward re-hashes, as the 64-row one does)
+    a.split = 1;  // (split 1: no keep-bit buffer, the S <= 128 backward re-hashes as the 64-row one does)
     hipLaunchKernelGGL(attn_fwd_s128_kernel<8>, dim3(1, H, B + 1), dim3(512), 0, st, a);
     if (sm == 2) return 0;
   }
@@ -440,13 +441,15 @@ int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const floa
                 int rows, const uint64_t* dmask, int q_live, const void* dresc, void* dres, int split,
                 hipStream_t st) {
   if (S % 64 != 0) return 1;
+  const int sm = split_mode(S, cu, split);
+  const bool s128 = use_s128(S) || sm == 2;
   // compact [CLS] gradients: the S <= 128 q_live = 1 kernel only
-  if ((dresc != nullptr) != (dres != nullptr) || (dres && (q_live != 1 || !use_s128(S)))) return 2;
+  if ((dresc != nullptr) != (dres != nullptr) || (dres && (q_live != 1 || !s128))) return 2;
   AttnArgs a{};
   a.dresc = (const bf16_t*)dresc; a.dres = (bf16_t*)dres;
   a.q_live = q_live;
   a.cu = cu;
-  a.dmask = use_s128(S) ? const_cast<uint64_t*>(dmask) : nullptr;
+  a.dmask = s128 ? const_cast<uint64_t*>(dmask) : nullptr;
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = (float*)lse;
   a.dctx = (const bf16_t*)dctx; a.delta = delta; a.dqkv = (bf16_t*)dqkv;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
@@ -455,7 +458,6 @@ int fd_attn_bwd(const void* qkv, const float* kbias, const void* ctx, const floa
     hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + (cu ? 1 : 0)), dim3(512), 0, st, a);
     return 0;
   }
-  const int sm = split_mode(S, cu, split);
   if (sm) {
     a.split = 1;
     hipLaunchKernelGGL(attn_bwd_s128_kernel, dim3(1, H, B + 1), dim3(512), 0, st, a);

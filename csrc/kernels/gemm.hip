@@ -1569,7 +1569,7 @@ __global__ __launch_bounds__(512, 2) void seq_attn_fwd_kernel(SeqQkvArgs g, Attn
   if (b < a.B) {
     int tok0, len;
     seq_span(a, b, tok0, len);
-    if (len > 0) sa_project(g, a, tok0, len, h, smem);
+    if (len > 0 && len <= 128) sa_project(g, a, tok0, len, h, smem);  // (longer: skipped by the body too)
   } else {  // filler rows of qkv: finite zeros (the separate GEMM's rows there are never read)
     zero_filler_at(a, const_cast<bf16_t*>(a.qkv), 3 * a.H * DH, 3, h, 0, 1);
   }
@@ -2349,14 +2349,17 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
                      void* ctx, float* lse, int B, int S, int H, const uint32_t* seed_ptr, uint32_t site, uint32_t thr,
                      float drop_scale, const int* cu, int rows, uint64_t* dmask, int q_live, void* cxc, void* xc,
                      const void* xres, int Bp, uint64_t* flags, int nflags, const int* cnt, int xsite, int* err,
-                     int mode, hipStream_t st) {
+                     int mode, int split, hipStream_t st) {
   const char* pf = g_gemm_pf;  // (an armed prefetch belongs to this call whatever happens below)
   const long long pf_bytes = g_gemm_pf_bytes;
   g_gemm_pf = nullptr;
   g_gemm_pf_bytes = 0;
   const int D = H * DH, N = 3 * D;
   if (mode != 1 && mode != 2) return 6;
-  if (M <= 0 || K % BKT || N % QA_BN || S % 64 || S > 128 || B <= 0 || !bias || !flags || !cnt || !err) return 1;
+  // split 2 (S > 128, varlen): the caller knows every sequence has <= 128 tokens (attention.hip split_mode)
+  const bool sh = split == 2 && cu && S <= 512 && mode == 2;
+  if (M <= 0 || K % BKT || N % QA_BN || S % 64 || (S > 128 && !sh) || B <= 0 || !bias || !flags || !cnt || !err)
+    return 1;
   if (xsite < 0 || xsite >= FD_LN_XSITES - 1) return 2;
   if ((cu ? rows : B * S) != M || (long long)M * N * 2 >= (1ll << 31)) return 3;
   if (cxc && (!xc || !xres || q_live != 1 || Bp < B)) return 4;
@@ -2378,6 +2381,7 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
   a.qkv = (const bf16_t*)qkv; a.kbias = kbias; a.ctx = (bf16_t*)ctx; a.lse = lse;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
+  a.split = S > 128 ? 1 : 0;  // (a sequence past 128 tokens is skipped, never staged past the LDS images)
   const int items = H * (B + (cu ? 1 : 0));
   if (mode == 2) {  // per-(sequence, head) projection + attention (no hand-off, no flags)
     // (sequence-major: an XCD's blocks share their sequences' x rows in its L2 -- -5 us per step over
@@ -2400,8 +2404,9 @@ int fd_gemm_attn_fwd(const void* x, const void* w, const float* bias, void* qkv,
 int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const float* lse, const void* dy,
                      const void* w, int M, int K, int splits, void* dqkv, int B, int S, int H,
                      const uint32_t* seed_ptr, uint32_t site, uint32_t thr, float drop_scale, const int* cu, int rows,
-                     const uint64_t* dmask, const void* dresc, void* dres, hipStream_t st) {
-  if (S % 64 || S > 128 || K % BKT || M <= 0 || B <= 0 || !dy || !w || splits <= 0 || (K / BKT) % splits) return 1;
+                     const uint64_t* dmask, const void* dresc, void* dres, int split, hipStream_t st) {
+  const bool sh = split == 2 && cu && S <= 512;  // (as fd_gemm_attn_fwd)
+  if (S % 64 || (S > 128 && !sh) || K % BKT || M <= 0 || B <= 0 || !dy || !w || splits <= 0 || (K / BKT) % splits) return 1;
   // compact [CLS] form: dy = the [CLS] rows' out-projection gradient [M >= B][K]; q_live 1
   if ((dresc != nullptr) != (dres != nullptr) || (dres ? M < B : (cu ? rows : B * S) != M)) return 2;
   AttnArgs a{};
@@ -2413,6 +2418,7 @@ int fd_attn_bwd_proj(const void* qkv, const float* kbias, const void* ctx, const
   a.dqkv = (bf16_t*)dqkv;
   a.seed_ptr = seed_ptr; a.site = site; a.drop_threshold = thr; a.drop_scale = drop_scale;
   a.B = B; a.S = S; a.H = H; a.scale = 0.125f; a.rows = rows;
+  a.split = S > 128 ? 1 : 0;
   static const int order = [] { const char* e = getenv("FD_ATTNBWD_SEQ_MAJOR"); return e ? atoi(e) : 1; }();
   OProjArgs pj{(const bf16_t*)dy, (const bf16_t*)w, M, K, K / BKT / splits, order};
   hipLaunchKernelGGL(attn_bwd_proj_kernel, dim3(H * (B + (cu ? 1 : 0))), dim3(512), 0, st, a, pj);

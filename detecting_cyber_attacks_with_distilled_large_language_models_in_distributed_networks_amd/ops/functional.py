@@ -212,11 +212,13 @@ class LayerFn(torch.autograd.Function):
         p_h = rc.p_hidden if rc.training else 0.0
         attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
         grad = ctx.needs_input_grad[0]
-        dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
-        if rc.fuse_ln and K.qkv_attn_ok(x.shape[0], x.shape[1], rc.S):
+        sh = rc.attn_short
+        dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device, short=sh) if grad else None
+        if rc.fuse_ln and K.qkv_attn_ok(x.shape[0], x.shape[1], rc.S, short=sh):
             # QKV projection + attention in one launch (the exchange epoch advances per forward)
             qkv, cx, lse = K.qkv_attn_fwd(x, L["qkv_w"], L["qkv_b"], rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site,
-                                          p_a, rc.cu, dmask, xsite=K.ln_xsite(idx, 0, False), prefetch=L["o_w"])
+                                          p_a, rc.cu, dmask, xsite=K.ln_xsite(idx, 0, False), prefetch=L["o_w"],
+                                          short=sh)
         else:
             qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"], prefetch=L["o_w"])  # (out_lin follows attention)
             cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask,
@@ -259,18 +261,19 @@ class LayerFn(torch.autograd.Function):
         p_h = rc.p_hidden if rc.training else 0.0
         attn_site, ffn_site = 16 + 4 * idx, 17 + 4 * idx
         grad = ctx.needs_input_grad[0]
-        dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device) if grad else None
+        sh = rc.attn_short
+        dmask = K.attn_keep_bits(rc.B, rc.S, rc.H, p_a, x.device, short=sh) if grad else None
         # only each sequence's first query row ([CLS]) is needed: the other rows' context is never read
         ci, rm = rc.cls_rows, rc.cls_rmap
-        if rc.fuse_ln and K.attn_cls_compact_ok(rc.S) and K.qkv_attn_ok(x.shape[0], x.shape[1], rc.S):
+        if rc.fuse_ln and K.attn_cls_compact_ok(rc.S, sh) and K.qkv_attn_ok(x.shape[0], x.shape[1], rc.S, short=sh):
             # QKV projection + [CLS]-row attention (+ the compact rows) in one launch
             qkv, cx, lse, cxc, xc = K.qkv_attn_fwd(x, L["qkv_w"], L["qkv_b"], rc.kbias, rc.B, rc.S, rc.H, rc.seed,
                                                    attn_site, p_a, rc.cu, dmask, q_live=1, cls=(x, ci.numel()),
-                                                   xsite=K.ln_xsite(idx, 0, False))
-        elif K.attn_cls_compact_ok(rc.S):  # the attention launch also writes the compact [CLS] rows
+                                                   xsite=K.ln_xsite(idx, 0, False), short=sh)
+        elif K.attn_cls_compact_ok(rc.S, sh):  # the attention launch also writes the compact [CLS] rows
             qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
             cx, lse, cxc, xc = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask,
-                                          q_live=1, cls=(x, ci.numel()))
+                                          q_live=1, cls=(x, ci.numel()), short=sh)
         else:
             qkv = K.linear_fwd(x, L["qkv_w"], L["qkv_b"])
             cx, lse = K.attn_fwd(qkv, rc.kbias, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu, dmask, q_live=1,
@@ -338,17 +341,18 @@ class LayerFn(torch.autograd.Function):
         dz1c, _ = K.linear_dx_ln_bwd(du, L["l1_w"], dz2, ao, L["ln1_w"], m1, r1, G["ln1_w"].buf, G["ln1_b"].buf,
                                      G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, xsite=K.ln_xsite(ctx.idx, 0, True),
                                      b_mn=True, prefetch=L["o_w"])
-        if K.attn_cls_compact_ok(rc.S) and K.attn_bwd_proj_ok(rc.S, cls=True):
+        sh = rc.attn_short
+        if K.attn_cls_compact_ok(rc.S, sh) and K.attn_bwd_proj_ok(rc.S, cls=True, short=sh):
             # the out-projection's dX of the [CLS] rows inside the attention backward, which also
             # scatters dz1c into the full layout
             dqkv, dz1 = K.attn_bwd_proj(qkv, rc.kbias, cx, lse, dz1c, L["o_w"], rc.B, rc.S, rc.H, rc.seed, attn_site,
-                                        p_a, rc.cu, ctx.dmask, dresc=dz1c)
-        elif K.attn_cls_compact_ok(rc.S):
+                                        p_a, rc.cu, ctx.dmask, dresc=dz1c, short=sh)
+        elif K.attn_cls_compact_ok(rc.S, sh):
             dcxc = K.linear_dx(dz1c, L["o_w"])
             # the attention backward reads the compact [CLS] gradient and scatters dz1c into the
             # full layout itself (every other row exactly 0)
             dqkv, dz1 = K.attn_bwd(qkv, rc.kbias, cx, lse, dcxc, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu,
-                                   ctx.dmask, q_live=1, dresc=dz1c)
+                                   ctx.dmask, q_live=1, dresc=dz1c, short=sh)
         else:
             dcxc = K.linear_dx(dz1c, L["o_w"])
             # the [CLS] rows' gradients back into the full layout (every other row exactly 0)
@@ -435,9 +439,9 @@ class LayerFn(torch.autograd.Function):
                               G["o_b"].buf, rc.seed, 0, 0.0, acc, None, jobs, zin=fused)
         if not rc.group_dw and batch is None:
             K.linear_dw(dz1, cx, G["o_w"].buf, acc)
-        if K.attn_bwd_proj_ok(rc.S):  # the out-projection's dX computed inside the attention backward
+        if K.attn_bwd_proj_ok(rc.S, short=rc.attn_short):  # the out-projection's dX inside the attention backward
             dqkv = K.attn_bwd_proj(qkv, rc.kbias, cx, lse, dz1, L["o_w"], rc.B, rc.S, rc.H, rc.seed, attn_site, p_a,
-                                   rc.cu, ctx.dmask)
+                                   rc.cu, ctx.dmask, short=rc.attn_short)
         else:
             dcx = K.linear_dx(dz1, L["o_w"])
             dqkv = K.attn_bwd(qkv, rc.kbias, cx, lse, dcx, rc.B, rc.S, rc.H, rc.seed, attn_site, p_a, rc.cu,

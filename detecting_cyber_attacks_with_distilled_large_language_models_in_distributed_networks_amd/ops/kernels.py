@@ -336,10 +336,11 @@ def mask_bias(mask: torch.Tensor) -> torch.Tensor:
     return bias
 
 
-def attn_keep_bits(B, S, H, p, device) -> Optional[torch.Tensor]:
+def attn_keep_bits(B, S, H, p, device, short: bool = False) -> Optional[torch.Tensor]:
     """Buffer for the dropout keep bits the S <= 128 attention forward hands to its backward
-    (which then reads them instead of re-hashing every probability twice); None when unused."""
-    if not threshold(p) or S > 128:
+    (which then reads them instead of re-hashing every probability twice); None when unused.
+    short: a varlen batch at S > 128 whose sequences all fit the S <= 128 kernels."""
+    if not threshold(p) or (S > 128 and not short):
         return None
     return torch.empty(B * H * 256, dtype=torch.int64, device=device)
 
@@ -349,8 +350,8 @@ def attn_keep_bits(B, S, H, p, device) -> Optional[torch.Tensor]:
 ATTN_CLS_COMPACT = _os.environ.get("FD_ATTN_CLS_COMPACT", "1") != "0"
 
 
-def attn_cls_compact_ok(S: int) -> bool:
-    return ATTN_CLS_COMPACT and S <= 128 and _os.environ.get("FD_ATTN_S128", "1") != "0"
+def attn_cls_compact_ok(S: int, short: bool = False) -> bool:
+    return ATTN_CLS_COMPACT and (S <= 128 or short) and _os.environ.get("FD_ATTN_S128", "1") != "0"
 
 
 def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, cls=None, short=False):
@@ -379,7 +380,7 @@ def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: in
     cxc = torch.empty(Bp, H * 64, dtype=torch.bfloat16, device=qkv.device)
     xc = torch.empty_like(cxc)
     ext().attn_fwd(qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None, q_live,
-                   cxc, xc, x)
+                   cxc, xc, x, split=2 if short and cu is not None else -1)
     return ctx, lse, cxc, xc
 
 
@@ -395,15 +396,26 @@ def attn_fwd(qkv, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: in
 FUSE_QKV_ATTN = int(_os.environ.get("FD_FUSE_QKV_ATTN", "2"))
 
 
-def qkv_attn_ok(M: int, D: int, S: int) -> bool:
-    """Shapes the fused QKV + attention launch takes (csrc/binding.cpp gemm_attn_fwd)."""
+# Short batches at S > 128 (data.PackedTokens): the producer-GEMM fusions of the S <= 128 attention take
+# them only with FD_ATTN_SHORT_FUSED=1 -- at the distillation config (seq256 bs64, 18 attention layers
+# per step) the per-(sequence, head) QKV projection measured +112 us per step and the out-projection
+# dX in the backward +16 us against the separate GEMMs (profiles/r6_ab_attn_short_fused.txt); the keep
+# bits hand-off and the compact [CLS] rows apply either way.
+ATTN_SHORT_FUSED = _os.environ.get("FD_ATTN_SHORT_FUSED", "0") != "0"
+
+
+def qkv_attn_ok(M: int, D: int, S: int, short: bool = False) -> bool:
+    """Shapes the fused QKV + attention launch takes (csrc/binding.cpp gemm_attn_fwd); short: a varlen
+    batch at S > 128 whose sequences all have <= 128 tokens (the per-(sequence, head) mode 2 only,
+    ``ATTN_SHORT_FUSED``)."""
+    short = short and ATTN_SHORT_FUSED
     return (FUSE_QKV_ATTN and not _SHARED_DEVICE and _os.environ.get("FD_ATTN_S128", "1") != "0"
-            and S in (64, 128) and D % 64 == 0 and M > 0 and M * 3 * D * 2 < 2 ** 31
+            and (S in (64, 128) or (short and FUSE_QKV_ATTN == 2 and S % 64 == 0 and S <= 512)) and D % 64 == 0 and M > 0 and M * 3 * D * 2 < 2 ** 31
             and ((M + 127) // 128) * (3 * D // 192) <= QA_FLAGS)
 
 
 def qkv_attn_fwd(x, w, b, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_live: int = 0, cls=None,
-                 xsite: int = 0, prefetch=None, mode=None):
+                 xsite: int = 0, prefetch=None, mode=None, short: bool = False):
     """``linear_fwd(x, w, b)`` then ``attn_fwd(qkv, ...)`` as one launch (``qkv_attn_ok``).  xsite:
     this launch's call site within the current exchange epoch (``ln_xsite``; the fused launches
     keep their own granules, so a block's LayerNorm site number can be reused); mode: 1 / 2 (see
@@ -424,7 +436,8 @@ def qkv_attn_fwd(x, w, b, kbias, B, S, H, seed, site, p, cu=None, dmask=None, q_
         kw["xc"] = torch.empty_like(kw["cxc"])
     ext().gemm_attn_fwd(x, w, b, qkv, kbias, ctx, lse, B, S, H, seed, site, thr, sc, cu, dmask if thr else None,
                         q_live, stats, cnt, err, int(xsite), prefetch=_pf(prefetch),
-                        mode=int(mode if mode is not None else (FUSE_QKV_ATTN or 1)), **kw)
+                        mode=int(mode if mode is not None else (FUSE_QKV_ATTN or 1)),
+                        split=2 if short and cu is not None else -1, **kw)
     if cls is None:
         return qkv, ctx, lse
     return qkv, ctx, lse, kw["cxc"], kw["xc"]
@@ -443,8 +456,9 @@ FUSE_ATTN_BWD = int(_os.environ.get("FD_FUSE_ATTN_BWD", "1"))
 FUSE_ATTN_BWD_CLS = int(_os.environ.get("FD_FUSE_ATTN_BWD_CLS", "1"))
 
 
-def attn_bwd_proj_ok(S: int, cls: bool = False) -> bool:
-    return (bool(FUSE_ATTN_BWD) and (not cls or bool(FUSE_ATTN_BWD_CLS)) and S in (64, 128)
+def attn_bwd_proj_ok(S: int, cls: bool = False, short: bool = False) -> bool:
+    short = short and ATTN_SHORT_FUSED
+    return (bool(FUSE_ATTN_BWD) and (not cls or bool(FUSE_ATTN_BWD_CLS)) and (S in (64, 128) or short)
             and _os.environ.get("FD_ATTN_S128", "1") != "0")
 
 
@@ -461,7 +475,8 @@ def _dx_splits(M: int, N: int, K: int) -> int:
     return s
 
 
-def attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, B, S, H, seed, site, p, cu=None, dmask=None, dresc=None):
+def attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, B, S, H, seed, site, p, cu=None, dmask=None, dresc=None,
+                  short: bool = False):
     """``attn_bwd(qkv, kbias, ctx, lse, linear_dx(dy, w), ...)`` as one launch (S <= 128): dy [rows, K]
     is the out-projection's output gradient, w [K, H 64] its weight.  dresc (the pruned block's
     compact form, q_live 1): dy is the [CLS] rows' gradient [Bp, K] and, as in ``attn_bwd``, the launch
@@ -472,11 +487,12 @@ def attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, B, S, H, seed, site, p, cu=None, 
     splits = _dx_splits(dy.shape[0], w.shape[1], dy.shape[1])
     if dresc is None:
         ext().attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, dqkv, B, S, H, seed, site, thr, sc, cu,
-                            dmask if thr else None, splits)
+                            dmask if thr else None, splits, split=2 if short and cu is not None else -1)
         return dqkv
     dres = torch.empty_like(ctx)
     ext().attn_bwd_proj(qkv, kbias, ctx, lse, dy, w, dqkv, B, S, H, seed, site, thr, sc, cu,
-                        dmask if thr else None, splits, dresc.contiguous(), dres)
+                        dmask if thr else None, splits, dresc.contiguous(), dres,
+                        split=2 if short and cu is not None else -1)
     return dqkv, dres
 
 
@@ -497,7 +513,7 @@ def attn_bwd(qkv, kbias, ctx, lse, dctx, B, S, H, seed, site, p, cu=None, dmask=
         return dqkv
     dres = torch.empty_like(ctx)
     ext().attn_bwd(qkv, kbias, ctx, lse, dctx.contiguous(), delta, dqkv, B, S, H, seed, site, thr, sc, cu,
-                   dmask if thr else None, q_live, dresc.contiguous(), dres)
+                   dmask if thr else None, q_live, dresc.contiguous(), dres, split=2 if short and cu is not None else -1)
     return dqkv, dres
 
 

@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out/${1:-r6short}
 mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_packed_gpu.py tests/test_kernels_gpu.py tests/test_model_gpu.py -x -q \
+timeout -k 10 400 python -u -m pytest tests/test_packed_gpu.py tests/test_kernels_gpu.py tests/test_model_gpu.py tests/test_prune_gpu.py tests/test_qkv_attn_gpu.py -x -q \
   --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
 for i in 1 2; do

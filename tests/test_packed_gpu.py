@@ -262,12 +262,21 @@ def test_short_batch_attention_bitwise():
     lmax = int(mask.sum(1).max())
     assert lmax <= 128
     res = []
-    for tok, graph in ((tokens, False), (PackedTokens(tokens, lmax), False), (PackedTokens(tokens, lmax), True)):
-        m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=8)
-        m.train()
-        st = GraphedTrainStep(make_step_fn(m, ArenaAdam(m, lr=1e-3)), warmup=1, enabled=graph, bucket=m.packed_rows)
-        losses = [float(st(ids, mask, labels, tok)) for _ in range(3)]
-        torch.cuda.synchronize()
-        res.append((losses, m.arena.master.clone()))
-    assert res[0][0] == res[1][0] == res[2][0]
-    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[1][1], res[2][1])
+    fused0 = K.ATTN_SHORT_FUSED
+    try:
+        # the S <= 128 producer-GEMM fusions in short mode (opt-in, FD_ATTN_SHORT_FUSED) are bitwise too
+        for tok, graph, fused in ((tokens, False, False), (PackedTokens(tokens, lmax), False, False),
+                                  (PackedTokens(tokens, lmax), True, False), (PackedTokens(tokens, lmax), False, True)):
+            K.ATTN_SHORT_FUSED = fused
+            m = DDoSClassifier(config=cfg, device="cuda", impl="hip", seed=8)
+            m.train()
+            st = GraphedTrainStep(make_step_fn(m, ArenaAdam(m, lr=1e-3)), warmup=1, enabled=graph,
+                                  bucket=m.packed_rows)
+            losses = [float(st(ids, mask, labels, tok)) for _ in range(3)]
+            torch.cuda.synchronize()
+            res.append((losses, m.arena.master.clone()))
+    finally:
+        K.ATTN_SHORT_FUSED = fused0
+    assert res[0][0] == res[1][0] == res[2][0] == res[3][0]
+    for r in res[1:]:
+        assert torch.equal(res[0][1], r[1])
