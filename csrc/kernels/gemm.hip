@@ -2129,7 +2129,11 @@ int pick_cfg(int kind, int M, int N, int K) {
     // FD_GEMM_WIDE_CFG=<id>: configuration of the N >= 1536 NT GEMMs (QKV / FFN1 forward, FFN2 dX)
     static const int wide = [] { const char* e = getenv("FD_GEMM_WIDE_CFG"); return e ? atoi(e) : -1; }();
     if (cfg_instantiated(wide) && N >= 1536 && M >= 1024 && M <= 4096 && tiles_of(wide, M, N) > 0) return wide;
-    if (N % 192 == 0 && N >= 3072 && M >= 3584) return 3;
+    // M >= 3584 (the distillation config's ~5.1 k packed rows, bs256 inference): 8-wave 128 x 192 tiles
+    // -- 39.9 vs 49.4 us (256 x 192) for FFN1 at M = 5184, never slower from 4 k to 20 k rows
+    // (profiles/r6_gemm_cfg_sweep_ffn_large_m.txt).  FD_GEMM_BIG_CFG=<id> overrides (3: the old pick).
+    static const int big = [] { const char* e = getenv("FD_GEMM_BIG_CFG"); return e ? atoi(e) : 6; }();
+    if (N % 192 == 0 && N >= 3072 && M >= 3584 && cfg_instantiated(big) && tiles_of(big, M, N) > 0) return big;
     if (N % 128 == 0 && N >= 3072 && M >= 2048) return 1;
     if (N % 192 == 0 && N >= 1536 && M >= 2048) return 6;
     // (N = 768 on 64 x 64 tiles -- 2-3 blocks per CU -- was faster in isolation but not in the
