@@ -2307,7 +2307,9 @@ int fd_gemm_ex(int kind, int epi, const void* A, const void* B, void* C, int M, 
     // only the staged-fp32 epilogues sum columns: 128 x {128, 64} tiles (never 256-row ones)
     if (epi != EPI_GELU_BWD && epi != EPI_ADD) return 2;
     if (kind != 0 && kind != 1) return 2;
-    if (CFGS[id].bm != 128 && cfg_override(kind) < 0) id = 8;  // (small-M 64-row tiles: 128 x 64)
+    // small-M 64-row tiles: 128 x 64; M >= 3584 (the 256-row pick): 128 x 128 -- the GELU' dX at M = 5184
+    // 44.7 vs 49.3 us (128 x 64), profiles/r6_gemm_cfg_sweep_ffn_large_m.txt
+    if (CFGS[id].bm != 128 && cfg_override(kind) < 0) id = (CFGS[id].bm > 128 && N % 128 == 0) ? 1 : 8;
     if (CFGS[id].bm != 128 || (CFGS[id].bn != 128 && CFGS[id].bn != 64) || N % CFGS[id].bn) {
       // the shape's tile has no staged-fp32 epilogue (e.g. 256 x 192 at M >= 3.5 k): launch
       // nothing, report 0 blocks -- the caller runs the plain GEMM + a column-sum pass
